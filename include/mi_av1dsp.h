@@ -1,0 +1,112 @@
+/*
+ * mi_av1dsp.h — C-ABI boundary of the MI355X-native AV1 decode-DSP path.
+ *
+ * Drop-in for rav1d's DSP function-pointer tables (Rav1dDSPContext, src/internal.rs:111-121;
+ * C twin src/internal.h:61-69). Two surfaces:
+ *
+ *  1. Batched per-frame API (the performance path): the host front-end hands the device one
+ *     descriptor list per frame and per stage, after pass-1 entropy (src/decode.rs:1203-1282,
+ *     src/thread_task.rs:1048-1068). All buffers are device pointers; work is enqueued on the
+ *     caller's HIP stream (passed as an opaque `void*`) and returns without synchronising.
+ *
+ *  2. Table-compatible per-call entry points (mi_dsp_*): exactly the reference's per-block
+ *     signatures (trailing bitdepth_max always passed, as in rav1d). Buffers may be host or
+ *     device memory; each call is a synchronous single-block device launch. They exist for
+ *     drop-in parity testing, not speed (launch cost >> work).
+ *
+ * Conventions, as in the reference:
+ *  - pixel = uint8_t (8 bpc) or uint16_t (10/12 bpc); coef = int16_t (8 bpc) or int32_t;
+ *    strides are in BYTES (include/common/bitdepth.rs:113-125).
+ *  - return 0 or a negative errno, matching Dav1dResult (src/error.rs:27-45):
+ *    -EINVAL bad descriptor, -ENOMEM allocation, -EIO device fault/launch failure,
+ *    -ENODEV no usable gfx950 device.
+ *  - No HIP/torch types appear in this header.
+ */
+#ifndef MI_AV1DSP_H
+#define MI_AV1DSP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MI_AV1DSP_ABI_VERSION 1
+
+/* ------------------------------------------------------------------------------------ */
+/* Shared descriptors                                                                    */
+/* ------------------------------------------------------------------------------------ */
+
+/* A picture resident in device memory. Mirrors the plane/stride part of Dav1dPicture
+ * (include/dav1d/picture.rs; C include/dav1d/picture.h:59-90). layout: Dav1dPixelLayout
+ * (0 I400, 1 I420, 2 I422, 3 I444). stride[1] is shared by both chroma planes. */
+typedef struct MiPicture {
+    void     *data[3];
+    ptrdiff_t stride[2];
+    int32_t   w, h;          /* luma size in pixels */
+    int32_t   layout;
+    int32_t   bpc;           /* 8, 10 or 12 */
+} MiPicture;
+
+/* One transform block of the frame's coefficient arena (pass-2 input of itxfm_add:
+ * src/recon.rs:1781-1788, 2674-2682, 3116, 4013). The arena stores each block's
+ * coefficients column-major with column height min(h,32) — exactly the layout itxfm_add
+ * reads (coeff[y + x*sh], src/itx.rs:128-142). 16 bytes. */
+typedef struct MiTxBlock {
+    uint32_t coef_off;       /* offset in coefficients (not bytes) into the arena */
+    uint16_t x, y;           /* top-left pixel in `plane` */
+    uint8_t  plane;          /* 0 Y, 1 U, 2 V */
+    uint8_t  tx;             /* RectTxfmSize (src/levels.rs:46-82) */
+    uint8_t  txtp;           /* TxfmType 0..15, or 16 = WHT_WHT (lossless) */
+    uint8_t  flags;          /* reserved, 0 */
+    int32_t  eob;            /* end-of-block as passed to itxfm_add */
+} MiTxBlock;
+
+#define MI_N_RECT_TX_SIZES 19
+
+/* ------------------------------------------------------------------------------------ */
+/* Context                                                                               */
+/* ------------------------------------------------------------------------------------ */
+
+typedef struct MiCtx MiCtx;
+
+/* Create a context bound to `device` (HIP ordinal). One context per decoder
+ * frame-context; calls on one context are serialised by the caller (src/internal.rs
+ * Rav1dFrameContext), different contexts are independent. */
+int  mi_ctx_create(int device, MiCtx **out);
+void mi_ctx_destroy(MiCtx *ctx);
+/* Last device-side error observed by the context (0 if none). */
+int  mi_ctx_last_error(const MiCtx *ctx);
+const char *mi_version(void);
+
+/* ------------------------------------------------------------------------------------ */
+/* Batched per-frame API                                                                 */
+/* ------------------------------------------------------------------------------------ */
+
+/* Inverse transform + add for a whole frame.
+ * `blocks` (device) must be grouped by tx size: blocks of size s are
+ * blocks[size_start[s] .. size_start[s+1]) (host array of 20 entries). Within a group,
+ * sorting by txtp / eob==0 reduces wave divergence but is not required.
+ * Blocks must not overlap (true of any AV1 frame). `coef` is the device arena.
+ * flags: MI_ITX_KEEP_COEFS leaves the arena untouched; by default the consumed
+ * coefficients are zeroed as the reference's itxfm_add does (src/itx.rs:152-158). */
+#define MI_ITX_KEEP_COEFS 1u
+int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
+                 const uint32_t size_start[MI_N_RECT_TX_SIZES + 1], void *coef,
+                 unsigned flags, void *stream);
+
+/* ------------------------------------------------------------------------------------ */
+/* Table-compatible per-call entry points                                                */
+/* ------------------------------------------------------------------------------------ */
+
+/* itxfm_add[tx][txtp] (src/itx.rs:190-196; C src/itx.h:37-44). Replaces
+ * inv_txfm_add_rust / dav1d_inv_txfm_add_<type>_<w>x<h>_<bpc>bpc_<isa>. Returns 0 or -errno
+ * (the reference's fn returns void; a non-zero return here means nothing was written). */
+int mi_dsp_itxfm_add(int tx, int txtp, void *dst, ptrdiff_t stride, void *coeff, int eob,
+                     int bitdepth_max);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MI_AV1DSP_H */

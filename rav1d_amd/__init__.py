@@ -1,0 +1,77 @@
+"""rav1d_amd — MI355X-native AV1 decode-DSP path behind rav1d's DSP tables.
+
+The product is the C-ABI library ``librav1d_amd.so`` (header ``include/mi_av1dsp.h``),
+built from the gfx950 HIP sources in ``csrc/``. This package is the host-side mirror used
+by tests and the benchmark: it loads the library, describes its structs for ctypes/numpy,
+and wraps the entry points. There is no CPU fallback: if the library is missing or has no
+GPU, calls fail loudly.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librav1d_amd.so")
+
+_lib = None
+
+
+class MiError(RuntimeError):
+    pass
+
+
+# --- struct mirrors (include/mi_av1dsp.h) ---------------------------------------------
+
+class MiPicture(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p * 3), ("stride", ctypes.c_ssize_t * 2),
+                ("w", ctypes.c_int32), ("h", ctypes.c_int32),
+                ("layout", ctypes.c_int32), ("bpc", ctypes.c_int32)]
+
+
+TXBLOCK_DTYPE = np.dtype([("coef_off", "<u4"), ("x", "<u2"), ("y", "<u2"), ("plane", "u1"),
+                          ("tx", "u1"), ("txtp", "u1"), ("flags", "u1"), ("eob", "<i4")])
+assert TXBLOCK_DTYPE.itemsize == 16
+
+N_RECT_TX_SIZES = 19
+ITX_KEEP_COEFS = 1
+
+_VP = ctypes.c_void_p
+
+
+def _sig(lib, name, res, args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = args
+    return f
+
+
+def lib():
+    """Load librav1d_amd.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MiError(f"{LIB_PATH} missing: run `python -m rav1d_amd.build` (hipcc, gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    _sig(L, "mi_version", ctypes.c_char_p, [])
+    _sig(L, "mi_ctx_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_VP)])
+    _sig(L, "mi_ctx_destroy", None, [_VP])
+    _sig(L, "mi_ctx_last_error", ctypes.c_int, [_VP])
+    _sig(L, "mi_itx_frame", ctypes.c_int,
+         [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.POINTER(ctypes.c_uint32), _VP, ctypes.c_uint, _VP])
+    _sig(L, "mi_dsp_itxfm_add", ctypes.c_int,
+         [ctypes.c_int, ctypes.c_int, _VP, ctypes.c_ssize_t, _VP, ctypes.c_int, ctypes.c_int])
+    _lib = L
+    return L
+
+
+# Every symbol include/mi_av1dsp.h declares (checked by tests/test_abi.py).
+EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
+            "mi_itx_frame", "mi_dsp_itxfm_add"]
+
+
+def check(rc, what):
+    if rc != 0:
+        raise MiError(f"{what} failed: {rc} ({os.strerror(-rc) if rc < 0 else rc})")
+    return rc

@@ -1,0 +1,179 @@
+// capi.cpp — the C-ABI of include/mi_av1dsp.h: contexts, the batched per-frame entry points
+// and the table-compatible per-call entry points.
+//
+// The per-call entry points keep the reference's contract (caller owns buffers, callee zeroes
+// the consumed coefficients, src/itx.rs:152-158) and accept host or device pointers; they run
+// a one-block launch synchronously on a private stream of device 0.
+#include <errno.h>
+#include <mutex>
+#include <string.h>
+#include <vector>
+#include "common.h"
+
+struct MiCtx {
+    int device = 0;
+    int last_error = 0;
+};
+
+namespace {
+
+int fail(MiCtx *c, int e) {
+    if (c) c->last_error = e;
+    return e;
+}
+
+bool is_device_ptr(const void *p) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+}
+
+// Private state for the synchronous per-call entry points.
+struct CallState {
+    std::mutex mu;
+    bool ready = false;
+    int err = 0;
+    hipStream_t stream = nullptr;
+    uint8_t *scratch = nullptr;     // pixels / coefficients / descriptors
+    size_t scratch_bytes = 0;
+    int init() {
+        if (ready) return err;
+        ready = true;
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return err = -ENODEV;
+        if (hipSetDevice(0) != hipSuccess) return err = -ENODEV;
+        if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return err = -EIO;
+        scratch_bytes = 1 << 20;
+        if (hipMalloc(&scratch, scratch_bytes) != hipSuccess) return err = -ENOMEM;
+        return err = 0;
+    }
+};
+CallState g_call;
+
+} // namespace
+
+extern "C" {
+
+const char *mi_version(void) { return "rav1d_amd mi_av1dsp 0.1 (gfx950)"; }
+
+int mi_ctx_create(int device, MiCtx **out) {
+    if (!out) return -EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return -ENODEV;
+    MiCtx *c = new (std::nothrow) MiCtx;
+    if (!c) return -ENOMEM;
+    c->device = device;
+    *out = c;
+    return 0;
+}
+
+void mi_ctx_destroy(MiCtx *ctx) { delete ctx; }
+
+int mi_ctx_last_error(const MiCtx *ctx) { return ctx ? ctx->last_error : -EINVAL; }
+
+int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
+                 const uint32_t size_start[MI_N_RECT_TX_SIZES + 1], void *coef, unsigned flags,
+                 void *stream) {
+    if (!ctx || !pic || !size_start) return fail(ctx, -EINVAL);
+    if (pic->bpc != 8 && pic->bpc != 10 && pic->bpc != 12) return fail(ctx, -EINVAL);
+    mi::ItxArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int p = 0; p < 3; p++) {
+        a.plane[p] = (uint8_t *)pic->data[p];
+        a.stride[p] = pic->stride[p ? 1 : 0];
+    }
+    a.blocks = blocks;
+    a.coef = (uint8_t *)coef;
+    a.bdmax = (1 << pic->bpc) - 1;
+    a.zero_coefs = (flags & MI_ITX_KEEP_COEFS) ? 0 : 1;
+    int wg = 0;
+    for (int s = 0; s < MI_N_RECT_TX_SIZES; s++) {
+        if (size_start[s + 1] < size_start[s]) return fail(ctx, -EINVAL);
+        const int n = (int)(size_start[s + 1] - size_start[s]);
+        a.wg_start[s] = wg;
+        a.blk_start[s] = (int)size_start[s];
+        wg += (n + mi::itx_blocks_per_wg(s) - 1) / mi::itx_blocks_per_wg(s);
+    }
+    a.wg_start[MI_N_RECT_TX_SIZES] = wg;
+    a.blk_start[MI_N_RECT_TX_SIZES] = (int)size_start[MI_N_RECT_TX_SIZES];
+    if (wg == 0) return 0;
+    if (!blocks || !coef) return fail(ctx, -EINVAL);
+    const int r = mi::launch_itx_frame(a, wg, pic->bpc, (hipStream_t)stream);
+    return r ? fail(ctx, -EIO) : 0;
+}
+
+// ---- table-compatible per-call entry points ------------------------------------------
+
+int mi_dsp_itxfm_add(int tx, int txtp, void *dst, ptrdiff_t stride, void *coeff, int eob,
+                     int bitdepth_max) {
+    if (tx < 0 || tx >= MI_N_RECT_TX_SIZES || !mi::itx_type_valid(tx, txtp) || !dst || !coeff ||
+        eob < 0)
+        return -EINVAL;
+    const int bpc = bitdepth_max == 255 ? 8 : bitdepth_max == 1023 ? 10 : bitdepth_max == 4095 ? 12 : 0;
+    if (!bpc) return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    if (hipSetDevice(0) != hipSuccess) return -ENODEV;
+
+    const mi::TxDim d = mi::tx_dim(tx);
+    const int px = bpc == 8 ? 1 : 2, cb = bpc == 8 ? 2 : 4;
+    const size_t ncoef = (size_t)mi::imin_c(d.w, 32) * mi::imin_c(d.h, 32);
+    const size_t row_bytes = (size_t)d.w * px;
+    hipStream_t s = g_call.stream;
+
+    // device layout in scratch: [pixels h*row_bytes][coef][descriptor]
+    uint8_t *dpix = g_call.scratch;
+    uint8_t *dcoef = dpix + 64 * 128;
+    MiTxBlock *dblk = (MiTxBlock *)(dcoef + 32 * 32 * 4);
+
+    const bool dst_dev = is_device_ptr(dst), cf_dev = is_device_ptr(coeff);
+    std::vector<uint8_t> hpix;
+    if (dst_dev) {
+        for (int y = 0; y < d.h; y++)
+            if (hipMemcpyAsync(dpix + y * row_bytes, (uint8_t *)dst + y * stride, row_bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
+                return -EIO;
+    } else {
+        hpix.resize(row_bytes * d.h);
+        for (int y = 0; y < d.h; y++) memcpy(&hpix[y * row_bytes], (uint8_t *)dst + y * stride, row_bytes);
+        if (hipMemcpyAsync(dpix, hpix.data(), hpix.size(), hipMemcpyHostToDevice, s) != hipSuccess) return -EIO;
+    }
+    if (hipMemcpyAsync(dcoef, coeff, ncoef * cb, cf_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s) != hipSuccess)
+        return -EIO;
+    MiTxBlock hb{};
+    hb.tx = (uint8_t)tx;
+    hb.txtp = (uint8_t)txtp;
+    hb.eob = eob;
+    if (hipMemcpyAsync(dblk, &hb, sizeof(hb), hipMemcpyHostToDevice, s) != hipSuccess) return -EIO;
+
+    mi::ItxArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int p = 0; p < 3; p++) { a.plane[p] = dpix; a.stride[p] = (int64_t)row_bytes; }
+    a.blocks = dblk;
+    a.coef = dcoef;
+    a.bdmax = bitdepth_max;
+    a.zero_coefs = 1;
+    for (int k = 0; k <= MI_N_RECT_TX_SIZES; k++) {
+        a.wg_start[k] = k > tx ? 1 : 0;
+        a.blk_start[k] = k > tx ? 1 : 0;
+    }
+    if (mi::launch_itx_frame(a, 1, bpc, s)) return -EIO;
+
+    if (dst_dev) {
+        for (int y = 0; y < d.h; y++)
+            if (hipMemcpyAsync((uint8_t *)dst + y * stride, dpix + y * row_bytes, row_bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
+                return -EIO;
+    } else {
+        if (hipMemcpyAsync(hpix.data(), dpix, hpix.size(), hipMemcpyDeviceToHost, s) != hipSuccess) return -EIO;
+    }
+    if (hipMemcpyAsync(coeff, dcoef, ncoef * cb, cf_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s) != hipSuccess)
+        return -EIO;
+    if (hipStreamSynchronize(s) != hipSuccess) return -EIO;
+    if (!dst_dev)
+        for (int y = 0; y < d.h; y++) memcpy((uint8_t *)dst + y * stride, &hpix[y * row_bytes], row_bytes);
+    return 0;
+}
+
+} // extern "C"

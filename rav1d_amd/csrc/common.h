@@ -1,0 +1,60 @@
+// common.h — shared host/device definitions for the gfx950 DSP library.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include "../../include/mi_av1dsp.h"
+
+namespace mi {
+
+// RectTxfmSize -> dimensions (src/levels.rs:46-82) and the inverse-transform row shift
+// (src/itx.rs:439-457; C src/itx_tmpl.c:142-160).
+struct TxDim { int w, h, shift; };
+__host__ __device__ constexpr TxDim tx_dim(int tx) {
+    constexpr TxDim t[19] = {
+        { 4, 4, 0 },   { 8, 8, 1 },   { 16, 16, 2 }, { 32, 32, 2 }, { 64, 64, 2 },
+        { 4, 8, 0 },   { 8, 4, 0 },   { 8, 16, 1 },  { 16, 8, 1 },  { 16, 32, 1 },
+        { 32, 16, 1 }, { 32, 64, 1 }, { 64, 32, 1 }, { 4, 16, 1 },  { 16, 4, 1 },
+        { 8, 32, 2 },  { 32, 8, 2 },  { 16, 64, 2 }, { 64, 16, 2 },
+    };
+    return t[tx];
+}
+__host__ __device__ constexpr int imin_c(int a, int b) { return a < b ? a : b; }
+__host__ __device__ constexpr int imax_c(int a, int b) { return a > b ? a : b; }
+
+// Lanes per transform block in the itx kernel: one lane per row in the row pass, one lane
+// per column in the column pass.
+__host__ __device__ constexpr int itx_lanes(int tx) {
+    return imax_c(imin_c(tx_dim(tx).h, 32), tx_dim(tx).w);
+}
+constexpr int kItxThreads = 256;
+__host__ __device__ constexpr int itx_blocks_per_wg(int tx) { return kItxThreads / itx_lanes(tx); }
+
+// Which transform types are legal for a size (src/itx.rs:400-457): 16 types for sizes up to
+// 16 on both sides except 16x16 (12 types), DCT_DCT + IDTX when a side is 32, DCT_DCT only
+// when a side is 64. WHT_WHT (16) only for 4x4.
+__host__ __device__ constexpr bool itx_type_valid(int tx, int txtp) {
+    const TxDim d = tx_dim(tx);
+    const int m = imax_c(d.w, d.h);
+    if (txtp == 16) return tx == 0;
+    if (m == 64) return txtp == 0;
+    if (m == 32) return txtp == 0 || txtp == 9;
+    if (d.w == 16 && d.h == 16) return txtp <= 11;
+    return txtp < 16;
+}
+
+struct ItxArgs {
+    uint8_t *plane[3];
+    int64_t stride[3];
+    const MiTxBlock *blocks;
+    uint8_t *coef;
+    int bdmax;
+    int zero_coefs;
+    int wg_start[20];
+    int blk_start[20];
+};
+
+// launchers (itx.hip)
+int launch_itx_frame(const ItxArgs &a, int total_wg, int bpc, hipStream_t s);
+
+} // namespace mi

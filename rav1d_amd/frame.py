@@ -1,0 +1,123 @@
+"""Device-resident pictures and the batched per-frame calls.
+
+Pictures follow dav1d's default allocator layout (rav1d src/picture.rs:98-115): width and
+height aligned to 128, a luma stride of the aligned row bytes (+64 B when it is a multiple
+of 1024, to break cache-set aliasing), chroma planes subsampled per layout. Each plane is a
+torch uint8 tensor of shape (rows, stride_bytes) on the device; 16-bit pictures are the same
+bytes viewed as little-endian uint16. torch is only the allocator/stream provider here.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import MiPicture, MiError, check, lib
+
+LAYOUT_I400, LAYOUT_I420, LAYOUT_I422, LAYOUT_I444 = 0, 1, 2, 3
+
+
+def _align(v, a):
+    return (v + a - 1) // a * a
+
+
+def plane_geometry(w, h, layout, bpc):
+    """(luma (rows, stride), chroma (rows, stride), chroma (w, h)) in bytes, as the reference."""
+    pxb = 1 if bpc == 8 else 2
+    aw, ah = _align(w, 128), _align(h, 128)
+    ss_hor = layout in (LAYOUT_I420, LAYOUT_I422)
+    ss_ver = layout == LAYOUT_I420
+    y_stride = aw * pxb
+    if y_stride % 1024 == 0:
+        y_stride += 64
+    uv_stride = (aw >> ss_hor) * pxb
+    if uv_stride % 1024 == 0:
+        uv_stride += 64
+    cw, ch = (w + ss_hor) >> ss_hor, (h + ss_ver) >> ss_ver
+    return (ah, y_stride), (ah >> ss_ver, uv_stride), (cw, ch)
+
+
+class Frame:
+    """A picture whose three planes live in device (or host) memory."""
+
+    def __init__(self, w, h, bpc=10, layout=LAYOUT_I420, device="cuda"):
+        self.w, self.h, self.bpc, self.layout = w, h, bpc, layout
+        (yr, ys), (cr, cs), (cw, ch) = plane_geometry(w, h, layout, bpc)
+        self.cw, self.ch = cw, ch
+        self.pxb = 1 if bpc == 8 else 2
+        self.strides = [ys, cs, cs]
+        rows = [yr, cr, cr]
+        n = 1 if layout == LAYOUT_I400 else 3
+        self.planes = [torch.zeros((rows[p], self.strides[p]), dtype=torch.uint8, device=device)
+                       for p in range(n)]
+
+    def dims(self, p):
+        return (self.w, self.h) if p == 0 else (self.cw, self.ch)
+
+    def picture(self):
+        pic = MiPicture()
+        for p in range(3):
+            pic.data[p] = self.planes[min(p, len(self.planes) - 1)].data_ptr()
+        pic.stride[0], pic.stride[1] = self.strides[0], self.strides[1]
+        pic.w, pic.h, pic.layout, pic.bpc = self.w, self.h, self.layout, self.bpc
+        return pic
+
+    # numpy views (copies across the device boundary)
+    def plane_np(self, p):
+        b = self.planes[p].cpu().numpy()
+        w, h = self.dims(p)
+        if self.pxb == 2:
+            return b.view("<u2")[:h, :w].copy()
+        return b[:h, :w].copy()
+
+    def set_plane_np(self, p, arr):
+        w, h = self.dims(p)
+        dt = np.uint16 if self.pxb == 2 else np.uint8
+        host = self.planes[p].cpu().numpy().copy()
+        view = host.view("<u2") if self.pxb == 2 else host
+        view[:h, :w] = np.asarray(arr, dtype=dt)[:h, :w]
+        self.planes[p].copy_(torch.from_numpy(host))
+
+    def raw_np(self, p):
+        """Whole plane including padding, as bytes (rows, stride)."""
+        return self.planes[p].cpu().numpy()
+
+    def clone(self):
+        f = Frame.__new__(Frame)
+        f.__dict__.update(self.__dict__)
+        f.planes = [t.clone() for t in self.planes]
+        return f
+
+
+class Context:
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        check(lib().mi_ctx_create(device, ctypes.byref(h)), "mi_ctx_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().mi_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def itx_frame(ctx, frame, blocks_dev, size_start, coef_dev, flags=0, stream=None):
+    """mi_itx_frame: inverse transform + add for all blocks of a frame (device tensors)."""
+    pic = frame.picture()
+    ss = (ctypes.c_uint32 * 20)(*[int(v) for v in size_start])
+    if blocks_dev.dtype != torch.uint8 or not blocks_dev.is_cuda:
+        raise MiError("blocks must be a device uint8 tensor holding MiTxBlock records")
+    rc = lib().mi_itx_frame(ctx.h, ctypes.byref(pic), ctypes.c_void_p(blocks_dev.data_ptr()), ss,
+                            ctypes.c_void_p(coef_dev.data_ptr()), flags, _stream_ptr(stream))
+    check(rc, "mi_itx_frame")

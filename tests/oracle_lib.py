@@ -1,0 +1,58 @@
+"""ctypes binding of oracle/liboracle.so — the CPU restatement used as the parity checker.
+
+TEST INFRASTRUCTURE ONLY (see oracle/oracle.h). Builds the oracle with make if needed.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
+
+_o = None
+_VP = ctypes.c_void_p
+
+
+def load_oracle():
+    global _o
+    if _o is not None:
+        return _o
+    srcs = [f for f in os.listdir(ORACLE_DIR) if f.endswith((".c", ".h"))]
+    if not os.path.exists(ORACLE_SO) or any(
+            os.path.getmtime(os.path.join(ORACLE_DIR, f)) > os.path.getmtime(ORACLE_SO) for f in srcs):
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+    o = ctypes.CDLL(ORACLE_SO)
+    o.oracle_itxfm_add.argtypes = [ctypes.c_int, ctypes.c_int, _VP, ctypes.c_ssize_t, _VP, ctypes.c_int, ctypes.c_int]
+    o.oracle_itxfm_add.restype = None
+    o.oracle_itx_frame.argtypes = [_VP, _VP, _VP, ctypes.c_int, _VP, ctypes.c_int]
+    o.oracle_itx_frame.restype = None
+    o.oracle_itx_1d.argtypes = [ctypes.c_int, ctypes.c_int, _VP, ctypes.c_ssize_t, ctypes.c_int, ctypes.c_int]
+    o.oracle_itx_1d.restype = None
+    _o = o
+    return o
+
+
+def ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def itx_1d(kind, n, vec, lo=-(1 << 20), hi=(1 << 20) - 1):
+    c = np.ascontiguousarray(vec, dtype=np.int32).copy()
+    load_oracle().oracle_itx_1d(kind, n, ptr(c), 1, lo, hi)
+    return c
+
+
+def itx_frame(planes, blocks, coef, bpc):
+    """Run the oracle over numpy planes (list of 2-D arrays, modified in place) and arena."""
+    o = load_oracle()
+    arrs = [np.ascontiguousarray(p) for p in planes]
+    while len(arrs) < 3:
+        arrs.append(arrs[0])
+    pp = (ctypes.c_void_p * 3)(*[a.ctypes.data for a in arrs])
+    st = (ctypes.c_ssize_t * 3)(*[a.strides[0] for a in arrs])
+    b = np.ascontiguousarray(blocks)
+    o.oracle_itx_frame(pp, st, ptr(b), len(b), ptr(coef), (1 << bpc) - 1)
+    return arrs[:len(planes)]

@@ -1,0 +1,91 @@
+"""GPU parity: the HIP itx path vs the oracle restatement, bit-exact.
+
+Follows the reference's checkasm pattern (tests/checkasm/itx.c:131-302): identical random
+but valid inputs through both implementations, compare destination pixels and the zeroed
+coefficient buffer.
+"""
+import numpy as np
+import pytest
+import torch
+
+from rav1d_amd import ITX_KEEP_COEFS, lib
+from rav1d_amd.frame import Frame, itx_frame
+from rav1d_amd.synth import TX_DIMS, make_coefs, make_itx_frame, tx_types
+from tests import oracle_lib
+from tests.oracle_lib import ptr
+
+pytestmark = pytest.mark.gpu
+
+
+def run_frame(gpu, fr, flags=0):
+    f = Frame(fr["w"], fr["h"], fr["bpc"], fr["layout"])
+    for p, arr in enumerate(fr["planes"]):
+        f.set_plane_np(p, arr)
+    blocks = torch.from_numpy(fr["blocks"].view(np.uint8).copy()).cuda()
+    coef = torch.from_numpy(fr["coef"].copy()).cuda()
+    itx_frame(gpu, f, blocks, fr["size_start"], coef, flags)
+    torch.cuda.synchronize()
+    return [f.plane_np(p) for p in range(len(fr["planes"]))], coef.cpu().numpy()
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_itx_frame_matches_oracle(gpu, bpc, seed):
+    fr = make_itx_frame(256, 192, bpc=bpc, seed=seed, with_wht=(seed == 2))
+    got, coef_after = run_frame(gpu, fr)
+    ref_planes = [p.copy() for p in fr["planes"]]
+    ref_coef = fr["coef"].copy()
+    ref = oracle_lib.itx_frame(ref_planes, fr["blocks"], ref_coef, bpc)
+    for p in range(3):
+        assert np.array_equal(got[p], ref[p]), f"plane {p} differs"
+    assert not coef_after.any() and not ref_coef.any()
+
+
+def test_itx_keep_coefs_flag(gpu):
+    fr = make_itx_frame(128, 128, bpc=10, seed=5)
+    _, coef_after = run_frame(gpu, fr, flags=ITX_KEEP_COEFS)
+    assert np.array_equal(coef_after, fr["coef"])
+
+
+@pytest.mark.parametrize("bpc", [8, 10])
+def test_itx_frame_1080p_matches_oracle(gpu, bpc):
+    fr = make_itx_frame(1920, 1080, bpc=bpc, seed=0x1D1C0001)
+    got, _ = run_frame(gpu, fr)
+    ref = oracle_lib.itx_frame([p.copy() for p in fr["planes"]], fr["blocks"], fr["coef"].copy(), bpc)
+    for p in range(3):
+        assert np.array_equal(got[p], ref[p])
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+def test_per_call_table_entries(gpu, bpc):
+    """mi_dsp_itxfm_add over every (size, type) with full/partial/DC coefficients, host buffers."""
+    L = lib()
+    o = oracle_lib.load_oracle()
+    rng = np.random.default_rng(100 + bpc)
+    cdt = np.int16 if bpc == 8 else np.int32
+    dt = np.uint8 if bpc == 8 else np.uint16
+    for tx, (w, h) in enumerate(TX_DIMS):
+        types = tx_types(tx) + ([16] if tx == 0 else [])
+        for txtp in types:
+            for regime in (0, 1, 2):
+                if regime == 0 and txtp != 0:
+                    continue
+                c, eob = make_coefs(rng, tx, txtp, regime, bpc)
+                if txtp == 16:
+                    c = np.clip(c // 64, -(1 << (bpc + 2)), 1 << (bpc + 2))
+                c = c.astype(cdt)
+                d = rng.integers(0, 1 << bpc, size=(h, w + 16)).astype(dt)
+                c_ref, d_ref = c.copy(), d.copy()
+                o.oracle_itxfm_add(tx, txtp, ptr(d_ref), d_ref.strides[0], ptr(c_ref), eob, (1 << bpc) - 1)
+                rc = L.mi_dsp_itxfm_add(tx, txtp, ptr(d), d.strides[0], ptr(c), eob, (1 << bpc) - 1)
+                assert rc == 0
+                assert np.array_equal(d, d_ref), (tx, txtp, regime)
+                assert not c.any()
+
+
+def test_per_call_rejects_bad_args(gpu):
+    L = lib()
+    d = np.zeros((64, 64), np.uint16)
+    c = np.zeros(1024, np.int32)
+    assert L.mi_dsp_itxfm_add(4, 9, ptr(d), 128, ptr(c), 0, 1023) == -22   # IDTX illegal at 64x64
+    assert L.mi_dsp_itxfm_add(0, 0, ptr(d), 128, ptr(c), 0, 1000) == -22   # bad bitdepth_max
