@@ -65,6 +65,29 @@ typedef struct MiTxBlock {
 
 #define MI_N_RECT_TX_SIZES 19
 
+/* Per-128x128 loop-filter / CDEF metadata: byte-identical to the reference's Av1Filter
+ * (src/lf_mask.rs:40-51; C src/lf_mask.h:51-57), so the host can hand over f->lf.mask as is.
+ * Edge masks must already carry the tile-boundary fixups of rav1d_loopfilter_sbrow_cols
+ * (src/lf_apply.rs:625-705). 1348 bytes, 2-byte aligned. */
+typedef struct MiAv1Filter {
+    uint16_t filter_y[2][32][3][2];   /* [0 col edges, 1 row edges][pos][wd 4/8/16][half] */
+    uint16_t filter_uv[2][32][2][2];  /* [dir][pos][wd 4/6][half] */
+    int8_t   cdef_idx[4];             /* per 64x64, -1 = unset */
+    uint16_t noskip_mask[16][2];      /* per 8x8, stored on a 4x8 basis */
+} MiAv1Filter;
+
+/* Frame-level deblocking inputs (Rav1dFrameData.lf, src/internal.rs:557-576). */
+typedef struct MiLoopFilter {
+    const uint8_t *level;        /* device: [u8;4] per 4x4 unit {Y col-edge, Y row-edge, U, V};
+                                  * U/V slots are addressed at chroma 4x4 coordinates */
+    ptrdiff_t b4_stride;         /* level entries per row */
+    const MiAv1Filter *masks;    /* device: [sb128h][sb128w] */
+    int32_t sb128w;
+    int32_t filter_y;            /* frame_hdr.loopfilter.level_y[0] || level_y[1] */
+    int32_t filter_uv;           /* level_u || level_v */
+    uint8_t lim_e[64], lim_i[64];/* Av1FilterLUT.e / .i (rav1d_calc_eih) */
+} MiLoopFilter;
+
 /* ------------------------------------------------------------------------------------ */
 /* Context                                                                               */
 /* ------------------------------------------------------------------------------------ */
@@ -95,6 +118,11 @@ const char *mi_version(void);
 int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
                  const uint32_t size_start[MI_N_RECT_TX_SIZES + 1], void *coef,
                  unsigned flags, void *stream);
+
+/* Deblock a whole frame in place: all column edges (every plane), then all row edges.
+ * Equivalent to the reference's per-sbrow cols/rows interleaving;
+ * replaces rav1d_loopfilter_sbrow_cols/_rows (src/lf_apply.rs:597-834). */
+int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, void *stream);
 
 /* ------------------------------------------------------------------------------------ */
 /* Table-compatible per-call entry points                                                */

@@ -29,6 +29,12 @@ class MiPicture(ctypes.Structure):
                 ("layout", ctypes.c_int32), ("bpc", ctypes.c_int32)]
 
 
+class MiLoopFilter(ctypes.Structure):
+    _fields_ = [("level", ctypes.c_void_p), ("b4_stride", ctypes.c_ssize_t), ("masks", ctypes.c_void_p),
+                ("sb128w", ctypes.c_int32), ("filter_y", ctypes.c_int32), ("filter_uv", ctypes.c_int32),
+                ("lim_e", ctypes.c_uint8 * 64), ("lim_i", ctypes.c_uint8 * 64)]
+
+
 TXBLOCK_DTYPE = np.dtype([("coef_off", "<u4"), ("x", "<u2"), ("y", "<u2"), ("plane", "u1"),
                           ("tx", "u1"), ("txtp", "u1"), ("flags", "u1"), ("eob", "<i4")])
 assert TXBLOCK_DTYPE.itemsize == 16
@@ -62,13 +68,14 @@ def lib():
          [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.POINTER(ctypes.c_uint32), _VP, ctypes.c_uint, _VP])
     _sig(L, "mi_dsp_itxfm_add", ctypes.c_int,
          [ctypes.c_int, ctypes.c_int, _VP, ctypes.c_ssize_t, _VP, ctypes.c_int, ctypes.c_int])
+    _sig(L, "mi_deblock_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiLoopFilter), _VP])
     _lib = L
     return L
 
 
 # Every symbol include/mi_av1dsp.h declares (checked by tests/test_abi.py).
 EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
-            "mi_itx_frame", "mi_dsp_itxfm_add"]
+            "mi_itx_frame", "mi_deblock_frame", "mi_dsp_itxfm_add"]
 
 
 def check(rc, what):

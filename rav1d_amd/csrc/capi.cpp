@@ -105,6 +105,53 @@ int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
     return r ? fail(ctx, -EIO) : 0;
 }
 
+int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, void *stream) {
+    if (!ctx || !pic || !lf) return fail(ctx, -EINVAL);
+    if (pic->bpc != 8 && pic->bpc != 10 && pic->bpc != 12) return fail(ctx, -EINVAL);
+    if (!lf->filter_y) return 0;   // deblocking off for the frame (recon.rs:4047-4060)
+    if (!lf->level || !lf->masks || lf->sb128w <= 0) return fail(ctx, -EINVAL);
+    mi::LfArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int p = 0; p < 3; p++) {
+        a.plane[p] = (uint8_t *)pic->data[p];
+        a.stride[p] = pic->stride[p ? 1 : 0];
+    }
+    a.level = (const uint32_t *)lf->level;
+    a.b4_stride = lf->b4_stride;
+    a.masks = lf->masks;
+    a.w4 = (pic->w + 3) >> 2;
+    a.h4 = (pic->h + 3) >> 2;
+    a.sb128w = lf->sb128w;
+    a.sb128h = (pic->h + 127) >> 7;
+    if (a.sb128w != (pic->w + 127) >> 7 || a.b4_stride < (int64_t)a.sb128w * 32) return fail(ctx, -EINVAL);
+    a.ss_hor = pic->layout == 1 || pic->layout == 2;
+    a.ss_ver = pic->layout == 1;
+    a.bdmax = (1 << pic->bpc) - 1;
+    a.bdm8 = pic->bpc - 8;
+    a.filter_uv = pic->layout != 0 && lf->filter_uv;
+    memcpy(a.lim_e, lf->lim_e, 64);
+    memcpy(a.lim_i, lf->lim_i, 64);
+    const int nplanes = a.filter_uv ? 3 : 1;
+    mi::LfArgs cols = a, rows = a;
+    int nc = 0, nr = 0;
+    for (int p = 0; p < 3; p++) {
+        const int sh = p ? a.ss_hor : 0, sv = p ? a.ss_ver : 0;
+        cols.blk_start[p] = nc;
+        rows.blk_start[p] = nr;
+        if (p >= nplanes) continue;
+        cols.units_x[p] = (a.w4 + sh) >> sh;
+        cols.rows[p] = (a.sb128h * 128) >> sv;
+        nc += ((cols.units_x[p] + 63) / 64) * ((cols.rows[p] + 3) / 4);
+        rows.units_x[p] = (a.sb128w * 128) >> sh;
+        rows.rows[p] = p ? a.sb128h * (32 >> sv) : a.h4;
+        nr += ((rows.units_x[p] + 63) / 64) * ((rows.rows[p] + 3) / 4);
+    }
+    cols.blk_start[3] = nc;
+    rows.blk_start[3] = nr;
+    const int r = mi::launch_deblock(cols, rows, pic->bpc, (hipStream_t)stream);
+    return r ? fail(ctx, -EIO) : 0;
+}
+
 // ---- table-compatible per-call entry points ------------------------------------------
 
 int mi_dsp_itxfm_add(int tx, int txtp, void *dst, ptrdiff_t stride, void *coeff, int eob,

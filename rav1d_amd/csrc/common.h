@@ -57,4 +57,19 @@ struct ItxArgs {
 // launchers (itx.hip)
 int launch_itx_frame(const ItxArgs &a, int total_wg, int bpc, hipStream_t s);
 
+struct LfArgs {
+    uint8_t *plane[3];
+    int64_t stride[3];
+    const uint32_t *level;     // [u8;4] packed little-endian
+    int64_t b4_stride;
+    const MiAv1Filter *masks;
+    int sb128w, sb128h;
+    int w4, h4, ss_hor, ss_ver, bdmax, bdm8, filter_uv;
+    int blk_start[4];          // flattened workgroup ranges per plane
+    int units_x[3], rows[3];   // thread space per plane
+    uint8_t lim_e[64], lim_i[64];
+};
+// launchers (lf.hip)
+int launch_deblock(const LfArgs &cols, const LfArgs &rows, int bpc, hipStream_t s);
+
 } // namespace mi

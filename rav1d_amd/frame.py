@@ -11,7 +11,7 @@ import ctypes
 import numpy as np
 import torch
 
-from . import MiPicture, MiError, check, lib
+from . import MiLoopFilter, MiPicture, MiError, check, lib
 
 LAYOUT_I400, LAYOUT_I420, LAYOUT_I422, LAYOUT_I444 = 0, 1, 2, 3
 
@@ -121,3 +121,27 @@ def itx_frame(ctx, frame, blocks_dev, size_start, coef_dev, flags=0, stream=None
     rc = lib().mi_itx_frame(ctx.h, ctypes.byref(pic), ctypes.c_void_p(blocks_dev.data_ptr()), ss,
                             ctypes.c_void_p(coef_dev.data_ptr()), flags, _stream_ptr(stream))
     check(rc, "mi_itx_frame")
+
+
+class LoopFilterMeta:
+    """Device copies of the deblocking inputs (MiLoopFilter)."""
+
+    def __init__(self, lf):
+        self.level = torch.from_numpy(np.ascontiguousarray(lf["level"]).reshape(-1)).cuda()
+        self.masks = torch.from_numpy(np.ascontiguousarray(lf["masks"]).view(np.uint8).reshape(-1)).cuda()
+        s = MiLoopFilter()
+        s.level = self.level.data_ptr()
+        s.b4_stride = int(lf["b4_stride"])
+        s.masks = self.masks.data_ptr()
+        s.sb128w = int(lf["sb128w"])
+        s.filter_y = int(lf["filter_y"])
+        s.filter_uv = int(lf["filter_uv"])
+        s.lim_e[:] = [int(v) for v in lf["lim_e"]]
+        s.lim_i[:] = [int(v) for v in lf["lim_i"]]
+        self.s = s
+
+
+def deblock_frame(ctx, frame, meta, stream=None):
+    pic = frame.picture()
+    check(lib().mi_deblock_frame(ctx.h, ctypes.byref(pic), ctypes.byref(meta.s), _stream_ptr(stream)),
+          "mi_deblock_frame")

@@ -172,3 +172,132 @@ def itx_algorithmic_bytes(blocks, bpc, zero_coefs=True):
     ncoef = np.where(dconly, 1, ncoef)
     per = cb * ncoef * (2 if zero_coefs else 1) + 2 * pxb * w * h + 16
     return int(per.sum())
+
+
+# ---------------------------------------------------------------------------------------
+# Deblocking metadata (Av1Filter masks + level map), derived from a transform tiling the way
+# rav1d's lf_mask builds them (src/lf_mask.rs:130-378): an edge at every transform-block
+# boundary, filter-width index = min over the two sides of log2(tx extent / 4 px), capped at
+# 2 (luma: 4/8/16) or 1 (chroma: 4/6).
+# ---------------------------------------------------------------------------------------
+
+AV1FILTER_DTYPE = np.dtype([("filter_y", "<u2", (2, 32, 3, 2)), ("filter_uv", "<u2", (2, 32, 2, 2)),
+                            ("cdef_idx", "i1", (4,)), ("noskip_mask", "<u2", (16, 2))])
+assert AV1FILTER_DTYPE.itemsize == 1348
+
+
+def calc_eih(sharp):
+    """Av1FilterLUT e/i for a sharpness (rav1d src/lf_mask.rs:608-626)."""
+    e = np.zeros(64, np.uint8)
+    i = np.zeros(64, np.uint8)
+    for level in range(64):
+        limit = level
+        if sharp > 0:
+            limit >>= (sharp + 3) >> 2
+            limit = min(limit, 9 - sharp)
+        limit = max(limit, 1)
+        i[level] = limit
+        e[level] = 2 * (level + 2) + limit
+    return e, i
+
+
+def _unit_maps(blocks, nux, nuy):
+    lw = np.zeros((nuy, nux), np.int8)
+    lh = np.zeros((nuy, nux), np.int8)
+    sx = np.zeros((nuy, nux), bool)
+    sy = np.zeros((nuy, nux), bool)
+    bid = np.full((nuy, nux), -1, np.int32)
+    for i, (x, y, tx) in enumerate(blocks):
+        w, h = TX_DIMS[tx]
+        x4, y4, w4, h4 = x >> 2, y >> 2, w >> 2, h >> 2
+        lw[y4:y4 + h4, x4:x4 + w4] = int(w4).bit_length() - 1
+        lh[y4:y4 + h4, x4:x4 + w4] = int(h4).bit_length() - 1
+        sx[y4:y4 + h4, x4] = True
+        sy[y4, x4:x4 + w4] = True
+        bid[y4:y4 + h4, x4:x4 + w4] = i
+    return lw, lh, sx, sy, bid
+
+
+def make_lf_meta(tilings, w, h, layout, rng, sharpness=None, zero_level_frac=0.08):
+    """Returns dict(level=(rows, b4_stride, 4) u8, masks=Av1Filter[sb128h, sb128w], lim_e, lim_i,
+    b4_stride, sb128w, filter_y, filter_uv)."""
+    ss_hor = 1 if layout in (1, 2) else 0
+    ss_ver = 1 if layout == 1 else 0
+    w4, h4 = (w + 3) >> 2, (h + 3) >> 2
+    sb128w, sb128h = (w + 127) >> 7, (h + 127) >> 7
+    b4_stride = sb128w * 32
+    level = np.zeros((sb128h * 32, b4_stride, 4), np.uint8)
+    masks = np.zeros((sb128h, sb128w), AV1FILTER_DTYPE)
+    fy = np.zeros((sb128h, sb128w, 2, 32, 3, 2), np.uint16)
+    fuv = np.zeros((sb128h, sb128w, 2, 32, 2, 2), np.uint16)
+    for p, blocks in enumerate(tilings):
+        luma = p == 0
+        sh, sv = (0, 0) if luma else (ss_hor, ss_ver)
+        nux, nuy = (w4 + sh) >> sh, (h4 + sv) >> sv
+        lw, lh, sx, sy, bid = _unit_maps(blocks, nux, nuy)
+        cap = 2 if luma else 1
+        lwc, lhc = np.minimum(lw, cap), np.minimum(lh, cap)
+        # per-block levels: slots (0, 1) for luma col/row edges, slot 1+p for chroma
+        nb = len(blocks)
+        lv = rng.integers(1, 64, size=(nb, 2)).astype(np.uint8)
+        lv[rng.random((nb, 2)) < zero_level_frac] = 0
+        valid = bid >= 0
+        if luma:
+            level[:nuy, :nux, 0][valid] = lv[bid[valid], 0]
+            level[:nuy, :nux, 1][valid] = lv[bid[valid], 1]
+        else:
+            level[:nuy, :nux, 1 + p][valid] = lv[bid[valid], 0]
+        csw, csh = 32 >> sh, 32 >> sv
+        # column edges
+        uy, ux = np.nonzero(sx & valid)
+        left = np.where(ux > 0, lwc[uy, np.maximum(ux - 1, 0)], lwc[uy, ux])
+        k = np.minimum(left, lwc[uy, ux]).astype(np.int64)
+        X, x, Y, yy = ux // csw, ux % csw, uy // csh, uy % csh
+        hb = 16 >> sv
+        half, bit = yy // hb, yy % hb
+        tgt = fy if luma else fuv
+        flat = tgt.reshape(-1)
+        shp = tgt.shape  # (sbh, sbw, 2, 32, K, 2)
+        idx = np.ravel_multi_index((Y, X, np.zeros_like(Y), x, k, half), shp)
+        np.bitwise_or.at(flat, idx, (1 << bit).astype(np.uint16))
+        # row edges
+        uy, ux = np.nonzero(sy & valid)
+        up = np.where(uy > 0, lhc[np.maximum(uy - 1, 0), ux], lhc[uy, ux])
+        k = np.minimum(up, lhc[uy, ux]).astype(np.int64)
+        X, xx, Y, y = ux // csw, ux % csw, uy // csh, uy % csh
+        hb = 16 >> sh
+        half, bit = xx // hb, xx % hb
+        idx = np.ravel_multi_index((Y, X, np.ones_like(Y), y, k, half), shp)
+        np.bitwise_or.at(flat, idx, (1 << bit).astype(np.uint16))
+    masks["filter_y"] = fy
+    masks["filter_uv"] = fuv
+    if sharpness is None:
+        sharpness = int(rng.integers(0, 8))
+    e, i = calc_eih(sharpness)
+    return dict(level=level, masks=masks, lim_e=e, lim_i=i, b4_stride=b4_stride, sb128w=sb128w,
+                filter_y=1, filter_uv=1 if layout != 0 else 0, sharpness=sharpness)
+
+
+def make_tilings(w, h, layout, rng):
+    ss_hor = 1 if layout in (1, 2) else 0
+    ss_ver = 1 if layout == 1 else 0
+    cw, ch = (w + ss_hor) >> ss_hor, (h + ss_ver) >> ss_ver
+    out = [tile_plane(w, h, rng, sb=64)]
+    if layout != 0:
+        t = tile_plane(cw, ch, rng, sb=64 >> ss_hor)
+        out += [t, t]
+    return out
+
+
+def make_mixed_texture(rng, w, h, bpc):
+    """Blocky content mixing flat and textured 8x8 regions so every deblock branch fires."""
+    bdmax = (1 << bpc) - 1
+    base = make_texture(rng, w, h, bpc).astype(np.int64)
+    amp = np.array([0, 1, 3, 8, 40]) * (bdmax // 255 + 1)
+    tiles = rng.integers(0, len(amp), size=((h + 7) // 8, (w + 7) // 8))
+    a = np.kron(amp[tiles], np.ones((8, 8), np.int64))[:h, :w]
+    offs = np.kron(rng.integers(-20, 21, size=tiles.shape) * (bdmax // 255 + 1), np.ones((8, 8), np.int64))[:h, :w]
+    smooth = (np.arange(w)[None, :] // 16 + np.arange(h)[:, None] // 16) * (bdmax // 255 + 1)
+    noise = rng.integers(-1, 2, size=(h, w)) * a + rng.integers(0, 2, size=(h, w)) * (a > 0)
+    img = np.where(a == 0, (bdmax // 2 + smooth % 7) + offs, base + offs + noise)
+    return np.clip(img, 0, bdmax).astype(np.uint16 if bpc > 8 else np.uint8)

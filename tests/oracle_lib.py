@@ -56,3 +56,23 @@ def itx_frame(planes, blocks, coef, bpc):
     b = np.ascontiguousarray(blocks)
     o.oracle_itx_frame(pp, st, ptr(b), len(b), ptr(coef), (1 << bpc) - 1)
     return arrs[:len(planes)]
+
+
+def deblock_frame(planes, bpc, layout, w, h, lf, sb128=1):
+    """Oracle whole-frame deblock in the reference's sbrow order; planes modified in place."""
+    o = load_oracle()
+    f = o.oracle_deblock_frame
+    f.restype = None
+    f.argtypes = [_VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _VP,
+                  ctypes.c_ssize_t, _VP, ctypes.c_int, ctypes.c_int, _VP, _VP, ctypes.c_int, ctypes.c_int]
+    arrs = [np.ascontiguousarray(p) for p in planes]
+    while len(arrs) < 3:
+        arrs.append(arrs[0])
+    pp = (ctypes.c_void_p * 3)(*[a.ctypes.data for a in arrs])
+    st = (ctypes.c_ssize_t * 3)(*[a.strides[0] for a in arrs])
+    level = np.ascontiguousarray(lf["level"])
+    masks = np.ascontiguousarray(lf["masks"])
+    e = np.ascontiguousarray(lf["lim_e"]); i = np.ascontiguousarray(lf["lim_i"])
+    f(pp, st, w, h, layout, bpc, ptr(level), lf["b4_stride"], ptr(masks), lf["sb128w"], sb128,
+      ptr(e), ptr(i), lf["filter_y"], lf["filter_uv"])
+    return arrs[:len(planes)]
