@@ -88,6 +88,17 @@ typedef struct MiLoopFilter {
     uint8_t lim_e[64], lim_i[64];/* Av1FilterLUT.e / .i (rav1d_calc_eih) */
 } MiLoopFilter;
 
+/* Frame-level CDEF parameters (Dav1dFrameHeader.cdef, include/dav1d/headers.rs:2324;
+ * C include/dav1d/headers.h Dav1dCdefParams) plus the per-64x64 indices/skip masks that live
+ * in the Av1Filter array. */
+typedef struct MiCdef {
+    const MiAv1Filter *masks;    /* device: [sb128h][sb128w] (cdef_idx, noskip_mask) */
+    int32_t sb128w;
+    int32_t damping;             /* frame_hdr.cdef.damping (3..6) */
+    uint8_t y_strength[8];       /* pri << 2 | sec, as coded */
+    uint8_t uv_strength[8];
+} MiCdef;
+
 /* ------------------------------------------------------------------------------------ */
 /* Context                                                                               */
 /* ------------------------------------------------------------------------------------ */
@@ -123,6 +134,12 @@ int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
  * Equivalent to the reference's per-sbrow cols/rows interleaving;
  * replaces rav1d_loopfilter_sbrow_cols/_rows (src/lf_apply.rs:597-834). */
 int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, void *stream);
+
+/* CDEF for a whole frame, out of place: reads the deblocked picture `src` (never written)
+ * and writes `dst` (blocks the reference skips are copied). Replaces rav1d_cdef_brow
+ * (src/cdef_apply.rs:159-507). `src` and `dst` must have identical geometry. */
+int mi_cdef_frame(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const MiCdef *cdef,
+                  void *stream);
 
 /* ------------------------------------------------------------------------------------ */
 /* Table-compatible per-call entry points                                                */

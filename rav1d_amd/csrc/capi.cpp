@@ -152,6 +152,38 @@ int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, v
     return r ? fail(ctx, -EIO) : 0;
 }
 
+int mi_cdef_frame(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const MiCdef *cd,
+                  void *stream) {
+    if (!ctx || !src || !dst || !cd || !cd->masks) return fail(ctx, -EINVAL);
+    if (src->bpc != dst->bpc || src->w != dst->w || src->h != dst->h || src->layout != dst->layout ||
+        src->stride[0] != dst->stride[0] || src->stride[1] != dst->stride[1])
+        return fail(ctx, -EINVAL);
+    if (src->bpc != 8 && src->bpc != 10 && src->bpc != 12) return fail(ctx, -EINVAL);
+    mi::CdefArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int p = 0; p < 3; p++) {
+        a.src[p] = (const uint8_t *)src->data[p];
+        a.dst[p] = (uint8_t *)dst->data[p];
+        a.stride[p] = src->stride[p ? 1 : 0];
+    }
+    a.masks = cd->masks;
+    a.sb128w = cd->sb128w;
+    if (a.sb128w != (src->w + 127) >> 7) return fail(ctx, -EINVAL);
+    a.bw4 = ((src->w + 7) >> 3) << 1;
+    a.bh4 = ((src->h + 7) >> 3) << 1;
+    a.layout = src->layout;
+    a.ss_hor = src->layout == 1 || src->layout == 2;
+    a.ss_ver = src->layout == 1;
+    a.bdm8 = src->bpc - 8;
+    a.damping = cd->damping + a.bdm8;
+    memcpy(a.y_strength, cd->y_strength, 8);
+    memcpy(a.uv_strength, cd->uv_strength, 8);
+    a.tiles_x = (a.bw4 * 4 + 63) / 64;
+    const int tiles_y = (a.bh4 * 4 + 63) / 64;
+    const int r = mi::launch_cdef(a, a.tiles_x * tiles_y, src->bpc, (hipStream_t)stream);
+    return r ? fail(ctx, -EIO) : 0;
+}
+
 // ---- table-compatible per-call entry points ------------------------------------------
 
 int mi_dsp_itxfm_add(int tx, int txtp, void *dst, ptrdiff_t stride, void *coeff, int eob,

@@ -1,0 +1,269 @@
+// cdef.hip — whole-frame CDEF on gfx950, out of place (deblocked D -> C).
+//
+// Replaces rav1d_cdef_brow (rav1d src/cdef_apply.rs:159-507) and the DSP cdef.dir/cdef.fb[3]
+// (src/cdef.rs:545-1031; C src/cdef_tmpl.c). The reference filters in place and keeps line and
+// column backups so every block reads deblocked (pre-CDEF) samples only; reading an immutable
+// D and writing C gives the same result without backups.
+//
+// One 256-lane workgroup per 64x64 luma unit (the granularity of cdef_idx, so strengths are
+// workgroup-uniform) plus its co-located chroma. The tile and a 2-px halo are staged in LDS as
+// int16 with i16::MIN where the reference's padding marks samples unavailable (frame edges,
+// cdef.rs:567-665). Phase 1: 64 lanes find the 8x8 directions; phase 2: every lane filters
+// pixels straight out of LDS and streams C back with coalesced stores.
+#include "common.h"
+
+namespace mi {
+
+
+__constant__ int8_t k_cdef_dir[8][2][2] = {
+    { { -1, 1 }, { -2, 2 } }, { { 0, 1 }, { -1, 2 } }, { { 0, 1 }, { 0, 2 } }, { { 0, 1 }, { 1, 2 } },
+    { { 1, 1 }, { 2, 2 } },   { { 1, 0 }, { 2, 1 } },  { { 1, 0 }, { 2, 0 } }, { { 1, 0 }, { 2, -1 } },
+};
+
+constexpr int kTY = 68, kTS = 72;          // luma tile rows / LDS row stride (int16)
+
+__device__ __forceinline__ int constrain(int diff, int thr, int shift) {
+    const int ad = abs(diff);
+    const int v = min(ad, max(0, thr - (ad >> shift)));
+    return diff < 0 ? -v : v;
+}
+
+__device__ __forceinline__ int ulog2i(unsigned v) { return 31 - __clz(v); }
+
+__device__ __forceinline__ int adjust_strength(int strength, unsigned var) {
+    if (!var) return 0;
+    const int i = (var >> 6) ? min(ulog2i(var >> 6), 12) : 0;
+    return (strength * (4 + i) + 8) >> 4;
+}
+
+// 8x8 direction search on an LDS tile (cdef.rs:921-1031).
+__device__ int find_dir(const int16_t *t, int ts, int bdm8, unsigned *var) {
+    int hv0[8] = {}, hv1[8] = {}, dg0[15] = {}, dg1[15] = {}, al[4][11] = {};
+#pragma unroll
+    for (int y = 0; y < 8; y++) {
+#pragma unroll
+        for (int x = 0; x < 8; x++) {
+            const int p = ((int)t[y * ts + x] >> bdm8) - 128;
+            dg0[y + x] += p;
+            al[0][y + (x >> 1)] += p;
+            hv0[y] += p;
+            al[1][3 + y - (x >> 1)] += p;
+            dg1[7 + y - x] += p;
+            al[2][3 - (y >> 1) + x] += p;
+            hv1[x] += p;
+            al[3][(y >> 1) + x] += p;
+        }
+    }
+    const unsigned dv[7] = { 840, 420, 280, 210, 168, 140, 120 };
+    unsigned cost[8] = {};
+#pragma unroll
+    for (int n = 0; n < 8; n++) {
+        cost[2] += (unsigned)(hv0[n] * hv0[n]);
+        cost[6] += (unsigned)(hv1[n] * hv1[n]);
+    }
+    cost[2] *= 105;
+    cost[6] *= 105;
+#pragma unroll
+    for (int n = 0; n < 7; n++) {
+        cost[0] += (unsigned)(dg0[n] * dg0[n] + dg0[14 - n] * dg0[14 - n]) * dv[n];
+        cost[4] += (unsigned)(dg1[n] * dg1[n] + dg1[14 - n] * dg1[14 - n]) * dv[n];
+    }
+    cost[0] += (unsigned)(dg0[7] * dg0[7]) * 105;
+    cost[4] += (unsigned)(dg1[7] * dg1[7]) * 105;
+#pragma unroll
+    for (int n = 0; n < 4; n++) {
+        unsigned c = 0;
+#pragma unroll
+        for (int m = 0; m < 5; m++) c += (unsigned)(al[n][3 + m] * al[n][3 + m]);
+        c *= 105;
+#pragma unroll
+        for (int m = 0; m < 3; m++)
+            c += (unsigned)(al[n][m] * al[n][m] + al[n][10 - m] * al[n][10 - m]) * dv[2 * m + 1];
+        cost[2 * n + 1] = c;
+    }
+    int best = 0;
+    unsigned bc = cost[0];
+#pragma unroll
+    for (int n = 1; n < 8; n++)
+        if (cost[n] > bc) { bc = cost[n]; best = n; }
+    *var = (bc - cost[best ^ 4]) >> 10;
+    return best;
+}
+
+// Filter one pixel at LDS position (x, y); c = centre sample. Returns the new value.
+__device__ __forceinline__ int cdef_px(const int16_t *t, int ts, int x, int y, int pri, int sec,
+                                       int dir, int damping, int bdm8) {
+    const int c = t[y * ts + x];
+    int sum = 0, mx = c;
+    unsigned mn = (unsigned)c & 0xffff;   // i16 sentinel compares as unsigned 0x8000+ (large)
+    if (pri) {
+        const int shift = max(0, damping - ulog2i(pri));
+        int tap = 4 - ((pri >> bdm8) & 1);
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int o = k_cdef_dir[dir][k][0] * ts + k_cdef_dir[dir][k][1];
+            const int a = t[y * ts + x + o], b = t[y * ts + x - o];
+            sum += tap * (constrain(a - c, pri, shift) + constrain(b - c, pri, shift));
+            tap = (tap & 3) | 2;
+            mn = min(mn, (unsigned)a & 0xffff); mx = max(mx, a);
+            mn = min(mn, (unsigned)b & 0xffff); mx = max(mx, b);
+        }
+    }
+    if (sec) {
+        const int shift = damping - ulog2i(sec);
+        const int d2 = (dir + 2) & 7, d6 = (dir + 6) & 7;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int o2 = k_cdef_dir[d2][k][0] * ts + k_cdef_dir[d2][k][1];
+            const int o3 = k_cdef_dir[d6][k][0] * ts + k_cdef_dir[d6][k][1];
+            const int s0 = t[y * ts + x + o2], s1 = t[y * ts + x - o2];
+            const int s2 = t[y * ts + x + o3], s3 = t[y * ts + x - o3];
+            sum += (2 - k) * (constrain(s0 - c, sec, shift) + constrain(s1 - c, sec, shift) +
+                              constrain(s2 - c, sec, shift) + constrain(s3 - c, sec, shift));
+            mn = min(mn, (unsigned)s0 & 0xffff); mx = max(mx, s0);
+            mn = min(mn, (unsigned)s1 & 0xffff); mx = max(mx, s1);
+            mn = min(mn, (unsigned)s2 & 0xffff); mx = max(mx, s2);
+            mn = min(mn, (unsigned)s3 & 0xffff); mx = max(mx, s3);
+        }
+    }
+    int v = c + ((sum - (sum < 0) + 8) >> 4);
+    if (pri && sec) v = min(max(v, (int)mn), mx);
+    return v;
+}
+
+template <typename Px>
+__device__ __forceinline__ void load_tile(int16_t *t, int ts, int rows, int cols, const uint8_t *src,
+                                          int64_t stride, int x0, int y0, int fw, int fh) {
+    for (int i = threadIdx.x; i < rows * cols; i += 256) {
+        const int r = i / cols, c = i % cols;
+        const int x = x0 - 2 + c, y = y0 - 2 + r;
+        int16_t v = INT16_MIN;
+        if (x >= 0 && y >= 0 && x < fw && y < fh)
+            v = (int16_t) reinterpret_cast<const Px *>(src + (int64_t)y * stride)[x];
+        t[r * ts + c] = v;
+    }
+}
+
+template <typename Px>
+__global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
+    extern __shared__ int16_t smem[];
+    const int cw = 64 >> a.ss_hor, ch = 64 >> a.ss_ver, cts = cw + 8;
+    int16_t *ty = smem;
+    int16_t *tuv[2] = { smem + kTY * kTS, smem + kTY * kTS + (ch + 4) * cts };
+    __shared__ int8_t bdir[64];
+    __shared__ int8_t bflag[64];          // bit0 luma filtered, bit1 chroma filtered
+    __shared__ int16_t bpri[64];
+
+    const int tx = blockIdx.x % a.tiles_x, tyy = blockIdx.x / a.tiles_x;
+    const int x0 = tx * 64, y0 = tyy * 64;
+    const MiAv1Filter *lf = &a.masks[(tyy >> 1) * a.sb128w + (tx >> 1)];
+    const int cdef_idx = lf->cdef_idx[(tyy & 1) * 2 + (tx & 1)];
+    const int y_lvl = cdef_idx >= 0 ? a.y_strength[cdef_idx] : 0;
+    const int uv_lvl = cdef_idx >= 0 && a.layout ? a.uv_strength[cdef_idx] : 0;
+    const int nplanes = a.layout ? 3 : 1;
+    const int fwy = a.bw4 * 4, fhy = a.bh4 * 4;
+    const int fwc = fwy >> a.ss_hor, fhc = fhy >> a.ss_ver;
+
+    if (!y_lvl && !uv_lvl) {
+        // untouched 64x64 unit: C = D
+        for (int p = 0; p < nplanes; p++) {
+            const int sh = p ? a.ss_hor : 0, sv = p ? a.ss_ver : 0;
+            const int pw = 64 >> sh, ph = 64 >> sv, px0 = x0 >> sh, py0 = y0 >> sv;
+            for (int i = threadIdx.x; i < pw * ph; i += 256) {
+                const int r = i / pw, c = i % pw;
+                const int64_t off = (int64_t)(py0 + r) * a.stride[p];
+                reinterpret_cast<Px *>(a.dst[p] + off)[px0 + c] = reinterpret_cast<const Px *>(a.src[p] + off)[px0 + c];
+            }
+        }
+        return;
+    }
+
+    const int bdm8 = a.bdm8;
+    const int y_pri = (y_lvl >> 2) << bdm8;
+    int y_sec = y_lvl & 3; y_sec += y_sec == 3; y_sec <<= bdm8;
+    const int uv_pri = (uv_lvl >> 2) << bdm8;
+    int uv_sec = uv_lvl & 3; uv_sec += uv_sec == 3; uv_sec <<= bdm8;
+
+    load_tile<Px>(ty, kTS, 68, 68, a.src[0], a.stride[0], x0, y0, fwy, fhy);
+    if (uv_lvl) {
+        load_tile<Px>(tuv[0], cts, ch + 4, cw + 4, a.src[1], a.stride[1], x0 >> a.ss_hor, y0 >> a.ss_ver, fwc, fhc);
+        load_tile<Px>(tuv[1], cts, ch + 4, cw + 4, a.src[2], a.stride[2], x0 >> a.ss_hor, y0 >> a.ss_ver, fwc, fhc);
+    }
+    __syncthreads();
+
+    if (threadIdx.x < 64) {
+        const int b = threadIdx.x, bxl = b & 7, byl = b >> 3;
+        const int bx = (x0 >> 2) + bxl * 2, by = (y0 >> 2) + byl * 2;   // 4-px units
+        int flag = 0, dir = 0, pri = 0;
+        if (bx < a.bw4 && by < a.bh4) {
+            const int by_idx = (by & 30) >> 1;
+            const unsigned noskip = (unsigned)lf->noskip_mask[by_idx][1] << 16 | lf->noskip_mask[by_idx][0];
+            if (noskip & (3u << (bx & 30))) {
+                unsigned var = 0;
+                if (y_pri || uv_pri) dir = find_dir(ty + (byl * 8 + 2) * kTS + bxl * 8 + 2, kTS, bdm8, &var);
+                if (y_pri) {
+                    pri = adjust_strength(y_pri, var);
+                    if (pri || y_sec) flag |= 1;
+                } else if (y_sec) {
+                    flag |= 1;
+                }
+                if (uv_lvl) flag |= 2;
+            }
+        }
+        bdir[b] = (int8_t)dir;
+        bflag[b] = (int8_t)flag;
+        bpri[b] = (int16_t)pri;
+    }
+    __syncthreads();
+
+    // luma
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int r = i >> 6, c = i & 63;
+        const int b = (r >> 3) * 8 + (c >> 3);
+        const int gx = x0 + c, gy = y0 + r;
+        Px *dp = reinterpret_cast<Px *>(a.dst[0] + (int64_t)gy * a.stride[0]) + gx;
+        int v;
+        if (bflag[b] & 1) {
+            const int pri = y_pri ? bpri[b] : 0;
+            const int dir = y_pri ? bdir[b] : 0;
+            v = cdef_px(ty, kTS, c + 2, r + 2, pri, y_sec, dir, a.damping, bdm8);
+        } else if (gx < fwy && gy < fhy) {
+            v = ty[(r + 2) * kTS + c + 2];
+        } else {
+            v = reinterpret_cast<const Px *>(a.src[0] + (int64_t)gy * a.stride[0])[gx];
+        }
+        *dp = (Px)v;
+    }
+    // chroma
+    if (a.layout) {
+        const int uvw = 8 >> a.ss_hor, uvh = 8 >> a.ss_ver;
+        const uint8_t dirmap422[8] = { 7, 0, 2, 4, 5, 6, 6, 6 };
+        for (int i = threadIdx.x; i < 2 * cw * ch; i += 256) {
+            const int p = 1 + i / (cw * ch), j = i % (cw * ch);
+            const int r = j / cw, c = j % cw;
+            const int b = (r / uvh) * 8 + (c / uvw);
+            const int gx = (x0 >> a.ss_hor) + c, gy = (y0 >> a.ss_ver) + r;
+            Px *dp = reinterpret_cast<Px *>(a.dst[p] + (int64_t)gy * a.stride[p]) + gx;
+            const int16_t *t = tuv[p - 1];
+            int v;
+            if (bflag[b] & 2) {
+                const int d = uv_pri ? (a.layout == 2 ? dirmap422[bdir[b]] : bdir[b]) : 0;
+                v = cdef_px(t, cts, c + 2, r + 2, uv_pri, uv_sec, d, a.damping - 1, bdm8);
+            } else {
+                v = reinterpret_cast<const Px *>(a.src[p] + (int64_t)gy * a.stride[p])[gx];
+            }
+            *dp = (Px)v;
+        }
+    }
+}
+
+int launch_cdef(const CdefArgs &a, int tiles, int bpc, hipStream_t s) {
+    if (tiles <= 0) return 0;
+    const int cw = 64 >> a.ss_hor, ch = 64 >> a.ss_ver;
+    const size_t lds = sizeof(int16_t) * (kTY * kTS + (a.layout ? 2 * (ch + 4) * (cw + 8) : 0));
+    if (bpc == 8) hipLaunchKernelGGL(cdef_kernel<uint8_t>, dim3(tiles), dim3(256), lds, s, a);
+    else hipLaunchKernelGGL(cdef_kernel<uint16_t>, dim3(tiles), dim3(256), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+} // namespace mi

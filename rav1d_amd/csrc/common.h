@@ -72,4 +72,18 @@ struct LfArgs {
 // launchers (lf.hip)
 int launch_deblock(const LfArgs &cols, const LfArgs &rows, int bpc, hipStream_t s);
 
+struct CdefArgs {
+    const uint8_t *src[3];
+    uint8_t *dst[3];
+    int64_t stride[3];
+    const MiAv1Filter *masks;
+    int sb128w, tiles_x;
+    int bw4, bh4;                 // frame size in 4-px units, 8-px aligned (f->bw, f->bh)
+    int ss_hor, ss_ver, layout;
+    int bdm8, damping;            // damping already includes bitdepth_min_8
+    uint8_t y_strength[8], uv_strength[8];
+};
+// launchers (cdef.hip)
+int launch_cdef(const CdefArgs &a, int tiles, int bpc, hipStream_t s);
+
 } // namespace mi

@@ -11,7 +11,7 @@ import ctypes
 import numpy as np
 import torch
 
-from . import MiLoopFilter, MiPicture, MiError, check, lib
+from . import MiCdef, MiLoopFilter, MiPicture, MiError, check, lib
 
 LAYOUT_I400, LAYOUT_I420, LAYOUT_I422, LAYOUT_I444 = 0, 1, 2, 3
 
@@ -145,3 +145,24 @@ def deblock_frame(ctx, frame, meta, stream=None):
     pic = frame.picture()
     check(lib().mi_deblock_frame(ctx.h, ctypes.byref(pic), ctypes.byref(meta.s), _stream_ptr(stream)),
           "mi_deblock_frame")
+
+
+class CdefMeta:
+    """Device copy of the Av1Filter array + frame CDEF params (MiCdef)."""
+
+    def __init__(self, masks, cdef, masks_dev=None):
+        self.masks = masks_dev if masks_dev is not None else \
+            torch.from_numpy(np.ascontiguousarray(masks).view(np.uint8).reshape(-1)).cuda()
+        s = MiCdef()
+        s.masks = self.masks.data_ptr()
+        s.sb128w = int(masks.shape[1])
+        s.damping = int(cdef["damping"])
+        s.y_strength[:] = [int(v) for v in cdef["y_strength"]]
+        s.uv_strength[:] = [int(v) for v in cdef["uv_strength"]]
+        self.s = s
+
+
+def cdef_frame(ctx, src, dst, meta, stream=None):
+    ps, pd = src.picture(), dst.picture()
+    check(lib().mi_cdef_frame(ctx.h, ctypes.byref(ps), ctypes.byref(pd), ctypes.byref(meta.s),
+                              _stream_ptr(stream)), "mi_cdef_frame")

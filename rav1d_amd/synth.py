@@ -301,3 +301,22 @@ def make_mixed_texture(rng, w, h, bpc):
     noise = rng.integers(-1, 2, size=(h, w)) * a + rng.integers(0, 2, size=(h, w)) * (a > 0)
     img = np.where(a == 0, (bdmax // 2 + smooth % 7) + offs, base + offs + noise)
     return np.clip(img, 0, bdmax).astype(np.uint16 if bpc > 8 else np.uint8)
+
+
+def add_cdef_meta(lf, rng, skip_frac=0.2, idx_unset_frac=0.1):
+    """Fill cdef_idx / noskip_mask of an Av1Filter array in place and draw frame CDEF params
+    within the ranges the bitstream allows (rav1d src/obu.rs cdef params: damping 3..6,
+    strengths 6 bits each)."""
+    m = lf["masks"]
+    sbh, sbw = m.shape
+    idx = rng.integers(0, 8, size=(sbh, sbw, 4)).astype(np.int8)
+    idx[rng.random((sbh, sbw, 4)) < idx_unset_frac] = -1
+    m["cdef_idx"] = idx
+    bits = (rng.random((sbh, sbw, 16, 2, 16)) >= skip_frac)
+    weights = (1 << np.arange(16)).astype(np.uint32)
+    m["noskip_mask"] = (bits * weights).sum(-1).astype(np.uint16)
+    ys = rng.integers(0, 64, size=8).astype(np.uint8)
+    uvs = rng.integers(0, 64, size=8).astype(np.uint8)
+    ys[rng.random(8) < 0.15] = 0
+    uvs[rng.random(8) < 0.15] = 0
+    return dict(damping=int(rng.integers(3, 7)), y_strength=ys, uv_strength=uvs)

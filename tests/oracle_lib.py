@@ -76,3 +76,24 @@ def deblock_frame(planes, bpc, layout, w, h, lf, sb128=1):
     f(pp, st, w, h, layout, bpc, ptr(level), lf["b4_stride"], ptr(masks), lf["sb128w"], sb128,
       ptr(e), ptr(i), lf["filter_y"], lf["filter_uv"])
     return arrs[:len(planes)]
+
+
+def cdef_frame(src_planes, bpc, layout, w, h, masks, cdef):
+    """Oracle whole-frame CDEF: returns new planes (src untouched). Planes must be 128-aligned."""
+    o = load_oracle()
+    f = o.oracle_cdef_frame
+    f.restype = None
+    f.argtypes = [_VP, _VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _VP,
+                  ctypes.c_int, ctypes.c_int, _VP, _VP]
+    srcs = [np.ascontiguousarray(p) for p in src_planes]
+    dsts = [np.zeros_like(p) for p in srcs]
+    while len(srcs) < 3:
+        srcs.append(srcs[0]); dsts.append(dsts[0])
+    sp = (ctypes.c_void_p * 3)(*[a.ctypes.data for a in srcs])
+    dp = (ctypes.c_void_p * 3)(*[a.ctypes.data for a in dsts])
+    st = (ctypes.c_ssize_t * 3)(*[a.strides[0] for a in srcs])
+    m = np.ascontiguousarray(masks)
+    ys = np.ascontiguousarray(cdef["y_strength"], np.uint8)
+    uvs = np.ascontiguousarray(cdef["uv_strength"], np.uint8)
+    f(dp, sp, st, w, h, layout, bpc, ptr(m), m.shape[1], cdef["damping"], ptr(ys), ptr(uvs))
+    return dsts[:len(src_planes)]
