@@ -99,6 +99,26 @@ typedef struct MiCdef {
     uint8_t uv_strength[8];
 } MiCdef;
 
+/* Loop-restoration unit parameters, byte-identical to Av1RestorationUnit / Av1Restoration
+ * (src/lf_mask.rs:31-38, 55-58; C src/lf_mask.h:42-62). type: Dav1dRestorationType
+ * (0 NONE, 2 WIENER, 3 + sgr_idx for SGRPROJ). */
+typedef struct MiAv1RestorationUnit {
+    uint8_t type;
+    int8_t  filter_h[3];
+    int8_t  filter_v[3];
+    int8_t  sgr_weights[2];
+} MiAv1RestorationUnit;
+typedef struct MiAv1Restoration {
+    MiAv1RestorationUnit lr[3][4];   /* [plane][64x64 quadrant of the 128x128] */
+} MiAv1Restoration;                  /* 108 bytes */
+
+typedef struct MiLr {
+    const MiAv1Restoration *lr_mask; /* device: [sb128h][sb128w] (f->lf.lr_mask) */
+    int32_t sb128w;
+    int32_t restore_planes;          /* bit0 Y, bit1 U, bit2 V (f->lf.restore_planes) */
+    int32_t unit_size_log2[2];       /* frame_hdr.restoration.unit_size[luma, chroma] */
+} MiLr;
+
 /* ------------------------------------------------------------------------------------ */
 /* Context                                                                               */
 /* ------------------------------------------------------------------------------------ */
@@ -140,6 +160,14 @@ int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, v
  * (src/cdef_apply.rs:159-507). `src` and `dst` must have identical geometry. */
 int mi_cdef_frame(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const MiCdef *cdef,
                   void *stream);
+
+/* Loop restoration for a whole frame: reads the CDEF output `cdef` inside each 64-row stripe
+ * and the deblocked picture `deblocked` for the rows across stripe edges (the rows the
+ * reference keeps in f->lf.lr_lpf_line, src/lf_apply.rs:24-141), writes `dst`. Planes not
+ * in restore_planes, and units of type NONE, are copied. Replaces rav1d_lr_sbrow
+ * (src/lr_apply.rs:261-329). All three pictures share one geometry. */
+int mi_lr_frame(MiCtx *ctx, const MiPicture *cdef, const MiPicture *deblocked,
+                const MiPicture *dst, const MiLr *lr, void *stream);
 
 /* ------------------------------------------------------------------------------------ */
 /* Table-compatible per-call entry points                                                */

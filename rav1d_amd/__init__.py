@@ -40,6 +40,11 @@ class MiCdef(ctypes.Structure):
                 ("y_strength", ctypes.c_uint8 * 8), ("uv_strength", ctypes.c_uint8 * 8)]
 
 
+class MiLr(ctypes.Structure):
+    _fields_ = [("lr_mask", ctypes.c_void_p), ("sb128w", ctypes.c_int32), ("restore_planes", ctypes.c_int32),
+                ("unit_size_log2", ctypes.c_int32 * 2)]
+
+
 TXBLOCK_DTYPE = np.dtype([("coef_off", "<u4"), ("x", "<u2"), ("y", "<u2"), ("plane", "u1"),
                           ("tx", "u1"), ("txtp", "u1"), ("flags", "u1"), ("eob", "<i4")])
 assert TXBLOCK_DTYPE.itemsize == 16
@@ -76,13 +81,16 @@ def lib():
     _sig(L, "mi_deblock_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiLoopFilter), _VP])
     _sig(L, "mi_cdef_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
                                             ctypes.POINTER(MiCdef), _VP])
+    _sig(L, "mi_lr_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
+                                          ctypes.POINTER(MiPicture), ctypes.POINTER(MiLr), _VP])
     _lib = L
     return L
 
 
 # Every symbol include/mi_av1dsp.h declares (checked by tests/test_abi.py).
 EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
-            "mi_itx_frame", "mi_deblock_frame", "mi_cdef_frame", "mi_dsp_itxfm_add"]
+            "mi_itx_frame", "mi_deblock_frame", "mi_cdef_frame", "mi_lr_frame",
+            "mi_dsp_itxfm_add"]
 
 
 def check(rc, what):

@@ -184,6 +184,57 @@ int mi_cdef_frame(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const 
     return r ? fail(ctx, -EIO) : 0;
 }
 
+static bool same_geometry(const MiPicture *a, const MiPicture *b) {
+    return a->bpc == b->bpc && a->w == b->w && a->h == b->h && a->layout == b->layout &&
+           a->stride[0] == b->stride[0] && a->stride[1] == b->stride[1];
+}
+
+int mi_lr_frame(MiCtx *ctx, const MiPicture *cdef, const MiPicture *deblocked, const MiPicture *dst,
+                const MiLr *lr, void *stream) {
+    if (!ctx || !cdef || !deblocked || !dst || !lr) return fail(ctx, -EINVAL);
+    if (!same_geometry(cdef, deblocked) || !same_geometry(cdef, dst)) return fail(ctx, -EINVAL);
+    if (cdef->bpc != 8 && cdef->bpc != 10 && cdef->bpc != 12) return fail(ctx, -EINVAL);
+    if (lr->restore_planes && (!lr->lr_mask || lr->sb128w != (cdef->w + 127) >> 7)) return fail(ctx, -EINVAL);
+    const int ss_hor = cdef->layout == 1 || cdef->layout == 2, ss_ver = cdef->layout == 1;
+    for (int c = 0; c < 2; c++) {
+        const int l2 = lr->unit_size_log2[c];
+        if ((lr->restore_planes & (c ? 6 : 1)) && (l2 < 5 || l2 > 8)) return fail(ctx, -EINVAL);
+    }
+    mi::LrArgs a;
+    memset(&a, 0, sizeof(a));
+    a.lr_mask = lr->lr_mask;
+    a.sb128w = lr->sb128w;
+    a.restore = lr->restore_planes;
+    a.bd = cdef->bpc;
+    a.ss_hor = ss_hor;
+    a.ss_ver = ss_ver;
+    a.unit_log2[0] = lr->unit_size_log2[0];
+    a.unit_log2[1] = lr->unit_size_log2[1];
+    const int nplanes = cdef->layout ? 3 : 1;
+    int nb = 0;
+    for (int p = 0; p < 3; p++) {
+        a.blk_start[p] = nb;
+        if (p >= nplanes) continue;
+        a.src[p] = (const uint8_t *)cdef->data[p];
+        a.lpf[p] = (const uint8_t *)deblocked->data[p];
+        a.dst[p] = (uint8_t *)dst->data[p];
+        a.stride[p] = cdef->stride[p ? 1 : 0];
+        const int sh = p ? ss_hor : 0, sv = p ? ss_ver : 0;
+        a.pw[p] = (cdef->w + sh) >> sh;
+        a.ph[p] = (cdef->h + sv) >> sv;
+        const int us = 1 << lr->unit_size_log2[p ? 1 : 0];
+        a.tw[p] = ((a.restore >> p) & 1) && us < 64 ? 32 : 64;
+        a.tiles_x[p] = (a.pw[p] + a.tw[p] - 1) / a.tw[p];
+        // stripes: 64 luma rows, the first 56 (lr_apply.rs:54)
+        int stripes = 0;
+        while ((stripes ? (64 * stripes - 8) >> sv : 0) < a.ph[p]) stripes++;
+        nb += stripes * a.tiles_x[p];
+    }
+    a.blk_start[3] = nb;
+    const int r = mi::launch_lr(a, cdef->bpc, (hipStream_t)stream);
+    return r ? fail(ctx, -EIO) : 0;
+}
+
 // ---- table-compatible per-call entry points ------------------------------------------
 
 int mi_dsp_itxfm_add(int tx, int txtp, void *dst, ptrdiff_t stride, void *coeff, int eob,

@@ -86,4 +86,18 @@ struct CdefArgs {
 // launchers (cdef.hip)
 int launch_cdef(const CdefArgs &a, int tiles, int bpc, hipStream_t s);
 
+struct LrArgs {
+    const uint8_t *src[3];        // CDEF output C
+    const uint8_t *lpf[3];        // deblocked D (rows across stripe edges)
+    uint8_t *dst[3];
+    int64_t stride[3];
+    const MiAv1Restoration *lr_mask;
+    int sb128w, restore, bd, ss_hor, ss_ver;
+    int unit_log2[2];
+    int pw[3], ph[3], tw[3], tiles_x[3];
+    int blk_start[4];
+};
+// launchers (lr.hip)
+int launch_lr(const LrArgs &a, int bpc, hipStream_t s);
+
 } // namespace mi

@@ -1,0 +1,248 @@
+// lr.hip — whole-frame loop restoration (Wiener / self-guided) on gfx950.
+//
+// Replaces rav1d_lr_sbrow / lr_sbrow / lr_stripe (rav1d src/lr_apply.rs:28-329) and the DSP
+// lr.wiener[2] / lr.sgr[3] (src/looprestoration.rs:139-912; C looprestoration_tmpl.c).
+//
+// The reference works in place, unit by unit, keeping the pre-LR left columns of the previous
+// unit and a line buffer of deblocked rows around every stripe boundary. Reading the CDEF output
+// C (immutable) inside the stripe and the deblocked picture D for the rows beyond a stripe edge
+// gives exactly the samples it sees, so every (stripe, 32/64-px column tile) is independent:
+// one 256-lane workgroup each, the (h+6) x (w+6) window staged once in LDS, both filter passes
+// (or the box sums and the A/B maps of the self-guided filter) computed from LDS, and the
+// output streamed to a separate picture O.
+#include "common.h"
+
+namespace mi {
+
+constexpr int kLrWin = 72;             // LDS window row stride (ints), >= 64 + 6
+constexpr int kLrAB = 68;              // A/B row stride
+
+__constant__ uint16_t k_sgr_params[16][2] = {
+    { 140, 3236 }, { 112, 2158 }, { 93, 1618 }, { 80, 1438 }, { 70, 1295 }, { 58, 1177 },
+    { 47, 1079 },  { 37, 996 },   { 30, 925 },  { 25, 863 },  { 0, 2589 },  { 0, 1618 },
+    { 0, 1177 },   { 0, 925 },    { 56, 0 },    { 22, 0 },
+};
+
+__device__ __forceinline__ unsigned sgr_x_by_x(unsigned z) {
+    // round(256 / (z + 1)), pinned to 255 at z = 0 and 0 at z = 255 (dav1d_sgr_x_by_x)
+    if (z == 0) return 255;
+    if (z >= 255) return 0;
+    return (256 + ((z + 1) >> 1)) / (z + 1);
+}
+
+template <typename Px>
+__device__ __forceinline__ int ld_px(const uint8_t *base, int64_t stride, int y, int x) {
+    return reinterpret_cast<const Px *>(base + (int64_t)y * stride)[x];
+}
+
+// Self-guided A/B maps for radius r (n = 25 or 9) over rows -1..sh (every other row for 5x5),
+// cols -1..tw. A holds the "b" term, B holds x, as after the reference's inversion.
+__device__ void sgr_ab(const int *win, int *A, int *B, int sh, int tw, int r, unsigned s,
+                       int bdm8) {
+    const int n = (2 * r + 1) * (2 * r + 1);
+    const unsigned one_by_x = n == 25 ? 164 : 455;
+    const int step = r == 2 ? 2 : 1;
+    const int nrows = r == 2 ? (sh + 3) / 2 : sh + 2;      // rows -1, -1+step, ... < sh+1
+    const int ncols = tw + 2;
+    for (int i = threadIdx.x; i < nrows * ncols; i += 256) {
+        const int jr = i / ncols, ic = i % ncols;
+        const int y = -1 + jr * step, x = ic - 1;
+        int sum = 0, sq = 0;
+        for (int dy = -r; dy <= r; dy++) {
+            const int *row = win + (y + 3 + dy) * kLrWin + x + 3;
+            for (int dx = -r; dx <= r; dx++) {
+                const int v = row[dx];
+                sum += v;
+                sq += v * v;
+            }
+        }
+        const int a = (sq + ((1 << (2 * bdm8)) >> 1)) >> (2 * bdm8);
+        const int b = (sum + ((1 << bdm8) >> 1)) >> bdm8;
+        const unsigned p = (unsigned)max(a * n - b * b, 0);
+        const unsigned z = (p * s + (1u << 19)) >> 20;
+        const unsigned xv = sgr_x_by_x(z);
+        A[(y + 1) * kLrAB + x + 1] = (int)((xv * (unsigned)sum * one_by_x + (1u << 11)) >> 12);
+        B[(y + 1) * kLrAB + x + 1] = (int)xv;
+    }
+}
+
+// Self-guided output term for pixel (j, i) (looprestoration.rs selfguided_filter tail).
+__device__ __forceinline__ int sgr_px(const int *A, const int *B, int j, int i, int src, int r) {
+#define AA(y, x) A[((y) + 1) * kLrAB + (x) + 1]
+#define BB(y, x) B[((y) + 1) * kLrAB + (x) + 1]
+    if (r == 2) {
+        if (!(j & 1)) {
+            const int a = (BB(j - 1, i) + BB(j + 1, i)) * 6 +
+                          (BB(j - 1, i - 1) + BB(j + 1, i - 1) + BB(j - 1, i + 1) + BB(j + 1, i + 1)) * 5;
+            const int b = (AA(j - 1, i) + AA(j + 1, i)) * 6 +
+                          (AA(j - 1, i - 1) + AA(j + 1, i - 1) + AA(j - 1, i + 1) + AA(j + 1, i + 1)) * 5;
+            return (b - a * src + (1 << 8)) >> 9;
+        }
+        const int a = BB(j, i) * 6 + (BB(j, i - 1) + BB(j, i + 1)) * 5;
+        const int b = AA(j, i) * 6 + (AA(j, i - 1) + AA(j, i + 1)) * 5;
+        return (b - a * src + (1 << 7)) >> 8;
+    }
+    const int a = (BB(j, i) + BB(j, i - 1) + BB(j, i + 1) + BB(j - 1, i) + BB(j + 1, i)) * 4 +
+                  (BB(j - 1, i - 1) + BB(j + 1, i - 1) + BB(j - 1, i + 1) + BB(j + 1, i + 1)) * 3;
+    const int b = (AA(j, i) + AA(j, i - 1) + AA(j, i + 1) + AA(j - 1, i) + AA(j + 1, i)) * 4 +
+                  (AA(j - 1, i - 1) + AA(j + 1, i - 1) + AA(j - 1, i + 1) + AA(j + 1, i + 1)) * 3;
+    return (b - a * src + (1 << 8)) >> 9;
+#undef AA
+#undef BB
+}
+
+// Stripe (64 luma rows, offset 8 up; first stripe 56) -> plane rows.
+__device__ __forceinline__ int stripe_start(int k, int ssv) { return k ? (64 * k - 8) >> ssv : 0; }
+
+template <typename Px>
+__global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
+    extern __shared__ int lsm[];
+    int *win = lsm;                                    // [70][kLrWin]
+    int *A = win + 70 * kLrWin;                        // [66][kLrAB]
+    int *B = A + 66 * kLrAB;                           // [66][kLrAB]
+    int *hor = A;                                      // Wiener: [70][64] aliases A/B
+
+    const int blk = blockIdx.x;
+    const int p = blk < a.blk_start[1] ? 0 : blk < a.blk_start[2] ? 1 : 2;
+    const int lb = blk - a.blk_start[p];
+    const int tiles = a.tiles_x[p];
+    const int k = lb / tiles, ti = lb % tiles;
+    const int ssv = p ? a.ss_ver : 0, ssh = p ? a.ss_hor : 0;
+    const int pw = a.pw[p], ph = a.ph[p];
+    const int tw_full = a.tw[p];
+    const int x0 = ti * tw_full;
+    const int tw = min(tw_full, pw - x0);
+    const int S = stripe_start(k, ssv);
+    const int E = min(stripe_start(k + 1, ssv), ph);
+    const int sh = E - S;
+    const uint8_t *C = a.src[p];
+    const uint8_t *D = a.lpf[p];
+    uint8_t *O = a.dst[p];
+    const int64_t st = a.stride[p];
+
+    // restoration unit of this tile (lr_apply.rs:151-259 indexing)
+    int type = 0;
+    const MiAv1RestorationUnit *u = nullptr;
+    if (a.restore & (1 << p)) {
+        const int us = 1 << a.unit_log2[p ? 1 : 0];
+        const int nu = max(1, (pw + (us >> 1)) / us);
+        const int uc = min(x0 / us, nu - 1);
+        const int xu = uc * us;
+        int ay = ((64 * k) >> ssv) & ~(us - 1);
+        if (ay && ay + (us >> 1) > ph) ay -= us;
+        ay <<= ssv;
+        const int sbi = (ay >> 7) * a.sb128w + (xu >> (7 - ssh));
+        const int ui = (((ay >> 6) & 1) << 1) + ((xu >> (6 - ssh)) & 1);
+        u = &a.lr_mask[sbi].lr[p][ui];
+        type = u->type;
+    }
+    if (type == 0) {   // RESTORATION_NONE: O = C
+        for (int i = threadIdx.x; i < sh * tw; i += 256) {
+            const int r = i / tw, c = i % tw;
+            reinterpret_cast<Px *>(O + (int64_t)(S + r) * st)[x0 + c] = (Px)ld_px<Px>(C, st, S + r, x0 + c);
+        }
+        return;
+    }
+
+    // ---- stage the (sh+6) x (tw+6) window (C inside the stripe, D across its edges) ----
+    const bool have_top = k > 0, have_bottom = E < ph;
+    const int wr = sh + 6, wc = tw + 6;
+    for (int i = threadIdx.x; i < wr * wc; i += 256) {
+        const int r = i / wc - 3, c = i % wc - 3;
+        const int cc = min(max(x0 + c, 0), pw - 1);
+        int v;
+        if (r >= 0 && r < sh) v = ld_px<Px>(C, st, S + r, cc);
+        else if (r < 0) v = have_top ? ld_px<Px>(D, st, S - 2 + (r == -1), cc) : ld_px<Px>(C, st, S, cc);
+        else v = have_bottom ? ld_px<Px>(D, st, min(E + (r > sh), ph - 1), cc) : ld_px<Px>(C, st, E - 1, cc);
+        win[(r + 3) * kLrWin + c + 3] = v;
+    }
+    __syncthreads();
+
+    const int bd = a.bd, bdmax = (1 << bd) - 1;
+    if (type == 2) {
+        // ---- Wiener (looprestoration.rs:299-370) ----
+        int fh[7], fv[7];
+        fh[0] = fh[6] = u->filter_h[0]; fh[1] = fh[5] = u->filter_h[1]; fh[2] = fh[4] = u->filter_h[2];
+        fh[3] = 128 - 2 * (fh[0] + fh[1] + fh[2]);
+        fv[0] = fv[6] = u->filter_v[0]; fv[1] = fv[5] = u->filter_v[1]; fv[2] = fv[4] = u->filter_v[2];
+        fv[3] = 128 - 2 * (fv[0] + fv[1] + fv[2]);
+        const int rbh = bd == 12 ? 5 : 3, rbv = bd == 12 ? 9 : 11;
+        const int clip_h = (1 << (bd + 1 + 7 - rbh)) - 1;
+        for (int i = threadIdx.x; i < wr * tw; i += 256) {
+            const int r = i / tw, c = i % tw;
+            const int *row = win + r * kLrWin + c;
+            int sum = 1 << (bd + 6);
+#pragma unroll
+            for (int t = 0; t < 7; t++) sum += row[t] * fh[t];
+            hor[r * 64 + c] = min(max((sum + (1 << (rbh - 1))) >> rbh, 0), clip_h);
+        }
+        __syncthreads();
+        const int off = 1 << (bd + rbv - 1);
+        for (int i = threadIdx.x; i < sh * tw; i += 256) {
+            const int r = i / tw, c = i % tw;
+            int sum = -off;
+#pragma unroll
+            for (int t = 0; t < 7; t++) sum += hor[(r + t) * 64 + c] * fv[t];
+            const int v = min(max((sum + (1 << (rbv - 1))) >> rbv, 0), bdmax);
+            reinterpret_cast<Px *>(O + (int64_t)(S + r) * st)[x0 + c] = (Px)v;
+        }
+        return;
+    }
+
+    // ---- self-guided (looprestoration.rs:566-912) ----
+    const int sidx = type - 3;
+    const int s0 = k_sgr_params[sidx][0], s1 = k_sgr_params[sidx][1];
+    const int w0 = u->sgr_weights[0];
+    const int w1 = 128 - (u->sgr_weights[0] + u->sgr_weights[1]);
+    const int bdm8 = bd - 8;
+    constexpr int kMaxPx = 16;                         // 64x64 / 256 lanes
+    int acc[kMaxPx];
+#pragma unroll
+    for (int q = 0; q < kMaxPx; q++) acc[q] = 0;
+    if (s0) {
+        sgr_ab(win, A, B, sh, tw, 2, (unsigned)s0, bdm8);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kMaxPx; q++) {
+            const int i = threadIdx.x + q * 256;
+            if (i < sh * tw) {
+                const int r = i / tw, c = i % tw;
+                acc[q] += w0 * sgr_px(A, B, r, c, win[(r + 3) * kLrWin + c + 3], 2);
+            }
+        }
+        __syncthreads();
+    }
+    if (s1) {
+        sgr_ab(win, A, B, sh, tw, 1, (unsigned)s1, bdm8);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kMaxPx; q++) {
+            const int i = threadIdx.x + q * 256;
+            if (i < sh * tw) {
+                const int r = i / tw, c = i % tw;
+                acc[q] += w1 * sgr_px(A, B, r, c, win[(r + 3) * kLrWin + c + 3], 1);
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < kMaxPx; q++) {
+        const int i = threadIdx.x + q * 256;
+        if (i < sh * tw) {
+            const int r = i / tw, c = i % tw;
+            const int px = win[(r + 3) * kLrWin + c + 3];
+            const int v = min(max(px + ((acc[q] + (1 << 10)) >> 11), 0), bdmax);
+            reinterpret_cast<Px *>(O + (int64_t)(S + r) * st)[x0 + c] = (Px)v;
+        }
+    }
+}
+
+int launch_lr(const LrArgs &a, int bpc, hipStream_t s) {
+    const int n = a.blk_start[3];
+    if (n <= 0) return 0;
+    const size_t lds = sizeof(int) * (70 * kLrWin + 2 * 66 * kLrAB);
+    if (bpc == 8) hipLaunchKernelGGL(lr_kernel<uint8_t>, dim3(n), dim3(256), lds, s, a);
+    else hipLaunchKernelGGL(lr_kernel<uint16_t>, dim3(n), dim3(256), lds, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+} // namespace mi

@@ -11,7 +11,7 @@ import ctypes
 import numpy as np
 import torch
 
-from . import MiCdef, MiLoopFilter, MiPicture, MiError, check, lib
+from . import MiCdef, MiLoopFilter, MiLr, MiPicture, MiError, check, lib
 
 LAYOUT_I400, LAYOUT_I420, LAYOUT_I422, LAYOUT_I444 = 0, 1, 2, 3
 
@@ -166,3 +166,23 @@ def cdef_frame(ctx, src, dst, meta, stream=None):
     ps, pd = src.picture(), dst.picture()
     check(lib().mi_cdef_frame(ctx.h, ctypes.byref(ps), ctypes.byref(pd), ctypes.byref(meta.s),
                               _stream_ptr(stream)), "mi_cdef_frame")
+
+
+class LrMeta:
+    """Device copy of the Av1Restoration array + frame LR params (MiLr)."""
+
+    def __init__(self, lr):
+        m = np.ascontiguousarray(lr["lr_mask"])
+        self.mask = torch.from_numpy(m.view(np.uint8).reshape(-1)).cuda()
+        s = MiLr()
+        s.lr_mask = self.mask.data_ptr()
+        s.sb128w = int(m.shape[1])
+        s.restore_planes = int(lr["restore_planes"])
+        s.unit_size_log2[0], s.unit_size_log2[1] = [int(v) for v in lr["unit_size_log2"]]
+        self.s = s
+
+
+def lr_frame(ctx, cdef, deblocked, dst, meta, stream=None):
+    pc, pd, po = cdef.picture(), deblocked.picture(), dst.picture()
+    check(lib().mi_lr_frame(ctx.h, ctypes.byref(pc), ctypes.byref(pd), ctypes.byref(po),
+                            ctypes.byref(meta.s), _stream_ptr(stream)), "mi_lr_frame")

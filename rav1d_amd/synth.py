@@ -320,3 +320,52 @@ def add_cdef_meta(lf, rng, skip_frac=0.2, idx_unset_frac=0.1):
     ys[rng.random(8) < 0.15] = 0
     uvs[rng.random(8) < 0.15] = 0
     return dict(damping=int(rng.integers(3, 7)), y_strength=ys, uv_strength=uvs)
+
+
+# ---------------------------------------------------------------------------------------
+# Loop-restoration units (Av1Restoration per 128x128: lr[3 planes][4 units]), with the
+# parameter ranges read_restoration_info can code (rav1d src/decode.rs:3786-3838).
+# ---------------------------------------------------------------------------------------
+
+RESTUNIT_DTYPE = np.dtype([("type", "u1"), ("filter_h", "i1", (3,)), ("filter_v", "i1", (3,)),
+                           ("sgr_weights", "i1", (2,))])
+AV1RESTORATION_DTYPE = np.dtype([("lr", RESTUNIT_DTYPE, (3, 4))])
+assert AV1RESTORATION_DTYPE.itemsize == 108
+RESTORATION_NONE, RESTORATION_SWITCHABLE, RESTORATION_WIENER, RESTORATION_SGRPROJ = 0, 1, 2, 3
+
+SGR_PARAMS = [(140, 3236), (112, 2158), (93, 1618), (80, 1438), (70, 1295), (58, 1177), (47, 1079),
+              (37, 996), (30, 925), (25, 863), (0, 2589), (0, 1618), (0, 1177), (0, 925), (56, 0),
+              (22, 0)]
+
+
+def make_lr_meta(w, h, layout, rng, sb128=1, unit_log2=None, p_none=0.2, p_wiener=0.4):
+    sbw, sbh = (w + 127) >> 7, (h + 127) >> 7
+    m = np.zeros((sbh, sbw), AV1RESTORATION_DTYPE)
+    u = m["lr"]  # (sbh, sbw, 3, 4)
+    shape = u.shape
+    r = rng.random(shape)
+    typ = np.where(r < p_none, RESTORATION_NONE,
+                   np.where(r < p_none + p_wiener, RESTORATION_WIENER,
+                            RESTORATION_SGRPROJ + rng.integers(0, 16, size=shape)))
+    u["type"] = typ
+    fh = np.stack([rng.integers(-5, 11, size=shape), rng.integers(-23, 9, size=shape),
+                   rng.integers(-17, 47, size=shape)], -1)
+    fv = np.stack([rng.integers(-5, 11, size=shape), rng.integers(-23, 9, size=shape),
+                   rng.integers(-17, 47, size=shape)], -1)
+    fh[:, :, 1:, :, 0] = 0   # chroma wiener is 5-tap
+    fv[:, :, 1:, :, 0] = 0
+    u["filter_h"] = fh
+    u["filter_v"] = fv
+    sidx = np.clip(typ - RESTORATION_SGRPROJ, 0, 15)
+    s0 = np.array([p[0] for p in SGR_PARAMS])[sidx]
+    s1 = np.array([p[1] for p in SGR_PARAMS])[sidx]
+    w0 = np.where(s0 == 0, 0, rng.integers(-96, 32, size=shape))
+    w1 = np.where(s1 == 0, 95, rng.integers(-32, 96, size=shape))
+    u["sgr_weights"] = np.stack([w0, w1], -1)
+    m["lr"] = u
+    if unit_log2 is None:
+        ly = int(rng.integers(6 + sb128, 9))
+        lc = max(5, ly - int(rng.integers(0, 2))) if layout == 1 else ly
+        unit_log2 = (ly, lc)
+    return dict(lr_mask=m, unit_size_log2=tuple(unit_log2), restore_planes=7 if layout else 1,
+                sb128=sb128)

@@ -97,3 +97,24 @@ def cdef_frame(src_planes, bpc, layout, w, h, masks, cdef):
     uvs = np.ascontiguousarray(cdef["uv_strength"], np.uint8)
     f(dp, sp, st, w, h, layout, bpc, ptr(m), m.shape[1], cdef["damping"], ptr(ys), ptr(uvs))
     return dsts[:len(src_planes)]
+
+
+def lr_frame(cdef_planes, deblocked_planes, bpc, layout, w, h, lr):
+    """Oracle whole-frame loop restoration (in-place reference algorithm on a copy)."""
+    o = load_oracle()
+    f = o.oracle_lr_frame
+    f.restype = None
+    f.argtypes = [_VP, _VP, _VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                  ctypes.c_int, ctypes.c_int, _VP, _VP, ctypes.c_int]
+    c = [np.ascontiguousarray(p) for p in cdef_planes]
+    d = [np.ascontiguousarray(p) for p in deblocked_planes]
+    o_ = [np.zeros_like(p) for p in c]
+    while len(c) < 3:
+        c.append(c[0]); d.append(d[0]); o_.append(o_[0])
+    arr = lambda L: (ctypes.c_void_p * 3)(*[a.ctypes.data for a in L])
+    st = (ctypes.c_ssize_t * 3)(*[a.strides[0] for a in c])
+    ul = np.array(lr["unit_size_log2"], np.int32)
+    m = np.ascontiguousarray(lr["lr_mask"])
+    f(arr(o_), arr(c), arr(d), st, w, h, layout, bpc, lr["sb128"], lr["restore_planes"], ptr(ul),
+      ptr(m), m.shape[1])
+    return o_[:len(cdef_planes)]
