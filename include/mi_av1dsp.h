@@ -119,6 +119,28 @@ typedef struct MiLr {
     int32_t unit_size_log2[2];       /* frame_hdr.restoration.unit_size[luma, chroma] */
 } MiLr;
 
+/* Film-grain parameters, byte-identical to Dav1dFilmGrainData (include/dav1d/headers.h:
+ * 315-333; Rust Rav1dFilmGrainData include/dav1d/headers.rs:1585-1610). */
+typedef struct MiFilmGrainData {
+    unsigned seed;
+    int num_y_points;
+    uint8_t y_points[14][2];
+    int chroma_scaling_from_luma;
+    int num_uv_points[2];
+    uint8_t uv_points[2][10][2];
+    int scaling_shift;
+    int ar_coeff_lag;
+    int8_t ar_coeffs_y[24];
+    int8_t ar_coeffs_uv[2][25 + 3];
+    uint64_t ar_coeff_shift;
+    int grain_scale_shift;
+    int uv_mult[2];
+    int uv_luma_mult[2];
+    int uv_offset[2];
+    int overlap_flag;
+    int clip_to_restricted_range;
+} MiFilmGrainData;
+
 /* ------------------------------------------------------------------------------------ */
 /* Context                                                                               */
 /* ------------------------------------------------------------------------------------ */
@@ -168,6 +190,17 @@ int mi_cdef_frame(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const 
  * (src/lr_apply.rs:261-329). All three pictures share one geometry. */
 int mi_lr_frame(MiCtx *ctx, const MiPicture *cdef, const MiPicture *deblocked,
                 const MiPicture *dst, const MiLr *lr, void *stream);
+
+/* Film grain (output only; reference frames stay grain-free): out = in + grain. Replaces
+ * rav1d_apply_grain (src/fg_apply.rs:272-284 = prep_grain + apply_grain_row per 32 rows).
+ * mtrx_identity: seq_hdr.mtrx == DAV1D_MC_IDENTITY (restricted-range chroma clip).
+ * The split form lets a caller run the pixel-independent prep (grain templates, scaling
+ * LUTs, block offsets) on a side stream at frame start; apply uses the context's last prep. */
+int mi_film_grain_frame(MiCtx *ctx, const MiPicture *in, const MiPicture *out,
+                        const MiFilmGrainData *data, int mtrx_identity, void *stream);
+int mi_film_grain_prep(MiCtx *ctx, const MiPicture *in, const MiFilmGrainData *data, void *stream);
+int mi_film_grain_apply(MiCtx *ctx, const MiPicture *in, const MiPicture *out,
+                        const MiFilmGrainData *data, int mtrx_identity, void *stream);
 
 /* ------------------------------------------------------------------------------------ */
 /* Table-compatible per-call entry points                                                */

@@ -45,6 +45,19 @@ class MiLr(ctypes.Structure):
                 ("unit_size_log2", ctypes.c_int32 * 2)]
 
 
+class MiFilmGrainData(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint), ("num_y_points", ctypes.c_int), ("y_points", (ctypes.c_uint8 * 2) * 14),
+                ("chroma_scaling_from_luma", ctypes.c_int), ("num_uv_points", ctypes.c_int * 2),
+                ("uv_points", ((ctypes.c_uint8 * 2) * 10) * 2), ("scaling_shift", ctypes.c_int),
+                ("ar_coeff_lag", ctypes.c_int), ("ar_coeffs_y", ctypes.c_int8 * 24),
+                ("ar_coeffs_uv", (ctypes.c_int8 * 28) * 2), ("ar_coeff_shift", ctypes.c_uint64),
+                ("grain_scale_shift", ctypes.c_int), ("uv_mult", ctypes.c_int * 2), ("uv_luma_mult", ctypes.c_int * 2),
+                ("uv_offset", ctypes.c_int * 2), ("overlap_flag", ctypes.c_int), ("clip_to_restricted_range", ctypes.c_int)]
+
+
+assert ctypes.sizeof(MiFilmGrainData) == 224
+
+
 TXBLOCK_DTYPE = np.dtype([("coef_off", "<u4"), ("x", "<u2"), ("y", "<u2"), ("plane", "u1"),
                           ("tx", "u1"), ("txtp", "u1"), ("flags", "u1"), ("eob", "<i4")])
 assert TXBLOCK_DTYPE.itemsize == 16
@@ -83,6 +96,10 @@ def lib():
                                             ctypes.POINTER(MiCdef), _VP])
     _sig(L, "mi_lr_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
                                           ctypes.POINTER(MiPicture), ctypes.POINTER(MiLr), _VP])
+    for n in ("mi_film_grain_frame", "mi_film_grain_apply"):
+        _sig(L, n, ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
+                                  ctypes.POINTER(MiFilmGrainData), ctypes.c_int, _VP])
+    _sig(L, "mi_film_grain_prep", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiFilmGrainData), _VP])
     _lib = L
     return L
 
@@ -90,6 +107,7 @@ def lib():
 # Every symbol include/mi_av1dsp.h declares (checked by tests/test_abi.py).
 EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
             "mi_itx_frame", "mi_deblock_frame", "mi_cdef_frame", "mi_lr_frame",
+            "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply",
             "mi_dsp_itxfm_add"]
 
 

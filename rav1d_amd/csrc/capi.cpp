@@ -13,6 +13,16 @@
 struct MiCtx {
     int device = 0;
     int last_error = 0;
+    // film-grain scratch (grain templates, scaling LUTs, block offsets)
+    int16_t *fg_lut = nullptr;
+    uint8_t *fg_scaling = nullptr;
+    uint8_t *fg_offsets = nullptr;
+    size_t fg_offsets_bytes = 0;
+    ~MiCtx() {
+        if (fg_lut) (void)hipFree(fg_lut);
+        if (fg_scaling) (void)hipFree(fg_scaling);
+        if (fg_offsets) (void)hipFree(fg_offsets);
+    }
 };
 
 namespace {
@@ -52,6 +62,11 @@ struct CallState {
     }
 };
 CallState g_call;
+
+bool same_geometry(const MiPicture *a, const MiPicture *b) {
+    return a->bpc == b->bpc && a->w == b->w && a->h == b->h && a->layout == b->layout &&
+           a->stride[0] == b->stride[0] && a->stride[1] == b->stride[1];
+}
 
 } // namespace
 
@@ -184,11 +199,6 @@ int mi_cdef_frame(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const 
     return r ? fail(ctx, -EIO) : 0;
 }
 
-static bool same_geometry(const MiPicture *a, const MiPicture *b) {
-    return a->bpc == b->bpc && a->w == b->w && a->h == b->h && a->layout == b->layout &&
-           a->stride[0] == b->stride[0] && a->stride[1] == b->stride[1];
-}
-
 int mi_lr_frame(MiCtx *ctx, const MiPicture *cdef, const MiPicture *deblocked, const MiPicture *dst,
                 const MiLr *lr, void *stream) {
     if (!ctx || !cdef || !deblocked || !dst || !lr) return fail(ctx, -EINVAL);
@@ -233,6 +243,86 @@ int mi_lr_frame(MiCtx *ctx, const MiPicture *cdef, const MiPicture *deblocked, c
     a.blk_start[3] = nb;
     const int r = mi::launch_lr(a, cdef->bpc, (hipStream_t)stream);
     return r ? fail(ctx, -EIO) : 0;
+}
+
+static int fg_setup(MiCtx *ctx, const MiPicture *in, const MiPicture *out, const MiFilmGrainData *data,
+                    int is_id, mi::FgArgs &a) {
+    static std::once_flag once;
+    static int tables_rc = 0;
+    std::call_once(once, [] { tables_rc = mi::init_fg_tables(); });
+    if (tables_rc) return -EIO;
+    if (in->bpc != 8 && in->bpc != 10 && in->bpc != 12) return -EINVAL;
+    if (data->num_y_points < 0 || data->num_y_points > 14 || data->ar_coeff_lag < 0 || data->ar_coeff_lag > 3 ||
+        data->num_uv_points[0] < 0 || data->num_uv_points[0] > 10 || data->num_uv_points[1] < 0 ||
+        data->num_uv_points[1] > 10 || data->ar_coeff_shift < 6 || data->ar_coeff_shift > 9)
+        return -EINVAL;
+    memset(&a, 0, sizeof(a));
+    a.data = *data;
+    a.bpc = in->bpc;
+    a.layout = in->layout;
+    a.ss_x = in->layout == 1 || in->layout == 2;
+    a.ss_y = in->layout == 1;
+    a.w = in->w;
+    a.h = in->h;
+    a.is_id = is_id;
+    a.nrows = (in->h + 31) >> 5;
+    a.nblocks = (in->w + 31) >> 5;
+    if (!ctx->fg_lut && hipMalloc(&ctx->fg_lut, 3 * 73 * 82 * sizeof(int16_t)) != hipSuccess) return -ENOMEM;
+    if (!ctx->fg_scaling && hipMalloc(&ctx->fg_scaling, 3 * 4096) != hipSuccess) return -ENOMEM;
+    const size_t ob = (size_t)a.nrows * a.nblocks;
+    if (ob > ctx->fg_offsets_bytes) {
+        if (ctx->fg_offsets) (void)hipFree(ctx->fg_offsets);
+        ctx->fg_offsets = nullptr;
+        if (hipMalloc(&ctx->fg_offsets, ob) != hipSuccess) return -ENOMEM;
+        ctx->fg_offsets_bytes = ob;
+    }
+    a.lut = ctx->fg_lut;
+    a.scaling = ctx->fg_scaling;
+    a.offsets = ctx->fg_offsets;
+    if (out) {
+        if (!same_geometry(in, out)) return -EINVAL;
+        const int nplanes = in->layout ? 3 : 1;
+        int nb = 0;
+        for (int p = 0; p < 3; p++) {
+            a.blk_start[p] = nb;
+            if (p >= nplanes) continue;
+            a.src[p] = (const uint8_t *)in->data[p];
+            a.dst[p] = (uint8_t *)out->data[p];
+            a.stride[p] = in->stride[p ? 1 : 0];
+            const int sh = p ? a.ss_x : 0, sv = p ? a.ss_y : 0;
+            a.pw[p] = (in->w + sh) >> sh;
+            a.ph[p] = (in->h + sv) >> sv;
+            a.chunks[p] = (a.pw[p] + 3) / 4;
+            a.grain[p] = p == 0 ? data->num_y_points != 0
+                                : (data->chroma_scaling_from_luma || data->num_uv_points[p - 1]);
+            nb += (int)(((int64_t)a.chunks[p] * a.ph[p] + 255) / 256);
+        }
+        a.blk_start[3] = nb;
+    }
+    return 0;
+}
+
+int mi_film_grain_prep(MiCtx *ctx, const MiPicture *in, const MiFilmGrainData *data, void *stream) {
+    if (!ctx || !in || !data) return fail(ctx, -EINVAL);
+    mi::FgArgs a;
+    if (int e = fg_setup(ctx, in, nullptr, data, 0, a)) return fail(ctx, e);
+    return mi::launch_fg(a, (hipStream_t)stream, true, false) ? fail(ctx, -EIO) : 0;
+}
+
+int mi_film_grain_apply(MiCtx *ctx, const MiPicture *in, const MiPicture *out, const MiFilmGrainData *data,
+                        int mtrx_identity, void *stream) {
+    if (!ctx || !in || !out || !data) return fail(ctx, -EINVAL);
+    mi::FgArgs a;
+    if (int e = fg_setup(ctx, in, out, data, mtrx_identity, a)) return fail(ctx, e);
+    return mi::launch_fg(a, (hipStream_t)stream, false, true) ? fail(ctx, -EIO) : 0;
+}
+
+int mi_film_grain_frame(MiCtx *ctx, const MiPicture *in, const MiPicture *out, const MiFilmGrainData *data,
+                        int mtrx_identity, void *stream) {
+    if (!ctx || !in || !out || !data) return fail(ctx, -EINVAL);
+    mi::FgArgs a;
+    if (int e = fg_setup(ctx, in, out, data, mtrx_identity, a)) return fail(ctx, e);
+    return mi::launch_fg(a, (hipStream_t)stream, true, true) ? fail(ctx, -EIO) : 0;
 }
 
 // ---- table-compatible per-call entry points ------------------------------------------

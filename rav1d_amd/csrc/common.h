@@ -100,4 +100,20 @@ struct LrArgs {
 // launchers (lr.hip)
 int launch_lr(const LrArgs &a, int bpc, hipStream_t s);
 
+struct FgArgs {
+    MiFilmGrainData data;
+    const uint8_t *src[3];
+    uint8_t *dst[3];
+    int64_t stride[3];
+    int16_t *lut;                 // [3][73][82]
+    uint8_t *scaling;             // [3][4096]
+    uint8_t *offsets;             // [nrows][nblocks]
+    int bpc, layout, ss_x, ss_y, w, h, is_id, nrows, nblocks;
+    int pw[3], ph[3], chunks[3], grain[3];
+    int blk_start[4];
+};
+// launchers (fg.hip)
+int init_fg_tables();
+int launch_fg(const FgArgs &a, hipStream_t s, bool prep, bool apply);
+
 } // namespace mi

@@ -11,7 +11,7 @@ import ctypes
 import numpy as np
 import torch
 
-from . import MiCdef, MiLoopFilter, MiLr, MiPicture, MiError, check, lib
+from . import MiCdef, MiFilmGrainData, MiLoopFilter, MiLr, MiPicture, MiError, check, lib
 
 LAYOUT_I400, LAYOUT_I420, LAYOUT_I422, LAYOUT_I444 = 0, 1, 2, 3
 
@@ -186,3 +186,36 @@ def lr_frame(ctx, cdef, deblocked, dst, meta, stream=None):
     pc, pd, po = cdef.picture(), deblocked.picture(), dst.picture()
     check(lib().mi_lr_frame(ctx.h, ctypes.byref(pc), ctypes.byref(pd), ctypes.byref(po),
                             ctypes.byref(meta.s), _stream_ptr(stream)), "mi_lr_frame")
+
+
+def film_grain_data(fg):
+    """dict (rav1d_amd.synth.make_fg_params) -> MiFilmGrainData"""
+    d = MiFilmGrainData()
+    d.seed = fg["seed"]
+    d.num_y_points = fg["num_y_points"]
+    for i, (a, b) in enumerate(fg["y_points"]):
+        d.y_points[i][0], d.y_points[i][1] = a, b
+    d.chroma_scaling_from_luma = fg["chroma_scaling_from_luma"]
+    for pl in range(2):
+        d.num_uv_points[pl] = fg["num_uv_points"][pl]
+        for i, (a, b) in enumerate(fg["uv_points"][pl]):
+            d.uv_points[pl][i][0], d.uv_points[pl][i][1] = a, b
+        for i, v in enumerate(fg["ar_coeffs_uv"][pl]):
+            d.ar_coeffs_uv[pl][i] = v
+        d.uv_mult[pl], d.uv_luma_mult[pl], d.uv_offset[pl] = fg["uv_mult"][pl], fg["uv_luma_mult"][pl], fg["uv_offset"][pl]
+    d.scaling_shift = fg["scaling_shift"]
+    d.ar_coeff_lag = fg["ar_coeff_lag"]
+    for i, v in enumerate(fg["ar_coeffs_y"]):
+        d.ar_coeffs_y[i] = v
+    d.ar_coeff_shift = fg["ar_coeff_shift"]
+    d.grain_scale_shift = fg["grain_scale_shift"]
+    d.overlap_flag = fg["overlap_flag"]
+    d.clip_to_restricted_range = fg["clip_to_restricted_range"]
+    return d
+
+
+def film_grain_frame(ctx, src, dst, fg, is_id=0, stream=None):
+    d = film_grain_data(fg)
+    ps, pd = src.picture(), dst.picture()
+    check(lib().mi_film_grain_frame(ctx.h, ctypes.byref(ps), ctypes.byref(pd), ctypes.byref(d), is_id,
+                                    _stream_ptr(stream)), "mi_film_grain_frame")

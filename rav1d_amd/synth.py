@@ -369,3 +369,31 @@ def make_lr_meta(w, h, layout, rng, sb128=1, unit_log2=None, p_none=0.2, p_wiene
         unit_log2 = (ly, lc)
     return dict(lr_mask=m, unit_size_log2=tuple(unit_log2), restore_planes=7 if layout else 1,
                 sb128=sb128)
+
+
+def _points(rng, nmax):
+    n = int(rng.integers(0, nmax + 1))
+    xs = np.sort(rng.choice(256, size=n, replace=False)) if n else np.zeros(0, int)
+    return [(int(x), int(rng.integers(0, 256))) for x in xs]
+
+
+def make_fg_params(rng, layout=1, force_y=True):
+    """Random but codable Dav1dFilmGrainData (ranges of rav1d src/obu.rs parse_film_grain)."""
+    yp = _points(rng, 14)
+    if force_y and not yp:
+        yp = [(0, 40), (255, 90)]
+    csfl = int(layout != 0 and rng.random() < 0.25)
+    uvp = [[], []] if (csfl or layout == 0) else [_points(rng, 10), _points(rng, 10)]
+    lag = int(rng.integers(0, 4))
+    ncy = 2 * lag * (lag + 1)
+    small = lambda n: [int(v) for v in np.clip(rng.normal(0, 20, size=n), -128, 127)]
+    return dict(seed=int(rng.integers(0, 1 << 16)), num_y_points=len(yp), y_points=yp,
+                chroma_scaling_from_luma=csfl, num_uv_points=[len(uvp[0]), len(uvp[1])], uv_points=uvp,
+                scaling_shift=int(rng.integers(8, 12)), ar_coeff_lag=lag,
+                ar_coeffs_y=small(ncy) + [0] * (24 - ncy),
+                ar_coeffs_uv=[small(ncy + 1) + [0] * (28 - ncy - 1) for _ in range(2)],
+                ar_coeff_shift=int(rng.integers(6, 10)), grain_scale_shift=int(rng.integers(0, 4)),
+                uv_mult=[int(rng.integers(-128, 128)) for _ in range(2)],
+                uv_luma_mult=[int(rng.integers(-128, 128)) for _ in range(2)],
+                uv_offset=[int(rng.integers(-256, 256)) for _ in range(2)],
+                overlap_flag=int(rng.random() < 0.7), clip_to_restricted_range=int(rng.random() < 0.5))

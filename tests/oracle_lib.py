@@ -118,3 +118,32 @@ def lr_frame(cdef_planes, deblocked_planes, bpc, layout, w, h, lr):
     f(arr(o_), arr(c), arr(d), st, w, h, layout, bpc, lr["sb128"], lr["restore_planes"], ptr(ul),
       ptr(m), m.shape[1])
     return o_[:len(cdef_planes)]
+
+
+def film_grain(in_planes, bpc, layout, w, h, fg, is_id=0):
+    """Oracle rav1d_apply_grain: returns output planes (input untouched). 128-aligned planes."""
+    from rav1d_amd.frame import film_grain_data
+    o = load_oracle()
+    f = o.oracle_fg_apply
+    f.restype = None
+    f.argtypes = [_VP, _VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _VP, ctypes.c_int]
+    src = [np.ascontiguousarray(p) for p in in_planes]
+    dst = [np.zeros_like(p) for p in src]
+    while len(src) < 3:
+        src.append(src[0]); dst.append(dst[0])
+    arr = lambda L: (ctypes.c_void_p * 3)(*[a.ctypes.data for a in L])
+    st = (ctypes.c_ssize_t * 3)(*[a.strides[0] for a in src])
+    d = film_grain_data(fg)
+    f(arr(dst), arr(src), st, w, h, layout, bpc, ctypes.byref(d), is_id)
+    return dst[:len(in_planes)]
+
+
+def fg_grain_y(fg, bpc):
+    from rav1d_amd.frame import film_grain_data
+    o = load_oracle()
+    o.oracle_fg_generate_grain_y.restype = None
+    o.oracle_fg_generate_grain_y.argtypes = [_VP, _VP, ctypes.c_int]
+    buf = np.zeros((73, 82), np.int16)
+    d = film_grain_data(fg)
+    o.oracle_fg_generate_grain_y(ptr(buf), ctypes.byref(d), (1 << bpc) - 1)
+    return buf
