@@ -397,3 +397,53 @@ def make_fg_params(rng, layout=1, force_y=True):
                 uv_luma_mult=[int(rng.integers(-128, 128)) for _ in range(2)],
                 uv_offset=[int(rng.integers(-256, 256)) for _ in range(2)],
                 overlap_flag=int(rng.random() < 0.7), clip_to_restricted_range=int(rng.random() < 0.5))
+
+
+def itx_blocks_from_tilings(tilings, bpc, rng, dc_frac=0.6, full_frac=0.1):
+    recs, chunks, off = [], [], 0
+    for p, blocks in enumerate(tilings):
+        for (x, y, tx) in blocks:
+            if rng.random() < dc_frac:
+                txtp, regime = 0, 0
+            else:
+                types = tx_types(tx)
+                txtp = types[int(rng.integers(len(types)))]
+                regime = 2 if rng.random() < full_frac / (1 - dc_frac) else 1
+            c, eob = make_coefs(rng, tx, txtp, regime, bpc)
+            recs.append((off, x, y, p, tx, txtp, 0, eob))
+            chunks.append(c)
+            off += c.size
+    blocks = np.array(recs, dtype=TXBLOCK_DTYPE)
+    coef = np.concatenate(chunks).astype(np.int16 if bpc == 8 else np.int32)
+    order = np.lexsort((blocks["coef_off"], blocks["eob"] > 0, blocks["txtp"], blocks["tx"]))
+    blocks = blocks[order]
+    size_start = np.searchsorted(blocks["tx"], np.arange(N_RECT_TX_SIZES + 1)).astype(np.uint32)
+    return blocks, size_start, coef
+
+
+def make_frame(w, h, bpc=10, layout=1, seed=0x4C100001, sb128=1, with_fg=True):
+    """One synthetic frame's worth of post-entropy descriptors for every implemented stage,
+    all derived from one transform tiling: prediction planes, itx blocks + coefficient arena,
+    deblock masks/levels, CDEF indices/strengths, LR units, film-grain parameters."""
+    rng = np.random.default_rng(seed)
+    til = make_tilings(w, h, layout, rng)
+    blocks, size_start, coef = itx_blocks_from_tilings(til, bpc, rng)
+    lf = make_lf_meta(til, w, h, layout, rng)
+    cd = add_cdef_meta(lf, rng)
+    lr = make_lr_meta(w, h, layout, rng, sb128=sb128)
+    ss_h = 1 if layout in (1, 2) else 0
+    ss_v = 1 if layout == 1 else 0
+    planes = [make_mixed_texture(rng, w, h, bpc)]
+    if layout:
+        planes += [make_mixed_texture(rng, (w + ss_h) >> ss_h, (h + ss_v) >> ss_v, bpc) for _ in range(2)]
+    fg = make_fg_params(rng, layout) if with_fg else None
+    return dict(w=w, h=h, bpc=bpc, layout=layout, planes=planes, blocks=blocks, size_start=size_start,
+                coef=coef, lf=lf, cdef=cd, lr=lr, fg=fg)
+
+
+def frame_bytes(w, h, bpc, layout=1):
+    pxb = 1 if bpc == 8 else 2
+    ss_h = 1 if layout in (1, 2) else 0
+    ss_v = 1 if layout == 1 else 0
+    c = ((w + ss_h) >> ss_h) * ((h + ss_v) >> ss_v) if layout else 0
+    return (w * h + 2 * c) * pxb
