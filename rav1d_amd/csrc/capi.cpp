@@ -104,16 +104,9 @@ int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
     a.coef = (uint8_t *)coef;
     a.bdmax = (1 << pic->bpc) - 1;
     a.zero_coefs = (flags & MI_ITX_KEEP_COEFS) ? 0 : 1;
-    int wg = 0;
-    for (int s = 0; s < MI_N_RECT_TX_SIZES; s++) {
-        if (size_start[s + 1] < size_start[s]) return fail(ctx, -EINVAL);
-        const int n = (int)(size_start[s + 1] - size_start[s]);
-        a.wg_start[s] = wg;
-        a.blk_start[s] = (int)size_start[s];
-        wg += (n + mi::itx_blocks_per_wg(s) - 1) / mi::itx_blocks_per_wg(s);
-    }
-    a.wg_start[MI_N_RECT_TX_SIZES] = wg;
-    a.blk_start[MI_N_RECT_TX_SIZES] = (int)size_start[MI_N_RECT_TX_SIZES];
+    for (int k = 0; k < MI_N_RECT_TX_SIZES; k++)
+        if (size_start[k + 1] < size_start[k]) return fail(ctx, -EINVAL);
+    const int wg = mi::itx_fill_schedule(a, size_start);
     if (wg == 0) return 0;
     if (!blocks || !coef) return fail(ctx, -EINVAL);
     const int r = mi::launch_itx_frame(a, wg, pic->bpc, (hipStream_t)stream);
@@ -375,11 +368,10 @@ int mi_dsp_itxfm_add(int tx, int txtp, void *dst, ptrdiff_t stride, void *coeff,
     a.coef = dcoef;
     a.bdmax = bitdepth_max;
     a.zero_coefs = 1;
-    for (int k = 0; k <= MI_N_RECT_TX_SIZES; k++) {
-        a.wg_start[k] = k > tx ? 1 : 0;
-        a.blk_start[k] = k > tx ? 1 : 0;
-    }
-    if (mi::launch_itx_frame(a, 1, bpc, s)) return -EIO;
+    uint32_t ss1[MI_N_RECT_TX_SIZES + 1];
+    for (int k = 0; k <= MI_N_RECT_TX_SIZES; k++) ss1[k] = k > tx ? 1 : 0;
+    const int nwg = mi::itx_fill_schedule(a, ss1);
+    if (mi::launch_itx_frame(a, nwg, bpc, s)) return -EIO;
 
     if (dst_dev) {
         for (int y = 0; y < d.h; y++)

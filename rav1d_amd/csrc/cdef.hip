@@ -15,10 +15,17 @@
 namespace mi {
 
 
-__constant__ int8_t k_cdef_dir[8][2][2] = {
-    { { -1, 1 }, { -2, 2 } }, { { 0, 1 }, { -1, 2 } }, { { 0, 1 }, { 0, 2 } }, { { 0, 1 }, { 1, 2 } },
-    { { 1, 1 }, { 2, 2 } },   { { 1, 0 }, { 2, 1 } },  { { 1, 0 }, { 2, 0 } }, { { 1, 0 }, { 2, -1 } },
-};
+// Tap offsets (dy, dx) per direction and distance (dav1d_cdef_directions, src/tables.rs:698),
+// packed as 4-bit (value + 2) nibbles indexed by direction so that a per-lane direction
+// selects its offsets with shifts instead of a divergent table load.
+//   dir:        0   1   2   3   4   5   6   7
+//   k=0 dy:    -1   0   0   0   1   1   1   1      dx: 1 1 1 1 1 0 0 0
+//   k=1 dy:    -2  -1   0   1   2   2   2   2      dx: 2 2 2 2 2 1 0 -1
+__device__ __forceinline__ int nib(unsigned packed, int dir) { return (int)((packed >> (4 * dir)) & 15) - 2; }
+__device__ __forceinline__ int dir_off(int dir, int k, int ts) {
+    constexpr unsigned DY0 = 0x33332221u, DX0 = 0x22233333u, DY1 = 0x44443210u, DX1 = 0x12344444u;
+    return k == 0 ? nib(DY0, dir) * ts + nib(DX0, dir) : nib(DY1, dir) * ts + nib(DX1, dir);
+}
 
 constexpr int kTY = 68, kTS = 72;          // luma tile rows / LDS row stride (int16)
 
@@ -101,7 +108,7 @@ __device__ __forceinline__ int cdef_px(const int16_t *t, int ts, int x, int y, i
         int tap = 4 - ((pri >> bdm8) & 1);
 #pragma unroll
         for (int k = 0; k < 2; k++) {
-            const int o = k_cdef_dir[dir][k][0] * ts + k_cdef_dir[dir][k][1];
+            const int o = dir_off(dir, k, ts);
             const int a = t[y * ts + x + o], b = t[y * ts + x - o];
             sum += tap * (constrain(a - c, pri, shift) + constrain(b - c, pri, shift));
             tap = (tap & 3) | 2;
@@ -114,8 +121,8 @@ __device__ __forceinline__ int cdef_px(const int16_t *t, int ts, int x, int y, i
         const int d2 = (dir + 2) & 7, d6 = (dir + 6) & 7;
 #pragma unroll
         for (int k = 0; k < 2; k++) {
-            const int o2 = k_cdef_dir[d2][k][0] * ts + k_cdef_dir[d2][k][1];
-            const int o3 = k_cdef_dir[d6][k][0] * ts + k_cdef_dir[d6][k][1];
+            const int o2 = dir_off(d2, k, ts);
+            const int o3 = dir_off(d6, k, ts);
             const int s0 = t[y * ts + x + o2], s1 = t[y * ts + x - o2];
             const int s2 = t[y * ts + x + o3], s3 = t[y * ts + x - o3];
             sum += (2 - k) * (constrain(s0 - c, sec, shift) + constrain(s1 - c, sec, shift) +

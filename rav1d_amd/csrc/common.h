@@ -50,9 +50,15 @@ struct ItxArgs {
     uint8_t *coef;
     int bdmax;
     int zero_coefs;
-    int wg_start[20];
-    int blk_start[20];
+    int wg_start[20];   // first workgroup of the i-th size in launch order (small sizes first)
+    int wg_size[19];    // tx size launched i-th
+    int blk_start[20];  // block ranges per tx size (enum order, as the caller groups them)
+    int large_wg0;      // first workgroup of the large-size launch
 };
+// launch order of tx sizes: every side <= 16 first, then sizes with a 32/64 side
+constexpr int kItxLaunchOrder[19] = { 0, 1, 2, 5, 6, 7, 8, 13, 14, 3, 4, 9, 10, 11, 12, 15, 16, 17, 18 };
+constexpr int kItxNumSmall = 9;
+int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start);
 
 // launchers (itx.hip)
 int launch_itx_frame(const ItxArgs &a, int total_wg, int bpc, hipStream_t s);

@@ -1,17 +1,24 @@
 // itx.hip — batched inverse transform + add for a whole frame on gfx950.
 //
 // Replaces the per-block itxfm_add[tx][txtp] calls made from recon (rav1d src/recon.rs:
-// 1781-1788, 2674-2682, 3116, 4013) with one launch per frame. Semantics per block are
-// inv_txfm_add_rust (src/itx.rs:64-188; C src/itx_tmpl.c:40-100) and the lossless WHT
-// (src/itx.rs:475-526; C src/itx_tmpl.c:162-181).
+// 1781-1788, 2674-2682, 3116, 4013). Semantics per block are inv_txfm_add_rust
+// (src/itx.rs:64-188; C src/itx_tmpl.c:40-100) and the lossless WHT (src/itx.rs:475-526).
 //
-// Mapping. Blocks arrive grouped by tx size; a 256-lane workgroup takes BPW blocks of one
-// size. Within a block, lane j first runs the 1-D row transform of row j (coefficients read
-// straight from the arena's column-major layout, so lanes j..j+sh-1 read consecutive
-// addresses), writes the shifted/clipped row to LDS, then after one barrier runs the 1-D
-// column transform of column j and adds it to the picture (lanes of a block touch
-// consecutive pixels of each row). Butterflies live entirely in VGPRs; no MFMA (these are
-// small fixed integer networks, not contractions).
+// Mapping. Blocks arrive grouped by tx size (and by type / DC-only inside a size, so control
+// flow is wave-uniform almost everywhere). Two launches per frame: sizes whose sides are all
+// <= 16 (about 97 % of blocks in real frames; small register and LDS footprint, so many
+// workgroups per CU hide the descriptor -> coefficient -> pixel latency chain) and sizes with
+// a 32- or 64-point side. A 256-lane workgroup takes BPW blocks of one size:
+//   1. every lane reads its block descriptor and immediately issues the loads of the
+//      destination pixels it will own in step 4 (4-pixel row chunks, 4/8-byte vector loads),
+//      so they are in flight during the transforms;
+//   2. lane j runs the 1-D row transform of row j in VGPRs (coefficients read straight from
+//      the arena's column-major layout: consecutive lanes read consecutive words) and writes
+//      the shifted/clipped row to LDS;
+//   3. lane j runs the 1-D column transform of column j and writes (c + 8) >> 4 back to LDS;
+//   4. lanes add the residual rows to their prefetched pixel chunks and store them as vectors.
+// DC-only blocks skip 2 and 3. Butterflies live entirely in VGPRs; no MFMA (small fixed
+// integer networks, not contractions).
 #include "common.h"
 #include "itx_1d.h"
 
@@ -21,18 +28,58 @@ namespace mi {
 __constant__ uint8_t k_col_kind[16] = { KD, KA, KD, KA, KF, KD, KF, KA, KF, KI, KD, KI, KA, KI, KF, KI };
 __constant__ uint8_t k_row_kind[16] = { KD, KD, KA, KA, KD, KF, KF, KF, KA, KI, KI, KD, KI, KA, KI, KF };
 
-// Largest per-WG LDS need: BPW * SH * (W + 1) ints over all sizes (32x32/32x64: 8*32*33).
-constexpr int kItxLdsInts = 8 * 32 * 33;
+__host__ __device__ constexpr bool itx_is_large(int tx) {
+    return tx_dim(tx).w >= 32 || tx_dim(tx).h >= 32;
+}
+template <int TX>
+__host__ __device__ constexpr int itx_lds_elems() {
+    return itx_blocks_per_wg(TX) * imin_c(tx_dim(TX).h, 32) * (tx_dim(TX).w + 1);
+}
+__host__ __device__ constexpr int itx_lds_max(bool large) {
+    int m = 0;
+    for (int t = 0; t < 19; t++)
+        if (itx_is_large(t) == large) {
+            const int e = itx_blocks_per_wg(t) * imin_c(tx_dim(t).h, 32) * (tx_dim(t).w + 1);
+            m = e > m ? e : m;
+        }
+    return m;
+}
 
-template <int TX, typename Px, typename Cf, bool Wide>
-__device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, int *lds) {
+template <typename Px> struct Vec4;
+template <> struct Vec4<uint8_t> { using T = uint32_t; };
+template <> struct Vec4<uint16_t> { using T = uint2; };
+
+template <typename Px>
+__device__ __forceinline__ void unpack4(const typename Vec4<Px>::T &v, int *o) {
+    if constexpr (sizeof(Px) == 1) {
+        o[0] = v & 0xff; o[1] = (v >> 8) & 0xff; o[2] = (v >> 16) & 0xff; o[3] = v >> 24;
+    } else {
+        o[0] = v.x & 0xffff; o[1] = v.x >> 16; o[2] = v.y & 0xffff; o[3] = v.y >> 16;
+    }
+}
+template <typename Px>
+__device__ __forceinline__ typename Vec4<Px>::T pack4(const int *o) {
+    if constexpr (sizeof(Px) == 1) {
+        return (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) | ((uint32_t)o[3] << 24);
+    } else {
+        uint2 v;
+        v.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+        v.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+        return v;
+    }
+}
+
+template <int TX, typename Px, typename Cf, typename Lt, bool Wide>
+__device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     constexpr TxDim D = tx_dim(TX);
     constexpr int Wd = D.w, Ht = D.h, SH = imin_c(Ht, 32), SW = imin_c(Wd, 32);
     constexpr int TPB = itx_lanes(TX), BPW = kItxThreads / TPB;
-    constexpr int LS = Wd + 1;                       // padded LDS row stride (ints)
+    constexpr int LS = Wd + 1;                        // padded LDS row stride
     constexpr bool Rect2 = (Wd == 2 * Ht) || (Ht == 2 * Wd);
     constexpr int Shift = D.shift, Rnd = (1 << Shift) >> 1;
-    static_assert(BPW * SH * LS <= kItxLdsInts, "itx LDS budget");
+    constexpr int CPR = Wd / 4;                       // 4-px chunks per row
+    constexpr int NCH = (Ht * CPR + TPB - 1) / TPB;   // chunks per lane
+    using V = typename Vec4<Px>::T;
 
     const int t = threadIdx.x;
     const int lb = t / TPB, j = t % TPB;
@@ -45,14 +92,34 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, int *lds) {
     Cf *cf = reinterpret_cast<Cf *>(a.coef) + b.coef_off;
     const bool wht = (TX == 0) && b.txtp == 16;
     const bool dconly = b.txtp == 0 && b.eob < 1;
-    int *tmp = lds + lb * SH * LS;
+    Lt *tmp = lds + lb * SH * LS;
+
+    // ---- 1. prefetch destination chunks ----
+    uint8_t *pbase = a.plane[b.plane] + (int64_t)b.y * a.stride[b.plane] + (int64_t)b.x * sizeof(Px);
+    const int64_t st = a.stride[b.plane];
+    V pix[NCH];
+#pragma unroll
+    for (int k = 0; k < NCH; k++) {
+        const int c = j + k * TPB;
+        if (valid && c < Ht * CPR)
+            pix[k] = *reinterpret_cast<const V *>(pbase + (int64_t)(c / CPR) * st + (c % CPR) * 4 * sizeof(Px));
+    }
 
     int row_lo, col_lo;
     if constexpr (sizeof(Px) == 1) { row_lo = -32768; col_lo = -32768; }
     else { row_lo = (int)((unsigned)~bdmax << 7); col_lo = (int)((unsigned)~bdmax << 5); }
     const int row_hi = ~row_lo, col_hi = ~col_lo;
 
-    // ---- row pass ----
+    int dc = 0;
+    if (valid && dconly) {
+        dc = (int)cf[0];
+        if (Rect2) dc = (dc * 181 + 128) >> 8;
+        dc = (dc * 181 + 128) >> 8;
+        dc = (dc + Rnd) >> Shift;
+        dc = (dc * 181 + 128 + 2048) >> 12;
+    }
+
+    // ---- 2. row pass ----
     if (valid && !dconly && j < SH) {
         int r[Wd];
 #pragma unroll
@@ -73,79 +140,142 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, int *lds) {
                 for (int x = 0; x < 4; x++) r[x] >>= 2;
                 iwht4(r);
 #pragma unroll
-                for (int x = 0; x < 4; x++) tmp[j * LS + x] = r[x];
+                for (int x = 0; x < 4; x++) tmp[j * LS + x] = (Lt)r[x];
             }
         }
         if (!wht) {
             itx1d<Wide, Wd>(k_row_kind[b.txtp], r, row_lo, row_hi);
 #pragma unroll
             for (int x = 0; x < Wd; x++)
-                tmp[j * LS + x] = clampi((r[x] + Rnd) >> Shift, col_lo, col_hi);
+                tmp[j * LS + x] = (Lt)clampi((r[x] + Rnd) >> Shift, col_lo, col_hi);
         }
     }
     __syncthreads();
 
-    // ---- column pass + add ----
-    if (valid && j < Wd) {
-        Px *dst = reinterpret_cast<Px *>(a.plane[b.plane] + (int64_t)b.y * a.stride[b.plane]) + b.x + j;
-        const int64_t ps = a.stride[b.plane] / (int64_t)sizeof(Px);
-        if (dconly) {
-            int dc = (int)cf[0];
-            if (Rect2) dc = (dc * 181 + 128) >> 8;
-            dc = (dc * 181 + 128) >> 8;
-            dc = (dc + Rnd) >> Shift;
-            dc = (dc * 181 + 128 + 2048) >> 12;
-#pragma unroll 4
-            for (int y = 0; y < Ht; y++)
-                dst[y * ps] = (Px)clampi((int)dst[y * ps] + dc, 0, bdmax);
+    // ---- 3. column pass: residual back into LDS (rows >= SH are reused as needed) ----
+    int colres[Ht];
+    if (valid && !dconly && j < Wd) {
+        int c[Ht];
+#pragma unroll
+        for (int y = 0; y < Ht; y++) c[y] = y < SH ? (int)tmp[y * LS + j] : 0;
+        if (wht) {
+            if constexpr (TX == 0) {
+                iwht4(c);
+#pragma unroll
+                for (int y = 0; y < 4; y++) colres[y] = c[y];
+            }
         } else {
-            int c[Ht];
+            itx1d<Wide, Ht>(k_col_kind[b.txtp], c, col_lo, col_hi);
 #pragma unroll
-            for (int y = 0; y < Ht; y++) c[y] = y < SH ? tmp[y * LS + j] : 0;
-            if (wht) {
-                if constexpr (TX == 0) {
-                    iwht4(c);
+            for (int y = 0; y < Ht; y++) colres[y] = (c[y] + 8) >> 4;
+        }
+    }
+    if constexpr (Ht > SH) {
+        // 64-row blocks: the LDS slab only holds 32 rows; write the residual in two halves
+        __syncthreads();
 #pragma unroll
-                    for (int y = 0; y < 4; y++)
-                        dst[y * ps] = (Px)clampi((int)dst[y * ps] + c[y], 0, bdmax);
+        for (int half = 0; half < 2; half++) {
+            if (valid && !dconly && j < Wd) {
+#pragma unroll
+                for (int y = 0; y < SH; y++) tmp[y * LS + j] = (Lt)colres[half * SH + y];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < NCH; k++) {
+                const int c = j + k * TPB;
+                const int y = c / CPR;
+                if (valid && c < Ht * CPR && (y / SH) == half) {
+                    int px[4];
+                    unpack4<Px>(pix[k], px);
+                    const int x0 = (c % CPR) * 4;
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        px[q] = clampi(px[q] + (dconly ? dc : (int)tmp[(y - half * SH) * LS + x0 + q]), 0, bdmax);
+                    *reinterpret_cast<V *>(pbase + (int64_t)y * st + x0 * sizeof(Px)) = pack4<Px>(px);
                 }
-            } else {
-                itx1d<Wide, Ht>(k_col_kind[b.txtp], c, col_lo, col_hi);
+            }
+            __syncthreads();
+        }
+    } else {
+        __syncthreads();
+        if (valid && !dconly && j < Wd) {
 #pragma unroll
-                for (int y = 0; y < Ht; y++)
-                    dst[y * ps] = (Px)clampi((int)dst[y * ps] + ((c[y] + 8) >> 4), 0, bdmax);
+            for (int y = 0; y < Ht; y++) tmp[y * LS + j] = (Lt)colres[y];
+        }
+        __syncthreads();
+        // ---- 4. add + vector stores ----
+#pragma unroll
+        for (int k = 0; k < NCH; k++) {
+            const int c = j + k * TPB;
+            if (valid && c < Ht * CPR) {
+                const int y = c / CPR, x0 = (c % CPR) * 4;
+                int px[4];
+                unpack4<Px>(pix[k], px);
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    px[q] = clampi(px[q] + (dconly ? dc : (int)tmp[y * LS + x0 + q]), 0, bdmax);
+                *reinterpret_cast<V *>(pbase + (int64_t)y * st + x0 * sizeof(Px)) = pack4<Px>(px);
             }
         }
     }
-    // DC-only blocks clear their single coefficient after all lanes consumed it.
-    __syncthreads();
     if (valid && dconly && j == 0 && a.zero_coefs) cf[0] = 0;
 }
 
-template <typename Px, typename Cf, bool Wide>
+template <typename Px, typename Cf, typename Lt, bool Wide, bool Large>
 __global__ __launch_bounds__(kItxThreads) void itx_frame_kernel(ItxArgs a) {
-    __shared__ int lds[kItxLdsInts];
-    const int wg = blockIdx.x;
-    int s = 0;
-    while (s < 18 && wg >= a.wg_start[s + 1]) s++;
-    const int lwg = wg - a.wg_start[s];
-    switch (s) {
-#define CASE(n) case n: itx_size<n, Px, Cf, Wide>(a, lwg, lds); break;
-        CASE(0) CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9)
-        CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16) CASE(17) CASE(18)
+    __shared__ Lt lds[itx_lds_max(Large)];
+    const int wg = blockIdx.x + (Large ? a.large_wg0 : 0);
+    int i = Large ? kItxNumSmall : 0;
+    while (i < 18 && wg >= a.wg_start[i + 1]) i++;
+    const int s = a.wg_size[i];
+    const int lwg = wg - a.wg_start[i];
+    if constexpr (!Large) {
+        switch (s) {
+#define CASE(n) case n: itx_size<n, Px, Cf, Lt, Wide>(a, lwg, lds); break;
+            CASE(0) CASE(1) CASE(2) CASE(5) CASE(6) CASE(7) CASE(8) CASE(13) CASE(14)
 #undef CASE
-    default: break;
+        default: break;
+        }
+    } else {
+        switch (s) {
+#define CASE(n) case n: itx_size<n, Px, Cf, Lt, Wide>(a, lwg, lds); break;
+            CASE(3) CASE(4) CASE(9) CASE(10) CASE(11) CASE(12) CASE(15) CASE(16) CASE(17) CASE(18)
+#undef CASE
+        default: break;
+        }
     }
+}
+
+template <typename Px, typename Cf, typename Lt, bool Wide>
+static void launch2(const ItxArgs &a, int small_wg, int large_wg, hipStream_t s) {
+    if (small_wg)
+        hipLaunchKernelGGL((itx_frame_kernel<Px, Cf, Lt, Wide, false>), dim3(small_wg), dim3(kItxThreads), 0, s, a);
+    if (large_wg)
+        hipLaunchKernelGGL((itx_frame_kernel<Px, Cf, Lt, Wide, true>), dim3(large_wg), dim3(kItxThreads), 0, s, a);
+}
+
+int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start) {
+    int wg = 0;
+    for (int i = 0; i < 19; i++) {
+        const int sz = kItxLaunchOrder[i];
+        if (i == kItxNumSmall) a.large_wg0 = wg;
+        a.wg_start[i] = wg;
+        a.wg_size[i] = sz;
+        const int n = (int)(size_start[sz + 1] - size_start[sz]);
+        wg += (n + itx_blocks_per_wg(sz) - 1) / itx_blocks_per_wg(sz);
+    }
+    a.wg_start[19] = wg;
+    for (int k = 0; k <= 19; k++) a.blk_start[k] = (int)size_start[k];
+    return wg;
 }
 
 int launch_itx_frame(const ItxArgs &a, int total_wg, int bpc, hipStream_t s) {
     if (total_wg <= 0) return 0;
-    if (bpc == 8)
-        hipLaunchKernelGGL((itx_frame_kernel<uint8_t, int16_t, false>), dim3(total_wg), dim3(kItxThreads), 0, s, a);
-    else if (bpc == 10)
-        hipLaunchKernelGGL((itx_frame_kernel<uint16_t, int32_t, false>), dim3(total_wg), dim3(kItxThreads), 0, s, a);
-    else
-        hipLaunchKernelGGL((itx_frame_kernel<uint16_t, int32_t, true>), dim3(total_wg), dim3(kItxThreads), 0, s, a);
+    // workgroup ranges are laid out size by size; small sizes first (see capi: ordering)
+    const int small_wg = a.large_wg0, large_wg = total_wg - a.large_wg0;
+    if (bpc == 8) launch2<uint8_t, int16_t, int16_t, false>(a, small_wg, large_wg, s);
+    else if (bpc == 10) launch2<uint16_t, int32_t, int16_t, false>(a, small_wg, large_wg, s);
+    else launch2<uint16_t, int32_t, int32_t, true>(a, small_wg, large_wg, s);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

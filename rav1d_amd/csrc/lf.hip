@@ -100,8 +100,17 @@ __device__ __forceinline__ int lvl_at(const LfArgs &a, int uy, int ux, int slot)
 }
 
 // ---- column edges (filtering along rows) ----
+// E/I limits of the frame's sharpness (Av1FilterLUT) staged in LDS: lanes index them with
+// their own level, which would otherwise be divergent reads of the kernel-argument segment.
+__device__ __forceinline__ void stage_lut(const LfArgs &a, uint8_t *le, uint8_t *li) {
+    if (threadIdx.x < 64) { le[threadIdx.x] = a.lim_e[threadIdx.x]; li[threadIdx.x] = a.lim_i[threadIdx.x]; }
+    __syncthreads();
+}
+
 template <typename Px>
 __global__ __launch_bounds__(256) void lf_cols_kernel(LfArgs a) {
+    __shared__ uint8_t le[64], li[64];
+    stage_lut(a, le, li);
     const int b = blockIdx.x;
     const int p = b < a.blk_start[1] ? 0 : b < a.blk_start[2] ? 1 : 2;
     const int lb = b - a.blk_start[p];
@@ -138,12 +147,14 @@ __global__ __launch_bounds__(256) void lf_cols_kernel(LfArgs a) {
     if (!L) return;
     if (ux * 4 < (wd == 16 ? 7 : wd / 2)) return;   // malformed mask: never reached for valid AV1
     Px *q0 = reinterpret_cast<Px *>(a.plane[p] + (int64_t)y * a.stride[p]) + ux * 4;
-    filter_line<Px>(q0, 1, wd, a.lim_e[L], a.lim_i[L], L >> 4, a.bdm8, a.bdmax);
+    filter_line<Px>(q0, 1, wd, le[L], li[L], L >> 4, a.bdm8, a.bdmax);
 }
 
 // ---- row edges (filtering along columns) ----
 template <typename Px>
 __global__ __launch_bounds__(256) void lf_rows_kernel(LfArgs a) {
+    __shared__ uint8_t le[64], li[64];
+    stage_lut(a, le, li);
     const int b = blockIdx.x;
     const int p = b < a.blk_start[1] ? 0 : b < a.blk_start[2] ? 1 : 2;
     const int lb = b - a.blk_start[p];
@@ -179,7 +190,7 @@ __global__ __launch_bounds__(256) void lf_rows_kernel(LfArgs a) {
     if (uy * 4 < (wd == 16 ? 7 : wd / 2)) return;
     const int64_t ps = a.stride[p] / (int64_t)sizeof(Px);
     Px *q0 = reinterpret_cast<Px *>(a.plane[p] + (int64_t)uy * 4 * a.stride[p]) + x;
-    filter_line<Px>(q0, ps, wd, a.lim_e[L], a.lim_i[L], L >> 4, a.bdm8, a.bdmax);
+    filter_line<Px>(q0, ps, wd, le[L], li[L], L >> 4, a.bdm8, a.bdmax);
 }
 
 int launch_deblock(const LfArgs &cols, const LfArgs &rows, int bpc, hipStream_t s) {

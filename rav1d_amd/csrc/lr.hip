@@ -14,7 +14,7 @@
 
 namespace mi {
 
-constexpr int kLrWin = 72;             // LDS window row stride (ints), >= 64 + 6
+constexpr int kLrWin = 72;             // LDS window row stride (int16), >= 64 + 6
 constexpr int kLrAB = 68;              // A/B row stride
 
 __constant__ uint16_t k_sgr_params[16][2] = {
@@ -35,42 +35,62 @@ __device__ __forceinline__ int ld_px(const uint8_t *base, int64_t stride, int y,
     return reinterpret_cast<const Px *>(base + (int64_t)y * stride)[x];
 }
 
-// Self-guided A/B maps for radius r (n = 25 or 9) over rows -1..sh (every other row for 5x5),
-// cols -1..tw. A holds the "b" term, B holds x, as after the reference's inversion.
-__device__ void sgr_ab(const int *win, int *A, int *B, int sh, int tw, int r, unsigned s,
-                       int bdm8) {
-    const int n = (2 * r + 1) * (2 * r + 1);
-    const unsigned one_by_x = n == 25 ? 164 : 455;
-    const int step = r == 2 ? 2 : 1;
-    const int nrows = r == 2 ? (sh + 3) / 2 : sh + 2;      // rows -1, -1+step, ... < sh+1
-    const int ncols = tw + 2;
-    for (int i = threadIdx.x; i < nrows * ncols; i += 256) {
-        const int jr = i / ncols, ic = i % ncols;
-        const int y = -1 + jr * step, x = ic - 1;
-        int sum = 0, sq = 0;
-        for (int dy = -r; dy <= r; dy++) {
-            const int *row = win + (y + 3 + dy) * kLrWin + x + 3;
-            for (int dx = -r; dx <= r; dx++) {
-                const int v = row[dx];
-                sum += v;
-                sq += v * v;
-            }
+// Self-guided A/B maps (looprestoration.rs selfguided_filter, first half) for radius R over
+// rows -1..sh (every other row for R = 2) and cols -1..tw. Lane (tx, ty) owns column tx (and
+// tx + 64 for the two extra columns) and a quarter of the rows, and slides a (2R+1)-row
+// window of horizontal sums down its column: 2R+1 LDS reads per position.
+template <int R>
+__device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, unsigned s, int bdm8) {
+    constexpr int n = (2 * R + 1) * (2 * R + 1);
+    constexpr unsigned one_by_x = n == 25 ? 164 : 455;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int nrows = sh + 2;                         // y = -1 .. sh
+    const int per = (nrows + 3) >> 2;
+    const int y0 = -1 + ty * per, y1 = min(-1 + (ty + 1) * per, sh + 1);
+    for (int c = tx; c < tw + 2; c += 64) {
+        const int x = c - 1;                          // position column (-1 .. tw)
+        const int16_t *col = win + x + 3;
+        int rs[2 * R + 1], rq[2 * R + 1];
+#pragma unroll
+        for (int k = 0; k < 2 * R; k++) {             // rows y0-R .. y0+R-1
+            const int16_t *row = col + (y0 - R + k + 3) * kLrWin;
+            int s1 = 0, q1 = 0;
+#pragma unroll
+            for (int dx = -R; dx <= R; dx++) { const int v = row[dx]; s1 += v; q1 += v * v; }
+            rs[k] = s1; rq[k] = q1;
         }
-        const int a = (sq + ((1 << (2 * bdm8)) >> 1)) >> (2 * bdm8);
-        const int b = (sum + ((1 << bdm8) >> 1)) >> bdm8;
-        const unsigned p = (unsigned)max(a * n - b * b, 0);
-        const unsigned z = (p * s + (1u << 19)) >> 20;
-        const unsigned xv = sgr_x_by_x(z);
-        A[(y + 1) * kLrAB + x + 1] = (int)((xv * (unsigned)sum * one_by_x + (1u << 11)) >> 12);
-        B[(y + 1) * kLrAB + x + 1] = (int)xv;
+        for (int y = y0; y < y1; y++) {
+            {
+                const int16_t *row = col + (y + R + 3) * kLrWin;
+                int s1 = 0, q1 = 0;
+#pragma unroll
+                for (int dx = -R; dx <= R; dx++) { const int v = row[dx]; s1 += v; q1 += v * v; }
+                rs[2 * R] = s1; rq[2 * R] = q1;
+            }
+            if (R == 1 || !((y + 1) & 1)) {
+                int sum = 0, sq = 0;
+#pragma unroll
+                for (int k = 0; k <= 2 * R; k++) { sum += rs[k]; sq += rq[k]; }
+                const int a = (sq + ((1 << (2 * bdm8)) >> 1)) >> (2 * bdm8);
+                const int b = (sum + ((1 << bdm8) >> 1)) >> bdm8;
+                const unsigned p = (unsigned)max(a * n - b * b, 0);
+                const unsigned z = (p * s + (1u << 19)) >> 20;
+                const unsigned xv = sgr_x_by_x(z);
+                A[(y + 1) * kLrAB + x + 1] = (int)((xv * (unsigned)sum * one_by_x + (1u << 11)) >> 12);
+                B[(y + 1) * kLrAB + x + 1] = (int16_t)xv;
+            }
+#pragma unroll
+            for (int k = 0; k < 2 * R; k++) { rs[k] = rs[k + 1]; rq[k] = rq[k + 1]; }
+        }
     }
 }
 
 // Self-guided output term for pixel (j, i) (looprestoration.rs selfguided_filter tail).
-__device__ __forceinline__ int sgr_px(const int *A, const int *B, int j, int i, int src, int r) {
+template <int R>
+__device__ __forceinline__ int sgr_px(const int *A, const int16_t *B, int j, int i, int src) {
 #define AA(y, x) A[((y) + 1) * kLrAB + (x) + 1]
-#define BB(y, x) B[((y) + 1) * kLrAB + (x) + 1]
-    if (r == 2) {
+#define BB(y, x) ((int)B[((y) + 1) * kLrAB + (x) + 1])
+    if (R == 2) {
         if (!(j & 1)) {
             const int a = (BB(j - 1, i) + BB(j + 1, i)) * 6 +
                           (BB(j - 1, i - 1) + BB(j + 1, i - 1) + BB(j - 1, i + 1) + BB(j + 1, i + 1)) * 5;
@@ -96,22 +116,21 @@ __device__ __forceinline__ int stripe_start(int k, int ssv) { return k ? (64 * k
 
 template <typename Px>
 __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
-    extern __shared__ int lsm[];
-    int *win = lsm;                                    // [70][kLrWin]
-    int *A = win + 70 * kLrWin;                        // [66][kLrAB]
-    int *B = A + 66 * kLrAB;                           // [66][kLrAB]
-    int *hor = A;                                      // Wiener: [70][64] aliases A/B
+    __shared__ int16_t win[70 * kLrWin];
+    __shared__ int A[66 * kLrAB];
+    __shared__ int16_t B[66 * kLrAB];
+    int16_t *hor = reinterpret_cast<int16_t *>(A);    // Wiener: [70][64] aliases A
 
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int blk = blockIdx.x;
     const int p = blk < a.blk_start[1] ? 0 : blk < a.blk_start[2] ? 1 : 2;
     const int lb = blk - a.blk_start[p];
     const int tiles = a.tiles_x[p];
-    const int k = lb / tiles, ti = lb % tiles;
+    const int k = lb / tiles, ti = lb - k * tiles;
     const int ssv = p ? a.ss_ver : 0, ssh = p ? a.ss_hor : 0;
     const int pw = a.pw[p], ph = a.ph[p];
-    const int tw_full = a.tw[p];
-    const int x0 = ti * tw_full;
-    const int tw = min(tw_full, pw - x0);
+    const int x0 = ti * a.tw[p];
+    const int tw = min(a.tw[p], pw - x0);
     const int S = stripe_start(k, ssv);
     const int E = min(stripe_start(k + 1, ssv), ph);
     const int sh = E - S;
@@ -119,6 +138,8 @@ __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
     const uint8_t *D = a.lpf[p];
     uint8_t *O = a.dst[p];
     const int64_t st = a.stride[p];
+    // lane (tx, ty) owns output column tx, rows [ty*16, ty*16+16)
+    const int r0 = ty * 16, r1 = min(r0 + 16, sh);
 
     // restoration unit of this tile (lr_apply.rs:151-259 indexing)
     int type = 0;
@@ -137,24 +158,27 @@ __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
         type = u->type;
     }
     if (type == 0) {   // RESTORATION_NONE: O = C
-        for (int i = threadIdx.x; i < sh * tw; i += 256) {
-            const int r = i / tw, c = i % tw;
-            reinterpret_cast<Px *>(O + (int64_t)(S + r) * st)[x0 + c] = (Px)ld_px<Px>(C, st, S + r, x0 + c);
-        }
+        if (tx < tw)
+            for (int r = r0; r < r1; r++)
+                reinterpret_cast<Px *>(O + (int64_t)(S + r) * st)[x0 + tx] = (Px)ld_px<Px>(C, st, S + r, x0 + tx);
         return;
     }
 
     // ---- stage the (sh+6) x (tw+6) window (C inside the stripe, D across its edges) ----
     const bool have_top = k > 0, have_bottom = E < ph;
     const int wr = sh + 6, wc = tw + 6;
-    for (int i = threadIdx.x; i < wr * wc; i += 256) {
-        const int r = i / wc - 3, c = i % wc - 3;
-        const int cc = min(max(x0 + c, 0), pw - 1);
-        int v;
-        if (r >= 0 && r < sh) v = ld_px<Px>(C, st, S + r, cc);
-        else if (r < 0) v = have_top ? ld_px<Px>(D, st, S - 2 + (r == -1), cc) : ld_px<Px>(C, st, S, cc);
-        else v = have_bottom ? ld_px<Px>(D, st, min(E + (r > sh), ph - 1), cc) : ld_px<Px>(C, st, E - 1, cc);
-        win[(r + 3) * kLrWin + c + 3] = v;
+    for (int rr = ty; rr < wr; rr += 4) {
+        const int r = rr - 3;
+        int yy;
+        const uint8_t *src;
+        if (r >= 0 && r < sh) { src = C; yy = S + r; }
+        else if (r < 0) { src = have_top ? D : C; yy = have_top ? S - 2 + (r == -1) : S; }
+        else { src = have_bottom ? D : C; yy = have_bottom ? min(E + (r > sh), ph - 1) : E - 1; }
+        const Px *row = reinterpret_cast<const Px *>(src + (int64_t)yy * st);
+        for (int cc = tx; cc < wc; cc += 64) {
+            const int xg = min(max(x0 + cc - 3, 0), pw - 1);
+            win[rr * kLrWin + cc] = (int16_t)row[xg];
+        }
     }
     __syncthreads();
 
@@ -168,23 +192,31 @@ __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
         fv[3] = 128 - 2 * (fv[0] + fv[1] + fv[2]);
         const int rbh = bd == 12 ? 5 : 3, rbv = bd == 12 ? 9 : 11;
         const int clip_h = (1 << (bd + 1 + 7 - rbh)) - 1;
-        for (int i = threadIdx.x; i < wr * tw; i += 256) {
-            const int r = i / tw, c = i % tw;
-            const int *row = win + r * kLrWin + c;
-            int sum = 1 << (bd + 6);
+        if (tx < tw) {
+            for (int rr = ty; rr < wr; rr += 4) {
+                const int16_t *row = win + rr * kLrWin + tx;
+                int sum = 1 << (bd + 6);
 #pragma unroll
-            for (int t = 0; t < 7; t++) sum += row[t] * fh[t];
-            hor[r * 64 + c] = min(max((sum + (1 << (rbh - 1))) >> rbh, 0), clip_h);
+                for (int t = 0; t < 7; t++) sum += (int)row[t] * fh[t];
+                hor[rr * 64 + tx] = (int16_t)min(max((sum + (1 << (rbh - 1))) >> rbh, 0), clip_h);
+            }
         }
         __syncthreads();
-        const int off = 1 << (bd + rbv - 1);
-        for (int i = threadIdx.x; i < sh * tw; i += 256) {
-            const int r = i / tw, c = i % tw;
-            int sum = -off;
+        if (tx < tw && r0 < r1) {
+            const int off = 1 << (bd + rbv - 1);
+            int h[22];
 #pragma unroll
-            for (int t = 0; t < 7; t++) sum += hor[(r + t) * 64 + c] * fv[t];
-            const int v = min(max((sum + (1 << (rbv - 1))) >> rbv, 0), bdmax);
-            reinterpret_cast<Px *>(O + (int64_t)(S + r) * st)[x0 + c] = (Px)v;
+            for (int q = 0; q < 22; q++) h[q] = r0 + q < wr ? (int)(uint16_t)hor[(r0 + q) * 64 + tx] : 0;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                if (r0 + q < r1) {
+                    int sum = -off;
+#pragma unroll
+                    for (int t = 0; t < 7; t++) sum += h[q + t] * fv[t];
+                    const int v = min(max((sum + (1 << (rbv - 1))) >> rbv, 0), bdmax);
+                    reinterpret_cast<Px *>(O + (int64_t)(S + r0 + q) * st)[x0 + tx] = (Px)v;
+                }
+            }
         }
         return;
     }
@@ -195,43 +227,38 @@ __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
     const int w0 = u->sgr_weights[0];
     const int w1 = 128 - (u->sgr_weights[0] + u->sgr_weights[1]);
     const int bdm8 = bd - 8;
-    constexpr int kMaxPx = 16;                         // 64x64 / 256 lanes
-    int acc[kMaxPx];
+    int acc[16];
 #pragma unroll
-    for (int q = 0; q < kMaxPx; q++) acc[q] = 0;
+    for (int q = 0; q < 16; q++) acc[q] = 0;
     if (s0) {
-        sgr_ab(win, A, B, sh, tw, 2, (unsigned)s0, bdm8);
+        sgr_ab<2>(win, A, B, sh, tw, (unsigned)s0, bdm8);
         __syncthreads();
+        if (tx < tw) {
 #pragma unroll
-        for (int q = 0; q < kMaxPx; q++) {
-            const int i = threadIdx.x + q * 256;
-            if (i < sh * tw) {
-                const int r = i / tw, c = i % tw;
-                acc[q] += w0 * sgr_px(A, B, r, c, win[(r + 3) * kLrWin + c + 3], 2);
-            }
+            for (int q = 0; q < 16; q++)
+                if (r0 + q < r1)
+                    acc[q] += w0 * sgr_px<2>(A, B, r0 + q, tx, win[(r0 + q + 3) * kLrWin + tx + 3]);
         }
         __syncthreads();
     }
     if (s1) {
-        sgr_ab(win, A, B, sh, tw, 1, (unsigned)s1, bdm8);
+        sgr_ab<1>(win, A, B, sh, tw, (unsigned)s1, bdm8);
         __syncthreads();
+        if (tx < tw) {
 #pragma unroll
-        for (int q = 0; q < kMaxPx; q++) {
-            const int i = threadIdx.x + q * 256;
-            if (i < sh * tw) {
-                const int r = i / tw, c = i % tw;
-                acc[q] += w1 * sgr_px(A, B, r, c, win[(r + 3) * kLrWin + c + 3], 1);
-            }
+            for (int q = 0; q < 16; q++)
+                if (r0 + q < r1)
+                    acc[q] += w1 * sgr_px<1>(A, B, r0 + q, tx, win[(r0 + q + 3) * kLrWin + tx + 3]);
         }
     }
+    if (tx < tw) {
 #pragma unroll
-    for (int q = 0; q < kMaxPx; q++) {
-        const int i = threadIdx.x + q * 256;
-        if (i < sh * tw) {
-            const int r = i / tw, c = i % tw;
-            const int px = win[(r + 3) * kLrWin + c + 3];
-            const int v = min(max(px + ((acc[q] + (1 << 10)) >> 11), 0), bdmax);
-            reinterpret_cast<Px *>(O + (int64_t)(S + r) * st)[x0 + c] = (Px)v;
+        for (int q = 0; q < 16; q++) {
+            if (r0 + q < r1) {
+                const int px = win[(r0 + q + 3) * kLrWin + tx + 3];
+                const int v = min(max(px + ((acc[q] + (1 << 10)) >> 11), 0), bdmax);
+                reinterpret_cast<Px *>(O + (int64_t)(S + r0 + q) * st)[x0 + tx] = (Px)v;
+            }
         }
     }
 }
@@ -239,9 +266,8 @@ __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
 int launch_lr(const LrArgs &a, int bpc, hipStream_t s) {
     const int n = a.blk_start[3];
     if (n <= 0) return 0;
-    const size_t lds = sizeof(int) * (70 * kLrWin + 2 * 66 * kLrAB);
-    if (bpc == 8) hipLaunchKernelGGL(lr_kernel<uint8_t>, dim3(n), dim3(256), lds, s, a);
-    else hipLaunchKernelGGL(lr_kernel<uint16_t>, dim3(n), dim3(256), lds, s, a);
+    if (bpc == 8) hipLaunchKernelGGL(lr_kernel<uint8_t>, dim3(n), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(lr_kernel<uint16_t>, dim3(n), dim3(256), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
