@@ -260,7 +260,7 @@ static int fg_setup(MiCtx *ctx, const MiPicture *in, const MiPicture *out, const
     a.is_id = is_id;
     a.nrows = (in->h + 31) >> 5;
     a.nblocks = (in->w + 31) >> 5;
-    if (!ctx->fg_lut && hipMalloc(&ctx->fg_lut, 3 * 73 * 82 * sizeof(int16_t)) != hipSuccess) return -ENOMEM;
+    if (!ctx->fg_lut && hipMalloc(&ctx->fg_lut, 3 * 73 * 88 * sizeof(int16_t)) != hipSuccess) return -ENOMEM;
     if (!ctx->fg_scaling && hipMalloc(&ctx->fg_scaling, 3 * 4096) != hipSuccess) return -ENOMEM;
     const size_t ob = (size_t)a.nrows * a.nblocks;
     if (ob > ctx->fg_offsets_bytes) {
@@ -285,10 +285,10 @@ static int fg_setup(MiCtx *ctx, const MiPicture *in, const MiPicture *out, const
             const int sh = p ? a.ss_x : 0, sv = p ? a.ss_y : 0;
             a.pw[p] = (in->w + sh) >> sh;
             a.ph[p] = (in->h + sv) >> sv;
-            a.chunks[p] = (a.pw[p] + 3) / 4;
+            a.chunks[p] = (a.pw[p] + 511) / 512;   // 64-lane waves per row, 8 contiguous px per lane
             a.grain[p] = p == 0 ? data->num_y_points != 0
                                 : (data->chroma_scaling_from_luma || data->num_uv_points[p - 1]);
-            nb += (int)(((int64_t)a.chunks[p] * a.ph[p] + 255) / 256);
+            nb += (int)(((int64_t)a.chunks[p] * a.ph[p] + 3) / 4);
         }
         a.blk_start[3] = nb;
     }

@@ -138,25 +138,43 @@ __device__ __forceinline__ int cdef_px(const int16_t *t, int ts, int x, int y, i
     return v;
 }
 
-template <typename Px>
-__device__ __forceinline__ void load_tile(int16_t *t, int ts, int rows, int cols, const uint8_t *src,
-                                          int64_t stride, int x0, int y0, int fw, int fh) {
-    for (int i = threadIdx.x; i < rows * cols; i += 256) {
-        const int r = i / cols, c = i % cols;
-        const int x = x0 - 2 + c, y = y0 - 2 + r;
-        int16_t v = INT16_MIN;
-        if (x >= 0 && y >= 0 && x < fw && y < fh)
-            v = (int16_t) reinterpret_cast<const Px *>(src + (int64_t)y * stride)[x];
-        t[r * ts + c] = v;
+// Tile loader: the (ROWS x COLS) window at (x0-2, y0-2) as int16, i16::MIN outside the frame.
+// All loads of the calling lane are issued before the first LDS store (fully unrolled, constant
+// divisors) so their HBM latencies overlap.
+template <typename Px, int ROWS, int COLS>
+struct TileLoad {
+    static constexpr int N = ROWS * COLS, IT = (N + 255) / 256;
+    int16_t v[IT];
+    __device__ __forceinline__ void fetch(const uint8_t *src, int64_t stride, int x0, int y0, int fw, int fh) {
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            const int i = threadIdx.x + 256 * k;
+            const int r = i / COLS, c = i - r * COLS;
+            const int x = x0 - 2 + c, y = y0 - 2 + r;
+            v[k] = INT16_MIN;
+            if (i < N && x >= 0 && y >= 0 && x < fw && y < fh)
+                v[k] = (int16_t) reinterpret_cast<const Px *>(src + (int64_t)y * stride)[x];
+        }
     }
-}
+    __device__ __forceinline__ void store(int16_t *t, int ts) const {
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            const int i = threadIdx.x + 256 * k;
+            const int r = i / COLS, c = i - r * COLS;
+            if (i < N) t[r * ts + c] = v[k];
+        }
+    }
+};
 
-template <typename Px>
+// One 64x64 luma unit (+ co-located chroma) per 256-lane workgroup. L = layout (0 I400,
+// 1 I420, 2 I422, 3 I444), compile-time so every tile index is a shift or a constant divide.
+template <typename Px, int L>
 __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
-    extern __shared__ int16_t smem[];
-    const int cw = 64 >> a.ss_hor, ch = 64 >> a.ss_ver, cts = cw + 8;
-    int16_t *ty = smem;
-    int16_t *tuv[2] = { smem + kTY * kTS, smem + kTY * kTS + (ch + 4) * cts };
+    constexpr int SSH = L == 1 || L == 2, SSV = L == 1;
+    constexpr int CW = 64 >> SSH, CH = 64 >> SSV, CTS = CW + 8;
+    constexpr int UVW = 8 >> SSH, UVH = 8 >> SSV;
+    __shared__ int16_t ty[kTY * kTS];
+    __shared__ int16_t tuv[2][L ? (CH + 4) * CTS : 1];
     __shared__ int8_t bdir[64];
     __shared__ int8_t bflag[64];          // bit0 luma filtered, bit1 chroma filtered
     __shared__ int16_t bpri[64];
@@ -166,20 +184,22 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
     const MiAv1Filter *lf = &a.masks[(tyy >> 1) * a.sb128w + (tx >> 1)];
     const int cdef_idx = lf->cdef_idx[(tyy & 1) * 2 + (tx & 1)];
     const int y_lvl = cdef_idx >= 0 ? a.y_strength[cdef_idx] : 0;
-    const int uv_lvl = cdef_idx >= 0 && a.layout ? a.uv_strength[cdef_idx] : 0;
-    const int nplanes = a.layout ? 3 : 1;
+    const int uv_lvl = cdef_idx >= 0 && L ? a.uv_strength[cdef_idx] : 0;
     const int fwy = a.bw4 * 4, fhy = a.bh4 * 4;
-    const int fwc = fwy >> a.ss_hor, fhc = fhy >> a.ss_ver;
+    const int fwc = fwy >> SSH, fhc = fhy >> SSV;
 
     if (!y_lvl && !uv_lvl) {
-        // untouched 64x64 unit: C = D
-        for (int p = 0; p < nplanes; p++) {
-            const int sh = p ? a.ss_hor : 0, sv = p ? a.ss_ver : 0;
-            const int pw = 64 >> sh, ph = 64 >> sv, px0 = x0 >> sh, py0 = y0 >> sv;
-            for (int i = threadIdx.x; i < pw * ph; i += 256) {
-                const int r = i / pw, c = i % pw;
-                const int64_t off = (int64_t)(py0 + r) * a.stride[p];
-                reinterpret_cast<Px *>(a.dst[p] + off)[px0 + c] = reinterpret_cast<const Px *>(a.src[p] + off)[px0 + c];
+        // untouched 64x64 unit: C = D, 8 bytes per lane
+        constexpr int PX8 = 8 / sizeof(Px);
+#pragma unroll
+        for (int p = 0; p < (L ? 3 : 1); p++) {
+            const int pw = p ? CW : 64, ph = p ? CH : 64;
+            const int px0 = p ? x0 >> SSH : x0, py0 = p ? y0 >> SSV : y0;
+            const int cpr = pw / PX8;   // 8-byte chunks per row
+            for (int i = threadIdx.x; i < cpr * ph; i += 256) {
+                const int r = i / cpr, c = i - r * cpr;
+                const int64_t off = (int64_t)(py0 + r) * a.stride[p] + (int64_t)(px0 + c * PX8) * sizeof(Px);
+                *reinterpret_cast<uint2 *>(a.dst[p] + off) = *reinterpret_cast<const uint2 *>(a.src[p] + off);
             }
         }
         return;
@@ -191,10 +211,19 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
     const int uv_pri = (uv_lvl >> 2) << bdm8;
     int uv_sec = uv_lvl & 3; uv_sec += uv_sec == 3; uv_sec <<= bdm8;
 
-    load_tile<Px>(ty, kTS, 68, 68, a.src[0], a.stride[0], x0, y0, fwy, fhy);
-    if (uv_lvl) {
-        load_tile<Px>(tuv[0], cts, ch + 4, cw + 4, a.src[1], a.stride[1], x0 >> a.ss_hor, y0 >> a.ss_ver, fwc, fhc);
-        load_tile<Px>(tuv[1], cts, ch + 4, cw + 4, a.src[2], a.stride[2], x0 >> a.ss_hor, y0 >> a.ss_ver, fwc, fhc);
+    {
+        TileLoad<Px, 68, 68> ly;
+        TileLoad<Px, CH + 4, CW + 4> lu, lv;
+        ly.fetch(a.src[0], a.stride[0], x0, y0, fwy, fhy);
+        if (L && uv_lvl) {
+            lu.fetch(a.src[1], a.stride[1], x0 >> SSH, y0 >> SSV, fwc, fhc);
+            lv.fetch(a.src[2], a.stride[2], x0 >> SSH, y0 >> SSV, fwc, fhc);
+        }
+        ly.store(ty, kTS);
+        if (L && uv_lvl) {
+            lu.store(tuv[0], CTS);
+            lv.store(tuv[1], CTS);
+        }
     }
     __syncthreads();
 
@@ -223,8 +252,10 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
     }
     __syncthreads();
 
-    // luma
-    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    // luma: one wave per 64-px row
+#pragma unroll 4
+    for (int k = 0; k < 16; k++) {
+        const int i = threadIdx.x + 256 * k;
         const int r = i >> 6, c = i & 63;
         const int b = (r >> 3) * 8 + (c >> 3);
         const int gx = x0 + c, gy = y0 + r;
@@ -242,20 +273,21 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
         *dp = (Px)v;
     }
     // chroma
-    if (a.layout) {
-        const int uvw = 8 >> a.ss_hor, uvh = 8 >> a.ss_ver;
-        const uint8_t dirmap422[8] = { 7, 0, 2, 4, 5, 6, 6, 6 };
-        for (int i = threadIdx.x; i < 2 * cw * ch; i += 256) {
-            const int p = 1 + i / (cw * ch), j = i % (cw * ch);
-            const int r = j / cw, c = j % cw;
-            const int b = (r / uvh) * 8 + (c / uvw);
-            const int gx = (x0 >> a.ss_hor) + c, gy = (y0 >> a.ss_ver) + r;
+    if (L) {
+        constexpr int NC = CW * CH;
+#pragma unroll 2
+        for (int k = 0; k < 2 * NC / 256; k++) {
+            const int i = threadIdx.x + 256 * k;
+            const int p = 1 + (i >= NC), j = i - (p - 1) * NC;
+            const int r = j / CW, c = j % CW;
+            const int b = (r / UVH) * 8 + (c / UVW);
+            const int gx = (x0 >> SSH) + c, gy = (y0 >> SSV) + r;
             Px *dp = reinterpret_cast<Px *>(a.dst[p] + (int64_t)gy * a.stride[p]) + gx;
-            const int16_t *t = tuv[p - 1];
             int v;
             if (bflag[b] & 2) {
-                const int d = uv_pri ? (a.layout == 2 ? dirmap422[bdir[b]] : bdir[b]) : 0;
-                v = cdef_px(t, cts, c + 2, r + 2, uv_pri, uv_sec, d, a.damping - 1, bdm8);
+                int d = uv_pri ? bdir[b] : 0;
+                if (L == 2 && uv_pri) d = nib(0x66654207u, d) + 2;   // 4:2:2 direction remap {7,0,2,4,5,6,6,6}
+                v = cdef_px(tuv[p - 1], CTS, c + 2, r + 2, uv_pri, uv_sec, d, a.damping - 1, bdm8);
             } else {
                 v = reinterpret_cast<const Px *>(a.src[p] + (int64_t)gy * a.stride[p])[gx];
             }
@@ -266,10 +298,18 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
 
 int launch_cdef(const CdefArgs &a, int tiles, int bpc, hipStream_t s) {
     if (tiles <= 0) return 0;
-    const int cw = 64 >> a.ss_hor, ch = 64 >> a.ss_ver;
-    const size_t lds = sizeof(int16_t) * (kTY * kTS + (a.layout ? 2 * (ch + 4) * (cw + 8) : 0));
-    if (bpc == 8) hipLaunchKernelGGL(cdef_kernel<uint8_t>, dim3(tiles), dim3(256), lds, s, a);
-    else hipLaunchKernelGGL(cdef_kernel<uint16_t>, dim3(tiles), dim3(256), lds, s, a);
+#define MI_CDEF_LAUNCH(L)                                                                            \
+    do {                                                                                             \
+        if (bpc == 8) cdef_kernel<uint8_t, L><<<tiles, 256, 0, s>>>(a);                               \
+        else cdef_kernel<uint16_t, L><<<tiles, 256, 0, s>>>(a);                                       \
+    } while (0)
+    switch (a.layout) {
+    case 0: MI_CDEF_LAUNCH(0); break;
+    case 1: MI_CDEF_LAUNCH(1); break;
+    case 2: MI_CDEF_LAUNCH(2); break;
+    default: MI_CDEF_LAUNCH(3); break;
+    }
+#undef MI_CDEF_LAUNCH
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

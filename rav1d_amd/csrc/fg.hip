@@ -10,8 +10,8 @@
 // the auto-regressive filter runs as a skewed wavefront (row y lags row y-1 by lag+1
 // columns, one LDS barrier per step); scaling LUTs are filled from their closed form; the
 // per-(32-row, 32-col) block offsets are drawn by one lane per block row.
-// apply: one lane per 4 output pixels of one plane row; grain templates, scaling LUTs and
-// offsets are read through L1/L2 (a few tens of KB, cache resident).
+// apply: one wave per 512-pixel row segment, lane-contiguous pixels; grain templates and
+// offsets are read through L1/L2 (cache resident), the scaling LUT from LDS.
 #include "common.h"
 
 namespace mi {
@@ -22,6 +22,7 @@ __constant__ int16_t k_gauss[2048] = {
 __constant__ uint16_t k_lfsr_jump[256][16];   // M^(24*i) as 16 column vectors
 
 constexpr int kGW = 82, kGH = 73, kDrawsPerLane = 24;
+constexpr int kGP = 88;   // pitch of the exported templates (16-byte rows for vector loads)
 
 __device__ __forceinline__ unsigned lfsr_step(unsigned s) {
     const unsigned bit = (s ^ (s >> 1) ^ (s >> 3) ^ (s >> 12)) & 1;
@@ -128,7 +129,10 @@ __global__ __launch_bounds__(256) void fg_prep_kernel(FgArgs a) {
                  on ? (threadIdx.x & 127) : -1);
     }
     // export templates
-    for (int i = threadIdx.x; i < 3 * kGH * kGW; i += 256) a.lut[i] = (&lut[0][0][0])[i];
+    for (int i = threadIdx.x; i < 3 * kGH * kGP; i += 256) {
+        const int r = i / kGP, c = i - r * kGP;
+        a.lut[i] = c < kGW ? (&lut[0][0][0])[r * kGW + c] : 0;
+    }
 
     // scaling LUTs
     const int size = 1 << a.bpc;
@@ -154,88 +158,261 @@ __global__ __launch_bounds__(256) void fg_prep_kernel(FgArgs a) {
 __device__ __forceinline__ int lut_at(const int16_t *lut, int rv, int subx, int suby, int bx, int by, int x, int y) {
     const int ox = 3 + (2 >> subx) * (3 + (rv >> 4));
     const int oy = 3 + (2 >> suby) * (3 + (rv & 0xF));
-    return lut[(oy + y + (32 >> suby) * by) * kGW + ox + x + (32 >> subx) * bx];
+    return lut[(oy + y + (32 >> suby) * by) * kGP + ox + x + (32 >> subx) * bx];
+}
+
+__device__ __forceinline__ int blend(int a, int b, int wa, int wb, int gmin, int gmax) {
+    return min(max(round2i(a * wa + b * wb, 5), gmin), gmax);
+}
+
+// Position of one 8-pixel chunk inside its grain block and the block offsets it needs.
+struct GrainPos {
+    int sx, sy, yy, xx0, bi;
+    int rc, rl, rt, rtl;        // offsets: own block, left, top, top-left
+    bool hx, vy;                // inside the horizontal / vertical overlap band
+};
+
+// 8 grain samples of template `lut` for a chunk (filmgrain.rs fgy/fguv inner loops, with the
+// overlap blends), `g` out. Template loads: three aligned 8-byte loads + a funnel shift.
+__device__ __forceinline__ void grain8(const int16_t *lut, const GrainPos &q, int gmin, int gmax, int g[8]) {
+    {
+        const int ox = 3 + (2 >> q.sx) * (3 + (q.rc >> 4));
+        const int oy = 3 + (2 >> q.sy) * (3 + (q.rc & 0xF));
+        const int s0 = (oy + q.yy) * kGP + ox + q.xx0, sh = s0 & 3;
+        const uint2 *v = reinterpret_cast<const uint2 *>(lut + (s0 - sh));
+        const uint2 q0 = v[0], q1 = v[1], q2 = v[2];
+        const uint32_t w[6] = { q0.x, q0.y, q1.x, q1.y, q2.x, q2.y };
+        uint32_t u[5], o[4];
+#pragma unroll
+        for (int i = 0; i < 5; i++) u[i] = sh & 2 ? w[i + 1] : w[i];
+#pragma unroll
+        for (int i = 0; i < 4; i++) o[i] = sh & 1 ? __builtin_amdgcn_alignbyte(u[i + 1], u[i], 2) : u[i];
+#pragma unroll
+        for (int j = 0; j < 8; j++) g[j] = (int)(int16_t)(o[j >> 1] >> (16 * (j & 1)));
+    }
+    if (!(q.hx || q.vy)) return;
+    const int sx = q.sx, sy = q.sy, yy = q.yy, xx0 = q.xx0;
+    const int xstart = q.hx ? 2 >> sx : 0;
+    const int wy0 = sy ? 23 : (yy & 1 ? 17 : 27), wy1 = sy ? 22 : (yy & 1 ? 27 : 17);
+    int left[2] = { 0, 0 }, top[8], tl[2] = { 0, 0 };
+    if (q.hx) {
+#pragma unroll
+        for (int j = 0; j < 2; j++) left[j] = lut_at(lut, q.rl, sx, sy, 1, 0, xx0 + j, yy);
+    }
+    if (q.vy) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) top[j] = lut_at(lut, q.rt, sx, sy, 0, 1, xx0 + j, yy);
+        if (q.hx) {
+#pragma unroll
+            for (int j = 0; j < 2; j++) tl[j] = lut_at(lut, q.rtl, sx, sy, 1, 1, xx0 + j, yy);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const bool inx = j < xstart;
+        const int xx = xx0 + j;
+        const int wx0 = sx ? 23 : (xx & 1 ? 17 : 27), wx1 = sx ? 22 : (xx & 1 ? 27 : 17);
+        if (inx && !q.vy) {
+            g[j] = blend(left[j & 1], g[j], wx0, wx1, gmin, gmax);
+        } else if (!inx && q.vy) {
+            g[j] = blend(top[j], g[j], wy0, wy1, gmin, gmax);
+        } else if (inx && q.vy) {
+            const int tp = blend(tl[j & 1], top[j], wx0, wx1, gmin, gmax);
+            const int gg = blend(left[j & 1], g[j], wx0, wx1, gmin, gmax);
+            g[j] = blend(tp, gg, wy0, wy1, gmin, gmax);
+        }
+    }
+}
+
+// 8 pixels <-> one 8-byte (u8) or 16-byte (u16) vector, unpacked to / packed from ints.
+__device__ __forceinline__ void unpack8(const uint2 v, int e[8]) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) { e[j] = (v.x >> (8 * j)) & 0xff; e[4 + j] = (v.y >> (8 * j)) & 0xff; }
+}
+__device__ __forceinline__ void unpack8(const uint4 v, int e[8]) {
+    const uint32_t w[4] = { v.x, v.y, v.z, v.w };
+#pragma unroll
+    for (int j = 0; j < 4; j++) { e[2 * j] = w[j] & 0xffff; e[2 * j + 1] = w[j] >> 16; }
+}
+template <typename Px> struct Vec8;
+template <> struct Vec8<uint8_t> {
+    using T = uint2;
+    static __device__ __forceinline__ T pack(const int e[8]) {
+        T v;
+        v.x = (uint32_t)e[0] | (uint32_t)e[1] << 8 | (uint32_t)e[2] << 16 | (uint32_t)e[3] << 24;
+        v.y = (uint32_t)e[4] | (uint32_t)e[5] << 8 | (uint32_t)e[6] << 16 | (uint32_t)e[7] << 24;
+        return v;
+    }
+};
+template <> struct Vec8<uint16_t> {
+    using T = uint4;
+    static __device__ __forceinline__ T pack(const int e[8]) {
+        T v;
+        v.x = (uint32_t)e[0] | (uint32_t)e[1] << 16;
+        v.y = (uint32_t)e[2] | (uint32_t)e[3] << 16;
+        v.z = (uint32_t)e[4] | (uint32_t)e[5] << 16;
+        v.w = (uint32_t)e[6] | (uint32_t)e[7] << 16;
+        return v;
+    }
+};
+
+template <typename Px>
+__device__ __forceinline__ void load8(int e[8], const Px *src, int n) {
+    if (n == 8) {
+        unpack8(*reinterpret_cast<const typename Vec8<Px>::T *>(src), e);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) e[j] = j < n ? src[j] : 0;
+    }
 }
 
 template <typename Px>
+__device__ __forceinline__ void store8(Px *dst, const int e[8], int n) {
+    if (n == 8) {
+        *reinterpret_cast<typename Vec8<Px>::T *>(dst) = Vec8<Px>::pack(e);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (j < n) dst[j] = (Px)e[j];
+    }
+}
+
+// One lane per 8-pixel chunk of a plane row, one wave per 512-pixel row segment (fgy_32x32xn /
+// fguv_32x32xn, filmgrain.rs:404-830, re-cut by output chunk). A chunk never straddles a grain
+// block (32 wide, 16 when subsampled), so the block offset and the column inside the block are
+// per chunk; overlap blending touches only the first 2 (1) columns and rows of a block, and its
+// loads are issued together inside one branch. The scaling LUT is staged in LDS while the pixel
+// loads are in flight.
+template <typename Px>
 __global__ __launch_bounds__(256) void fg_apply_kernel(FgArgs a) {
+    __shared__ uint32_t scl32[1024];
+    const uint8_t *scl = reinterpret_cast<const uint8_t *>(scl32);
     const int b = blockIdx.x;
     const int p = b < a.blk_start[1] ? 0 : b < a.blk_start[2] ? 1 : 2;
-    const int lb = b - a.blk_start[p];
-    const int chunks = a.chunks[p];
-    const int idx = lb * 256 + threadIdx.x;
-    const int y = idx / chunks, x0 = (idx % chunks) * 4;
-    const int pw = a.pw[p], ph = a.ph[p];
-    if (y >= ph) return;
     const MiFilmGrainData &d = a.data;
-    const int sx = p ? a.ss_x : 0, sy = p ? a.ss_y : 0;
+    const bool grain = a.grain[p];
+    const int wpr = a.chunks[p];   // waves per plane row
+    const int t = (b - a.blk_start[p]) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int y = t / wpr, seg = t - y * wpr;
+    const int pw = a.pw[p], ph = a.ph[p];
+    const int x0 = (seg * 64 + (threadIdx.x & 63)) * 8;
+    const bool active = y < ph && x0 < pw;
+    const int n = active ? min(8, pw - x0) : 0;
     const int64_t st = a.stride[p];
-    const Px *src = reinterpret_cast<const Px *>(a.src[p] + (int64_t)y * st);
-    Px *dst = reinterpret_cast<Px *>(a.dst[p] + (int64_t)y * st);
-    if (!a.grain[p]) {
-        for (int x = x0; x < min(x0 + 4, pw); x++) dst[x] = src[x];
+    const Px *src = reinterpret_cast<const Px *>(a.src[p] + (int64_t)y * st) + x0;
+    Px *dst = reinterpret_cast<Px *>(a.dst[p] + (int64_t)y * st) + x0;
+    if (!grain) {   // uniform per workgroup: plain copy, no staging
+        if (active) {
+            int e[8];
+            load8(e, src, n);
+            store8(dst, e, n);
+        }
         return;
     }
+
+    // scaling LUT (1 << bpc entries) -> registers; written to LDS after the pixel loads issue
+    const int nw = (1 << a.bpc) >> 2;
+    uint32_t lutw[4];
+    {
+        const uint32_t *g = reinterpret_cast<const uint32_t *>(
+            a.scaling + (p && !d.chroma_scaling_from_luma ? p : 0) * 4096);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int i = threadIdx.x + 256 * k;
+            lutw[k] = i < nw ? g[i] : 0;
+        }
+    }
+    int sv[8];
+    if (active) load8(sv, src, n);
+    const int sx = p ? a.ss_x : 0, sy = p ? a.ss_y : 0;
+
+    // co-located luma (chroma planes): 8 << sx samples from x0 << sx, clamped at w - 1
+    int lum[8];
+    if (p && active) {
+        const int lx0 = x0 << sx;
+        const Px *luma = reinterpret_cast<const Px *>(a.src[0] + (int64_t)(y << sy) * a.stride[0]);
+        if (sx) {
+            int l0[8], l1[8];
+            if (lx0 + 16 <= a.w) {
+                load8(l0, luma + lx0, 8);
+                load8(l1, luma + lx0 + 8, 8);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    l0[j] = luma[min(lx0 + j, a.w - 1)];
+                    l1[j] = luma[min(lx0 + 8 + j, a.w - 1)];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                lum[j] = (l0[2 * j] + l0[2 * j + 1] + 1) >> 1;
+                lum[4 + j] = (l1[2 * j] + l1[2 * j + 1] + 1) >> 1;
+            }
+        } else if (n == 8) {
+            load8(lum, luma + lx0, 8);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) lum[j] = luma[min(lx0 + j, a.w - 1)];
+        }
+    }
+
+    // grain samples of this chunk's block
     const int bdm8 = a.bpc - 8, bdmax = (1 << a.bpc) - 1;
     const int gctr = 128 << bdm8, gmin = -gctr, gmax = gctr - 1;
+    int g[8];
+    if (active) {
+        GrainPos q;
+        q.sx = sx; q.sy = sy;
+        const int bsh = 32 >> sy, bsw = 32 >> sx;
+        const int row = y >> (5 - sy);
+        q.yy = y & (bsh - 1);
+        q.bi = x0 >> (5 - sx);
+        q.xx0 = x0 & (bsw - 1);
+        const uint8_t *offr = a.offsets + row * a.nblocks;
+        const uint8_t *offp = row ? offr - a.nblocks : offr;
+        q.rc = offr[q.bi];
+        q.hx = q.vy = false;
+        q.rl = q.rt = q.rtl = 0;
+        if (d.overlap_flag) {
+            const int bh = p ? (min(a.h - row * 32, 32) + sy) >> sy : min(a.h - row * 32, 32);
+            const int ystart = row ? min(2 >> sy, bh) : 0;
+            q.hx = q.bi > 0 && q.xx0 == 0;     // blocks are >= 1 px wide: xstart > 0 iff bi > 0
+            q.vy = q.yy < ystart;
+            if (q.hx) q.rl = offr[q.bi - 1];
+            if (q.vy) q.rt = offp[q.bi];
+            if (q.hx && q.vy) q.rtl = offp[q.bi - 1];
+        }
+        grain8(a.lut + p * kGH * kGP, q, gmin, gmax, g);
+    }
+
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int i = threadIdx.x + 256 * k;
+        if (i < nw) scl32[i] = lutw[k];
+    }
+    __syncthreads();
+    if (!active) return;
+
     int minv = 0, maxv = bdmax;
     if (d.clip_to_restricted_range) {
         minv = 16 << bdm8;
         maxv = (p == 0 || a.is_id ? 235 : 240) << bdm8;
     }
-    const int bsh = 32 >> sy, bsw = 32 >> sx;
-    const int row = y / bsh, yy = y % bsh;
-    const int bh = p ? (min(a.h - row * 32, 32) + sy) >> sy : min(a.h - row * 32, 32);
-    const int16_t *lut = a.lut + p * kGH * kGW;
-    const uint8_t *scl = a.scaling + (p && !d.chroma_scaling_from_luma ? p : 0) * 4096;
-    const uint8_t *offr = a.offsets + row * a.nblocks;
-    const uint8_t *offp = row ? a.offsets + (row - 1) * a.nblocks : offr;
-    const int wl[2][2] = { { 27, 17 }, { 17, 27 } };
-    const int ws[2] = { 23, 22 };
-    const Px *luma = nullptr;
-    int64_t lrow = 0;
-    if (p) {
-        lrow = (int64_t)(row * 32 + (yy << sy));
-        luma = reinterpret_cast<const Px *>(a.src[0] + lrow * a.stride[0]);
-    }
-    for (int x = x0; x < min(x0 + 4, pw); x++) {
-        const int bi = x / bsw, xx = x % bsw;
-        const int bw = min(bsw, pw - bi * bsw);
-        const int ystart = d.overlap_flag && row ? min(2 >> sy, bh) : 0;
-        const int xstart = d.overlap_flag && bi ? min(2 >> sx, bw) : 0;
-        const int rc = offr[bi];
-        int grain = lut_at(lut, rc, sx, sy, 0, 0, xx, yy);
-        const int wx0 = sx ? ws[0] : wl[xx & 1][0], wx1 = sx ? ws[1] : wl[xx & 1][1];
-        const int wy0 = sy ? ws[0] : wl[yy & 1][0], wy1 = sy ? ws[1] : wl[yy & 1][1];
-        if (xx < xstart && yy >= ystart) {
-            const int old = lut_at(lut, offr[bi - 1], sx, sy, 1, 0, xx, yy);
-            grain = min(max(round2i(old * wx0 + grain * wx1, 5), gmin), gmax);
-        } else if (xx >= xstart && yy < ystart) {
-            const int old = lut_at(lut, offp[bi], sx, sy, 0, 1, xx, yy);
-            grain = min(max(round2i(old * wy0 + grain * wy1, 5), gmin), gmax);
-        } else if (xx < xstart && yy < ystart) {
-            int top = lut_at(lut, offp[bi], sx, sy, 0, 1, xx, yy);
-            int old = lut_at(lut, offp[bi - 1], sx, sy, 1, 1, xx, yy);
-            top = min(max(round2i(old * wx0 + top * wx1, 5), gmin), gmax);
-            old = lut_at(lut, offr[bi - 1], sx, sy, 1, 0, xx, yy);
-            grain = min(max(round2i(old * wx0 + grain * wx1, 5), gmin), gmax);
-            grain = min(max(round2i(top * wy0 + grain * wy1, 5), gmin), gmax);
-        }
-        const int s = src[x];
-        int val = s;
+    int ov[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        int val = sv[j];
         if (p) {
-            const int lx = x << sx;
-            int avg = luma[lx];
-            if (sx) avg = (avg + luma[min(lx + 1, a.w - 1)] + 1) >> 1;
-            val = avg;
+            val = lum[j];
             if (!d.chroma_scaling_from_luma) {
-                const int comb = avg * d.uv_luma_mult[p - 1] + s * d.uv_mult[p - 1];
+                const int comb = lum[j] * d.uv_luma_mult[p - 1] + sv[j] * d.uv_mult[p - 1];
                 val = min(max((comb >> 6) + d.uv_offset[p - 1] * (1 << bdm8), 0), bdmax);
             }
         }
-        const int noise = round2i(scl[val] * grain, d.scaling_shift);
-        dst[x] = (Px)min(max(s + noise, minv), maxv);
+        const int noise = round2i(scl[val] * g[j], d.scaling_shift);
+        ov[j] = min(max(sv[j] + noise, minv), maxv);
     }
+    store8(dst, ov, n);
 }
 
 int init_fg_tables() {
@@ -271,8 +448,8 @@ int init_fg_tables() {
 int launch_fg(const FgArgs &a, hipStream_t s, bool prep, bool apply) {
     if (prep) hipLaunchKernelGGL(fg_prep_kernel, dim3(1), dim3(256), 0, s, a);
     if (apply && a.blk_start[3] > 0) {
-        if (a.bpc == 8) hipLaunchKernelGGL(fg_apply_kernel<uint8_t>, dim3(a.blk_start[3]), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL(fg_apply_kernel<uint16_t>, dim3(a.blk_start[3]), dim3(256), 0, s, a);
+        if (a.bpc == 8) fg_apply_kernel<uint8_t><<<a.blk_start[3], 256, 0, s>>>(a);
+        else fg_apply_kernel<uint16_t><<<a.blk_start[3], 256, 0, s>>>(a);
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }

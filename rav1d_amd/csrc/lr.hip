@@ -43,11 +43,13 @@ template <int R>
 __device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, unsigned s, int bdm8) {
     constexpr int n = (2 * R + 1) * (2 * R + 1);
     constexpr unsigned one_by_x = n == 25 ? 164 : 455;
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    // 66 columns x 3 row groups = 198 lanes, one column each
+    const int g = threadIdx.x / 66, c = threadIdx.x - g * 66;
+    if (g >= 3 || c >= tw + 2) return;
     const int nrows = sh + 2;                         // y = -1 .. sh
-    const int per = (nrows + 3) >> 2;
-    const int y0 = -1 + ty * per, y1 = min(-1 + (ty + 1) * per, sh + 1);
-    for (int c = tx; c < tw + 2; c += 64) {
+    const int per = (nrows + 2) / 3;
+    const int y0 = -1 + g * per, y1 = min(-1 + (g + 1) * per, sh + 1);
+    {
         const int x = c - 1;                          // position column (-1 .. tw)
         const int16_t *col = win + x + 3;
         int rs[2 * R + 1], rq[2 * R + 1];
@@ -85,30 +87,58 @@ __device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, u
     }
 }
 
-// Self-guided output term for pixel (j, i) (looprestoration.rs selfguided_filter tail).
+// Self-guided output terms for rows r0..r0+15 of column i (looprestoration.rs selfguided_filter
+// tail). The lane walks down its column keeping, per A/B row, the centre value c and the sum of
+// its two horizontal neighbours s in registers: 3 A + 3 B LDS reads per row instead of 9 + 9.
 template <int R>
-__device__ __forceinline__ int sgr_px(const int *A, const int16_t *B, int j, int i, int src) {
-#define AA(y, x) A[((y) + 1) * kLrAB + (x) + 1]
-#define BB(y, x) ((int)B[((y) + 1) * kLrAB + (x) + 1])
-    if (R == 2) {
-        if (!(j & 1)) {
-            const int a = (BB(j - 1, i) + BB(j + 1, i)) * 6 +
-                          (BB(j - 1, i - 1) + BB(j + 1, i - 1) + BB(j - 1, i + 1) + BB(j + 1, i + 1)) * 5;
-            const int b = (AA(j - 1, i) + AA(j + 1, i)) * 6 +
-                          (AA(j - 1, i - 1) + AA(j + 1, i - 1) + AA(j - 1, i + 1) + AA(j + 1, i + 1)) * 5;
-            return (b - a * src + (1 << 8)) >> 9;
+__device__ __forceinline__ void sgr_px16(const int *A, const int16_t *B, int r0, int r1, int i,
+                                         const int16_t *win, int w, int acc[16]) {
+    const int *a0 = A + i + 1;
+    const int16_t *b0 = B + i + 1;
+    auto ld = [&](int y, int &ca, int &sa, int &cb, int &sb) {
+        const int *ar = a0 + (y + 1) * kLrAB;
+        const int16_t *br = b0 + (y + 1) * kLrAB;
+        ca = ar[0]; sa = ar[-1] + ar[1];
+        cb = br[0]; sb = br[-1] + br[1];
+    };
+    if (R == 1) {
+        int ca0, sa0, cb0, sb0, ca1, sa1, cb1, sb1, ca2, sa2, cb2, sb2;
+        ld(r0 - 1, ca0, sa0, cb0, sb0);
+        ld(r0, ca1, sa1, cb1, sb1);
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            ld(r0 + q + 1, ca2, sa2, cb2, sb2);
+            if (r0 + q < r1) {
+                const int src = win[(r0 + q + 3) * kLrWin + i + 3];
+                const int a = (cb1 + sb1 + cb0 + cb2) * 4 + (sb0 + sb2) * 3;
+                const int b = (ca1 + sa1 + ca0 + ca2) * 4 + (sa0 + sa2) * 3;
+                acc[q] += w * ((b - a * src + (1 << 8)) >> 9);
+            }
+            ca0 = ca1; sa0 = sa1; cb0 = cb1; sb0 = sb1;
+            ca1 = ca2; sa1 = sa2; cb1 = cb2; sb1 = sb2;
         }
-        const int a = BB(j, i) * 6 + (BB(j, i - 1) + BB(j, i + 1)) * 5;
-        const int b = AA(j, i) * 6 + (AA(j, i - 1) + AA(j, i + 1)) * 5;
-        return (b - a * src + (1 << 7)) >> 8;
+    } else {
+        // A/B exist on odd rows: even j uses rows j-1 and j+1, odd j uses row j (r0 is even)
+        int cau, sau, cbu, sbu, cad, sad, cbd, sbd;
+        ld(r0 - 1, cau, sau, cbu, sbu);
+#pragma unroll
+        for (int q = 0; q < 16; q += 2) {
+            ld(r0 + q + 1, cad, sad, cbd, sbd);
+            if (r0 + q < r1) {
+                const int src = win[(r0 + q + 3) * kLrWin + i + 3];
+                const int a = (cbu + cbd) * 6 + (sbu + sbd) * 5;
+                const int b = (cau + cad) * 6 + (sau + sad) * 5;
+                acc[q] += w * ((b - a * src + (1 << 8)) >> 9);
+            }
+            if (r0 + q + 1 < r1) {
+                const int src = win[(r0 + q + 4) * kLrWin + i + 3];
+                const int a = cbd * 6 + sbd * 5;
+                const int b = cad * 6 + sad * 5;
+                acc[q + 1] += w * ((b - a * src + (1 << 7)) >> 8);
+            }
+            cau = cad; sau = sad; cbu = cbd; sbu = sbd;
+        }
     }
-    const int a = (BB(j, i) + BB(j, i - 1) + BB(j, i + 1) + BB(j - 1, i) + BB(j + 1, i)) * 4 +
-                  (BB(j - 1, i - 1) + BB(j + 1, i - 1) + BB(j - 1, i + 1) + BB(j + 1, i + 1)) * 3;
-    const int b = (AA(j, i) + AA(j, i - 1) + AA(j, i + 1) + AA(j - 1, i) + AA(j + 1, i)) * 4 +
-                  (AA(j - 1, i - 1) + AA(j + 1, i - 1) + AA(j - 1, i + 1) + AA(j + 1, i + 1)) * 3;
-    return (b - a * src + (1 << 8)) >> 9;
-#undef AA
-#undef BB
 }
 
 // Stripe (64 luma rows, offset 8 up; first stripe 56) -> plane rows.
@@ -158,26 +188,43 @@ __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
         type = u->type;
     }
     if (type == 0) {   // RESTORATION_NONE: O = C
-        if (tx < tw)
-            for (int r = r0; r < r1; r++)
-                reinterpret_cast<Px *>(O + (int64_t)(S + r) * st)[x0 + tx] = (Px)ld_px<Px>(C, st, S + r, x0 + tx);
+        if (tx < tw) {
+            int v[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) v[q] = r0 + q < r1 ? ld_px<Px>(C, st, S + r0 + q, x0 + tx) : 0;
+#pragma unroll
+            for (int q = 0; q < 16; q++)
+                if (r0 + q < r1) reinterpret_cast<Px *>(O + (int64_t)(S + r0 + q) * st)[x0 + tx] = (Px)v[q];
+        }
         return;
     }
 
     // ---- stage the (sh+6) x (tw+6) window (C inside the stripe, D across its edges) ----
     const bool have_top = k > 0, have_bottom = E < ph;
     const int wr = sh + 6, wc = tw + 6;
-    for (int rr = ty; rr < wr; rr += 4) {
-        const int r = rr - 3;
-        int yy;
-        const uint8_t *src;
-        if (r >= 0 && r < sh) { src = C; yy = S + r; }
-        else if (r < 0) { src = have_top ? D : C; yy = have_top ? S - 2 + (r == -1) : S; }
-        else { src = have_bottom ? D : C; yy = have_bottom ? min(E + (r > sh), ph - 1) : E - 1; }
-        const Px *row = reinterpret_cast<const Px *>(src + (int64_t)yy * st);
-        for (int cc = tx; cc < wc; cc += 64) {
-            const int xg = min(max(x0 + cc - 3, 0), pw - 1);
-            win[rr * kLrWin + cc] = (int16_t)row[xg];
+    // all 18 row loads of this lane are issued before the first LDS store (latency overlap)
+    int16_t v0[18], v1[18];
+#pragma unroll
+    for (int q = 0; q < 18; q++) {
+        const int rr = ty + 4 * q, r = rr - 3;
+        v0[q] = v1[q] = 0;
+        if (rr < wr) {
+            int yy;
+            const uint8_t *src;
+            if (r >= 0 && r < sh) { src = C; yy = S + r; }
+            else if (r < 0) { src = have_top ? D : C; yy = have_top ? S - 2 + (r == -1) : S; }
+            else { src = have_bottom ? D : C; yy = have_bottom ? min(E + (r > sh), ph - 1) : E - 1; }
+            const Px *row = reinterpret_cast<const Px *>(src + (int64_t)yy * st);
+            v0[q] = (int16_t)row[min(max(x0 + tx - 3, 0), pw - 1)];
+            if (tx + 64 < wc) v1[q] = (int16_t)row[min(x0 + tx + 61, pw - 1)];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 18; q++) {
+        const int rr = ty + 4 * q;
+        if (rr < wr) {
+            win[rr * kLrWin + tx] = v0[q];
+            if (tx + 64 < wc) win[rr * kLrWin + tx + 64] = v1[q];
         }
     }
     __syncthreads();
@@ -233,23 +280,13 @@ __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
     if (s0) {
         sgr_ab<2>(win, A, B, sh, tw, (unsigned)s0, bdm8);
         __syncthreads();
-        if (tx < tw) {
-#pragma unroll
-            for (int q = 0; q < 16; q++)
-                if (r0 + q < r1)
-                    acc[q] += w0 * sgr_px<2>(A, B, r0 + q, tx, win[(r0 + q + 3) * kLrWin + tx + 3]);
-        }
+        if (tx < tw) sgr_px16<2>(A, B, r0, r1, tx, win, w0, acc);
         __syncthreads();
     }
     if (s1) {
         sgr_ab<1>(win, A, B, sh, tw, (unsigned)s1, bdm8);
         __syncthreads();
-        if (tx < tw) {
-#pragma unroll
-            for (int q = 0; q < 16; q++)
-                if (r0 + q < r1)
-                    acc[q] += w1 * sgr_px<1>(A, B, r0 + q, tx, win[(r0 + q + 3) * kLrWin + tx + 3]);
-        }
+        if (tx < tw) sgr_px16<1>(A, B, r0, r1, tx, win, w1, acc);
     }
     if (tx < tw) {
 #pragma unroll
