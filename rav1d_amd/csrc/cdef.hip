@@ -138,9 +138,10 @@ __device__ __forceinline__ int cdef_px(const int16_t *t, int ts, int x, int y, i
     return v;
 }
 
-// Tile loader: the (ROWS x COLS) window at (x0-2, y0-2) as int16, i16::MIN outside the frame.
-// All loads of the calling lane are issued before the first LDS store (fully unrolled, constant
-// divisors) so their HBM latencies overlap.
+// Tile loader: the (ROWS x COLS) window at (x0-2, y0-2) as int16, i16::MIN outside the frame,
+// written twice: T[r][c] and T1[r][c-1] (T shifted left by one sample), so that any horizontal
+// sample pair (c, c+1) is one aligned 32-bit LDS word in T (c even) or T1 (c odd). All loads of
+// the calling lane are issued before the first LDS store (unrolled, constant divisors).
 template <typename Px, int ROWS, int COLS>
 struct TileLoad {
     static constexpr int N = ROWS * COLS, IT = (N + 255) / 256;
@@ -156,15 +157,162 @@ struct TileLoad {
                 v[k] = (int16_t) reinterpret_cast<const Px *>(src + (int64_t)y * stride)[x];
         }
     }
-    __device__ __forceinline__ void store(int16_t *t, int ts) const {
+    __device__ __forceinline__ void store(int16_t *t, int16_t *t1, int ts) const {
 #pragma unroll
         for (int k = 0; k < IT; k++) {
             const int i = threadIdx.x + 256 * k;
             const int r = i / COLS, c = i - r * COLS;
-            if (i < N) t[r * ts + c] = v[k];
+            if (i < N) {
+                t[r * ts + c] = v[k];
+                if (c) t1[r * ts + c - 1] = v[k];
+            }
         }
     }
 };
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// constrain() (cdef.rs:545) on two samples at once. d = sat(p - c): a sentinel tap gives
+// d = -32768 and |d| = 32767 (saturated), so its contribution is 0 exactly as in 32-bit.
+__device__ __forceinline__ s16x2 constrain2(s16x2 d, s16x2 thr, s16x2 shift) {
+    const s16x2 zero = { 0, 0 };
+    const s16x2 ad = __builtin_elementwise_max(d, __builtin_elementwise_sub_sat(zero, d));
+    const s16x2 m = __builtin_elementwise_max(zero, thr - (ad >> shift));
+    return __builtin_elementwise_max(__builtin_elementwise_min(d, m), zero - m);
+}
+
+// byte offset of tap (dy, dx) from a pair's base in T: pairs at odd dx come from T1
+template <int TS, int T1OFF>
+__device__ __forceinline__ int tap_delta(int dy, int dx) {
+    return dy * TS * 2 + (dx - (dx & 1)) * 2 + (dx & 1) * T1OFF;
+}
+
+struct PairTaps {
+    int pri[4], sec[8];      // byte deltas: pri (k0+, k0-, k1+, k1-), sec (d2 k0 +-, d6 k0 +-, d2 k1 +-, d6 k1 +-)
+};
+
+template <int TS, int T1OFF>
+__device__ __forceinline__ void make_taps(PairTaps &t, int dir) {
+    constexpr unsigned DY0 = 0x33332221u, DX0 = 0x22233333u, DY1 = 0x44443210u, DX1 = 0x12344444u;
+    const int d2 = (dir + 2) & 7, d6 = (dir + 6) & 7;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const unsigned DY = k ? DY1 : DY0, DX = k ? DX1 : DX0;
+        const int py = nib(DY, dir), px = nib(DX, dir);
+        t.pri[2 * k] = tap_delta<TS, T1OFF>(py, px);
+        t.pri[2 * k + 1] = tap_delta<TS, T1OFF>(-py, -px);
+        const int ay = nib(DY, d2), ax = nib(DX, d2), by = nib(DY, d6), bx = nib(DX, d6);
+        t.sec[4 * k] = tap_delta<TS, T1OFF>(ay, ax);
+        t.sec[4 * k + 1] = tap_delta<TS, T1OFF>(-ay, -ax);
+        t.sec[4 * k + 2] = tap_delta<TS, T1OFF>(by, bx);
+        t.sec[4 * k + 3] = tap_delta<TS, T1OFF>(-by, -bx);
+    }
+}
+
+__device__ __forceinline__ s16x2 ld2(const char *p) { return *reinterpret_cast<const s16x2 *>(p); }
+
+// cdef_filter_block_c inner loop (cdef.rs:668-790) for the pixel pair whose base is P.
+__device__ __forceinline__ s16x2 cdef_pair(const char *P, const PairTaps &t, int pri, int sec,
+                                           int damping, int bdm8) {
+    const s16x2 c = ld2(P);
+    s16x2 sum = { 0, 0 }, mx = c;
+    u16x2 mn = __builtin_bit_cast(u16x2, c);
+    if (pri) {
+        const short sh = (short)max(0, damping - ulog2i(pri));
+        const s16x2 thr = { (short)pri, (short)pri }, shv = { sh, sh };
+        const short tap0 = (short)(4 - ((pri >> bdm8) & 1)), tap1 = (short)((tap0 & 3) | 2);
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const s16x2 a = ld2(P + t.pri[2 * k]), b = ld2(P + t.pri[2 * k + 1]);
+            const s16x2 v = constrain2(__builtin_elementwise_sub_sat(a, c), thr, shv) +
+                            constrain2(__builtin_elementwise_sub_sat(b, c), thr, shv);
+            const short tp = k ? tap1 : tap0;
+            const s16x2 tpv = { tp, tp };
+            sum += tpv * v;
+            mn = __builtin_elementwise_min(mn, __builtin_bit_cast(u16x2, a));
+            mn = __builtin_elementwise_min(mn, __builtin_bit_cast(u16x2, b));
+            mx = __builtin_elementwise_max(mx, a);
+            mx = __builtin_elementwise_max(mx, b);
+        }
+    }
+    if (sec) {
+        const short sh = (short)(damping - ulog2i(sec));
+        const s16x2 thr = { (short)sec, (short)sec }, shv = { sh, sh };
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            s16x2 v = { 0, 0 };
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const s16x2 a = ld2(P + t.sec[4 * k + j]);
+                v += constrain2(__builtin_elementwise_sub_sat(a, c), thr, shv);
+                mn = __builtin_elementwise_min(mn, __builtin_bit_cast(u16x2, a));
+                mx = __builtin_elementwise_max(mx, a);
+            }
+            sum += k ? v : v + v;
+        }
+    }
+    const s16x2 one5 = { 15, 15 }, eight = { 8, 8 }, four = { 4, 4 };
+    s16x2 v = c + ((sum + (sum >> one5) + eight) >> four);
+    if (pri && sec) v = __builtin_elementwise_min(__builtin_elementwise_max(v, __builtin_bit_cast(s16x2, mn)), mx);
+    return v;
+}
+
+template <typename Px> __device__ __forceinline__ void store_pair(Px *d, s16x2 v);
+template <> __device__ __forceinline__ void store_pair<uint16_t>(uint16_t *d, s16x2 v) {
+    *reinterpret_cast<s16x2 *>(d) = v;
+}
+template <> __device__ __forceinline__ void store_pair<uint8_t>(uint8_t *d, s16x2 v) {
+    *reinterpret_cast<uint16_t *>(d) = (uint16_t)((v.x & 0xff) | (v.y << 8));
+}
+template <typename Px> __device__ __forceinline__ void copy_pair(Px *d, const Px *s);
+template <> __device__ __forceinline__ void copy_pair<uint16_t>(uint16_t *d, const uint16_t *s) {
+    *reinterpret_cast<uint32_t *>(d) = *reinterpret_cast<const uint32_t *>(s);
+}
+template <> __device__ __forceinline__ void copy_pair<uint8_t>(uint8_t *d, const uint8_t *s) {
+    *reinterpret_cast<uint16_t *>(d) = *reinterpret_cast<const uint16_t *>(s);
+}
+
+// Filter (or copy) one plane of the unit as pixel pairs. W x H plane pixels, BW x BH pixels per
+// direction block; LP lanes (lane index `lane`) each own one pair column and NR consecutive rows.
+template <typename Px, int W, int H, int BW, int BH, int LP, int TS, int T1OFF, int MASK, bool TILE_COPY>
+__device__ __forceinline__ void filter_plane(const int16_t *T, int lane, const int8_t *bdir,
+                                             const int8_t *bflag, const int16_t *bpri, bool adj_pri,
+                                             int pri_lvl, int sec, int damping, int bdm8, bool remap422,
+                                             const uint8_t *src, uint8_t *dst, int64_t stride,
+                                             int gx0, int gy0, int fw, int fh) {
+    constexpr int PW = W / 2, NR = H * PW / LP, RB = NR < BH ? NR : BH;
+    const int pc = lane % PW, rg = lane / PW, x = 2 * pc;
+#pragma unroll
+    for (int bb = 0; bb < NR / RB; bb++) {
+        const int r0 = rg * NR + bb * RB;
+        const int b = (r0 / BH) * 8 + x / BW;
+        const int flag = bflag[b];
+        const int gx = gx0 + x;
+        if (flag & MASK) {
+            const int pri = adj_pri ? bpri[b] : pri_lvl;
+            int dir = pri_lvl ? bdir[b] : 0;
+            if (remap422 && pri_lvl) dir = nib(0x66654207u, dir) + 2;   // {7,0,2,4,5,6,6,6}
+            PairTaps t;
+            make_taps<TS, T1OFF>(t, dir);
+#pragma unroll
+            for (int i = 0; i < RB; i++) {
+                const int r = r0 + i;
+                const char *P = reinterpret_cast<const char *>(T + (r + 2) * TS + x + 2);
+                const s16x2 v = cdef_pair(P, t, pri, sec, damping, bdm8);
+                store_pair<Px>(reinterpret_cast<Px *>(dst + (int64_t)(gy0 + r) * stride) + gx, v);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < RB; i++) {
+                const int r = r0 + i, gy = gy0 + r;
+                Px *dp = reinterpret_cast<Px *>(dst + (int64_t)gy * stride) + gx;
+                if (TILE_COPY && gx < fw && gy < fh) store_pair<Px>(dp, ld2(reinterpret_cast<const char *>(T + (r + 2) * TS + x + 2)));
+                else copy_pair<Px>(dp, reinterpret_cast<const Px *>(src + (int64_t)gy * stride) + gx);
+            }
+        }
+    }
+}
 
 // One 64x64 luma unit (+ co-located chroma) per 256-lane workgroup. L = layout (0 I400,
 // 1 I420, 2 I422, 3 I444), compile-time so every tile index is a shift or a constant divide.
@@ -173,8 +321,9 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
     constexpr int SSH = L == 1 || L == 2, SSV = L == 1;
     constexpr int CW = 64 >> SSH, CH = 64 >> SSV, CTS = CW + 8;
     constexpr int UVW = 8 >> SSH, UVH = 8 >> SSV;
-    __shared__ int16_t ty[kTY * kTS];
-    __shared__ int16_t tuv[2][L ? (CH + 4) * CTS : 1];
+    constexpr int YN = kTY * kTS, CN = L ? (CH + 4) * CTS : 2;
+    __shared__ int16_t ty[2 * YN];                 // T, T1
+    __shared__ int16_t tuv[2][2 * CN];             // per chroma plane: T, T1
     __shared__ int8_t bdir[64];
     __shared__ int8_t bflag[64];          // bit0 luma filtered, bit1 chroma filtered
     __shared__ int16_t bpri[64];
@@ -219,10 +368,10 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
             lu.fetch(a.src[1], a.stride[1], x0 >> SSH, y0 >> SSV, fwc, fhc);
             lv.fetch(a.src[2], a.stride[2], x0 >> SSH, y0 >> SSV, fwc, fhc);
         }
-        ly.store(ty, kTS);
+        ly.store(ty, ty + YN, kTS);
         if (L && uv_lvl) {
-            lu.store(tuv[0], CTS);
-            lv.store(tuv[1], CTS);
+            lu.store(tuv[0], tuv[0] + CN, CTS);
+            lv.store(tuv[1], tuv[1] + CN, CTS);
         }
     }
     __syncthreads();
@@ -252,47 +401,17 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
     }
     __syncthreads();
 
-    // luma: one wave per 64-px row
-#pragma unroll 4
-    for (int k = 0; k < 16; k++) {
-        const int i = threadIdx.x + 256 * k;
-        const int r = i >> 6, c = i & 63;
-        const int b = (r >> 3) * 8 + (c >> 3);
-        const int gx = x0 + c, gy = y0 + r;
-        Px *dp = reinterpret_cast<Px *>(a.dst[0] + (int64_t)gy * a.stride[0]) + gx;
-        int v;
-        if (bflag[b] & 1) {
-            const int pri = y_pri ? bpri[b] : 0;
-            const int dir = y_pri ? bdir[b] : 0;
-            v = cdef_px(ty, kTS, c + 2, r + 2, pri, y_sec, dir, a.damping, bdm8);
-        } else if (gx < fwy && gy < fhy) {
-            v = ty[(r + 2) * kTS + c + 2];
-        } else {
-            v = reinterpret_cast<const Px *>(a.src[0] + (int64_t)gy * a.stride[0])[gx];
-        }
-        *dp = (Px)v;
-    }
-    // chroma
+    // luma: 2048 pairs, 8 rows of one 8x8 block per lane
+    filter_plane<Px, 64, 64, 8, 8, 256, kTS, YN * 2, 1, true>(
+        ty, threadIdx.x, bdir, bflag, bpri, y_pri != 0, y_pri, y_sec, a.damping, bdm8, false,
+        a.src[0], a.dst[0], a.stride[0], x0, y0, fwy, fhy);
     if (L) {
-        constexpr int NC = CW * CH;
-#pragma unroll 2
-        for (int k = 0; k < 2 * NC / 256; k++) {
-            const int i = threadIdx.x + 256 * k;
-            const int p = 1 + (i >= NC), j = i - (p - 1) * NC;
-            const int r = j / CW, c = j % CW;
-            const int b = (r / UVH) * 8 + (c / UVW);
-            const int gx = (x0 >> SSH) + c, gy = (y0 >> SSV) + r;
-            Px *dp = reinterpret_cast<Px *>(a.dst[p] + (int64_t)gy * a.stride[p]) + gx;
-            int v;
-            if (bflag[b] & 2) {
-                int d = uv_pri ? bdir[b] : 0;
-                if (L == 2 && uv_pri) d = nib(0x66654207u, d) + 2;   // 4:2:2 direction remap {7,0,2,4,5,6,6,6}
-                v = cdef_px(tuv[p - 1], CTS, c + 2, r + 2, uv_pri, uv_sec, d, a.damping - 1, bdm8);
-            } else {
-                v = reinterpret_cast<const Px *>(a.src[p] + (int64_t)gy * a.stride[p])[gx];
-            }
-            *dp = (Px)v;
-        }
+        // chroma: lanes 0..127 U, 128..255 V (damping - 1, cdef_apply.rs)
+        const int p = 1 + (threadIdx.x >> 7);
+        // (the chroma tile is only staged when uv_lvl != 0: unfiltered chroma copies from D)
+        filter_plane<Px, CW, CH, UVW, UVH, 128, CTS, CN * 2, 2, false>(
+            tuv[p - 1], threadIdx.x & 127, bdir, bflag, bpri, false, uv_pri, uv_sec, a.damping - 1, bdm8,
+            L == 2, a.src[p], a.dst[p], a.stride[p], x0 >> SSH, y0 >> SSV, fwc, fhc);
     }
 }
 
