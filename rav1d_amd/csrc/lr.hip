@@ -7,7 +7,8 @@
 // unit and a line buffer of deblocked rows around every stripe boundary. Reading the CDEF output
 // C (immutable) inside the stripe and the deblocked picture D for the rows beyond a stripe edge
 // gives exactly the samples it sees, so every (stripe, 32/64-px column tile) is independent:
-// one 256-lane workgroup each, the (h+6) x (w+6) window staged once in LDS, both filter passes
+// one 512-lane workgroup each (8 waves, so 4 resident tiles fill a CU), the (h+6) x (w+6)
+// window staged once in LDS, both filter passes
 // (or the box sums and the A/B maps of the self-guided filter) computed from LDS, and the
 // output streamed to a separate picture O.
 #include "common.h"
@@ -16,6 +17,11 @@ namespace mi {
 
 constexpr int kLrWin = 72;             // LDS window row stride (int16), >= 64 + 6
 constexpr int kLrAB = 68;              // A/B row stride
+constexpr int kNY = 8;                 // waves (row groups) per workgroup
+constexpr int kNR = 64 / kNY;          // output rows per lane
+constexpr int kNT = 64 * kNY;          // lanes per workgroup
+constexpr int kWL = (70 + kNY - 1) / kNY;   // window rows loaded per lane
+constexpr int kABG = kNT / 66;         // A/B row groups (66 columns each)
 
 __constant__ uint16_t k_sgr_params[16][2] = {
     { 140, 3236 }, { 112, 2158 }, { 93, 1618 }, { 80, 1438 }, { 70, 1295 }, { 58, 1177 },
@@ -43,11 +49,11 @@ template <int R>
 __device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, unsigned s, int bdm8) {
     constexpr int n = (2 * R + 1) * (2 * R + 1);
     constexpr unsigned one_by_x = n == 25 ? 164 : 455;
-    // 66 columns x 3 row groups = 198 lanes, one column each
+    // 66 columns x kABG row groups, one column per lane
     const int g = threadIdx.x / 66, c = threadIdx.x - g * 66;
-    if (g >= 3 || c >= tw + 2) return;
+    if (g >= kABG || c >= tw + 2) return;
     const int nrows = sh + 2;                         // y = -1 .. sh
-    const int per = (nrows + 2) / 3;
+    const int per = (nrows + kABG - 1) / kABG;
     const int y0 = -1 + g * per, y1 = min(-1 + (g + 1) * per, sh + 1);
     {
         const int x = c - 1;                          // position column (-1 .. tw)
@@ -87,12 +93,12 @@ __device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, u
     }
 }
 
-// Self-guided output terms for rows r0..r0+15 of column i (looprestoration.rs selfguided_filter
+// Self-guided output terms for rows r0..r0+kNR-1 of column i (looprestoration.rs selfguided_filter
 // tail). The lane walks down its column keeping, per A/B row, the centre value c and the sum of
 // its two horizontal neighbours s in registers: 3 A + 3 B LDS reads per row instead of 9 + 9.
 template <int R>
-__device__ __forceinline__ void sgr_px16(const int *A, const int16_t *B, int r0, int r1, int i,
-                                         const int16_t *win, int w, int acc[16]) {
+__device__ __forceinline__ void sgr_px(const int *A, const int16_t *B, int r0, int r1, int i,
+                                       const int16_t *win, int w, int acc[kNR]) {
     const int *a0 = A + i + 1;
     const int16_t *b0 = B + i + 1;
     auto ld = [&](int y, int &ca, int &sa, int &cb, int &sb) {
@@ -106,7 +112,7 @@ __device__ __forceinline__ void sgr_px16(const int *A, const int16_t *B, int r0,
         ld(r0 - 1, ca0, sa0, cb0, sb0);
         ld(r0, ca1, sa1, cb1, sb1);
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
+        for (int q = 0; q < kNR; q++) {
             ld(r0 + q + 1, ca2, sa2, cb2, sb2);
             if (r0 + q < r1) {
                 const int src = win[(r0 + q + 3) * kLrWin + i + 3];
@@ -122,7 +128,7 @@ __device__ __forceinline__ void sgr_px16(const int *A, const int16_t *B, int r0,
         int cau, sau, cbu, sbu, cad, sad, cbd, sbd;
         ld(r0 - 1, cau, sau, cbu, sbu);
 #pragma unroll
-        for (int q = 0; q < 16; q += 2) {
+        for (int q = 0; q < kNR; q += 2) {
             ld(r0 + q + 1, cad, sad, cbd, sbd);
             if (r0 + q < r1) {
                 const int src = win[(r0 + q + 3) * kLrWin + i + 3];
@@ -145,7 +151,7 @@ __device__ __forceinline__ void sgr_px16(const int *A, const int16_t *B, int r0,
 __device__ __forceinline__ int stripe_start(int k, int ssv) { return k ? (64 * k - 8) >> ssv : 0; }
 
 template <typename Px>
-__global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
+__global__ __launch_bounds__(kNT) void lr_kernel(LrArgs a) {
     __shared__ int16_t win[70 * kLrWin];
     __shared__ int A[66 * kLrAB];
     __shared__ int16_t B[66 * kLrAB];
@@ -168,8 +174,8 @@ __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
     const uint8_t *D = a.lpf[p];
     uint8_t *O = a.dst[p];
     const int64_t st = a.stride[p];
-    // lane (tx, ty) owns output column tx, rows [ty*16, ty*16+16)
-    const int r0 = ty * 16, r1 = min(r0 + 16, sh);
+    // lane (tx, ty) owns output column tx, rows [ty*kNR, ty*kNR+kNR)
+    const int r0 = ty * kNR, r1 = min(r0 + kNR, sh);
 
     // restoration unit of this tile (lr_apply.rs:151-259 indexing)
     int type = 0;
@@ -189,11 +195,11 @@ __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
     }
     if (type == 0) {   // RESTORATION_NONE: O = C
         if (tx < tw) {
-            int v[16];
+            int v[kNR];
 #pragma unroll
-            for (int q = 0; q < 16; q++) v[q] = r0 + q < r1 ? ld_px<Px>(C, st, S + r0 + q, x0 + tx) : 0;
+            for (int q = 0; q < kNR; q++) v[q] = r0 + q < r1 ? ld_px<Px>(C, st, S + r0 + q, x0 + tx) : 0;
 #pragma unroll
-            for (int q = 0; q < 16; q++)
+            for (int q = 0; q < kNR; q++)
                 if (r0 + q < r1) reinterpret_cast<Px *>(O + (int64_t)(S + r0 + q) * st)[x0 + tx] = (Px)v[q];
         }
         return;
@@ -202,11 +208,11 @@ __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
     // ---- stage the (sh+6) x (tw+6) window (C inside the stripe, D across its edges) ----
     const bool have_top = k > 0, have_bottom = E < ph;
     const int wr = sh + 6, wc = tw + 6;
-    // all 18 row loads of this lane are issued before the first LDS store (latency overlap)
-    int16_t v0[18], v1[18];
+    // all row loads of this lane are issued before the first LDS store (latency overlap)
+    int16_t v0[kWL], v1[kWL];
 #pragma unroll
-    for (int q = 0; q < 18; q++) {
-        const int rr = ty + 4 * q, r = rr - 3;
+    for (int q = 0; q < kWL; q++) {
+        const int rr = ty + kNY * q, r = rr - 3;
         v0[q] = v1[q] = 0;
         if (rr < wr) {
             int yy;
@@ -220,8 +226,8 @@ __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
         }
     }
 #pragma unroll
-    for (int q = 0; q < 18; q++) {
-        const int rr = ty + 4 * q;
+    for (int q = 0; q < kWL; q++) {
+        const int rr = ty + kNY * q;
         if (rr < wr) {
             win[rr * kLrWin + tx] = v0[q];
             if (tx + 64 < wc) win[rr * kLrWin + tx + 64] = v1[q];
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
         const int rbh = bd == 12 ? 5 : 3, rbv = bd == 12 ? 9 : 11;
         const int clip_h = (1 << (bd + 1 + 7 - rbh)) - 1;
         if (tx < tw) {
-            for (int rr = ty; rr < wr; rr += 4) {
+            for (int rr = ty; rr < wr; rr += kNY) {
                 const int16_t *row = win + rr * kLrWin + tx;
                 int sum = 1 << (bd + 6);
 #pragma unroll
@@ -251,11 +257,11 @@ __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
         __syncthreads();
         if (tx < tw && r0 < r1) {
             const int off = 1 << (bd + rbv - 1);
-            int h[22];
+            int h[kNR + 6];
 #pragma unroll
-            for (int q = 0; q < 22; q++) h[q] = r0 + q < wr ? (int)(uint16_t)hor[(r0 + q) * 64 + tx] : 0;
+            for (int q = 0; q < kNR + 6; q++) h[q] = r0 + q < wr ? (int)(uint16_t)hor[(r0 + q) * 64 + tx] : 0;
 #pragma unroll
-            for (int q = 0; q < 16; q++) {
+            for (int q = 0; q < kNR; q++) {
                 if (r0 + q < r1) {
                     int sum = -off;
 #pragma unroll
@@ -274,23 +280,23 @@ __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
     const int w0 = u->sgr_weights[0];
     const int w1 = 128 - (u->sgr_weights[0] + u->sgr_weights[1]);
     const int bdm8 = bd - 8;
-    int acc[16];
+    int acc[kNR];
 #pragma unroll
-    for (int q = 0; q < 16; q++) acc[q] = 0;
+    for (int q = 0; q < kNR; q++) acc[q] = 0;
     if (s0) {
         sgr_ab<2>(win, A, B, sh, tw, (unsigned)s0, bdm8);
         __syncthreads();
-        if (tx < tw) sgr_px16<2>(A, B, r0, r1, tx, win, w0, acc);
+        if (tx < tw) sgr_px<2>(A, B, r0, r1, tx, win, w0, acc);
         __syncthreads();
     }
     if (s1) {
         sgr_ab<1>(win, A, B, sh, tw, (unsigned)s1, bdm8);
         __syncthreads();
-        if (tx < tw) sgr_px16<1>(A, B, r0, r1, tx, win, w1, acc);
+        if (tx < tw) sgr_px<1>(A, B, r0, r1, tx, win, w1, acc);
     }
     if (tx < tw) {
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
+        for (int q = 0; q < kNR; q++) {
             if (r0 + q < r1) {
                 const int px = win[(r0 + q + 3) * kLrWin + tx + 3];
                 const int v = min(max(px + ((acc[q] + (1 << 10)) >> 11), 0), bdmax);
@@ -303,8 +309,8 @@ __global__ __launch_bounds__(256) void lr_kernel(LrArgs a) {
 int launch_lr(const LrArgs &a, int bpc, hipStream_t s) {
     const int n = a.blk_start[3];
     if (n <= 0) return 0;
-    if (bpc == 8) hipLaunchKernelGGL(lr_kernel<uint8_t>, dim3(n), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(lr_kernel<uint16_t>, dim3(n), dim3(256), 0, s, a);
+    if (bpc == 8) hipLaunchKernelGGL(lr_kernel<uint8_t>, dim3(n), dim3(kNT), 0, s, a);
+    else hipLaunchKernelGGL(lr_kernel<uint16_t>, dim3(n), dim3(kNT), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
