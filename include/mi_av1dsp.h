@@ -141,6 +141,26 @@ typedef struct MiFilmGrainData {
     int clip_to_restricted_range;
 } MiFilmGrainData;
 
+/* One motion-compensated prediction unit: a block's rectangle in one plane (24 bytes).
+ * Replaces the per-block arguments of recon's mc() (src/recon.rs:2025-2203; C
+ * recon_tmpl.c:962-1011) plus the compound dispatch (recon_tmpl.c:1836-1921). */
+#define MI_MC_AVG  0   /* COMP_INTER_AVG: avg(tmp[0], tmp[1]) */
+#define MI_MC_WAVG 1   /* COMP_INTER_WEIGHTED_AVG: w_avg(tmp[0], tmp[1], weight) */
+#define MI_MC_MASK 2   /* COMP_INTER_WEDGE (and chroma of SEG): mask(tmp[sign], tmp[!sign], mask) */
+#define MI_MC_SEG  3   /* COMP_INTER_SEG, luma: w_mask(tmp[sign], tmp[!sign]); writes the chroma mask */
+typedef struct MiMcBlock {
+    uint16_t x, y;          /* top-left, plane pixels */
+    uint8_t  w, h;          /* plane pixels, 2..128 (bw4 * h_mul, bh4 * v_mul) */
+    uint8_t  plane;         /* 0..2 */
+    uint8_t  filter2d;      /* enum Filter2d (src/levels.rs): 0..8 8-tap (h, v) pairs, 9 bilinear */
+    int16_t  mvx[2], mvy[2];/* per reference, luma 1/8-pel units as coded (mv.x, mv.y) */
+    int8_t   ref[2];        /* index into the refs[] array; ref[1] < 0: single prediction (put) */
+    uint8_t  comp;          /* MI_MC_* for compound units */
+    uint8_t  param;         /* bits 0-4: w_avg weight (jnt_weights), bit 7: mask_sign */
+    uint32_t mask_off;      /* byte offset into the mask buffer (MASK: w*h read; SEG: written at
+                               the chroma resolution, (w >> ss_hor) * (h >> ss_ver)) */
+} MiMcBlock;
+
 /* ------------------------------------------------------------------------------------ */
 /* Context                                                                               */
 /* ------------------------------------------------------------------------------------ */
@@ -176,6 +196,17 @@ int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
  * Equivalent to the reference's per-sbrow cols/rows interleaving;
  * replaces rav1d_loopfilter_sbrow_cols/_rows (src/lf_apply.rs:597-834). */
 int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, void *stream);
+
+/* Motion compensation for a whole frame: writes the inter prediction of every unit into
+ * `cur` (itx then adds the residual). `refs` (host array of nrefs pictures, device planes,
+ * grain-free, same size as cur) are read with edge replication (emu_edge, mc_tmpl.c:798-845).
+ * `blocks` (device) must list all luma units first: luma = blocks[plane_start[0] ..
+ * plane_start[1]), chroma = [plane_start[1] .. plane_start[3]) — chroma of a SEG unit reads
+ * the mask its luma unit wrote. `masks` (device) holds MASK inputs and SEG outputs.
+ * Scaled references, OBMC, warped and inter-intra units are not batched here yet. */
+int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
+                const MiMcBlock *blocks, const uint32_t plane_start[4], uint8_t *masks,
+                void *stream);
 
 /* CDEF for a whole frame, out of place: reads the deblocked picture `src` (never written)
  * and writes `dst` (blocks the reference skips are copied). Replaces rav1d_cdef_brow

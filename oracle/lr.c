@@ -419,7 +419,6 @@ void oracle_lr_frame(void *const dst[3], void *const cdef[3], void *const debloc
     }
     for (int p = 0; p < nplanes; p++) {
         if (!(restore_planes & (1 << p))) continue;
-        const int pw = p ? (w + f.ss_hor) >> f.ss_hor : w;
         const int ph = p ? (h + f.ss_ver) >> f.ss_ver : h;
         const int bw8 = p ? ((((w + 7) >> 3) << 3) >> f.ss_hor) : (((w + 7) >> 3) << 3);
         build_lpf(&f, p, deblocked[p], strides[p], bw8, ph);

@@ -1,0 +1,471 @@
+/*
+ * mc.c — CPU restatement of the motion-compensation DSP family. TEST INFRASTRUCTURE ONLY.
+ *
+ * Follows rav1d src/mc.rs (`*_rust` fallbacks) == dav1d C src/mc_tmpl.c:
+ *   put/prep 8-tap         mc_tmpl.c:100-200, 228-290   (mc.rs put_8tap_rust :130-209, prep :277)
+ *   put/prep 8-tap scaled  mc_tmpl.c:201-227, 291-330
+ *   put/prep bilinear      mc_tmpl.c:380-560            (mc.rs :431-652)
+ *   avg / w_avg / mask     mc_tmpl.c:561-620            (mc.rs :654-745)
+ *   blend / blend_v / _h   mc_tmpl.c:621-660            (mc.rs :747-810)
+ *   w_mask                 mc_tmpl.c:661-712            (mc.rs :812-883)
+ *   warp 8x8 / 8x8t        mc_tmpl.c:714-796            (mc.rs :885-1030)
+ *   emu_edge               mc_tmpl.c:798-845            (mc.rs :1032-1112)
+ *   resize                 mc_tmpl.c:847-875            (mc.rs :1114-1172)
+ * and the per-block driver `mc()` + compound dispatch of recon (recon_tmpl.c:962-1070,
+ * 1836-1925; rav1d src/recon.rs:2025-2203, 3236-3428).
+ *
+ * Pixels are uint8_t (bpc 8) or uint16_t (bpc 10/12); strides in bytes; intermediates int16.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle.h"
+
+static const int8_t subpel[6][15][8] = {
+#include "../rav1d_amd/csrc/tables/mc_subpel_filters.inc"
+};
+static const int8_t warp_filter[193][8] = {
+#include "../rav1d_amd/csrc/tables/mc_warp_filter.inc"
+};
+static const int8_t resize_filter[64][8] = {
+#include "../rav1d_amd/csrc/tables/resize_filter.inc"
+};
+static const uint8_t obmc_masks[64] = {
+#include "../rav1d_amd/csrc/tables/obmc_masks.inc"
+};
+
+static inline int clip(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+
+typedef struct {
+    int bpc, ib, bias, bdmax;
+} Bd;
+
+static Bd bd_of(int bpc) {
+    Bd b = { bpc, bpc == 8 ? 4 : 14 - bpc, bpc == 8 ? 0 : 8192, (1 << bpc) - 1 };
+    return b;
+}
+
+static inline int ldp(const void *p, ptrdiff_t stride, int y, int x, int bpc) {
+    const uint8_t *r = (const uint8_t *)p + y * stride;
+    return bpc == 8 ? r[x] : ((const uint16_t *)r)[x];
+}
+static inline void stp(void *p, ptrdiff_t stride, int y, int x, int v, int bpc) {
+    uint8_t *r = (uint8_t *)p + y * stride;
+    if (bpc == 8) r[x] = (uint8_t)v;
+    else ((uint16_t *)r)[x] = (uint16_t)v;
+}
+
+/* filter2d (levels.rs Filter2d, order horizontal/vertical) -> (type_h, type_v); 0 regular,
+ * 1 smooth, 2 sharp (mc_tmpl.c:331-341 filter_fns instantiations) */
+static const uint8_t f2d_h[9] = { 0, 0, 0, 2, 2, 2, 1, 1, 1 };
+static const uint8_t f2d_v[9] = { 0, 1, 2, 0, 1, 2, 0, 1, 2 };
+
+static const int8_t *hfilter(int mx, int w, int type_h) {
+    if (!mx) return NULL;
+    return w > 4 ? subpel[type_h][mx - 1] : subpel[3 + (type_h & 1)][mx - 1];
+}
+static const int8_t *vfilter(int my, int h, int type_v) {
+    if (!my) return NULL;
+    return h > 4 ? subpel[type_v][my - 1] : subpel[3 + (type_v & 1)][my - 1];
+}
+
+/* 8-tap sum over src samples at x + k*step, k = -3..4 (FILTER_8TAP) */
+static int tap8_px(const void *src, ptrdiff_t stride, int y, int x, int dy, int dx, const int8_t *F, int bpc) {
+    int s = 0;
+    for (int k = 0; k < 8; k++) s += F[k] * ldp(src, stride, y + (k - 3) * dy, x + (k - 3) * dx, bpc);
+    return s;
+}
+static int tap8_mid(const int16_t *mid, int ms, int y, int x, const int8_t *F) {
+    int s = 0;
+    for (int k = 0; k < 8; k++) s += F[k] * mid[(y + k - 3) * ms + x];
+    return s;
+}
+static inline int rnd(int v, int sh) { return (v + ((1 << sh) >> 1)) >> sh; }
+
+/* put_8tap_c (mc_tmpl.c:100-176) / prep_8tap_c (:228-290); out16 != NULL selects prep */
+static void mc_8tap(void *dst, ptrdiff_t ds, int16_t *tmp, const void *src, ptrdiff_t ss, int w, int h,
+                    int mx, int my, int filter_type, Bd b) {
+    const int8_t *fh = hfilter(mx, w, filter_type & 3), *fv = vfilter(my, h, filter_type >> 2);
+    const int ib = b.ib;
+    if (fh && fv) {
+        int16_t *mid = malloc(sizeof(int16_t) * 128 * 135);
+        for (int y = 0; y < h + 7; y++)
+            for (int x = 0; x < w; x++)
+                mid[y * 128 + x] = (int16_t)rnd(tap8_px(src, ss, y - 3, x, 0, 1, fh, b.bpc), 6 - ib);
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                if (tmp) tmp[y * w + x] = (int16_t)(rnd(tap8_mid(mid, 128, y + 3, x, fv), 6) - b.bias);
+                else stp(dst, ds, y, x, clip(rnd(tap8_mid(mid, 128, y + 3, x, fv), 6 + ib), 0, b.bdmax), b.bpc);
+            }
+        free(mid);
+    } else if (fh) {
+        const int irnd = 32 + ((1 << (6 - ib)) >> 1);
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                const int s = tap8_px(src, ss, y, x, 0, 1, fh, b.bpc);
+                if (tmp) tmp[y * w + x] = (int16_t)(rnd(s, 6 - ib) - b.bias);
+                else stp(dst, ds, y, x, clip((s + irnd) >> 6, 0, b.bdmax), b.bpc);
+            }
+    } else if (fv) {
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                const int s = tap8_px(src, ss, y, x, 1, 0, fv, b.bpc);
+                if (tmp) tmp[y * w + x] = (int16_t)(rnd(s, 6 - ib) - b.bias);
+                else stp(dst, ds, y, x, clip(rnd(s, 6), 0, b.bdmax), b.bpc);
+            }
+    } else {
+        /* put_c / prep_c (mc_tmpl.c:52-78) */
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                const int v = ldp(src, ss, y, x, b.bpc);
+                if (tmp) tmp[y * w + x] = (int16_t)((v << ib) - b.bias);
+                else stp(dst, ds, y, x, v, b.bpc);
+            }
+    }
+}
+
+/* put_bilin_c / prep_bilin_c (mc_tmpl.c:380-500): FILTER_BILIN = 16*a + m*(b-a) */
+static void mc_bilin(void *dst, ptrdiff_t ds, int16_t *tmp, const void *src, ptrdiff_t ss, int w, int h,
+                     int mx, int my, Bd b) {
+    const int ib = b.ib;
+#define BIL_PX(y, x, m, dy, dx) (16 * ldp(src, ss, y, x, b.bpc) + (m) * (ldp(src, ss, (y) + (dy), (x) + (dx), b.bpc) - ldp(src, ss, y, x, b.bpc)))
+    if (mx && my) {
+        int16_t *mid = malloc(sizeof(int16_t) * 128 * 129);
+        for (int y = 0; y < h + 1; y++)
+            for (int x = 0; x < w; x++) mid[y * 128 + x] = (int16_t)rnd(BIL_PX(y, x, mx, 0, 1), 4 - ib);
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                const int a = mid[y * 128 + x], c = mid[(y + 1) * 128 + x];
+                const int s = 16 * a + my * (c - a);
+                if (tmp) tmp[y * w + x] = (int16_t)(rnd(s, 4) - b.bias);
+                else stp(dst, ds, y, x, clip(rnd(s, 4 + ib), 0, b.bdmax), b.bpc);
+            }
+        free(mid);
+    } else if (mx) {
+        const int irnd = (1 << ib) >> 1;
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                const int px = rnd(BIL_PX(y, x, mx, 0, 1), 4 - ib);
+                if (tmp) tmp[y * w + x] = (int16_t)(px - b.bias);
+                else stp(dst, ds, y, x, clip((px + irnd) >> ib, 0, b.bdmax), b.bpc);
+            }
+    } else if (my) {
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                const int s = BIL_PX(y, x, my, 1, 0);
+                if (tmp) tmp[y * w + x] = (int16_t)(rnd(s, 4 - ib) - b.bias);
+                else stp(dst, ds, y, x, clip(rnd(s, 4), 0, b.bdmax), b.bpc);
+            }
+    } else {
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                const int v = ldp(src, ss, y, x, b.bpc);
+                if (tmp) tmp[y * w + x] = (int16_t)((v << ib) - b.bias);
+                else stp(dst, ds, y, x, v, b.bpc);
+            }
+    }
+#undef BIL_PX
+}
+
+void oracle_mc_put(int filter2d, void *dst, ptrdiff_t dst_stride, const void *src, ptrdiff_t src_stride,
+                   int w, int h, int mx, int my, int bpc) {
+    const Bd b = bd_of(bpc);
+    if (filter2d == 9) mc_bilin(dst, dst_stride, NULL, src, src_stride, w, h, mx, my, b);
+    else mc_8tap(dst, dst_stride, NULL, src, src_stride, w, h, mx, my, f2d_h[filter2d] | f2d_v[filter2d] << 2, b);
+}
+
+void oracle_mc_prep(int filter2d, int16_t *tmp, const void *src, ptrdiff_t src_stride,
+                    int w, int h, int mx, int my, int bpc) {
+    const Bd b = bd_of(bpc);
+    if (filter2d == 9) mc_bilin(NULL, 0, tmp, src, src_stride, w, h, mx, my, b);
+    else mc_8tap(NULL, 0, tmp, src, src_stride, w, h, mx, my, f2d_h[filter2d] | f2d_v[filter2d] << 2, b);
+}
+
+/* put/prep_8tap_scaled_c (mc_tmpl.c:201-227, 291-330) and bilin_scaled (:445-470, 528-560):
+ * positions in 1/1024 pel, step dx/dy */
+void oracle_mc_scaled(int filter2d, int prep, void *dst, ptrdiff_t dst_stride, int16_t *tmp,
+                      const void *src, ptrdiff_t src_stride, int w, int h, int mx, int my,
+                      int dx, int dy, int bpc) {
+    const Bd b = bd_of(bpc);
+    const int ib = b.ib;
+    if (filter2d == 9) {
+        const int tmp_h = (((h - 1) * dy + my) >> 10) + 2;
+        int16_t *mid = malloc(sizeof(int16_t) * 128 * (256 + 1));
+        for (int y = 0; y < tmp_h; y++) {
+            int imx = mx, ioff = 0;
+            for (int x = 0; x < w; x++) {
+                const int m = imx >> 6;
+                const int a = ldp(src, src_stride, y, ioff, b.bpc), c = ldp(src, src_stride, y, ioff + 1, b.bpc);
+                mid[y * 128 + x] = (int16_t)rnd(16 * a + m * (c - a), 4 - ib);
+                imx += dx;
+                ioff += imx >> 10;
+                imx &= 0x3ff;
+            }
+        }
+        int row = 0;
+        for (int y = 0; y < h; y++) {
+            for (int x = 0; x < w; x++) {
+                const int a = mid[row * 128 + x], c = mid[(row + 1) * 128 + x];
+                const int s = 16 * a + (my >> 6) * (c - a);
+                if (prep) tmp[y * w + x] = (int16_t)(rnd(s, 4) - b.bias);
+                else stp(dst, dst_stride, y, x, clip(rnd(s, 4 + ib), 0, b.bdmax), b.bpc);
+            }
+            my += dy;
+            row += my >> 10;
+            my &= 0x3ff;
+        }
+        free(mid);
+        return;
+    }
+    const int ft = f2d_h[filter2d] | f2d_v[filter2d] << 2;
+    const int tmp_h = (((h - 1) * dy + my) >> 10) + 8;
+    int16_t *mid = malloc(sizeof(int16_t) * 128 * (256 + 7));
+    for (int y = 0; y < tmp_h; y++) {
+        int imx = mx, ioff = 0;
+        for (int x = 0; x < w; x++) {
+            const int8_t *fh = hfilter(imx >> 6, w, ft & 3);
+            mid[y * 128 + x] = (int16_t)(fh ? rnd(tap8_px(src, src_stride, y - 3, ioff, 0, 1, fh, b.bpc), 6 - ib)
+                                            : ldp(src, src_stride, y - 3, ioff, b.bpc) << ib);
+            imx += dx;
+            ioff += imx >> 10;
+            imx &= 0x3ff;
+        }
+    }
+    int row = 3;
+    const int irnd = (1 << ib) >> 1;
+    for (int y = 0; y < h; y++) {
+        const int8_t *fv = vfilter(my >> 6, h, ft >> 2);
+        for (int x = 0; x < w; x++) {
+            if (prep) {
+                tmp[y * w + x] = (int16_t)((fv ? rnd(tap8_mid(mid, 128, row, x, fv), 6) : mid[row * 128 + x]) - b.bias);
+            } else {
+                const int v = fv ? rnd(tap8_mid(mid, 128, row, x, fv), 6 + ib) : (mid[row * 128 + x] + irnd) >> ib;
+                stp(dst, dst_stride, y, x, clip(v, 0, b.bdmax), b.bpc);
+            }
+        }
+        my += dy;
+        row += my >> 10;
+        my &= 0x3ff;
+    }
+    free(mid);
+}
+
+/* avg_c / w_avg_c / mask_c (mc_tmpl.c:561-620) */
+void oracle_mc_avg(void *dst, ptrdiff_t ds, const int16_t *t1, const int16_t *t2, int w, int h, int bpc) {
+    const Bd b = bd_of(bpc);
+    const int sh = b.ib + 1, r = (1 << b.ib) + b.bias * 2;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) stp(dst, ds, y, x, clip((t1[y * w + x] + t2[y * w + x] + r) >> sh, 0, b.bdmax), bpc);
+}
+void oracle_mc_w_avg(void *dst, ptrdiff_t ds, const int16_t *t1, const int16_t *t2, int w, int h, int weight, int bpc) {
+    const Bd b = bd_of(bpc);
+    const int sh = b.ib + 4, r = (8 << b.ib) + b.bias * 16;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++)
+            stp(dst, ds, y, x, clip((t1[y * w + x] * weight + t2[y * w + x] * (16 - weight) + r) >> sh, 0, b.bdmax), bpc);
+}
+void oracle_mc_mask(void *dst, ptrdiff_t ds, const int16_t *t1, const int16_t *t2, int w, int h,
+                    const uint8_t *mask, int bpc) {
+    const Bd b = bd_of(bpc);
+    const int sh = b.ib + 6, r = (32 << b.ib) + b.bias * 64;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const int m = mask[y * w + x];
+            stp(dst, ds, y, x, clip((t1[y * w + x] * m + t2[y * w + x] * (64 - m) + r) >> sh, 0, b.bdmax), bpc);
+        }
+}
+
+/* w_mask_c (mc_tmpl.c:661-712): blend with a difference-derived mask, store it at the
+ * chroma resolution given by (ss_hor, ss_ver) */
+void oracle_mc_w_mask(void *dst, ptrdiff_t ds, const int16_t *t1, const int16_t *t2, int w, int h,
+                      uint8_t *mask, int sign, int ss_hor, int ss_ver, int bpc) {
+    const Bd b = bd_of(bpc);
+    const int sh = b.ib + 6, r = (32 << b.ib) + b.bias * 64;
+    const int mask_sh = bpc + b.ib - 4, mask_rnd = 1 << (mask_sh - 5);
+    for (int y = 0, hh = h; y < h; y++, hh--) {
+        const int16_t *a = t1 + y * w, *c = t2 + y * w;
+        for (int x = 0; x < w; x++) {
+            int m = 38 + ((abs(a[x] - c[x]) + mask_rnd) >> mask_sh);
+            m = m < 64 ? m : 64;
+            stp(dst, ds, y, x, clip((a[x] * m + c[x] * (64 - m) + r) >> sh, 0, b.bdmax), bpc);
+            if (ss_hor) {
+                x++;
+                int n = 38 + ((abs(a[x] - c[x]) + mask_rnd) >> mask_sh);
+                n = n < 64 ? n : 64;
+                stp(dst, ds, y, x, clip((a[x] * n + c[x] * (64 - n) + r) >> sh, 0, b.bdmax), bpc);
+                if (hh & ss_ver) mask[x >> 1] = (uint8_t)((m + n + mask[x >> 1] + 2 - sign) >> 2);
+                else if (ss_ver) mask[x >> 1] = (uint8_t)(m + n);
+                else mask[x >> 1] = (uint8_t)((m + n + 1 - sign) >> 1);
+            } else {
+                mask[x] = (uint8_t)m;
+            }
+        }
+        if (!ss_ver || (hh & 1)) mask += w >> ss_hor;
+    }
+}
+
+/* blend_c / blend_v_c / blend_h_c (mc_tmpl.c:621-660) */
+#define BLEND_PX(a, b, m) ((((a) * (64 - (m)) + (b) * (m)) + 32) >> 6)
+void oracle_mc_blend(void *dst, ptrdiff_t ds, const void *tmp, int w, int h, const uint8_t *mask, int bpc) {
+    const int ts = w * (bpc == 8 ? 1 : 2);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++)
+            stp(dst, ds, y, x, BLEND_PX(ldp(dst, ds, y, x, bpc), ldp(tmp, ts, y, x, bpc), mask[y * w + x]), bpc);
+}
+void oracle_mc_blend_v(void *dst, ptrdiff_t ds, const void *tmp, int w, int h, int bpc) {
+    const int ts = w * (bpc == 8 ? 1 : 2);
+    const uint8_t *mask = &obmc_masks[w];
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < (w * 3) >> 2; x++)
+            stp(dst, ds, y, x, BLEND_PX(ldp(dst, ds, y, x, bpc), ldp(tmp, ts, y, x, bpc), mask[x]), bpc);
+}
+void oracle_mc_blend_h(void *dst, ptrdiff_t ds, const void *tmp, int w, int h, int bpc) {
+    const int ts = w * (bpc == 8 ? 1 : 2);
+    const uint8_t *mask = &obmc_masks[h];
+    for (int y = 0; y < (h * 3) >> 2; y++)
+        for (int x = 0; x < w; x++)
+            stp(dst, ds, y, x, BLEND_PX(ldp(dst, ds, y, x, bpc), ldp(tmp, ts, y, x, bpc), mask[y]), bpc);
+}
+
+/* warp_affine_8x8_c / _8x8t_c (mc_tmpl.c:714-796); tmp_stride in elements */
+void oracle_mc_warp8x8(int prep, void *dst, ptrdiff_t ds, int16_t *tmp, ptrdiff_t tmp_stride,
+                       const void *src, ptrdiff_t ss, const int16_t abcd[4], int mx, int my, int bpc) {
+    const Bd b = bd_of(bpc);
+    int16_t mid[15 * 8];
+    for (int y = 0; y < 15; y++, mx += abcd[1])
+        for (int x = 0, tmx = mx; x < 8; x++, tmx += abcd[0]) {
+            const int8_t *F = warp_filter[64 + ((tmx + 512) >> 10)];
+            mid[y * 8 + x] = (int16_t)rnd(tap8_px(src, ss, y - 3, x, 0, 1, F, bpc), 7 - b.ib);
+        }
+    for (int y = 0; y < 8; y++, my += abcd[3])
+        for (int x = 0, tmy = my; x < 8; x++, tmy += abcd[2]) {
+            const int8_t *F = warp_filter[64 + ((tmy + 512) >> 10)];
+            const int s = tap8_mid(mid, 8, y + 3, x, F);
+            if (prep) tmp[y * tmp_stride + x] = (int16_t)(rnd(s, 7) - b.bias);
+            else stp(dst, ds, y, x, clip(rnd(s, 7 + b.ib), 0, b.bdmax), bpc);
+        }
+}
+
+/* emu_edge_c (mc_tmpl.c:798-845) */
+void oracle_mc_emu_edge(int bw, int bh, int iw, int ih, int x, int y, void *dst, ptrdiff_t ds,
+                        const void *ref, ptrdiff_t rs, int bpc) {
+    const int pb = bpc == 8 ? 1 : 2;
+    const uint8_t *r = (const uint8_t *)ref + clip(y, 0, ih - 1) * rs + clip(x, 0, iw - 1) * pb;
+    const int left_ext = clip(-x, 0, bw - 1), right_ext = clip(x + bw - iw, 0, bw - 1);
+    const int top_ext = clip(-y, 0, bh - 1), bottom_ext = clip(y + bh - ih, 0, bh - 1);
+    const int center_w = bw - left_ext - right_ext, center_h = bh - top_ext - bottom_ext;
+    uint8_t *d = dst;
+    uint8_t *blk = d + top_ext * ds;
+    for (int yy = 0; yy < center_h; yy++) {
+        memcpy(blk + left_ext * pb, r, (size_t)center_w * pb);
+        for (int k = 0; k < left_ext; k++) stp(blk, 0, 0, k, ldp(blk, 0, 0, left_ext, bpc), bpc);
+        for (int k = 0; k < right_ext; k++)
+            stp(blk, 0, 0, left_ext + center_w + k, ldp(blk, 0, 0, left_ext + center_w - 1, bpc), bpc);
+        r += rs;
+        blk += ds;
+    }
+    blk = d + top_ext * ds;
+    for (int yy = 0; yy < top_ext; yy++) {
+        memcpy(d, blk, (size_t)bw * pb);
+        d += ds;
+    }
+    d += center_h * ds;
+    for (int yy = 0; yy < bottom_ext; yy++) {
+        memcpy(d, d - ds, (size_t)bw * pb);
+        d += ds;
+    }
+}
+
+/* resize_c (mc_tmpl.c:847-875) */
+void oracle_mc_resize(void *dst, ptrdiff_t ds, const void *src, ptrdiff_t ss, int dst_w, int h,
+                      int src_w, int dx, int mx0, int bpc) {
+    const int bdmax = (1 << bpc) - 1;
+    for (int y = 0; y < h; y++) {
+        int mx = mx0, src_x = -1;
+        for (int x = 0; x < dst_w; x++) {
+            const int8_t *F = resize_filter[mx >> 8];
+            int s = 0;
+            for (int k = 0; k < 8; k++) s += F[k] * ldp(src, ss, y, clip(src_x - 3 + k, 0, src_w - 1), bpc);
+            stp(dst, ds, y, x, clip((-s + 64) >> 7, 0, bdmax), bpc);
+            mx += dx;
+            src_x += mx >> 14;
+            mx &= 0x3fff;
+        }
+    }
+}
+
+/* ---- frame driver: recon mc() + compound dispatch over MiMcBlock descriptors ---- */
+
+typedef struct {
+    uint16_t x, y;
+    uint8_t w, h, plane, filter2d;
+    int16_t mvx[2], mvy[2];
+    int8_t ref[2];
+    uint8_t comp, param;     /* param: w_avg weight (bits 0-4), mask sign (bit 7) */
+    uint32_t mask_off;
+} McBlock;   /* == MiMcBlock (include/mi_av1dsp.h), 24 bytes */
+
+/* mc() (recon_tmpl.c:962-1011) for a same-size reference: emu_edge when the filter support
+ * leaves the picture, then put (dst) or prep (tmp). */
+static void mc_block(const McBlock *bk, int i, void *dst, ptrdiff_t ds, int16_t *tmp,
+                     const void *refp, ptrdiff_t rs, int rw, int rh, int ss_hor, int ss_ver, int bpc) {
+    const int mvx = bk->mvx[i], mvy = bk->mvy[i];
+    const int mx = mvx & (15 >> !ss_hor), my = mvy & (15 >> !ss_ver);
+    const int dx = bk->x + (mvx >> (3 + ss_hor)), dy = bk->y + (mvy >> (3 + ss_ver));
+    const int w = (rw + ss_hor) >> ss_hor, h = (rh + ss_ver) >> ss_ver;
+    const int pb = bpc == 8 ? 1 : 2;
+    const void *ref;
+    ptrdiff_t ref_stride = rs;
+    uint8_t *emu = NULL;
+    if (dx < !!mx * 3 || dy < !!my * 3 || dx + bk->w + !!mx * 4 > w || dy + bk->h + !!my * 4 > h) {
+        emu = malloc((size_t)192 * 192 * pb);
+        oracle_mc_emu_edge(bk->w + !!mx * 7, bk->h + !!my * 7, w, h, dx - !!mx * 3, dy - !!my * 3,
+                           emu, 192 * pb, refp, rs, bpc);
+        ref = emu + (192 * !!my * 3 + !!mx * 3) * pb;
+        ref_stride = 192 * pb;
+    } else {
+        ref = (const uint8_t *)refp + dy * rs + dx * pb;
+    }
+    if (tmp) oracle_mc_prep(bk->filter2d, tmp, ref, ref_stride, bk->w, bk->h, mx << !ss_hor, my << !ss_ver, bpc);
+    else oracle_mc_put(bk->filter2d, dst, ds, ref, ref_stride, bk->w, bk->h, mx << !ss_hor, my << !ss_ver, bpc);
+    free(emu);
+}
+
+void oracle_mc_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layout, int bpc,
+                     void *const *const refs, const ptrdiff_t *ref_strides, const int *ref_wh,
+                     const void *blocks, int n, uint8_t *masks) {
+    const McBlock *bl = blocks;
+    const int pb = bpc == 8 ? 1 : 2;
+    const int chr_ss_hor = layout == 1 || layout == 2, chr_ss_ver = layout == 1;
+    int16_t *t0 = malloc(sizeof(int16_t) * 128 * 128), *t1 = malloc(sizeof(int16_t) * 128 * 128);
+    for (int k = 0; k < n; k++) {
+        const McBlock *bk = &bl[k];
+        const int p = bk->plane;
+        const int ss_hor = p && layout != 3, ss_ver = p && layout == 1;
+        const ptrdiff_t ds = cur_stride[p ? 1 : 0];
+        uint8_t *dst = (uint8_t *)cur[p] + bk->y * ds + bk->x * pb;
+        int16_t *tmp[2] = { t0, t1 };
+        const int nref = bk->ref[1] >= 0 ? 2 : 1;
+        for (int i = 0; i < nref; i++) {
+            const int r = bk->ref[i];
+            mc_block(bk, i, dst, ds, nref == 2 ? tmp[i] : NULL, refs[r * 3 + p], ref_strides[r * 2 + (p ? 1 : 0)],
+                     ref_wh[r * 2], ref_wh[r * 2 + 1], ss_hor, ss_ver, bpc);
+        }
+        if (nref == 1) continue;
+        const int s = bk->param >> 7;
+        switch (bk->comp) {   /* recon_tmpl.c:1857-1921 */
+        case 0: oracle_mc_avg(dst, ds, t0, t1, bk->w, bk->h, bpc); break;
+        case 1: oracle_mc_w_avg(dst, ds, t0, t1, bk->w, bk->h, bk->param & 31, bpc); break;
+        case 2: oracle_mc_mask(dst, ds, tmp[s], tmp[!s], bk->w, bk->h, masks + bk->mask_off, bpc); break;
+        case 3: {
+            /* w_mask[chr_layout_idx]: I400/I444 -> 444, I422 -> 422, I420 -> 420 */
+            const int sh = layout == 0 ? 0 : chr_ss_hor, sv = layout == 0 ? 0 : chr_ss_ver;
+            oracle_mc_w_mask(dst, ds, tmp[s], tmp[!s], bk->w, bk->h, masks + bk->mask_off, s, sh, sv, bpc);
+            break;
+        }
+        }
+    }
+    free(t0);
+    free(t1);
+}

@@ -39,6 +39,37 @@ void oracle_itx_frame(void *const planes[3], const ptrdiff_t strides[3],
 /* 1-D transforms exposed for the numeric sanity tests (kind: 0 dct,1 adst,2 flipadst,3 identity,4 wht) */
 void oracle_itx_1d(int kind, int n, int32_t *c, ptrdiff_t stride, int min, int max);
 
+/* ---- mc (src/mc.rs; C twin src/mc_tmpl.c), pixels u8/u16 by bpc, strides in bytes ---- */
+/* filter2d: levels.rs Filter2d (0..8 8-tap combos, 9 bilinear); mx/my in 1/16 pel */
+void oracle_mc_put(int filter2d, void *dst, ptrdiff_t dst_stride, const void *src, ptrdiff_t src_stride,
+                   int w, int h, int mx, int my, int bpc);
+void oracle_mc_prep(int filter2d, int16_t *tmp, const void *src, ptrdiff_t src_stride,
+                    int w, int h, int mx, int my, int bpc);
+void oracle_mc_scaled(int filter2d, int prep, void *dst, ptrdiff_t dst_stride, int16_t *tmp,
+                      const void *src, ptrdiff_t src_stride, int w, int h, int mx, int my,
+                      int dx, int dy, int bpc);
+void oracle_mc_avg(void *dst, ptrdiff_t ds, const int16_t *t1, const int16_t *t2, int w, int h, int bpc);
+void oracle_mc_w_avg(void *dst, ptrdiff_t ds, const int16_t *t1, const int16_t *t2, int w, int h,
+                     int weight, int bpc);
+void oracle_mc_mask(void *dst, ptrdiff_t ds, const int16_t *t1, const int16_t *t2, int w, int h,
+                    const uint8_t *mask, int bpc);
+void oracle_mc_w_mask(void *dst, ptrdiff_t ds, const int16_t *t1, const int16_t *t2, int w, int h,
+                      uint8_t *mask, int sign, int ss_hor, int ss_ver, int bpc);
+void oracle_mc_blend(void *dst, ptrdiff_t ds, const void *tmp, int w, int h, const uint8_t *mask, int bpc);
+void oracle_mc_blend_v(void *dst, ptrdiff_t ds, const void *tmp, int w, int h, int bpc);
+void oracle_mc_blend_h(void *dst, ptrdiff_t ds, const void *tmp, int w, int h, int bpc);
+void oracle_mc_warp8x8(int prep, void *dst, ptrdiff_t ds, int16_t *tmp, ptrdiff_t tmp_stride,
+                       const void *src, ptrdiff_t ss, const int16_t abcd[4], int mx, int my, int bpc);
+void oracle_mc_emu_edge(int bw, int bh, int iw, int ih, int x, int y, void *dst, ptrdiff_t ds,
+                        const void *ref, ptrdiff_t rs, int bpc);
+void oracle_mc_resize(void *dst, ptrdiff_t ds, const void *src, ptrdiff_t ss, int dst_w, int h,
+                      int src_w, int dx, int mx0, int bpc);
+/* Frame driver: recon mc() + compound dispatch (recon_tmpl.c:962-1011, 1836-1921) over
+ * MiMcBlock records; refs[r*3+p] plane pointers, ref_strides[r*2+{0,1}], ref_wh[r*2+{0,1}]. */
+void oracle_mc_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layout, int bpc,
+                     void *const *const refs, const ptrdiff_t *ref_strides, const int *ref_wh,
+                     const void *blocks, int n, uint8_t *masks);
+
 #ifdef __cplusplus
 }
 #endif

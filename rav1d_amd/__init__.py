@@ -62,6 +62,12 @@ TXBLOCK_DTYPE = np.dtype([("coef_off", "<u4"), ("x", "<u2"), ("y", "<u2"), ("pla
                           ("tx", "u1"), ("txtp", "u1"), ("flags", "u1"), ("eob", "<i4")])
 assert TXBLOCK_DTYPE.itemsize == 16
 
+MCBLOCK_DTYPE = np.dtype([("x", "<u2"), ("y", "<u2"), ("w", "u1"), ("h", "u1"), ("plane", "u1"),
+                          ("filter2d", "u1"), ("mvx", "<i2", 2), ("mvy", "<i2", 2), ("ref", "i1", 2),
+                          ("comp", "u1"), ("param", "u1"), ("mask_off", "<u4")])
+assert MCBLOCK_DTYPE.itemsize == 24
+MC_AVG, MC_WAVG, MC_MASK, MC_SEG = 0, 1, 2, 3
+
 N_RECT_TX_SIZES = 19
 ITX_KEEP_COEFS = 1
 
@@ -91,6 +97,8 @@ def lib():
          [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.POINTER(ctypes.c_uint32), _VP, ctypes.c_uint, _VP])
     _sig(L, "mi_dsp_itxfm_add", ctypes.c_int,
          [ctypes.c_int, ctypes.c_int, _VP, ctypes.c_ssize_t, _VP, ctypes.c_int, ctypes.c_int])
+    _sig(L, "mi_mc_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture), ctypes.c_int,
+                                          _VP, ctypes.POINTER(ctypes.c_uint32), _VP, _VP])
     _sig(L, "mi_deblock_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiLoopFilter), _VP])
     _sig(L, "mi_cdef_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
                                             ctypes.POINTER(MiCdef), _VP])
@@ -106,7 +114,7 @@ def lib():
 
 # Every symbol include/mi_av1dsp.h declares (checked by tests/test_abi.py).
 EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
-            "mi_itx_frame", "mi_deblock_frame", "mi_cdef_frame", "mi_lr_frame",
+            "mi_itx_frame", "mi_mc_frame", "mi_deblock_frame", "mi_cdef_frame", "mi_lr_frame",
             "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply",
             "mi_dsp_itxfm_add"]
 

@@ -113,6 +113,50 @@ int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
     return r ? fail(ctx, -EIO) : 0;
 }
 
+int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
+                const MiMcBlock *blocks, const uint32_t plane_start[4], uint8_t *masks,
+                void *stream) {
+    if (!ctx || !cur || !plane_start) return fail(ctx, -EINVAL);
+    if (cur->bpc != 8 && cur->bpc != 10 && cur->bpc != 12) return fail(ctx, -EINVAL);
+    if (nrefs < 0 || nrefs > 7 || (nrefs && !refs)) return fail(ctx, -EINVAL);
+    if (plane_start[0] > plane_start[1] || plane_start[1] > plane_start[2] || plane_start[2] > plane_start[3])
+        return fail(ctx, -EINVAL);
+    if (plane_start[3] == plane_start[0]) return 0;
+    if (!blocks || !nrefs) return fail(ctx, -EINVAL);
+    mi::McArgs a;
+    memset(&a, 0, sizeof(a));
+    const int ss_hor = cur->layout == 1 || cur->layout == 2, ss_ver = cur->layout == 1;
+    for (int p = 0; p < 3; p++) a.dst[p] = (uint8_t *)cur->data[p];
+    a.dst_stride[0] = cur->stride[0];
+    a.dst_stride[1] = cur->stride[1];
+    for (int r = 0; r < nrefs; r++) {
+        // scaled references take the mc_scaled path of the reference: not batched here
+        if (!same_geometry(cur, &refs[r])) return fail(ctx, -EINVAL);
+        for (int p = 0; p < 3; p++) {
+            const int sh = p ? ss_hor : 0, sv = p ? ss_ver : 0;
+            a.ref[r][p] = (const uint8_t *)refs[r].data[p];
+            a.ref_w[r][p] = (refs[r].w + sh) >> sh;
+            a.ref_h[r][p] = (refs[r].h + sv) >> sv;
+        }
+        a.ref_stride[r][0] = refs[r].stride[0];
+        a.ref_stride[r][1] = refs[r].stride[1];
+    }
+    a.blocks = blocks;
+    a.masks = masks;
+    a.bpc = cur->bpc;
+    a.ib = cur->bpc == 8 ? 4 : 14 - cur->bpc;
+    a.bias = cur->bpc == 8 ? 0 : 8192;
+    a.bdmax = (1 << cur->bpc) - 1;
+    a.layout = cur->layout;
+    a.seg_ss_hor = cur->layout ? ss_hor : 0;   // w_mask[chr_layout_idx] (recon_tmpl.c:1868)
+    a.seg_ss_ver = cur->layout ? ss_ver : 0;
+    hipStream_t s = (hipStream_t)stream;
+    // luma first: chroma units of SEG blocks read the mask their luma unit writes
+    int r = mi::launch_mc(a, (int)plane_start[0], (int)(plane_start[1] - plane_start[0]), s);
+    if (!r) r = mi::launch_mc(a, (int)plane_start[1], (int)(plane_start[3] - plane_start[1]), s);
+    return r ? fail(ctx, -EIO) : 0;
+}
+
 int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, void *stream) {
     if (!ctx || !pic || !lf) return fail(ctx, -EINVAL);
     if (pic->bpc != 8 && pic->bpc != 10 && pic->bpc != 12) return fail(ctx, -EINVAL);

@@ -92,6 +92,20 @@ struct CdefArgs {
 // launchers (cdef.hip)
 int launch_cdef(const CdefArgs &a, int tiles, int bpc, hipStream_t s);
 
+struct McArgs {
+    uint8_t *dst[3];
+    int64_t dst_stride[2];
+    const uint8_t *ref[7][3];
+    int64_t ref_stride[7][2];
+    int ref_w[7][3], ref_h[7][3];    // plane dimensions (clamp bounds)
+    const MiMcBlock *blocks;
+    uint8_t *masks;
+    int bpc, ib, bias, bdmax, layout;
+    int seg_ss_hor, seg_ss_ver;      // w_mask[chr_layout_idx] subsampling of the SEG mask
+};
+// launchers (mc.hip)
+int launch_mc(const McArgs &a, int first, int count, hipStream_t s);
+
 struct LrArgs {
     const uint8_t *src[3];        // CDEF output C
     const uint8_t *lpf[3];        // deblocked D (rows across stripe edges)

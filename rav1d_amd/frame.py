@@ -62,6 +62,15 @@ class Frame:
         return pic
 
     # numpy views (copies across the device boundary)
+    def buffer_np(self, p):
+        """The whole allocated plane (aligned rows x stride) as pixels."""
+        b = self.planes[p].cpu().numpy()
+        return b.view("<u2").copy() if self.pxb == 2 else b.copy()
+
+    def set_buffer_np(self, p, arr):
+        a = np.ascontiguousarray(arr, dtype=np.uint16 if self.pxb == 2 else np.uint8)
+        self.planes[p].copy_(torch.from_numpy(a.view(np.uint8).reshape(self.planes[p].shape)))
+
     def plane_np(self, p):
         b = self.planes[p].cpu().numpy()
         w, h = self.dims(p)
@@ -121,6 +130,25 @@ def itx_frame(ctx, frame, blocks_dev, size_start, coef_dev, flags=0, stream=None
     rc = lib().mi_itx_frame(ctx.h, ctypes.byref(pic), ctypes.c_void_p(blocks_dev.data_ptr()), ss,
                             ctypes.c_void_p(coef_dev.data_ptr()), flags, _stream_ptr(stream))
     check(rc, "mi_itx_frame")
+
+
+class McMeta:
+    """Device copies of a frame's MC units (MiMcBlock, luma first) and mask buffer."""
+
+    def __init__(self, units, plane_start, masks):
+        self.n = len(units)
+        self.blocks = torch.from_numpy(np.ascontiguousarray(units).view(np.uint8).copy()).cuda()
+        self.masks = torch.from_numpy(np.ascontiguousarray(masks).copy()).cuda()
+        self.plane_start = (ctypes.c_uint32 * 4)(*[int(v) for v in plane_start])
+
+
+def mc_frame(ctx, cur, refs, meta, stream=None):
+    """mi_mc_frame: inter prediction of every unit into `cur` from the reference Frames."""
+    pics = (MiPicture * len(refs))(*[r.picture() for r in refs])
+    rc = lib().mi_mc_frame(ctx.h, ctypes.byref(cur.picture()), pics, len(refs),
+                           ctypes.c_void_p(meta.blocks.data_ptr()), meta.plane_start,
+                           ctypes.c_void_p(meta.masks.data_ptr()), _stream_ptr(stream))
+    check(rc, "mi_mc_frame")
 
 
 class LoopFilterMeta:

@@ -9,7 +9,7 @@ function of (geometry, seed), so the same inputs regenerate bit-identically anyw
 """
 import numpy as np
 
-from . import TXBLOCK_DTYPE, N_RECT_TX_SIZES
+from . import MCBLOCK_DTYPE, TXBLOCK_DTYPE, N_RECT_TX_SIZES
 
 # RectTxfmSize (rav1d src/levels.rs:46-82): (w, h)
 TX_DIMS = [(4, 4), (8, 8), (16, 16), (32, 32), (64, 64), (4, 8), (8, 4), (8, 16), (16, 8),
@@ -447,3 +447,122 @@ def frame_bytes(w, h, bpc, layout=1):
     ss_v = 1 if layout == 1 else 0
     c = ((w + ss_h) >> ss_h) * ((h + ss_v) >> ss_v) if layout else 0
     return (w * h + 2 * c) * pxb
+
+
+# ---- motion compensation -------------------------------------
+
+def partition_blocks(w, h, rng, sb=64, min_bs=8, p_split=0.55):
+    """Quadtree partition of the frame into AV1-shaped inter blocks (square, 2:1 / 1:2 and
+    4:1 / 1:4 as the PARTITION_H/V/H4/V4 shapes give), (x, y, bw, bh) luma pixels. Only
+    blocks whose top-left lies inside the frame are emitted (as the reference decodes)."""
+    out = []
+
+    def rec(x, y, s):
+        if x >= w or y >= h:
+            return
+        if s > min_bs and rng.random() < p_split:
+            for dy in (0, s // 2):
+                for dx in (0, s // 2):
+                    rec(x + dx, y + dy, s // 2)
+            return
+        r = rng.random()
+        if r < 0.6 or s < 16:
+            out.append((x, y, s, s))
+        elif r < 0.75:
+            out.extend([(x, y, s, s // 2), (x, y + s // 2, s, s // 2)])
+        elif r < 0.9:
+            out.extend([(x, y, s // 2, s), (x + s // 2, y, s // 2, s)])
+        elif r < 0.95 and s >= 32:
+            out.extend([(x, y + k * s // 4, s, s // 4) for k in range(4)])
+        elif s >= 32:
+            out.extend([(x + k * s // 4, y, s // 4, s) for k in range(4)])
+        else:
+            out.append((x, y, s, s))
+
+    for y in range(0, h, sb):
+        for x in range(0, w, sb):
+            rec(x, y, sb)
+    return [b for b in out if b[0] < w and b[1] < h]
+
+
+def _mc_record(x, y, bw, bh, plane, f2d, mvs, refs, comp, param, mask_off):
+    return (x, y, bw, bh, plane, f2d, (mvs[0][0], mvs[1][0]), (mvs[0][1], mvs[1][1]), refs, comp, param, mask_off)
+
+
+def make_mc_units(w, h, layout, rng, nrefs=2, compound_frac=0.3, mv_px=64, sb=64, min_bs=8, blocks=None):
+    """Inter prediction units for one frame: every block predicted from one reference (put)
+    or two (compound: avg / w_avg / mask / seg, uniformly), filters uniform over the nine
+    8-tap pairs and bilinear, MVs uniform in +-mv_px at 1/8 pel. Returns (units sorted luma
+    first, plane_start[4], mask buffer)."""
+    ss_h = 1 if layout in (1, 2) else 0
+    ss_v = 1 if layout == 1 else 0
+    seg_h, seg_v = (ss_h, ss_v) if layout else (0, 0)
+    if blocks is None:
+        blocks = partition_blocks(w, h, rng, sb=sb, min_bs=min_bs)
+    luma, chroma, masks, moff = [], [], [], 0
+    for (x, y, bw, bh) in blocks:
+        f2d = int(rng.integers(0, 10))
+        mvs = [(int(rng.integers(-8 * mv_px, 8 * mv_px + 1)), int(rng.integers(-8 * mv_px, 8 * mv_px + 1)))
+               for _ in range(2)]
+        cmp_ = nrefs > 1 and rng.random() < compound_frac
+        if cmp_:
+            r = rng.choice(nrefs, 2, replace=False)
+            refs = (int(r[0]), int(r[1]))
+            comp = int(rng.integers(0, 4))
+            param = int(rng.integers(1, 16)) if comp == 1 else (int(rng.integers(0, 2)) << 7)
+        else:
+            refs, comp, param = (int(rng.integers(0, nrefs)), -1), 0, 0
+        loff = 0
+        if cmp_ and comp == 2:
+            masks.append(rng.integers(0, 65, size=bw * bh).astype(np.uint8))
+            loff, moff = moff, moff + bw * bh
+        elif cmp_ and comp == 3:
+            n = (bw >> seg_h) * (bh >> seg_v)
+            masks.append(np.zeros(n, np.uint8))
+            loff, moff = moff, moff + n
+        luma.append(_mc_record(x, y, bw, bh, 0, f2d, mvs, refs, comp, param, loff))
+        if layout:
+            cw, ch = bw >> ss_h, bh >> ss_v
+            ccomp, coff = comp, loff
+            if cmp_ and comp == 2:          # chroma wedge: its own mask at chroma resolution
+                masks.append(rng.integers(0, 65, size=cw * ch).astype(np.uint8))
+                coff, moff = moff, moff + cw * ch
+            elif cmp_ and comp == 3:        # chroma of SEG: mask() with the luma-written mask
+                ccomp = 2
+            for pl in (1, 2):
+                chroma.append(_mc_record(x >> ss_h, y >> ss_v, cw, ch, pl, f2d, mvs, refs, ccomp, param, coff))
+    units = np.array(luma + chroma, dtype=MCBLOCK_DTYPE)
+    plane_start = np.array([0, len(luma), len(luma) + len(chroma) // 2 if layout else len(luma),
+                            len(luma) + len(chroma)], np.uint32)
+    mask_buf = np.concatenate(masks) if masks else np.zeros(1, np.uint8)
+    if mask_buf.size == 0:
+        mask_buf = np.zeros(1, np.uint8)
+    return units, plane_start, mask_buf
+
+
+def make_mc_grid_units(pw, ph, uw, uh, plane, rng, nrefs=2, compound_frac=0.5, mv_px=24):
+    """A plane tiled with uw x uh units (any size 2..128, including the 4-tap w/h <= 4 cases),
+    for kernel-shape coverage. Compound only where uw, uh >= 8 (as AV1); no SEG/MASK here."""
+    recs = []
+    for y in range(0, ph, uh):
+        for x in range(0, pw, uw):
+            f2d = int(rng.integers(0, 10))
+            mvs = [(int(rng.integers(-8 * mv_px, 8 * mv_px + 1)), int(rng.integers(-8 * mv_px, 8 * mv_px + 1)))
+                   for _ in range(2)]
+            if uw >= 8 and uh >= 8 and rng.random() < compound_frac:
+                r = rng.choice(nrefs, 2, replace=False)
+                comp = int(rng.integers(0, 2))
+                recs.append(_mc_record(x, y, uw, uh, plane, f2d, mvs, (int(r[0]), int(r[1])), comp,
+                                       int(rng.integers(1, 16)) if comp else 0, 0))
+            else:
+                recs.append(_mc_record(x, y, uw, uh, plane, f2d, mvs, (int(rng.integers(0, nrefs)), -1), 0, 0, 0))
+    return np.array(recs, dtype=MCBLOCK_DTYPE)
+
+
+def mc_algorithmic_bytes(units, bpc):
+    """per unit, pixB * [sum over refs (w+7)(h+7) + w*h] (+ mask bytes)."""
+    pxb = 1 if bpc == 8 else 2
+    w = units["w"].astype(np.int64)
+    h = units["h"].astype(np.int64)
+    nref = 1 + (units["ref"][:, 1] >= 0)
+    return int((pxb * (nref * (w + 7) * (h + 7) + w * h)).sum())

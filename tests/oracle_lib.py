@@ -147,3 +147,42 @@ def fg_grain_y(fg, bpc):
     d = film_grain_data(fg)
     o.oracle_fg_generate_grain_y(ptr(buf), ctypes.byref(d), (1 << bpc) - 1)
     return buf
+
+
+def _mc_sigs(o):
+    if getattr(o, "_mc_ready", False):
+        return
+    o.oracle_mc_frame.argtypes = [_VP, _VP, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP, _VP, ctypes.c_int, _VP]
+    o.oracle_mc_frame.restype = None
+    o.oracle_mc_put.argtypes = [ctypes.c_int, _VP, ctypes.c_ssize_t, _VP, ctypes.c_ssize_t] + [ctypes.c_int] * 5
+    o.oracle_mc_prep.argtypes = [ctypes.c_int, _VP, _VP, ctypes.c_ssize_t] + [ctypes.c_int] * 5
+    o.oracle_mc_emu_edge.argtypes = [ctypes.c_int] * 6 + [_VP, ctypes.c_ssize_t, _VP, ctypes.c_ssize_t, ctypes.c_int]
+    o.oracle_mc_avg.argtypes = [_VP, ctypes.c_ssize_t, _VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    o.oracle_mc_w_mask.argtypes = [_VP, ctypes.c_ssize_t, _VP, _VP] + [ctypes.c_int] * 2 + [_VP] + [ctypes.c_int] * 4
+    for n in ("oracle_mc_put", "oracle_mc_prep", "oracle_mc_emu_edge", "oracle_mc_avg", "oracle_mc_w_mask"):
+        getattr(o, n).restype = None
+    o._mc_ready = True
+
+
+def mc_frame(cur_planes, ref_frames, bpc, layout, w, h, units, masks):
+    """Oracle frame MC. cur_planes: padded planes (modified copies returned); ref_frames: list
+    of padded plane lists; units: MCBLOCK_DTYPE array (luma first); masks: uint8 buffer."""
+    o = load_oracle()
+    _mc_sigs(o)
+    cur = [np.ascontiguousarray(p).copy() for p in cur_planes]
+    while len(cur) < 3:
+        cur.append(cur[0])
+    refs = [[np.ascontiguousarray(p) for p in f] for f in ref_frames]
+    for f in refs:
+        while len(f) < 3:
+            f.append(f[0])
+    cp = (ctypes.c_void_p * 3)(*[a.ctypes.data for a in cur])
+    cs = (ctypes.c_ssize_t * 2)(cur[0].strides[0], cur[1].strides[0])
+    rp = (ctypes.c_void_p * (3 * len(refs)))(*[a.ctypes.data for f in refs for a in f])
+    rs = (ctypes.c_ssize_t * (2 * len(refs)))(*[s for f in refs for s in (f[0].strides[0], f[1].strides[0])])
+    rwh = (ctypes.c_int * (2 * len(refs)))(*[v for _ in refs for v in (w, h)])
+    u = np.ascontiguousarray(units)
+    m = np.ascontiguousarray(masks).copy()
+    o.oracle_mc_frame(cp, cs, layout, bpc, rp, rs, rwh, ptr(u), len(u), ptr(m))
+    n = 3 if layout else 1
+    return cur[:n], m
