@@ -1,10 +1,12 @@
-"""Benchmark: decoded Mpixels/s of the post-entropy AV1 reconstruction DSP path, 4K 10-bit 4:2:0.
+"""Benchmark: decoded Mpixels/s of the post-entropy AV1 reconstruction DSP path,
+4K 10-bit 4:2:0 inter frames (BASELINE.json configs[2]: mc + loopfilter + cdef + looprestoration).
 
-One step = one frame through every implemented GPU stage, inputs resident in HBM:
-  itx (inverse transform + add into the prediction) -> deblock (all column edges, then all
-  row edges) -> CDEF (D -> C) -> loop restoration (C + D -> O) -> film grain (O -> output).
-Motion compensation and intra prediction are not implemented yet: the
-prediction planes are synthetic and resident. Descriptors follow SURVEY.md §8(d).
+One step = one frame through every GPU stage, inputs resident in HBM:
+  MC (inter prediction of every block from 2 resident reference pictures) -> itx (residual
+  add) -> deblock (all column edges, then all row edges) -> CDEF (D -> C) -> loop restoration
+  (C + D -> O, the reference picture). Descriptors follow SURVEY.md §8(d) config 3.
+Film grain (output-only, configs[3] = 8K10) is timed separately on an 8K10 frame and
+reported under "film_grain_8k10"; it is not part of the headline step.
 
 `python bench.py` runs 1 GPU. Under torch.distributed.run every rank drives its own GPU on
 its own independent stream (replicas; no data-path collective; "scaling": "weak"); the
@@ -27,7 +29,7 @@ sys.path.insert(0, ROOT)
 
 from rav1d_amd import ITX_KEEP_COEFS  # noqa: E402
 from rav1d_amd import frame as F  # noqa: E402
-from rav1d_amd.synth import frame_bytes, itx_algorithmic_bytes, make_frame  # noqa: E402
+from rav1d_amd.synth import frame_bytes, itx_algorithmic_bytes, make_frame, mc_algorithmic_bytes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 W, H, BPC, LAYOUT = 3840, 2160, 10, 1
@@ -42,15 +44,24 @@ class Pipeline:
         self.A = F.Frame(w, h, bpc, lay)      # prediction -> recon -> deblocked (in place)
         self.B = F.Frame(w, h, bpc, lay)      # CDEF output
         self.O = F.Frame(w, h, bpc, lay)      # LR output (the reference frame)
-        self.G = F.Frame(w, h, bpc, lay)      # displayed picture with film grain
+        self.G = F.Frame(w, h, bpc, lay) if fr["fg"] else None   # displayed picture with film grain
         for p, a in enumerate(fr["planes"]):
             self.A.set_plane_np(p, a)
+        self.refs, self.mc = [], None
+        if fr.get("mc") is not None:
+            for planes in fr["refs"]:
+                r = F.Frame(w, h, bpc, lay)
+                for p, a in enumerate(planes):
+                    r.set_plane_np(p, a)
+                self.refs.append(r)
+            self.mc = F.McMeta(*fr["mc"])
+            self.ref_pics = (F.MiPicture * len(self.refs))(*[r.picture() for r in self.refs])
         self.blocks = torch.from_numpy(fr["blocks"].view(np.uint8).copy()).cuda()
         self.coef = torch.from_numpy(fr["coef"].copy()).cuda()
         self.lf = F.LoopFilterMeta(fr["lf"])
         self.cdef = F.CdefMeta(fr["lf"]["masks"], fr["cdef"], masks_dev=self.lf.masks)
         self.lr = F.LrMeta(fr["lr"])
-        self.fgd = F.film_grain_data(fr["fg"])
+        self.fgd = F.film_grain_data(fr["fg"]) if fr["fg"] else None
         self.side = torch.cuda.Stream()
         fb = frame_bytes(w, h, bpc, lay)
         # algorithmic bytes per launch: read inputs once, write outputs once
@@ -63,7 +74,9 @@ class Pipeline:
             "lr": 2 * fb + fb * 4 // 64 + fr["lr"]["lr_mask"].nbytes,
             "fg": 2 * fb,
         }
-        self.kernels = {"itx": "itx_frame_kernel", "deblock": "lf_cols_kernel+lf_rows_kernel",
+        if self.mc is not None:
+            self.algo["mc"] = mc_algorithmic_bytes(fr["mc"][0], bpc) + fr["mc"][2].nbytes
+        self.kernels = {"mc": "mc_kernel", "itx": "itx_frame_kernel", "deblock": "lf_cols_kernel+lf_rows_kernel",
                         "cdef": "cdef_kernel", "lr": "lr_kernel", "fg": "fg_apply_kernel"}
 
     def step(self, stream, ev=None):
@@ -71,16 +84,18 @@ class Pipeline:
         lib = F.lib()
         ctx = self.ctx.h
         sp = F._stream_ptr(stream)
-        pa, pb, po, pg = self.A.picture(), self.B.picture(), self.O.picture(), self.G.picture()
+        pa, pb, po = self.A.picture(), self.B.picture(), self.O.picture()
 
-        # film-grain prep depends only on the grain parameters: side stream, overlapped
-        start = torch.cuda.Event()
-        start.record(stream)
-        self.side.wait_event(start)
-        F.check(lib.mi_film_grain_prep(ctx, ctypes.byref(pa), ctypes.byref(self.fgd),
-                                       F._stream_ptr(self.side)), "fg prep")
-        prep_done = torch.cuda.Event()
-        prep_done.record(self.side)
+        prep_done = None
+        if self.fgd is not None:
+            # film-grain prep depends only on the grain parameters: side stream, overlapped
+            start = torch.cuda.Event()
+            start.record(stream)
+            self.side.wait_event(start)
+            F.check(lib.mi_film_grain_prep(ctx, ctypes.byref(pa), ctypes.byref(self.fgd),
+                                           F._stream_ptr(self.side)), "fg prep")
+            prep_done = torch.cuda.Event()
+            prep_done.record(self.side)
 
         def timed(name, fn):
             if ev is not None:
@@ -92,6 +107,10 @@ class Pipeline:
             else:
                 fn()
 
+        if self.mc is not None:
+            timed("mc", lambda: F.check(lib.mi_mc_frame(ctx, ctypes.byref(pa), self.ref_pics, len(self.refs),
+                                                        ctypes.c_void_p(self.mc.blocks.data_ptr()), self.mc.plane_start,
+                                                        ctypes.c_void_p(self.mc.masks.data_ptr()), sp), "mc"))
         ss = (ctypes.c_uint32 * 20)(*[int(v) for v in self.fr["size_start"]])
         timed("itx", lambda: F.check(lib.mi_itx_frame(ctx, ctypes.byref(pa), ctypes.c_void_p(self.blocks.data_ptr()),
                                                       ss, ctypes.c_void_p(self.coef.data_ptr()), ITX_KEEP_COEFS, sp), "itx"))
@@ -100,14 +119,52 @@ class Pipeline:
                                                         ctypes.byref(self.cdef.s), sp), "cdef"))
         timed("lr", lambda: F.check(lib.mi_lr_frame(ctx, ctypes.byref(pb), ctypes.byref(pa), ctypes.byref(po),
                                                     ctypes.byref(self.lr.s), sp), "lr"))
-        stream.wait_event(prep_done)
-        timed("fg", lambda: F.check(lib.mi_film_grain_apply(ctx, ctypes.byref(po), ctypes.byref(pg),
-                                                            ctypes.byref(self.fgd), 0, sp), "fg"))
+        if self.fgd is not None:
+            pg = self.G.picture()
+            stream.wait_event(prep_done)
+            timed("fg", lambda: F.check(lib.mi_film_grain_apply(ctx, ctypes.byref(po), ctypes.byref(pg),
+                                                                ctypes.byref(self.fgd), 0, sp), "fg"))
+
+
+def film_grain_8k(ctx, stream, reps=20):
+    """configs[3]: film grain on an 8K10 frame (prep + apply), HBM-bound stress. Returns
+    (Mpixels/s of apply, apply ms, prep ms, apply GB/s algorithmic)."""
+    from rav1d_amd.synth import make_fg_params, make_texture
+    w, h, bpc = 7680, 4320, 10
+    rng = np.random.default_rng(0xF6000001)
+    src, dst = F.Frame(w, h, bpc, 1), F.Frame(w, h, bpc, 1)
+    for p in range(3):
+        pw, ph = src.dims(p)
+        src.set_plane_np(p, make_texture(rng, pw, ph, bpc))
+    fg = make_fg_params(rng, 1)
+    fg["overlap_flag"] = 1
+    d = F.film_grain_data(fg)
+    lib = F.lib()
+    ps, pd = src.picture(), dst.picture()
+    sp = F._stream_ptr(stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    for _ in range(3):
+        F.check(lib.mi_film_grain_frame(ctx.h, ctypes.byref(ps), ctypes.byref(pd), ctypes.byref(d), 0, sp), "fg")
+    torch.cuda.synchronize()
+    prep_t, apply_t = 0.0, 0.0
+    for _ in range(reps):
+        ev[0].record(stream)
+        F.check(lib.mi_film_grain_prep(ctx.h, ctypes.byref(ps), ctypes.byref(d), sp), "fg prep")
+        ev[1].record(stream)
+        F.check(lib.mi_film_grain_apply(ctx.h, ctypes.byref(ps), ctypes.byref(pd), ctypes.byref(d), 0, sp), "fg apply")
+        ev[2].record(stream)
+        torch.cuda.synchronize()
+        prep_t += ev[0].elapsed_time(ev[1])
+        apply_t += ev[1].elapsed_time(ev[2])
+    apply_ms, prep_ms = apply_t / reps, prep_t / reps
+    fb = frame_bytes(w, h, bpc, 1)
+    return dict(mpx_per_s=round(w * h / (apply_ms / 1e3) / 1e6, 1), apply_ms=round(apply_ms, 4),
+                prep_ms=round(prep_ms, 4), apply_gbs=round(2 * fb / (apply_ms / 1e3) / 1e9, 1))
 
 
 def cpu_baseline(fr, budget_s=20.0):
     """The oracle (single-threaded C restatement, oracle/) on a bounded sample of the same
-    workload: whole 4K10 frames through all stages until ~budget_s. Luma Mpixels/s."""
+    workload: whole 4K10 inter frames through all stages until ~budget_s. Luma Mpixels/s."""
     from tests.pipeline import oracle_pipeline
     n, t0 = 0, time.perf_counter()
     while True:
@@ -117,8 +174,8 @@ def cpu_baseline(fr, budget_s=20.0):
         if el > budget_s or n >= 20:
             break
     return dict(value=round(n * fr["w"] * fr["h"] / el / 1e6, 3), unit="Mpixels/s", cores=1, kind="port",
-                sample=f"{n} frame(s) of the same synthetic 4K10 descriptors through oracle/ "
-                       f"(itx+deblock+cdef+lr+film grain), 1 thread, {el:.1f}s")
+                sample=f"{n} frame(s) of the same synthetic 4K10 inter descriptors through oracle/ "
+                       f"(mc+itx+deblock+cdef+lr), 1 thread, {el:.1f}s")
 
 
 def main():
@@ -127,6 +184,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fg", action="store_true", help="skip the separate 8K10 film-grain measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -137,7 +195,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     stream = torch.cuda.current_stream()
 
-    fr = make_frame(W, H, BPC, LAYOUT, seed=0x4C100001 + rank)
+    fr = make_frame(W, H, BPC, LAYOUT, seed=0x4C100001 + rank, with_fg=False, with_mc=True)
     ctx = F.Context(local)
     pipe = Pipeline(ctx, fr)
     torch.cuda.synchronize()
@@ -186,9 +244,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u16",
-            "data": "synthetic (seeded frame descriptors per SURVEY.md §8d; no CPU front-end yet)",
-            "config": {"workload": f"4K10 4:2:0 {W}x{H} frame: itx+deblock+cdef+lr+film_grain "
-                                   f"(mc/ipred not yet implemented; prediction planes resident)",
+            "data": "synthetic (seeded inter-frame descriptors per SURVEY.md §8d config 3; no CPU front-end yet)",
+            "config": {"workload": f"4K10 4:2:0 {W}x{H} inter frame: mc (2 refs, 30% compound) + itx residual "
+                                   f"+ deblock + cdef + lr",
                        "parallelism": f"replicas{world} (one independent stream per GPU)"},
             "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
             "stage_gbs": {k: round(pipe.algo[k] / (stage_ms[k] / 1e3) / 1e9, 1) for k in stage_ms if k in pipe.algo},
@@ -197,6 +255,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                          "algo_bytes_per_launch": pipe.algo[dom]},
         }
+        if world == 1 and not args.no_fg:
+            out["film_grain_8k10"] = film_grain_8k(ctx, stream)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(fr)
         print(json.dumps(out))

@@ -421,10 +421,12 @@ def itx_blocks_from_tilings(tilings, bpc, rng, dc_frac=0.6, full_frac=0.1):
     return blocks, size_start, coef
 
 
-def make_frame(w, h, bpc=10, layout=1, seed=0x4C100001, sb128=1, with_fg=True):
+def make_frame(w, h, bpc=10, layout=1, seed=0x4C100001, sb128=1, with_fg=True, with_mc=False, nrefs=2):
     """One synthetic frame's worth of post-entropy descriptors for every implemented stage,
     all derived from one transform tiling: prediction planes, itx blocks + coefficient arena,
-    deblock masks/levels, CDEF indices/strengths, LR units, film-grain parameters."""
+    deblock masks/levels, CDEF indices/strengths, LR units, film-grain parameters.
+    with_mc: an inter frame — `nrefs` textured reference
+    pictures and MC units whose prediction replaces the resident prediction planes."""
     rng = np.random.default_rng(seed)
     til = make_tilings(w, h, layout, rng)
     blocks, size_start, coef = itx_blocks_from_tilings(til, bpc, rng)
@@ -437,8 +439,15 @@ def make_frame(w, h, bpc=10, layout=1, seed=0x4C100001, sb128=1, with_fg=True):
     if layout:
         planes += [make_mixed_texture(rng, (w + ss_h) >> ss_h, (h + ss_v) >> ss_v, bpc) for _ in range(2)]
     fg = make_fg_params(rng, layout) if with_fg else None
-    return dict(w=w, h=h, bpc=bpc, layout=layout, planes=planes, blocks=blocks, size_start=size_start,
-                coef=coef, lf=lf, cdef=cd, lr=lr, fg=fg)
+    fr = dict(w=w, h=h, bpc=bpc, layout=layout, planes=planes, blocks=blocks, size_start=size_start,
+              coef=coef, lf=lf, cdef=cd, lr=lr, fg=fg, refs=None, mc=None)
+    if with_mc:
+        cw, ch = (w + ss_h) >> ss_h, (h + ss_v) >> ss_v
+        fr["refs"] = [[make_texture(rng, w, h, bpc)] +
+                      ([make_texture(rng, cw, ch, bpc) for _ in range(2)] if layout else [])
+                      for _ in range(nrefs)]
+        fr["mc"] = make_mc_units(w, h, layout, rng, nrefs=nrefs)
+    return fr
 
 
 def frame_bytes(w, h, bpc, layout=1):

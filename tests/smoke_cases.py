@@ -18,3 +18,26 @@ def run_smoke(ctx, oracle_lib, np, torch):
     for p in range(3):
         if not np.array_equal(f.plane_np(p), ref[p]):
             raise AssertionError(f"smoke: itx plane {p} differs from the oracle")
+
+    # inter prediction: a small 4:2:0 frame of MC units (single + compound) vs the oracle
+    from rav1d_amd.frame import McMeta, mc_frame
+    from rav1d_amd.synth import make_mc_units, make_texture
+    rng = np.random.default_rng(7)
+    w, h = 128, 96
+    refs = []
+    for _ in range(2):
+        r = Frame(w, h, 10, 1)
+        for p in range(3):
+            pw, ph = r.dims(p)
+            r.set_plane_np(p, make_texture(rng, pw, ph, 10))
+        refs.append(r)
+    units, ps, masks = make_mc_units(w, h, 1, rng, compound_frac=0.5, mv_px=16)
+    cur = Frame(w, h, 10, 1)
+    meta = McMeta(units, ps, masks)
+    mc_frame(ctx, cur, refs, meta)
+    torch.cuda.synchronize()
+    exp, _ = oracle_lib.mc_frame([cur.buffer_np(p) * 0 for p in range(3)],
+                                 [[r.buffer_np(p) for p in range(3)] for r in refs], 10, 1, w, h, units, masks)
+    for p in range(3):
+        if not np.array_equal(cur.buffer_np(p), exp[p]):
+            raise AssertionError(f"smoke: mc plane {p} differs from the oracle")
