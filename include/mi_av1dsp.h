@@ -200,13 +200,16 @@ int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, v
 /* Motion compensation for a whole frame: writes the inter prediction of every unit into
  * `cur` (itx then adds the residual). `refs` (host array of nrefs pictures, device planes,
  * grain-free, same size as cur) are read with edge replication (emu_edge, mc_tmpl.c:798-845).
- * `blocks` (device) must list all luma units first: luma = blocks[plane_start[0] ..
- * plane_start[1]), chroma = [plane_start[1] .. plane_start[3]) — chroma of a SEG unit reads
- * the mask its luma unit wrote. `masks` (device) holds MASK inputs and SEG outputs.
- * Scaled references, OBMC, warped and inter-intra units are not batched here yet. */
+ * `blocks` (device) are bucketed by plane group g (0 luma, 1 chroma) and shape class
+ * c = log2(w) * 8 + log2(h): the units of (g, c) are
+ * blocks[class_start[g * MI_MC_NCLASS + c] .. class_start[g * MI_MC_NCLASS + c + 1]) (host
+ * array, non-decreasing; all luma before all chroma). Luma runs first: chroma units of SEG
+ * blocks read the mask their luma unit wrote. `masks` (device) holds MASK inputs and SEG
+ * outputs. Scaled references, OBMC, warped and inter-intra units are not batched here yet. */
+#define MI_MC_NCLASS 64
 int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
-                const MiMcBlock *blocks, const uint32_t plane_start[4], uint8_t *masks,
-                void *stream);
+                const MiMcBlock *blocks, const uint32_t class_start[2 * MI_MC_NCLASS + 1],
+                uint8_t *masks, void *stream);
 
 /* CDEF for a whole frame, out of place: reads the deblocked picture `src` (never written)
  * and writes `dst` (blocks the reference skips are copied). Replaces rav1d_cdef_brow

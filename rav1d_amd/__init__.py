@@ -67,6 +67,7 @@ MCBLOCK_DTYPE = np.dtype([("x", "<u2"), ("y", "<u2"), ("w", "u1"), ("h", "u1"), 
                           ("comp", "u1"), ("param", "u1"), ("mask_off", "<u4")])
 assert MCBLOCK_DTYPE.itemsize == 24
 MC_AVG, MC_WAVG, MC_MASK, MC_SEG = 0, 1, 2, 3
+MC_NCLASS = 64
 
 N_RECT_TX_SIZES = 19
 ITX_KEEP_COEFS = 1

@@ -114,14 +114,14 @@ int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
 }
 
 int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
-                const MiMcBlock *blocks, const uint32_t plane_start[4], uint8_t *masks,
+                const MiMcBlock *blocks, const uint32_t class_start[2 * MI_MC_NCLASS + 1], uint8_t *masks,
                 void *stream) {
-    if (!ctx || !cur || !plane_start) return fail(ctx, -EINVAL);
+    if (!ctx || !cur || !class_start) return fail(ctx, -EINVAL);
     if (cur->bpc != 8 && cur->bpc != 10 && cur->bpc != 12) return fail(ctx, -EINVAL);
     if (nrefs < 0 || nrefs > 7 || (nrefs && !refs)) return fail(ctx, -EINVAL);
-    if (plane_start[0] > plane_start[1] || plane_start[1] > plane_start[2] || plane_start[2] > plane_start[3])
-        return fail(ctx, -EINVAL);
-    if (plane_start[3] == plane_start[0]) return 0;
+    for (int k = 0; k < 2 * MI_MC_NCLASS; k++)
+        if (class_start[k] > class_start[k + 1]) return fail(ctx, -EINVAL);
+    if (class_start[2 * MI_MC_NCLASS] == class_start[0]) return 0;
     if (!blocks || !nrefs) return fail(ctx, -EINVAL);
     mi::McArgs a;
     memset(&a, 0, sizeof(a));
@@ -150,10 +150,13 @@ int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nre
     a.layout = cur->layout;
     a.seg_ss_hor = cur->layout ? ss_hor : 0;   // w_mask[chr_layout_idx] (recon_tmpl.c:1868)
     a.seg_ss_ver = cur->layout ? ss_ver : 0;
+    memcpy(a.class_start, class_start, sizeof(a.class_start));
+    const int w0 = mi::mc_plan(a, 0), w1 = mi::mc_plan(a, 1);
+    if (w0 < 0 || w1 < 0) return fail(ctx, -EINVAL);
     hipStream_t s = (hipStream_t)stream;
     // luma first: chroma units of SEG blocks read the mask their luma unit writes
-    int r = mi::launch_mc(a, (int)plane_start[0], (int)(plane_start[1] - plane_start[0]), s);
-    if (!r) r = mi::launch_mc(a, (int)plane_start[1], (int)(plane_start[3] - plane_start[1]), s);
+    int r = mi::launch_mc(a, 0, w0, s);
+    if (!r) r = mi::launch_mc(a, 1, w1, s);
     return r ? fail(ctx, -EIO) : 0;
 }
 

@@ -102,9 +102,12 @@ struct McArgs {
     uint8_t *masks;
     int bpc, ib, bias, bdmax, layout;
     int seg_ss_hor, seg_ss_ver;      // w_mask[chr_layout_idx] subsampling of the SEG mask
+    uint32_t class_start[2 * MI_MC_NCLASS + 1];
+    uint32_t first_wave[2][MI_MC_NCLASS + 1];
 };
-// launchers (mc.hip)
-int launch_mc(const McArgs &a, int first, int count, hipStream_t s);
+// launchers (mc.hip): mc_plan fills first_wave[g] and returns the wave count of group g
+int mc_plan(McArgs &a, int g);
+int launch_mc(const McArgs &a, int g, int waves, hipStream_t s);
 
 struct LrArgs {
     const uint8_t *src[3];        // CDEF output C

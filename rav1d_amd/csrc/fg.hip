@@ -143,16 +143,26 @@ __global__ __launch_bounds__(256) void fg_prep_kernel(FgArgs a) {
         else if (d.num_uv_points[pl - 1]) v = scaling_entry(d.uv_points[pl - 1], d.num_uv_points[pl - 1], e, bdm8);
         a.scaling[pl * 4096 + e] = (uint8_t)v;
     }
-    // per-block offsets, one lane per 32-row block row (filmgrain.rs row_seed + draws)
-    for (int row = threadIdx.x; row < a.nrows; row += 256) {
-        unsigned s = d.seed;
-        s ^= (unsigned)(((row * 37 + 178) & 0xFF) << 8);
-        s ^= (unsigned)((row * 173 + 105) & 0xFF);
-        for (int b = 0; b < a.nblocks; b++) {
-            s = lfsr_step(s);
-            a.offsets[row * a.nblocks + b] = (uint8_t)((s >> 8) & 0xff);
-        }
-    }
+}
+
+// Per-block offsets (filmgrain.rs row_seed + one 8-bit draw per 32-wide block along the row):
+// one lane per (block row, block). Draw b of a row is the LFSR state after b + 1 steps from
+// the row seed: jump by M^(24 q) (k_lfsr_jump) then at most 23 single steps.
+__global__ __launch_bounds__(256) void fg_offsets_kernel(FgArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.nrows * a.nblocks) return;
+    const int row = i / a.nblocks, b = i - row * a.nblocks;
+    unsigned s = a.data.seed;
+    s ^= (unsigned)(((row * 37 + 178) & 0xFF) << 8);
+    s ^= (unsigned)((row * 173 + 105) & 0xFF);
+    s &= 0xffff;
+    const int n = b + 1, q = n / kDrawsPerLane, r = n - q * kDrawsPerLane;
+    unsigned t = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+        if ((s >> j) & 1) t ^= k_lfsr_jump[q][j];
+    for (int k = 0; k < r; k++) t = lfsr_step(t);
+    a.offsets[i] = (uint8_t)((t >> 8) & 0xff);
 }
 
 __device__ __forceinline__ int lut_at(const int16_t *lut, int rv, int subx, int suby, int bx, int by, int x, int y) {
@@ -446,7 +456,11 @@ int init_fg_tables() {
 }
 
 int launch_fg(const FgArgs &a, hipStream_t s, bool prep, bool apply) {
-    if (prep) hipLaunchKernelGGL(fg_prep_kernel, dim3(1), dim3(256), 0, s, a);
+    if (prep) {
+        hipLaunchKernelGGL(fg_prep_kernel, dim3(1), dim3(256), 0, s, a);
+        const int nb = a.nrows * a.nblocks;
+        if (nb > 0) hipLaunchKernelGGL(fg_offsets_kernel, dim3((nb + 255) / 256), dim3(256), 0, s, a);
+    }
     if (apply && a.blk_start[3] > 0) {
         if (a.bpc == 8) fg_apply_kernel<uint8_t><<<a.blk_start[3], 256, 0, s>>>(a);
         else fg_apply_kernel<uint16_t><<<a.blk_start[3], 256, 0, s>>>(a);

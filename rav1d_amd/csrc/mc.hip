@@ -4,14 +4,17 @@
 // 2025-2203, 3236-3428; C recon_tmpl.c:962-1011, 1836-1921) and the DSP mc[10]/mct[10]
 // (8-tap and bilinear put/prep), avg, w_avg, mask, w_mask (src/mc.rs; C mc_tmpl.c).
 //
-// One wave per prediction unit (a block's rectangle in one plane, up to 128x128). The unit is
-// cut into tiles of TW = min(w, 64) columns; the wave's 64 lanes form G = 64 / TW groups of
-// TW lanes, each group owning up to 16 consecutive rows, so a tile has TH = min(h, 16 G) rows.
-// Per tile and reference: the (TH+7) x (TW+7) reference window is staged in LDS with clamped
-// coordinates (identical to emu_edge's edge replication, mc_tmpl.c:798-845), the horizontal
-// pass writes TH+7 rows of intermediates to LDS, and each lane runs the vertical pass down its
-// column with an 8-entry register window. Compound predictions keep both references' prep
-// values in registers and blend them before a single coalesced store.
+// Work decomposition. Units (one block's rectangle in one plane) arrive bucketed by shape
+// class (log2 w, log2 h). Every lane owns one output column and R = min(h, 8) consecutive
+// rows. A class whose unit needs at most 64 such lanes packs U = min(64 / lanes, 8) units into
+// one wave; a larger unit is cut into 64-lane tiles, one wave each. One wave = one workgroup.
+//
+// Per item: both references' windows (rows + 7) x (cols + 7) are staged in LDS in one loop
+// with clamped coordinates (identical to emu_edge's replication, mc_tmpl.c:798-845), then a
+// single barrier. Each lane evaluates the horizontal 8-tap for its column on its R + 7 rows
+// straight from LDS as five v_dot2_i32_i16 on aligned sample pairs (odd columns use the tap
+// set shifted by one), feeds the vertical 8-tap through a register window, and blends the
+// two predictions in registers (avg / w_avg / mask / w_mask) before the store.
 #include "common.h"
 
 namespace mi {
@@ -20,53 +23,41 @@ __constant__ int8_t k_subpel[6][15][8] = {
 #include "tables/mc_subpel_filters.inc"
 };
 
-constexpr int kWinMax = 1640;    // max (TH+7)*(TW+7) over unit shapes (23*71, 71*23, 39*39)
-constexpr int kMidMax = 1480;    // max (TH+7)*TW (23*64, 71*16, 39*32)
+typedef short s16x2 __attribute__((ext_vector_type(2)));
 
-// filter2d (Filter2d, horizontal/vertical order) -> subpel filter types (0 regular, 1 smooth, 2 sharp)
+constexpr int kMaxU = 8;           // units packed per wave (bounds the LDS windows)
+constexpr int kWinElems = 2240;    // per reference: max over classes of U * (rows+7) * (cols+8) (4x16: 2208)
+
+// filter2d (Filter2d, horizontal/vertical order) -> subpel filter type (0 regular, 1 smooth, 2 sharp)
 __device__ __forceinline__ int f2d_type_h(int f) { return (int)((0x111222000ull >> (4 * f)) & 15); }
 __device__ __forceinline__ int f2d_type_v(int f) { return (int)((0x210210210ull >> (4 * f)) & 15); }
 
-// Taps of one direction: 8 ints (bilinear as [0,0,0,16-m,m,0,0,0]); has = filter present.
-struct Taps {
-    int f[8];
-    bool has;
+__device__ __forceinline__ uint32_t pack2(int lo, int hi) { return (uint32_t)(lo & 0xffff) | ((uint32_t)hi << 16); }
+
+// Shape-class geometry (all wave-uniform).
+struct ClassGeom {
+    int w, h, TW, R, lanes_u, U, T, TR, ctiles;
 };
 
-__device__ __forceinline__ Taps make_taps(int m, int n, int type, bool bilin) {
-    Taps t;
-    t.has = m != 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) t.f[k] = 0;
-    if (!t.has) return t;
-    if (bilin) {
-        t.f[3] = 16 - m;
-        t.f[4] = m;
+__device__ __forceinline__ ClassGeom class_geom(int c) {
+    ClassGeom g;
+    g.w = 1 << (c >> 3);
+    g.h = 1 << (c & 7);
+    g.TW = min(g.w, 64);
+    g.R = min(g.h, 8);
+    g.lanes_u = g.TW * (g.h / g.R);
+    if (g.lanes_u <= 64) {
+        g.U = min(64 / g.lanes_u, kMaxU);
+        g.T = 1;
+        g.TR = g.h;
+        g.ctiles = 1;
     } else {
-        const int row = n > 4 ? type : 3 + (type & 1);
-#pragma unroll
-        for (int k = 0; k < 8; k++) t.f[k] = k_subpel[row][m - 1][k];
+        g.U = 1;
+        g.TR = (64 / g.TW) * g.R;
+        g.ctiles = g.w / g.TW;
+        g.T = g.ctiles * (g.h / g.TR);
     }
-    return t;
-}
-
-struct McUnit {
-    int x, y, w, h, plane, filter2d, nref, comp, param;
-    int mvx[2], mvy[2], ref[2];
-    uint32_t mask_off;
-};
-
-__device__ __forceinline__ McUnit load_unit(const MiMcBlock *b) {
-    McUnit u;
-    u.x = b->x; u.y = b->y; u.w = b->w; u.h = b->h;
-    u.plane = b->plane; u.filter2d = b->filter2d;
-    u.mvx[0] = b->mvx[0]; u.mvx[1] = b->mvx[1];
-    u.mvy[0] = b->mvy[0]; u.mvy[1] = b->mvy[1];
-    u.ref[0] = b->ref[0]; u.ref[1] = b->ref[1];
-    u.nref = b->ref[1] >= 0 ? 2 : 1;
-    u.comp = b->comp; u.param = b->param;
-    u.mask_off = b->mask_off;
-    return u;
+    return g;
 }
 
 template <typename Px>
@@ -74,202 +65,272 @@ __device__ __forceinline__ int ldpx(const uint8_t *base, int64_t stride, int y, 
     return reinterpret_cast<const Px *>(base + (int64_t)y * stride)[x];
 }
 
-// One reference's prediction for the tile (tx0, ty0) of unit u: put (pixel) or prep (int16
-// intermediate) values for this lane's rows, out[q] for row g*R + q, column c.
+// Per-lane view of one reference of its unit.
+struct RefSel {
+    const uint8_t *base;
+    int64_t stride;
+    int iw, ih, dx, dy, mx, my;
+};
+
 template <typename Px, bool PREP>
-__device__ __forceinline__ void predict_tile(const McArgs &a, const McUnit &u, int i, int tx0, int ty0,
-                                             int TW, int TH, int R, int16_t *win, int16_t *mid, int out[16]) {
-    const int lane = threadIdx.x;
-    const int p = u.plane;
-    const int ssh = p && a.layout != 3, ssv = p && a.layout == 1;
-    const int r = u.ref[i];
-    const int mvx = u.mvx[i], mvy = u.mvy[i];
-    const int mx = (mvx & (15 >> !ssh)) << !ssh, my = (mvy & (15 >> !ssv)) << !ssv;
-    const int dx = u.x + (mvx >> (3 + ssh)) + tx0, dy = u.y + (mvy >> (3 + ssv)) + ty0;
-    const uint8_t *ref = a.ref[r][p];
-    const int64_t rs = a.ref_stride[r][p ? 1 : 0];
-    const int iw = a.ref_w[r][p], ih = a.ref_h[r][p];
-    const bool bilin = u.filter2d == 9;
-    const Taps fh = make_taps(mx, u.w, bilin ? 0 : f2d_type_h(u.filter2d), bilin);
-    const Taps fv = make_taps(my, u.h, bilin ? 0 : f2d_type_v(u.filter2d), bilin);
+__device__ __forceinline__ void predict(const McArgs &a, const int16_t *win, int WS, const RefSel &s, int f2d,
+                                        int w, int h, int col, int r0, int R, int out[8]) {
+    const bool bilin = f2d == 9;
     const int SH = bilin ? 4 : 6, ib = a.ib;
-
-    // stage the window: rows dy-3 .. dy+TH+3, cols dx-3 .. dx+TW+3, clamped to the plane
-    const int WC = TW + 7, WR = TH + 7, NW = WC * WR;
-    const uint32_t inv = (1u << 20) / WC + 1;          // (k * inv) >> 20 == k / WC for k < 2^20 / WC^2
-    __syncthreads();                                   // previous users of win / mid are done
-    for (int k = lane; k < NW; k += 64) {
-        const int rr = (int)(((uint32_t)k * inv) >> 20), cc = k - rr * WC;
-        const int yy = min(max(dy - 3 + rr, 0), ih - 1), xx = min(max(dx - 3 + cc, 0), iw - 1);
-        win[k] = (int16_t)ldpx<Px>(ref, rs, yy, xx);
+    int fh[8] = { 0, 0, 0, 0, 0, 0, 0, 0 }, fv[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
+    if (s.mx) {
+        if (bilin) { fh[3] = 16 - s.mx; fh[4] = s.mx; }
+        else {
+            const int t = f2d_type_h(f2d), row = w > 4 ? t : 3 + (t & 1);
+#pragma unroll
+            for (int k = 0; k < 8; k++) fh[k] = k_subpel[row][s.mx - 1][k];
+        }
     }
-    __syncthreads();
-
-    const int c = lane & (TW - 1), g = lane / TW;
-    const int r0 = g * R;
-    if (fh.has) {
-        // horizontal pass: mid[rr][cc] for rr in [0, WR) when a vertical filter follows,
-        // else only this lane's rows 3 .. TH+2 are needed (computed directly below)
-        if (fv.has) {
-            for (int k = lane; k < WR * TW; k += 64) {
-                const int rr = k / TW, cc = k & (TW - 1);
-                const int16_t *w = win + rr * WC + cc;
-                int s = 0;
+    if (s.my) {
+        if (bilin) { fv[3] = 16 - s.my; fv[4] = s.my; }
+        else {
+            const int t = f2d_type_v(f2d), row = h > 4 ? t : 3 + (t & 1);
 #pragma unroll
-                for (int t = 0; t < 8; t++) s += fh.f[t] * w[t];
-                mid[k] = (int16_t)((s + ((1 << (SH - ib)) >> 1)) >> (SH - ib));
-            }
-            __syncthreads();
-            if (r0 < TH) {
-                int v[8];
-                const int16_t *m = mid + r0 * TW + c;
+            for (int k = 0; k < 8; k++) fv[k] = k_subpel[row][s.my - 1][k];
+        }
+    }
+    // horizontal taps as 5 aligned pairs: even column (f0,f1)..(f6,f7),(0,0); odd column
+    // starts one sample left: (0,f0),(f1,f2),..,(f7,0)
+    const bool odd = col & 1;
+    uint32_t hp[5];
 #pragma unroll
-                for (int t = 0; t < 7; t++) v[t] = m[t * TW];
+    for (int j = 0; j < 5; j++) {
+        const int lo = odd ? (j ? fh[2 * j - 1] : 0) : (j < 4 ? fh[2 * j] : 0);
+        const int hi = odd ? (j < 4 ? fh[2 * j] : 0) : (j < 4 ? fh[2 * j + 1] : 0);
+        hp[j] = pack2(lo, hi);
+    }
+    const uint32_t *wrow = reinterpret_cast<const uint32_t *>(win + r0 * WS + (col & ~1));
+    const int WS2 = WS >> 1;
+    auto hsum = [&](int rr) {
+        const uint32_t *p = wrow + rr * WS2;
+        int s2 = 0;
 #pragma unroll
-                for (int q = 0; q < 16; q++) {
-                    if (q < R) {
-                        v[7] = m[(q + 7) * TW];
-                        int s = 0;
+        for (int j = 0; j < 5; j++)
+            s2 = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, p[j]), __builtin_bit_cast(s16x2, hp[j]), s2, false);
+        return s2;
+    };
+    auto center = [&](int rr) { return (int)win[(r0 + rr) * WS + col + 3]; };
+    const int hsh = SH - ib, hrnd = (1 << hsh) >> 1;
+    if (s.mx && s.my) {
+        int v[8];
 #pragma unroll
-                        for (int t = 0; t < 8; t++) s += fv.f[t] * v[t];
-                        out[q] = PREP ? ((s + ((1 << SH) >> 1)) >> SH) - a.bias
-                                      : min(max((s + ((1 << (SH + ib)) >> 1)) >> (SH + ib), 0), a.bdmax);
+        for (int t = 0; t < 7; t++) v[t] = (hsum(t) + hrnd) >> hsh;
 #pragma unroll
-                        for (int t = 0; t < 7; t++) v[t] = v[t + 1];
-                    }
-                }
-            }
-        } else if (r0 < TH) {
+        for (int q = 0; q < 8; q++) {
+            if (q < R) {
+                v[7] = (hsum(q + 7) + hrnd) >> hsh;
+                int sum = 0;
 #pragma unroll
-            for (int q = 0; q < 16; q++) {
-                if (q < R) {
-                    const int16_t *w = win + (r0 + q + 3) * WC + c;
-                    int s = 0;
+                for (int t = 0; t < 8; t++) sum += fv[t] * v[t];
+                out[q] = PREP ? ((sum + ((1 << SH) >> 1)) >> SH) - a.bias
+                              : min(max((sum + ((1 << (SH + ib)) >> 1)) >> (SH + ib), 0), a.bdmax);
 #pragma unroll
-                    for (int t = 0; t < 8; t++) s += fh.f[t] * w[t];
-                    const int px = (s + ((1 << (SH - ib)) >> 1)) >> (SH - ib);
-                    out[q] = PREP ? px - a.bias : min(max((px + ((1 << ib) >> 1)) >> ib, 0), a.bdmax);
-                }
+                for (int t = 0; t < 7; t++) v[t] = v[t + 1];
             }
         }
-    } else if (r0 < TH) {
-        if (fv.has) {
-            int v[8];
-            const int16_t *w = win + r0 * WC + c + 3;
+    } else if (s.mx) {
 #pragma unroll
-            for (int t = 0; t < 7; t++) v[t] = w[t * WC];
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-                if (q < R) {
-                    v[7] = w[(q + 7) * WC];
-                    int s = 0;
-#pragma unroll
-                    for (int t = 0; t < 8; t++) s += fv.f[t] * v[t];
-                    out[q] = PREP ? ((s + ((1 << (SH - ib)) >> 1)) >> (SH - ib)) - a.bias
-                                  : min(max((s + ((1 << SH) >> 1)) >> SH, 0), a.bdmax);
-#pragma unroll
-                    for (int t = 0; t < 7; t++) v[t] = v[t + 1];
-                }
+        for (int q = 0; q < 8; q++) {
+            if (q < R) {
+                const int px = (hsum(q + 3) + hrnd) >> hsh;
+                out[q] = PREP ? px - a.bias : min(max((px + ((1 << ib) >> 1)) >> ib, 0), a.bdmax);
             }
-        } else {
-#pragma unroll
-            for (int q = 0; q < 16; q++)
-                if (q < R) {
-                    const int px = win[(r0 + q + 3) * WC + c + 3];
-                    out[q] = PREP ? (px << ib) - a.bias : px;
-                }
         }
+    } else if (s.my) {
+        int v[8];
+#pragma unroll
+        for (int t = 0; t < 7; t++) v[t] = center(t);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            if (q < R) {
+                v[7] = center(q + 7);
+                int sum = 0;
+#pragma unroll
+                for (int t = 0; t < 8; t++) sum += fv[t] * v[t];
+                out[q] = PREP ? ((sum + hrnd) >> hsh) - a.bias : min(max((sum + ((1 << SH) >> 1)) >> SH, 0), a.bdmax);
+#pragma unroll
+                for (int t = 0; t < 7; t++) v[t] = v[t + 1];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+            if (q < R) out[q] = PREP ? (center(q + 3) << ib) - a.bias : center(q + 3);
     }
 }
 
 template <typename Px>
-__global__ __launch_bounds__(64) void mc_kernel(McArgs a, int first) {
-    __shared__ int16_t win[kWinMax];
-    __shared__ int16_t mid[kMidMax];
-    __shared__ uint8_t mtile[1024];            // SEG: per-pixel blend weights of the tile (TH*TW <= 1024)
-    const McUnit u = load_unit(&a.blocks[first + blockIdx.x]);
+__global__ __launch_bounds__(64) void mc_kernel(McArgs a, int g) {
+    __shared__ __attribute__((aligned(16))) int16_t win[2][kWinElems];
     const int lane = threadIdx.x;
-    const int TW = min(u.w, 64), G = 64 / TW, TH = min(u.h, 16 * G);
-    const int R = (TH + G - 1) / G;
-    const int c = lane & (TW - 1), g = lane / TW, r0 = g * R;
-    const int p = u.plane;
-    const int64_t ds = a.dst_stride[p ? 1 : 0];
-    uint8_t *dst = a.dst[p];
-    const int sign = u.param >> 7;
+    const int wave = blockIdx.x;
+    // class of this wave: last class whose first wave <= wave (wave-uniform scan)
+    const uint32_t *fw = a.first_wave[g];
+    int c = 0;
+    for (int k = 1; k < MI_MC_NCLASS; k++)
+        if (fw[k] <= (uint32_t)wave) c = k;
+    const ClassGeom G = class_geom(c);
+    const int item = wave - (int)fw[c];
+    const uint32_t cls_begin = a.class_start[g * MI_MC_NCLASS + c], cls_end = a.class_start[g * MI_MC_NCLASS + c + 1];
 
-    for (int ty0 = 0; ty0 < u.h; ty0 += TH) {
-        for (int tx0 = 0; tx0 < u.w; tx0 += TW) {
-            int o0[16], o1[16];
-            if (u.nref == 1) {
-                predict_tile<Px, false>(a, u, 0, tx0, ty0, TW, TH, R, win, mid, o0);
+    // this lane's unit, tile origin, column and rows
+    int uu, tx0 = 0, ty0 = 0, rg, col;
+    uint32_t ui;
+    if (G.T == 1) {
+        uu = lane / G.lanes_u;
+        const int li = lane - uu * G.lanes_u;
+        rg = li / G.TW;
+        col = li - rg * G.TW;
+        ui = cls_begin + (uint32_t)item * G.U + uu;
+    } else {
+        uu = 0;
+        const int tile = item % G.T;
+        ui = cls_begin + (uint32_t)(item / G.T);
+        tx0 = (tile % G.ctiles) * G.TW;
+        ty0 = (tile / G.ctiles) * G.TR;
+        rg = lane / G.TW;
+        col = lane - rg * G.TW;
+    }
+    const bool active = uu < G.U && ui < cls_end;
+    const MiMcBlock b = a.blocks[active ? ui : cls_begin];
+    const int p = b.plane;
+    const int ssh = p && a.layout != 3, ssv = p && a.layout == 1;
+    const int nref = b.ref[1] >= 0 ? 2 : 1;
+    RefSel rs[2];
 #pragma unroll
-                for (int q = 0; q < 16; q++)
-                    if (q < R && r0 + q < TH)
-                        reinterpret_cast<Px *>(dst + (int64_t)(u.y + ty0 + r0 + q) * ds)[u.x + tx0 + c] = (Px)o0[q];
-                continue;
+    for (int i = 0; i < 2; i++) {
+        const int r = b.ref[i] >= 0 ? b.ref[i] : b.ref[0];
+        const int mvx = b.mvx[i], mvy = b.mvy[i];
+        rs[i].base = a.ref[r][p];
+        rs[i].stride = a.ref_stride[r][p ? 1 : 0];
+        rs[i].iw = a.ref_w[r][p];
+        rs[i].ih = a.ref_h[r][p];
+        rs[i].mx = (mvx & (15 >> !ssh)) << !ssh;
+        rs[i].my = (mvy & (15 >> !ssv)) << !ssv;
+        rs[i].dx = b.x + (mvx >> (3 + ssh)) + tx0 - 3;
+        rs[i].dy = b.y + (mvy >> (3 + ssv)) + ty0 - 3;
+    }
+
+    // stage windows: rows TR + 7, cols TW + 7 (row stride WS = TW + 8, even)
+    const int WC = G.TW + 7, WR = G.TR + 7, WS = G.TW + 8, WN = WR * WS;
+    const uint32_t inv = (1u << 20) / WC + 1;          // (e * inv) >> 20 == e / WC for e < 2^20 / WC^2
+    if (active) {
+        const int li = G.T == 1 ? lane - uu * G.lanes_u : lane;
+        const int nl = G.T == 1 ? G.lanes_u : 64;
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            if (i >= nref) break;
+            int16_t *wdst = win[i] + uu * WN;
+            for (int e = li; e < WR * WC; e += nl) {
+                const int rr = (int)(((uint32_t)e * inv) >> 20), cc = e - rr * WC;
+                const int yy = min(max(rs[i].dy + rr, 0), rs[i].ih - 1);
+                const int xx = min(max(rs[i].dx + cc, 0), rs[i].iw - 1);
+                wdst[rr * WS + cc] = (int16_t)ldpx<Px>(rs[i].base, rs[i].stride, yy, xx);
             }
-            predict_tile<Px, true>(a, u, 0, tx0, ty0, TW, TH, R, win, mid, o0);
-            predict_tile<Px, true>(a, u, 1, tx0, ty0, TW, TH, R, win, mid, o1);
-            const int ib = a.ib;
-            if (u.comp == MI_MC_SEG) {
-                // w_mask (mc_tmpl.c:661-712): per-pixel weight from |t1 - t2| (t1 = tmp[sign])
-                const int mask_sh = a.bpc + ib - 4, mask_rnd = 1 << (mask_sh - 5);
-                const int sh = ib + 6, rnd = (32 << ib) + a.bias * 64;
-#pragma unroll
-                for (int q = 0; q < 16; q++) {
-                    if (q < R && r0 + q < TH) {
-                        const int t1 = sign ? o1[q] : o0[q], t2 = sign ? o0[q] : o1[q];
-                        const int m = min(38 + ((abs(t1 - t2) + mask_rnd) >> mask_sh), 64);
-                        mtile[(r0 + q) * TW + c] = (uint8_t)m;
-                        o0[q] = min(max((t1 * m + t2 * (64 - m) + rnd) >> sh, 0), a.bdmax);
-                    }
-                }
-                __syncthreads();
-                // chroma-resolution mask (w_mask_444/422/420 by the chroma layout)
-                const int msh = a.seg_ss_hor, msv = a.seg_ss_ver;
-                const int mw = TW >> msh, mh = TH >> msv, mstride = u.w >> msh;
-                uint8_t *mo = a.masks + u.mask_off + (ty0 >> msv) * mstride + (tx0 >> msh);
-                for (int k = lane; k < mw * mh; k += 64) {
-                    const int yy = k / mw, xx = k - yy * mw;
-                    const uint8_t *m0 = mtile + (yy << msv) * TW + (xx << msh);
-                    int v;
-                    if (msh && msv) v = (m0[0] + m0[1] + m0[TW] + m0[TW + 1] + 2 - sign) >> 2;
-                    else if (msh) v = (m0[0] + m0[1] + 1 - sign) >> 1;
-                    else v = m0[0];
-                    mo[yy * mstride + xx] = (uint8_t)v;
-                }
-            } else {
-                const uint8_t *mk = a.masks + u.mask_off;
-#pragma unroll
-                for (int q = 0; q < 16; q++) {
-                    if (q < R && r0 + q < TH) {
-                        int v;
-                        if (u.comp == MI_MC_AVG) {
-                            v = (o0[q] + o1[q] + (1 << ib) + a.bias * 2) >> (ib + 1);
-                        } else if (u.comp == MI_MC_WAVG) {
-                            const int wt = u.param & 31;
-                            v = (o0[q] * wt + o1[q] * (16 - wt) + (8 << ib) + a.bias * 16) >> (ib + 4);
-                        } else {
-                            const int m = mk[(ty0 + r0 + q) * u.w + tx0 + c];
-                            const int t1 = sign ? o1[q] : o0[q], t2 = sign ? o0[q] : o1[q];
-                            v = (t1 * m + t2 * (64 - m) + (32 << ib) + a.bias * 64) >> (ib + 6);
-                        }
-                        o0[q] = min(max(v, 0), a.bdmax);
-                    }
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 16; q++)
-                if (q < R && r0 + q < TH)
-                    reinterpret_cast<Px *>(dst + (int64_t)(u.y + ty0 + r0 + q) * ds)[u.x + tx0 + c] = (Px)o0[q];
         }
     }
+    __syncthreads();
+    if (!active) return;
+
+    const int r0 = rg * G.R, R = G.R;
+    int o0[8], o1[8];
+    const int64_t ds = a.dst_stride[p ? 1 : 0];
+    uint8_t *dst = a.dst[p] + (int64_t)(b.y + ty0 + r0) * ds;
+    const int x = b.x + tx0 + col;
+    if (nref == 1) {
+        predict<Px, false>(a, win[0] + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+            if (q < R) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];
+        return;
+    }
+    predict<Px, true>(a, win[0] + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
+    predict<Px, true>(a, win[1] + uu * WN, WS, rs[1], b.filter2d, b.w, b.h, col, r0, R, o1);
+    const int ib = a.ib, sign = b.param >> 7;
+    if (b.comp == MI_MC_SEG) {
+        // w_mask (mc_tmpl.c:661-712): per-pixel weight from |t1 - t2|, t1 = tmp[sign]
+        const int mask_sh = a.bpc + ib - 4, mask_rnd = 1 << (mask_sh - 5);
+        const int sh = ib + 6, rnd = (32 << ib) + a.bias * 64;
+        const int msh = a.seg_ss_hor, msv = a.seg_ss_ver, mstride = b.w >> msh;
+        const int yb = ty0 + r0, xb = tx0 + col;
+        uint8_t *mo = a.masks + b.mask_off;
+        int mprev = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            if (q < R) {
+                const int t1 = sign ? o1[q] : o0[q], t2 = sign ? o0[q] : o1[q];
+                const int m = min(38 + ((abs(t1 - t2) + mask_rnd) >> mask_sh), 64);
+                o0[q] = min(max((t1 * m + t2 * (64 - m) + rnd) >> sh, 0), a.bdmax);
+                // neighbour column (lane ^ 1 holds column ^ 1 of the same rows)
+                const int mn = msh ? __shfl_xor(m, 1) : 0;
+                if (!msh) {
+                    mo[(yb + q) * mstride + xb] = (uint8_t)m;
+                } else if (!msv) {
+                    if (!(col & 1)) mo[(yb + q) * mstride + (xb >> 1)] = (uint8_t)((m + mn + 1 - sign) >> 1);
+                } else if (q & 1) {
+                    if (!(col & 1)) mo[((yb + q) >> 1) * mstride + (xb >> 1)] = (uint8_t)((mprev + m + mn + 2 - sign) >> 2);
+                } else {
+                    mprev = m + mn;
+                }
+            }
+        }
+    } else {
+        const uint8_t *mk = a.masks + b.mask_off;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            if (q < R) {
+                int v;
+                if (b.comp == MI_MC_AVG) {
+                    v = (o0[q] + o1[q] + (1 << ib) + a.bias * 2) >> (ib + 1);
+                } else if (b.comp == MI_MC_WAVG) {
+                    const int wt = b.param & 31;
+                    v = (o0[q] * wt + o1[q] * (16 - wt) + (8 << ib) + a.bias * 16) >> (ib + 4);
+                } else {
+                    const int m = mk[(ty0 + r0 + q) * b.w + tx0 + col];
+                    const int t1 = sign ? o1[q] : o0[q], t2 = sign ? o0[q] : o1[q];
+                    v = (t1 * m + t2 * (64 - m) + (32 << ib) + a.bias * 64) >> (ib + 6);
+                }
+                o0[q] = min(max(v, 0), a.bdmax);
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+        if (q < R) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];
 }
 
-int launch_mc(const McArgs &a, int first, int count, hipStream_t s) {
-    if (count <= 0) return 0;
-    if (a.bpc == 8) mc_kernel<uint8_t><<<count, 64, 0, s>>>(a, first);
-    else mc_kernel<uint16_t><<<count, 64, 0, s>>>(a, first);
+// Waves per class for one plane group: packed small units or one wave per 64-lane tile.
+int mc_plan(McArgs &a, int g) {
+    uint32_t waves = 0;
+    for (int c = 0; c < MI_MC_NCLASS; c++) {
+        a.first_wave[g][c] = waves;
+        const uint32_t n = a.class_start[g * MI_MC_NCLASS + c + 1] - a.class_start[g * MI_MC_NCLASS + c];
+        if (!n) continue;
+        const int lw = c >> 3, lh = c & 7;
+        if (lw < 1 || lh < 1) return -1;                    // widths/heights are 2..128
+        const int w = 1 << lw, h = 1 << lh;
+        const int TW = w < 64 ? w : 64, R = h < 8 ? h : 8, lanes = TW * (h / R);
+        if (lanes <= 64) {
+            const int U = 64 / lanes < kMaxU ? 64 / lanes : kMaxU;
+            waves += (n + U - 1) / U;
+        } else {
+            const int TR = (64 / TW) * R;
+            waves += n * (uint32_t)((w / TW) * (h / TR));
+        }
+    }
+    a.first_wave[g][MI_MC_NCLASS] = waves;
+    return (int)waves;
+}
+
+int launch_mc(const McArgs &a, int g, int waves, hipStream_t s) {
+    if (waves <= 0) return 0;
+    if (a.bpc == 8) mc_kernel<uint8_t><<<waves, 64, 0, s>>>(a, g);
+    else mc_kernel<uint16_t><<<waves, 64, 0, s>>>(a, g);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -11,7 +11,7 @@ import ctypes
 import numpy as np
 import torch
 
-from . import MiCdef, MiFilmGrainData, MiLoopFilter, MiLr, MiPicture, MiError, check, lib
+from . import MC_NCLASS, MiCdef, MiFilmGrainData, MiLoopFilter, MiLr, MiPicture, MiError, check, lib
 
 LAYOUT_I400, LAYOUT_I420, LAYOUT_I422, LAYOUT_I444 = 0, 1, 2, 3
 
@@ -133,20 +133,21 @@ def itx_frame(ctx, frame, blocks_dev, size_start, coef_dev, flags=0, stream=None
 
 
 class McMeta:
-    """Device copies of a frame's MC units (MiMcBlock, luma first) and mask buffer."""
+    """Device copies of a frame's MC units (MiMcBlock, bucketed by plane group and shape
+    class; see mc_sort_units) and mask buffer."""
 
-    def __init__(self, units, plane_start, masks):
+    def __init__(self, units, class_start, masks):
         self.n = len(units)
         self.blocks = torch.from_numpy(np.ascontiguousarray(units).view(np.uint8).copy()).cuda()
         self.masks = torch.from_numpy(np.ascontiguousarray(masks).copy()).cuda()
-        self.plane_start = (ctypes.c_uint32 * 4)(*[int(v) for v in plane_start])
+        self.class_start = (ctypes.c_uint32 * (2 * MC_NCLASS + 1))(*[int(v) for v in class_start])
 
 
 def mc_frame(ctx, cur, refs, meta, stream=None):
     """mi_mc_frame: inter prediction of every unit into `cur` from the reference Frames."""
     pics = (MiPicture * len(refs))(*[r.picture() for r in refs])
     rc = lib().mi_mc_frame(ctx.h, ctypes.byref(cur.picture()), pics, len(refs),
-                           ctypes.c_void_p(meta.blocks.data_ptr()), meta.plane_start,
+                           ctypes.c_void_p(meta.blocks.data_ptr()), meta.class_start,
                            ctypes.c_void_p(meta.masks.data_ptr()), _stream_ptr(stream))
     check(rc, "mi_mc_frame")
 

@@ -9,7 +9,7 @@ function of (geometry, seed), so the same inputs regenerate bit-identically anyw
 """
 import numpy as np
 
-from . import MCBLOCK_DTYPE, TXBLOCK_DTYPE, N_RECT_TX_SIZES
+from . import MC_NCLASS, MCBLOCK_DTYPE, TXBLOCK_DTYPE, N_RECT_TX_SIZES
 
 # RectTxfmSize (rav1d src/levels.rs:46-82): (w, h)
 TX_DIMS = [(4, 4), (8, 8), (16, 16), (32, 32), (64, 64), (4, 8), (8, 4), (8, 16), (16, 8),
@@ -501,8 +501,8 @@ def _mc_record(x, y, bw, bh, plane, f2d, mvs, refs, comp, param, mask_off):
 def make_mc_units(w, h, layout, rng, nrefs=2, compound_frac=0.3, mv_px=64, sb=64, min_bs=8, blocks=None):
     """Inter prediction units for one frame: every block predicted from one reference (put)
     or two (compound: avg / w_avg / mask / seg, uniformly), filters uniform over the nine
-    8-tap pairs and bilinear, MVs uniform in +-mv_px at 1/8 pel. Returns (units sorted luma
-    first, plane_start[4], mask buffer)."""
+    8-tap pairs and bilinear, MVs uniform in +-mv_px at 1/8 pel. Returns (units bucketed by
+    plane group and shape class, class_start[2 * MC_NCLASS + 1], mask buffer)."""
     ss_h = 1 if layout in (1, 2) else 0
     ss_v = 1 if layout == 1 else 0
     seg_h, seg_v = (ss_h, ss_v) if layout else (0, 0)
@@ -540,18 +540,32 @@ def make_mc_units(w, h, layout, rng, nrefs=2, compound_frac=0.3, mv_px=64, sb=64
                 ccomp = 2
             for pl in (1, 2):
                 chroma.append(_mc_record(x >> ss_h, y >> ss_v, cw, ch, pl, f2d, mvs, refs, ccomp, param, coff))
-    units = np.array(luma + chroma, dtype=MCBLOCK_DTYPE)
-    plane_start = np.array([0, len(luma), len(luma) + len(chroma) // 2 if layout else len(luma),
-                            len(luma) + len(chroma)], np.uint32)
+    units, class_start = mc_sort_units(np.array(luma + chroma, dtype=MCBLOCK_DTYPE))
     mask_buf = np.concatenate(masks) if masks else np.zeros(1, np.uint8)
     if mask_buf.size == 0:
         mask_buf = np.zeros(1, np.uint8)
-    return units, plane_start, mask_buf
+    return units, class_start, mask_buf
+
+
+def mc_class_of(units):
+    """Shape class log2(w) * 8 + log2(h) of each unit (include/mi_av1dsp.h MI_MC_NCLASS)."""
+    return (np.log2(units["w"]).astype(np.int64) * 8 + np.log2(units["h"]).astype(np.int64))
+
+
+def mc_sort_units(units):
+    """Bucket units by (plane group, shape class) as mi_mc_frame requires: returns the
+    stably sorted units and class_start[2 * MC_NCLASS + 1]."""
+    grp = (units["plane"] > 0).astype(np.int64)
+    key = grp * MC_NCLASS + mc_class_of(units)
+    order = np.argsort(key, kind="stable")
+    cs = np.searchsorted(key[order], np.arange(2 * MC_NCLASS + 1)).astype(np.uint32)
+    return units[order], cs
 
 
 def make_mc_grid_units(pw, ph, uw, uh, plane, rng, nrefs=2, compound_frac=0.5, mv_px=24):
     """A plane tiled with uw x uh units (any size 2..128, including the 4-tap w/h <= 4 cases),
-    for kernel-shape coverage. Compound only where uw, uh >= 8 (as AV1); no SEG/MASK here."""
+    for kernel-shape coverage. Compound only where uw, uh >= 8 (as AV1); no SEG/MASK here.
+    Returns (units, class_start)."""
     recs = []
     for y in range(0, ph, uh):
         for x in range(0, pw, uw):
@@ -565,7 +579,7 @@ def make_mc_grid_units(pw, ph, uw, uh, plane, rng, nrefs=2, compound_frac=0.5, m
                                        int(rng.integers(1, 16)) if comp else 0, 0))
             else:
                 recs.append(_mc_record(x, y, uw, uh, plane, f2d, mvs, (int(rng.integers(0, nrefs)), -1), 0, 0, 0))
-    return np.array(recs, dtype=MCBLOCK_DTYPE)
+    return mc_sort_units(np.array(recs, dtype=MCBLOCK_DTYPE))
 
 
 def mc_algorithmic_bytes(units, bpc):

@@ -31,9 +31,9 @@ def run_smoke(ctx, oracle_lib, np, torch):
             pw, ph = r.dims(p)
             r.set_plane_np(p, make_texture(rng, pw, ph, 10))
         refs.append(r)
-    units, ps, masks = make_mc_units(w, h, 1, rng, compound_frac=0.5, mv_px=16)
+    units, cs, masks = make_mc_units(w, h, 1, rng, compound_frac=0.5, mv_px=16)
     cur = Frame(w, h, 10, 1)
-    meta = McMeta(units, ps, masks)
+    meta = McMeta(units, cs, masks)
     mc_frame(ctx, cur, refs, meta)
     torch.cuda.synchronize()
     exp, _ = oracle_lib.mc_frame([cur.buffer_np(p) * 0 for p in range(3)],

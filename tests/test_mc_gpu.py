@@ -23,12 +23,12 @@ def make_refs(w, h, bpc, layout, n, rng):
     return refs
 
 
-def run_case(gpu, w, h, bpc, layout, units, plane_start, masks, refs, rng):
+def run_case(gpu, w, h, bpc, layout, units, class_start, masks, refs, rng):
     cur = Frame(w, h, bpc, layout)
     init = [rng.integers(0, 1 << bpc, size=cur.buffer_np(p).shape) for p in range(len(cur.planes))]
     for p, a in enumerate(init):
         cur.set_buffer_np(p, a)
-    meta = McMeta(units, plane_start, masks)
+    meta = McMeta(units, class_start, masks)
     mc_frame(gpu, cur, refs, meta)
     torch.cuda.synchronize()
     ref_np = [[r.buffer_np(p) for p in range(len(r.planes))] for r in refs]
@@ -66,9 +66,28 @@ def test_mc_unit_shapes(gpu, shape):
     w, h, bpc = 256, 256, 10
     rng = np.random.default_rng(uw * 131 + uh)
     refs = make_refs(w, h, bpc, 0, 2, rng)
-    units = make_mc_grid_units(w, h, uw, uh, 0, rng)
-    ps = np.array([0, len(units), len(units), len(units)], np.uint32)
-    run_case(gpu, w, h, bpc, 0, units, ps, np.zeros(1, np.uint8), refs, rng)
+    units, cs = make_mc_grid_units(w, h, uw, uh, 0, rng)
+    run_case(gpu, w, h, bpc, 0, units, cs, np.zeros(1, np.uint8), refs, rng)
+
+
+@pytest.mark.parametrize("layout", [1, 2])
+def test_mc_chroma_small_shapes(gpu, layout):
+    """Chroma-sized units (2xN / Nx2 under 4:2:0 / 4:2:2) mixed in one frame's chroma group."""
+    w, h, bpc = 128, 128, 8
+    rng = np.random.default_rng(11 + layout)
+    refs = make_refs(w, h, bpc, layout, 2, rng)
+    cw, ch = w >> 1, h >> (layout == 1)
+    parts = [make_mc_grid_units(cw, ch // 4, uw, uh, pl, rng)[0] for pl in (1, 2)
+             for (uw, uh) in [(2, 2), (4, 2)]]
+    # stack the grids in disjoint row bands of the chroma planes
+    from rav1d_amd.synth import mc_sort_units
+    allu = []
+    for k, u in enumerate(parts):
+        u = u.copy()
+        u["y"] += (k % 2) * (ch // 4)
+        allu.append(u)
+    units, cs = mc_sort_units(np.concatenate(allu))
+    run_case(gpu, w, h, bpc, layout, units, cs, np.zeros(1, np.uint8), refs, rng)
 
 
 def test_mc_4k10_matches_oracle(gpu):

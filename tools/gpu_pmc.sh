@@ -15,7 +15,7 @@ for P in "FETCH_SIZE" "WRITE_SIZE" \
          "SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $OUT/$TAG/p$i -o p -- \
-      python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/$TAG/p$i.log 2>&1 \
+      python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-fg > $OUT/$TAG/p$i.log 2>&1 \
       || { echo "pass $i failed"; tail -20 $OUT/$TAG/p$i.log; exit 1; }
 done
 python3 $R/tools/pmc_summary.py $OUT/$TAG > $OUT/$TAG/summary.txt && cat $OUT/$TAG/summary.txt
