@@ -25,8 +25,19 @@ __constant__ int8_t k_subpel[6][15][8] = {
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kMaxU = 8;           // units packed per wave (bounds the LDS windows)
-constexpr int kWinElems = 2240;    // per reference: max over classes of U * (rows+7) * (cols+8) (4x16: 2208)
+constexpr int kMaxU = 8;           // units packed per wave
+#ifndef MC_STAGE_BATCH
+#define MC_STAGE_BATCH 8
+#endif
+constexpr int kStageBatch = MC_STAGE_BATCH;   // window loads in flight per lane before their LDS stores
+constexpr int kWinElems = 2240;    // window budget (elements), 4x16 units: 8 x 23 x 12 = 2208
+
+// units per wave for a class whose unit needs `lanes` lanes and a (TR+7) x (TW+8) window
+__host__ __device__ __forceinline__ int units_per_wave(int lanes, int wn) {
+    int u = 64 / lanes;
+    u = u < kMaxU ? u : kMaxU;
+    return u < kWinElems / wn ? u : kWinElems / wn;
+}
 
 // filter2d (Filter2d, horizontal/vertical order) -> subpel filter type (0 regular, 1 smooth, 2 sharp)
 __device__ __forceinline__ int f2d_type_h(int f) { return (int)((0x111222000ull >> (4 * f)) & 15); }
@@ -47,9 +58,9 @@ __device__ __forceinline__ ClassGeom class_geom(int c) {
     g.R = min(g.h, 8);
     g.lanes_u = g.TW * (g.h / g.R);
     if (g.lanes_u <= 64) {
-        g.U = min(64 / g.lanes_u, kMaxU);
         g.T = 1;
         g.TR = g.h;
+        g.U = units_per_wave(g.lanes_u, (g.TR + 7) * (g.TW + 8));
         g.ctiles = 1;
     } else {
         g.U = 1;
@@ -72,27 +83,27 @@ struct RefSel {
     int iw, ih, dx, dy, mx, my;
 };
 
-template <typename Px, bool PREP>
+// One reference's prediction for this lane's column and R rows (put: pixels, PREP: the int16
+// intermediate of mct). All four cases of put/prep_8tap_c and put/prep_bilin_c (2-D, h only,
+// v only, copy) run as the 2-D filter: a missing direction gets the identity tap 1 << SH at
+// the centre, and every shift on the identity side is exact, e.g. h only, put:
+// ((mid << SH) + 2^(SH+ib-1)) >> (SH+ib) == (mid + 2^(ib-1)) >> ib. No lane diverges.
+template <bool PREP>
 __device__ __forceinline__ void predict(const McArgs &a, const int16_t *win, int WS, const RefSel &s, int f2d,
                                         int w, int h, int col, int r0, int R, int out[8]) {
     const bool bilin = f2d == 9;
-    const int SH = bilin ? 4 : 6, ib = a.ib;
-    int fh[8] = { 0, 0, 0, 0, 0, 0, 0, 0 }, fv[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
-    if (s.mx) {
-        if (bilin) { fh[3] = 16 - s.mx; fh[4] = s.mx; }
-        else {
-            const int t = f2d_type_h(f2d), row = w > 4 ? t : 3 + (t & 1);
+    const int SH = bilin ? 4 : 6, ib = a.ib, one = 1 << SH;
+    const int th = f2d_type_h(f2d), tv = f2d_type_v(f2d);
+    const int8_t *ph = k_subpel[w > 4 ? th : 3 + (th & 1)][max(s.mx, 1) - 1];
+    const int8_t *pv = k_subpel[h > 4 ? tv : 3 + (tv & 1)][max(s.my, 1) - 1];
+    int fh[8], fv[8];
 #pragma unroll
-            for (int k = 0; k < 8; k++) fh[k] = k_subpel[row][s.mx - 1][k];
-        }
-    }
-    if (s.my) {
-        if (bilin) { fv[3] = 16 - s.my; fv[4] = s.my; }
-        else {
-            const int t = f2d_type_v(f2d), row = h > 4 ? t : 3 + (t & 1);
-#pragma unroll
-            for (int k = 0; k < 8; k++) fv[k] = k_subpel[row][s.my - 1][k];
-        }
+    for (int k = 0; k < 8; k++) {
+        const int id = k == 3 ? one : 0;
+        const int bh = k == 3 ? 16 - s.mx : k == 4 ? s.mx : 0;
+        const int bv = k == 3 ? 16 - s.my : k == 4 ? s.my : 0;
+        fh[k] = bilin ? bh : s.mx ? (int)ph[k] : id;
+        fv[k] = bilin ? bv : s.my ? (int)pv[k] : id;
     }
     // horizontal taps as 5 aligned pairs: even column (f0,f1)..(f6,f7),(0,0); odd column
     // starts one sample left: (0,f0),(f1,f2),..,(f7,0)
@@ -106,61 +117,30 @@ __device__ __forceinline__ void predict(const McArgs &a, const int16_t *win, int
     }
     const uint32_t *wrow = reinterpret_cast<const uint32_t *>(win + r0 * WS + (col & ~1));
     const int WS2 = WS >> 1;
-    auto hsum = [&](int rr) {
+    const int hsh = SH - ib, hrnd = (1 << hsh) >> 1;
+    auto hmid = [&](int rr) {
         const uint32_t *p = wrow + rr * WS2;
-        int s2 = 0;
+        int s2 = hrnd;
 #pragma unroll
         for (int j = 0; j < 5; j++)
             s2 = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, p[j]), __builtin_bit_cast(s16x2, hp[j]), s2, false);
-        return s2;
+        return s2 >> hsh;
     };
-    auto center = [&](int rr) { return (int)win[(r0 + rr) * WS + col + 3]; };
-    const int hsh = SH - ib, hrnd = (1 << hsh) >> 1;
-    if (s.mx && s.my) {
-        int v[8];
+    const int vsh = PREP ? SH : SH + ib, vrnd = (1 << vsh) >> 1;
+    int v[8];
 #pragma unroll
-        for (int t = 0; t < 7; t++) v[t] = (hsum(t) + hrnd) >> hsh;
+    for (int t = 0; t < 7; t++) v[t] = hmid(t);
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-            if (q < R) {
-                v[7] = (hsum(q + 7) + hrnd) >> hsh;
-                int sum = 0;
+    for (int q = 0; q < 8; q++) {
+        if (q < R) {
+            v[7] = hmid(q + 7);
+            int sum = vrnd;
 #pragma unroll
-                for (int t = 0; t < 8; t++) sum += fv[t] * v[t];
-                out[q] = PREP ? ((sum + ((1 << SH) >> 1)) >> SH) - a.bias
-                              : min(max((sum + ((1 << (SH + ib)) >> 1)) >> (SH + ib), 0), a.bdmax);
+            for (int t = 0; t < 8; t++) sum += fv[t] * v[t];
+            out[q] = PREP ? (sum >> vsh) - a.bias : min(max(sum >> vsh, 0), a.bdmax);
 #pragma unroll
-                for (int t = 0; t < 7; t++) v[t] = v[t + 1];
-            }
+            for (int t = 0; t < 7; t++) v[t] = v[t + 1];
         }
-    } else if (s.mx) {
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            if (q < R) {
-                const int px = (hsum(q + 3) + hrnd) >> hsh;
-                out[q] = PREP ? px - a.bias : min(max((px + ((1 << ib) >> 1)) >> ib, 0), a.bdmax);
-            }
-        }
-    } else if (s.my) {
-        int v[8];
-#pragma unroll
-        for (int t = 0; t < 7; t++) v[t] = center(t);
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            if (q < R) {
-                v[7] = center(q + 7);
-                int sum = 0;
-#pragma unroll
-                for (int t = 0; t < 8; t++) sum += fv[t] * v[t];
-                out[q] = PREP ? ((sum + hrnd) >> hsh) - a.bias : min(max((sum + ((1 << SH) >> 1)) >> SH, 0), a.bdmax);
-#pragma unroll
-                for (int t = 0; t < 7; t++) v[t] = v[t + 1];
-            }
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < 8; q++)
-            if (q < R) out[q] = PREP ? (center(q + 3) << ib) - a.bias : center(q + 3);
     }
 }
 
@@ -216,24 +196,36 @@ __global__ __launch_bounds__(64) void mc_kernel(McArgs a, int g) {
         rs[i].dy = b.y + (mvy >> (3 + ssv)) + ty0 - 3;
     }
 
-    // stage windows: rows TR + 7, cols TW + 7 (row stride WS = TW + 8, even)
+    // stage the references' windows: rows TR + 7, cols TW + 7 (row stride WS = TW + 8, even),
+    // flattened over the unit's staging lanes, kStageBatch loads in flight per lane before
+    // their LDS stores; both references of a compound unit are staged before one barrier.
     const int WC = G.TW + 7, WR = G.TR + 7, WS = G.TW + 8, WN = WR * WS;
-    const uint32_t inv = (1u << 20) / WC + 1;          // (e * inv) >> 20 == e / WC for e < 2^20 / WC^2
-    if (active) {
+    const uint32_t inv = (1u << 20) / WC + 1;      // (e * inv) >> 20 == e / WC for e < 2^20 / WC^2
+    auto stage = [&](const RefSel &r, int16_t *buf) {
+        if (!active) return;
         const int li = G.T == 1 ? lane - uu * G.lanes_u : lane;
         const int nl = G.T == 1 ? G.lanes_u : 64;
+        const int NE = WR * WC;
+        int16_t *wdst = buf + uu * WN;
+        for (int e0 = li; e0 < NE; e0 += kStageBatch * nl) {
+            int v[kStageBatch], o[kStageBatch];
 #pragma unroll
-        for (int i = 0; i < 2; i++) {
-            if (i >= nref) break;
-            int16_t *wdst = win[i] + uu * WN;
-            for (int e = li; e < WR * WC; e += nl) {
-                const int rr = (int)(((uint32_t)e * inv) >> 20), cc = e - rr * WC;
-                const int yy = min(max(rs[i].dy + rr, 0), rs[i].ih - 1);
-                const int xx = min(max(rs[i].dx + cc, 0), rs[i].iw - 1);
-                wdst[rr * WS + cc] = (int16_t)ldpx<Px>(rs[i].base, rs[i].stride, yy, xx);
+            for (int k = 0; k < kStageBatch; k++) {
+                const int e = e0 + k * nl;
+                const int ec = e < NE ? e : li;
+                const int rr = (int)(((uint32_t)ec * inv) >> 20), cc = ec - rr * WC;
+                const int yy = min(max(r.dy + rr, 0), r.ih - 1);
+                const int xx = min(max(r.dx + cc, 0), r.iw - 1);
+                v[k] = ldpx<Px>(r.base, r.stride, yy, xx);
+                o[k] = e < NE ? rr * WS + cc : -1;
             }
+#pragma unroll
+            for (int k = 0; k < kStageBatch; k++)
+                if (o[k] >= 0) wdst[o[k]] = (int16_t)v[k];
         }
-    }
+    };
+    stage(rs[0], win[0]);
+    if (nref == 2) stage(rs[1], win[1]);
     __syncthreads();
     if (!active) return;
 
@@ -243,14 +235,14 @@ __global__ __launch_bounds__(64) void mc_kernel(McArgs a, int g) {
     uint8_t *dst = a.dst[p] + (int64_t)(b.y + ty0 + r0) * ds;
     const int x = b.x + tx0 + col;
     if (nref == 1) {
-        predict<Px, false>(a, win[0] + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
+        predict<false>(a, win[0] + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
 #pragma unroll
         for (int q = 0; q < 8; q++)
             if (q < R) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];
         return;
     }
-    predict<Px, true>(a, win[0] + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
-    predict<Px, true>(a, win[1] + uu * WN, WS, rs[1], b.filter2d, b.w, b.h, col, r0, R, o1);
+    predict<true>(a, win[0] + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
+    predict<true>(a, win[1] + uu * WN, WS, rs[1], b.filter2d, b.w, b.h, col, r0, R, o1);
     const int ib = a.ib, sign = b.param >> 7;
     if (b.comp == MI_MC_SEG) {
         // w_mask (mc_tmpl.c:661-712): per-pixel weight from |t1 - t2|, t1 = tmp[sign]
@@ -316,10 +308,12 @@ int mc_plan(McArgs &a, int g) {
         const int w = 1 << lw, h = 1 << lh;
         const int TW = w < 64 ? w : 64, R = h < 8 ? h : 8, lanes = TW * (h / R);
         if (lanes <= 64) {
-            const int U = 64 / lanes < kMaxU ? 64 / lanes : kMaxU;
+            const int U = units_per_wave(lanes, (h + 7) * (TW + 8));
+            if (U < 1) return -1;                           // shape outside AV1's (aspect > 8:1)
             waves += (n + U - 1) / U;
         } else {
             const int TR = (64 / TW) * R;
+            if ((TR + 7) * (TW + 8) > kWinElems) return -1;
             waves += n * (uint32_t)((w / TW) * (h / TR));
         }
     }
