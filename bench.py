@@ -76,6 +76,8 @@ class Pipeline:
         }
         if self.mc is not None:
             self.algo["mc"] = mc_algorithmic_bytes(fr["mc"][0], bpc) + fr["mc"][2].nbytes
+        # kernel launches per stage per frame: mc = luma + chroma group, deblock = cols + rows
+        self.launches = {"mc": 2, "itx": 1, "deblock": 2, "cdef": 1, "lr": 1, "fg": 1}
         self.kernels = {"mc": "mc_kernel", "itx": "itx_frame_kernel", "deblock": "lf_cols_kernel+lf_rows_kernel",
                         "cdef": "cdef_kernel", "lr": "lr_kernel", "fg": "fg_apply_kernel"}
 
@@ -160,6 +162,17 @@ def film_grain_8k(ctx, stream, reps=20):
     fb = frame_bytes(w, h, bpc, 1)
     return dict(mpx_per_s=round(w * h / (apply_ms / 1e3) / 1e6, 1), apply_ms=round(apply_ms, 4),
                 prep_ms=round(prep_ms, 4), apply_gbs=round(2 * fb / (apply_ms / 1e3) / 1e9, 1))
+
+
+def pmc_traffic(stage):
+    """HBM bytes per step of `stage` from the committed PMC run (profiles/r01_traffic.json,
+    written by tools/traffic_json.py from tools/gpu_pmc.sh's FETCH_SIZE / WRITE_SIZE passes of
+    this same bench command, calibrated per access width by tools/pmc_calib). None if absent."""
+    path = os.path.join(ROOT, "profiles", "r01_traffic.json")
+    if not os.path.exists(path):
+        return None
+    ent = json.load(open(path)).get("stages", {}).get(stage)
+    return None if ent is None else ent.get("hbm_bytes_per_step")
 
 
 def cpu_baseline(fr, budget_s=20.0):
@@ -252,8 +265,8 @@ def main():
             "stage_gbs": {k: round(pipe.algo[k] / (stage_ms[k] / 1e3) / 1e9, 1) for k in stage_ms if k in pipe.algo},
             "roofline": {"kernel": pipe.kernels[dom], "stage": dom, "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "algo_bytes_per_launch": pipe.algo[dom]},
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom),
+                         "algo_bytes_per_step": pipe.algo[dom], "launches_per_step": pipe.launches[dom]},
         }
         if world == 1 and not args.no_fg:
             out["film_grain_8k10"] = film_grain_8k(ctx, stream)

@@ -161,6 +161,26 @@ typedef struct MiMcBlock {
                                the chroma resolution, (w >> ss_hor) * (h >> ss_ver)) */
 } MiMcBlock;
 
+/* One intra-predicted block (24 bytes) for the batched intra entry. Mode = the reference's
+ * intra_pred[] slot (src/levels.rs IntraPredMode implementation modes: 0 DC, 1 V, 2 H,
+ * 3 LEFT_DC, 4 TOP_DC, 5 DC_128, 6 Z1, 7 Z2, 8 Z3, 9 SMOOTH, 10 SMOOTH_V, 11 SMOOTH_H,
+ * 12 PAETH, 13 FILTER), MI_IPRED_CFL + dc slot for cfl_pred, or MI_IPRED_PAL for pal_pred. */
+#define MI_IPRED_CFL 32   /* + 0 DC, 3 LEFT_DC, 4 TOP_DC, 5 DC_128 (cfl_pred[], ipred.rs:236) */
+#define MI_IPRED_PAL 64   /* palette (8 pixels) at edge_off, indices (w*h bytes) at idx + aux_off */
+typedef struct MiIpredBlock {
+    uint32_t edge_off;      /* pixel index of the topleft sample in the edge buffer */
+    uint32_t aux_off;       /* CfL: int16 index into ac (w*h entries); PAL: byte index into idx */
+    uint16_t x, y;          /* destination, plane pixels */
+    uint8_t  w, h;          /* 4..64 (FILTER <= 32) */
+    uint8_t  plane;
+    uint8_t  mode;
+    uint16_t angle;         /* the intra_pred `angle` argument: angle | is_sm << 9 | edge filter << 10,
+                               or the filter index for FILTER (ipred.rs:48-58, 866-868) */
+    uint16_t max_w, max_h;  /* max_width / max_height (Z2 edge-filter limits) */
+    int8_t   alpha;         /* CfL alpha */
+    uint8_t  pad;
+} MiIpredBlock;
+
 /* ------------------------------------------------------------------------------------ */
 /* Context                                                                               */
 /* ------------------------------------------------------------------------------------ */
@@ -191,6 +211,14 @@ const char *mi_version(void);
 int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
                  const uint32_t size_start[MI_N_RECT_TX_SIZES + 1], void *coef,
                  unsigned flags, void *stream);
+
+/* Intra prediction of n independent blocks (one wavefront step of a frame, or any set of
+ * blocks whose edges are final): writes each block into `pic` from its gathered edges
+ * (rav1d_prepare_intra_edges output, src/ipred_prepare.rs:118-204). `blocks`, `edges`
+ * (pixels of pic's bit depth), `ac` (int16) and `idx` (bytes) are device arrays; ac / idx may
+ * be NULL when no CfL / palette block is present. */
+int mi_ipred_blocks(MiCtx *ctx, const MiPicture *pic, const MiIpredBlock *blocks, int n,
+                    const void *edges, const int16_t *ac, const uint8_t *idx, void *stream);
 
 /* Deblock a whole frame in place: all column edges (every plane), then all row edges.
  * Equivalent to the reference's per-sbrow cols/rows interleaving;
@@ -245,6 +273,12 @@ int mi_film_grain_apply(MiCtx *ctx, const MiPicture *in, const MiPicture *out,
  * (the reference's fn returns void; a non-zero return here means nothing was written). */
 int mi_dsp_itxfm_add(int tx, int txtp, void *dst, ptrdiff_t stride, void *coeff, int eob,
                      int bitdepth_max);
+
+/* intra_pred[mode] (src/ipred.rs:48-58; C src/ipred.h:47-53) on one block: topleft points
+ * into the caller's edge buffer (samples topleft[-(w+h)] .. topleft[w+h] are read). Host or
+ * device pointers; synchronous. Replaces ipred_*_rust / dav1d_ipred_*_<bpc>bpc_<isa>. */
+int mi_dsp_intra_pred(int mode, void *dst, ptrdiff_t stride, const void *topleft, int w, int h,
+                      int angle, int max_width, int max_height, int bitdepth_max);
 
 #ifdef __cplusplus
 }

@@ -70,6 +70,18 @@ void oracle_mc_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layo
                      void *const *const refs, const ptrdiff_t *ref_strides, const int *ref_wh,
                      const void *blocks, int n, uint8_t *masks);
 
+/* ---- ipred (src/ipred.rs; C twin src/ipred_tmpl.c) ---- */
+/* mode = intra_pred[] slot: 0 DC,1 V,2 H,3 LEFT_DC,4 TOP_DC,5 DC_128,6 Z1,7 Z2,8 Z3,9 SMOOTH,
+ * 10 SMOOTH_V,11 SMOOTH_H,12 PAETH,13 FILTER; `angle` carries is_sm (bit 9) and the edge-filter
+ * enable (bit 10) for Z1-Z3, the filter index for FILTER. */
+void oracle_intra_pred(int mode, void *dst, ptrdiff_t stride, const void *topleft, int w, int h,
+                       int angle, int max_w, int max_h, int bpc);
+void oracle_cfl_ac(int16_t *ac, const void *ypx, ptrdiff_t stride, int w_pad, int h_pad, int cw, int ch,
+                   int ss_hor, int ss_ver, int bpc);
+void oracle_cfl_pred(int mode, void *dst, ptrdiff_t stride, const void *topleft, int w, int h,
+                     const int16_t *ac, int alpha, int bpc);
+void oracle_pal_pred(void *dst, ptrdiff_t stride, const void *pal, const uint8_t *idx, int w, int h, int bpc);
+
 #ifdef __cplusplus
 }
 #endif

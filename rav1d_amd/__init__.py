@@ -66,6 +66,12 @@ MCBLOCK_DTYPE = np.dtype([("x", "<u2"), ("y", "<u2"), ("w", "u1"), ("h", "u1"), 
                           ("filter2d", "u1"), ("mvx", "<i2", 2), ("mvy", "<i2", 2), ("ref", "i1", 2),
                           ("comp", "u1"), ("param", "u1"), ("mask_off", "<u4")])
 assert MCBLOCK_DTYPE.itemsize == 24
+IPRED_DTYPE = np.dtype([("edge_off", "<u4"), ("aux_off", "<u4"), ("x", "<u2"), ("y", "<u2"), ("w", "u1"),
+                        ("h", "u1"), ("plane", "u1"), ("mode", "u1"), ("angle", "<u2"), ("max_w", "<u2"),
+                        ("max_h", "<u2"), ("alpha", "i1"), ("pad", "u1")])
+assert IPRED_DTYPE.itemsize == 24
+IPRED_CFL, IPRED_PAL = 32, 64
+
 MC_AVG, MC_WAVG, MC_MASK, MC_SEG = 0, 1, 2, 3
 MC_NCLASS = 64
 
@@ -100,6 +106,8 @@ def lib():
          [ctypes.c_int, ctypes.c_int, _VP, ctypes.c_ssize_t, _VP, ctypes.c_int, ctypes.c_int])
     _sig(L, "mi_mc_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture), ctypes.c_int,
                                           _VP, ctypes.POINTER(ctypes.c_uint32), _VP, _VP])
+    _sig(L, "mi_ipred_blocks", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.c_int, _VP, _VP, _VP, _VP])
+    _sig(L, "mi_dsp_intra_pred", ctypes.c_int, [ctypes.c_int, _VP, ctypes.c_ssize_t, _VP] + [ctypes.c_int] * 6)
     _sig(L, "mi_deblock_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiLoopFilter), _VP])
     _sig(L, "mi_cdef_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
                                             ctypes.POINTER(MiCdef), _VP])
@@ -115,9 +123,9 @@ def lib():
 
 # Every symbol include/mi_av1dsp.h declares (checked by tests/test_abi.py).
 EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
-            "mi_itx_frame", "mi_mc_frame", "mi_deblock_frame", "mi_cdef_frame", "mi_lr_frame",
+            "mi_itx_frame", "mi_mc_frame", "mi_ipred_blocks", "mi_deblock_frame", "mi_cdef_frame", "mi_lr_frame",
             "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply",
-            "mi_dsp_itxfm_add"]
+            "mi_dsp_itxfm_add", "mi_dsp_intra_pred"]
 
 
 def check(rc, what):

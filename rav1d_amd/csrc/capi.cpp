@@ -160,6 +160,26 @@ int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nre
     return r ? fail(ctx, -EIO) : 0;
 }
 
+int mi_ipred_blocks(MiCtx *ctx, const MiPicture *pic, const MiIpredBlock *blocks, int n,
+                    const void *edges, const int16_t *ac, const uint8_t *idx, void *stream) {
+    if (!ctx || !pic || n < 0) return fail(ctx, -EINVAL);
+    if (pic->bpc != 8 && pic->bpc != 10 && pic->bpc != 12) return fail(ctx, -EINVAL);
+    if (!n) return 0;
+    if (!blocks || !edges) return fail(ctx, -EINVAL);
+    mi::IpredArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int p = 0; p < 3; p++) a.dst[p] = (uint8_t *)pic->data[p];
+    a.stride[0] = pic->stride[0];
+    a.stride[1] = pic->stride[1];
+    a.blocks = blocks;
+    a.edges = (const uint8_t *)edges;
+    a.ac = ac;
+    a.idx = idx;
+    a.bpc = pic->bpc;
+    a.bdmax = (1 << pic->bpc) - 1;
+    return mi::launch_ipred(a, n, (hipStream_t)stream) ? fail(ctx, -EIO) : 0;
+}
+
 int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, void *stream) {
     if (!ctx || !pic || !lf) return fail(ctx, -EINVAL);
     if (pic->bpc != 8 && pic->bpc != 10 && pic->bpc != 12) return fail(ctx, -EINVAL);
@@ -432,6 +452,59 @@ int mi_dsp_itxfm_add(int tx, int txtp, void *dst, ptrdiff_t stride, void *coeff,
     if (hipStreamSynchronize(s) != hipSuccess) return -EIO;
     if (!dst_dev)
         for (int y = 0; y < d.h; y++) memcpy((uint8_t *)dst + y * stride, &hpix[y * row_bytes], row_bytes);
+    return 0;
+}
+
+int mi_dsp_intra_pred(int mode, void *dst, ptrdiff_t stride, const void *topleft, int w, int h,
+                      int angle, int max_width, int max_height, int bitdepth_max) {
+    if (mode < 0 || mode > 13 || !dst || !topleft || w < 4 || h < 4 || w > 64 || h > 64 ||
+        (w & (w - 1)) || (h & (h - 1)) || (mode == 13 && (w > 32 || h > 32)))
+        return -EINVAL;
+    const int bpc = bitdepth_max == 255 ? 8 : bitdepth_max == 1023 ? 10 : bitdepth_max == 4095 ? 12 : 0;
+    if (!bpc) return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    if (hipSetDevice(0) != hipSuccess) return -ENODEV;
+    const int px = bpc == 8 ? 1 : 2;
+    const size_t row_bytes = (size_t)w * px;
+    hipStream_t s = g_call.stream;
+    // device scratch: [pixels 64 rows x 128 B][edge 257 samples][descriptor]
+    uint8_t *dpix = g_call.scratch;
+    uint8_t *dedge = dpix + 64 * 128;
+    MiIpredBlock *dblk = (MiIpredBlock *)(dedge + 1024);
+    const int ext = w + h;                      // samples read on each side of topleft
+    const uint8_t *esrc = (const uint8_t *)topleft - (ptrdiff_t)ext * px;
+    const hipMemcpyKind ek = is_device_ptr(topleft) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (hipMemcpyAsync(dedge, esrc, (size_t)(2 * ext + 1) * px, ek, s) != hipSuccess) return -EIO;
+    MiIpredBlock hb{};
+    hb.edge_off = (uint32_t)ext;
+    hb.w = (uint8_t)w;
+    hb.h = (uint8_t)h;
+    hb.mode = (uint8_t)mode;
+    hb.angle = (uint16_t)angle;
+    hb.max_w = (uint16_t)max_width;
+    hb.max_h = (uint16_t)max_height;
+    if (hipMemcpyAsync(dblk, &hb, sizeof(hb), hipMemcpyHostToDevice, s) != hipSuccess) return -EIO;
+    mi::IpredArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int p = 0; p < 3; p++) a.dst[p] = dpix;
+    a.stride[0] = a.stride[1] = (int64_t)row_bytes;
+    a.blocks = dblk;
+    a.edges = dedge;
+    a.bpc = bpc;
+    a.bdmax = bitdepth_max;
+    if (mi::launch_ipred(a, 1, s)) return -EIO;
+    const bool dst_dev = is_device_ptr(dst);
+    std::vector<uint8_t> hpix(dst_dev ? 0 : row_bytes * h);
+    for (int y = 0; y < h; y++) {
+        const hipError_t e = dst_dev
+            ? hipMemcpyAsync((uint8_t *)dst + y * stride, dpix + y * row_bytes, row_bytes, hipMemcpyDeviceToDevice, s)
+            : hipMemcpyAsync(&hpix[y * row_bytes], dpix + y * row_bytes, row_bytes, hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) return -EIO;
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) return -EIO;
+    if (!dst_dev)
+        for (int y = 0; y < h; y++) memcpy((uint8_t *)dst + y * stride, &hpix[y * row_bytes], row_bytes);
     return 0;
 }
 

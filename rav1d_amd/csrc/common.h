@@ -109,6 +109,18 @@ struct McArgs {
 int mc_plan(McArgs &a, int g);
 int launch_mc(const McArgs &a, int g, int waves, hipStream_t s);
 
+struct IpredArgs {
+    uint8_t *dst[3];
+    int64_t stride[2];
+    const MiIpredBlock *blocks;
+    const uint8_t *edges;
+    const int16_t *ac;
+    const uint8_t *idx;
+    int bpc, bdmax;
+};
+// launchers (ipred.hip)
+int launch_ipred(const IpredArgs &a, int n, hipStream_t s);
+
 struct LrArgs {
     const uint8_t *src[3];        // CDEF output C
     const uint8_t *lpf[3];        // deblocked D (rows across stripe edges)

@@ -186,3 +186,51 @@ def mc_frame(cur_planes, ref_frames, bpc, layout, w, h, units, masks):
     o.oracle_mc_frame(cp, cs, layout, bpc, rp, rs, rwh, ptr(u), len(u), ptr(m))
     n = 3 if layout else 1
     return cur[:n], m
+
+
+def _ipred_sigs(o):
+    if getattr(o, "_ipred_ready", False):
+        return
+    o.oracle_intra_pred.argtypes = [ctypes.c_int, _VP, ctypes.c_ssize_t, _VP] + [ctypes.c_int] * 6
+    o.oracle_cfl_pred.argtypes = [ctypes.c_int, _VP, ctypes.c_ssize_t, _VP, ctypes.c_int, ctypes.c_int, _VP,
+                                  ctypes.c_int, ctypes.c_int]
+    o.oracle_cfl_ac.argtypes = [_VP, _VP, ctypes.c_ssize_t] + [ctypes.c_int] * 7
+    o.oracle_pal_pred.argtypes = [_VP, ctypes.c_ssize_t, _VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    for n in ("oracle_intra_pred", "oracle_cfl_pred", "oracle_cfl_ac", "oracle_pal_pred"):
+        getattr(o, n).restype = None
+    o._ipred_ready = True
+
+
+def intra_pred(mode, edges, tl_index, w, h, angle, max_w, max_h, bpc):
+    """Oracle intra_pred[mode] on a 1-D edge array (pixels) with topleft at tl_index."""
+    o = load_oracle()
+    _ipred_sigs(o)
+    dt = np.uint8 if bpc == 8 else np.uint16
+    e = np.ascontiguousarray(edges, dtype=dt)
+    dst = np.zeros((h, w), dt)
+    o.oracle_intra_pred(mode, ptr(dst), dst.strides[0], ctypes.c_void_p(e.ctypes.data + tl_index * e.itemsize),
+                        w, h, angle, max_w, max_h, bpc)
+    return dst
+
+
+def cfl_pred(mode, edges, tl_index, w, h, ac, alpha, bpc):
+    o = load_oracle()
+    _ipred_sigs(o)
+    dt = np.uint8 if bpc == 8 else np.uint16
+    e = np.ascontiguousarray(edges, dtype=dt)
+    dst = np.zeros((h, w), dt)
+    a = np.ascontiguousarray(ac, dtype=np.int16)
+    o.oracle_cfl_pred(mode, ptr(dst), dst.strides[0], ctypes.c_void_p(e.ctypes.data + tl_index * e.itemsize),
+                      w, h, ptr(a), alpha, bpc)
+    return dst
+
+
+def pal_pred(pal, idx, w, h, bpc):
+    o = load_oracle()
+    _ipred_sigs(o)
+    dt = np.uint8 if bpc == 8 else np.uint16
+    p = np.ascontiguousarray(pal, dtype=dt)
+    i = np.ascontiguousarray(idx, dtype=np.uint8)
+    dst = np.zeros((h, w), dt)
+    o.oracle_pal_pred(ptr(dst), dst.strides[0], ptr(p), ptr(i), w, h, bpc)
+    return dst

@@ -1,0 +1,96 @@
+"""Oracle self-checks for intra prediction (CPU only): oracle/ipred.c against an independent
+numpy restatement of ipred_tmpl.c for the non-directional modes and CfL / palette, and
+structural properties of the directional modes. Parity with the reference is unpinned
+(DESIGN.md §Oracle)."""
+import numpy as np
+import pytest
+
+from tests import oracle_lib
+
+SMW = None
+
+
+def sm_weights():
+    global SMW
+    if SMW is None:
+        import os
+        txt = open(os.path.join(oracle_lib.ROOT, "rav1d_amd", "csrc", "tables", "sm_weights.inc")).read()
+        SMW = np.array([int(v) for v in txt.split("*/", 1)[1].replace(",", " ").split()], np.int64)
+    return SMW
+
+
+def np_pred(mode, e, t, w, h, bpc):
+    top = e[t + 1:t + 1 + w].astype(np.int64)
+    left = e[t - h:t][::-1].astype(np.int64)       # left[i] = topleft[-(1+i)]
+    c = int(e[t])
+    X, Y = np.meshgrid(np.arange(w), np.arange(h))
+    if mode == 1:
+        return np.broadcast_to(top, (h, w))
+    if mode == 2:
+        return np.broadcast_to(left[:, None], (h, w))
+    if mode == 12:
+        T, L = top[X], left[Y]
+        base = L + T - c
+        ld, td, tld = abs(L - base), abs(T - base), abs(c - base)
+        return np.where((ld <= td) & (ld <= tld), L, np.where(td <= tld, T, c))
+    sw = sm_weights()
+    right, bottom = int(e[t + w]), int(e[t - h])
+    wv, wh = sw[h + Y], sw[w + X]
+    if mode == 9:
+        return (wv * top[X] + (256 - wv) * bottom + wh * left[Y] + (256 - wh) * right + 256) >> 9
+    if mode == 10:
+        return (wv * top[X] + (256 - wv) * bottom + 128) >> 8
+    if mode == 11:
+        return (wh * left[Y] + (256 - wh) * right + 128) >> 8
+    if mode in (0, 3, 4):
+        tsum, lsum = int(top.sum()), int(left.sum())
+        if mode == 4:
+            return np.full((h, w), (tsum + (w >> 1)) >> int(np.log2(w)))
+        if mode == 3:
+            return np.full((h, w), (lsum + (h >> 1)) >> int(np.log2(h)))
+        dc = (tsum + lsum + ((w + h) >> 1)) >> ((w + h) & -(w + h)).bit_length() - 1
+        if w != h:
+            q = w > 2 * h or h > 2 * w
+            dc = (dc * ((0x3334 if q else 0x5556) if bpc == 8 else (0x6667 if q else 0xAAAB))) >> (16 if bpc == 8 else 17)
+        return np.full((h, w), dc)
+    if mode == 5:
+        return np.full((h, w), 128 if bpc == 8 else (1 << (bpc - 1)))
+    raise ValueError(mode)
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+def test_oracle_nondirectional_match_numpy(bpc):
+    rng = np.random.default_rng(bpc)
+    for _ in range(300):
+        w, h = [4, 8, 16, 32, 64][rng.integers(0, 5)], [4, 8, 16, 32, 64][rng.integers(0, 5)]
+        if max(w, h) > 4 * min(w, h):
+            continue
+        mode = int(rng.choice([0, 1, 2, 3, 4, 5, 9, 10, 11, 12]))
+        e = rng.integers(0, 1 << bpc, size=2 * 130 + 1)
+        got = oracle_lib.intra_pred(mode, e, 130, w, h, 0, w, h, bpc)
+        assert np.array_equal(got.astype(np.int64), np_pred(mode, e, 130, w, h, bpc)), (mode, w, h)
+
+
+def test_oracle_z1_45_degrees_is_diagonal_copy():
+    """Z1 at 45 degrees without edge filtering: dst[y][x] = top[x + y + 1] (dx = 64)."""
+    rng = np.random.default_rng(1)
+    e = rng.integers(0, 1024, size=261)
+    got = oracle_lib.intra_pred(6, e, 130, 8, 8, 45, 8, 8, 10)
+    top = e[131:]
+    exp = np.array([[top[min(x + y + 1, 8 + 8 - 1)] for x in range(8)] for y in range(8)])
+    assert np.array_equal(got, exp)
+
+
+def test_oracle_cfl_and_palette():
+    rng = np.random.default_rng(2)
+    e = rng.integers(0, 1024, size=261)
+    ac = rng.integers(-2000, 2000, size=64).astype(np.int16)
+    for mode, alpha in ((0, 5), (3, -7), (4, 16), (5, -16)):
+        got = oracle_lib.cfl_pred(mode, e, 130, 8, 8, ac, alpha, 10).astype(np.int64)
+        dc = int(np_pred(mode, e, 130, 8, 8, 10)[0, 0])
+        diff = alpha * ac.astype(np.int64).reshape(8, 8)
+        exp = np.clip(dc + np.sign(diff) * ((abs(diff) + 32) >> 6), 0, 1023)
+        assert np.array_equal(got, exp)
+    pal = rng.integers(0, 1024, size=8)
+    idx = rng.integers(0, 8, size=32).astype(np.uint8)
+    assert np.array_equal(oracle_lib.pal_pred(pal, idx, 8, 4, 10), pal[idx].reshape(4, 8))

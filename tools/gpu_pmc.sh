@@ -10,9 +10,12 @@ mkdir -p $OUT/$TAG
 cd /tmp && export TMPDIR=/tmp
 [ -n "$LIST" ] && { timeout -k 10 120 rocprofv3 -L > $OUT/$TAG/counters_list.txt 2>&1 || true; }
 i=0
-for P in "FETCH_SIZE" "WRITE_SIZE" \
-         "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU" \
-         "SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+PASSES=("FETCH_SIZE" "WRITE_SIZE" \
+        "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU" \
+        "SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES GRBM_GUI_ACTIVE")
+# TRAFFIC_ONLY=1: just the two HBM byte passes
+[ -n "$TRAFFIC_ONLY" ] && PASSES=("FETCH_SIZE" "WRITE_SIZE")
+for P in "${PASSES[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $OUT/$TAG/p$i -o p -- \
       python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-fg > $OUT/$TAG/p$i.log 2>&1 \
