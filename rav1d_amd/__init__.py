@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librav1d_amd.so")
+LIB_PATH = os.environ.get("MI_LIB") or os.path.join(HERE, "librav1d_amd.so")
 
 _lib = None
 

@@ -11,12 +11,15 @@ from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-OUT = os.path.join(HERE, "librav1d_amd.so")
-BUILD = os.path.join(HERE, "build")
+# MI_BUILD_VARIANT=name builds an experiment variant (librav1d_amd_<name>.so, with
+# MI_EXTRA_FLAGS added) next to the product library; load it with MI_LIB=<path>.
+_VAR = os.environ.get("MI_BUILD_VARIANT", "")
+OUT = os.path.join(HERE, f"librav1d_amd_{_VAR}.so" if _VAR else "librav1d_amd.so")
+BUILD = os.path.join(HERE, f"build_{_VAR}" if _VAR else "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
-         "-I" + os.path.join(HERE, "..", "include")]
+         "-I" + os.path.join(HERE, "..", "include")] + os.environ.get("MI_EXTRA_FLAGS", "").split()
 
 
 def sources():

@@ -328,7 +328,8 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
     __shared__ int8_t bflag[64];          // bit0 luma filtered, bit1 chroma filtered
     __shared__ int16_t bpri[64];
 
-    const int tx = blockIdx.x % a.tiles_x, tyy = blockIdx.x / a.tiles_x;
+    const int bid = xcd_block(blockIdx.x, gridDim.x);
+    const int tx = bid % a.tiles_x, tyy = bid / a.tiles_x;
     const int x0 = tx * 64, y0 = tyy * 64;
     const MiAv1Filter *lf = &a.masks[(tyy >> 1) * a.sb128w + (tx >> 1)];
     const int cdef_idx = lf->cdef_idx[(tyy & 1) * 2 + (tx & 1)];

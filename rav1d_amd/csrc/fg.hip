@@ -47,39 +47,58 @@ __device__ void grain_fill(int16_t *buf, int gw, int gh, unsigned seed, int shif
     }
 }
 
-// Auto-regressive pass as a skewed wavefront. `lane_base` selects the lanes that own rows.
-__device__ void grain_ar(int16_t *buf, const int16_t *buf_y, int gw, int gh, const int8_t *coef,
-                         int lag, int shift, int gmin, int gmax, bool chroma, bool luma_term,
-                         int subx, int suby, int lane) {
-    const int skew = lag + 1;
+// Auto-regressive pass as a skewed wavefront: lane r owns row 3 + r; at step t it filters
+// column 3 + t - (LAG + 1) r, so every tap of the previous rows and columns is final. LAG is a
+// template parameter: the taps unroll into independent LDS reads at immediate offsets and the
+// coefficients sit in scalar registers, so a step costs one round of LDS latency + a barrier.
+template <int LAG, bool CHROMA>
+__device__ void grain_ar(int16_t *buf, const int16_t *buf_y, int gw, int gh, const int8_t *coef_g,
+                         int shift, int gmin, int gmax, bool luma_term, int subx, int suby, int lane) {
+    constexpr int NT = 2 * LAG * LAG + 2 * LAG;         // taps before the centre (generate_grain_*)
+    constexpr int skew = LAG + 1;
+    int coef[NT + 1];
+#pragma unroll
+    for (int i = 0; i <= NT; i++) coef[i] = coef_g[i];
     const int nrows = gh - 3, ncols = gw - 6;
     const int steps = ncols + skew * (nrows - 1);
+    const bool own = lane >= 0 && lane < nrows;
+    const int y = 3 + lane;
+    int lterm = 0;
     for (int t = 0; t < steps; t++) {
-        const int r = lane;
-        if (r >= 0 && r < nrows) {
-            const int x = 3 + t - skew * r, y = 3 + r;
-            if (x >= 3 && x < gw - 3) {
-                int sum = 0, ci = 0;
-                for (int dy = -lag; dy <= 0; dy++)
-                    for (int dx = -lag; dx <= lag; dx++) {
-                        if (!dx && !dy) {
-                            if (chroma && luma_term) {
-                                int l = 0;
-                                const int lx = ((x - 3) << subx) + 3, ly = ((y - 3) << suby) + 3;
-                                for (int i = 0; i <= suby; i++)
-                                    for (int j = 0; j <= subx; j++) l += buf_y[(ly + i) * kGW + lx + j];
-                                sum += round2i(l, subx + suby) * coef[ci];
-                            }
-                            dy = 1;   // leave both loops
-                            break;
-                        }
-                        sum += coef[ci++] * buf[(y + dy) * kGW + x + dx];
-                    }
-                const int g = buf[y * kGW + x] + round2i(sum, shift);
-                buf[y * kGW + x] = (int16_t)min(max(g, gmin), gmax);
+        const int x = 3 + t - skew * lane;
+        if (own && x >= 3 && x < gw - 3) {
+            const int16_t *p = buf + y * kGW + x;
+            int sum = 0, ci = 0;
+#pragma unroll
+            for (int dy = -LAG; dy <= 0; dy++)
+#pragma unroll
+                for (int dx = -LAG; dx <= LAG; dx++) {
+                    if (dy == 0 && dx == 0) break;
+                    sum += coef[ci++] * p[dy * kGW + dx];
+                }
+            if (CHROMA && luma_term) {
+                const int lx = ((x - 3) << subx) + 3, ly = ((y - 3) << suby) + 3;
+                const int16_t *q = buf_y + ly * kGW + lx;
+                lterm = q[0];
+                if (subx) lterm += q[1];
+                if (suby) { lterm += q[kGW]; if (subx) lterm += q[kGW + 1]; }
+                sum += round2i(lterm, subx + suby) * coef[NT];
             }
+            const int g = p[0] + round2i(sum, shift);
+            buf[y * kGW + x] = (int16_t)min(max(g, gmin), gmax);
         }
         __syncthreads();
+    }
+}
+
+template <bool CHROMA>
+__device__ void grain_ar_lag(int lag, int16_t *buf, const int16_t *buf_y, int gw, int gh, const int8_t *coef,
+                             int shift, int gmin, int gmax, bool luma_term, int subx, int suby, int lane) {
+    switch (lag) {
+    case 0: grain_ar<0, CHROMA>(buf, buf_y, gw, gh, coef, shift, gmin, gmax, luma_term, subx, suby, lane); break;
+    case 1: grain_ar<1, CHROMA>(buf, buf_y, gw, gh, coef, shift, gmin, gmax, luma_term, subx, suby, lane); break;
+    case 2: grain_ar<2, CHROMA>(buf, buf_y, gw, gh, coef, shift, gmin, gmax, luma_term, subx, suby, lane); break;
+    default: grain_ar<3, CHROMA>(buf, buf_y, gw, gh, coef, shift, gmin, gmax, luma_term, subx, suby, lane); break;
     }
 }
 
@@ -118,15 +137,15 @@ __global__ __launch_bounds__(256) void fg_prep_kernel(FgArgs a) {
     if (uv0) grain_fill(&lut[1][0][0], cw, chh, d.seed ^ 0xb524, shift);
     if (uv1) grain_fill(&lut[2][0][0], cw, chh, d.seed ^ 0x49d8, shift);
     __syncthreads();
-    grain_ar(&lut[0][0][0], nullptr, kGW, kGH, d.ar_coeffs_y, d.ar_coeff_lag, (int)d.ar_coeff_shift,
-             -gctr, gctr - 1, false, false, 0, 0, threadIdx.x);
+    grain_ar_lag<false>(d.ar_coeff_lag, &lut[0][0][0], nullptr, kGW, kGH, d.ar_coeffs_y, (int)d.ar_coeff_shift,
+                        -gctr, gctr - 1, false, 0, 0, threadIdx.x);
     // both chroma templates advance together: lanes 0..127 own U rows, 128..255 own V rows
     {
         const int pl = threadIdx.x >> 7;
         const bool on = pl ? uv1 : uv0;
-        grain_ar(&lut[1 + pl][0][0], &lut[0][0][0], cw, chh, d.ar_coeffs_uv[pl], d.ar_coeff_lag,
-                 (int)d.ar_coeff_shift, -gctr, gctr - 1, true, d.num_y_points != 0, a.ss_x, a.ss_y,
-                 on ? (threadIdx.x & 127) : -1);
+        grain_ar_lag<true>(d.ar_coeff_lag, &lut[1 + pl][0][0], &lut[0][0][0], cw, chh, d.ar_coeffs_uv[pl],
+                           (int)d.ar_coeff_shift, -gctr, gctr - 1, d.num_y_points != 0, a.ss_x, a.ss_y,
+                           on ? (threadIdx.x & 127) : -1);
     }
     // export templates
     for (int i = threadIdx.x; i < 3 * kGH * kGP; i += 256) {

@@ -111,7 +111,7 @@ template <typename Px>
 __global__ __launch_bounds__(256) void lf_cols_kernel(LfArgs a) {
     __shared__ uint8_t le[64], li[64];
     stage_lut(a, le, li);
-    const int b = blockIdx.x;
+    const int b = xcd_block(blockIdx.x, gridDim.x);
     const int p = b < a.blk_start[1] ? 0 : b < a.blk_start[2] ? 1 : 2;
     const int lb = b - a.blk_start[p];
     const int bx = (a.units_x[p] + 63) >> 6;
@@ -155,7 +155,7 @@ template <typename Px>
 __global__ __launch_bounds__(256) void lf_rows_kernel(LfArgs a) {
     __shared__ uint8_t le[64], li[64];
     stage_lut(a, le, li);
-    const int b = blockIdx.x;
+    const int b = xcd_block(blockIdx.x, gridDim.x);
     const int p = b < a.blk_start[1] ? 0 : b < a.blk_start[2] ? 1 : 2;
     const int lb = b - a.blk_start[p];
     const int bx = (a.units_x[p] + 63) >> 6;

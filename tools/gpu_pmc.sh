@@ -14,7 +14,7 @@ PASSES=("FETCH_SIZE" "WRITE_SIZE" \
         "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU" \
         "SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES GRBM_GUI_ACTIVE")
 # TRAFFIC_ONLY=1: just the two HBM byte passes
-[ -n "$TRAFFIC_ONLY" ] && PASSES=("FETCH_SIZE" "WRITE_SIZE")
+[ -n "$TRAFFIC_ONLY" ] && PASSES=("FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B")
 for P in "${PASSES[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $OUT/$TAG/p$i -o p -- \

@@ -11,9 +11,10 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 [ -x $R/tools/pmc_calib ] || { echo "tools/pmc_calib not built"; exit 1; }
-for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 180 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/calib_$C -o p -- \
-      $R/tools/pmc_calib > $OUT/calib_$C.log 2>&1 || { echo "calib $C failed"; tail -20 $OUT/calib_$C.log; exit 1; }
+for C in FETCH_SIZE WRITE_SIZE "TCC_EA0_RDREQ TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B"; do
+  D=${C%% *}
+  timeout -k 10 180 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/calib_$D -o p -- \
+      $R/tools/pmc_calib > $OUT/calib_$D.log 2>&1 || { echo "calib $D failed"; tail -20 $OUT/calib_$D.log; exit 1; }
 done
 echo "calibration done"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o p -- \

@@ -16,9 +16,9 @@ __global__ void rd(const T *__restrict__ src, size_t n, uint32_t *__restrict__ s
         const uint32_t *p = reinterpret_cast<const uint32_t *>(&v);
         if constexpr (sizeof(T) >= 4) {
 #pragma unroll
-            for (int k = 0; k < (int)(sizeof(T) / 4); k++) acc ^= p[k];
+            for (int k = 0; k < (int)(sizeof(T) / 4); k++) acc = acc * 31u + p[k];
         } else {
-            acc ^= (uint32_t)v;
+            acc = acc * 31u + (uint32_t)v;     // not a plain xor: keeps the test below reachable
         }
     }
     if (acc == 0x9E3779B9u) sink[threadIdx.x] = acc;  // never true for the zero-filled input

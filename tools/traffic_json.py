@@ -36,7 +36,7 @@ def calib(root):
             kind = "rd" if k.startswith("rd<") else "wr" if k.startswith("wr<") else None
             if kind is None or c not in d:
                 continue
-            t = k[3:].rstrip(">")
+            t = k[3:-1].strip()
             width = {"unsigned short": 2, "unsigned int": 4, "HIP_vector_type<unsigned int, 2u>": 8,
                      "HIP_vector_type<unsigned int, 4u>": 16, "uint2": 8, "uint4": 16}.get(t)
             if width is None:
@@ -46,14 +46,29 @@ def calib(root):
     return f
 
 
+def sized_bytes(d):
+    """Read bytes from the request-size counters: 32/64/128-B requests at their own size."""
+    if "TCC_EA0_RDREQ_128B" not in d:
+        return None
+    return 32 * d.get("TCC_EA0_RDREQ_32B", 0.0) + 64 * d.get("TCC_EA0_RDREQ_64B", 0.0) + 128 * d["TCC_EA0_RDREQ_128B"]
+
+
 def main():
     root = sys.argv[1]
     fac = calib(root)
     fetch = collect(os.path.join(root, "pmc", "p1"))
     write = collect(os.path.join(root, "pmc", "p2"))
+    req = collect(os.path.join(root, "pmc", "p3"))
+    creq = collect(os.path.join(root, "calib_TCC_EA0_RDREQ"))
+    # calibration of the sized count: true bytes / sized bytes per read width (expect 1.0)
+    sized_cal = {}
+    for k, d in creq.items():
+        if k.startswith("rd<") and sized_bytes(d):
+            sized_cal[k[3:-1].strip()] = round(CALIB_BYTES / sized_bytes(d), 4)
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over "
                      "`bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-fg`; counters in KB",
            "calibration": {f"{c}@{w}B": round(v, 4) for (c, w), v in sorted(fac.items())},
+           "sized_read_calibration": sized_cal,
            "kernels": {}, "stages": {}}
     for k in sorted(set(fetch) | set(write)):
         out["kernels"][k] = {"dispatches": fetch.get(k, {}).get("_dispatches"),
@@ -68,10 +83,20 @@ def main():
         fr = sum(fetch[k]["FETCH_SIZE"] * fetch[k]["_dispatches"] for k in ks) * 1024 / frames
         wr = sum(write[k]["WRITE_SIZE"] * write[k]["_dispatches"] for k in ks) * 1024 / frames
         fr_f, wr_f = fac.get(("FETCH_SIZE", rw), 1.0), fac.get(("WRITE_SIZE", ww), 1.0)
-        out["stages"][st] = {"kernels": ks, "read_width": rw, "write_width": ww,
-                             "fetch_bytes_raw": int(fr), "write_bytes_raw": int(wr),
-                             "fetch_factor": round(fr_f, 4), "write_factor": round(wr_f, 4),
-                             "hbm_bytes_per_step": int(fr * fr_f + wr * wr_f)}
+        ent = {"kernels": ks, "read_width": rw, "write_width": ww,
+               "fetch_bytes_raw": int(fr), "write_bytes_raw": int(wr),
+               "fetch_factor": round(fr_f, 4), "write_factor": round(wr_f, 4),
+               "hbm_bytes_per_step_width_factor": int(fr * fr_f + wr * wr_f)}
+        rd = None
+        if all(k in req and sized_bytes(req[k]) is not None for k in ks):
+            rd = sum(sized_bytes(req[k]) * req[k]["_dispatches"] for k in ks) / frames
+            ent["read_bytes_sized"] = int(rd)
+            ent["read_requests"] = {c: int(sum(req[k].get(c, 0.0) * req[k]["_dispatches"] for k in ks) / frames)
+                                    for c in ("TCC_EA0_RDREQ", "TCC_EA0_RDREQ_32B", "TCC_EA0_RDREQ_64B",
+                                              "TCC_EA0_RDREQ_128B")}
+        # preferred: reads at their request sizes (calibrated to 1.0 on the streaming kernels), writes exact
+        ent["hbm_bytes_per_step"] = int(rd + wr * wr_f) if rd is not None else ent["hbm_bytes_per_step_width_factor"]
+        out["stages"][st] = ent
     print(json.dumps(out, indent=1))
 
 
