@@ -8,7 +8,8 @@
 // start): the 16-bit LFSR is linear over GF(2), so lane i jumps straight to its slice of the
 // random sequence with a precomputed matrix power and the grain templates fill in parallel;
 // the auto-regressive filter runs as a skewed wavefront (row y lags row y-1 by lag+1
-// columns, one LDS barrier per step); scaling LUTs are filled from their closed form; the
+// columns, one LDS barrier per step; the chroma templates trail the luma one by just enough
+// steps to see final luma grain); scaling LUTs are filled from their closed form; the
 // per-(32-row, 32-col) block offsets are drawn by one lane per block row.
 // apply: one wave per 512-pixel row segment, lane-contiguous pixels; grain templates and
 // offsets are read through L1/L2 (cache resident), the scaling LUT from LDS.
@@ -22,7 +23,8 @@ __constant__ int16_t k_gauss[2048] = {
 __constant__ uint16_t k_lfsr_jump[256][16];   // M^(24*i) as 16 column vectors
 
 constexpr int kGW = 82, kGH = 73, kDrawsPerLane = 24;
-constexpr int kGP = 88;   // pitch of the exported templates (16-byte rows for vector loads)
+constexpr int kGP = 88;             // pitch of the exported templates (16-byte rows for vector loads)
+constexpr int kPrepThreads = 384;   // prep: 3 x 128 lanes (luma, U, V template rows)
 
 __device__ __forceinline__ unsigned lfsr_step(unsigned s) {
     const unsigned bit = (s ^ (s >> 1) ^ (s >> 3) ^ (s >> 12)) & 1;
@@ -30,42 +32,74 @@ __device__ __forceinline__ unsigned lfsr_step(unsigned s) {
 }
 __device__ __forceinline__ int round2i(int x, int sh) { return (x + ((1 << sh) >> 1)) >> sh; }
 
-// Random fill of one grain template (generate_grain_*: first loop).
-__device__ void grain_fill(int16_t *buf, int gw, int gh, unsigned seed, int shift) {
-    const int n = gw * gh;
-    for (int lane = threadIdx.x; lane * kDrawsPerLane < n; lane += 256) {
-        unsigned s = 0;
+// Random fill of the grain templates (generate_grain_*: first loop), all planes at once: job j
+// is lane `j - first job of its plane` of that plane's draw sequence. The 24 LFSR states of a
+// job are stepped first, then the 24 table reads issue back to back.
+__device__ void grain_fill_all(int16_t (*lut)[kGH][kGW], unsigned seed, int shift, bool uv0, bool uv1,
+                               int cw, int chh) {
+    const int nl = kGW * kGH, nc = cw * chh;
+    const int jl = (nl + kDrawsPerLane - 1) / kDrawsPerLane, jc = (nc + kDrawsPerLane - 1) / kDrawsPerLane;
+    const int jobs = jl + (uv0 ? jc : 0) + (uv1 ? jc : 0);
+    for (int j = threadIdx.x; j < jobs; j += kPrepThreads) {
+        int pl, lane;
+        if (j < jl) pl = 0, lane = j;
+        else if (uv0 && j < jl + jc) pl = 1, lane = j - jl;
+        else pl = 2, lane = j - jl - (uv0 ? jc : 0);
+        const unsigned sd = pl == 0 ? seed : pl == 1 ? seed ^ 0xb524 : seed ^ 0x49d8;
+        const int gw = pl ? cw : kGW, n = pl ? nc : nl;
+        unsigned st = 0;
 #pragma unroll
-        for (int j = 0; j < 16; j++)
-            if ((seed >> j) & 1) s ^= k_lfsr_jump[lane][j];
+        for (int b = 0; b < 16; b++)
+            if ((sd >> b) & 1) st ^= k_lfsr_jump[lane][b];
+        int idx[kDrawsPerLane];
+#pragma unroll
+        for (int k = 0; k < kDrawsPerLane; k++) {
+            st = lfsr_step(st);
+            idx[k] = (st >> 5) & 0x7ff;
+        }
+        int v[kDrawsPerLane];
+#pragma unroll
+        for (int k = 0; k < kDrawsPerLane; k++) v[k] = k_gauss[idx[k]];
+        int16_t *buf = &lut[pl][0][0];
         const int d0 = lane * kDrawsPerLane;
-        for (int k = 0; k < kDrawsPerLane && d0 + k < n; k++) {
-            s = lfsr_step(s);
-            const int d = d0 + k;
-            buf[(d / gw) * kGW + d % gw] = (int16_t)round2i(k_gauss[(s >> 5) & 0x7ff], shift);
+        int r = d0 / gw, c = d0 - r * gw;
+#pragma unroll
+        for (int k = 0; k < kDrawsPerLane; k++) {
+            if (d0 + k < n) buf[r * kGW + c] = (int16_t)round2i(v[k], shift);
+            if (++c == gw) c = 0, r++;
         }
     }
 }
 
-// Auto-regressive pass as a skewed wavefront: lane r owns row 3 + r; at step t it filters
-// column 3 + t - (LAG + 1) r, so every tap of the previous rows and columns is final. LAG is a
-// template parameter: the taps unroll into independent LDS reads at immediate offsets and the
-// coefficients sit in scalar registers, so a step costs one round of LDS latency + a barrier.
-template <int LAG, bool CHROMA>
-__device__ void grain_ar(int16_t *buf, const int16_t *buf_y, int gw, int gh, const int8_t *coef_g,
-                         int shift, int gmin, int gmax, bool luma_term, int subx, int suby, int lane) {
-    constexpr int NT = 2 * LAG * LAG + 2 * LAG;         // taps before the centre (generate_grain_*)
-    constexpr int skew = LAG + 1;
+// Luma and both chroma templates in one skewed wavefront: threads 0-127 own luma rows,
+// 128-255 U rows, 256-383 V rows. Chroma sample (r, c) needs the luma samples under it final;
+// luma (Y, X) is final after step (X - 3) + skew (Y - 3), so the chroma wavefront can start
+// t0 = 1 + max over (r, c) of [last luma step it reads - its own step] steps after the luma
+// one, instead of after the whole luma template (8K10 4:2:0, lag 3: 353 steps, not 526).
+template <int LAG>
+__device__ void grain_ar_all(int16_t (*lut)[kGH][kGW], const MiFilmGrainData &d, bool uv0, bool uv1,
+                             int cw, int chh, int subx, int suby, int gmin, int gmax) {
+    constexpr int NT = 2 * LAG * LAG + 2 * LAG, skew = LAG + 1;
+    const int role = threadIdx.x >> 7, lane = threadIdx.x & 127;   // role: wave-uniform
+    const int8_t *cg = role == 0 ? d.ar_coeffs_y : d.ar_coeffs_uv[role - 1];
     int coef[NT + 1];
 #pragma unroll
-    for (int i = 0; i <= NT; i++) coef[i] = coef_g[i];
-    const int nrows = gh - 3, ncols = gw - 6;
-    const int steps = ncols + skew * (nrows - 1);
-    const bool own = lane >= 0 && lane < nrows;
+    for (int i = 0; i <= NT; i++) coef[i] = cg[i];
+    const int gw = role ? cw : kGW, gh = role ? chh : kGH;
+    const bool on = role == 0 || (role == 1 ? uv0 : uv1);
+    const bool own = on && lane < gh - 3;
+    const bool lterm = role && d.num_y_points;
+    const int shift = (int)d.ar_coeff_shift;
+    const int cmax = cw - 7, rmax = chh - 4;
+    const int t0 = 1 + cmax * ((1 << subx) - 1) + subx + skew * (rmax * ((1 << suby) - 1) + suby);
+    const int lsteps = (kGW - 6) + skew * (kGH - 4);
+    const int csteps = (cw - 6) + skew * (chh - 4);
+    const int steps = max(lsteps, uv0 || uv1 ? t0 + csteps : 0);
+    const int tstart = role ? t0 : 0;
+    int16_t *buf = &lut[role][0][0];
     const int y = 3 + lane;
-    int lterm = 0;
     for (int t = 0; t < steps; t++) {
-        const int x = 3 + t - skew * lane;
+        const int x = 3 + (t - tstart) - skew * lane;
         if (own && x >= 3 && x < gw - 3) {
             const int16_t *p = buf + y * kGW + x;
             int sum = 0, ci = 0;
@@ -76,29 +110,18 @@ __device__ void grain_ar(int16_t *buf, const int16_t *buf_y, int gw, int gh, con
                     if (dy == 0 && dx == 0) break;
                     sum += coef[ci++] * p[dy * kGW + dx];
                 }
-            if (CHROMA && luma_term) {
+            if (lterm) {
                 const int lx = ((x - 3) << subx) + 3, ly = ((y - 3) << suby) + 3;
-                const int16_t *q = buf_y + ly * kGW + lx;
-                lterm = q[0];
-                if (subx) lterm += q[1];
-                if (suby) { lterm += q[kGW]; if (subx) lterm += q[kGW + 1]; }
-                sum += round2i(lterm, subx + suby) * coef[NT];
+                const int16_t *q = &lut[0][ly][lx];
+                int l = q[0];
+                if (subx) l += q[1];
+                if (suby) { l += q[kGW]; if (subx) l += q[kGW + 1]; }
+                sum += round2i(l, subx + suby) * coef[NT];
             }
             const int g = p[0] + round2i(sum, shift);
             buf[y * kGW + x] = (int16_t)min(max(g, gmin), gmax);
         }
         __syncthreads();
-    }
-}
-
-template <bool CHROMA>
-__device__ void grain_ar_lag(int lag, int16_t *buf, const int16_t *buf_y, int gw, int gh, const int8_t *coef,
-                             int shift, int gmin, int gmax, bool luma_term, int subx, int suby, int lane) {
-    switch (lag) {
-    case 0: grain_ar<0, CHROMA>(buf, buf_y, gw, gh, coef, shift, gmin, gmax, luma_term, subx, suby, lane); break;
-    case 1: grain_ar<1, CHROMA>(buf, buf_y, gw, gh, coef, shift, gmin, gmax, luma_term, subx, suby, lane); break;
-    case 2: grain_ar<2, CHROMA>(buf, buf_y, gw, gh, coef, shift, gmin, gmax, luma_term, subx, suby, lane); break;
-    default: grain_ar<3, CHROMA>(buf, buf_y, gw, gh, coef, shift, gmin, gmax, luma_term, subx, suby, lane); break;
     }
 }
 
@@ -123,7 +146,7 @@ __device__ int scaling_entry(const uint8_t (*pts)[2], int num, int e, int shx) {
     return ((base & 0xff) + (r >> shx)) & 0xff;
 }
 
-__global__ __launch_bounds__(256) void fg_prep_kernel(FgArgs a) {
+__global__ __launch_bounds__(kPrepThreads) void fg_prep_kernel(FgArgs a) {
     __shared__ int16_t lut[3][kGH][kGW];
     const MiFilmGrainData &d = a.data;
     const int bdm8 = a.bpc - 8;
@@ -133,29 +156,23 @@ __global__ __launch_bounds__(256) void fg_prep_kernel(FgArgs a) {
     const bool uv1 = a.layout && (d.num_uv_points[1] || d.chroma_scaling_from_luma);
     const int cw = a.ss_x ? 44 : kGW, chh = a.ss_y ? 38 : kGH;
 
-    grain_fill(&lut[0][0][0], kGW, kGH, d.seed, shift);
-    if (uv0) grain_fill(&lut[1][0][0], cw, chh, d.seed ^ 0xb524, shift);
-    if (uv1) grain_fill(&lut[2][0][0], cw, chh, d.seed ^ 0x49d8, shift);
+    grain_fill_all(lut, d.seed, shift, uv0, uv1, cw, chh);
     __syncthreads();
-    grain_ar_lag<false>(d.ar_coeff_lag, &lut[0][0][0], nullptr, kGW, kGH, d.ar_coeffs_y, (int)d.ar_coeff_shift,
-                        -gctr, gctr - 1, false, 0, 0, threadIdx.x);
-    // both chroma templates advance together: lanes 0..127 own U rows, 128..255 own V rows
-    {
-        const int pl = threadIdx.x >> 7;
-        const bool on = pl ? uv1 : uv0;
-        grain_ar_lag<true>(d.ar_coeff_lag, &lut[1 + pl][0][0], &lut[0][0][0], cw, chh, d.ar_coeffs_uv[pl],
-                           (int)d.ar_coeff_shift, -gctr, gctr - 1, d.num_y_points != 0, a.ss_x, a.ss_y,
-                           on ? (threadIdx.x & 127) : -1);
+    switch (d.ar_coeff_lag) {
+    case 0: grain_ar_all<0>(lut, d, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
+    case 1: grain_ar_all<1>(lut, d, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
+    case 2: grain_ar_all<2>(lut, d, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
+    default: grain_ar_all<3>(lut, d, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
     }
     // export templates
-    for (int i = threadIdx.x; i < 3 * kGH * kGP; i += 256) {
+    for (int i = threadIdx.x; i < 3 * kGH * kGP; i += kPrepThreads) {
         const int r = i / kGP, c = i - r * kGP;
         a.lut[i] = c < kGW ? (&lut[0][0][0])[r * kGW + c] : 0;
     }
 
     // scaling LUTs
     const int size = 1 << a.bpc;
-    for (int i = threadIdx.x; i < 3 * size; i += 256) {
+    for (int i = threadIdx.x; i < 3 * size; i += kPrepThreads) {
         const int pl = i / size, e = i % size;
         int v = 0;
         if (pl == 0) { if (d.num_y_points || d.chroma_scaling_from_luma) v = scaling_entry(d.y_points, d.num_y_points, e, bdm8); }
@@ -476,7 +493,7 @@ int init_fg_tables() {
 
 int launch_fg(const FgArgs &a, hipStream_t s, bool prep, bool apply) {
     if (prep) {
-        hipLaunchKernelGGL(fg_prep_kernel, dim3(1), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(fg_prep_kernel, dim3(1), dim3(kPrepThreads), 0, s, a);
         const int nb = a.nrows * a.nblocks;
         if (nb > 0) hipLaunchKernelGGL(fg_offsets_kernel, dim3((nb + 255) / 256), dim3(256), 0, s, a);
     }
