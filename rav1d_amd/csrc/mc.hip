@@ -10,7 +10,7 @@
 // one wave; a larger unit is cut into 64-lane tiles, one wave each. One wave = one workgroup.
 //
 // Per item: both references' windows (rows + 7) x (cols + 7) are staged in LDS in one loop
-// with clamped coordinates (identical to emu_edge's replication, mc_tmpl.c:798-845), then a
+// of 4-sample quads with clamped coordinates (identical to emu_edge's replication, mc_tmpl.c:798-845), then a
 // single barrier. Each lane evaluates the horizontal 8-tap for its column on its R + 7 rows
 // straight from LDS as five v_dot2_i32_i16 on aligned sample pairs (odd columns use the tap
 // set shifted by one), feeds the vertical 8-tap through a register window, and blends the
@@ -25,12 +25,18 @@ __constant__ int8_t k_subpel[6][15][8] = {
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kMaxU = 8;           // units packed per wave
+#ifndef MC_MAX_U
+#define MC_MAX_U 16
+#endif
+constexpr int kMaxU = MC_MAX_U;    // units packed per wave
 #ifndef MC_STAGE_BATCH
 #define MC_STAGE_BATCH 8
 #endif
 constexpr int kStageBatch = MC_STAGE_BATCH;   // window loads in flight per lane before their LDS stores
 constexpr int kWinElems = 2240;    // window budget (elements), 4x16 units: 8 x 23 x 12 = 2208
+
+// LDS window row stride for a tile TW wide: >= TW + 7 samples, a multiple of 4 (quad stores)
+__host__ __device__ __forceinline__ int win_stride(int TW) { return (TW + 11) & ~3; }
 
 // units per wave for a class whose unit needs `lanes` lanes and a (TR+7) x (TW+8) window
 __host__ __device__ __forceinline__ int units_per_wave(int lanes, int wn) {
@@ -60,7 +66,7 @@ __device__ __forceinline__ ClassGeom class_geom(int c) {
     if (g.lanes_u <= 64) {
         g.T = 1;
         g.TR = g.h;
-        g.U = units_per_wave(g.lanes_u, (g.TR + 7) * (g.TW + 8));
+        g.U = units_per_wave(g.lanes_u, (g.TR + 7) * win_stride(g.TW));
         g.ctiles = 1;
     } else {
         g.U = 1;
@@ -71,10 +77,10 @@ __device__ __forceinline__ ClassGeom class_geom(int c) {
     return g;
 }
 
-template <typename Px>
-__device__ __forceinline__ int ldpx(const uint8_t *base, int64_t stride, int y, int x) {
-    return reinterpret_cast<const Px *>(base + (int64_t)y * stride)[x];
-}
+// unaligned global reads (gfx950 serves them in one access): 4 x u16, 4 x u8
+struct __attribute__((packed, aligned(2))) U2a { uint32_t x, y; };
+typedef uint32_t U1a __attribute__((aligned(1)));
+
 
 // Per-lane view of one reference of its unit.
 struct RefSel {
@@ -196,32 +202,55 @@ __global__ __launch_bounds__(64) void mc_kernel(McArgs a, int g) {
         rs[i].dy = b.y + (mvy >> (3 + ssv)) + ty0 - 3;
     }
 
-    // stage the references' windows: rows TR + 7, cols TW + 7 (row stride WS = TW + 8, even),
-    // flattened over the unit's staging lanes, kStageBatch loads in flight per lane before
-    // their LDS stores; both references of a compound unit are staged before one barrier.
-    const int WC = G.TW + 7, WR = G.TR + 7, WS = G.TW + 8, WN = WR * WS;
-    const uint32_t inv = (1u << 20) / WC + 1;      // (e * inv) >> 20 == e / WC for e < 2^20 / WC^2
+    // stage the references' windows: rows TR + 7, cols TW + 7 (row stride WS, a multiple of
+    // 4), as quads of 4 samples (one unaligned 4- or 8-byte load, one 8-byte LDS store),
+    // flattened over the unit's staging lanes, kStageBatch quads in flight per lane before
+    // their LDS stores; both references of a compound unit are staged before one barrier. Rows are clamped (emu_edge's replication, mc_tmpl.c:798-845); a window that
+    // crosses the left or right picture edge clamps per sample.
+    const int WR = G.TR + 7, WS = win_stride(G.TW), WN = WR * WS;
+    const int Q = WS >> 2;                          // quads per window row
+    const uint32_t inv = (1u << 20) / Q + 1;        // (e * inv) >> 20 == e / Q for e < 2^20 / Q^2
     auto stage = [&](const RefSel &r, int16_t *buf) {
         if (!active) return;
         const int li = G.T == 1 ? lane - uu * G.lanes_u : lane;
         const int nl = G.T == 1 ? G.lanes_u : 64;
-        const int NE = WR * WC;
+        const int NE = WR * Q;
+        const bool inside = r.dx >= 0 && r.dx + WS <= r.iw;
         int16_t *wdst = buf + uu * WN;
         for (int e0 = li; e0 < NE; e0 += kStageBatch * nl) {
-            int v[kStageBatch], o[kStageBatch];
+            uint32_t v0[kStageBatch], v1[kStageBatch];
+            int o[kStageBatch];
 #pragma unroll
             for (int k = 0; k < kStageBatch; k++) {
                 const int e = e0 + k * nl;
                 const int ec = e < NE ? e : li;
-                const int rr = (int)(((uint32_t)ec * inv) >> 20), cc = ec - rr * WC;
+                const int rr = (int)(((uint32_t)ec * inv) >> 20), qq = ec - rr * Q;
                 const int yy = min(max(r.dy + rr, 0), r.ih - 1);
-                const int xx = min(max(r.dx + cc, 0), r.iw - 1);
-                v[k] = ldpx<Px>(r.base, r.stride, yy, xx);
-                o[k] = e < NE ? rr * WS + cc : -1;
+                const int x0 = r.dx + 4 * qq;
+                const uint8_t *row = r.base + (int64_t)yy * r.stride;
+                if (inside) {
+                    if (sizeof(Px) == 2) {
+                        const U2a q = *reinterpret_cast<const U2a *>(row + 2 * x0);
+                        v0[k] = q.x;
+                        v1[k] = q.y;
+                    } else {
+                        const uint32_t q = *reinterpret_cast<const U1a *>(row + x0);
+                        v0[k] = (q & 0xffu) | ((q & 0xff00u) << 8);
+                        v1[k] = ((q >> 16) & 0xffu) | ((q >> 8) & 0xff0000u);
+                    }
+                } else {
+                    int px[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        px[j] = reinterpret_cast<const Px *>(row)[min(max(x0 + j, 0), r.iw - 1)];
+                    v0[k] = pack2(px[0], px[1]);
+                    v1[k] = pack2(px[2], px[3]);
+                }
+                o[k] = e < NE ? rr * WS + 4 * qq : -1;
             }
 #pragma unroll
             for (int k = 0; k < kStageBatch; k++)
-                if (o[k] >= 0) wdst[o[k]] = (int16_t)v[k];
+                if (o[k] >= 0) *reinterpret_cast<uint2 *>(wdst + o[k]) = make_uint2(v0[k], v1[k]);
         }
     };
     stage(rs[0], win[0]);
@@ -308,12 +337,12 @@ int mc_plan(McArgs &a, int g) {
         const int w = 1 << lw, h = 1 << lh;
         const int TW = w < 64 ? w : 64, R = h < 8 ? h : 8, lanes = TW * (h / R);
         if (lanes <= 64) {
-            const int U = units_per_wave(lanes, (h + 7) * (TW + 8));
+            const int U = units_per_wave(lanes, (h + 7) * win_stride(TW));
             if (U < 1) return -1;                           // shape outside AV1's (aspect > 8:1)
             waves += (n + U - 1) / U;
         } else {
             const int TR = (64 / TW) * R;
-            if ((TR + 7) * (TW + 8) > kWinElems) return -1;
+            if ((TR + 7) * win_stride(TW) > kWinElems) return -1;
             waves += n * (uint32_t)((w / TW) * (h / TR));
         }
     }
