@@ -112,7 +112,7 @@ class Pipeline:
         if self.mc is not None:
             timed("mc", lambda: F.check(lib.mi_mc_frame(ctx, ctypes.byref(pa), self.ref_pics, len(self.refs),
                                                         ctypes.c_void_p(self.mc.blocks.data_ptr()), self.mc.class_start,
-                                                        ctypes.c_void_p(self.mc.masks.data_ptr()), sp), "mc"))
+                                                        ctypes.c_void_p(self.mc.masks.data_ptr()), None, sp), "mc"))
         ss = (ctypes.c_uint32 * 20)(*[int(v) for v in self.fr["size_start"]])
         timed("itx", lambda: F.check(lib.mi_itx_frame(ctx, ctypes.byref(pa), ctypes.c_void_p(self.blocks.data_ptr()),
                                                       ss, ctypes.c_void_p(self.coef.data_ptr()), ITX_KEEP_COEFS, sp), "itx"))

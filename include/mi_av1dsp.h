@@ -148,6 +148,15 @@ typedef struct MiFilmGrainData {
 #define MI_MC_WAVG 1   /* COMP_INTER_WEIGHTED_AVG: w_avg(tmp[0], tmp[1], weight) */
 #define MI_MC_MASK 2   /* COMP_INTER_WEDGE (and chroma of SEG): mask(tmp[sign], tmp[!sign], mask) */
 #define MI_MC_SEG  3   /* COMP_INTER_SEG, luma: w_mask(tmp[sign], tmp[!sign]); writes the chroma mask */
+/* single-reference units (ref[1] < 0) with a non-default destination: */
+#define MI_MC_OBMC_H 4 /* OBMC lap of the above neighbour (obmc(), recon.rs:2225-2266): put w x h, then
+                          blend_h into cur: rows y < (param * 3) >> 2, mask obmc_masks[param + y];
+                          param = the blend height v_mul * oh4, h = the lap height rounded up to a
+                          power of two (the extra rows are not stored) */
+#define MI_MC_OBMC_V 5 /* OBMC lap of the left neighbour (recon.rs:2267-2306): put w x h, then
+                          blend_v into cur: columns x < (w * 3) >> 2, mask obmc_masks[w + x] */
+#define MI_MC_PREP   6 /* prep (mct) into the int16 tmp arena at element mask_off, row pitch w: one
+                          side of a compound whose other side is warped or scaled (mi_mc_combine) */
 typedef struct MiMcBlock {
     uint16_t x, y;          /* top-left, plane pixels */
     uint8_t  w, h;          /* plane pixels, 2..128 (bw4 * h_mul, bh4 * v_mul) */
@@ -180,6 +189,39 @@ typedef struct MiIpredBlock {
     int8_t   alpha;         /* CfL alpha */
     uint8_t  pad;
 } MiIpredBlock;
+
+/* One 8x8 block of a warped prediction (warp_affine, recon.rs:2311-2400): the arguments of
+ * one warp8x8 / warp8x8t call with the source position instead of a pointer (40 bytes). */
+typedef struct MiWarpBlock {
+    uint16_t x, y;          /* destination top-left, plane pixels */
+    uint8_t  plane;
+    int8_t   ref;           /* index into refs[] */
+    uint8_t  prep;          /* 0: warp8x8 into cur; 1: warp8x8t into tmp at tmp_off, pitch tmp_stride */
+    uint8_t  pad0;
+    int32_t  dx, dy;        /* warp_affine's dx, dy: the 8x8's source origin (window = dx-3 .. dx+11) */
+    int32_t  mx, my;        /* filter phases as passed to warp8x8 */
+    int16_t  abcd[4];       /* Rav1dWarpedMotionParams.abcd */
+    uint32_t tmp_off;       /* int16 element offset of the block in tmp */
+    uint16_t tmp_stride;    /* elements */
+    uint16_t pad1;
+} MiWarpBlock;
+
+/* One compound combine from two prep intermediates in the tmp arena (the avg / w_avg / mask /
+ * w_mask step of recon_b_inter, recon.rs:3292-3331, when a side was warped or scaled). 24 bytes. */
+typedef struct MiMcCombine {
+    uint16_t x, y;          /* destination, plane pixels */
+    uint8_t  w, h;          /* plane pixels */
+    uint8_t  plane;
+    uint8_t  comp;          /* MI_MC_AVG .. MI_MC_SEG */
+    uint8_t  param;         /* as MiMcBlock.param */
+    uint8_t  pad[3];
+    uint32_t tmp_off[2];    /* element offsets of tmp[0], tmp[1] (row pitch w) */
+    uint32_t mask_off;      /* as MiMcBlock.mask_off */
+} MiMcCombine;
+
+#define MI_IPRED_II 128    /* mode flag: inter-intra, blend the prediction into the existing
+                              (inter) pixels with the mask at idx + aux_off (mc.blend,
+                              recon.rs:3524-3543): only with slots 0-12 */
 
 /* ------------------------------------------------------------------------------------ */
 /* Context                                                                               */
@@ -237,7 +279,32 @@ int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, v
 #define MI_MC_NCLASS 64
 int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
                 const MiMcBlock *blocks, const uint32_t class_start[2 * MI_MC_NCLASS + 1],
-                uint8_t *masks, void *stream);
+                uint8_t *masks, int16_t *tmp, void *stream);
+/* OBMC: the caller runs mi_mc_frame a second time with the above-neighbour laps
+ * (MI_MC_OBMC_H units) and a third time with the left-neighbour laps (MI_MC_OBMC_V), as
+ * obmc() blends above before left. `tmp` (device, int16) receives MI_MC_PREP units; may be
+ * NULL without them. */
+
+/* Scaled references (recon.rs:2124-2202): units whose reference differs in size from cur, put
+ * (single) or MI_MC_PREP into tmp. Positions and steps follow f->svc (scale_fac,
+ * decode.rs:4776) from the picture sizes. `blocks` is a device array of n units, any order. */
+int mi_mc_scaled(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
+                 const MiMcBlock *blocks, int n, int16_t *tmp, void *stream);
+
+/* Warped motion (warp_affine, recon.rs:2311-2400): n 8x8 blocks (device array), edge
+ * replication as emu_edge. */
+int mi_mc_warp(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
+               const MiWarpBlock *blocks, int n, int16_t *tmp, void *stream);
+
+/* Compound combine of two tmp intermediates into cur (device arrays; SEG writes masks). */
+int mi_mc_combine(MiCtx *ctx, const MiPicture *cur, const MiMcCombine *units, int n,
+                  const int16_t *tmp, uint8_t *masks, void *stream);
+
+/* Super-resolution upscale of a whole frame (rav1d_filter_sbrow_resize, recon.rs:4215-4285,
+ * over all rows; mc.resize): src is the coded-width picture, dst the upscaled one (same height,
+ * layout, bpc). Step and start per plane follow scale_fac / get_upscale_x0 (decode.rs:4644,
+ * 4776, 4872-4878). */
+int mi_superres_frame(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, void *stream);
 
 /* CDEF for a whole frame, out of place: reads the deblocked picture `src` (never written)
  * and writes `dst` (blocks the reference skips are copied). Replaces rav1d_cdef_brow

@@ -434,7 +434,7 @@ static void mc_block(const McBlock *bk, int i, void *dst, ptrdiff_t ds, int16_t 
 
 void oracle_mc_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layout, int bpc,
                      void *const *const refs, const ptrdiff_t *ref_strides, const int *ref_wh,
-                     const void *blocks, int n, uint8_t *masks) {
+                     const void *blocks, int n, uint8_t *masks, int16_t *tmp_arena) {
     const McBlock *bl = blocks;
     const int pb = bpc == 8 ? 1 : 2;
     const int chr_ss_hor = layout == 1 || layout == 2, chr_ss_ver = layout == 1;
@@ -447,6 +447,27 @@ void oracle_mc_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layo
         uint8_t *dst = (uint8_t *)cur[p] + bk->y * ds + bk->x * pb;
         int16_t *tmp[2] = { t0, t1 };
         const int nref = bk->ref[1] >= 0 ? 2 : 1;
+        if (nref == 1 && bk->comp >= 4) {
+            const int r = bk->ref[0];
+            const void *rp = refs[r * 3 + p];
+            const ptrdiff_t rs = ref_strides[r * 2 + (p ? 1 : 0)];
+            if (bk->comp == 6) {   /* prep into the tmp arena (one side of a combined compound) */
+                mc_block(bk, 0, NULL, 0, tmp_arena + bk->mask_off, rp, rs, ref_wh[r * 2], ref_wh[r * 2 + 1],
+                         ss_hor, ss_ver, bpc);
+                continue;
+            }
+            /* OBMC lap (obmc(), recon_tmpl.c:1013-1068): mc() into the lap buffer at the
+             * reference's own lap geometry, then blend_h / blend_v */
+            McBlock lb = *bk;
+            const int v_mul = 4 >> ss_ver;
+            if (bk->comp == 4) lb.h = (uint8_t)((((bk->param / v_mul) * 3 + 3) >> 2) * v_mul);
+            uint8_t *lap = malloc((size_t)128 * 128 * pb);
+            mc_block(&lb, 0, lap, lb.w * pb, NULL, rp, rs, ref_wh[r * 2], ref_wh[r * 2 + 1], ss_hor, ss_ver, bpc);
+            if (bk->comp == 4) oracle_mc_blend_h(dst, ds, lap, bk->w, bk->param, bpc);
+            else oracle_mc_blend_v(dst, ds, lap, bk->w, bk->h, bpc);
+            free(lap);
+            continue;
+        }
         for (int i = 0; i < nref; i++) {
             const int r = bk->ref[i];
             mc_block(bk, i, dst, ds, nref == 2 ? tmp[i] : NULL, refs[r * 3 + p], ref_strides[r * 2 + (p ? 1 : 0)],
@@ -468,4 +489,143 @@ void oracle_mc_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layo
     }
     free(t0);
     free(t1);
+}
+
+/* ---- scaled references, warp, combine, super-resolution (frame drivers) ---- */
+
+/* mc() scaled branch (recon_tmpl.c:1012-1060 / recon.rs:2124-2202) over MiMcBlock units:
+ * comp 6 = prep into tmp_arena + mask_off, otherwise put into cur. cur_w/cur_h: luma size of
+ * the current frame; ref_wh: luma sizes of the references. */
+static int scale_fac(int ref_sz, int this_sz) { return ((ref_sz << 14) + (this_sz >> 1)) / this_sz; }
+void oracle_mc_scaled_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layout, int bpc, int cur_w,
+                            int cur_h, void *const *const refs, const ptrdiff_t *ref_strides, const int *ref_wh,
+                            const void *blocks, int n, int16_t *tmp_arena) {
+    const McBlock *bl = blocks;
+    const int pb = bpc == 8 ? 1 : 2;
+    for (int k = 0; k < n; k++) {
+        const McBlock *bk = &bl[k];
+        const int p = bk->plane, r = bk->ref[0];
+        const int ss_hor = p && layout != 3, ss_ver = p && layout == 1;
+        const int sx = scale_fac(ref_wh[r * 2], cur_w), sy = scale_fac(ref_wh[r * 2 + 1], cur_h);
+        const int stx = (sx + 8) >> 4, sty = (sy + 8) >> 4;
+        const int mvx = bk->mvx[0], mvy = bk->mvy[0];
+        const int opy = (bk->y << 4) + mvy * (1 << !ss_ver), opx = (bk->x << 4) + mvx * (1 << !ss_hor);
+        const int64_t tx = (int64_t)opx * sx + (int64_t)(sx - 0x4000) * 8;
+        const int64_t ty = (int64_t)opy * sy + (int64_t)(sy - 0x4000) * 8;
+        const int pos_x = (int)(tx < 0 ? -((-tx + 128) >> 8) : (tx + 128) >> 8) + 32;
+        const int pos_y = (int)(ty < 0 ? -((-ty + 128) >> 8) : (ty + 128) >> 8) + 32;
+        const int left = pos_x >> 10, top = pos_y >> 10;
+        const int right = ((pos_x + (bk->w - 1) * stx) >> 10) + 1, bottom = ((pos_y + (bk->h - 1) * sty) >> 10) + 1;
+        const int w = (ref_wh[r * 2] + ss_hor) >> ss_hor, h = (ref_wh[r * 2 + 1] + ss_ver) >> ss_ver;
+        const void *rp = refs[r * 3 + p];
+        ptrdiff_t rs = ref_strides[r * 2 + (p ? 1 : 0)];
+        const void *ref;
+        uint8_t *emu = NULL;
+        if (left < 3 || top < 3 || right + 4 > w || bottom + 4 > h) {
+            emu = malloc((size_t)320 * 320 * pb);
+            oracle_mc_emu_edge(right - left + 7, bottom - top + 7, w, h, left - 3, top - 3, emu, 320 * pb, rp, rs, bpc);
+            ref = emu + (320 * 3 + 3) * pb;
+            rs = 320 * pb;
+        } else {
+            ref = (const uint8_t *)rp + top * rs + left * pb;
+        }
+        const ptrdiff_t ds = cur_stride[p ? 1 : 0];
+        uint8_t *dst = (uint8_t *)cur[p] + bk->y * ds + bk->x * pb;
+        const int prep = bk->comp == 6;
+        oracle_mc_scaled(bk->filter2d, prep, dst, ds, prep ? tmp_arena + bk->mask_off : NULL, ref, rs, bk->w, bk->h,
+                         pos_x & 0x3ff, pos_y & 0x3ff, stx, sty, bpc);
+        free(emu);
+    }
+}
+
+typedef struct {
+    uint16_t x, y;
+    uint8_t plane;
+    int8_t ref;
+    uint8_t prep, pad0;
+    int32_t dx, dy, mx, my;
+    int16_t abcd[4];
+    uint32_t tmp_off;
+    uint16_t tmp_stride, pad1;
+} WarpBlock;   /* == MiWarpBlock, 40 bytes */
+
+/* warp_affine's per-8x8 step (recon_tmpl.c:1070-1120): emu_edge of the 15x15 window when it
+ * leaves the picture, then warp8x8 / warp8x8t. */
+void oracle_mc_warp_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layout, int bpc,
+                          void *const *const refs, const ptrdiff_t *ref_strides, const int *ref_wh,
+                          const void *blocks, int n, int16_t *tmp_arena) {
+    const WarpBlock *bl = blocks;
+    const int pb = bpc == 8 ? 1 : 2;
+    uint8_t emu[32 * 15 * 2];
+    for (int k = 0; k < n; k++) {
+        const WarpBlock *bk = &bl[k];
+        const int p = bk->plane, r = bk->ref;
+        const int ss_hor = p && layout != 3, ss_ver = p && layout == 1;
+        const int w = (ref_wh[r * 2] + ss_hor) >> ss_hor, h = (ref_wh[r * 2 + 1] + ss_ver) >> ss_ver;
+        const void *rp = refs[r * 3 + p];
+        ptrdiff_t rs = ref_strides[r * 2 + (p ? 1 : 0)];
+        const void *ref;
+        if (bk->dx < 3 || bk->dx + 8 + 4 > w || bk->dy < 3 || bk->dy + 8 + 4 > h) {
+            oracle_mc_emu_edge(15, 15, w, h, bk->dx - 3, bk->dy - 3, emu, 32 * pb, rp, rs, bpc);
+            ref = emu + (32 * 3 + 3) * pb;
+            rs = 32 * pb;
+        } else {
+            ref = (const uint8_t *)rp + bk->dy * rs + bk->dx * pb;
+        }
+        const ptrdiff_t ds = cur_stride[p ? 1 : 0];
+        uint8_t *dst = (uint8_t *)cur[p] + bk->y * ds + bk->x * pb;
+        oracle_mc_warp8x8(bk->prep, dst, ds, tmp_arena + bk->tmp_off, bk->tmp_stride, ref, rs, bk->abcd, bk->mx, bk->my,
+                          bpc);
+    }
+}
+
+typedef struct {
+    uint16_t x, y;
+    uint8_t w, h, plane, comp, param, pad[3];
+    uint32_t tmp_off[2], mask_off;
+} McCombine;   /* == MiMcCombine, 24 bytes */
+
+void oracle_mc_combine_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layout, int bpc,
+                             const void *units, int n, const int16_t *tmp_arena, uint8_t *masks) {
+    const McCombine *ul = units;
+    const int pb = bpc == 8 ? 1 : 2;
+    const int chr_ss_hor = layout == 1 || layout == 2, chr_ss_ver = layout == 1;
+    for (int k = 0; k < n; k++) {
+        const McCombine *u = &ul[k];
+        const ptrdiff_t ds = cur_stride[u->plane ? 1 : 0];
+        uint8_t *dst = (uint8_t *)cur[u->plane] + u->y * ds + u->x * pb;
+        const int16_t *t[2] = { tmp_arena + u->tmp_off[0], tmp_arena + u->tmp_off[1] };
+        const int s = u->param >> 7;
+        switch (u->comp) {
+        case 0: oracle_mc_avg(dst, ds, t[0], t[1], u->w, u->h, bpc); break;
+        case 1: oracle_mc_w_avg(dst, ds, t[0], t[1], u->w, u->h, u->param & 31, bpc); break;
+        case 2: oracle_mc_mask(dst, ds, t[s], t[!s], u->w, u->h, masks + u->mask_off, bpc); break;
+        case 3: {
+            const int sh = layout == 0 ? 0 : chr_ss_hor, sv = layout == 0 ? 0 : chr_ss_ver;
+            oracle_mc_w_mask(dst, ds, t[s], t[!s], u->w, u->h, masks + u->mask_off, s, sh, sv, bpc);
+            break;
+        }
+        }
+    }
+}
+
+/* rav1d_filter_sbrow_resize over every row (recon_tmpl.c:2330-2370; decode.rs:4644, 4776,
+ * 4872-4878): src is coded-width (src_w luma), dst the upscaled width (dst_w luma). */
+static int upscale_x0(int in_w, int out_w, int step) {
+    const int err = out_w * step - (in_w << 14);
+    const int x0 = (-((out_w - in_w) << 13) + (out_w >> 1)) / out_w + 128 - err / 2;
+    return x0 & 0x3fff;
+}
+void oracle_superres_frame(void *const src[3], const ptrdiff_t src_stride[2], void *const dst[3],
+                           const ptrdiff_t dst_stride[2], int layout, int bpc, int src_w, int dst_w, int h) {
+    const int ss_hor = layout == 1 || layout == 2, ss_ver = layout == 1;
+    const int in_cw = (src_w + ss_hor) >> ss_hor, out_cw = (dst_w + ss_hor) >> ss_hor;
+    const int step[2] = { scale_fac(src_w, dst_w), scale_fac(in_cw, out_cw) };
+    const int start[2] = { upscale_x0(src_w, dst_w, step[0]), upscale_x0(in_cw, out_cw, step[1]) };
+    const int bw4 = ((src_w + 7) >> 3) << 1;   /* f->bw: 4-px units, 8-px aligned */
+    for (int p = 0; p < (layout ? 3 : 1); p++) {
+        const int sh = p ? ss_hor : 0, sv = p ? ss_ver : 0;
+        oracle_mc_resize(dst[p], dst_stride[p ? 1 : 0], src[p], src_stride[p ? 1 : 0], (dst_w + sh) >> sh,
+                         (h + sv) >> sv, (4 * bw4 + sh) >> sh, step[!!p], start[!!p], bpc);
+    }
 }

@@ -68,7 +68,17 @@ void oracle_mc_resize(void *dst, ptrdiff_t ds, const void *src, ptrdiff_t ss, in
  * MiMcBlock records; refs[r*3+p] plane pointers, ref_strides[r*2+{0,1}], ref_wh[r*2+{0,1}]. */
 void oracle_mc_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layout, int bpc,
                      void *const *const refs, const ptrdiff_t *ref_strides, const int *ref_wh,
-                     const void *blocks, int n, uint8_t *masks);
+                     const void *blocks, int n, uint8_t *masks, int16_t *tmp_arena);
+void oracle_mc_scaled_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layout, int bpc, int cur_w,
+                            int cur_h, void *const *const refs, const ptrdiff_t *ref_strides, const int *ref_wh,
+                            const void *blocks, int n, int16_t *tmp_arena);
+void oracle_mc_warp_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layout, int bpc,
+                          void *const *const refs, const ptrdiff_t *ref_strides, const int *ref_wh,
+                          const void *blocks, int n, int16_t *tmp_arena);
+void oracle_mc_combine_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layout, int bpc,
+                             const void *units, int n, const int16_t *tmp_arena, uint8_t *masks);
+void oracle_superres_frame(void *const src[3], const ptrdiff_t src_stride[2], void *const dst[3],
+                           const ptrdiff_t dst_stride[2], int layout, int bpc, int src_w, int dst_w, int h);
 
 /* ---- ipred (src/ipred.rs; C twin src/ipred_tmpl.c) ---- */
 /* mode = intra_pred[] slot: 0 DC,1 V,2 H,3 LEFT_DC,4 TOP_DC,5 DC_128,6 Z1,7 Z2,8 Z3,9 SMOOTH,

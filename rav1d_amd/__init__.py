@@ -73,6 +73,15 @@ assert IPRED_DTYPE.itemsize == 24
 IPRED_CFL, IPRED_PAL = 32, 64
 
 MC_AVG, MC_WAVG, MC_MASK, MC_SEG = 0, 1, 2, 3
+MC_OBMC_H, MC_OBMC_V, MC_PREP = 4, 5, 6
+WARP_DTYPE = np.dtype([("x", "<u2"), ("y", "<u2"), ("plane", "u1"), ("ref", "i1"), ("prep", "u1"), ("pad0", "u1"),
+                       ("dx", "<i4"), ("dy", "<i4"), ("mx", "<i4"), ("my", "<i4"), ("abcd", "<i2", 4),
+                       ("tmp_off", "<u4"), ("tmp_stride", "<u2"), ("pad1", "<u2")])
+assert WARP_DTYPE.itemsize == 40
+COMBINE_DTYPE = np.dtype([("x", "<u2"), ("y", "<u2"), ("w", "u1"), ("h", "u1"), ("plane", "u1"), ("comp", "u1"),
+                          ("param", "u1"), ("pad", "u1", 3), ("tmp_off", "<u4", 2), ("mask_off", "<u4")])
+assert COMBINE_DTYPE.itemsize == 24
+IPRED_II = 128
 MC_NCLASS = 64
 
 N_RECT_TX_SIZES = 19
@@ -105,7 +114,12 @@ def lib():
     _sig(L, "mi_dsp_itxfm_add", ctypes.c_int,
          [ctypes.c_int, ctypes.c_int, _VP, ctypes.c_ssize_t, _VP, ctypes.c_int, ctypes.c_int])
     _sig(L, "mi_mc_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture), ctypes.c_int,
-                                          _VP, ctypes.POINTER(ctypes.c_uint32), _VP, _VP])
+                                          _VP, ctypes.POINTER(ctypes.c_uint32), _VP, _VP, _VP])
+    for n in ("mi_mc_scaled", "mi_mc_warp"):
+        _sig(L, n, ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture), ctypes.c_int,
+                                  _VP, ctypes.c_int, _VP, _VP])
+    _sig(L, "mi_mc_combine", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.c_int, _VP, _VP, _VP])
+    _sig(L, "mi_superres_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture), _VP])
     _sig(L, "mi_ipred_blocks", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.c_int, _VP, _VP, _VP, _VP])
     _sig(L, "mi_dsp_intra_pred", ctypes.c_int, [ctypes.c_int, _VP, ctypes.c_ssize_t, _VP] + [ctypes.c_int] * 6)
     _sig(L, "mi_deblock_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiLoopFilter), _VP])
@@ -123,7 +137,8 @@ def lib():
 
 # Every symbol include/mi_av1dsp.h declares (checked by tests/test_abi.py).
 EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
-            "mi_itx_frame", "mi_mc_frame", "mi_ipred_blocks", "mi_deblock_frame", "mi_cdef_frame", "mi_lr_frame",
+            "mi_itx_frame", "mi_mc_frame", "mi_mc_scaled", "mi_mc_warp", "mi_mc_combine", "mi_superres_frame",
+            "mi_ipred_blocks", "mi_deblock_frame", "mi_cdef_frame", "mi_lr_frame",
             "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply",
             "mi_dsp_itxfm_add", "mi_dsp_intra_pred"]
 

@@ -4,6 +4,7 @@
 // The per-call entry points keep the reference's contract (caller owns buffers, callee zeroes
 // the consumed coefficients, src/itx.rs:152-158) and accept host or device pointers; they run
 // a one-block launch synchronously on a private stream of device 0.
+#include <algorithm>
 #include <errno.h>
 #include <mutex>
 #include <string.h>
@@ -113,25 +114,23 @@ int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
     return r ? fail(ctx, -EIO) : 0;
 }
 
-int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
-                const MiMcBlock *blocks, const uint32_t class_start[2 * MI_MC_NCLASS + 1], uint8_t *masks,
-                void *stream) {
-    if (!ctx || !cur || !class_start) return fail(ctx, -EINVAL);
-    if (cur->bpc != 8 && cur->bpc != 10 && cur->bpc != 12) return fail(ctx, -EINVAL);
-    if (nrefs < 0 || nrefs > 7 || (nrefs && !refs)) return fail(ctx, -EINVAL);
-    for (int k = 0; k < 2 * MI_MC_NCLASS; k++)
-        if (class_start[k] > class_start[k + 1]) return fail(ctx, -EINVAL);
-    if (class_start[2 * MI_MC_NCLASS] == class_start[0]) return 0;
-    if (!blocks || !nrefs) return fail(ctx, -EINVAL);
-    mi::McArgs a;
+}  // extern "C"
+
+namespace {
+// McArgs from the current picture and the references (planes, strides, clamp bounds, bit
+// depth). same_size: the references must share cur's geometry (non-scaled MC, warp).
+int fill_mc_args(mi::McArgs &a, const MiPicture *cur, const MiPicture *refs, int nrefs, bool same_size) {
     memset(&a, 0, sizeof(a));
+    if (cur->bpc != 8 && cur->bpc != 10 && cur->bpc != 12) return -EINVAL;
+    if (nrefs < 0 || nrefs > 7 || (nrefs && !refs)) return -EINVAL;
     const int ss_hor = cur->layout == 1 || cur->layout == 2, ss_ver = cur->layout == 1;
     for (int p = 0; p < 3; p++) a.dst[p] = (uint8_t *)cur->data[p];
     a.dst_stride[0] = cur->stride[0];
     a.dst_stride[1] = cur->stride[1];
     for (int r = 0; r < nrefs; r++) {
-        // scaled references take the mc_scaled path of the reference: not batched here
-        if (!same_geometry(cur, &refs[r])) return fail(ctx, -EINVAL);
+        if (same_size ? !same_geometry(cur, &refs[r])
+                      : refs[r].bpc != cur->bpc || refs[r].layout != cur->layout || refs[r].w <= 0 || refs[r].h <= 0)
+            return -EINVAL;
         for (int p = 0; p < 3; p++) {
             const int sh = p ? ss_hor : 0, sv = p ? ss_ver : 0;
             a.ref[r][p] = (const uint8_t *)refs[r].data[p];
@@ -141,8 +140,6 @@ int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nre
         a.ref_stride[r][0] = refs[r].stride[0];
         a.ref_stride[r][1] = refs[r].stride[1];
     }
-    a.blocks = blocks;
-    a.masks = masks;
     a.bpc = cur->bpc;
     a.ib = cur->bpc == 8 ? 4 : 14 - cur->bpc;
     a.bias = cur->bpc == 8 ? 0 : 8192;
@@ -150,6 +147,26 @@ int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nre
     a.layout = cur->layout;
     a.seg_ss_hor = cur->layout ? ss_hor : 0;   // w_mask[chr_layout_idx] (recon_tmpl.c:1868)
     a.seg_ss_ver = cur->layout ? ss_ver : 0;
+    return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
+                const MiMcBlock *blocks, const uint32_t class_start[2 * MI_MC_NCLASS + 1], uint8_t *masks,
+                int16_t *tmp, void *stream) {
+    if (!ctx || !cur || !class_start) return fail(ctx, -EINVAL);
+    for (int k = 0; k < 2 * MI_MC_NCLASS; k++)
+        if (class_start[k] > class_start[k + 1]) return fail(ctx, -EINVAL);
+    mi::McArgs a;
+    // scaled references take mi_mc_scaled (the reference's mc_scaled path)
+    if (int e = fill_mc_args(a, cur, refs, nrefs, true)) return fail(ctx, e);
+    if (class_start[2 * MI_MC_NCLASS] == class_start[0]) return 0;
+    if (!blocks || !nrefs) return fail(ctx, -EINVAL);
+    a.blocks = blocks;
+    a.masks = masks;
+    a.tmp = tmp;
     memcpy(a.class_start, class_start, sizeof(a.class_start));
     const int w0 = mi::mc_plan(a, 0), w1 = mi::mc_plan(a, 1);
     if (w0 < 0 || w1 < 0) return fail(ctx, -EINVAL);
@@ -158,6 +175,79 @@ int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nre
     int r = mi::launch_mc(a, 0, w0, s);
     if (!r) r = mi::launch_mc(a, 1, w1, s);
     return r ? fail(ctx, -EIO) : 0;
+}
+
+int mi_mc_scaled(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
+                 const MiMcBlock *blocks, int n, int16_t *tmp, void *stream) {
+    if (!ctx || !cur || n < 0) return fail(ctx, -EINVAL);
+    mi::McArgs a;
+    if (int e = fill_mc_args(a, cur, refs, nrefs, false)) return fail(ctx, e);
+    if (!n) return 0;
+    if (!blocks || !nrefs) return fail(ctx, -EINVAL);
+    a.tmp = tmp;
+    return mi::launch_mc_scaled(a, blocks, n, cur->w, cur->h, (hipStream_t)stream) ? fail(ctx, -EIO) : 0;
+}
+
+int mi_mc_warp(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
+               const MiWarpBlock *blocks, int n, int16_t *tmp, void *stream) {
+    if (!ctx || !cur || n < 0) return fail(ctx, -EINVAL);
+    mi::McArgs a;
+    if (int e = fill_mc_args(a, cur, refs, nrefs, true)) return fail(ctx, e);
+    if (!n) return 0;
+    if (!blocks || !nrefs) return fail(ctx, -EINVAL);
+    a.tmp = tmp;
+    return mi::launch_mc_warp(a, blocks, n, (hipStream_t)stream) ? fail(ctx, -EIO) : 0;
+}
+
+int mi_mc_combine(MiCtx *ctx, const MiPicture *cur, const MiMcCombine *units, int n,
+                  const int16_t *tmp, uint8_t *masks, void *stream) {
+    if (!ctx || !cur || n < 0) return fail(ctx, -EINVAL);
+    mi::McArgs a;
+    if (int e = fill_mc_args(a, cur, nullptr, 0, true)) return fail(ctx, e);
+    if (!n) return 0;
+    if (!units || !tmp) return fail(ctx, -EINVAL);
+    a.tmp = const_cast<int16_t *>(tmp);
+    a.masks = masks;
+    return mi::launch_mc_combine(a, units, n, (hipStream_t)stream) ? fail(ctx, -EIO) : 0;
+}
+
+int mi_superres_frame(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, void *stream) {
+    if (!ctx || !src || !dst) return fail(ctx, -EINVAL);
+    if (src->bpc != dst->bpc || src->layout != dst->layout || src->h != dst->h || src->w <= 0 ||
+        dst->w < src->w || dst->w > 2 * src->w + 16 || (src->bpc != 8 && src->bpc != 10 && src->bpc != 12))
+        return fail(ctx, -EINVAL);
+    // scale_fac / get_upscale_x0 (decode.rs:4644-4648, 4776-4778, 4872-4878)
+    auto scale_fac = [](int ref_sz, int this_sz) { return ((ref_sz << 14) + (this_sz >> 1)) / this_sz; };
+    auto upscale_x0 = [](int in_w, int out_w, int step) {
+        const int err = out_w * step - (in_w << 14);
+        const int x0 = (-((out_w - in_w) << 13) + (out_w >> 1)) / out_w + 128 - err / 2;
+        return x0 & 0x3fff;
+    };
+    mi::SuperresArgs a;
+    memset(&a, 0, sizeof(a));
+    const int ss_hor = src->layout == 1 || src->layout == 2, ss_ver = src->layout == 1;
+    const int in_cw = (src->w + ss_hor) >> ss_hor, out_cw = (dst->w + ss_hor) >> ss_hor;
+    a.step[0] = scale_fac(src->w, dst->w);
+    a.step[1] = scale_fac(in_cw, out_cw);
+    a.start[0] = upscale_x0(src->w, dst->w, a.step[0]);
+    a.start[1] = upscale_x0(in_cw, out_cw, a.step[1]);
+    const int bw4 = ((src->w + 7) >> 3) << 1;   // f->bw
+    a.nplanes = src->layout ? 3 : 1;
+    for (int p = 0; p < a.nplanes; p++) {
+        const int sh = p ? ss_hor : 0, sv = p ? ss_ver : 0;
+        a.src[p] = (const uint8_t *)src->data[p];
+        a.dst[p] = (uint8_t *)dst->data[p];
+        a.src_w[p] = (4 * bw4 + sh) >> sh;
+        a.dst_w[p] = (dst->w + sh) >> sh;
+        a.h[p] = (src->h + sv) >> sv;
+        a.chunks = std::max(a.chunks, (a.dst_w[p] + 255) / 256);
+    }
+    a.src_stride[0] = src->stride[0];
+    a.src_stride[1] = src->stride[1];
+    a.dst_stride[0] = dst->stride[0];
+    a.dst_stride[1] = dst->stride[1];
+    a.bpc = src->bpc;
+    return mi::launch_superres(a, (hipStream_t)stream) ? fail(ctx, -EIO) : 0;
 }
 
 int mi_ipred_blocks(MiCtx *ctx, const MiPicture *pic, const MiIpredBlock *blocks, int n,

@@ -117,6 +117,7 @@ struct McArgs {
     int ref_w[7][3], ref_h[7][3];    // plane dimensions (clamp bounds)
     const MiMcBlock *blocks;
     uint8_t *masks;
+    int16_t *tmp;                    // MI_MC_PREP arena
     int bpc, ib, bias, bdmax, layout;
     int seg_ss_hor, seg_ss_ver;      // w_mask[chr_layout_idx] subsampling of the SEG mask
     uint32_t class_start[2 * MI_MC_NCLASS + 1];
@@ -125,6 +126,22 @@ struct McArgs {
 // launchers (mc.hip): mc_plan fills first_wave[g] and returns the wave count of group g
 int mc_plan(McArgs &a, int g);
 int launch_mc(const McArgs &a, int g, int waves, hipStream_t s);
+
+// scaled references, warp, combine (mc_ext.hip): McArgs supplies pictures and bit depth;
+// `units` is the device array of the entry point, cur_w / cur_h the current frame's luma size
+int launch_mc_scaled(const McArgs &a, const MiMcBlock *units, int n, int cur_w, int cur_h, hipStream_t s);
+int launch_mc_warp(const McArgs &a, const MiWarpBlock *blocks, int n, hipStream_t s);
+int launch_mc_combine(const McArgs &a, const MiMcCombine *units, int n, hipStream_t s);
+
+struct SuperresArgs {
+    const uint8_t *src[3];
+    uint8_t *dst[3];
+    int64_t src_stride[2], dst_stride[2];
+    int src_w[3], dst_w[3], h[3];   // per plane: resize source width (4 * f->bw), output width, rows
+    int step[2], start[2];          // luma, chroma
+    int bpc, nplanes, chunks;       // chunks: 256-px output segments per row (max over planes)
+};
+int launch_superres(const SuperresArgs &a, hipStream_t s);
 
 struct IpredArgs {
     uint8_t *dst[3];

@@ -93,8 +93,19 @@ __global__ __launch_bounds__(64) void ipred_kernel(IpredArgs a) {
     const int64_t st = a.stride[b.plane ? 1 : 0];
     uint8_t *dst = a.dst[b.plane] + (int64_t)b.y * st + (int64_t)b.x * sizeof(Px);
     const int bdmax = a.bdmax;
-    auto put = [&](int y, int x, int v) { reinterpret_cast<Px *>(dst + (int64_t)y * st)[x] = (Px)v; };
-    const int mode = b.mode;
+    // inter-intra (MI_IPRED_II): blend into the inter prediction with the block's mask
+    // (mc.blend, mc_tmpl.c:621-630); the address is formed before the uniform branch
+    const bool ii = b.mode & MI_IPRED_II;
+    const uint8_t *iim = a.idx + b.aux_off;
+    auto put = [&](int y, int x, int v) {
+        Px *d = reinterpret_cast<Px *>(dst + (int64_t)y * st) + x;
+        if (ii) {
+            const int m = iim[y * w + x];
+            v = (*d * (64 - m) + v * m + 32) >> 6;
+        }
+        *d = (Px)v;
+    };
+    const int mode = b.mode & ~MI_IPRED_II;
 
     if (mode >= MI_IPRED_PAL) {                      // pal_pred: palette at edge_off, indices in idx
         const uint8_t *idx = a.idx + b.aux_off;

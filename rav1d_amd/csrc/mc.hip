@@ -22,6 +22,9 @@ namespace mi {
 __constant__ int8_t k_subpel[6][15][8] = {
 #include "tables/mc_subpel_filters.inc"
 };
+__constant__ uint8_t k_obmc[64] = {
+#include "tables/obmc_masks.inc"
+};
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
@@ -264,7 +267,32 @@ __global__ __launch_bounds__(64) void mc_kernel(McArgs a, int g) {
     uint8_t *dst = a.dst[p] + (int64_t)(b.y + ty0 + r0) * ds;
     const int x = b.x + tx0 + col;
     if (nref == 1) {
+        if (b.comp == MI_MC_PREP) {
+            // one side of a compound combined later (mi_mc_combine): the mct intermediate
+            predict<true>(a, win[0] + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
+            int16_t *t = a.tmp + b.mask_off + (ty0 + r0) * b.w + tx0 + col;
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (q < R) t[q * b.w] = (int16_t)o0[q];
+            return;
+        }
         predict<false>(a, win[0] + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
+        if (b.comp == MI_MC_OBMC_H || b.comp == MI_MC_OBMC_V) {
+            // OBMC lap blended into the block's prediction (blend_h / blend_v, mc_tmpl.c:636-660)
+            const bool above = b.comp == MI_MC_OBMC_H;
+            const int yb = ty0 + r0, xb = tx0 + col;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int y = yb + q;
+                const bool on = q < R && (above ? y < ((b.param * 3) >> 2) : xb < ((b.w * 3) >> 2));
+                if (on) {
+                    const int m = k_obmc[above ? b.param + y : b.w + xb];
+                    Px *d = reinterpret_cast<Px *>(dst + (int64_t)q * ds) + x;
+                    *d = (Px)((*d * (64 - m) + o0[q] * m + 32) >> 6);
+                }
+            }
+            return;
+        }
 #pragma unroll
         for (int q = 0; q < 8; q++)
             if (q < R) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];

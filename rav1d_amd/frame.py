@@ -143,13 +143,51 @@ class McMeta:
         self.class_start = (ctypes.c_uint32 * (2 * MC_NCLASS + 1))(*[int(v) for v in class_start])
 
 
-def mc_frame(ctx, cur, refs, meta, stream=None):
-    """mi_mc_frame: inter prediction of every unit into `cur` from the reference Frames."""
+def _dptr(t):
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def mc_frame(ctx, cur, refs, meta, stream=None, tmp=None):
+    """mi_mc_frame: inter prediction of every unit into `cur` from the reference Frames.
+    tmp: optional int16 device tensor (arena for MI_MC_PREP units)."""
     pics = (MiPicture * len(refs))(*[r.picture() for r in refs])
     rc = lib().mi_mc_frame(ctx.h, ctypes.byref(cur.picture()), pics, len(refs),
                            ctypes.c_void_p(meta.blocks.data_ptr()), meta.class_start,
-                           ctypes.c_void_p(meta.masks.data_ptr()), _stream_ptr(stream))
+                           ctypes.c_void_p(meta.masks.data_ptr()), _dptr(tmp), _stream_ptr(stream))
     check(rc, "mi_mc_frame")
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).cuda()
+
+
+def mc_scaled(ctx, cur, refs, units, tmp, stream=None):
+    """mi_mc_scaled over MiMcBlock units (numpy) whose references differ in size from cur."""
+    pics = (MiPicture * len(refs))(*[r.picture() for r in refs])
+    u = _dev(units)
+    check(lib().mi_mc_scaled(ctx.h, ctypes.byref(cur.picture()), pics, len(refs), ctypes.c_void_p(u.data_ptr()),
+                             len(units), _dptr(tmp), _stream_ptr(stream)), "mi_mc_scaled")
+    return u
+
+
+def mc_warp(ctx, cur, refs, blocks, tmp, stream=None):
+    pics = (MiPicture * len(refs))(*[r.picture() for r in refs])
+    b = _dev(blocks)
+    check(lib().mi_mc_warp(ctx.h, ctypes.byref(cur.picture()), pics, len(refs), ctypes.c_void_p(b.data_ptr()),
+                           len(blocks), _dptr(tmp), _stream_ptr(stream)), "mi_mc_warp")
+    return b
+
+
+def mc_combine(ctx, cur, units, tmp, masks, stream=None):
+    u = _dev(units)
+    check(lib().mi_mc_combine(ctx.h, ctypes.byref(cur.picture()), ctypes.c_void_p(u.data_ptr()), len(units),
+                              _dptr(tmp), _dptr(masks), _stream_ptr(stream)), "mi_mc_combine")
+    return u
+
+
+def superres_frame(ctx, src, dst, stream=None):
+    check(lib().mi_superres_frame(ctx.h, ctypes.byref(src.picture()), ctypes.byref(dst.picture()),
+                                  _stream_ptr(stream)), "mi_superres_frame")
 
 
 class LoopFilterMeta:

@@ -557,8 +557,8 @@ def mc_sort_units(units):
     stably sorted units and class_start[2 * MC_NCLASS + 1]."""
     grp = (units["plane"] > 0).astype(np.int64)
     key = grp * MC_NCLASS + mc_class_of(units)
-    # within a class, single before compound and compound grouped by type: waves stay uniform
-    sub = np.where(units["ref"][:, 1] >= 0, 1 + units["comp"].astype(np.int64), 0)
+    # within a class, units grouped by compound type / single-reference destination: waves stay uniform
+    sub = units["comp"].astype(np.int64) + 16 * (units["ref"][:, 1] < 0)
     order = np.lexsort((sub, key))
     cs = np.searchsorted(key[order], np.arange(2 * MC_NCLASS + 1)).astype(np.uint32)
     return units[order], cs

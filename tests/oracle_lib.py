@@ -152,8 +152,16 @@ def fg_grain_y(fg, bpc):
 def _mc_sigs(o):
     if getattr(o, "_mc_ready", False):
         return
-    o.oracle_mc_frame.argtypes = [_VP, _VP, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP, _VP, ctypes.c_int, _VP]
+    o.oracle_mc_frame.argtypes = [_VP, _VP, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP, _VP, ctypes.c_int, _VP, _VP]
     o.oracle_mc_frame.restype = None
+    o.oracle_mc_scaled_frame.argtypes = [_VP, _VP] + [ctypes.c_int] * 4 + [_VP, _VP, _VP, _VP, ctypes.c_int, _VP]
+    o.oracle_mc_warp_frame.argtypes = [_VP, _VP, ctypes.c_int, ctypes.c_int, _VP, _VP, _VP, _VP, ctypes.c_int, _VP]
+    o.oracle_mc_combine_frame.argtypes = [_VP, _VP, ctypes.c_int, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP]
+    o.oracle_superres_frame.argtypes = [_VP, _VP, _VP, _VP] + [ctypes.c_int] * 5
+    o.oracle_mc_blend.argtypes = [_VP, ctypes.c_ssize_t, _VP, ctypes.c_int, ctypes.c_int, _VP, ctypes.c_int]
+    for n in ("oracle_mc_scaled_frame", "oracle_mc_warp_frame", "oracle_mc_combine_frame", "oracle_superres_frame",
+              "oracle_mc_blend"):
+        getattr(o, n).restype = None
     o.oracle_mc_put.argtypes = [ctypes.c_int, _VP, ctypes.c_ssize_t, _VP, ctypes.c_ssize_t] + [ctypes.c_int] * 5
     o.oracle_mc_prep.argtypes = [ctypes.c_int, _VP, _VP, ctypes.c_ssize_t] + [ctypes.c_int] * 5
     o.oracle_mc_emu_edge.argtypes = [ctypes.c_int] * 6 + [_VP, ctypes.c_ssize_t, _VP, ctypes.c_ssize_t, ctypes.c_int]
@@ -164,28 +172,99 @@ def _mc_sigs(o):
     o._mc_ready = True
 
 
-def mc_frame(cur_planes, ref_frames, bpc, layout, w, h, units, masks):
+class _McFrameArgs:
+    """ctypes views of padded current / reference planes for the oracle's MC frame drivers."""
+
+    def __init__(self, cur_planes, ref_frames, ref_wh):
+        self.cur = [np.ascontiguousarray(p).copy() for p in cur_planes]
+        while len(self.cur) < 3:
+            self.cur.append(self.cur[0])
+        self.refs = [[np.ascontiguousarray(p) for p in f] for f in ref_frames]
+        for f in self.refs:
+            while len(f) < 3:
+                f.append(f[0])
+        self.cp = (ctypes.c_void_p * 3)(*[a.ctypes.data for a in self.cur])
+        self.cs = (ctypes.c_ssize_t * 2)(self.cur[0].strides[0], self.cur[1].strides[0])
+        refs = self.refs
+        self.rp = (ctypes.c_void_p * max(1, 3 * len(refs)))(*[a.ctypes.data for f in refs for a in f])
+        self.rs = (ctypes.c_ssize_t * max(1, 2 * len(refs)))(*[s for f in refs for s in (f[0].strides[0], f[1].strides[0])])
+        self.rwh = (ctypes.c_int * max(1, 2 * len(refs)))(*[v for wh in ref_wh for v in wh])
+
+
+def mc_frame(cur_planes, ref_frames, bpc, layout, w, h, units, masks, tmp=None):
     """Oracle frame MC. cur_planes: padded planes (modified copies returned); ref_frames: list
-    of padded plane lists; units: MCBLOCK_DTYPE array (luma first); masks: uint8 buffer."""
+    of padded plane lists; units: MCBLOCK_DTYPE array (luma first); masks: uint8 buffer; tmp:
+    int16 arena for MI_MC_PREP units (modified copy returned as the third value if given)."""
     o = load_oracle()
     _mc_sigs(o)
-    cur = [np.ascontiguousarray(p).copy() for p in cur_planes]
-    while len(cur) < 3:
-        cur.append(cur[0])
-    refs = [[np.ascontiguousarray(p) for p in f] for f in ref_frames]
-    for f in refs:
-        while len(f) < 3:
-            f.append(f[0])
-    cp = (ctypes.c_void_p * 3)(*[a.ctypes.data for a in cur])
-    cs = (ctypes.c_ssize_t * 2)(cur[0].strides[0], cur[1].strides[0])
-    rp = (ctypes.c_void_p * (3 * len(refs)))(*[a.ctypes.data for f in refs for a in f])
-    rs = (ctypes.c_ssize_t * (2 * len(refs)))(*[s for f in refs for s in (f[0].strides[0], f[1].strides[0])])
-    rwh = (ctypes.c_int * (2 * len(refs)))(*[v for _ in refs for v in (w, h)])
+    fa = _McFrameArgs(cur_planes, ref_frames, [(w, h)] * len(ref_frames))
     u = np.ascontiguousarray(units)
     m = np.ascontiguousarray(masks).copy()
-    o.oracle_mc_frame(cp, cs, layout, bpc, rp, rs, rwh, ptr(u), len(u), ptr(m))
+    t = np.zeros(1, np.int16) if tmp is None else np.ascontiguousarray(tmp, dtype=np.int16).copy()
+    o.oracle_mc_frame(fa.cp, fa.cs, layout, bpc, fa.rp, fa.rs, fa.rwh, ptr(u), len(u), ptr(m), ptr(t))
     n = 3 if layout else 1
-    return cur[:n], m
+    if tmp is None:
+        return fa.cur[:n], m
+    return fa.cur[:n], m, t
+
+
+def mc_scaled_frame(cur_planes, ref_frames, ref_wh, bpc, layout, w, h, units, tmp):
+    o = load_oracle()
+    _mc_sigs(o)
+    fa = _McFrameArgs(cur_planes, ref_frames, ref_wh)
+    u = np.ascontiguousarray(units)
+    t = np.ascontiguousarray(tmp, dtype=np.int16).copy()
+    o.oracle_mc_scaled_frame(fa.cp, fa.cs, layout, bpc, w, h, fa.rp, fa.rs, fa.rwh, ptr(u), len(u), ptr(t))
+    return fa.cur[:3 if layout else 1], t
+
+
+def mc_warp_frame(cur_planes, ref_frames, bpc, layout, w, h, blocks, tmp):
+    o = load_oracle()
+    _mc_sigs(o)
+    fa = _McFrameArgs(cur_planes, ref_frames, [(w, h)] * len(ref_frames))
+    b = np.ascontiguousarray(blocks)
+    t = np.ascontiguousarray(tmp, dtype=np.int16).copy()
+    o.oracle_mc_warp_frame(fa.cp, fa.cs, layout, bpc, fa.rp, fa.rs, fa.rwh, ptr(b), len(b), ptr(t))
+    return fa.cur[:3 if layout else 1], t
+
+
+def mc_combine_frame(cur_planes, bpc, layout, units, tmp, masks):
+    o = load_oracle()
+    _mc_sigs(o)
+    fa = _McFrameArgs(cur_planes, [], [])
+    u = np.ascontiguousarray(units)
+    t = np.ascontiguousarray(tmp, dtype=np.int16)
+    m = np.ascontiguousarray(masks).copy()
+    o.oracle_mc_combine_frame(fa.cp, fa.cs, layout, bpc, ptr(u), len(u), ptr(t), ptr(m))
+    return fa.cur[:3 if layout else 1], m
+
+
+def superres_frame(src_planes, dst_planes, bpc, layout, src_w, dst_w, h):
+    o = load_oracle()
+    _mc_sigs(o)
+    src = [np.ascontiguousarray(p) for p in src_planes]
+    dst = [np.ascontiguousarray(p).copy() for p in dst_planes]
+    while len(src) < 3:
+        src.append(src[0])
+        dst.append(dst[0])
+    sp = (ctypes.c_void_p * 3)(*[a.ctypes.data for a in src])
+    ss = (ctypes.c_ssize_t * 2)(src[0].strides[0], src[1].strides[0])
+    dp = (ctypes.c_void_p * 3)(*[a.ctypes.data for a in dst])
+    dss = (ctypes.c_ssize_t * 2)(dst[0].strides[0], dst[1].strides[0])
+    o.oracle_superres_frame(sp, ss, dp, dss, layout, bpc, src_w, dst_w, h)
+    return dst[:3 if layout else 1]
+
+
+def mc_blend(dst, tmp, mask, bpc):
+    """mc.blend (inter-intra): dst (h, w) pixels blended with tmp under mask, in a copy."""
+    o = load_oracle()
+    _mc_sigs(o)
+    d = np.ascontiguousarray(dst).copy()
+    t = np.ascontiguousarray(tmp, dtype=d.dtype)
+    m = np.ascontiguousarray(mask, dtype=np.uint8)
+    h, w = d.shape
+    o.oracle_mc_blend(ptr(d), d.strides[0], ptr(t), w, h, ptr(m), bpc)
+    return d
 
 
 def _ipred_sigs(o):
