@@ -219,6 +219,37 @@ typedef struct MiMcCombine {
     uint32_t mask_off;      /* as MiMcBlock.mask_off */
 } MiMcCombine;
 
+/* One intra-predicted transform block whose edges the device gathers from the picture itself
+ * (rav1d_prepare_intra_edges, src/ipred_prepare.rs:118-204, run in the kernel), 32 bytes.
+ * Neighbour pixels must be final when the launch runs: one dependency level per launch. The
+ * picture holds unfiltered reconstruction for the whole frame (deblocking runs after all
+ * recon), so the reference's pre-filter top-SB-row backup (recon.rs:2532-2540) is the picture
+ * row itself. */
+#define MI_INTRA_HAVE_LEFT   1u   /* x > tile column start (recon.rs:2554) */
+#define MI_INTRA_HAVE_TOP    2u   /* y > tile row start */
+#define MI_INTRA_TOP_RIGHT   4u   /* EdgeFlags::I444_TOP_HAS_RIGHT (or the I420/I422 flag for chroma) */
+#define MI_INTRA_BOTTOM_LEFT 8u   /* EdgeFlags::I444_LEFT_HAS_BOTTOM (or chroma flag) */
+#define MI_INTRA_SMOOTH_NB  16u   /* sm_flag / sm_uv_flag of a neighbour (angle bit 9) */
+#define MI_INTRA_EDGE_FILTER 32u  /* seq_hdr.intra_edge_filter (angle bit 10) */
+#define MI_INTRA_II         64u   /* inter-intra: blend into the pixels with the mask at idx + aux_off */
+typedef struct MiIntraBlock {
+    uint16_t x, y;          /* plane pixels */
+    uint8_t  w, h;          /* transform size, pixels (4..64) */
+    uint8_t  plane;
+    uint8_t  mode;          /* y_mode / uv_mode as coded (levels.rs IntraPredMode DC_PRED .. PAETH_PRED
+                               = 0 .. 12), 13 = filter intra (FILTER_PRED), MI_IPRED_CFL (uv CfL, edges
+                               as DC_PRED), MI_IPRED_PAL (palette) */
+    int8_t   angle;         /* angle delta (-3 .. 3) of a directional mode */
+    uint8_t  flags;         /* MI_INTRA_* */
+    uint8_t  filt_idx;      /* filter-intra mode (FILTER) */
+    int8_t   alpha;         /* CfL alpha */
+    uint16_t tile_w, tile_h;/* tile column / row end, plane pixels (edge availability limits) */
+    uint16_t max_w, max_h;  /* intra_pred's max_width / max_height */
+    uint32_t aux_off;       /* CfL: int16 index into ac; PAL: byte index into idx; II: mask byte index */
+    uint32_t pal_off;       /* PAL: pixel index of the block's 8-entry palette in `pal` */
+    uint32_t reserved;
+} MiIntraBlock;
+
 #define MI_IPRED_II 128    /* mode flag: inter-intra, blend the prediction into the existing
                               (inter) pixels with the mask at idx + aux_off (mc.blend,
                               recon.rs:3524-3543): only with slots 0-12 */
@@ -265,6 +296,13 @@ int mi_ipred_blocks(MiCtx *ctx, const MiPicture *pic, const MiIpredBlock *blocks
 /* Deblock a whole frame in place: all column edges (every plane), then all row edges.
  * Equivalent to the reference's per-sbrow cols/rows interleaving;
  * replaces rav1d_loopfilter_sbrow_cols/_rows (src/lf_apply.rs:597-834). */
+/* Intra prediction of n independent transform blocks with device-side edge gathering from
+ * `pic` (MiIntraBlock): the batched replacement of recon_b_intra's per-tx-block
+ * prepare_intra_edges + intra_pred / cfl_pred / pal_pred (recon.rs:2402-3160). ac / idx / pal
+ * are device arrays (may be NULL when unused). */
+int mi_intra_blocks(MiCtx *ctx, const MiPicture *pic, const MiIntraBlock *blocks, int n,
+                    const int16_t *ac, const uint8_t *idx, const void *pal, void *stream);
+
 int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, void *stream);
 
 /* Motion compensation for a whole frame: writes the inter prediction of every unit into

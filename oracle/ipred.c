@@ -400,3 +400,137 @@ void oracle_pal_pred(void *dst, ptrdiff_t stride, const void *pal, const uint8_t
             D(dst, stride, y, x, bpc == 8 ? ((const uint8_t *)pal)[i] : ((const uint16_t *)pal)[i], bpc);
         }
 }
+
+/* ---- rav1d_prepare_intra_edges (src/ipred_prepare.rs:118-204; C ipred_prepare_tmpl.c) ----
+ * In pixel units: x, y, the block's top-left; tile_w / tile_h the tile's column / row end
+ * (the reference's w, h in 4-px units times 4); w, h the transform size. Fills topleft[-2h ..
+ * 2w] and returns the implementation mode; *angle in: delta, out: the final angle. */
+static const uint8_t needs_tab[14] = { 3, 2, 1, 1, 2, 0, 14, 7, 21, 3, 3, 3, 7, 7 };  /* :76-115 */
+static const uint8_t mode_angle[8] = { 90, 180, 45, 135, 113, 157, 203, 67 };
+enum { N_LEFT = 1, N_TOP = 2, N_TOP_LEFT = 4, N_TOP_RIGHT = 8, N_BOTTOM_LEFT = 16 };
+
+int oracle_prepare_intra_edges(int x, int have_left, int y, int have_top, int tile_w, int tile_h,
+                               int top_has_right, int left_has_bottom, const void *pic, ptrdiff_t stride,
+                               int mode, int *angle, int w, int h, int filter_edge, void *topleft_, int bpc) {
+    const int pb = bpc == 8 ? 1 : 2;
+#define PIC(yy, xx) Dget((const uint8_t *)pic + (ptrdiff_t)(yy) * stride, 0, 0, (xx), bpc)
+#define TL(i) Dget((const uint8_t *)topleft_ + (ptrdiff_t)(i) * pb, 0, 0, 0, bpc)
+#define SET(i, v) D((uint8_t *)topleft_ + (ptrdiff_t)(i) * pb, 0, 0, 0, (v), bpc)
+    if (mode >= 1 && mode <= 8) {                         /* VERT_PRED ..= VERT_LEFT_PRED */
+        *angle = mode_angle[mode - 1] + 3 * *angle;
+        if (*angle <= 90) mode = *angle < 90 && have_top ? 6 : 1;
+        else if (*angle < 180) mode = 7;
+        else mode = *angle > 180 && have_left ? 8 : 2;
+    } else if (mode == 0) {                               /* av1_mode_conv */
+        mode = have_left ? (have_top ? 0 : 3) : (have_top ? 4 : 5);
+    } else if (mode == 12) {
+        mode = have_left ? (have_top ? 12 : 2) : (have_top ? 1 : 5);
+    }
+    const int needs = needs_tab[mode];
+    /* dst_top: row y - 1 starting at x - have_left */
+    if (needs & N_LEFT) {
+        const int sz = h;
+        if (have_left) {
+            const int px_have = sz < tile_h - y ? sz : tile_h - y;
+            for (int i = 0; i < px_have; i++) SET(-1 - i, PIC(y + i, x - 1));
+            for (int i = px_have; i < sz; i++) SET(-1 - i, TL(-px_have));
+        } else {
+            const int v = have_top ? PIC(y - 1, x) : (1 << bpc >> 1) + 1;
+            for (int i = 0; i < sz; i++) SET(-1 - i, v);
+        }
+        if (needs & N_BOTTOM_LEFT) {
+            const int hbl = !have_left || y + h >= tile_h ? 0 : left_has_bottom;
+            if (hbl) {
+                const int px_have = sz < tile_h - y - h ? sz : tile_h - y - h;
+                for (int i = 0; i < px_have; i++) SET(-1 - sz - i, PIC(y + sz + i, x - 1));
+                for (int i = px_have; i < sz; i++) SET(-1 - sz - i, TL(-sz - px_have));
+            } else {
+                const int v = TL(-sz);
+                for (int i = 0; i < sz; i++) SET(-1 - sz - i, v);
+            }
+        }
+    }
+    if (needs & N_TOP) {
+        const int sz = w;
+        if (have_top) {
+            const int px_have = sz < tile_w - x ? sz : tile_w - x;
+            for (int i = 0; i < px_have; i++) SET(1 + i, PIC(y - 1, x + i));
+            for (int i = px_have; i < sz; i++) SET(1 + i, TL(px_have));
+        } else {
+            const int v = have_left ? PIC(y, x - 1) : (1 << bpc >> 1) - 1;
+            for (int i = 0; i < sz; i++) SET(1 + i, v);
+        }
+        if (needs & N_TOP_RIGHT) {
+            const int htr = !have_top || x + w >= tile_w ? 0 : top_has_right;
+            if (htr) {
+                const int px_have = sz < tile_w - x - w ? sz : tile_w - x - w;
+                for (int i = 0; i < px_have; i++) SET(1 + sz + i, PIC(y - 1, x + sz + i));
+                for (int i = px_have; i < sz; i++) SET(1 + sz + i, TL(sz + px_have));
+            } else {
+                const int v = TL(sz);
+                for (int i = 0; i < sz; i++) SET(1 + sz + i, v);
+            }
+        }
+    }
+    if (needs & N_TOP_LEFT) {
+        int c = have_top ? PIC(y - 1, x - have_left) : have_left ? PIC(y, x - 1) : 1 << bpc >> 1;
+        if (mode == 7 && (w >> 2) + (h >> 2) >= 6 && filter_edge) c = ((TL(-1) + TL(1)) * 5 + c * 6 + 8) >> 4;
+        SET(0, c);
+    }
+#undef PIC
+#undef TL
+#undef SET
+    return mode;
+}
+
+/* recon_b_intra's per-transform-block step (recon.rs:2470-2600, 2735-2859) over MiIntraBlock
+ * records in order: palette, or prepare edges + intra_pred / cfl_pred, optionally blended
+ * (inter-intra, mc.blend). Sequential, so each block sees its predecessors' pixels. */
+typedef struct {
+    uint16_t x, y;
+    uint8_t w, h, plane, mode;
+    int8_t angle;
+    uint8_t flags, filt_idx;
+    int8_t alpha;
+    uint16_t tile_w, tile_h, max_w, max_h;
+    uint32_t aux_off, pal_off, reserved;
+} IntraBlock;   /* == MiIntraBlock, 32 bytes */
+
+void oracle_intra_blocks(void *const planes[3], const ptrdiff_t strides[2], int bpc, const void *blocks, int n,
+                         const int16_t *ac, const uint8_t *idx, const void *pal) {
+    const IntraBlock *bl = blocks;
+    const int pb = bpc == 8 ? 1 : 2;
+    uint8_t edge[(2 * 128 + 1) * 2], tmp[64 * 64 * 2];
+    for (int k = 0; k < n; k++) {
+        const IntraBlock *b = &bl[k];
+        const ptrdiff_t st = strides[b->plane ? 1 : 0];
+        uint8_t *dst = (uint8_t *)planes[b->plane] + b->y * st + b->x * pb;
+        const int ii = b->flags & 64;
+        uint8_t *out = ii ? tmp : dst;
+        const ptrdiff_t ost = ii ? b->w * pb : st;
+        if (b->mode == 64) {
+            oracle_pal_pred(out, ost, (const uint8_t *)pal + (size_t)b->pal_off * pb, idx + b->aux_off, b->w, b->h, bpc);
+        } else {
+            const int cfl = b->mode == 32;
+            int angle = b->angle;
+            void *tl = edge + 128 * pb;
+            const int m = oracle_prepare_intra_edges(b->x, b->flags & 1, b->y, (b->flags >> 1) & 1, b->tile_w, b->tile_h,
+                                                     (b->flags >> 2) & 1, (b->flags >> 3) & 1, planes[b->plane], st,
+                                                     cfl ? 0 : b->mode, &angle, b->w, b->h, (b->flags >> 5) & 1, tl, bpc);
+            if (cfl) {
+                oracle_cfl_pred(m, out, ost, tl, b->w, b->h, ac + b->aux_off, b->alpha, bpc);
+            } else {
+                const int aw = m == 13 ? b->filt_idx : angle | ((b->flags & 16) ? 512 : 0) | ((b->flags & 32) ? 1024 : 0);
+                oracle_intra_pred(m, out, ost, tl, b->w, b->h, aw, b->max_w, b->max_h, bpc);
+            }
+        }
+        if (ii) {
+            const uint8_t *mk = idx + b->aux_off;
+            for (int y = 0; y < b->h; y++)
+                for (int x = 0; x < b->w; x++) {
+                    const int a = Dget(dst, st, y, x, bpc), t = Dget(tmp, ost, y, x, bpc), mm = mk[y * b->w + x];
+                    D(dst, st, y, x, (a * (64 - mm) + t * mm + 32) >> 6, bpc);
+                }
+        }
+    }
+}

@@ -91,6 +91,11 @@ void oracle_cfl_ac(int16_t *ac, const void *ypx, ptrdiff_t stride, int w_pad, in
 void oracle_cfl_pred(int mode, void *dst, ptrdiff_t stride, const void *topleft, int w, int h,
                      const int16_t *ac, int alpha, int bpc);
 void oracle_pal_pred(void *dst, ptrdiff_t stride, const void *pal, const uint8_t *idx, int w, int h, int bpc);
+int oracle_prepare_intra_edges(int x, int have_left, int y, int have_top, int tile_w, int tile_h,
+                               int top_has_right, int left_has_bottom, const void *pic, ptrdiff_t stride,
+                               int mode, int *angle, int w, int h, int filter_edge, void *topleft, int bpc);
+void oracle_intra_blocks(void *const planes[3], const ptrdiff_t strides[2], int bpc, const void *blocks, int n,
+                         const int16_t *ac, const uint8_t *idx, const void *pal);
 
 #ifdef __cplusplus
 }

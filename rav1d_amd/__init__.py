@@ -71,6 +71,13 @@ IPRED_DTYPE = np.dtype([("edge_off", "<u4"), ("aux_off", "<u4"), ("x", "<u2"), (
                         ("max_h", "<u2"), ("alpha", "i1"), ("pad", "u1")])
 assert IPRED_DTYPE.itemsize == 24
 IPRED_CFL, IPRED_PAL = 32, 64
+INTRA_DTYPE = np.dtype([("x", "<u2"), ("y", "<u2"), ("w", "u1"), ("h", "u1"), ("plane", "u1"), ("mode", "u1"),
+                        ("angle", "i1"), ("flags", "u1"), ("filt_idx", "u1"), ("alpha", "i1"), ("tile_w", "<u2"),
+                        ("tile_h", "<u2"), ("max_w", "<u2"), ("max_h", "<u2"), ("aux_off", "<u4"),
+                        ("pal_off", "<u4"), ("reserved", "<u4")])
+assert INTRA_DTYPE.itemsize == 32
+INTRA_HAVE_LEFT, INTRA_HAVE_TOP, INTRA_TOP_RIGHT, INTRA_BOTTOM_LEFT = 1, 2, 4, 8
+INTRA_SMOOTH_NB, INTRA_EDGE_FILTER, INTRA_II = 16, 32, 64
 
 MC_AVG, MC_WAVG, MC_MASK, MC_SEG = 0, 1, 2, 3
 MC_OBMC_H, MC_OBMC_V, MC_PREP = 4, 5, 6
@@ -120,6 +127,7 @@ def lib():
                                   _VP, ctypes.c_int, _VP, _VP])
     _sig(L, "mi_mc_combine", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.c_int, _VP, _VP, _VP])
     _sig(L, "mi_superres_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture), _VP])
+    _sig(L, "mi_intra_blocks", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.c_int, _VP, _VP, _VP, _VP])
     _sig(L, "mi_ipred_blocks", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.c_int, _VP, _VP, _VP, _VP])
     _sig(L, "mi_dsp_intra_pred", ctypes.c_int, [ctypes.c_int, _VP, ctypes.c_ssize_t, _VP] + [ctypes.c_int] * 6)
     _sig(L, "mi_deblock_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiLoopFilter), _VP])
@@ -138,7 +146,7 @@ def lib():
 # Every symbol include/mi_av1dsp.h declares (checked by tests/test_abi.py).
 EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
             "mi_itx_frame", "mi_mc_frame", "mi_mc_scaled", "mi_mc_warp", "mi_mc_combine", "mi_superres_frame",
-            "mi_ipred_blocks", "mi_deblock_frame", "mi_cdef_frame", "mi_lr_frame",
+            "mi_ipred_blocks", "mi_intra_blocks", "mi_deblock_frame", "mi_cdef_frame", "mi_lr_frame",
             "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply",
             "mi_dsp_itxfm_add", "mi_dsp_intra_pred"]
 

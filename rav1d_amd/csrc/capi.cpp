@@ -270,6 +270,26 @@ int mi_ipred_blocks(MiCtx *ctx, const MiPicture *pic, const MiIpredBlock *blocks
     return mi::launch_ipred(a, n, (hipStream_t)stream) ? fail(ctx, -EIO) : 0;
 }
 
+int mi_intra_blocks(MiCtx *ctx, const MiPicture *pic, const MiIntraBlock *blocks, int n,
+                    const int16_t *ac, const uint8_t *idx, const void *pal, void *stream) {
+    if (!ctx || !pic || n < 0) return fail(ctx, -EINVAL);
+    if (pic->bpc != 8 && pic->bpc != 10 && pic->bpc != 12) return fail(ctx, -EINVAL);
+    if (!n) return 0;
+    if (!blocks) return fail(ctx, -EINVAL);
+    mi::IpredArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int p = 0; p < 3; p++) a.dst[p] = (uint8_t *)pic->data[p];
+    a.stride[0] = pic->stride[0];
+    a.stride[1] = pic->stride[1];
+    a.iblocks = blocks;
+    a.ac = ac;
+    a.idx = idx;
+    a.pal = (const uint8_t *)pal;
+    a.bpc = pic->bpc;
+    a.bdmax = (1 << pic->bpc) - 1;
+    return mi::launch_intra(a, n, (hipStream_t)stream) ? fail(ctx, -EIO) : 0;
+}
+
 int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, void *stream) {
     if (!ctx || !pic || !lf) return fail(ctx, -EINVAL);
     if (pic->bpc != 8 && pic->bpc != 10 && pic->bpc != 12) return fail(ctx, -EINVAL);

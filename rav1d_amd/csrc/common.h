@@ -150,10 +150,13 @@ struct IpredArgs {
     const uint8_t *edges;
     const int16_t *ac;
     const uint8_t *idx;
+    const MiIntraBlock *iblocks;     // mi_intra_blocks
+    const uint8_t *pal;
     int bpc, bdmax;
 };
 // launchers (ipred.hip)
 int launch_ipred(const IpredArgs &a, int n, hipStream_t s);
+int launch_intra(const IpredArgs &a, int n, hipStream_t s);
 
 struct LrArgs {
     const uint8_t *src[3];        // CDEF output C

@@ -82,14 +82,12 @@ __device__ void upsample_edge_par(int *out, int hsz, const Px *in_, int from, in
     }
 }
 
+// Predict one block from its gathered edge `tl` (global edge buffer or LDS). eb / ft: LDS
+// scratch for the directional edge and the filter-intra image.
 template <typename Px>
-__global__ __launch_bounds__(64) void ipred_kernel(IpredArgs a) {
-    __shared__ int eb[2 * 128 + 2];            // prepared edge (Z1/Z3: 2(w+h); Z2: 64 + 64 + 1)
-    __shared__ Px ft[32 * 32];                 // FILTER_PRED block image (up to 32x32)
-    const MiIpredBlock b = a.blocks[blockIdx.x];
+__device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredBlock &b, const Px *tl, int *eb, Px *ft) {
     const int lane = threadIdx.x;
     const int w = b.w, h = b.h, n = w * h;
-    const Px *tl = reinterpret_cast<const Px *>(a.edges) + b.edge_off;
     const int64_t st = a.stride[b.plane ? 1 : 0];
     uint8_t *dst = a.dst[b.plane] + (int64_t)b.y * st + (int64_t)b.x * sizeof(Px);
     const int bdmax = a.bdmax;
@@ -328,6 +326,139 @@ __global__ __launch_bounds__(64) void ipred_kernel(IpredArgs a) {
         }
         for (int i = lane; i < n; i += 64) put(i / w, i % w, ft[i]);
     }
+}
+
+template <typename Px>
+__global__ __launch_bounds__(64) void ipred_kernel(IpredArgs a) {
+    __shared__ int eb[2 * 128 + 2];            // prepared edge (Z1/Z3: 2(w+h); Z2: 64 + 64 + 1)
+    __shared__ Px ft[32 * 32];                 // FILTER_PRED block image (up to 32x32)
+    const MiIpredBlock b = a.blocks[blockIdx.x];
+    predict_block<Px>(a, b, reinterpret_cast<const Px *>(a.edges) + b.edge_off, eb, ft);
+}
+
+// ---- device-side rav1d_prepare_intra_edges (ipred_prepare.rs:118-204) ----
+
+// av1_intra_prediction_edges needs per implementation mode: LEFT 1, TOP 2, TOP_LEFT 4,
+// TOP_RIGHT 8, BOTTOM_LEFT 16 (ipred_prepare.rs:76-115)
+__constant__ uint8_t k_needs[14] = { 3, 2, 1, 1, 2, 0, 14, 7, 21, 3, 3, 3, 7, 7 };
+__constant__ uint8_t k_mode_angle[8] = { 90, 180, 45, 135, 113, 157, 203, 67 };
+
+template <typename Px>
+__global__ __launch_bounds__(64) void intra_kernel(IpredArgs a) {
+    __shared__ int eb[2 * 128 + 2];
+    __shared__ Px ft[32 * 32];
+    __shared__ Px edge[2 * 128 + 1];           // topleft at [128]
+    const MiIntraBlock ib = a.iblocks[blockIdx.x];
+    const int lane = threadIdx.x;
+    const int w = ib.w, h = ib.h, x = ib.x, y = ib.y;
+    const bool have_left = ib.flags & MI_INTRA_HAVE_LEFT, have_top = ib.flags & MI_INTRA_HAVE_TOP;
+    const int64_t st = a.stride[ib.plane ? 1 : 0];
+    const Px *pic = reinterpret_cast<const Px *>(a.dst[ib.plane]);
+    auto P = [&](int yy, int xx) -> int { return reinterpret_cast<const Px *>(reinterpret_cast<const uint8_t *>(pic) + (int64_t)yy * st)[xx]; };
+    const int bd = a.bpc;
+
+    MiIpredBlock b;
+    b.edge_off = 0;
+    b.aux_off = ib.aux_off;
+    b.x = ib.x;
+    b.y = ib.y;
+    b.w = ib.w;
+    b.h = ib.h;
+    b.plane = ib.plane;
+    b.max_w = ib.max_w;
+    b.max_h = ib.max_h;
+    b.alpha = ib.alpha;
+    b.pad = 0;
+    const int ii = ib.flags & MI_INTRA_II ? MI_IPRED_II : 0;
+    if (ib.mode == MI_IPRED_PAL) {
+        b.mode = MI_IPRED_PAL;
+        b.angle = 0;
+        predict_block<Px>(a, b, reinterpret_cast<const Px *>(a.pal) + ib.pal_off, eb, ft);
+        return;
+    }
+    // mode remap (ipred_prepare.rs:148-172): all wave-uniform
+    const bool cfl = ib.mode == MI_IPRED_CFL;
+    int m = cfl ? 0 : ib.mode, angle = 0;
+    if (m >= 1 && m <= 8) {
+        angle = k_mode_angle[m - 1] + 3 * ib.angle;
+        if (angle <= 90) m = angle < 90 && have_top ? 6 : 1;
+        else if (angle < 180) m = 7;
+        else m = angle > 180 && have_left ? 8 : 2;
+    } else if (m == 0 || m == 12) {
+        // av1_mode_conv[mode][have_left][have_top]
+        m = m == 0 ? (have_left ? (have_top ? 0 : 3) : (have_top ? 4 : 5))
+                   : (have_left ? (have_top ? 12 : 2) : (have_top ? 1 : 5));
+    } else if (m == 13) {
+        angle = ib.filt_idx;
+    }
+    const int needs = k_needs[m];
+    Px *tl = edge + 128;
+    const int tw4 = w >> 2, th4 = h >> 2;
+    // left column (+ bottom-left)
+    if (needs & 1) {
+        const int sz = h;
+        if (have_left) {
+            const int px_have = min(sz, (int)ib.tile_h - y);
+            for (int i = lane; i < sz; i += 64) tl[-1 - i] = (Px)P(y + min(i, px_have - 1), x - 1);
+        } else {
+            const int v = have_top ? P(y - 1, x) : (1 << bd >> 1) + 1;
+            for (int i = lane; i < sz; i += 64) tl[-1 - i] = (Px)v;
+        }
+        if (needs & 16) {
+            const bool hbl = have_left && y + h < (int)ib.tile_h && (ib.flags & MI_INTRA_BOTTOM_LEFT);
+            if (hbl) {
+                const int px_have = min(sz, (int)ib.tile_h - y - h);
+                for (int i = lane; i < sz; i += 64) tl[-1 - sz - i] = (Px)P(y + sz + min(i, px_have - 1), x - 1);
+            } else {
+                // bottom_left[..] = bottom_left[sz] = the last left sample (written above by this
+                // lane set: recompute it instead of reading LDS before the barrier)
+                const int last = have_left ? P(y + min(sz, (int)ib.tile_h - y) - 1, x - 1)
+                                           : (have_top ? P(y - 1, x) : (1 << bd >> 1) + 1);
+                for (int i = lane; i < sz; i += 64) tl[-1 - sz - i] = (Px)last;
+            }
+        }
+    }
+    // top row (+ top-right)
+    if (needs & 2) {
+        const int sz = w;
+        if (have_top) {
+            const int px_have = min(sz, (int)ib.tile_w - x);
+            for (int i = lane; i < sz; i += 64) tl[1 + i] = (Px)P(y - 1, x + min(i, px_have - 1));
+        } else {
+            const int v = have_left ? P(y, x - 1) : (1 << bd >> 1) - 1;
+            for (int i = lane; i < sz; i += 64) tl[1 + i] = (Px)v;
+        }
+        if (needs & 8) {
+            const bool htr = have_top && x + w < (int)ib.tile_w && (ib.flags & MI_INTRA_TOP_RIGHT);
+            if (htr) {
+                const int px_have = min(sz, (int)ib.tile_w - x - w);
+                for (int i = lane; i < sz; i += 64) tl[1 + sz + i] = (Px)P(y - 1, x + sz + min(i, px_have - 1));
+            } else {
+                const int last = have_top ? P(y - 1, x + min(sz, (int)ib.tile_w - x) - 1)
+                                          : (have_left ? P(y, x - 1) : (1 << bd >> 1) - 1);
+                for (int i = lane; i < sz; i += 64) tl[1 + sz + i] = (Px)last;
+            }
+        }
+    }
+    __syncthreads();
+    if ((needs & 4) && lane == 0) {
+        int c = have_top ? P(y - 1, x - (have_left ? 1 : 0)) : have_left ? P(y, x - 1) : 1 << bd >> 1;
+        if (m == 7 && tw4 + th4 >= 6 && (ib.flags & MI_INTRA_EDGE_FILTER))
+            c = ((tl[-1] + tl[1]) * 5 + c * 6 + 8) >> 4;
+        tl[0] = (Px)c;
+    }
+    __syncthreads();
+    b.mode = (uint8_t)((cfl ? MI_IPRED_CFL + m : m) | ii);
+    b.angle = (uint16_t)(angle | (ib.flags & MI_INTRA_SMOOTH_NB ? 512 : 0) | (ib.flags & MI_INTRA_EDGE_FILTER ? 1024 : 0));
+    if (m == 13) b.angle = (uint16_t)ib.filt_idx;
+    predict_block<Px>(a, b, tl, eb, ft);
+}
+
+int launch_intra(const IpredArgs &a, int n, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (a.bpc == 8) intra_kernel<uint8_t><<<n, 64, 0, s>>>(a);
+    else intra_kernel<uint16_t><<<n, 64, 0, s>>>(a);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 int launch_ipred(const IpredArgs &a, int n, hipStream_t s) {

@@ -63,3 +63,100 @@ def make_ipred_blocks(n, bpc, rng, sizes=SIZES, modes=None, plane_w=4096):
     return (blocks, np.concatenate(edges).astype(dt),
             np.concatenate(ac) if ac else np.zeros(1, np.int16),
             np.concatenate(idx) if idx else np.zeros(1, np.uint8), y + 64)
+
+
+def make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.5, pal_frac=0.05, cfl_frac=0.4,
+                     filter_frac=0.1, ii_frac=0.0, edge_filter=None):
+    """A whole intra frame as MiIntraBlock transform blocks in decode order (blocks in quadtree
+    z-order, luma then U then V per block, transform blocks raster within a block), with the
+    edge-availability flags a decoder would pass (top-right / bottom-left only where those
+    pixels are already decoded) and each block's dependency level (1 + the deepest level among
+    the blocks owning any pixel its edges may read). Returns dict(blocks (decode order),
+    order (indices sorted by level), level_start, ac, idx, pal). Single tile; w, h multiples
+    of 64."""
+    from . import (INTRA_BOTTOM_LEFT, INTRA_DTYPE, INTRA_EDGE_FILTER, INTRA_HAVE_LEFT, INTRA_HAVE_TOP, INTRA_II,
+                   INTRA_SMOOTH_NB, INTRA_TOP_RIGHT)
+    from .synth import partition_blocks
+    ss_h = 1 if layout in (1, 2) else 0
+    ss_v = 1 if layout == 1 else 0
+    nplanes = 3 if layout else 1
+    dims = [(w, h)] + [((w + ss_h) >> ss_h, (h + ss_v) >> ss_v)] * (nplanes - 1)
+    owner = [np.full((ph, pw), -1, np.int64) for pw, ph in dims]
+    level_of = []
+    if edge_filter is None:
+        edge_filter = int(rng.integers(0, 2))
+    recs, ac, idx, pal = [], [], [], []
+    n_ac = n_idx = n_pal = 0
+    dt = np.uint8 if bpc == 8 else np.uint16
+    for (bx, by, bw, bh) in partition_blocks(w, h, rng, sb=sb, min_bs=min_bs):
+        for pl in range(nplanes):
+            sh, sv = (ss_h, ss_v) if pl else (0, 0)
+            pw, ph = dims[pl]
+            px, py, pbw, pbh = bx >> sh, by >> sv, bw >> sh, bh >> sv
+            tw = pbw // 2 if pbw >= 8 and rng.random() < tx_split else pbw
+            th = pbh // 2 if pbh >= 8 and rng.random() < tx_split else pbh
+            tw, th = min(tw, 64), min(th, 64)
+            if tw * 4 < th:
+                th = tw * 4
+            if th * 4 < tw:
+                tw = th * 4
+            for ty in range(py, py + pbh, th):
+                for tx in range(px, px + pbw, tw):
+                    if tx >= pw or ty >= ph:
+                        continue
+                    own = owner[pl]
+                    flags = (INTRA_HAVE_LEFT if tx > 0 else 0) | (INTRA_HAVE_TOP if ty > 0 else 0)
+                    flags |= INTRA_EDGE_FILTER if edge_filter else 0
+                    flags |= INTRA_SMOOTH_NB if rng.random() < 0.3 else 0
+                    if ty > 0 and tx + tw < pw and (own[ty - 1, tx + tw:min(tx + 2 * tw, pw)] >= 0).all() \
+                            and rng.random() < 0.85:
+                        flags |= INTRA_TOP_RIGHT
+                    if tx > 0 and ty + th < ph and (own[ty + th:min(ty + 2 * th, ph), tx - 1] >= 0).all() \
+                            and rng.random() < 0.85:
+                        flags |= INTRA_BOTTOM_LEFT
+                    # dependency level from every pixel the edge may read
+                    deps = []
+                    if tx > 0:
+                        deps.append(own[ty:min(ty + 2 * th, ph), tx - 1])
+                    if ty > 0:
+                        deps.append(own[ty - 1, max(tx - 1, 0):min(tx + 2 * tw, pw)])
+                    lv = 0
+                    for d in deps:
+                        d = d[d >= 0]
+                        if d.size:
+                            lv = max(lv, 1 + max(level_of[i] for i in np.unique(d)))
+                    mode, angle, filt, alpha, aux, poff = 0, 0, 0, 0, 0, 0
+                    r = rng.random()
+                    if r < pal_frac:
+                        mode = 64
+                        pal.append(rng.integers(0, 1 << bpc, size=8).astype(dt))
+                        poff, n_pal = n_pal, n_pal + 8
+                        idx.append(rng.integers(0, 8, size=tw * th).astype(np.uint8))
+                        aux, n_idx = n_idx, n_idx + tw * th
+                    elif pl and r < pal_frac + cfl_frac:
+                        mode = 32
+                        alpha = int(rng.integers(-16, 17))
+                        ac.append(rng.integers(-400, 401, size=tw * th).astype(np.int16))
+                        aux, n_ac = n_ac, n_ac + tw * th
+                    elif tw <= 32 and th <= 32 and r < pal_frac + cfl_frac + filter_frac:
+                        mode, filt = 13, int(rng.integers(0, 5))
+                    else:
+                        mode = int(rng.integers(0, 13))
+                        if 1 <= mode <= 8:
+                            angle = int(rng.integers(-3, 4))
+                        if mode in (0, 1, 2, 9) and rng.random() < ii_frac:
+                            flags |= INTRA_II
+                            idx.append(rng.integers(0, 65, size=tw * th).astype(np.uint8))
+                            aux, n_idx = n_idx, n_idx + tw * th
+                    k = len(recs)
+                    recs.append((tx, ty, tw, th, pl, mode, angle, flags, filt, alpha, pw, ph, pw - tx, ph - ty,
+                                 aux, poff, 0))
+                    level_of.append(lv)
+                    own[ty:ty + th, tx:tx + tw] = k
+    blocks = np.array(recs, dtype=INTRA_DTYPE)
+    lv = np.array(level_of, np.int64)
+    order = np.argsort(lv, kind="stable")
+    level_start = np.searchsorted(lv[order], np.arange(lv.max() + 2)).astype(np.int64)
+    cat = lambda xs, d: np.concatenate(xs) if xs else np.zeros(1, d)  # noqa: E731
+    return dict(blocks=blocks, order=order, level_start=level_start, ac=cat(ac, np.int16), idx=cat(idx, np.uint8),
+                pal=cat(pal, dt))

@@ -275,7 +275,8 @@ def _ipred_sigs(o):
                                   ctypes.c_int, ctypes.c_int]
     o.oracle_cfl_ac.argtypes = [_VP, _VP, ctypes.c_ssize_t] + [ctypes.c_int] * 7
     o.oracle_pal_pred.argtypes = [_VP, ctypes.c_ssize_t, _VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]
-    for n in ("oracle_intra_pred", "oracle_cfl_pred", "oracle_cfl_ac", "oracle_pal_pred"):
+    o.oracle_intra_blocks.argtypes = [_VP, _VP, ctypes.c_int, _VP, ctypes.c_int, _VP, _VP, _VP]
+    for n in ("oracle_intra_pred", "oracle_cfl_pred", "oracle_cfl_ac", "oracle_pal_pred", "oracle_intra_blocks"):
         getattr(o, n).restype = None
     o._ipred_ready = True
 
@@ -313,3 +314,19 @@ def pal_pred(pal, idx, w, h, bpc):
     dst = np.zeros((h, w), dt)
     o.oracle_pal_pred(ptr(dst), dst.strides[0], ptr(p), ptr(i), w, h, bpc)
     return dst
+
+
+def intra_blocks(planes, bpc, blocks, ac, idx, pal):
+    """Oracle recon_b_intra step over MiIntraBlock records in order (edges gathered from the
+    planes as they are being written). planes: padded plane buffers (copies returned)."""
+    o = load_oracle()
+    _ipred_sigs(o)
+    pl = [np.ascontiguousarray(p).copy() for p in planes]
+    while len(pl) < 3:
+        pl.append(pl[0])
+    pp = (ctypes.c_void_p * 3)(*[a.ctypes.data for a in pl])
+    ps = (ctypes.c_ssize_t * 2)(pl[0].strides[0], pl[1].strides[0])
+    b = np.ascontiguousarray(blocks)
+    a_, i_, p_ = (np.ascontiguousarray(x) for x in (ac, idx, pal))
+    o.oracle_intra_blocks(pp, ps, bpc, ptr(b), len(b), ptr(a_), ptr(i_), ptr(p_))
+    return pl[:len(planes)]
