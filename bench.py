@@ -6,7 +6,8 @@ One step = one frame through every GPU stage, inputs resident in HBM:
   add) -> deblock (all column edges, then all row edges) -> CDEF (D -> C) -> loop restoration
   (C + D -> O, the reference picture). Descriptors follow SURVEY.md §8(d) config 3.
 Film grain (output-only, configs[3] = 8K10) is timed separately on an 8K10 frame and
-reported under "film_grain_8k10"; it is not part of the headline step.
+reported under "film_grain_8k10"; the intra path (configs[1], 1080p8: intra prediction +
+itx per dependency level) under "intra_1080p8". Neither is part of the headline step.
 
 `python bench.py` runs 1 GPU. Under torch.distributed.run every rank drives its own GPU on
 its own independent stream (replicas; no data-path collective; "scaling": "weak"); the
@@ -175,6 +176,46 @@ def pmc_traffic(stage):
     return None if ent is None else ent.get("hbm_bytes_per_step")
 
 
+def intra_1080p8(ctx, reps=5):
+    """configs[1]: a 1080p 8-bit 4:2:0 intra frame, intra prediction (device edge gathering)
+    + itx residual per dependency level (rav1d_amd.intra). Reported beside the headline, with
+    the level count that bounds it; the level sequence is replayed as a HIP graph."""
+    from rav1d_amd.intra import IntraFrame, make_intra_residuals
+    from rav1d_amd.ipred_synth import make_intra_frame
+    w, h, bpc = 1920, 1080, 8
+    rng = np.random.default_rng(0x1A7A0001)
+    fr = make_intra_residuals(make_intra_frame(w, h, bpc, 1, rng), bpc, rng)
+    cur = F.Frame(w, h, bpc, 1)
+    pic = cur.picture()
+    intra = IntraFrame(ctx, fr)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        intra.step(pic, s)
+        s.synchronize()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record(s)
+        for _ in range(reps):
+            intra.step(pic, s)
+        ev[1].record(s)
+        s.synchronize()
+        eager_ms = ev[0].elapsed_time(ev[1]) / reps
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            intra.step(pic, s)
+        g.replay()
+        s.synchronize()
+        ev[0].record(s)
+        for _ in range(reps):
+            g.replay()
+        ev[1].record(s)
+        s.synchronize()
+        graph_ms = ev[0].elapsed_time(ev[1]) / reps
+    ms = min(eager_ms, graph_ms)
+    return dict(mpx_per_s=round(w * h / (ms / 1e3) / 1e6, 1), ms_per_frame=round(ms, 3),
+                eager_ms=round(eager_ms, 3), graph_ms=round(graph_ms, 3), levels=len(intra.levels),
+                tx_blocks=int(len(fr["blocks"])), launches_per_frame=2 * len(intra.levels))
+
+
 def cpu_baseline(fr, budget_s=20.0):
     """The oracle (single-threaded C restatement, oracle/) on a bounded sample of the same
     workload: whole 4K10 inter frames through all stages until ~budget_s. Luma Mpixels/s."""
@@ -198,6 +239,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fg", action="store_true", help="skip the separate 8K10 film-grain measurement")
+    ap.add_argument("--no-intra", action="store_true", help="skip the separate 1080p8 intra measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -270,6 +312,8 @@ def main():
         }
         if world == 1 and not args.no_fg:
             out["film_grain_8k10"] = film_grain_8k(ctx, stream)
+        if world == 1 and not args.no_intra:
+            out["intra_1080p8"] = intra_1080p8(ctx)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(fr)
         print(json.dumps(out))

@@ -69,3 +69,27 @@ def test_intra_frame_block_mix(gpu, sb, min_bs):
     exp = oracle_lib.intra_blocks(init, bpc, fr["blocks"], fr["ac"], fr["idx"], fr["pal"])
     for p in range(len(cur.planes)):
         assert np.array_equal(cur.buffer_np(p), exp[p]), f"plane {p}"
+
+
+@pytest.mark.parametrize("bpc,layout", [(8, 1), (10, 1), (12, 3), (8, 0)])
+def test_intra_recon_with_residuals(gpu, bpc, layout):
+    """Full intra reconstruction (IntraFrame: per level, prediction then itx residual) vs the
+    oracle's interleaved per-block predict + itxfm_add in decode order."""
+    from rav1d_amd.intra import IntraFrame, make_intra_residuals
+    w, h = 192, 128
+    rng = np.random.default_rng(bpc * 31 + layout)
+    fr = make_intra_residuals(make_intra_frame(w, h, bpc, layout, rng), bpc, rng)
+    cur = Frame(w, h, bpc, layout)
+    init = [cur.buffer_np(p) for p in range(len(cur.planes))]
+    IntraFrame(gpu, fr).step(cur.picture())
+    torch.cuda.synchronize()
+    exp = [p.copy() for p in init]
+    for k in range(len(fr["blocks"])):
+        exp = oracle_lib.intra_blocks(exp, bpc, fr["blocks"][k:k + 1], fr["ac"], fr["idx"], fr["pal"])
+        t = fr["tx_blocks"][fr["tx_of_block"][k]:fr["tx_of_block"][k] + 1]
+        exp = oracle_lib.itx_frame(exp, t, fr["coef"].copy(), bpc)
+    for p in range(len(cur.planes)):
+        got = cur.buffer_np(p)
+        if not np.array_equal(got, exp[p]):
+            bad = np.argwhere(got != exp[p])
+            raise AssertionError(f"plane {p}: {len(bad)} mismatches, first at {bad[0]}")
