@@ -7,7 +7,7 @@ OUT=$R/gpurun_out
 mkdir -p $OUT
 TAG=${1:-run}
 cd $R
-timeout -k 10 900 python -m pytest tests -q -m gpu -x > $OUT/pytest_gpu_$TAG.log 2>&1 || { tail -30 $OUT/pytest_gpu_$TAG.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1 || { tail -30 $OUT/pytest_gpu_$TAG.log; exit 1; }
 tail -3 $OUT/pytest_gpu_$TAG.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 || { tail -20 $OUT/smoke_$TAG.log; exit 1; }
 tail -1 $OUT/smoke_$TAG.log
