@@ -3,7 +3,7 @@
 
 One step = one frame through every GPU stage, inputs resident in HBM:
   MC (inter prediction of every block from 2 resident reference pictures) -> itx (residual
-  add) -> deblock (all column edges, then all row edges) -> CDEF (D -> C) -> loop restoration
+  add) -> deblock (A -> D, 64x64 tiles: column edges then row edges) -> CDEF (D -> C) -> loop restoration
   (C + D -> O, the reference picture). Descriptors follow SURVEY.md §8(d) config 3.
 Film grain (output-only, configs[3] = 8K10) is timed separately on an 8K10 frame and
 reported under "film_grain_8k10"; the intra path (configs[1], 1080p8: intra prediction +
@@ -42,7 +42,8 @@ class Pipeline:
     def __init__(self, ctx, fr):
         self.ctx, self.fr = ctx, fr
         w, h, bpc, lay = fr["w"], fr["h"], fr["bpc"], fr["layout"]
-        self.A = F.Frame(w, h, bpc, lay)      # prediction -> recon -> deblocked (in place)
+        self.A = F.Frame(w, h, bpc, lay)      # prediction -> reconstruction
+        self.D = F.Frame(w, h, bpc, lay)      # deblocked (out of place: one fused tile launch)
         self.B = F.Frame(w, h, bpc, lay)      # CDEF output
         self.O = F.Frame(w, h, bpc, lay)      # LR output (the reference frame)
         self.G = F.Frame(w, h, bpc, lay) if fr["fg"] else None   # displayed picture with film grain
@@ -77,9 +78,9 @@ class Pipeline:
         }
         if self.mc is not None:
             self.algo["mc"] = mc_algorithmic_bytes(fr["mc"][0], bpc) + fr["mc"][2].nbytes
-        # kernel launches per stage per frame: mc = luma + chroma group, deblock = cols + rows
-        self.launches = {"mc": 2, "itx": 1, "deblock": 2, "cdef": 1, "lr": 1, "fg": 1}
-        self.kernels = {"mc": "mc_kernel", "itx": "itx_frame_kernel", "deblock": "lf_cols_kernel+lf_rows_kernel",
+        # kernel launches per stage per frame: mc = luma + chroma group
+        self.launches = {"mc": 2, "itx": 1, "deblock": 1, "cdef": 1, "lr": 1, "fg": 1}
+        self.kernels = {"mc": "mc_kernel", "itx": "itx_frame_kernel", "deblock": "lf_tile_kernel",
                         "cdef": "cdef_kernel", "lr": "lr_kernel", "fg": "fg_apply_kernel"}
 
     def step(self, stream, ev=None):
@@ -87,7 +88,7 @@ class Pipeline:
         lib = F.lib()
         ctx = self.ctx.h
         sp = F._stream_ptr(stream)
-        pa, pb, po = self.A.picture(), self.B.picture(), self.O.picture()
+        pa, pb, po, pd = self.A.picture(), self.B.picture(), self.O.picture(), self.D.picture()
 
         prep_done = None
         if self.fgd is not None:
@@ -117,10 +118,11 @@ class Pipeline:
         ss = (ctypes.c_uint32 * 20)(*[int(v) for v in self.fr["size_start"]])
         timed("itx", lambda: F.check(lib.mi_itx_frame(ctx, ctypes.byref(pa), ctypes.c_void_p(self.blocks.data_ptr()),
                                                       ss, ctypes.c_void_p(self.coef.data_ptr()), ITX_KEEP_COEFS, sp), "itx"))
-        timed("deblock", lambda: F.check(lib.mi_deblock_frame(ctx, ctypes.byref(pa), ctypes.byref(self.lf.s), sp), "lf"))
-        timed("cdef", lambda: F.check(lib.mi_cdef_frame(ctx, ctypes.byref(pa), ctypes.byref(pb),
+        timed("deblock", lambda: F.check(lib.mi_deblock_frame_to(ctx, ctypes.byref(pa), ctypes.byref(pd),
+                                                                 ctypes.byref(self.lf.s), sp), "lf"))
+        timed("cdef", lambda: F.check(lib.mi_cdef_frame(ctx, ctypes.byref(pd), ctypes.byref(pb),
                                                         ctypes.byref(self.cdef.s), sp), "cdef"))
-        timed("lr", lambda: F.check(lib.mi_lr_frame(ctx, ctypes.byref(pb), ctypes.byref(pa), ctypes.byref(po),
+        timed("lr", lambda: F.check(lib.mi_lr_frame(ctx, ctypes.byref(pb), ctypes.byref(pd), ctypes.byref(po),
                                                     ctypes.byref(self.lr.s), sp), "lr"))
         if self.fgd is not None:
             pg = self.G.picture()

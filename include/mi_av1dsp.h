@@ -305,6 +305,15 @@ int mi_intra_blocks(MiCtx *ctx, const MiPicture *pic, const MiIntraBlock *blocks
 
 int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, void *stream);
 
+/* Deblocking out of place: reads the reconstruction `src` (never written), writes the
+ * deblocked picture to `dst` over the 128-aligned plane area (dav1d's default picture
+ * geometry, src/picture.rs:98-115). One launch of 64x64 plane tiles, each filtering every
+ * column edge and then every row edge that reaches it from an LDS copy with a 16/12-px halo;
+ * bit-identical to mi_deblock_frame. Planes and strides must be 16-byte aligned. With
+ * src == dst it runs mi_deblock_frame (in place). */
+int mi_deblock_frame_to(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const MiLoopFilter *lf,
+                        void *stream);
+
 /* Motion compensation for a whole frame: writes the inter prediction of every unit into
  * `cur` (itx then adds the residual). `refs` (host array of nrefs pictures, device planes,
  * grain-free, same size as cur) are read with edge replication (emu_edge, mc_tmpl.c:798-845).

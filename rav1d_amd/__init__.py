@@ -131,6 +131,8 @@ def lib():
     _sig(L, "mi_ipred_blocks", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.c_int, _VP, _VP, _VP, _VP])
     _sig(L, "mi_dsp_intra_pred", ctypes.c_int, [ctypes.c_int, _VP, ctypes.c_ssize_t, _VP] + [ctypes.c_int] * 6)
     _sig(L, "mi_deblock_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiLoopFilter), _VP])
+    _sig(L, "mi_deblock_frame_to", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
+                                                  ctypes.POINTER(MiLoopFilter), _VP])
     _sig(L, "mi_cdef_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
                                             ctypes.POINTER(MiCdef), _VP])
     _sig(L, "mi_lr_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
@@ -146,7 +148,7 @@ def lib():
 # Every symbol include/mi_av1dsp.h declares (checked by tests/test_abi.py).
 EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
             "mi_itx_frame", "mi_mc_frame", "mi_mc_scaled", "mi_mc_warp", "mi_mc_combine", "mi_superres_frame",
-            "mi_ipred_blocks", "mi_intra_blocks", "mi_deblock_frame", "mi_cdef_frame", "mi_lr_frame",
+            "mi_ipred_blocks", "mi_intra_blocks", "mi_deblock_frame", "mi_deblock_frame_to", "mi_cdef_frame", "mi_lr_frame",
             "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply",
             "mi_dsp_itxfm_add", "mi_dsp_intra_pred"]
 

@@ -337,6 +337,69 @@ int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, v
     return r ? fail(ctx, -EIO) : 0;
 }
 
+int mi_deblock_frame_to(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const MiLoopFilter *lf,
+                        void *stream) {
+    if (!ctx || !src || !dst || !lf) return fail(ctx, -EINVAL);
+    if (src->bpc != 8 && src->bpc != 10 && src->bpc != 12) return fail(ctx, -EINVAL);
+    if (!same_geometry(src, dst)) return fail(ctx, -EINVAL);
+    if (src->data[0] == dst->data[0]) return mi_deblock_frame(ctx, dst, lf, stream);
+    const int sh = src->layout == 1 || src->layout == 2, sv = src->layout == 1;
+    const int nplanes = src->layout == 0 ? 1 : 3;
+    const size_t px = src->bpc == 8 ? 1 : 2;
+    const int sb128w = (src->w + 127) >> 7, sb128h = (src->h + 127) >> 7;
+    for (int p = 0; p < nplanes; p++)
+        if (src->stride[p ? 1 : 0] % 16 || (uintptr_t)src->data[p] % 16 || (uintptr_t)dst->data[p] % 16 ||
+            src->stride[p ? 1 : 0] < (ptrdiff_t)(((sb128w * 128) >> (p ? sh : 0)) * px))
+            return fail(ctx, -EINVAL);
+    if (!lf->filter_y) {   // deblocking off for the frame: the output is the input
+        for (int p = 0; p < nplanes; p++) {
+            const size_t rows = (size_t)(sb128h * 128) >> (p ? sv : 0);
+            const ptrdiff_t s = src->stride[p ? 1 : 0];
+            if (hipMemcpyAsync(dst->data[p], src->data[p], rows * s, hipMemcpyDeviceToDevice,
+                               (hipStream_t)stream) != hipSuccess)
+                return fail(ctx, -EIO);
+        }
+        return 0;
+    }
+    if (!lf->level || !lf->masks || lf->sb128w != sb128w || lf->b4_stride < (int64_t)sb128w * 32)
+        return fail(ctx, -EINVAL);
+    mi::LfTileArgs a;
+    memset(&a, 0, sizeof(a));
+    a.level = (const uint32_t *)lf->level;
+    a.b4_stride = lf->b4_stride;
+    a.masks = lf->masks;
+    a.sb128w = sb128w;
+    a.w4 = (src->w + 3) >> 2;
+    a.h4 = (src->h + 3) >> 2;
+    a.ss_hor = sh;
+    a.ss_ver = sv;
+    a.bdmax = (1 << src->bpc) - 1;
+    a.bdm8 = src->bpc - 8;
+    const int filter_uv = src->layout != 0 && lf->filter_uv;
+    memcpy(a.lim_e, lf->lim_e, 64);
+    memcpy(a.lim_i, lf->lim_i, 64);
+    int n = 0;
+    for (int p = 0; p < 3; p++) {
+        a.tile_start[p] = n;
+        if (p >= nplanes) continue;
+        const int h = p ? sh : 0, v = p ? sv : 0;
+        a.src[p] = (const uint8_t *)src->data[p];
+        a.dst[p] = (uint8_t *)dst->data[p];
+        a.stride[p] = src->stride[p ? 1 : 0];
+        a.pw[p] = (sb128w * 128) >> h;
+        a.ph[p] = (sb128h * 128) >> v;
+        // filter_uv off: chroma tiles are copies (no edge codes)
+        a.cols_ux[p] = p && !filter_uv ? 0 : (a.w4 + h) >> h;
+        a.cols_rows[p] = p && !filter_uv ? 0 : a.ph[p];
+        a.rows_px[p] = p && !filter_uv ? 0 : a.pw[p];
+        a.rows_uy[p] = p && !filter_uv ? 0 : p ? sb128h * (32 >> v) : a.h4;
+        a.tiles_x[p] = (a.pw[p] + 63) / 64;
+        n += a.tiles_x[p] * ((a.ph[p] + 63) / 64);
+    }
+    a.tile_start[3] = n;
+    return mi::launch_deblock_tiles(a, src->bpc, (hipStream_t)stream) ? fail(ctx, -EIO) : 0;
+}
+
 int mi_cdef_frame(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const MiCdef *cd,
                   void *stream) {
     if (!ctx || !src || !dst || !cd || !cd->masks) return fail(ctx, -EINVAL);

@@ -92,6 +92,22 @@ struct LfArgs {
     int units_x[3], rows[3];   // thread space per plane
     uint8_t lim_e[64], lim_i[64];
 };
+// fused out-of-place deblock (lf_tile_kernel): 64x64 plane tiles
+struct LfTileArgs {
+    const uint8_t *src[3];
+    uint8_t *dst[3];
+    int64_t stride[3];
+    const uint32_t *level;
+    int64_t b4_stride;
+    const MiAv1Filter *masks;
+    int sb128w, w4, h4, ss_hor, ss_ver, bdmax, bdm8;
+    int cols_ux[3], cols_rows[3];   // column edges: unit columns, pixel rows per plane
+    int rows_px[3], rows_uy[3];     // row edges: pixel columns, unit rows per plane
+    int pw[3], ph[3], tiles_x[3];   // staged plane area (128-aligned picture), tiles per row
+    int tile_start[4];
+    uint8_t lim_e[64], lim_i[64];
+};
+int launch_deblock_tiles(const LfTileArgs &a, int bpc, hipStream_t s);
 // launchers (lf.hip)
 int launch_deblock(const LfArgs &cols, const LfArgs &rows, int bpc, hipStream_t s);
 

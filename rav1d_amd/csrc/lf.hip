@@ -193,6 +193,335 @@ __global__ __launch_bounds__(256) void lf_rows_kernel(LfArgs a) {
     filter_line<Px>(q0, ps, wd, le[L], li[L], L >> 4, a.bdm8, a.bdmax);
 }
 
+// ---- fused, out-of-place deblock: one workgroup per 64x64 plane tile ----
+//
+// The tile plus a halo (16 px left/right, 12 rows above, 12 below) is staged in LDS once with
+// 16-B loads. All column edges whose footprint reaches the tile's columns are filtered over
+// every staged row, then all row edges whose footprint reaches the tile's rows over the
+// tile's columns, then the tile is stored with 16-B stores. This is "all column edges, then
+// all row edges" restricted to the tile, so the result equals the
+// two-pass kernels above. Out of place because a tile's halo must hold pre-filter pixels
+// while the neighbouring tile writes its own.
+//
+// Halo sizes: a row edge at e reads rows e-7..e+6 and writes e-6..e+5, so the row edges that
+// touch rows [y0, y0+64) are e in [y0-4, y0+68] (19 edges) and read rows [y0-11, y0+74]:
+// those rows must be column-filtered first; column edges e in [x0-4, x0+68] (19) read
+// columns [x0-11, x0+74].
+constexpr int kLfT = 64;                 // tile side (plane pixels)
+constexpr int kLfRows = kLfT + 24;       // staged rows: y0-12 .. y0+75
+constexpr int kLfCols = kLfT + 32;       // staged columns: x0-16 .. x0+79
+constexpr int kLfEdges = kLfT / 4 + 3;   // 19 edges per direction
+
+// The inputs of one edge unit's code, fetched with independent loads (no load depends on
+// another) so that a lane's units are all in flight at once.
+struct LfEdgeRaw {
+    uint16_t m[3];     // mask words for width index 0..2 (chroma: 0..1)
+    uint32_t lv, lvp;  // level word of the unit and of its left (dir 0) / upper (dir 1) neighbour
+    uint16_t bit;      // 0: the reference never filters this unit
+    uint8_t slot, luma;
+};
+
+// Column (dir 0) or row (dir 1) edge at 4-px unit (ux, uy) of plane p: the per-lane logic of
+// lf_cols/rows_kernel, split into fetch and decode.
+__device__ __forceinline__ LfEdgeRaw lf_edge_fetch(const LfTileArgs &a, int p, int dir, int ux, int uy) {
+    LfEdgeRaw r;
+    r.bit = 0; r.luma = p == 0; r.slot = p == 0 ? dir : 1 + p;
+    r.m[0] = r.m[1] = r.m[2] = 0; r.lv = r.lvp = 0;
+    if (ux <= 0 && dir == 0) return r;
+    if (uy <= 0 && dir == 1) return r;
+    if (ux < 0 || uy < 0) return r;
+    const uint16_t *m = nullptr;
+    int half = 0;
+    unsigned bit = 0;
+    if (dir == 0) {
+        if (ux >= a.cols_ux[p] || uy * 4 >= a.cols_rows[p]) return r;
+        if (p == 0) {
+            const int X = ux >> 5, x = ux & 31, Y = uy >> 5, yy = uy & 31;
+            half = yy >> 4;
+            if (half && a.h4 - 32 * Y <= 16) return r;
+            bit = 1u << (yy & 15);
+            m = &a.masks[Y * a.sb128w + X].filter_y[0][x][0][0];
+        } else {
+            const int csw = 32 >> a.ss_hor, csh = 32 >> a.ss_ver, hb = 16 >> a.ss_ver;
+            const int X = ux / csw, x = ux % csw, Y = uy / csh, yy = uy % csh;
+            half = yy >= hb;
+            if (half && a.h4 - 32 * Y <= 16) return r;
+            if (x >= ((min(32, a.w4 - X * 32) + a.ss_hor) >> a.ss_hor)) return r;
+            bit = 1u << (yy - half * hb);
+            m = &a.masks[Y * a.sb128w + X].filter_uv[0][x][0][0];
+        }
+    } else {
+        if (ux * 4 >= a.rows_px[p] || uy >= a.rows_uy[p]) return r;
+        if (p == 0) {
+            const int X = ux >> 5, xx = ux & 31, Y = uy >> 5, y = uy & 31;
+            half = xx >> 4;
+            bit = 1u << (xx & 15);
+            m = &a.masks[Y * a.sb128w + X].filter_y[1][y][0][0];
+        } else {
+            const int csw = 32 >> a.ss_hor, csh = 32 >> a.ss_ver, hb = 16 >> a.ss_hor;
+            const int X = ux / csw, xx = ux % csw, Y = uy / csh, y = uy % csh;
+            if (y >= ((min(a.h4 - 32 * Y, 32) + a.ss_ver) >> a.ss_ver)) return r;
+            half = xx >= hb;
+            bit = 1u << (xx - half * hb);
+            m = &a.masks[Y * a.sb128w + X].filter_uv[1][y][0][0];
+        }
+    }
+    r.bit = (uint16_t)bit;
+    r.m[0] = m[half];
+    r.m[1] = m[2 + half];
+    if (p == 0) r.m[2] = m[4 + half];
+    const uint32_t *lv = a.level + (int64_t)uy * a.b4_stride + ux;
+    r.lv = lv[0];
+    r.lvp = lv[dir ? -a.b4_stride : -1];
+    return r;
+}
+
+// (wd << 8) | L, or 0 when the unit is not filtered
+__device__ __forceinline__ int lf_edge_decode(const LfEdgeRaw &r, int dir, int ux, int uy) {
+    if (!r.bit) return 0;
+    const int wd = r.luma ? ((r.m[2] & r.bit) ? 16 : (r.m[1] & r.bit) ? 8 : (r.m[0] & r.bit) ? 4 : 0)
+                          : ((r.m[1] & r.bit) ? 6 : (r.m[0] & r.bit) ? 4 : 0);
+    if (!wd) return 0;
+    int L = (r.lv >> (8 * r.slot)) & 0xff;
+    if (!L) L = (r.lvp >> (8 * r.slot)) & 0xff;
+    if (!L) return 0;
+    if ((dir ? uy : ux) * 4 < (wd == 16 ? 7 : wd / 2)) return 0;
+    return (wd << 8) | L;
+}
+
+// The filter of one pixel line on registers: v[8] = q0, v[7] = p0, v[1] = p6, v[14] = q6
+// (loopfilter.rs:396-721). Returns false when the line is left unchanged.
+__device__ __forceinline__ bool filter_regs(int (&v)[16], int wd, int E, int I, int H, int bdm8,
+                                            int bdmax) {
+    const int F = 1 << bdm8;
+    E <<= bdm8; I <<= bdm8; H <<= bdm8;
+    const int p1 = v[6], p0 = v[7], q0 = v[8], q1 = v[9];
+    bool fm = abs(p1 - p0) <= I && abs(q1 - q0) <= I && abs(p0 - q0) * 2 + (abs(p1 - q1) >> 1) <= E;
+    const int p2 = v[5], q2 = v[10], p3 = v[4], q3 = v[11];
+    if (wd > 4) fm = fm && abs(p2 - p1) <= I && abs(q2 - q1) <= I;
+    if (wd > 6) fm = fm && abs(p3 - p2) <= I && abs(q3 - q2) <= I;
+    if (!fm) return false;
+    bool flat_in = false;
+    if (wd >= 6) flat_in = abs(p2 - p0) <= F && abs(p1 - p0) <= F && abs(q1 - q0) <= F && abs(q2 - q0) <= F;
+    if (wd >= 8) flat_in = flat_in && abs(p3 - p0) <= F && abs(q3 - q0) <= F;
+    if (wd == 16 && flat_in) {
+        const bool flat_out = abs(v[1] - p0) <= F && abs(v[2] - p0) <= F && abs(v[3] - p0) <= F &&
+                              abs(v[12] - q0) <= F && abs(v[13] - q0) <= F && abs(v[14] - q0) <= F;
+        if (flat_out) {
+            // 13-tap smoother: the output at v[j] (j = 2..13) is S_j >> 4 with
+            // S_j = sum_{t=-6..6} v[clamp(j+t, 1, 14)] + v[j-1] + v[j] + v[j+1]; S_{j+1} - S_j =
+            // v[clamp(j+7)] - v[clamp(j-6)] + v[j+2] - v[j-1], so one running sum serves all 12
+            int o[12];
+            int s = 8 + 6 * v[1] + v[2] + v[3] + v[4] + v[5] + v[6] + v[7] + v[8] + v[1] + v[2] + v[3];
+#pragma unroll
+            for (int k = 0; k < 12; k++) {
+                const int j = k + 2;
+                o[k] = s >> 4;
+                if (k < 11) {
+                    const int hi = j + 7 > 14 ? 14 : j + 7, lo = j - 6 < 1 ? 1 : j - 6;
+                    s += v[hi] - v[lo] + v[j + 2] - v[j - 1];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 12; k++) v[2 + k] = o[k];
+            return true;
+        }
+    }
+    if (wd >= 8 && flat_in) {
+        v[5] = (3 * p3 + 2 * p2 + p1 + p0 + q0 + 4) >> 3;
+        v[6] = (2 * p3 + p2 + 2 * p1 + p0 + q0 + q1 + 4) >> 3;
+        v[7] = (p3 + p2 + p1 + 2 * p0 + q0 + q1 + q2 + 4) >> 3;
+        v[8] = (p2 + p1 + p0 + 2 * q0 + q1 + q2 + q3 + 4) >> 3;
+        v[9] = (p1 + p0 + q0 + 2 * q1 + q2 + 2 * q3 + 4) >> 3;
+        v[10] = (p0 + q0 + q1 + 2 * q2 + 3 * q3 + 4) >> 3;
+    } else if (wd == 6 && flat_in) {
+        v[6] = (3 * p2 + 2 * p1 + 2 * p0 + q0 + 4) >> 3;
+        v[7] = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
+        v[8] = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
+        v[9] = (p0 + 2 * q0 + 2 * q1 + 3 * q2 + 4) >> 3;
+    } else {
+        const int dlo = -(128 << bdm8), dhi = (128 << bdm8) - 1;
+        const bool hev = abs(p1 - p0) > H || abs(q1 - q0) > H;
+        int f = hev ? min(max(p1 - q1, dlo), dhi) : 0;
+        f = min(max(3 * (q0 - p0) + f, dlo), dhi);
+        const int f1 = min(f + 4, dhi) >> 3;
+        const int f2 = min(f + 3, dhi) >> 3;
+        v[7] = min(max(p0 + f2, 0), bdmax);
+        v[8] = min(max(q0 - f1, 0), bdmax);
+        if (!hev) {
+            const int g = (f1 + 1) >> 1;
+            v[6] = min(max(p1 + g, 0), bdmax);
+            v[9] = min(max(q1 - g, 0), bdmax);
+        }
+    }
+    return true;
+}
+
+// first and one-past-last v[] index a filter of width wd may change
+__device__ __forceinline__ int lf_wlo(int wd) { return wd == 16 ? 2 : wd == 8 ? 5 : 6; }
+
+// wd -> work class (lines of one class run the same filter branch)
+__device__ __forceinline__ int lf_class(int wd) { return wd == 4 ? 0 : wd == 6 ? 1 : wd == 8 ? 2 : 3; }
+
+template <typename Px>
+__global__ __launch_bounds__(256) void lf_tile_kernel(LfTileArgs a) {
+    constexpr int VB = 16;                        // bytes per vector
+    constexpr int VPX = VB / sizeof(Px);          // pixels per vector
+    constexpr int P = kLfCols;                    // LDS pitch in pixels
+    constexpr int NV = (kLfRows / 4) * kLfEdges;  // column-edge units (4 lines each)
+    constexpr int NH = kLfEdges * (kLfT / 4);     // row-edge units
+    __shared__ __attribute__((aligned(16))) Px t[kLfRows * P];
+    // work lists: active edge units bucketed by width class, so that the lanes of a wave run
+    // one filter branch; entry = (unit index << 6) | L
+    __shared__ uint16_t listv[4][NV], listh[4][NH];
+    __shared__ int cnt[8];
+    __shared__ uint8_t le[64], li[64];
+    const int tid = threadIdx.x;
+    const int b = xcd_block(blockIdx.x, gridDim.x);
+    const int p = b < a.tile_start[1] ? 0 : b < a.tile_start[2] ? 1 : 2;
+    const int lb = b - a.tile_start[p];
+    const int x0 = (lb % a.tiles_x[p]) * kLfT, y0 = (lb / a.tiles_x[p]) * kLfT;
+    const int pw = a.pw[p], ph = a.ph[p];
+    const int64_t st = a.stride[p];
+    const uint8_t *src = a.src[p];
+    if (tid < 64) { le[tid] = a.lim_e[tid]; li[tid] = a.lim_i[tid]; }
+    if (tid < 8) cnt[tid] = 0;
+    __syncthreads();
+    // Stage rows y0-12 .. y0+75, columns x0-16 .. x0+79 (pixels outside the plane read as 0:
+    // no edge reaches them), and fetch every edge unit's mask and level words. All of these
+    // loads are independent and issued before any is used.
+    constexpr int VPR = P / VPX;                  // vectors per staged row
+    constexpr int NS = (kLfRows * VPR + 255) / 256;
+    constexpr int NU = (NV + NH + 255) / 256;
+    uint4 sv[NS];
+#pragma unroll
+    for (int j = 0; j < NS; j++) {
+        const int i = tid + 256 * j;
+        const int r = i / VPR, c = (i % VPR) * VPX;
+        const int y = y0 - 12 + r, x = x0 - 16 + c;
+        sv[j] = make_uint4(0, 0, 0, 0);
+        if (i < kLfRows * VPR && y >= 0 && y < ph && x >= 0 && x < pw)
+            sv[j] = *reinterpret_cast<const uint4 *>(src + (int64_t)y * st + (int64_t)x * sizeof(Px));
+    }
+    // Edge units. The outermost edge of each direction (k = 0, 18) reaches the tile only
+    // with the 16-wide filter (it writes e-6 .. e+5); narrower ones are skipped there.
+    const int ux0 = (x0 >> 2) - 1, uy0 = (y0 >> 2) - 3;   // unit of the first edge / staged row
+    LfEdgeRaw raw[NU];
+#pragma unroll
+    for (int j = 0; j < NU; j++) {
+        const int i = tid + 256 * j;
+        const bool v = i < NV;
+        const int u = v ? i : i - NV;
+        raw[j].bit = 0;
+#ifdef MI_LF_NOFETCH
+        if (0)
+#else
+        if (i < NV + NH)
+#endif
+            raw[j] = v ? lf_edge_fetch(a, p, 0, ux0 + u % kLfEdges, uy0 + u / kLfEdges)
+                       : lf_edge_fetch(a, p, 1, (x0 >> 2) + u % (kLfT / 4), (y0 >> 2) - 1 + u / (kLfT / 4));
+    }
+#pragma unroll
+    for (int j = 0; j < NS; j++) {
+        const int i = tid + 256 * j;
+        if (i < kLfRows * VPR) *reinterpret_cast<uint4 *>(&t[(i / VPR) * P + (i % VPR) * VPX]) = sv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < NU; j++) {
+        const int i = tid + 256 * j;
+        const bool v = i < NV;
+        const int u = v ? i : i - NV;
+        const int k = v ? u % kLfEdges : u / (kLfT / 4);
+        const int code = v ? lf_edge_decode(raw[j], 0, ux0 + k, 0)
+                           : lf_edge_decode(raw[j], 1, 0, (y0 >> 2) - 1 + k);
+        const int wd = code >> 8;
+        if (!wd || ((k == 0 || k == kLfEdges - 1) && wd != 16)) continue;
+        const int c = lf_class(wd);
+        const int slot = atomicAdd(&cnt[(v ? 0 : 4) + c], 1);
+        (v ? listv[c] : listh[c])[slot] = (uint16_t)((u << 6) | (code & 63));
+    }
+    __syncthreads();
+    // column edges: 4 lines per unit; the 16-px window [e-8, e+8) is 4 aligned 4-px quads
+    {
+        const int c0 = cnt[0] * 4, c1 = c0 + cnt[1] * 4, c2 = c1 + cnt[2] * 4, c3 = c2 + cnt[3] * 4;
+        for (int i = tid; i < c3; i += 256) {
+            const int c = i < c0 ? 0 : i < c1 ? 1 : i < c2 ? 2 : 3;
+            const int base = c == 0 ? 0 : c == 1 ? c0 : c == 2 ? c1 : c2;
+            const int e = listv[c][(i - base) >> 2];
+            const int u = e >> 6, L = e & 63;
+            const int wd = c == 0 ? 4 : c == 1 ? 6 : c == 2 ? 8 : 16;
+            const int r = (u / kLfEdges) * 4 + (i & 3), k = u % kLfEdges;
+            Px *w = &t[r * P + 4 + 4 * k];
+            int v[16];
+            if constexpr (sizeof(Px) == 2) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint2 d = reinterpret_cast<const uint2 *>(w)[q];
+                    v[4 * q] = d.x & 0xffff; v[4 * q + 1] = d.x >> 16;
+                    v[4 * q + 2] = d.y & 0xffff; v[4 * q + 3] = d.y >> 16;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t d = reinterpret_cast<const uint32_t *>(w)[q];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) v[4 * q + j] = (d >> (8 * j)) & 0xff;
+                }
+            }
+            if (!filter_regs(v, wd, le[L], li[L], L >> 4, a.bdm8, a.bdmax)) continue;
+            const int lo = lf_wlo(wd);
+#pragma unroll
+            for (int j = 2; j < 14; j++)
+                if (j >= lo && j < 16 - lo) w[j] = (Px)v[j];
+        }
+    }
+    __syncthreads();
+    // row edges: 4 pixel columns per unit
+    {
+        const int c0 = cnt[4] * 4, c1 = c0 + cnt[5] * 4, c2 = c1 + cnt[6] * 4, c3 = c2 + cnt[7] * 4;
+        for (int i = tid; i < c3; i += 256) {
+            const int c = i < c0 ? 0 : i < c1 ? 1 : i < c2 ? 2 : 3;
+            const int base = c == 0 ? 0 : c == 1 ? c0 : c == 2 ? c1 : c2;
+            const int e = listh[c][(i - base) >> 2];
+            const int u = e >> 6, L = e & 63;
+            const int wd = c == 0 ? 4 : c == 1 ? 6 : c == 2 ? 8 : 16;
+            const int k = u / (kLfT / 4), col = (u % (kLfT / 4)) * 4 + (i & 3);
+            // edge row e = y0 - 4 + 4k sits at staged row 8 + 4k; v[8] is that row
+            Px *w = &t[(4 * k) * P + 16 + col];
+            int v[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) v[j] = 0;
+            const int n = wd == 16 ? 7 : wd == 8 ? 4 : wd == 6 ? 3 : 2;
+#pragma unroll
+            for (int j = 1; j < 15; j++)
+                if (j >= 8 - n && j < 8 + n) v[j] = w[j * P];
+            if (!filter_regs(v, wd, le[L], li[L], L >> 4, a.bdm8, a.bdmax)) continue;
+            const int lo = lf_wlo(wd);
+#pragma unroll
+            for (int j = 2; j < 14; j++)
+                if (j >= lo && j < 16 - lo) w[j * P] = (Px)v[j];
+        }
+    }
+    __syncthreads();
+    uint8_t *dst = a.dst[p];
+    constexpr int VPT = kLfT / VPX;
+    for (int i = tid; i < kLfT * VPT; i += 256) {
+        const int r = i / VPT, c = (i % VPT) * VPX;
+        const int y = y0 + r, x = x0 + c;
+        if (y < ph && x < pw)
+            *reinterpret_cast<uint4 *>(dst + (int64_t)y * st + (int64_t)x * sizeof(Px)) =
+                *reinterpret_cast<const uint4 *>(&t[(12 + r) * P + 16 + c]);
+    }
+}
+
+int launch_deblock_tiles(const LfTileArgs &a, int bpc, hipStream_t s) {
+    const int n = a.tile_start[3];
+    if (!n) return 0;
+    if (bpc == 8) hipLaunchKernelGGL(lf_tile_kernel<uint8_t>, dim3(n), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(lf_tile_kernel<uint16_t>, dim3(n), dim3(256), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 int launch_deblock(const LfArgs &cols, const LfArgs &rows, int bpc, hipStream_t s) {
     const int nc = cols.blk_start[3], nr = rows.blk_start[3];
     if (bpc == 8) {

@@ -208,10 +208,16 @@ class LoopFilterMeta:
         self.s = s
 
 
-def deblock_frame(ctx, frame, meta, stream=None):
+def deblock_frame(ctx, frame, meta, stream=None, dst=None):
+    """In place (two launches: column edges, row edges) or, with `dst`, out of place (one
+    fused launch of 64x64 tiles)."""
     pic = frame.picture()
-    check(lib().mi_deblock_frame(ctx.h, ctypes.byref(pic), ctypes.byref(meta.s), _stream_ptr(stream)),
-          "mi_deblock_frame")
+    if dst is None:
+        check(lib().mi_deblock_frame(ctx.h, ctypes.byref(pic), ctypes.byref(meta.s), _stream_ptr(stream)),
+              "mi_deblock_frame")
+    else:
+        check(lib().mi_deblock_frame_to(ctx.h, ctypes.byref(pic), ctypes.byref(dst.picture()),
+                                        ctypes.byref(meta.s), _stream_ptr(stream)), "mi_deblock_frame_to")
 
 
 class CdefMeta:

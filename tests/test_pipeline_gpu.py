@@ -24,7 +24,7 @@ def test_pipeline_matches_oracle(gpu, geom):
     pipe.step(torch.cuda.current_stream())
     torch.cuda.synchronize()
     ref = oracle_pipeline(fr)
-    stages = [("recon_deblocked", pipe.A), ("cdef", pipe.B), ("lr", pipe.O)]
+    stages = [("recon_deblocked", pipe.D), ("cdef", pipe.B), ("lr", pipe.O)]
     if fg:
         stages.append(("out", pipe.G))
     for name, pic in stages:
