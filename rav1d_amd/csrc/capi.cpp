@@ -393,8 +393,8 @@ int mi_deblock_frame_to(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, 
         a.cols_rows[p] = p && !filter_uv ? 0 : a.ph[p];
         a.rows_px[p] = p && !filter_uv ? 0 : a.pw[p];
         a.rows_uy[p] = p && !filter_uv ? 0 : p ? sb128h * (32 >> v) : a.h4;
-        a.tiles_x[p] = (a.pw[p] + 63) / 64;
-        n += a.tiles_x[p] * ((a.ph[p] + 63) / 64);
+        a.tiles_x[p] = (a.pw[p] + mi::kLfTW - 1) / mi::kLfTW;
+        n += a.tiles_x[p] * ((a.ph[p] + mi::kLfTH - 1) / mi::kLfTH);
     }
     a.tile_start[3] = n;
     return mi::launch_deblock_tiles(a, src->bpc, (hipStream_t)stream) ? fail(ctx, -EIO) : 0;

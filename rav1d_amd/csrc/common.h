@@ -92,7 +92,11 @@ struct LfArgs {
     int units_x[3], rows[3];   // thread space per plane
     uint8_t lim_e[64], lim_i[64];
 };
-// fused out-of-place deblock (lf_tile_kernel): 64x64 plane tiles
+// fused out-of-place deblock (lf_tile_kernel): kLfTW x kLfTH plane tiles
+#ifndef MI_LF_TW
+#define MI_LF_TW 64   // 64x64 measured fastest at 4K10: 29.6 us vs 34.9 (128x64), 32.5 (32x64)
+#endif
+constexpr int kLfTW = MI_LF_TW, kLfTH = 64;
 struct LfTileArgs {
     const uint8_t *src[3];
     uint8_t *dst[3];

@@ -207,10 +207,10 @@ __global__ __launch_bounds__(256) void lf_rows_kernel(LfArgs a) {
 // touch rows [y0, y0+64) are e in [y0-4, y0+68] (19 edges) and read rows [y0-11, y0+74]:
 // those rows must be column-filtered first; column edges e in [x0-4, x0+68] (19) read
 // columns [x0-11, x0+74].
-constexpr int kLfT = 64;                 // tile side (plane pixels)
-constexpr int kLfRows = kLfT + 24;       // staged rows: y0-12 .. y0+75
-constexpr int kLfCols = kLfT + 32;       // staged columns: x0-16 .. x0+79
-constexpr int kLfEdges = kLfT / 4 + 3;   // 19 edges per direction
+constexpr int kLfRows = kLfTH + 24;       // staged rows: y0-12 .. y0+TH+11
+constexpr int kLfCols = kLfTW + 32;       // staged columns: x0-16 .. x0+TW+15
+constexpr int kLfEdgesV = kLfTW / 4 + 3;  // column edges reaching the tile
+constexpr int kLfEdgesH = kLfTH / 4 + 3;  // row edges reaching the tile
 
 // The inputs of one edge unit's code, fetched with independent loads (no load depends on
 // another) so that a lane's units are all in flight at once.
@@ -242,8 +242,9 @@ __device__ __forceinline__ LfEdgeRaw lf_edge_fetch(const LfTileArgs &a, int p, i
             bit = 1u << (yy & 15);
             m = &a.masks[Y * a.sb128w + X].filter_y[0][x][0][0];
         } else {
-            const int csw = 32 >> a.ss_hor, csh = 32 >> a.ss_ver, hb = 16 >> a.ss_ver;
-            const int X = ux / csw, x = ux % csw, Y = uy / csh, yy = uy % csh;
+            // csw = 32 >> ss_hor units per SB column, csh = 32 >> ss_ver, half = 16 >> ss_ver
+            const int lw = 5 - a.ss_hor, lh = 5 - a.ss_ver, hb = 16 >> a.ss_ver;
+            const int X = ux >> lw, x = ux & ((1 << lw) - 1), Y = uy >> lh, yy = uy & ((1 << lh) - 1);
             half = yy >= hb;
             if (half && a.h4 - 32 * Y <= 16) return r;
             if (x >= ((min(32, a.w4 - X * 32) + a.ss_hor) >> a.ss_hor)) return r;
@@ -258,8 +259,8 @@ __device__ __forceinline__ LfEdgeRaw lf_edge_fetch(const LfTileArgs &a, int p, i
             bit = 1u << (xx & 15);
             m = &a.masks[Y * a.sb128w + X].filter_y[1][y][0][0];
         } else {
-            const int csw = 32 >> a.ss_hor, csh = 32 >> a.ss_ver, hb = 16 >> a.ss_hor;
-            const int X = ux / csw, xx = ux % csw, Y = uy / csh, y = uy % csh;
+            const int lw = 5 - a.ss_hor, lh = 5 - a.ss_ver, hb = 16 >> a.ss_hor;
+            const int X = ux >> lw, xx = ux & ((1 << lw) - 1), Y = uy >> lh, y = uy & ((1 << lh) - 1);
             if (y >= ((min(a.h4 - 32 * Y, 32) + a.ss_ver) >> a.ss_ver)) return r;
             half = xx >= hb;
             bit = 1u << (xx - half * hb);
@@ -290,21 +291,21 @@ __device__ __forceinline__ int lf_edge_decode(const LfEdgeRaw &r, int dir, int u
 }
 
 // The filter of one pixel line on registers: v[8] = q0, v[7] = p0, v[1] = p6, v[14] = q6
-// (loopfilter.rs:396-721). Returns false when the line is left unchanged.
-__device__ __forceinline__ bool filter_regs(int (&v)[16], int wd, int E, int I, int H, int bdm8,
-                                            int bdmax) {
+// (loopfilter.rs:396-721), for a compile-time width. Returns false when the line is unchanged.
+template <int wd>
+__device__ __forceinline__ bool filter_regs(int (&v)[16], int E, int I, int H, int bdm8, int bdmax) {
     const int F = 1 << bdm8;
     E <<= bdm8; I <<= bdm8; H <<= bdm8;
     const int p1 = v[6], p0 = v[7], q0 = v[8], q1 = v[9];
     bool fm = abs(p1 - p0) <= I && abs(q1 - q0) <= I && abs(p0 - q0) * 2 + (abs(p1 - q1) >> 1) <= E;
     const int p2 = v[5], q2 = v[10], p3 = v[4], q3 = v[11];
-    if (wd > 4) fm = fm && abs(p2 - p1) <= I && abs(q2 - q1) <= I;
-    if (wd > 6) fm = fm && abs(p3 - p2) <= I && abs(q3 - q2) <= I;
+    if constexpr (wd > 4) fm = fm && abs(p2 - p1) <= I && abs(q2 - q1) <= I;
+    if constexpr (wd > 6) fm = fm && abs(p3 - p2) <= I && abs(q3 - q2) <= I;
     if (!fm) return false;
     bool flat_in = false;
-    if (wd >= 6) flat_in = abs(p2 - p0) <= F && abs(p1 - p0) <= F && abs(q1 - q0) <= F && abs(q2 - q0) <= F;
-    if (wd >= 8) flat_in = flat_in && abs(p3 - p0) <= F && abs(q3 - q0) <= F;
-    if (wd == 16 && flat_in) {
+    if constexpr (wd >= 6) flat_in = abs(p2 - p0) <= F && abs(p1 - p0) <= F && abs(q1 - q0) <= F && abs(q2 - q0) <= F;
+    if constexpr (wd >= 8) flat_in = flat_in && abs(p3 - p0) <= F && abs(q3 - q0) <= F;
+    if constexpr (wd == 16) if (flat_in) {
         const bool flat_out = abs(v[1] - p0) <= F && abs(v[2] - p0) <= F && abs(v[3] - p0) <= F &&
                               abs(v[12] - q0) <= F && abs(v[13] - q0) <= F && abs(v[14] - q0) <= F;
         if (flat_out) {
@@ -357,8 +358,78 @@ __device__ __forceinline__ bool filter_regs(int (&v)[16], int wd, int E, int I, 
     return true;
 }
 
-// first and one-past-last v[] index a filter of width wd may change
-__device__ __forceinline__ int lf_wlo(int wd) { return wd == 16 ? 2 : wd == 8 ? 5 : 6; }
+// Column edges of one width class: 4 lines per listed unit. The 16-px window [e-8, e+8) of
+// a line is 4 aligned 4-px quads of LDS. Write-back granules are chosen inside the span
+// no other edge of the direction touches (a wd-16 edge owns its whole window, a wd-8 edge
+// [e-4, e+4), a wd-4/6 edge [e-2, e+2)), so whole quads / pairs are stored.
+template <int WD, typename Px, int P>
+__device__ __forceinline__ void lf_cols_class(Px *t, const uint16_t *list, int n, const uint8_t *le,
+                                              const uint8_t *li, int bdm8, int bdmax) {
+    for (int i = threadIdx.x; i < n * 4; i += 256) {
+        const int e = list[i >> 2];
+        const int u = e >> 6, L = e & 63;
+        const int r = (u / kLfEdgesV) * 4 + (i & 3), k = u % kLfEdgesV;
+        Px *w = &t[r * P + 4 + 4 * k];
+        constexpr int q0 = WD == 16 ? 0 : 1, q1 = WD == 16 ? 4 : 3;   // quads loaded
+        int v[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) v[j] = 0;
+#pragma unroll
+        for (int q = q0; q < q1; q++) {
+            if constexpr (sizeof(Px) == 2) {
+                const uint2 d = reinterpret_cast<const uint2 *>(w)[q];
+                v[4 * q] = d.x & 0xffff; v[4 * q + 1] = d.x >> 16;
+                v[4 * q + 2] = d.y & 0xffff; v[4 * q + 3] = d.y >> 16;
+            } else {
+                const uint32_t d = reinterpret_cast<const uint32_t *>(w)[q];
+#pragma unroll
+                for (int j = 0; j < 4; j++) v[4 * q + j] = (d >> (8 * j)) & 0xff;
+            }
+        }
+        if (!filter_regs<WD>(v, le[L], li[L], L >> 4, bdm8, bdmax)) continue;
+        if constexpr (WD >= 8) {
+#pragma unroll
+            for (int q = q0; q < q1; q++) {
+                if constexpr (sizeof(Px) == 2)
+                    reinterpret_cast<uint2 *>(w)[q] = make_uint2(v[4 * q] | (v[4 * q + 1] << 16),
+                                                                 v[4 * q + 2] | (v[4 * q + 3] << 16));
+                else
+                    reinterpret_cast<uint32_t *>(w)[q] = v[4 * q] | (v[4 * q + 1] << 8) |
+                                                         (v[4 * q + 2] << 16) | (v[4 * q + 3] << 24);
+            }
+        } else {
+            if constexpr (sizeof(Px) == 2) {
+                reinterpret_cast<uint32_t *>(w)[3] = v[6] | (v[7] << 16);
+                reinterpret_cast<uint32_t *>(w)[4] = v[8] | (v[9] << 16);
+            } else {
+                reinterpret_cast<uint16_t *>(w)[3] = v[6] | (v[7] << 8);
+                reinterpret_cast<uint16_t *>(w)[4] = v[8] | (v[9] << 8);
+            }
+        }
+    }
+}
+
+// Row edges of one width class: 4 pixel columns per listed unit. Edge row e = y0 - 4 + 4k
+// sits at staged row 8 + 4k; v[8] is that row. (Two columns per lane with 2-pixel LDS
+// accesses measured slower: 28.8 -> 31.1 us at 4K10.)
+template <int WD, typename Px, int P>
+__device__ __forceinline__ void lf_rows_class(Px *t, const uint16_t *list, int n, const uint8_t *le,
+                                              const uint8_t *li, int bdm8, int bdmax) {
+    constexpr int nr = WD == 16 ? 7 : WD == 8 ? 4 : WD == 6 ? 3 : 2;   // rows read each side
+    constexpr int lo = WD == 16 ? 2 : WD == 8 ? 5 : 6;                 // rows [lo, 16 - lo) written
+    for (int i = threadIdx.x; i < n * 4; i += 256) {
+        const int e = list[i >> 2];
+        const int u = e >> 6, L = e & 63;
+        const int k = u / (kLfTW / 4), col = (u % (kLfTW / 4)) * 4 + (i & 3);
+        Px *w = &t[(4 * k) * P + 16 + col];
+        int v[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) v[j] = (j >= 8 - nr && j < 8 + nr) ? (int)w[j * P] : 0;
+        if (!filter_regs<WD>(v, le[L], li[L], L >> 4, bdm8, bdmax)) continue;
+#pragma unroll
+        for (int j = lo; j < 16 - lo; j++) w[j * P] = (Px)v[j];
+    }
+}
 
 // wd -> work class (lines of one class run the same filter branch)
 __device__ __forceinline__ int lf_class(int wd) { return wd == 4 ? 0 : wd == 6 ? 1 : wd == 8 ? 2 : 3; }
@@ -368,8 +439,8 @@ __global__ __launch_bounds__(256) void lf_tile_kernel(LfTileArgs a) {
     constexpr int VB = 16;                        // bytes per vector
     constexpr int VPX = VB / sizeof(Px);          // pixels per vector
     constexpr int P = kLfCols;                    // LDS pitch in pixels
-    constexpr int NV = (kLfRows / 4) * kLfEdges;  // column-edge units (4 lines each)
-    constexpr int NH = kLfEdges * (kLfT / 4);     // row-edge units
+    constexpr int NV = (kLfRows / 4) * kLfEdgesV; // column-edge units (4 lines each)
+    constexpr int NH = kLfEdgesH * (kLfTW / 4);   // row-edge units
     __shared__ __attribute__((aligned(16))) Px t[kLfRows * P];
     // work lists: active edge units bucketed by width class, so that the lanes of a wave run
     // one filter branch; entry = (unit index << 6) | L
@@ -380,7 +451,7 @@ __global__ __launch_bounds__(256) void lf_tile_kernel(LfTileArgs a) {
     const int b = xcd_block(blockIdx.x, gridDim.x);
     const int p = b < a.tile_start[1] ? 0 : b < a.tile_start[2] ? 1 : 2;
     const int lb = b - a.tile_start[p];
-    const int x0 = (lb % a.tiles_x[p]) * kLfT, y0 = (lb / a.tiles_x[p]) * kLfT;
+    const int x0 = (lb % a.tiles_x[p]) * kLfTW, y0 = (lb / a.tiles_x[p]) * kLfTH;
     const int pw = a.pw[p], ph = a.ph[p];
     const int64_t st = a.stride[p];
     const uint8_t *src = a.src[p];
@@ -418,8 +489,8 @@ __global__ __launch_bounds__(256) void lf_tile_kernel(LfTileArgs a) {
 #else
         if (i < NV + NH)
 #endif
-            raw[j] = v ? lf_edge_fetch(a, p, 0, ux0 + u % kLfEdges, uy0 + u / kLfEdges)
-                       : lf_edge_fetch(a, p, 1, (x0 >> 2) + u % (kLfT / 4), (y0 >> 2) - 1 + u / (kLfT / 4));
+            raw[j] = v ? lf_edge_fetch(a, p, 0, ux0 + u % kLfEdgesV, uy0 + u / kLfEdgesV)
+                       : lf_edge_fetch(a, p, 1, (x0 >> 2) + u % (kLfTW / 4), (y0 >> 2) - 1 + u / (kLfTW / 4));
     }
 #pragma unroll
     for (int j = 0; j < NS; j++) {
@@ -431,81 +502,30 @@ __global__ __launch_bounds__(256) void lf_tile_kernel(LfTileArgs a) {
         const int i = tid + 256 * j;
         const bool v = i < NV;
         const int u = v ? i : i - NV;
-        const int k = v ? u % kLfEdges : u / (kLfT / 4);
+        const int k = v ? u % kLfEdgesV : u / (kLfTW / 4);
         const int code = v ? lf_edge_decode(raw[j], 0, ux0 + k, 0)
                            : lf_edge_decode(raw[j], 1, 0, (y0 >> 2) - 1 + k);
         const int wd = code >> 8;
-        if (!wd || ((k == 0 || k == kLfEdges - 1) && wd != 16)) continue;
+        if (!wd || ((k == 0 || k == (v ? kLfEdgesV : kLfEdgesH) - 1) && wd != 16)) continue;
         const int c = lf_class(wd);
         const int slot = atomicAdd(&cnt[(v ? 0 : 4) + c], 1);
         (v ? listv[c] : listh[c])[slot] = (uint16_t)((u << 6) | (code & 63));
     }
     __syncthreads();
-    // column edges: 4 lines per unit; the 16-px window [e-8, e+8) is 4 aligned 4-px quads
-    {
-        const int c0 = cnt[0] * 4, c1 = c0 + cnt[1] * 4, c2 = c1 + cnt[2] * 4, c3 = c2 + cnt[3] * 4;
-        for (int i = tid; i < c3; i += 256) {
-            const int c = i < c0 ? 0 : i < c1 ? 1 : i < c2 ? 2 : 3;
-            const int base = c == 0 ? 0 : c == 1 ? c0 : c == 2 ? c1 : c2;
-            const int e = listv[c][(i - base) >> 2];
-            const int u = e >> 6, L = e & 63;
-            const int wd = c == 0 ? 4 : c == 1 ? 6 : c == 2 ? 8 : 16;
-            const int r = (u / kLfEdges) * 4 + (i & 3), k = u % kLfEdges;
-            Px *w = &t[r * P + 4 + 4 * k];
-            int v[16];
-            if constexpr (sizeof(Px) == 2) {
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const uint2 d = reinterpret_cast<const uint2 *>(w)[q];
-                    v[4 * q] = d.x & 0xffff; v[4 * q + 1] = d.x >> 16;
-                    v[4 * q + 2] = d.y & 0xffff; v[4 * q + 3] = d.y >> 16;
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const uint32_t d = reinterpret_cast<const uint32_t *>(w)[q];
-#pragma unroll
-                    for (int j = 0; j < 4; j++) v[4 * q + j] = (d >> (8 * j)) & 0xff;
-                }
-            }
-            if (!filter_regs(v, wd, le[L], li[L], L >> 4, a.bdm8, a.bdmax)) continue;
-            const int lo = lf_wlo(wd);
-#pragma unroll
-            for (int j = 2; j < 14; j++)
-                if (j >= lo && j < 16 - lo) w[j] = (Px)v[j];
-        }
-    }
+    // column edges, then row edges, one loop per width class
+    lf_cols_class<4, Px, P>(t, listv[0], cnt[0], le, li, a.bdm8, a.bdmax);
+    lf_cols_class<6, Px, P>(t, listv[1], cnt[1], le, li, a.bdm8, a.bdmax);
+    lf_cols_class<8, Px, P>(t, listv[2], cnt[2], le, li, a.bdm8, a.bdmax);
+    lf_cols_class<16, Px, P>(t, listv[3], cnt[3], le, li, a.bdm8, a.bdmax);
     __syncthreads();
-    // row edges: 4 pixel columns per unit
-    {
-        const int c0 = cnt[4] * 4, c1 = c0 + cnt[5] * 4, c2 = c1 + cnt[6] * 4, c3 = c2 + cnt[7] * 4;
-        for (int i = tid; i < c3; i += 256) {
-            const int c = i < c0 ? 0 : i < c1 ? 1 : i < c2 ? 2 : 3;
-            const int base = c == 0 ? 0 : c == 1 ? c0 : c == 2 ? c1 : c2;
-            const int e = listh[c][(i - base) >> 2];
-            const int u = e >> 6, L = e & 63;
-            const int wd = c == 0 ? 4 : c == 1 ? 6 : c == 2 ? 8 : 16;
-            const int k = u / (kLfT / 4), col = (u % (kLfT / 4)) * 4 + (i & 3);
-            // edge row e = y0 - 4 + 4k sits at staged row 8 + 4k; v[8] is that row
-            Px *w = &t[(4 * k) * P + 16 + col];
-            int v[16];
-#pragma unroll
-            for (int j = 0; j < 16; j++) v[j] = 0;
-            const int n = wd == 16 ? 7 : wd == 8 ? 4 : wd == 6 ? 3 : 2;
-#pragma unroll
-            for (int j = 1; j < 15; j++)
-                if (j >= 8 - n && j < 8 + n) v[j] = w[j * P];
-            if (!filter_regs(v, wd, le[L], li[L], L >> 4, a.bdm8, a.bdmax)) continue;
-            const int lo = lf_wlo(wd);
-#pragma unroll
-            for (int j = 2; j < 14; j++)
-                if (j >= lo && j < 16 - lo) w[j * P] = (Px)v[j];
-        }
-    }
+    lf_rows_class<4, Px, P>(t, listh[0], cnt[4], le, li, a.bdm8, a.bdmax);
+    lf_rows_class<6, Px, P>(t, listh[1], cnt[5], le, li, a.bdm8, a.bdmax);
+    lf_rows_class<8, Px, P>(t, listh[2], cnt[6], le, li, a.bdm8, a.bdmax);
+    lf_rows_class<16, Px, P>(t, listh[3], cnt[7], le, li, a.bdm8, a.bdmax);
     __syncthreads();
     uint8_t *dst = a.dst[p];
-    constexpr int VPT = kLfT / VPX;
-    for (int i = tid; i < kLfT * VPT; i += 256) {
+    constexpr int VPT = kLfTW / VPX;
+    for (int i = tid; i < kLfTH * VPT; i += 256) {
         const int r = i / VPT, c = (i % VPT) * VPX;
         const int y = y0 + r, x = x0 + c;
         if (y < ph && x < pw)
