@@ -7,7 +7,8 @@ One step = one frame through every GPU stage, inputs resident in HBM:
   (C + D -> O, the reference picture). Descriptors follow SURVEY.md §8(d) config 3.
 Film grain (output-only, configs[3] = 8K10) is timed separately on an 8K10 frame and
 reported under "film_grain_8k10"; the intra path (configs[1], 1080p8: intra prediction +
-itx per dependency level) under "intra_1080p8". Neither is part of the headline step.
+itx residual per block in one persistent launch) under "intra_1080p8". Neither is part of
+the headline step.
 
 `python bench.py` runs 1 GPU. Under torch.distributed.run every rank drives its own GPU on
 its own independent stream (replicas; no data-path collective; "scaling": "weak"); the
@@ -178,44 +179,53 @@ def pmc_traffic(stage):
     return None if ent is None else ent.get("hbm_bytes_per_step")
 
 
-def intra_1080p8(ctx, reps=5):
-    """configs[1]: a 1080p 8-bit 4:2:0 intra frame, intra prediction (device edge gathering)
-    + itx residual per dependency level (rav1d_amd.intra). Reported beside the headline, with
-    the level count that bounds it; the level sequence is replayed as a HIP graph."""
-    from rav1d_amd.intra import IntraFrame, make_intra_residuals
+def intra_1080p8(ctx, reps=5, nframes=8, ndesc=4):
+    """configs[1]: 1080p 8-bit 4:2:0 intra frames, intra prediction (device edge gathering) +
+    itx residual per transform block, reconstructed by the persistent fused kernel
+    (mi_intra_recon: one launch, per-block dependency waits, frame f on XCD f). Reports the
+    single-frame latency, the throughput of `nframes` independent frames per launch (an
+    all-intra stream's frames do not depend on each other; ndesc distinct synthetic descriptor
+    sets, cycled, each frame its own picture) and, for comparison, the per-level launch path
+    (two launches per dependency level, graph-replayed)."""
+    from rav1d_amd.intra import IntraFrame, device_status, intra_recon, make_intra_residuals
     from rav1d_amd.ipred_synth import make_intra_frame
     w, h, bpc = 1920, 1080, 8
-    rng = np.random.default_rng(0x1A7A0001)
-    fr = make_intra_residuals(make_intra_frame(w, h, bpc, 1, rng), bpc, rng)
-    cur = F.Frame(w, h, bpc, 1)
-    pic = cur.picture()
-    intra = IntraFrame(ctx, fr)
+    descs = []
+    for k in range(ndesc):
+        rng = np.random.default_rng(0x1A7A0001 + k)
+        descs.append(IntraFrame(ctx, make_intra_residuals(make_intra_frame(w, h, bpc, 1, rng), bpc, rng)))
+    curs = [F.Frame(w, h, bpc, 1) for _ in range(nframes)]
+    batch = [(descs[f % ndesc], curs[f].picture()) for f in range(nframes)]
     s = torch.cuda.Stream()
-    with torch.cuda.stream(s):
-        intra.step(pic, s)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+
+    def timed(fn):
+        fn()
         s.synchronize()
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record(s)
         for _ in range(reps):
-            intra.step(pic, s)
+            fn()
         ev[1].record(s)
         s.synchronize()
-        eager_ms = ev[0].elapsed_time(ev[1]) / reps
+        return ev[0].elapsed_time(ev[1]) / reps
+
+    with torch.cuda.stream(s):
+        one_ms = timed(lambda: intra_recon(ctx, batch[:1], s))
+        batch_ms = timed(lambda: intra_recon(ctx, batch, s))
+        device_status(ctx, s)
+        intra, pic = descs[0], batch[0][1]
         g = torch.cuda.CUDAGraph()
+        intra.step(pic, s)
         with torch.cuda.graph(g, stream=s):
             intra.step(pic, s)
-        g.replay()
-        s.synchronize()
-        ev[0].record(s)
-        for _ in range(reps):
-            g.replay()
-        ev[1].record(s)
-        s.synchronize()
-        graph_ms = ev[0].elapsed_time(ev[1]) / reps
-    ms = min(eager_ms, graph_ms)
-    return dict(mpx_per_s=round(w * h / (ms / 1e3) / 1e6, 1), ms_per_frame=round(ms, 3),
-                eager_ms=round(eager_ms, 3), graph_ms=round(graph_ms, 3), levels=len(intra.levels),
-                tx_blocks=int(len(fr["blocks"])), launches_per_frame=2 * len(intra.levels))
+        level_ms = timed(g.replay)
+    fr = descs[0].fr
+    return dict(mpx_per_s=round(nframes * w * h / (batch_ms / 1e3) / 1e6, 1),
+                fps=round(nframes / (batch_ms / 1e3), 1), ms_per_frame=round(one_ms, 3),
+                frames_per_launch=nframes, batch_ms=round(batch_ms, 3),
+                single_frame_mpx_per_s=round(w * h / (one_ms / 1e3) / 1e6, 1),
+                level_launch_ms=round(level_ms, 3), levels=len(intra.levels), tx_blocks=int(len(fr["blocks"])),
+                kernel="intra_recon_kernel (persistent; 128 one-wave workers per XCD)")
 
 
 def cpu_baseline(fr, budget_s=20.0):

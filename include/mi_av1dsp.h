@@ -293,9 +293,6 @@ int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
 int mi_ipred_blocks(MiCtx *ctx, const MiPicture *pic, const MiIpredBlock *blocks, int n,
                     const void *edges, const int16_t *ac, const uint8_t *idx, void *stream);
 
-/* Deblock a whole frame in place: all column edges (every plane), then all row edges.
- * Equivalent to the reference's per-sbrow cols/rows interleaving (SURVEY.md App. B.2);
- * replaces rav1d_loopfilter_sbrow_cols/_rows (src/lf_apply.rs:597-834). */
 /* Intra prediction of n independent transform blocks with device-side edge gathering from
  * `pic` (MiIntraBlock): the batched replacement of recon_b_intra's per-tx-block
  * prepare_intra_edges + intra_pred / cfl_pred / pal_pred (recon.rs:2402-3160). ac / idx / pal
@@ -303,6 +300,37 @@ int mi_ipred_blocks(MiCtx *ctx, const MiPicture *pic, const MiIpredBlock *blocks
 int mi_intra_blocks(MiCtx *ctx, const MiPicture *pic, const MiIntraBlock *blocks, int n,
                     const int16_t *ac, const uint8_t *idx, const void *pal, void *stream);
 
+/* Whole-frame intra reconstruction in ONE persistent launch: every transform block's
+ * prediction (as mi_intra_blocks) plus its residual (as mi_itx_frame), in dependency order,
+ * for up to 8 independent frames at once (frame f is reconstructed by the workgroups on XCD f,
+ * which share one L2). Replaces recon_b_intra's per-block prepare_intra_edges / intra_pred /
+ * itxfm_add sequence (recon.rs:2402-3160) for whole frames. Per frame (device arrays):
+ * blocks[n] in an order where every block comes after the blocks it depends on; tx[i] is the
+ * residual of blocks[i] (same plane, position and size); deps[dep_start[i] ..
+ * dep_start[i + 1]) are the indices (< i) of the blocks owning any pixel blocks[i]'s edges
+ * read. flags: MI_ITX_KEEP_COEFS as mi_itx_frame. A worker that waits ~0.5 s for a dependency
+ * gives up (no hang); mi_ctx_device_status reports it. */
+typedef struct MiIntraFrame {
+    MiPicture pic;
+    const MiIntraBlock *blocks;
+    const MiTxBlock *tx;
+    const int32_t *dep_start;
+    const int32_t *deps;
+    const int16_t *ac;
+    const uint8_t *idx;
+    const void *pal;
+    void *coef;
+    int32_t n;
+} MiIntraFrame;
+int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned flags, void *stream);
+
+/* Synchronise `stream` and report device-side failures of the context's persistent
+ * launches since the last call: 0, or -ETIMEDOUT (a dependency wait gave up). */
+int mi_ctx_device_status(MiCtx *ctx, void *stream);
+
+/* Deblock a whole frame in place: all column edges (every plane), then all row edges.
+ * Equivalent to the reference's per-sbrow cols/rows interleaving (SURVEY.md App. B.2);
+ * replaces rav1d_loopfilter_sbrow_cols/_rows (src/lf_apply.rs:597-834). */
 int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, void *stream);
 
 /* Deblocking out of place: reads the reconstruction `src` (never written), writes the

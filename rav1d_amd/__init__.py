@@ -29,6 +29,12 @@ class MiPicture(ctypes.Structure):
                 ("layout", ctypes.c_int32), ("bpc", ctypes.c_int32)]
 
 
+class MiIntraFrame(ctypes.Structure):
+    _fields_ = [("pic", MiPicture), ("blocks", ctypes.c_void_p), ("tx", ctypes.c_void_p),
+                ("dep_start", ctypes.c_void_p), ("deps", ctypes.c_void_p), ("ac", ctypes.c_void_p),
+                ("idx", ctypes.c_void_p), ("pal", ctypes.c_void_p), ("coef", ctypes.c_void_p), ("n", ctypes.c_int32)]
+
+
 class MiLoopFilter(ctypes.Structure):
     _fields_ = [("level", ctypes.c_void_p), ("b4_stride", ctypes.c_ssize_t), ("masks", ctypes.c_void_p),
                 ("sb128w", ctypes.c_int32), ("filter_y", ctypes.c_int32), ("filter_uv", ctypes.c_int32),
@@ -128,6 +134,8 @@ def lib():
     _sig(L, "mi_mc_combine", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.c_int, _VP, _VP, _VP])
     _sig(L, "mi_superres_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture), _VP])
     _sig(L, "mi_intra_blocks", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.c_int, _VP, _VP, _VP, _VP])
+    _sig(L, "mi_intra_recon", ctypes.c_int, [_VP, ctypes.POINTER(MiIntraFrame), ctypes.c_int, ctypes.c_uint, _VP])
+    _sig(L, "mi_ctx_device_status", ctypes.c_int, [_VP, _VP])
     _sig(L, "mi_ipred_blocks", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.c_int, _VP, _VP, _VP, _VP])
     _sig(L, "mi_dsp_intra_pred", ctypes.c_int, [ctypes.c_int, _VP, ctypes.c_ssize_t, _VP] + [ctypes.c_int] * 6)
     _sig(L, "mi_deblock_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiLoopFilter), _VP])
@@ -148,7 +156,7 @@ def lib():
 # Every symbol include/mi_av1dsp.h declares (checked by tests/test_abi.py).
 EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
             "mi_itx_frame", "mi_mc_frame", "mi_mc_scaled", "mi_mc_warp", "mi_mc_combine", "mi_superres_frame",
-            "mi_ipred_blocks", "mi_intra_blocks", "mi_deblock_frame", "mi_deblock_frame_to", "mi_cdef_frame", "mi_lr_frame",
+            "mi_ipred_blocks", "mi_intra_blocks", "mi_intra_recon", "mi_ctx_device_status", "mi_deblock_frame", "mi_deblock_frame_to", "mi_cdef_frame", "mi_lr_frame",
             "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply",
             "mi_dsp_itxfm_add", "mi_dsp_intra_pred"]
 

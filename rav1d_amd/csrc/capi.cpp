@@ -4,10 +4,13 @@
 // The per-call entry points keep the reference's contract (caller owns buffers, callee zeroes
 // the consumed coefficients, src/itx.rs:152-158) and accept host or device pointers; they run
 // a one-block launch synchronously on a private stream of device 0.
+#include <stdio.h>
+#include <stdlib.h>
 #include <algorithm>
 #include <errno.h>
 #include <mutex>
 #include <string.h>
+#include <string>
 #include <vector>
 #include "common.h"
 
@@ -19,7 +22,15 @@ struct MiCtx {
     uint8_t *fg_scaling = nullptr;
     uint8_t *fg_offsets = nullptr;
     size_t fg_offsets_bytes = 0;
+    // persistent intra reconstruction: per-block done epochs, queue heads, error word
+    uint32_t *ir_done = nullptr;
+    size_t ir_done_n = 0;
+    int *ir_words = nullptr;      // [0..7] queue heads, [8] error
+    uint32_t ir_epoch = 0;
+    int ir_last_n[8] = {0}, ir_last_frames = 0;
     ~MiCtx() {
+        if (ir_done) (void)hipFree(ir_done);
+        if (ir_words) (void)hipFree(ir_words);
         if (fg_lut) (void)hipFree(fg_lut);
         if (fg_scaling) (void)hipFree(fg_scaling);
         if (fg_offsets) (void)hipFree(fg_offsets);
@@ -110,7 +121,12 @@ int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
     const int wg = mi::itx_fill_schedule(a, size_start);
     if (wg == 0) return 0;
     if (!blocks || !coef) return fail(ctx, -EINVAL);
-    const int r = mi::launch_itx_frame(a, wg, pic->bpc, (hipStream_t)stream);
+    // The two launches stay serialised on the caller's stream: running the large sizes on a
+    // side stream (event fork/join) measured slower (4K10 itx 56 -> 74 us, 1080p8 intra
+    // 22.6 -> 33.2 ms) than the cross-queue dependency saves.
+    hipStream_t s = (hipStream_t)stream;
+    const int small_wg = a.large_wg0, large_wg = wg - a.large_wg0;
+    const int r = mi::launch_itx_frame(a, small_wg, large_wg, pic->bpc, s);
     return r ? fail(ctx, -EIO) : 0;
 }
 
@@ -288,6 +304,98 @@ int mi_intra_blocks(MiCtx *ctx, const MiPicture *pic, const MiIntraBlock *blocks
     a.bpc = pic->bpc;
     a.bdmax = (1 << pic->bpc) - 1;
     return mi::launch_intra(a, n, (hipStream_t)stream) ? fail(ctx, -EIO) : 0;
+}
+
+int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned flags, void *stream) {
+    if (!ctx || !frames || nframes < 1 || nframes > 8) return fail(ctx, -EINVAL);
+    const int bpc = frames[0].pic.bpc;
+    if (bpc != 8 && bpc != 10 && bpc != 12) return fail(ctx, -EINVAL);
+    size_t total = 0;
+    for (int f = 0; f < nframes; f++) {
+        const MiIntraFrame &fr = frames[f];
+        if (fr.pic.bpc != bpc || fr.n < 0 || (fr.n && (!fr.blocks || !fr.tx || !fr.dep_start || !fr.coef)))
+            return fail(ctx, -EINVAL);
+        total += (size_t)fr.n;
+    }
+    if (!ctx->ir_words) {
+        if (hipMalloc(&ctx->ir_words, 16 * sizeof(int)) != hipSuccess) return fail(ctx, -ENOMEM);
+        if (hipMemset(ctx->ir_words, 0, 16 * sizeof(int)) != hipSuccess) return fail(ctx, -EIO);
+    }
+    if (total > ctx->ir_done_n) {
+        if (ctx->ir_done) (void)hipFree(ctx->ir_done);
+        ctx->ir_done = nullptr;
+        ctx->ir_done_n = 0;
+        if (hipMalloc(&ctx->ir_done, total * sizeof(uint32_t)) != hipSuccess) return fail(ctx, -ENOMEM);
+        if (hipMemset(ctx->ir_done, 0, total * sizeof(uint32_t)) != hipSuccess) return fail(ctx, -EIO);
+        ctx->ir_done_n = total;
+        ctx->ir_epoch = 0;
+    }
+    if (++ctx->ir_epoch == 0) ctx->ir_epoch = 1;   // done words hold the epoch of the last call
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(ctx->ir_words, 0, 8 * sizeof(int), s) != hipSuccess) return fail(ctx, -EIO);
+    mi::IntraReconArgs a;
+    memset(&a, 0, sizeof(a));
+    a.err = ctx->ir_words + 8;
+#ifdef MI_IR_DEBUG
+    static int *dbg = nullptr;
+    if (!dbg && hipHostMalloc((void **)&dbg, 65536 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return fail(ctx, -ENOMEM);
+    memset(dbg, 0, 65536 * sizeof(int));
+    int *ddbg = nullptr;
+    (void)hipHostGetDevicePointer((void **)&ddbg, dbg, 0);
+    a.dbg = ddbg;
+    setenv("MI_IR_DBG_PTR", std::to_string((uintptr_t)dbg).c_str(), 1);
+#endif
+    a.epoch = ctx->ir_epoch;
+    a.nframes = nframes;
+    a.zero_coefs = (flags & MI_ITX_KEEP_COEFS) ? 0 : 1;
+    size_t off = 0;
+    for (int f = 0; f < nframes; f++) {
+        const MiIntraFrame &fr = frames[f];
+        mi::IntraReconFrame &d = a.fr[f];
+        for (int p = 0; p < 3; p++) d.ip.dst[p] = (uint8_t *)fr.pic.data[p];
+        d.ip.stride[0] = fr.pic.stride[0];
+        d.ip.stride[1] = fr.pic.stride[1];
+        d.ip.iblocks = fr.blocks;
+        d.ip.ac = fr.ac;
+        d.ip.idx = fr.idx;
+        d.ip.pal = (const uint8_t *)fr.pal;
+        d.ip.bpc = bpc;
+        d.ip.bdmax = (1 << bpc) - 1;
+        d.tx = fr.tx;
+        d.coef = (uint8_t *)fr.coef;
+        d.dep_start = fr.dep_start;
+        d.deps = fr.deps;
+        d.done = ctx->ir_done + off;
+        d.head = ctx->ir_words + f;
+        d.n = fr.n;
+        off += (size_t)fr.n;
+    }
+    ctx->ir_last_frames = nframes;
+    for (int f = 0; f < nframes; f++) ctx->ir_last_n[f] = frames[f].n;
+    // 128 one-wave workers per XCD (occupancy allows 3 per SIMD = 384 per XCD): a look-ahead
+    // of several dependency levels
+    return mi::launch_intra_recon(a, 128, s) ? fail(ctx, -EIO) : 0;
+}
+
+int mi_ctx_device_status(MiCtx *ctx, void *stream) {
+    if (!ctx) return -EINVAL;
+    if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(ctx, -EIO);
+    if (!ctx->ir_words) return 0;
+    int w[9];
+    if (hipMemcpy(w, ctx->ir_words, sizeof(w), hipMemcpyDeviceToHost) != hipSuccess) return fail(ctx, -EIO);
+    if (getenv("MI_DEBUG"))
+        fprintf(stderr, "mi_ctx_device_status: heads %d %d %d %d %d %d %d %d err %d\n", w[0], w[1], w[2], w[3], w[4],
+                w[5], w[6], w[7], w[8]);
+    if (w[8]) {
+        (void)hipMemset(ctx->ir_words + 8, 0, sizeof(int));
+        return fail(ctx, -ETIMEDOUT);
+    }
+    // every block of the last launch was taken by a worker (a frame whose XCD received no
+    // workgroup would be left untouched)
+    for (int f = 0; f < ctx->ir_last_frames; f++)
+        if (w[f] < ctx->ir_last_n[f]) return fail(ctx, -EIO);
+    return 0;
 }
 
 int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, void *stream) {
@@ -611,7 +719,7 @@ int mi_dsp_itxfm_add(int tx, int txtp, void *dst, ptrdiff_t stride, void *coeff,
     uint32_t ss1[MI_N_RECT_TX_SIZES + 1];
     for (int k = 0; k <= MI_N_RECT_TX_SIZES; k++) ss1[k] = k > tx ? 1 : 0;
     const int nwg = mi::itx_fill_schedule(a, ss1);
-    if (mi::launch_itx_frame(a, nwg, bpc, s)) return -EIO;
+    if (mi::launch_itx_frame(a, a.large_wg0, nwg - a.large_wg0, bpc, s)) return -EIO;
 
     if (dst_dev) {
         for (int y = 0; y < d.h; y++)

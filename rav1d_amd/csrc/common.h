@@ -78,7 +78,8 @@ constexpr int kItxNumSmall = 9;
 int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start);
 
 // launchers (itx.hip)
-int launch_itx_frame(const ItxArgs &a, int total_wg, int bpc, hipStream_t s);
+// small_wg / large_wg: workgroups of the two launches (either may be 0)
+int launch_itx_frame(const ItxArgs &a, int small_wg, int large_wg, int bpc, hipStream_t s);
 
 struct LfArgs {
     uint8_t *plane[3];
@@ -174,6 +175,24 @@ struct IpredArgs {
     const uint8_t *pal;
     int bpc, bdmax;
 };
+// persistent fused intra reconstruction (ipred.hip): frame f is worked on by XCD f
+struct IntraReconFrame {
+    IpredArgs ip;                 // picture planes / strides, iblocks, ac, idx, pal, bpc, bdmax
+    const MiTxBlock *tx;
+    uint8_t *coef;
+    const int32_t *dep_start, *deps;
+    uint32_t *done;               // per block: epoch when reconstructed
+    int *head;                    // queue head
+    int n;
+};
+struct IntraReconArgs {
+    IntraReconFrame fr[8];
+    int *err;
+    int *dbg;                     // MI_IR_DEBUG builds: host-mapped progress words
+    uint32_t epoch;
+    int nframes, zero_coefs;
+};
+int launch_intra_recon(const IntraReconArgs &a, int wg_per_xcd, hipStream_t s);
 // launchers (ipred.hip)
 int launch_ipred(const IpredArgs &a, int n, hipStream_t s);
 int launch_intra(const IpredArgs &a, int n, hipStream_t s);

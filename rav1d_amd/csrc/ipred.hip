@@ -14,6 +14,7 @@
 // row). FILTER_PRED (recursive 4x2 taps) runs as an anti-diagonal wavefront of 4x2 sub-blocks
 // over an LDS copy of the block.
 #include "common.h"
+#include "itx_1d.h"
 
 namespace mi {
 
@@ -26,6 +27,10 @@ __constant__ uint16_t k_dr_intra_derivative[44] = {
 __constant__ int8_t k_filter_intra_taps[5][64] = {
 #include "tables/filter_intra_taps.inc"
 };
+
+// TxfmType -> 1-D kinds (as itx.hip's k_row_kind / k_col_kind; levels.rs TxfmType is VERT_HORZ)
+__constant__ uint8_t k_col_kind_ip[16] = { KD, KA, KD, KA, KF, KD, KF, KA, KF, KI, KD, KI, KA, KI, KF, KI };
+__constant__ uint8_t k_row_kind_ip[16] = { KD, KD, KA, KA, KD, KF, KF, KF, KA, KI, KI, KD, KI, KA, KI, KF };
 
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
@@ -84,8 +89,9 @@ __device__ void upsample_edge_par(int *out, int hsz, const Px *in_, int from, in
 
 // Predict one block from its gathered edge `tl` (global edge buffer or LDS). eb / ft: LDS
 // scratch for the directional edge and the filter-intra image.
-template <typename Px>
-__device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredBlock &b, const Px *tl, int *eb, Px *ft) {
+template <typename Px, bool ToLds = false>
+__device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredBlock &b, const Px *tl, int *eb, Px *ft,
+                                              Px *lt = nullptr) {
     const int lane = threadIdx.x;
     const int w = b.w, h = b.h, n = w * h;
     const int64_t st = a.stride[b.plane ? 1 : 0];
@@ -95,8 +101,10 @@ __device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredB
     // (mc.blend, mc_tmpl.c:621-630); the address is formed before the uniform branch
     const bool ii = b.mode & MI_IPRED_II;
     const uint8_t *iim = a.idx + b.aux_off;
+    // ToLds: the prediction goes to the w x h LDS tile lt (the fused intra reconstruction
+    // adds the residual there); otherwise into the picture
     auto put = [&](int y, int x, int v) {
-        Px *d = reinterpret_cast<Px *>(dst + (int64_t)y * st) + x;
+        Px *d = ToLds ? lt + y * w + x : reinterpret_cast<Px *>(dst + (int64_t)y * st) + x;
         if (ii) {
             const int m = iim[y * w + x];
             v = (*d * (64 - m) + v * m + 32) >> 6;
@@ -343,18 +351,28 @@ __global__ __launch_bounds__(64) void ipred_kernel(IpredArgs a) {
 __constant__ uint8_t k_needs[14] = { 3, 2, 1, 1, 2, 0, 14, 7, 21, 3, 3, 3, 7, 7 };
 __constant__ uint8_t k_mode_angle[8] = { 90, 180, 45, 135, 113, 157, 203, 67 };
 
-template <typename Px>
-__global__ __launch_bounds__(64) void intra_kernel(IpredArgs a) {
-    __shared__ int eb[2 * 128 + 2];
-    __shared__ Px ft[32 * 32];
-    __shared__ Px edge[2 * 128 + 1];           // topleft at [128]
-    const MiIntraBlock ib = a.iblocks[blockIdx.x];
+// Gather one block's edges from the picture (rav1d_prepare_intra_edges) and predict it, one
+// wave. Fused (the persistent reconstruction kernel): neighbour pixels were stored by other
+// CUs of this XCD during the launch, so every picture read is an L1-bypassing `sc1` load
+// (L2-served), and the prediction goes to the LDS tile lt.
+template <typename Px, bool Fused>
+__device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlock &ib, int *eb, Px *ft, Px *edge,
+                                            Px *lt) {
     const int lane = threadIdx.x;
     const int w = ib.w, h = ib.h, x = ib.x, y = ib.y;
     const bool have_left = ib.flags & MI_INTRA_HAVE_LEFT, have_top = ib.flags & MI_INTRA_HAVE_TOP;
     const int64_t st = a.stride[ib.plane ? 1 : 0];
     const Px *pic = reinterpret_cast<const Px *>(a.dst[ib.plane]);
-    auto P = [&](int yy, int xx) -> int { return reinterpret_cast<const Px *>(reinterpret_cast<const uint8_t *>(pic) + (int64_t)yy * st)[xx]; };
+    auto P = [&](int yy, int xx) -> int {
+        const Px *q = reinterpret_cast<const Px *>(reinterpret_cast<const uint8_t *>(pic) + (int64_t)yy * st) + xx;
+        if constexpr (Fused) return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else return *q;
+    };
+    if constexpr (Fused) {
+        // inter-intra blends into the block's existing (inter) pixels: start the tile from them
+        if (ib.flags & MI_INTRA_II)
+            for (int i = lane; i < w * h; i += 64) lt[i] = (Px)P(y + i / w, x + i % w);
+    }
     const int bd = a.bpc;
 
     MiIpredBlock b;
@@ -373,7 +391,7 @@ __global__ __launch_bounds__(64) void intra_kernel(IpredArgs a) {
     if (ib.mode == MI_IPRED_PAL) {
         b.mode = MI_IPRED_PAL;
         b.angle = 0;
-        predict_block<Px>(a, b, reinterpret_cast<const Px *>(a.pal) + ib.pal_off, eb, ft);
+        predict_block<Px, Fused>(a, b, reinterpret_cast<const Px *>(a.pal) + ib.pal_off, eb, ft, lt);
         return;
     }
     // mode remap (ipred_prepare.rs:148-172): all wave-uniform
@@ -451,7 +469,208 @@ __global__ __launch_bounds__(64) void intra_kernel(IpredArgs a) {
     b.mode = (uint8_t)((cfl ? MI_IPRED_CFL + m : m) | ii);
     b.angle = (uint16_t)(angle | (ib.flags & MI_INTRA_SMOOTH_NB ? 512 : 0) | (ib.flags & MI_INTRA_EDGE_FILTER ? 1024 : 0));
     if (m == 13) b.angle = (uint16_t)ib.filt_idx;
-    predict_block<Px>(a, b, tl, eb, ft);
+    predict_block<Px, Fused>(a, b, tl, eb, ft, lt);
+}
+
+template <typename Px>
+__global__ __launch_bounds__(64) void intra_kernel(IpredArgs a) {
+    __shared__ int eb[2 * 128 + 2];
+    __shared__ Px ft[32 * 32];
+    __shared__ Px edge[2 * 128 + 1];           // topleft at [128]
+    intra_block<Px, false>(a, a.iblocks[blockIdx.x], eb, ft, edge, nullptr);
+}
+
+// ---- persistent fused intra reconstruction (mi_intra_recon) ----
+//
+// One launch reconstructs whole intra frames: prediction (intra_block) and the residual
+// (inverse transform + add) of every transform block, in dependency order, without a launch
+// per wavefront step. Frame f is worked on only by the workgroups the dispatcher placed on
+// XCD f (HW_REG_XCC_ID): those share one L2, so a block's pixels, stored plainly (the
+// vector L1 writes through), are visible to every other worker of the frame once the
+// storing wave has drained its stores; readers bypass L1 with `sc1` loads. Each worker wave
+// takes the next block from the frame's queue (an atomic head over blocks in dependency
+// order), waits until every block its edges read has been marked done with this launch's
+// epoch, predicts into an LDS tile, adds the residual there and stores the tile. Deadlock-free:
+// a block only waits on earlier queue entries, which running workers hold. A wait that
+// exceeds ~0.5 s flags the context's device error word and gives up (no hang).
+
+#ifndef MI_IR_SPIN_LOG2
+#define MI_IR_SPIN_LOG2 22
+#endif
+
+__device__ __forceinline__ unsigned xcc_id() {
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return v & 0xf;
+}
+
+// Inverse transform of one block by one wave, added into the w x h LDS tile lt: the
+// per-block semantics of itx_size (itx.hip), lane j = row j, then column j.
+template <int TX, typename Px, typename Cf, typename Lt, bool Wide>
+__device__ __forceinline__ void itx_tile(const MiTxBlock &b, Cf *cf, bool zero, int bdmax, Px *lt, Lt *tmp) {
+    constexpr TxDim D = tx_dim(TX);
+    constexpr int Wd = D.w, Ht = D.h, SH = imin_c(Ht, 32), SW = imin_c(Wd, 32);
+    constexpr int LS = Wd + 1;
+    constexpr bool Rect2 = (Wd == 2 * Ht) || (Ht == 2 * Wd);
+    constexpr int Shift = D.shift, Rnd = (1 << Shift) >> 1;
+    const int j = threadIdx.x;
+    const bool wht = (TX == 0) && b.txtp == 16;
+    if (b.txtp == 0 && b.eob < 1) {
+        int dc = (int)cf[0];
+        if (Rect2) dc = (dc * 181 + 128) >> 8;
+        dc = (dc * 181 + 128) >> 8;
+        dc = (dc + Rnd) >> Shift;
+        dc = (dc * 181 + 128 + 2048) >> 12;
+        for (int i = j; i < Wd * Ht; i += 64) lt[i] = (Px)clampi((int)lt[i] + dc, 0, bdmax);
+        if (zero && j == 0) cf[0] = 0;
+        return;
+    }
+    int row_lo, col_lo;
+    if constexpr (sizeof(Px) == 1) { row_lo = -32768; col_lo = -32768; }
+    else { row_lo = (int)((unsigned)~bdmax << 7); col_lo = (int)((unsigned)~bdmax << 5); }
+    const int row_hi = ~row_lo, col_hi = ~col_lo;
+    if (j < SH) {
+        int r[Wd];
+#pragma unroll
+        for (int x = 0; x < Wd; x++) r[x] = 0;
+#pragma unroll
+        for (int x = 0; x < SW; x++) {
+            const int v = (int)cf[j + x * SH];
+            if constexpr (Rect2) r[x] = (v * 181 + 128) >> 8;
+            else r[x] = v;
+        }
+        if (zero) {
+#pragma unroll
+            for (int x = 0; x < SW; x++) cf[j + x * SH] = 0;
+        }
+        if (wht) {
+            if constexpr (TX == 0) {
+#pragma unroll
+                for (int x = 0; x < 4; x++) r[x] >>= 2;
+                iwht4(r);
+#pragma unroll
+                for (int x = 0; x < 4; x++) tmp[j * LS + x] = (Lt)r[x];
+            }
+        } else {
+            itx1d<Wide, Wd>(k_row_kind_ip[b.txtp], r, row_lo, row_hi);
+#pragma unroll
+            for (int x = 0; x < Wd; x++) tmp[j * LS + x] = (Lt)clampi((r[x] + Rnd) >> Shift, col_lo, col_hi);
+        }
+    }
+    __syncthreads();
+    if (j < Wd) {
+        int c[Ht];
+#pragma unroll
+        for (int y = 0; y < Ht; y++) c[y] = y < SH ? (int)tmp[y * LS + j] : 0;
+        if (wht) {
+            if constexpr (TX == 0) {
+                iwht4(c);
+#pragma unroll
+                for (int y = 0; y < 4; y++) lt[y * Wd + j] = (Px)clampi((int)lt[y * Wd + j] + c[y], 0, bdmax);
+            }
+        } else {
+            itx1d<Wide, Ht>(k_col_kind_ip[b.txtp], c, col_lo, col_hi);
+#pragma unroll
+            for (int y = 0; y < Ht; y++) lt[y * Wd + j] = (Px)clampi((int)lt[y * Wd + j] + ((c[y] + 8) >> 4), 0, bdmax);
+        }
+    }
+}
+
+template <typename Px, typename Cf, typename Lt, bool Wide>
+__global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
+    __shared__ int eb[2 * 128 + 2];
+    __shared__ Px ft[32 * 32];
+    __shared__ Px edge[2 * 128 + 1];
+    __shared__ __attribute__((aligned(16))) Px lt[64 * 64];
+    __shared__ Lt tmp[32 * 65];
+    const unsigned f = xcc_id();
+#ifdef MI_IR_DEBUG
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(a.dbg + 16 + (f & 7), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_fetch_add(a.dbg + 32 + (blockIdx.x & 7), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+#define DBG(i, v) __hip_atomic_store(a.dbg + 64 + (i), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+#else
+#define DBG(i, v) do {} while (0)
+#endif
+    if ((int)f >= a.nframes) return;
+    const IntraReconFrame &fr = a.fr[f];
+    const int lane = threadIdx.x;
+    for (;;) {
+        // The block index must be provably wave-uniform and the loop free of lane-divergent
+        // branches: otherwise the structurizer may run lanes 1..63 into the next iteration
+        // ahead of lane 0's pop (observed: a livelock on the same block)
+        // (every lane executes the pop, lane 0 adds 1 and the others 0, so no lane-divergent
+        // branch exists at loop level)
+        const int i = __builtin_amdgcn_readfirstlane(atomicAdd(fr.head, lane == 0 ? 1 : 0));
+        if (i >= fr.n) return;
+        DBG(i, 1);
+        const MiIntraBlock ib = fr.ip.iblocks[i];
+        const MiTxBlock tb = fr.tx[i];
+        // wait for the blocks this one's edges read; wave-uniform loop exits (a ballot)
+        const int d0 = fr.dep_start[i], d1 = fr.dep_start[i + 1];
+        for (int base = d0; base < d1; base += 64) {
+            const int d = base + lane;
+            const uint32_t *flag = fr.done + (d < d1 ? fr.deps[d] : 0);
+            bool ok = d >= d1;
+            for (unsigned spins = 0;; spins++) {
+                if (!ok) ok = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
+                if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+                if (spins > (1u << MI_IR_SPIN_LOG2)) {
+                    atomicOr(a.err, 1);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        __syncthreads();
+        DBG(i, 2);
+        intra_block<Px, true>(fr.ip, ib, eb, ft, edge, lt);
+        __syncthreads();
+        DBG(i, 3);
+        Cf *cf = reinterpret_cast<Cf *>(fr.coef) + tb.coef_off;
+        DBG(1024 + i, tb.tx | (ib.w << 8) | (ib.h << 16) | (tb.txtp << 24));
+        switch (tb.tx) {
+#define CASE(n) case n: itx_tile<n, Px, Cf, Lt, Wide>(tb, cf, a.zero_coefs, fr.ip.bdmax, lt, tmp); break;
+            CASE(0) CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9)
+            CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16) CASE(17) CASE(18)
+#undef CASE
+        default: break;
+        }
+        DBG(i, 5);
+        __syncthreads();
+        DBG(i, 6);
+        // store the reconstructed tile: 4-pixel chunks
+        {
+            const int w = ib.w, h = ib.h, cpr = w >> 2;
+            const int64_t st = fr.ip.stride[ib.plane ? 1 : 0];
+            uint8_t *base = fr.ip.dst[ib.plane] + (int64_t)ib.y * st + (int64_t)ib.x * sizeof(Px);
+            for (int c = lane; c < h * cpr; c += 64) {
+                const int yy = c / cpr, xx = (c % cpr) * 4;
+                const Px *src = lt + yy * w + xx;
+                if constexpr (sizeof(Px) == 2)
+                    *reinterpret_cast<uint2 *>(base + yy * st + xx * 2) =
+                        make_uint2(src[0] | ((uint32_t)src[1] << 16), src[2] | ((uint32_t)src[3] << 16));
+                else
+                    *reinterpret_cast<uint32_t *>(base + yy * st + xx) =
+                        src[0] | ((uint32_t)src[1] << 8) | ((uint32_t)src[2] << 16) | ((uint32_t)src[3] << 24);
+            }
+        }
+        DBG(i, 7);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        DBG(i, 8);
+        __syncthreads();
+        DBG(i, 4);
+        __hip_atomic_store(fr.done + i, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // all lanes, same word
+    }
+}
+
+int launch_intra_recon(const IntraReconArgs &a, int wg_per_xcd, hipStream_t s) {
+    const int n = 8 * wg_per_xcd;
+    if (a.fr[0].ip.bpc == 8) intra_recon_kernel<uint8_t, int16_t, int16_t, false><<<n, 64, 0, s>>>(a);
+    else if (a.fr[0].ip.bpc == 10) intra_recon_kernel<uint16_t, int32_t, int16_t, false><<<n, 64, 0, s>>>(a);
+    else intra_recon_kernel<uint16_t, int32_t, int32_t, true><<<n, 64, 0, s>>>(a);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 int launch_intra(const IpredArgs &a, int n, hipStream_t s) {

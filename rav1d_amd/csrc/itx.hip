@@ -269,10 +269,8 @@ int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start) {
     return wg;
 }
 
-int launch_itx_frame(const ItxArgs &a, int total_wg, int bpc, hipStream_t s) {
-    if (total_wg <= 0) return 0;
-    // workgroup ranges are laid out size by size; small sizes first (see capi: ordering)
-    const int small_wg = a.large_wg0, large_wg = total_wg - a.large_wg0;
+int launch_itx_frame(const ItxArgs &a, int small_wg, int large_wg, int bpc, hipStream_t s) {
+    // workgroup ranges are laid out size by size; small sizes first (itx_fill_schedule)
     if (bpc == 8) launch2<uint8_t, int16_t, int16_t, false>(a, small_wg, large_wg, s);
     else if (bpc == 10) launch2<uint16_t, int32_t, int16_t, false>(a, small_wg, large_wg, s);
     else launch2<uint16_t, int32_t, int32_t, true>(a, small_wg, large_wg, s);

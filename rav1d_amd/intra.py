@@ -7,6 +7,9 @@ levels a decoder's block walk implies). Each level is two launches on one stream
 mi_intra_blocks (edges gathered on the device from the picture, then prediction) and
 mi_itx_frame over the same blocks' residuals (grouped by transform size within the level).
 Level L + 1 reads only pixels that levels <= L finished.
+
+IntraFrame.recon / intra_recon use the persistent fused path instead (mi_intra_recon): one
+launch for up to 8 frames, prediction + residual per block, per-block dependency waits.
 """
 import ctypes
 
@@ -71,6 +74,16 @@ class IntraFrame:
         self.coef = torch.from_numpy(fr["coef"].copy()).cuda()
         ls = fr["level_start"]
         self.levels = [(int(ls[i]), int(ls[i + 1])) for i in range(len(ls) - 1)]
+        # fused path: blocks in level order, their residual records in the same order, and the
+        # dependency lists as positions in that order
+        order = fr["order"]
+        pos = np.empty(len(order), np.int64)
+        pos[order] = np.arange(len(order))
+        dl = [pos[fr["deps"][k]] for k in order]
+        self.dep_start = torch.from_numpy(np.concatenate([[0], np.cumsum([len(d) for d in dl])]).astype(np.int32)).cuda()
+        deps = np.concatenate(dl).astype(np.int32) if sum(len(d) for d in dl) else np.zeros(1, np.int32)
+        self.deps = torch.from_numpy(deps).cuda()
+        self.tx_ord = dev(fr["tx_blocks"][fr["tx_of_block"][order]])
         self.ss = [(ctypes.c_uint32 * (N_RECT_TX_SIZES + 1))(*[int(v) for v in row]) for row in fr["tx_size_start"]]
 
     def step(self, pic, stream=None, keep_coefs=True):
@@ -86,3 +99,33 @@ class IntraFrame:
             t0 = int(self.fr["tx_level_off"][lv])
             F.check(lib.mi_itx_frame(h, ctypes.byref(pic), ctypes.c_void_p(self.tx.data_ptr() + 16 * t0), self.ss[lv],
                                      coef, flags, sp), "mi_itx_frame")
+
+    def frame_desc(self, pic):
+        """MiIntraFrame for the fused path (pic: MiPicture)."""
+        from . import MiIntraFrame
+        d = MiIntraFrame()
+        d.pic = pic
+        d.blocks, d.tx = self.blocks.data_ptr(), self.tx_ord.data_ptr()
+        d.dep_start, d.deps = self.dep_start.data_ptr(), self.deps.data_ptr()
+        d.ac, d.idx, d.pal = self.ac.data_ptr(), self.idx.data_ptr(), self.pal.data_ptr()
+        d.coef = self.coef.data_ptr()
+        d.n = len(self.fr["blocks"])
+        return d
+
+    def recon(self, pic, stream=None, keep_coefs=True):
+        """Whole-frame reconstruction in one persistent launch (mi_intra_recon)."""
+        intra_recon(self.ctx, [(self, pic)], stream, keep_coefs)
+
+
+def intra_recon(ctx, frames, stream=None, keep_coefs=True):
+    """Reconstruct up to 8 independent intra frames in one launch: frames = [(IntraFrame,
+    MiPicture)], frame f on XCD f."""
+    from . import MiIntraFrame
+    descs = (MiIntraFrame * len(frames))(*[f.frame_desc(p) for f, p in frames])
+    flags = ITX_KEEP_COEFS if keep_coefs else 0
+    F.check(F.lib().mi_intra_recon(ctx.h, descs, len(frames), flags, F._stream_ptr(stream)), "mi_intra_recon")
+
+
+def device_status(ctx, stream=None):
+    """Synchronise and raise if a persistent launch reported a failed dependency wait."""
+    F.check(F.lib().mi_ctx_device_status(ctx.h, F._stream_ptr(stream)), "mi_ctx_device_status")

@@ -72,7 +72,8 @@ def make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.5, pal_
     edge-availability flags a decoder would pass (top-right / bottom-left only where those
     pixels are already decoded) and each block's dependency level (1 + the deepest level among
     the blocks owning any pixel its edges may read). Returns dict(blocks (decode order),
-    order (indices sorted by level), level_start, ac, idx, pal). Single tile; w, h multiples
+    order (indices sorted by level), level_start, ac, idx, pal, deps (per block, decode-order
+    indices of those owners)). Single tile; w, h multiples
     of 64."""
     from . import (INTRA_BOTTOM_LEFT, INTRA_DTYPE, INTRA_EDGE_FILTER, INTRA_HAVE_LEFT, INTRA_HAVE_TOP, INTRA_II,
                    INTRA_SMOOTH_NB, INTRA_TOP_RIGHT)
@@ -82,7 +83,7 @@ def make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.5, pal_
     nplanes = 3 if layout else 1
     dims = [(w, h)] + [((w + ss_h) >> ss_h, (h + ss_v) >> ss_v)] * (nplanes - 1)
     owner = [np.full((ph, pw), -1, np.int64) for pw, ph in dims]
-    level_of = []
+    level_of, dep_lists = [], []
     if edge_filter is None:
         edge_filter = int(rng.integers(0, 2))
     recs, ac, idx, pal = [], [], [], []
@@ -121,10 +122,11 @@ def make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.5, pal_
                     if ty > 0:
                         deps.append(own[ty - 1, max(tx - 1, 0):min(tx + 2 * tw, pw)])
                     lv = 0
-                    for d in deps:
-                        d = d[d >= 0]
-                        if d.size:
-                            lv = max(lv, 1 + max(level_of[i] for i in np.unique(d)))
+                    dep_ids = np.unique(np.concatenate(deps)) if deps else np.zeros(0, np.int64)
+                    dep_ids = dep_ids[dep_ids >= 0]
+                    if dep_ids.size:
+                        lv = 1 + max(level_of[i] for i in dep_ids)
+                    dep_lists.append(dep_ids)
                     mode, angle, filt, alpha, aux, poff = 0, 0, 0, 0, 0, 0
                     r = rng.random()
                     if r < pal_frac:
@@ -159,4 +161,4 @@ def make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.5, pal_
     level_start = np.searchsorted(lv[order], np.arange(lv.max() + 2)).astype(np.int64)
     cat = lambda xs, d: np.concatenate(xs) if xs else np.zeros(1, d)  # noqa: E731
     return dict(blocks=blocks, order=order, level_start=level_start, ac=cat(ac, np.int16), idx=cat(idx, np.uint8),
-                pal=cat(pal, dt))
+                pal=cat(pal, dt), deps=dep_lists)

@@ -93,3 +93,62 @@ def test_intra_recon_with_residuals(gpu, bpc, layout):
         if not np.array_equal(got, exp[p]):
             bad = np.argwhere(got != exp[p])
             raise AssertionError(f"plane {p}: {len(bad)} mismatches, first at {bad[0]}")
+
+
+def _oracle_recon(init, fr, bpc):
+    exp = [p.copy() for p in init]
+    for k in range(len(fr["blocks"])):
+        exp = oracle_lib.intra_blocks(exp, bpc, fr["blocks"][k:k + 1], fr["ac"], fr["idx"], fr["pal"])
+        t = fr["tx_blocks"][fr["tx_of_block"][k]:fr["tx_of_block"][k] + 1]
+        exp = oracle_lib.itx_frame(exp, t, fr["coef"].copy(), bpc)
+    return exp
+
+
+@pytest.mark.parametrize("bpc,layout,ii", [(8, 1, 0.0), (10, 1, 0.2), (12, 3, 0.0), (8, 0, 0.0), (10, 2, 0.1)])
+def test_intra_recon_fused(gpu, bpc, layout, ii):
+    """The persistent fused path (mi_intra_recon: one launch, per-block dependency waits,
+    prediction + residual per block) vs the oracle's interleaved decode-order recon."""
+    from rav1d_amd.intra import IntraFrame, device_status, make_intra_residuals
+    w, h = 256, 192
+    rng = np.random.default_rng(bpc * 37 + layout)
+    fr = make_intra_residuals(make_intra_frame(w, h, bpc, layout, rng, ii_frac=ii), bpc, rng)
+    cur = Frame(w, h, bpc, layout)
+    for p in range(len(cur.planes)):
+        cur.set_buffer_np(p, rng.integers(0, 1 << bpc, size=cur.buffer_np(p).shape))
+    init = [cur.buffer_np(p) for p in range(len(cur.planes))]
+    intra = IntraFrame(gpu, fr)
+    for rep in range(2):   # a second launch (new epoch) over the same buffers must give the same result
+        for p in range(len(cur.planes)):
+            cur.set_buffer_np(p, init[p])
+        intra.recon(cur.picture())
+        device_status(gpu)
+        exp = _oracle_recon(init, fr, bpc)
+        for p in range(len(cur.planes)):
+            got = cur.buffer_np(p)
+            if not np.array_equal(got, exp[p]):
+                bad = np.argwhere(got != exp[p])
+                raise AssertionError(f"rep {rep} plane {p}: {len(bad)} mismatches, first at {bad[0]}")
+
+
+def test_intra_recon_fused_multi_frame(gpu):
+    """Eight different frames in one launch (frame f on XCD f), large blocks and deep chains,
+    coefficients zeroed after use (the itxfm_add contract)."""
+    from rav1d_amd.intra import IntraFrame, device_status, intra_recon, make_intra_residuals
+    w, h, bpc, layout = 320, 192, 10, 1
+    frames, curs, inits, frs = [], [], [], []
+    for f in range(8):
+        rng = np.random.default_rng(1000 + f)
+        fr = make_intra_residuals(make_intra_frame(w, h, bpc, layout, rng, sb=64 if f % 2 else 128,
+                                                   min_bs=8 if f % 2 else 16, tx_split=0.3), bpc, rng)
+        cur = Frame(w, h, bpc, layout)
+        inits.append([cur.buffer_np(p) for p in range(len(cur.planes))])
+        frs.append(fr)
+        frames.append(IntraFrame(gpu, fr))
+        curs.append(cur)
+    intra_recon(gpu, [(frames[f], curs[f].picture()) for f in range(8)], keep_coefs=False)
+    device_status(gpu)
+    for f in range(8):
+        exp = _oracle_recon(inits[f], frs[f], bpc)
+        for p in range(3):
+            assert np.array_equal(curs[f].buffer_np(p), exp[p]), f"frame {f} plane {p}"
+        assert int(torch.count_nonzero(frames[f].coef)) == 0, f"frame {f}: coefficients not zeroed"
