@@ -179,10 +179,10 @@ def pmc_traffic(stage):
     return None if ent is None else ent.get("hbm_bytes_per_step")
 
 
-def intra_1080p8(ctx, reps=5, nframes=8, ndesc=4):
+def intra_1080p8(ctx, reps=5, nframes=24, ndesc=4):
     """configs[1]: 1080p 8-bit 4:2:0 intra frames, intra prediction (device edge gathering) +
     itx residual per transform block, reconstructed by the persistent fused kernel
-    (mi_intra_recon: one launch, per-block dependency waits, frame f on XCD f). Reports the
+    (mi_intra_recon: one launch, per-block dependency waits, frame f on XCD f % 8). Reports the
     single-frame latency, the throughput of `nframes` independent frames per launch (an
     all-intra stream's frames do not depend on each other; ndesc distinct synthetic descriptor
     sets, cycled, each frame its own picture) and, for comparison, the per-level launch path
@@ -225,7 +225,7 @@ def intra_1080p8(ctx, reps=5, nframes=8, ndesc=4):
                 frames_per_launch=nframes, batch_ms=round(batch_ms, 3),
                 single_frame_mpx_per_s=round(w * h / (one_ms / 1e3) / 1e6, 1),
                 level_launch_ms=round(level_ms, 3), levels=len(intra.levels), tx_blocks=int(len(fr["blocks"])),
-                kernel="intra_recon_kernel (persistent; 128 one-wave workers per XCD)")
+                kernel="intra_recon_kernel (persistent, one-wave workers, 3 frames per XCD)")
 
 
 def cpu_baseline(fr, budget_s=20.0):

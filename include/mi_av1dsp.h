@@ -302,9 +302,9 @@ int mi_intra_blocks(MiCtx *ctx, const MiPicture *pic, const MiIntraBlock *blocks
 
 /* Whole-frame intra reconstruction in ONE persistent launch: every transform block's
  * prediction (as mi_intra_blocks) plus its residual (as mi_itx_frame), in dependency order,
- * for up to 8 independent frames at once (frame f is reconstructed by the workgroups on XCD f,
- * which share one L2). Replaces recon_b_intra's per-block prepare_intra_edges / intra_pred /
- * itxfm_add sequence (recon.rs:2402-3160) for whole frames. Per frame (device arrays):
+ * for independent frames at once (the workgroups of one frame share one XCD, hence one L2).
+ * Replaces recon_b_intra's per-block prepare_intra_edges / intra_pred / itxfm_add sequence (recon.rs:2402-3160) for whole frames. Up to 24 frames per call; frame f
+ * is reconstructed by the workgroups on XCD f % 8. Per frame (device arrays):
  * blocks[n] in an order where every block comes after the blocks it depends on; tx[i] is the
  * residual of blocks[i] (same plane, position and size); deps[dep_start[i] ..
  * dep_start[i + 1]) are the indices (< i) of the blocks owning any pixel blocks[i]'s edges

@@ -25,9 +25,9 @@ struct MiCtx {
     // persistent intra reconstruction: per-block done epochs, queue heads, error word
     uint32_t *ir_done = nullptr;
     size_t ir_done_n = 0;
-    int *ir_words = nullptr;      // [0..7] queue heads, [8] error
+    int *ir_words = nullptr;      // [0..63] queue heads, [64] error, [72..79] XCD worker ranks
     uint32_t ir_epoch = 0;
-    int ir_last_n[8] = {0}, ir_last_frames = 0;
+    int ir_last_n[mi::kIrMaxFrames] = {0}, ir_last_frames = 0;
     ~MiCtx() {
         if (ir_done) (void)hipFree(ir_done);
         if (ir_words) (void)hipFree(ir_words);
@@ -307,7 +307,7 @@ int mi_intra_blocks(MiCtx *ctx, const MiPicture *pic, const MiIntraBlock *blocks
 }
 
 int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned flags, void *stream) {
-    if (!ctx || !frames || nframes < 1 || nframes > 8) return fail(ctx, -EINVAL);
+    if (!ctx || !frames || nframes < 1 || nframes > mi::kIrMaxFrames) return fail(ctx, -EINVAL);
     const int bpc = frames[0].pic.bpc;
     if (bpc != 8 && bpc != 10 && bpc != 12) return fail(ctx, -EINVAL);
     size_t total = 0;
@@ -318,8 +318,8 @@ int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned
         total += (size_t)fr.n;
     }
     if (!ctx->ir_words) {
-        if (hipMalloc(&ctx->ir_words, 16 * sizeof(int)) != hipSuccess) return fail(ctx, -ENOMEM);
-        if (hipMemset(ctx->ir_words, 0, 16 * sizeof(int)) != hipSuccess) return fail(ctx, -EIO);
+        if (hipMalloc(&ctx->ir_words, 128 * sizeof(int)) != hipSuccess) return fail(ctx, -ENOMEM);
+        if (hipMemset(ctx->ir_words, 0, 128 * sizeof(int)) != hipSuccess) return fail(ctx, -EIO);
     }
     if (total > ctx->ir_done_n) {
         if (ctx->ir_done) (void)hipFree(ctx->ir_done);
@@ -332,23 +332,8 @@ int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned
     }
     if (++ctx->ir_epoch == 0) ctx->ir_epoch = 1;   // done words hold the epoch of the last call
     hipStream_t s = (hipStream_t)stream;
-    if (hipMemsetAsync(ctx->ir_words, 0, 8 * sizeof(int), s) != hipSuccess) return fail(ctx, -EIO);
     mi::IntraReconArgs a;
     memset(&a, 0, sizeof(a));
-    a.err = ctx->ir_words + 8;
-#ifdef MI_IR_DEBUG
-    static int *dbg = nullptr;
-    if (!dbg && hipHostMalloc((void **)&dbg, 65536 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
-        return fail(ctx, -ENOMEM);
-    memset(dbg, 0, 65536 * sizeof(int));
-    int *ddbg = nullptr;
-    (void)hipHostGetDevicePointer((void **)&ddbg, dbg, 0);
-    a.dbg = ddbg;
-    setenv("MI_IR_DBG_PTR", std::to_string((uintptr_t)dbg).c_str(), 1);
-#endif
-    a.epoch = ctx->ir_epoch;
-    a.nframes = nframes;
-    a.zero_coefs = (flags & MI_ITX_KEEP_COEFS) ? 0 : 1;
     size_t off = 0;
     for (int f = 0; f < nframes; f++) {
         const MiIntraFrame &fr = frames[f];
@@ -371,24 +356,46 @@ int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned
         d.n = fr.n;
         off += (size_t)fr.n;
     }
+    // queue heads and XCD worker ranks start from 0 in stream order
+    if (hipMemsetAsync(ctx->ir_words, 0, 64 * sizeof(int), s) != hipSuccess ||
+        hipMemsetAsync(ctx->ir_words + 72, 0, 8 * sizeof(int), s) != hipSuccess)
+        return fail(ctx, -EIO);
+    a.xcd_rank = ctx->ir_words + 72;
+    a.err = ctx->ir_words + 64;
+#ifdef MI_IR_DEBUG
+    static int *dbg = nullptr;
+    if (!dbg && hipHostMalloc((void **)&dbg, 65536 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return fail(ctx, -ENOMEM);
+    memset(dbg, 0, 65536 * sizeof(int));
+    int *ddbg = nullptr;
+    (void)hipHostGetDevicePointer((void **)&ddbg, dbg, 0);
+    a.dbg = ddbg;
+    setenv("MI_IR_DBG_PTR", std::to_string((uintptr_t)dbg).c_str(), 1);
+#endif
+    a.epoch = ctx->ir_epoch;
+    a.nframes = nframes;
+    a.zero_coefs = (flags & MI_ITX_KEEP_COEFS) ? 0 : 1;
     ctx->ir_last_frames = nframes;
     for (int f = 0; f < nframes; f++) ctx->ir_last_n[f] = frames[f].n;
-    // 128 one-wave workers per XCD (occupancy allows 3 per SIMD = 384 per XCD): a look-ahead
-    // of several dependency levels
-    return mi::launch_intra_recon(a, 128, s) ? fail(ctx, -EIO) : 0;
+    // one-wave workers per XCD (occupancy allows 3 per SIMD = 384 per XCD): 128, plus 64 per
+    // extra frame the XCD serves
+    const int per_xcd = (nframes + 7) / 8;
+    static const int wenv = getenv("MI_IR_WORKERS") ? atoi(getenv("MI_IR_WORKERS")) : 0;
+    const int wpx = wenv ? wenv : std::min(384, 128 + 64 * (per_xcd - 1));
+    return mi::launch_intra_recon(a, bpc, wpx, s) ? fail(ctx, -EIO) : 0;
 }
 
 int mi_ctx_device_status(MiCtx *ctx, void *stream) {
     if (!ctx) return -EINVAL;
     if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(ctx, -EIO);
     if (!ctx->ir_words) return 0;
-    int w[9];
+    int w[65];
     if (hipMemcpy(w, ctx->ir_words, sizeof(w), hipMemcpyDeviceToHost) != hipSuccess) return fail(ctx, -EIO);
     if (getenv("MI_DEBUG"))
         fprintf(stderr, "mi_ctx_device_status: heads %d %d %d %d %d %d %d %d err %d\n", w[0], w[1], w[2], w[3], w[4],
-                w[5], w[6], w[7], w[8]);
-    if (w[8]) {
-        (void)hipMemset(ctx->ir_words + 8, 0, sizeof(int));
+                w[5], w[6], w[7], w[64]);
+    if (w[64]) {
+        (void)hipMemset(ctx->ir_words + 64, 0, sizeof(int));
         return fail(ctx, -ETIMEDOUT);
     }
     // every block of the last launch was taken by a worker (a frame whose XCD received no

@@ -175,7 +175,7 @@ struct IpredArgs {
     const uint8_t *pal;
     int bpc, bdmax;
 };
-// persistent fused intra reconstruction (ipred.hip): frame f is worked on by XCD f
+// persistent fused intra reconstruction (ipred.hip): frame f is worked on by XCD f % 8
 struct IntraReconFrame {
     IpredArgs ip;                 // picture planes / strides, iblocks, ac, idx, pal, bpc, bdmax
     const MiTxBlock *tx;
@@ -185,14 +185,16 @@ struct IntraReconFrame {
     int *head;                    // queue head
     int n;
 };
+constexpr int kIrMaxFrames = 24;     // descriptors travel as kernel arguments (4 KB limit)
 struct IntraReconArgs {
-    IntraReconFrame fr[8];
+    IntraReconFrame fr[kIrMaxFrames];   // frame f on XCD f % 8
+    int *xcd_rank;                // [8] worker counters (zeroed per launch)
     int *err;
     int *dbg;                     // MI_IR_DEBUG builds: host-mapped progress words
     uint32_t epoch;
     int nframes, zero_coefs;
 };
-int launch_intra_recon(const IntraReconArgs &a, int wg_per_xcd, hipStream_t s);
+int launch_intra_recon(const IntraReconArgs &a, int bpc, int wg_per_xcd, hipStream_t s);
 // launchers (ipred.hip)
 int launch_ipred(const IpredArgs &a, int n, hipStream_t s);
 int launch_intra(const IpredArgs &a, int n, hipStream_t s);

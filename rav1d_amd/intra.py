@@ -118,8 +118,8 @@ class IntraFrame:
 
 
 def intra_recon(ctx, frames, stream=None, keep_coefs=True):
-    """Reconstruct up to 8 independent intra frames in one launch: frames = [(IntraFrame,
-    MiPicture)], frame f on XCD f."""
+    """Reconstruct up to 24 independent intra frames in one launch: frames = [(IntraFrame,
+    MiPicture)], frame f on XCD f % 8."""
     from . import MiIntraFrame
     descs = (MiIntraFrame * len(frames))(*[f.frame_desc(p) for f, p in frames])
     flags = ITX_KEEP_COEFS if keep_coefs else 0

@@ -130,13 +130,15 @@ def test_intra_recon_fused(gpu, bpc, layout, ii):
                 raise AssertionError(f"rep {rep} plane {p}: {len(bad)} mismatches, first at {bad[0]}")
 
 
-def test_intra_recon_fused_multi_frame(gpu):
-    """Eight different frames in one launch (frame f on XCD f), large blocks and deep chains,
-    coefficients zeroed after use (the itxfm_add contract)."""
+@pytest.mark.parametrize("nframes", [8, 19])
+def test_intra_recon_fused_multi_frame(gpu, nframes):
+    """Several different frames in one launch (frame f on XCD f % 8; 19 frames: XCDs serving
+    two and three frames), large blocks and deep chains, coefficients zeroed after use (the
+    itxfm_add contract)."""
     from rav1d_amd.intra import IntraFrame, device_status, intra_recon, make_intra_residuals
     w, h, bpc, layout = 320, 192, 10, 1
     frames, curs, inits, frs = [], [], [], []
-    for f in range(8):
+    for f in range(nframes):
         rng = np.random.default_rng(1000 + f)
         fr = make_intra_residuals(make_intra_frame(w, h, bpc, layout, rng, sb=64 if f % 2 else 128,
                                                    min_bs=8 if f % 2 else 16, tx_split=0.3), bpc, rng)
@@ -145,9 +147,9 @@ def test_intra_recon_fused_multi_frame(gpu):
         frs.append(fr)
         frames.append(IntraFrame(gpu, fr))
         curs.append(cur)
-    intra_recon(gpu, [(frames[f], curs[f].picture()) for f in range(8)], keep_coefs=False)
+    intra_recon(gpu, [(frames[f], curs[f].picture()) for f in range(nframes)], keep_coefs=False)
     device_status(gpu)
-    for f in range(8):
+    for f in range(nframes):
         exp = _oracle_recon(inits[f], frs[f], bpc)
         for p in range(3):
             assert np.array_equal(curs[f].buffer_np(p), exp[p]), f"frame {f} plane {p}"
