@@ -168,6 +168,10 @@ def film_grain_8k(ctx, stream, reps=20):
                 prep_ms=round(prep_ms, 4), apply_gbs=round(2 * fb / (apply_ms / 1e3) / 1e9, 1))
 
 
+def per_launch(v, launches):
+    return None if v is None else int(v // launches)
+
+
 def pmc_traffic(stage):
     """HBM bytes per step of `stage` from the committed PMC run (profiles/r01_traffic.json,
     written by tools/traffic_json.py from tools/gpu_pmc.sh's FETCH_SIZE / WRITE_SIZE passes of
@@ -244,6 +248,25 @@ def cpu_baseline(fr, budget_s=20.0):
                        f"(mc+itx+deblock+cdef+lr), 1 thread, {el:.1f}s")
 
 
+def timed_region(step, steps, sync, world, device):
+    """The timed region of the bench contract: barrier + sync, exactly `steps` steps, sync +
+    barrier, then the MAX of the per-rank wall times over all ranks (world > 1: an initialised
+    process group; `device` holds the reduction tensor: "cuda" under RCCL, "cpu" under gloo)."""
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -278,20 +301,7 @@ def main():
     torch.cuda.synchronize()
     stage_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        pipe.step(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = timed_region(lambda: pipe.step(stream), args.steps, torch.cuda.synchronize, world, "cuda")
 
     dom = max(stage_ms, key=stage_ms.get)
     achieved = pipe.algo[dom] / (stage_ms[dom] / 1e3) / 1e9
@@ -317,10 +327,15 @@ def main():
                        "parallelism": f"replicas{world} (one independent stream per GPU)"},
             "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
             "stage_gbs": {k: round(pipe.algo[k] / (stage_ms[k] / 1e3) / 1e9, 1) for k in stage_ms if k in pipe.algo},
+            # per launch: algorithmic bytes / mean launch duration (the stage's events span its
+            # launches_per_step launches); traffic = PMC HBM bytes per launch (r01_traffic.json)
             "roofline": {"kernel": pipe.kernels[dom], "stage": dom, "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom),
-                         "algo_bytes_per_step": pipe.algo[dom], "launches_per_step": pipe.launches[dom]},
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": per_launch(pmc_traffic(dom), pipe.launches[dom]),
+                         "algo_bytes_per_launch": pipe.algo[dom] // pipe.launches[dom],
+                         "launch_us": round(stage_ms[dom] * 1e3 / pipe.launches[dom], 2),
+                         "launches_per_step": pipe.launches[dom]},
         }
         if world == 1 and not args.no_fg:
             out["film_grain_8k10"] = film_grain_8k(ctx, stream)

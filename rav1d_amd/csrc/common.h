@@ -24,6 +24,17 @@ __device__ inline int xcd_block(int b, int n) {
 #endif
 }
 
+// Chunked XCD interleave: XCD b % 8 processes runs of C consecutive work items, the runs dealt
+// round robin over the XCDs. Neighbouring items (spatially sorted units) share one L2 while
+// every XCD still samples the whole list (balanced where the cost per item drifts along
+// it). Bijective on [0, n): whole rounds of 8 * C items are permuted, the tail is identity.
+__device__ inline int xcd_chunk(int b, int n, int C) {
+    const int full = n / (8 * C) * (8 * C);
+    if (b >= full || C <= 1) return b;
+    const int x = b & 7, r = b >> 3;
+    return ((r / C) * 8 + x) * C + (r % C);
+}
+
 // RectTxfmSize -> dimensions (src/levels.rs:46-82) and the inverse-transform row shift
 // (src/itx.rs:439-457; C src/itx_tmpl.c:142-160).
 struct TxDim { int w, h, shift; };

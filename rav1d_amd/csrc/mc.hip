@@ -157,7 +157,10 @@ template <typename Px>
 __global__ __launch_bounds__(64) void mc_kernel(McArgs a, int g) {
     __shared__ __attribute__((aligned(16))) int16_t win[2][kWinElems];
     const int lane = threadIdx.x;
-    const int wave = blockIdx.x;
+#ifndef MI_MC_XCD_CHUNK
+#define MI_MC_XCD_CHUNK 1
+#endif
+    const int wave = xcd_chunk(blockIdx.x, gridDim.x, MI_MC_XCD_CHUNK);
     // class of this wave: last class whose first wave <= wave (wave-uniform scan)
     const uint32_t *fw = a.first_wave[g];
     int c = 0;

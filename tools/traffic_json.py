@@ -21,7 +21,7 @@ CALIB_BYTES = 1 << 30
 STAGES = {
     "mc": (["mc_kernel"], 2, 2),                      # per-pixel u16 window gathers
     "itx": (["itx_frame_kernel"], 8, 2),
-    "deblock": (["lf_cols_kernel", "lf_rows_kernel"], 2, 2),
+    "deblock": (["lf_tile_kernel"], 16, 16),           # uint4 tile staging and stores
     "cdef": (["cdef_kernel"], 8, 8),                  # uint2 tile rows
     "lr": (["lr_kernel"], 2, 2),
 }
