@@ -422,6 +422,33 @@ int mi_dsp_itxfm_add(int tx, int txtp, void *dst, ptrdiff_t stride, void *coeff,
 int mi_dsp_intra_pred(int mode, void *dst, ptrdiff_t stride, const void *topleft, int w, int h,
                       int angle, int max_width, int max_height, int bitdepth_max);
 
+/* The remaining per-call entries of the intra, loop-filter and CDEF tables. Same contract as
+ * above: host or device pointers, synchronous, 0 (or the documented value) / -errno. The
+ * trailing bitdepth_max selects the pixel size where the reference's signature has none. */
+
+/* cfl_pred[mode] (src/ipred.rs:108-117, C ipred_tmpl.c:71-84): mode 0 DC, 3 LEFT_DC, 4 TOP_DC,
+ * 5 DC_128; ac: w * h int16 (cfl_ac's output). */
+int mi_dsp_cfl_pred(int mode, void *dst, ptrdiff_t stride, const void *topleft, int w, int h, const int16_t *ac,
+                    int alpha, int bitdepth_max);
+/* pal_pred (src/ipred.rs:138-145, 1433-1452): idx one byte per pixel, w * h. */
+int mi_dsp_pal_pred(void *dst, ptrdiff_t stride, const void *pal, const uint8_t *idx, int w, int h, int bitdepth_max);
+/* cfl_ac[layout - 1] (src/ipred.rs:82-90, 1326-1432): layout 1 I420, 2 I422, 3 I444. */
+int mi_dsp_cfl_ac(int layout, int16_t *ac, const void *y, ptrdiff_t stride, int w_pad, int h_pad, int cw, int ch,
+                  int bitdepth_max);
+/* loop_filter_sb[cls][dir] (src/loopfilter.rs:20-34, 745-985): cls 0 luma / 1 chroma, dir 0
+ * column edges (h_sb*) / 1 row edges (v_sb*); vmask[3] (luma) or [2] (chroma) bit k = 4-px
+ * unit k of the run; lvl points at the run's first [u8;4] level entry (already offset to
+ * the slot used), b4_stride entries per row; lut = Av1FilterLUT (e[64], i[64], ...). */
+int mi_dsp_loop_filter_sb(int cls, int dir, void *dst, ptrdiff_t stride, const uint32_t *vmask,
+                          const uint8_t (*lvl)[4], ptrdiff_t b4_stride, const void *lut, int wh, int bitdepth_max);
+/* cdef.fb[fb] (src/cdef.rs:35-56, 567-820): fb 0 8x8, 1 4x8, 2 4x4; left [h][2] pixels; top /
+ * bottom point at the block's column 0 of the two rows above / below (stride as dst); edges =
+ * CdefEdgeFlags (HAVE_LEFT 1, HAVE_RIGHT 2, HAVE_TOP 4, HAVE_BOTTOM 8). In place on dst. */
+int mi_dsp_cdef_filter(int fb, void *dst, ptrdiff_t stride, const void *left, const void *top, const void *bottom,
+                       int pri, int sec, int dir, int damping, int edges, int bitdepth_max);
+/* cdef.dir (src/cdef.rs:921-1031): returns the direction 0..7 (or -errno), *var the variance. */
+int mi_dsp_cdef_dir(const void *img, ptrdiff_t stride, unsigned *var, int bitdepth_max);
+
 #ifdef __cplusplus
 }
 #endif

@@ -138,6 +138,15 @@ def lib():
     _sig(L, "mi_ctx_device_status", ctypes.c_int, [_VP, _VP])
     _sig(L, "mi_ipred_blocks", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.c_int, _VP, _VP, _VP, _VP])
     _sig(L, "mi_dsp_intra_pred", ctypes.c_int, [ctypes.c_int, _VP, ctypes.c_ssize_t, _VP] + [ctypes.c_int] * 6)
+    _SS = ctypes.c_ssize_t
+    _sig(L, "mi_dsp_cfl_pred", ctypes.c_int, [ctypes.c_int, _VP, _SS, _VP, ctypes.c_int, ctypes.c_int, _VP,
+                                              ctypes.c_int, ctypes.c_int])
+    _sig(L, "mi_dsp_pal_pred", ctypes.c_int, [_VP, _SS, _VP, _VP, ctypes.c_int, ctypes.c_int, ctypes.c_int])
+    _sig(L, "mi_dsp_cfl_ac", ctypes.c_int, [ctypes.c_int, _VP, _VP, _SS] + [ctypes.c_int] * 5)
+    _sig(L, "mi_dsp_loop_filter_sb", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _VP, _SS, _VP, _VP, _SS, _VP,
+                                                    ctypes.c_int, ctypes.c_int])
+    _sig(L, "mi_dsp_cdef_filter", ctypes.c_int, [ctypes.c_int, _VP, _SS, _VP, _VP, _VP] + [ctypes.c_int] * 6)
+    _sig(L, "mi_dsp_cdef_dir", ctypes.c_int, [_VP, _SS, _VP, ctypes.c_int])
     _sig(L, "mi_deblock_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiLoopFilter), _VP])
     _sig(L, "mi_deblock_frame_to", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
                                                   ctypes.POINTER(MiLoopFilter), _VP])
@@ -158,7 +167,8 @@ EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error"
             "mi_itx_frame", "mi_mc_frame", "mi_mc_scaled", "mi_mc_warp", "mi_mc_combine", "mi_superres_frame",
             "mi_ipred_blocks", "mi_intra_blocks", "mi_intra_recon", "mi_ctx_device_status", "mi_deblock_frame", "mi_deblock_frame_to", "mi_cdef_frame", "mi_lr_frame",
             "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply",
-            "mi_dsp_itxfm_add", "mi_dsp_intra_pred"]
+            "mi_dsp_itxfm_add", "mi_dsp_intra_pred", "mi_dsp_cfl_pred", "mi_dsp_pal_pred", "mi_dsp_cfl_ac",
+            "mi_dsp_loop_filter_sb", "mi_dsp_cdef_filter", "mi_dsp_cdef_dir"]
 
 
 def check(rc, what):

@@ -796,4 +796,243 @@ int mi_dsp_intra_pred(int mode, void *dst, ptrdiff_t stride, const void *topleft
     return 0;
 }
 
+// ---- helpers of the remaining per-call entries: caller pixel windows <-> device scratch ----
+namespace {
+int bpc_of(int bitdepth_max) {
+    return bitdepth_max == 255 ? 8 : bitdepth_max == 1023 ? 10 : bitdepth_max == 4095 ? 12 : 0;
+}
+// rows [r0, r1) x bytes [b0, b1) around `base` (host or device, any stride sign) <-> a packed
+// device window of pitch (b1 - b0)
+int win_in(uint8_t *dev, const void *base, ptrdiff_t stride, int r0, int r1, ptrdiff_t b0, ptrdiff_t b1, hipStream_t s) {
+    for (int r = r0; r < r1; r++)
+        if (hipMemcpyAsync(dev + (size_t)(r - r0) * (b1 - b0), (const uint8_t *)base + r * stride + b0, b1 - b0,
+                           hipMemcpyDefault, s) != hipSuccess)
+            return -EIO;
+    return 0;
+}
+int win_out(void *base, ptrdiff_t stride, const uint8_t *dev, int r0, int r1, ptrdiff_t b0, ptrdiff_t b1, hipStream_t s) {
+    for (int r = r0; r < r1; r++)
+        if (hipMemcpyAsync((uint8_t *)base + r * stride + b0, dev + (size_t)(r - r0) * (b1 - b0), b1 - b0,
+                           hipMemcpyDefault, s) != hipSuccess)
+            return -EIO;
+    return hipStreamSynchronize(s) == hipSuccess ? 0 : -EIO;
+}
+int copy_in(void *dev, const void *src, size_t n, hipStream_t s) {
+    return hipMemcpyAsync(dev, src, n, hipMemcpyDefault, s) == hipSuccess ? 0 : -EIO;
+}
+}  // namespace
+
+extern "C" {
+
+int mi_dsp_cfl_pred(int mode, void *dst, ptrdiff_t stride, const void *topleft, int w, int h, const int16_t *ac,
+                    int alpha, int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || !dst || !topleft || !ac || (mode != 0 && mode != 3 && mode != 4 && mode != 5) || w < 4 || h < 4 ||
+        w > 32 || h > 32 || (w & (w - 1)) || (h & (h - 1)))
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    const int px = bpc == 8 ? 1 : 2;
+    hipStream_t s = g_call.stream;
+    uint8_t *dpix = g_call.scratch, *dedge = dpix + 64 * 128, *dac = dedge + 1024;
+    MiIpredBlock *dblk = (MiIpredBlock *)(dac + 64 * 64 * 2);
+    int e = copy_in(dedge, (const uint8_t *)topleft - (ptrdiff_t)h * px, (size_t)(w + h + 1) * px, s);
+    if (!e) e = copy_in(dac, ac, (size_t)w * h * 2, s);
+    MiIpredBlock hb{};
+    hb.edge_off = (uint32_t)h;
+    hb.w = (uint8_t)w;
+    hb.h = (uint8_t)h;
+    hb.mode = (uint8_t)(MI_IPRED_CFL + mode);
+    hb.alpha = (int8_t)alpha;
+    if (!e) e = copy_in(dblk, &hb, sizeof(hb), s);
+    if (e) return e;
+    mi::IpredArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int p = 0; p < 3; p++) a.dst[p] = dpix;
+    a.stride[0] = a.stride[1] = (int64_t)w * px;
+    a.blocks = dblk;
+    a.edges = dedge;
+    a.ac = (const int16_t *)dac;
+    a.bpc = bpc;
+    a.bdmax = bitdepth_max;
+    if (mi::launch_ipred(a, 1, s)) return -EIO;
+    return win_out(dst, stride, dpix, 0, h, 0, (ptrdiff_t)w * px, s);
+}
+
+int mi_dsp_pal_pred(void *dst, ptrdiff_t stride, const void *pal, const uint8_t *idx, int w, int h, int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || !dst || !pal || !idx || w < 4 || h < 4 || w > 64 || h > 64) return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    const int px = bpc == 8 ? 1 : 2;
+    hipStream_t s = g_call.stream;
+    uint8_t *dpix = g_call.scratch, *dpal = dpix + 64 * 128, *didx = dpal + 64;
+    MiIpredBlock *dblk = (MiIpredBlock *)(didx + 64 * 64);
+    int e = copy_in(dpal, pal, 8 * (size_t)px, s);
+    if (!e) e = copy_in(didx, idx, (size_t)w * h, s);
+    MiIpredBlock hb{};
+    hb.w = (uint8_t)w;
+    hb.h = (uint8_t)h;
+    hb.mode = MI_IPRED_PAL;
+    if (!e) e = copy_in(dblk, &hb, sizeof(hb), s);
+    if (e) return e;
+    mi::IpredArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int p = 0; p < 3; p++) a.dst[p] = dpix;
+    a.stride[0] = a.stride[1] = (int64_t)w * px;
+    a.blocks = dblk;
+    a.edges = dpal;
+    a.idx = didx;
+    a.bpc = bpc;
+    a.bdmax = bitdepth_max;
+    if (mi::launch_ipred(a, 1, s)) return -EIO;
+    return win_out(dst, stride, dpix, 0, h, 0, (ptrdiff_t)w * px, s);
+}
+
+int mi_dsp_cfl_ac(int layout, int16_t *ac, const void *y, ptrdiff_t stride, int w_pad, int h_pad, int cw, int ch,
+                  int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || !ac || !y || layout < 1 || layout > 3 || cw < 4 || ch < 4 || cw > 32 || ch > 32 ||
+        (cw & (cw - 1)) || (ch & (ch - 1)) || w_pad < 0 || h_pad < 0 || 4 * w_pad >= cw || 4 * h_pad >= ch)
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    const int px = bpc == 8 ? 1 : 2;
+    const int ss_hor = layout != 3, ss_ver = layout == 1;
+    const int rows = (ch - 4 * h_pad) << ss_ver, cols = (cw - 4 * w_pad) << ss_hor;
+    hipStream_t s = g_call.stream;
+    uint8_t *dy = g_call.scratch;
+    int16_t *dac = (int16_t *)(dy + 64 * 128);
+    if (int e = win_in(dy, y, stride, 0, rows, 0, (ptrdiff_t)cols * px, s)) return e;
+    mi::CflAcArgs a;
+    a.ac = dac;
+    a.y = dy;
+    a.stride = (int64_t)cols * px;
+    a.w_pad = w_pad;
+    a.h_pad = h_pad;
+    a.cw = cw;
+    a.ch = ch;
+    a.ss_hor = ss_hor;
+    a.ss_ver = ss_ver;
+    if (mi::launch_cfl_ac(a, bpc, s)) return -EIO;
+    if (hipMemcpyAsync(ac, dac, (size_t)cw * ch * 2, hipMemcpyDefault, s) != hipSuccess) return -EIO;
+    return hipStreamSynchronize(s) == hipSuccess ? 0 : -EIO;
+}
+
+int mi_dsp_loop_filter_sb(int cls, int dir, void *dst, ptrdiff_t stride, const uint32_t *vmask,
+                          const uint8_t (*lvl)[4], ptrdiff_t b4_stride, const void *lut, int wh, int bitdepth_max) {
+    (void)wh;
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || cls < 0 || cls > 1 || dir < 0 || dir > 1 || !dst || !vmask || !lvl || !lut) return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    const int px = bpc == 8 ? 1 : 2;
+    hipStream_t s = g_call.stream;
+    mi::LfCallArgs a;
+    memset(&a, 0, sizeof(a));
+    if (hipMemcpy(a.vmask, vmask, (cls ? 2 : 3) * sizeof(uint32_t), hipMemcpyDefault) != hipSuccess) return -EIO;
+    const unsigned vm = a.vmask[0] | a.vmask[1] | a.vmask[2];
+    if (!vm) return 0;
+    const int nu = 32 - __builtin_clz(vm);                 // units up to the highest set bit
+    // level pairs {unit, neighbour}: the caller's map is strided (b4_stride entries per row)
+    uint8_t lv[64] = {0};
+    const ptrdiff_t ul = dir == 0 ? b4_stride : 1, pl = dir == 0 ? -1 : -b4_stride;
+    for (int k = 0; k < nu; k++) {
+        if (!(vm & (1u << k))) continue;
+        if (hipMemcpy(&lv[2 * k], &lvl[k * ul][0], 1, hipMemcpyDefault) != hipSuccess ||
+            hipMemcpy(&lv[2 * k + 1], &lvl[k * ul + pl][0], 1, hipMemcpyDefault) != hipSuccess)
+            return -EIO;
+    }
+    uint8_t lt[128];
+    if (hipMemcpy(lt, lut, 128, hipMemcpyDefault) != hipSuccess) return -EIO;   // Av1FilterLUT.e, .i
+    memcpy(a.lim_e, lt, 64);
+    memcpy(a.lim_i, lt + 64, 64);
+    // the pixel window: 8 samples either side of the edge, 4 * nu along it
+    const int r0 = dir == 0 ? 0 : -8, r1 = dir == 0 ? 4 * nu : 8;
+    const ptrdiff_t b0 = (dir == 0 ? -8 : 0) * px, b1 = (dir == 0 ? 8 : 4 * nu) * px;
+    uint8_t *dwin = g_call.scratch, *dlv = dwin + (1 << 19);
+    if (int e = win_in(dwin, dst, stride, r0, r1, b0, b1, s)) return e;
+    if (int e = copy_in(dlv, lv, sizeof(lv), s)) return e;
+    a.dst = dwin + (size_t)(-r0) * (b1 - b0) - b0;
+    a.stride = b1 - b0;
+    a.lvl = dlv;
+    a.cls = cls;
+    a.dir = dir;
+    a.bdm8 = bpc - 8;
+    a.bdmax = bitdepth_max;
+    if (mi::launch_lf_sb_call(a, bpc, s)) return -EIO;
+    return win_out(dst, stride, dwin, r0, r1, b0, b1, s);
+}
+
+int mi_dsp_cdef_filter(int fb, void *dst, ptrdiff_t stride, const void *left, const void *top, const void *bottom,
+                       int pri, int sec, int dir, int damping, int edges, int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || fb < 0 || fb > 2 || !dst || dir < 0 || dir > 7 || pri < 0 || sec < 0) return -EINVAL;
+    const int w = fb == 0 ? 8 : 4, h = fb == 2 ? 4 : 8;
+    if (((edges & 1) && !left) || ((edges & 4) && !top) || ((edges & 8) && !bottom)) return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    const int px = bpc == 8 ? 1 : 2;
+    hipStream_t s = g_call.stream;
+    // one packed window, pitch P, column 0 = x - 2: rows 0-1 from top, 2..h+1 the block,
+    // h+2..h+3 from bottom; only the columns the edge flags allow are read from the caller
+    const ptrdiff_t P = (ptrdiff_t)(w + 4) * px;
+    const ptrdiff_t x0 = (edges & 1) ? -2 * px : 0, x1 = (ptrdiff_t)(w + ((edges & 2) ? 2 : 0)) * px;
+    uint8_t *win = g_call.scratch, *dleft = win + 4096, *dout = dleft + 4096;
+    auto rows = [&](const void *src, int r0, int n, ptrdiff_t c0) -> int {
+        for (int r = 0; r < n; r++)
+            if (hipMemcpyAsync(win + (size_t)(r0 + r) * P + 2 * px + c0, (const uint8_t *)src + r * stride + c0, x1 - c0,
+                               hipMemcpyDefault, s) != hipSuccess)
+                return -EIO;
+        return 0;
+    };
+    int e = rows(dst, 2, h, 0);
+    if (!e && (edges & 4)) e = rows(top, 0, 2, x0);
+    if (!e && (edges & 8)) e = rows(bottom, 2 + h, 2, x0);
+    if (!e && (edges & 1)) e = copy_in(dleft, left, (size_t)h * 2 * px, s);
+    if (e) return e;
+    mi::CdefCallArgs a;
+    memset(&a, 0, sizeof(a));
+    a.top = win + 2 * px;
+    a.dst = win + 2 * P + 2 * px;
+    a.bottom = win + (2 + h) * P + 2 * px;
+    a.left = dleft;
+    a.out = dout;
+    a.stride = P;
+    a.w = w;
+    a.h = h;
+    a.pri = pri;
+    a.sec = sec;
+    a.dir = dir;
+    a.damping = damping;
+    a.edges = edges;
+    a.bdm8 = bpc - 8;
+    if (mi::launch_cdef_call(a, bpc, false, s)) return -EIO;
+    return win_out(dst, stride, dout, 0, h, 0, (ptrdiff_t)w * px, s);
+}
+
+int mi_dsp_cdef_dir(const void *img, ptrdiff_t stride, unsigned *var, int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || !img || !var) return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    const int px = bpc == 8 ? 1 : 2;
+    hipStream_t s = g_call.stream;
+    uint8_t *win = g_call.scratch, *dout = win + 4096;
+    if (int e = win_in(win, img, stride, 0, 8, 0, 8 * px, s)) return e;
+    mi::CdefCallArgs a;
+    memset(&a, 0, sizeof(a));
+    a.dst = win;
+    a.out = dout;
+    a.stride = 8 * px;
+    a.bdm8 = bpc - 8;
+    if (mi::launch_cdef_call(a, bpc, true, s)) return -EIO;
+    int r[2];
+    if (hipMemcpyAsync(r, dout, sizeof(r), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    *var = (unsigned)r[1];
+    return r[0];
+}
+
+}  // extern "C"
 } // extern "C"

@@ -416,6 +416,68 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
     }
 }
 
+// ---- per-call cdef.fb[] / cdef.dir (cdef.rs:567-1031) ----
+// One block (8x8, 4x8 or 4x4): the padded i16 tile is built in LDS as the reference's
+// `padding` does (the block from dst, 2 columns from left, 2 rows above from top and below
+// from bottom, i16::MIN where `edges` says the neighbour is missing), then one lane per pixel.
+constexpr int kCallTs = 12;
+template <typename Px>
+__global__ __launch_bounds__(64) void cdef_call_kernel(CdefCallArgs a) {
+    __shared__ int16_t tb[kCallTs * kCallTs];
+    int16_t *t = tb + 2 * kCallTs + 2;
+    const int lane = threadIdx.x, w = a.w, h = a.h;
+    const int64_t ps = a.stride / (int64_t)sizeof(Px);
+    const Px *dst = reinterpret_cast<const Px *>(a.dst), *top = reinterpret_cast<const Px *>(a.top);
+    const Px *bot = reinterpret_cast<const Px *>(a.bottom), *left = reinterpret_cast<const Px *>(a.left);
+    for (int i = lane; i < kCallTs * kCallTs; i += 64) {
+        const int y = i / kCallTs - 2, x = i % kCallTs - 2;
+        int v = INT16_MIN;
+        if (y < h + 2 && x < w + 2) {
+            const bool in_x = x >= 0 ? (x < w || (a.edges & 2)) : (a.edges & 1);   // HAVE_RIGHT 2, HAVE_LEFT 1
+            const bool in_y = y >= 0 ? (y < h || (a.edges & 8)) : (a.edges & 4);   // HAVE_BOTTOM 8, HAVE_TOP 4
+            if (in_x && in_y) {
+                if (y < 0) v = top[(y + 2) * ps + x];
+                else if (y >= h) v = bot[(y - h) * ps + x];
+                else if (x < 0) v = left[y * 2 + 2 + x];
+                else v = dst[y * ps + x];
+            }
+        }
+        tb[i] = (int16_t)v;
+    }
+    __syncthreads();
+    if (lane < w * h) {
+        const int y = lane / w, x = lane % w;
+        const int v = cdef_px(t, kCallTs, x, y, a.pri, a.sec, a.dir, a.damping, a.bdm8);
+        reinterpret_cast<Px *>(a.out)[y * w + x] = (Px)v;
+    }
+}
+
+template <typename Px>
+__global__ __launch_bounds__(64) void cdef_dir_call_kernel(CdefCallArgs a) {
+    __shared__ int16_t t[64];
+    const int64_t ps = a.stride / (int64_t)sizeof(Px);
+    const int lane = threadIdx.x;
+    t[lane] = (int16_t)reinterpret_cast<const Px *>(a.dst)[(lane >> 3) * ps + (lane & 7)];
+    __syncthreads();
+    if (lane == 0) {
+        unsigned var;
+        const int d = find_dir(t, 8, a.bdm8, &var);
+        reinterpret_cast<int *>(a.out)[0] = d;
+        reinterpret_cast<unsigned *>(a.out)[1] = var;
+    }
+}
+
+int launch_cdef_call(const CdefCallArgs &a, int bpc, bool dir, hipStream_t s) {
+    if (dir) {
+        if (bpc == 8) cdef_dir_call_kernel<uint8_t><<<1, 64, 0, s>>>(a);
+        else cdef_dir_call_kernel<uint16_t><<<1, 64, 0, s>>>(a);
+    } else {
+        if (bpc == 8) cdef_call_kernel<uint8_t><<<1, 64, 0, s>>>(a);
+        else cdef_call_kernel<uint16_t><<<1, 64, 0, s>>>(a);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 int launch_cdef(const CdefArgs &a, int tiles, int bpc, hipStream_t s) {
     if (tiles <= 0) return 0;
 #define MI_CDEF_LAUNCH(L)                                                                            \

@@ -240,4 +240,31 @@ struct FgArgs {
 int init_fg_tables();
 int launch_fg(const FgArgs &a, hipStream_t s, bool prep, bool apply);
 
+// ---- per-call (table-compatible) entry points: single-block kernels ----
+struct LfCallArgs {
+    uint8_t *dst;
+    int64_t stride;
+    const uint8_t *lvl;             // [32][2]: unit level, neighbour level
+    uint32_t vmask[3];
+    int cls, dir, bdm8, bdmax;
+    uint8_t lim_e[64], lim_i[64];
+};
+int launch_lf_sb_call(const LfCallArgs &a, int bpc, hipStream_t s);   // lf.hip
+
+struct CdefCallArgs {
+    const uint8_t *dst, *left, *top, *bottom;   // dst: the block (read); left: [h][2]
+    uint8_t *out;                               // filter: w x h packed; dir: {dir, var}
+    int64_t stride;
+    int w, h, pri, sec, dir, damping, edges, bdm8;
+};
+int launch_cdef_call(const CdefCallArgs &a, int bpc, bool dir, hipStream_t s);   // cdef.hip
+
+struct CflAcArgs {
+    int16_t *ac;
+    const uint8_t *y;
+    int64_t stride;
+    int w_pad, h_pad, cw, ch, ss_hor, ss_ver;
+};
+int launch_cfl_ac(const CflAcArgs &a, int bpc, hipStream_t s);   // ipred.hip
+
 } // namespace mi

@@ -694,6 +694,43 @@ int launch_intra_recon(const IntraReconArgs &a, int bpc, int wg_per_xcd, hipStre
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// ---- cfl_ac (ipred.rs:1326-1432; C ipred_tmpl.c:658-700) ----
+// The chroma block's AC of the (subsampled) luma: each sample is the sum of its 1/2/4 luma
+// pixels scaled to <<3 total, w_pad / h_pad 4-px groups replicated from the last real
+// column / row, then the rounded mean subtracted. One wave, the mean by a wave reduction.
+template <typename Px>
+__global__ __launch_bounds__(64) void cfl_ac_kernel(CflAcArgs a) {
+    const int lane = threadIdx.x, cw = a.cw, ch = a.ch;
+    const int rw = cw - 4 * a.w_pad, rh = ch - 4 * a.h_pad;   // real (unpadded) extent
+    const int64_t ps = a.stride / (int64_t)sizeof(Px);
+    const Px *y = reinterpret_cast<const Px *>(a.y);
+    const int sh = 1 + !a.ss_ver + !a.ss_hor;
+    int sum = 0;
+    for (int i = lane; i < cw * ch; i += 64) {
+        const int r = min(i / cw, rh - 1), c = min(i % cw, rw - 1);
+        const int yy = r << a.ss_ver, xx = c << a.ss_hor;
+        int s = y[yy * ps + xx];
+        if (a.ss_hor) s += y[yy * ps + xx + 1];
+        if (a.ss_ver) {
+            s += y[(yy + 1) * ps + xx];
+            if (a.ss_hor) s += y[(yy + 1) * ps + xx + 1];
+        }
+        s <<= sh;
+        a.ac[i] = (int16_t)s;
+        sum += s;
+    }
+    sum = wave_sum(sum);
+    const int log2sz = __ffs(cw) - 1 + __ffs(ch) - 1;
+    const int mean = (sum + ((1 << log2sz) >> 1)) >> log2sz;
+    for (int i = lane; i < cw * ch; i += 64) a.ac[i] = (int16_t)(a.ac[i] - mean);
+}
+
+int launch_cfl_ac(const CflAcArgs &a, int bpc, hipStream_t s) {
+    if (bpc == 8) cfl_ac_kernel<uint8_t><<<1, 64, 0, s>>>(a);
+    else cfl_ac_kernel<uint16_t><<<1, 64, 0, s>>>(a);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 int launch_intra(const IpredArgs &a, int n, hipStream_t s) {
     if (n <= 0) return 0;
     if (a.bpc == 8) intra_kernel<uint8_t><<<n, 64, 0, s>>>(a);

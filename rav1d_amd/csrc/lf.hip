@@ -542,6 +542,33 @@ int launch_deblock_tiles(const LfTileArgs &a, int bpc, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// ---- per-call loop_filter_sb[cls][dir] (loopfilter.rs:745-985) ----
+// One lane per pixel line of the (up to 32) 4-px units of one edge run: bit k of the masks
+// selects unit k; dst is the edge's first q0 sample. Units of one run never overlap.
+template <typename Px>
+__global__ __launch_bounds__(128) void lf_sb_call_kernel(LfCallArgs a) {
+    const int k = threadIdx.x >> 2, line = threadIdx.x & 3;
+    const unsigned bit = 1u << k;
+    const unsigned vm = a.cls == 0 ? (a.vmask[0] | a.vmask[1] | a.vmask[2]) : (a.vmask[0] | a.vmask[1]);
+    if (!(vm & bit)) return;
+    // lvl: per unit {its level slot, the left (dir 0) / upper (dir 1) neighbour's}, gathered
+    // from the caller's strided [u8;4] map by the entry point
+    int L = a.lvl[2 * k] ? a.lvl[2 * k] : a.lvl[2 * k + 1];
+    if (!L) return;
+    const int wd = a.cls == 0 ? 4 << ((a.vmask[2] & bit) ? 2 : !!(a.vmask[1] & bit)) : 4 + 2 * !!(a.vmask[1] & bit);
+    const int64_t ps = a.stride / (int64_t)sizeof(Px);
+    // dir 0 (column edges): unit k is rows 4k..4k+3, filtering along the row (step 1);
+    // dir 1 (row edges): unit k is columns 4k..4k+3, filtering down the column (step ps)
+    Px *q0 = reinterpret_cast<Px *>(a.dst) + (a.dir == 0 ? (4 * k + line) * ps : 4 * k + line);
+    filter_line<Px>(q0, a.dir == 0 ? 1 : ps, wd, a.lim_e[L], a.lim_i[L], L >> 4, a.bdm8, a.bdmax);
+}
+
+int launch_lf_sb_call(const LfCallArgs &a, int bpc, hipStream_t s) {
+    if (bpc == 8) lf_sb_call_kernel<uint8_t><<<1, 128, 0, s>>>(a);
+    else lf_sb_call_kernel<uint16_t><<<1, 128, 0, s>>>(a);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 int launch_deblock(const LfArgs &cols, const LfArgs &rows, int bpc, hipStream_t s) {
     const int nc = cols.blk_start[3], nr = rows.blk_start[3];
     if (bpc == 8) {

@@ -1,0 +1,146 @@
+"""GPU parity of the remaining table-compatible per-call entries (cfl_pred, pal_pred, cfl_ac,
+loop_filter_sb, cdef.fb, cdef.dir) vs the oracle's per-call restatements, host buffers in
+and out as a rav1d DSP-table caller would pass them. Bit-exact."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from rav1d_amd import lib
+from rav1d_amd.synth import calc_eih, make_texture
+from tests import oracle_lib
+
+pytestmark = pytest.mark.gpu
+_VP, _SS = ctypes.c_void_p, ctypes.c_ssize_t
+
+
+def _o():
+    o = oracle_lib.load_oracle()
+    o.oracle_cfl_ac.argtypes = [_VP, _VP, _SS] + [ctypes.c_int] * 7
+    o.oracle_cfl_ac.restype = None
+    o.oracle_lf_sb.argtypes = [ctypes.c_int, ctypes.c_int, _VP, _SS, _VP, _VP, _SS, _VP, _VP, ctypes.c_int,
+                               ctypes.c_int]
+    o.oracle_lf_sb.restype = None
+    o.oracle_cdef_filter_block.argtypes = [_VP, _SS, _VP, _SS, _VP, _VP, _VP] + [ctypes.c_int] * 8
+    o.oracle_cdef_filter_block.restype = None
+    o.oracle_cdef_find_dir.argtypes = [_VP, _SS, _VP, ctypes.c_int]
+    o.oracle_cdef_find_dir.restype = ctypes.c_int
+    return o
+
+
+def P(a, off=0):
+    return ctypes.c_void_p(a.ctypes.data + off * a.itemsize)
+
+
+def _dt(bpc):
+    return np.uint8 if bpc == 8 else np.uint16
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+def test_cfl_pred_pal_pred(gpu, bpc):
+    rng = np.random.default_rng(bpc)
+    bdmax = (1 << bpc) - 1
+    for _ in range(60):
+        w, h = (int(v) for v in rng.choice([4, 8, 16, 32], 2))
+        mode = int(rng.choice([0, 3, 4, 5]))
+        edges = rng.integers(0, bdmax + 1, size=2 * 64 + 1).astype(_dt(bpc))
+        ac = rng.integers(-(bdmax << 3), (bdmax << 3) + 1, size=w * h).astype(np.int16)
+        alpha = int(rng.integers(-16, 17))
+        exp = oracle_lib.cfl_pred(mode, edges, 64, w, h, ac, alpha, bpc)
+        got = np.zeros((h, w), _dt(bpc))
+        assert lib().mi_dsp_cfl_pred(mode, P(got), got.strides[0], P(edges, 64), w, h, P(ac), alpha, bdmax) == 0
+        assert np.array_equal(got, exp), (mode, w, h)
+        w, h = (int(v) for v in rng.choice([4, 8, 16, 32, 64], 2))
+        pal = rng.integers(0, bdmax + 1, size=8).astype(_dt(bpc))
+        idx = rng.integers(0, 8, size=w * h).astype(np.uint8)
+        exp = oracle_lib.pal_pred(pal, idx, w, h, bpc)
+        got = np.zeros((h, w + 3), _dt(bpc))     # a wider destination: the stride is honoured
+        assert lib().mi_dsp_pal_pred(P(got), got.strides[0], P(pal), P(idx), w, h, bdmax) == 0
+        assert np.array_equal(got[:, :w], exp) and not got[:, w:].any()
+
+
+@pytest.mark.parametrize("bpc", [8, 10])
+@pytest.mark.parametrize("layout", [1, 2, 3])
+def test_cfl_ac(gpu, bpc, layout):
+    o = _o()
+    rng = np.random.default_rng(layout * 3 + bpc)
+    ss_hor, ss_ver = int(layout != 3), int(layout == 1)
+    for _ in range(40):
+        cw, ch = (int(v) for v in rng.choice([4, 8, 16, 32], 2))
+        w_pad, h_pad = int(rng.integers(0, cw // 4)), int(rng.integers(0, ch // 4))
+        y = rng.integers(0, 1 << bpc, size=(ch << ss_ver, (cw << ss_hor) + 5)).astype(_dt(bpc))
+        exp = np.zeros(cw * ch, np.int16)
+        o.oracle_cfl_ac(P(exp), P(y), y.strides[0], w_pad, h_pad, cw, ch, ss_hor, ss_ver, bpc)
+        got = np.zeros(cw * ch, np.int16)
+        assert lib().mi_dsp_cfl_ac(layout, P(got), P(y), y.strides[0], w_pad, h_pad, cw, ch, (1 << bpc) - 1) == 0
+        assert np.array_equal(got, exp), (cw, ch, w_pad, h_pad)
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+@pytest.mark.parametrize("cls,dir", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_loop_filter_sb(gpu, bpc, cls, dir):
+    o = _o()
+    rng = np.random.default_rng(bpc * 10 + cls * 2 + dir)
+    bdmax = (1 << bpc) - 1
+    for it in range(12):
+        pic = make_texture(rng, 160, 160, bpc)
+        # flat regions so that the wide filters fire
+        pic[rng.random(pic.shape) < 0.3] = pic[0, 0]
+        b4_stride = 48
+        lvl = rng.integers(0, 64, size=(40, b4_stride, 4)).astype(np.uint8)
+        lvl[rng.random(lvl.shape) < 0.15] = 0
+        vm = rng.integers(0, 1 << 32, size=3, dtype=np.uint64).astype(np.uint32)
+        if cls:
+            vm[2] = 0
+        vm[1] &= ~vm[2]
+        vm[0] &= ~(vm[1] | vm[2])
+        vm[0] |= rng.integers(0, 1 << 32, dtype=np.uint64).astype(np.uint32) & ~(vm[1] | vm[2])
+        e, i = calc_eih(int(rng.integers(0, 8)))
+        lut = np.zeros(144, np.uint8)
+        lut[:64], lut[64:128] = e, i
+        x0, y0 = 16, 16
+        slot = 0 if cls == 0 else 2               # run start: level entry (2, 3), neighbours valid
+        ref = pic.copy()
+        o.oracle_lf_sb(cls, dir, P(ref, y0 * 160 + x0), ref.strides[0], P(vm),
+                       ctypes.c_void_p(lvl.ctypes.data + (2 * b4_stride + 3) * 4 + slot), b4_stride,
+                       P(lut), P(lut, 64), 32, bdmax)
+        got = pic.copy()
+        rc = lib().mi_dsp_loop_filter_sb(cls, dir, P(got, y0 * 160 + x0), got.strides[0], P(vm),
+                                         ctypes.c_void_p(lvl.ctypes.data + (2 * b4_stride + 3) * 4 + slot),
+                                         b4_stride, P(lut), 32, bdmax)
+        assert rc == 0
+        assert np.array_equal(got, ref), f"iteration {it}: {np.argwhere(got != ref)[:4]}"
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+def test_cdef_filter_and_dir(gpu, bpc):
+    o = _o()
+    rng = np.random.default_rng(77 + bpc)
+    bdmax = (1 << bpc) - 1
+    bdm8 = bpc - 8
+    for it in range(80):
+        fb = int(rng.integers(0, 3))
+        w, h = (8 if fb == 0 else 4), (4 if fb == 2 else 8)
+        pic = make_texture(rng, 32, 32, bpc)
+        x0, y0 = 8, 8
+        left = np.ascontiguousarray(pic[y0:y0 + h, x0 - 2:x0])
+        edges = int(rng.integers(0, 16))
+        pri = int(rng.integers(0, 16)) << bdm8
+        sec = int(rng.choice([0, 1, 2, 4])) << bdm8
+        d = int(rng.integers(0, 8))
+        damping = int(rng.integers(3, 7)) + bdm8 - (fb > 0)
+        src = pic.copy()
+        ref = pic.copy()
+        o.oracle_cdef_filter_block(P(ref, y0 * 32 + x0), ref.strides[0], P(src, y0 * 32 + x0), src.strides[0],
+                                   P(left), P(src, (y0 - 2) * 32 + x0), P(src, (y0 + h) * 32 + x0),
+                                   pri, sec, d, damping, w, h, edges, bdmax)
+        got = pic.copy()
+        rc = lib().mi_dsp_cdef_filter(fb, P(got, y0 * 32 + x0), got.strides[0], P(left),
+                                      P(src, (y0 - 2) * 32 + x0), P(src, (y0 + h) * 32 + x0),
+                                      pri, sec, d, damping, edges, bdmax)
+        assert rc == 0
+        assert np.array_equal(got, ref), (it, fb, edges, pri, sec, d)
+        var_o, var_g = ctypes.c_uint(0), ctypes.c_uint(0)
+        d_o = o.oracle_cdef_find_dir(P(pic, y0 * 32 + x0), pic.strides[0], ctypes.byref(var_o), bdmax)
+        d_g = lib().mi_dsp_cdef_dir(P(pic, y0 * 32 + x0), pic.strides[0], ctypes.byref(var_g), bdmax)
+        assert (d_g, var_g.value) == (d_o, var_o.value)
