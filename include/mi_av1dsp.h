@@ -449,6 +449,31 @@ int mi_dsp_cdef_filter(int fb, void *dst, ptrdiff_t stride, const void *left, co
 /* cdef.dir (src/cdef.rs:921-1031): returns the direction 0..7 (or -errno), *var the variance. */
 int mi_dsp_cdef_dir(const void *img, ptrdiff_t stride, unsigned *var, int bitdepth_max);
 
+/* Rav1dMCDSPContext (src/mc.rs:1174-1338; C src/mc.h:38-108). mc[filter2d] / mct[filter2d]:
+ * filter2d = Filter2d 0..8 (8-tap regular/smooth/sharp pairs) or 9 (bilinear); mx / my in
+ * 1/16 pel; src at the block origin with the filter reach (3 before, 4 after) readable;
+ * prep writes w * h int16 intermediates (PREP_BIAS applied). */
+int mi_dsp_mc_put(int filter2d, void *dst, ptrdiff_t dst_stride, const void *src, ptrdiff_t src_stride, int w, int h,
+                  int mx, int my, int bitdepth_max);
+int mi_dsp_mc_prep(int filter2d, int16_t *tmp, const void *src, ptrdiff_t src_stride, int w, int h, int mx, int my,
+                   int bitdepth_max);
+/* avg / w_avg / mask / w_mask[layout - 1] (layout 1 I420, 2 I422, 3 I444; mask written at the
+ * chroma resolution) / blend / blend_v / blend_h (OBMC, obmc_masks) / emu_edge. */
+int mi_dsp_mc_avg(void *dst, ptrdiff_t dst_stride, const int16_t *tmp1, const int16_t *tmp2, int w, int h,
+                  int bitdepth_max);
+int mi_dsp_mc_w_avg(void *dst, ptrdiff_t dst_stride, const int16_t *tmp1, const int16_t *tmp2, int w, int h, int weight,
+                    int bitdepth_max);
+int mi_dsp_mc_mask(void *dst, ptrdiff_t dst_stride, const int16_t *tmp1, const int16_t *tmp2, int w, int h,
+                   const uint8_t *mask, int bitdepth_max);
+int mi_dsp_mc_w_mask(int layout, void *dst, ptrdiff_t dst_stride, const int16_t *tmp1, const int16_t *tmp2, int w,
+                     int h, uint8_t *mask, int sign, int bitdepth_max);
+int mi_dsp_mc_blend(void *dst, ptrdiff_t dst_stride, const void *tmp, int w, int h, const uint8_t *mask,
+                    int bitdepth_max);
+int mi_dsp_mc_blend_v(void *dst, ptrdiff_t dst_stride, const void *tmp, int w, int h, int bitdepth_max);
+int mi_dsp_mc_blend_h(void *dst, ptrdiff_t dst_stride, const void *tmp, int w, int h, int bitdepth_max);
+int mi_dsp_mc_emu_edge(int bw, int bh, int iw, int ih, int x, int y, void *dst, ptrdiff_t dst_stride, const void *ref,
+                       ptrdiff_t ref_stride, int bitdepth_max);
+
 #ifdef __cplusplus
 }
 #endif

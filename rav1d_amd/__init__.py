@@ -147,6 +147,17 @@ def lib():
                                                     ctypes.c_int, ctypes.c_int])
     _sig(L, "mi_dsp_cdef_filter", ctypes.c_int, [ctypes.c_int, _VP, _SS, _VP, _VP, _VP] + [ctypes.c_int] * 6)
     _sig(L, "mi_dsp_cdef_dir", ctypes.c_int, [_VP, _SS, _VP, ctypes.c_int])
+    _I = ctypes.c_int
+    _sig(L, "mi_dsp_mc_put", _I, [_I, _VP, _SS, _VP, _SS, _I, _I, _I, _I, _I])
+    _sig(L, "mi_dsp_mc_prep", _I, [_I, _VP, _VP, _SS, _I, _I, _I, _I, _I])
+    _sig(L, "mi_dsp_mc_avg", _I, [_VP, _SS, _VP, _VP, _I, _I, _I])
+    _sig(L, "mi_dsp_mc_w_avg", _I, [_VP, _SS, _VP, _VP, _I, _I, _I, _I])
+    _sig(L, "mi_dsp_mc_mask", _I, [_VP, _SS, _VP, _VP, _I, _I, _VP, _I])
+    _sig(L, "mi_dsp_mc_w_mask", _I, [_I, _VP, _SS, _VP, _VP, _I, _I, _VP, _I, _I])
+    _sig(L, "mi_dsp_mc_blend", _I, [_VP, _SS, _VP, _I, _I, _VP, _I])
+    for n in ("mi_dsp_mc_blend_v", "mi_dsp_mc_blend_h"):
+        _sig(L, n, _I, [_VP, _SS, _VP, _I, _I, _I])
+    _sig(L, "mi_dsp_mc_emu_edge", _I, [_I, _I, _I, _I, _I, _I, _VP, _SS, _VP, _SS, _I])
     _sig(L, "mi_deblock_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiLoopFilter), _VP])
     _sig(L, "mi_deblock_frame_to", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
                                                   ctypes.POINTER(MiLoopFilter), _VP])
@@ -168,7 +179,9 @@ EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error"
             "mi_ipred_blocks", "mi_intra_blocks", "mi_intra_recon", "mi_ctx_device_status", "mi_deblock_frame", "mi_deblock_frame_to", "mi_cdef_frame", "mi_lr_frame",
             "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply",
             "mi_dsp_itxfm_add", "mi_dsp_intra_pred", "mi_dsp_cfl_pred", "mi_dsp_pal_pred", "mi_dsp_cfl_ac",
-            "mi_dsp_loop_filter_sb", "mi_dsp_cdef_filter", "mi_dsp_cdef_dir"]
+            "mi_dsp_loop_filter_sb", "mi_dsp_cdef_filter", "mi_dsp_cdef_dir", "mi_dsp_mc_put", "mi_dsp_mc_prep",
+            "mi_dsp_mc_avg", "mi_dsp_mc_w_avg", "mi_dsp_mc_mask", "mi_dsp_mc_w_mask", "mi_dsp_mc_blend",
+            "mi_dsp_mc_blend_v", "mi_dsp_mc_blend_h", "mi_dsp_mc_emu_edge"]
 
 
 def check(rc, what):

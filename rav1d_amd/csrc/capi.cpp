@@ -1034,5 +1034,171 @@ int mi_dsp_cdef_dir(const void *img, ptrdiff_t stride, unsigned *var, int bitdep
     return r[0];
 }
 
+// ---- mc table (src/mc.rs:1174-1338): put / prep, combine, blend, emu_edge ----
+namespace {
+void mc_call_bd(mi::McCallArgs &a, int bpc, int bdmax) {
+    a.bpc = bpc;
+    a.ib = bpc == 8 ? 4 : 14 - bpc;
+    a.bias = bpc == 8 ? 0 : 8192;
+    a.bdmax = bdmax;
+}
+bool mc_dims_ok(int w, int h) { return w >= 2 && h >= 2 && w <= 128 && h <= 128; }
+}  // namespace
+
+int mi_dsp_mc_put(int filter2d, void *dst, ptrdiff_t dst_stride, const void *src, ptrdiff_t src_stride, int w, int h,
+                  int mx, int my, int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || !dst || !src || filter2d < 0 || filter2d > 9 || !mc_dims_ok(w, h) || mx < 0 || mx > 15 || my < 0 ||
+        my > 15)
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    const int px = bpc == 8 ? 1 : 2;
+    hipStream_t s = g_call.stream;
+    // source window: rows -3 .. h+4, columns -3 .. w+4 (8-tap reach; bilinear uses +1)
+    const int r0 = filter2d == 9 ? 0 : -3, r1 = h + (filter2d == 9 ? 1 : 5);
+    const ptrdiff_t b0 = (filter2d == 9 ? 0 : -3) * px, b1 = (ptrdiff_t)(w + (filter2d == 9 ? 1 : 5)) * px;
+    uint8_t *win = g_call.scratch, *dout = win + (1 << 19);
+    if (int e = win_in(win, src, src_stride, r0, r1, b0, b1, s)) return e;
+    mi::McCallArgs a;
+    memset(&a, 0, sizeof(a));
+    a.src = win + (size_t)(-r0) * (b1 - b0) - b0;
+    a.src_stride = b1 - b0;
+    a.dst = dout;
+    a.dst_stride = (int64_t)w * px;
+    a.w = w; a.h = h; a.mx = mx; a.my = my; a.filter2d = filter2d;
+    mc_call_bd(a, bpc, bitdepth_max);
+    if (mi::launch_mc_call(a, 0, s)) return -EIO;
+    return win_out(dst, dst_stride, dout, 0, h, 0, (ptrdiff_t)w * px, s);
+}
+
+int mi_dsp_mc_prep(int filter2d, int16_t *tmp, const void *src, ptrdiff_t src_stride, int w, int h, int mx, int my,
+                   int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || !tmp || !src || filter2d < 0 || filter2d > 9 || !mc_dims_ok(w, h) || mx < 0 || mx > 15 || my < 0 ||
+        my > 15)
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    const int px = bpc == 8 ? 1 : 2;
+    hipStream_t s = g_call.stream;
+    const int r0 = filter2d == 9 ? 0 : -3, r1 = h + (filter2d == 9 ? 1 : 5);
+    const ptrdiff_t b0 = (filter2d == 9 ? 0 : -3) * px, b1 = (ptrdiff_t)(w + (filter2d == 9 ? 1 : 5)) * px;
+    uint8_t *win = g_call.scratch;
+    int16_t *dtmp = (int16_t *)(win + (1 << 19));
+    if (int e = win_in(win, src, src_stride, r0, r1, b0, b1, s)) return e;
+    mi::McCallArgs a;
+    memset(&a, 0, sizeof(a));
+    a.src = win + (size_t)(-r0) * (b1 - b0) - b0;
+    a.src_stride = b1 - b0;
+    a.tmp1 = dtmp;
+    a.prep = 1;
+    a.w = w; a.h = h; a.mx = mx; a.my = my; a.filter2d = filter2d;
+    mc_call_bd(a, bpc, bitdepth_max);
+    if (mi::launch_mc_call(a, 0, s)) return -EIO;
+    if (hipMemcpyAsync(tmp, dtmp, (size_t)w * h * 2, hipMemcpyDefault, s) != hipSuccess) return -EIO;
+    return hipStreamSynchronize(s) == hipSuccess ? 0 : -EIO;
+}
+
+namespace {
+// avg / w_avg / mask / w_mask / blend*: op as mc_call_comb_kernel
+int mc_combine(int op, void *dst, ptrdiff_t ds, const int16_t *t1, const int16_t *t2, const void *tmp_px,
+               int w, int h, const uint8_t *mask, uint8_t *mask_out, int weight, int sign, int layout, int bdmax) {
+    const int bpc = bpc_of(bdmax);
+    if (!bpc || !dst || !mc_dims_ok(w, h)) return -EINVAL;
+    if ((op <= 3 && (!t1 || !t2)) || ((op == 2 || op == 4) && !mask) || (op == 3 && !mask_out) ||
+        (op >= 4 && !tmp_px) || (op == 3 && (layout < 1 || layout > 3)))
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    const int px = bpc == 8 ? 1 : 2;
+    hipStream_t s = g_call.stream;
+    const size_t n = (size_t)w * h;
+    uint8_t *dd = g_call.scratch, *d1 = dd + 65536, *d2 = d1 + 65536, *dm = d2 + 65536, *dmo = dm + 16384,
+            *dt = dmo + 16384;
+    mi::McCallArgs a;
+    memset(&a, 0, sizeof(a));
+    int e = 0;
+    if (op <= 3) {
+        e = copy_in(d1, t1, n * 2, s);
+        if (!e) e = copy_in(d2, t2, n * 2, s);
+    }
+    if (!e && (op == 2 || op == 4)) e = copy_in(dm, mask, n, s);
+    if (!e && op >= 4) e = copy_in(dt, tmp_px, n * px, s);
+    if (!e && op >= 4) e = win_in(dd, dst, ds, 0, h, 0, (ptrdiff_t)w * px, s);   // blends read dst
+    if (e) return e;
+    a.dst = dd;
+    a.dst_stride = (int64_t)w * px;
+    a.tmp1 = (int16_t *)d1;
+    a.tmp2 = (const int16_t *)d2;
+    a.mask = dm;
+    a.mask_out = dmo;
+    a.src = dt;
+    a.w = w; a.h = h; a.op = op; a.weight = weight; a.sign = sign;
+    a.ss_hor = layout == 1 || layout == 2;
+    a.ss_ver = layout == 1;
+    mc_call_bd(a, bpc, bdmax);
+    if (mi::launch_mc_call(a, 1, s)) return -EIO;
+    if (op == 3 && hipMemcpyAsync(mask_out, dmo, (size_t)(w >> a.ss_hor) * (h >> a.ss_ver), hipMemcpyDefault, s) != hipSuccess)
+        return -EIO;
+    return win_out(dst, ds, dd, 0, h, 0, (ptrdiff_t)w * px, s);
+}
+}  // namespace
+
+int mi_dsp_mc_avg(void *dst, ptrdiff_t dst_stride, const int16_t *tmp1, const int16_t *tmp2, int w, int h,
+                  int bitdepth_max) {
+    return mc_combine(0, dst, dst_stride, tmp1, tmp2, nullptr, w, h, nullptr, nullptr, 0, 0, 0, bitdepth_max);
+}
+int mi_dsp_mc_w_avg(void *dst, ptrdiff_t dst_stride, const int16_t *tmp1, const int16_t *tmp2, int w, int h, int weight,
+                    int bitdepth_max) {
+    return mc_combine(1, dst, dst_stride, tmp1, tmp2, nullptr, w, h, nullptr, nullptr, weight, 0, 0, bitdepth_max);
+}
+int mi_dsp_mc_mask(void *dst, ptrdiff_t dst_stride, const int16_t *tmp1, const int16_t *tmp2, int w, int h,
+                   const uint8_t *mask, int bitdepth_max) {
+    return mc_combine(2, dst, dst_stride, tmp1, tmp2, nullptr, w, h, mask, nullptr, 0, 0, 0, bitdepth_max);
+}
+int mi_dsp_mc_w_mask(int layout, void *dst, ptrdiff_t dst_stride, const int16_t *tmp1, const int16_t *tmp2, int w,
+                     int h, uint8_t *mask, int sign, int bitdepth_max) {
+    return mc_combine(3, dst, dst_stride, tmp1, tmp2, nullptr, w, h, nullptr, mask, 0, sign, layout, bitdepth_max);
+}
+int mi_dsp_mc_blend(void *dst, ptrdiff_t dst_stride, const void *tmp, int w, int h, const uint8_t *mask,
+                    int bitdepth_max) {
+    return mc_combine(4, dst, dst_stride, nullptr, nullptr, tmp, w, h, mask, nullptr, 0, 0, 0, bitdepth_max);
+}
+int mi_dsp_mc_blend_v(void *dst, ptrdiff_t dst_stride, const void *tmp, int w, int h, int bitdepth_max) {
+    return mc_combine(5, dst, dst_stride, nullptr, nullptr, tmp, w, h, nullptr, nullptr, 0, 0, 0, bitdepth_max);
+}
+int mi_dsp_mc_blend_h(void *dst, ptrdiff_t dst_stride, const void *tmp, int w, int h, int bitdepth_max) {
+    return mc_combine(6, dst, dst_stride, nullptr, nullptr, tmp, w, h, nullptr, nullptr, 0, 0, 0, bitdepth_max);
+}
+
+int mi_dsp_mc_emu_edge(int bw, int bh, int iw, int ih, int x, int y, void *dst, ptrdiff_t dst_stride, const void *ref,
+                       ptrdiff_t ref_stride, int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || !dst || !ref || bw < 1 || bh < 1 || bw > 256 || bh > 256 || iw < 1 || ih < 1) return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    const int px = bpc == 8 ? 1 : 2;
+    hipStream_t s = g_call.stream;
+    auto clip = [](int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; };
+    // the reference pixels the block can reach: the clamped rectangle
+    const int ry0 = clip(y, 0, ih - 1), ry1 = clip(y + bh - 1, 0, ih - 1) + 1;
+    const int rx0 = clip(x, 0, iw - 1), rx1 = clip(x + bw - 1, 0, iw - 1) + 1;
+    uint8_t *win = g_call.scratch, *dout = win + (1 << 19);
+    if (int e = win_in(win, (const uint8_t *)ref + (ptrdiff_t)ry0 * ref_stride + (ptrdiff_t)rx0 * px, ref_stride, 0,
+                       ry1 - ry0, 0, (ptrdiff_t)(rx1 - rx0) * px, s))
+        return e;
+    mi::McCallArgs a;
+    memset(&a, 0, sizeof(a));
+    a.src = win;
+    a.src_stride = (int64_t)(rx1 - rx0) * px;
+    a.dst = dout;
+    a.dst_stride = (int64_t)bw * px;
+    a.w = bw; a.h = bh; a.mx = x; a.my = y; a.iw = iw; a.ih = ih;
+    mc_call_bd(a, bpc, bitdepth_max);
+    if (mi::launch_mc_call(a, 2, s)) return -EIO;
+    return win_out(dst, dst_stride, dout, 0, bh, 0, (ptrdiff_t)bw * px, s);
+}
+
 }  // extern "C"
 } // extern "C"

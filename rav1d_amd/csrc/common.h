@@ -267,4 +267,18 @@ struct CflAcArgs {
 };
 int launch_cfl_ac(const CflAcArgs &a, int bpc, hipStream_t s);   // ipred.hip
 
+struct McCallArgs {
+    uint8_t *dst;                 // put / combine destination (pixels)
+    const uint8_t *src;           // put / prep source at the block origin; blend: tmp pixels; emu: clamped rect
+    int16_t *tmp1;                // prep output, or the first combine input
+    const int16_t *tmp2;
+    const uint8_t *mask;          // mask / blend input
+    uint8_t *mask_out;            // w_mask output
+    int64_t dst_stride, src_stride;
+    int w, h, mx, my, filter2d, prep, op, weight, sign, ss_hor, ss_ver, iw, ih;
+    int bpc, ib, bias, bdmax;
+};
+// kind 0 put / prep, 1 combine (op), 2 emu_edge (mc_call.hip)
+int launch_mc_call(const McCallArgs &a, int kind, hipStream_t s);
+
 } // namespace mi

@@ -144,3 +144,100 @@ def test_cdef_filter_and_dir(gpu, bpc):
         d_o = o.oracle_cdef_find_dir(P(pic, y0 * 32 + x0), pic.strides[0], ctypes.byref(var_o), bdmax)
         d_g = lib().mi_dsp_cdef_dir(P(pic, y0 * 32 + x0), pic.strides[0], ctypes.byref(var_g), bdmax)
         assert (d_g, var_g.value) == (d_o, var_o.value)
+
+
+def _mc_sigs(o):
+    I = ctypes.c_int
+    o.oracle_mc_put.argtypes = [I, _VP, _SS, _VP, _SS, I, I, I, I, I]
+    o.oracle_mc_prep.argtypes = [I, _VP, _VP, _SS, I, I, I, I, I]
+    o.oracle_mc_avg.argtypes = [_VP, _SS, _VP, _VP, I, I, I]
+    o.oracle_mc_w_avg.argtypes = [_VP, _SS, _VP, _VP, I, I, I, I]
+    o.oracle_mc_mask.argtypes = [_VP, _SS, _VP, _VP, I, I, _VP, I]
+    o.oracle_mc_w_mask.argtypes = [_VP, _SS, _VP, _VP, I, I, _VP, I, I, I, I]
+    o.oracle_mc_blend.argtypes = [_VP, _SS, _VP, I, I, _VP, I]
+    o.oracle_mc_blend_v.argtypes = [_VP, _SS, _VP, I, I, I]
+    o.oracle_mc_blend_h.argtypes = [_VP, _SS, _VP, I, I, I]
+    o.oracle_mc_emu_edge.argtypes = [I, I, I, I, I, I, _VP, _SS, _VP, _SS, I]
+    for f in ("put", "prep", "avg", "w_avg", "mask", "w_mask", "blend", "blend_v", "blend_h", "emu_edge"):
+        getattr(o, "oracle_mc_" + f).restype = None
+    return o
+
+
+SIZES = [2, 4, 8, 16, 32, 64, 128]
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+def test_mc_put_prep(gpu, bpc):
+    o = _mc_sigs(_o())
+    rng = np.random.default_rng(500 + bpc)
+    bdmax = (1 << bpc) - 1
+    for it in range(60):
+        w, h = int(rng.choice(SIZES)), int(rng.choice(SIZES))
+        f2d = int(rng.integers(0, 10))
+        mx, my = int(rng.integers(0, 16)) * int(rng.random() < 0.8), int(rng.integers(0, 16)) * int(rng.random() < 0.8)
+        src = make_texture(rng, 144, 144, bpc)
+        off = 8 * 144 + 8
+        ref = np.zeros((h, w + 2), _dt(bpc))
+        got = np.zeros((h, w + 2), _dt(bpc))
+        o.oracle_mc_put(f2d, P(ref), ref.strides[0], P(src, off), src.strides[0], w, h, mx, my, bpc)
+        assert lib().mi_dsp_mc_put(f2d, P(got), got.strides[0], P(src, off), src.strides[0], w, h, mx, my, bdmax) == 0
+        assert np.array_equal(got, ref), ("put", it, f2d, w, h, mx, my)
+        rt = np.zeros(w * h, np.int16)
+        gt = np.zeros(w * h, np.int16)
+        o.oracle_mc_prep(f2d, P(rt), P(src, off), src.strides[0], w, h, mx, my, bpc)
+        assert lib().mi_dsp_mc_prep(f2d, P(gt), P(src, off), src.strides[0], w, h, mx, my, bdmax) == 0
+        assert np.array_equal(gt, rt), ("prep", it, f2d, w, h, mx, my)
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+def test_mc_combine_blend_emu(gpu, bpc):
+    o = _mc_sigs(_o())
+    rng = np.random.default_rng(600 + bpc)
+    bdmax = (1 << bpc) - 1
+    for it in range(40):
+        w, h = int(rng.choice(SIZES[1:])), int(rng.choice(SIZES[1:]))
+        t = [np.zeros(w * h, np.int16) for _ in range(2)]
+        for k in range(2):
+            src = make_texture(rng, w + 16, h + 16, bpc)
+            o.oracle_mc_prep(int(rng.integers(0, 10)), P(t[k]), P(src, 4 * (w + 16) + 4), src.strides[0], w, h,
+                             int(rng.integers(0, 16)), int(rng.integers(0, 16)), bpc)
+        m = rng.integers(0, 65, size=w * h).astype(np.uint8)
+        weight = int(rng.integers(1, 16))
+        for name in ("avg", "w_avg", "mask"):
+            ref = np.zeros((h, w), _dt(bpc))
+            got = np.zeros((h, w), _dt(bpc))
+            extra = {"avg": [], "w_avg": [weight], "mask": [P(m)]}[name]
+            getattr(o, "oracle_mc_" + name)(P(ref), ref.strides[0], P(t[0]), P(t[1]), w, h, *extra, bpc)
+            assert getattr(lib(), "mi_dsp_mc_" + name)(P(got), got.strides[0], P(t[0]), P(t[1]), w, h, *extra,
+                                                        bdmax) == 0
+            assert np.array_equal(got, ref), (name, w, h)
+        for layout, (sh, sv) in ((1, (1, 1)), (2, (1, 0)), (3, (0, 0))):
+            sign = int(rng.integers(0, 2))
+            ref = np.zeros((h, w), _dt(bpc))
+            got = np.zeros((h, w), _dt(bpc))
+            rm = np.zeros((h >> sv) * (w >> sh), np.uint8)
+            gm = np.zeros_like(rm)
+            o.oracle_mc_w_mask(P(ref), ref.strides[0], P(t[0]), P(t[1]), w, h, P(rm), sign, sh, sv, bpc)
+            assert lib().mi_dsp_mc_w_mask(layout, P(got), got.strides[0], P(t[0]), P(t[1]), w, h, P(gm), sign,
+                                          bdmax) == 0
+            assert np.array_equal(got, ref) and np.array_equal(gm, rm), ("w_mask", layout, w, h)
+        dst0 = make_texture(rng, w, h, bpc)
+        tmp = make_texture(rng, w, h, bpc)
+        for name, extra in (("blend", [P(m)]), ("blend_v", []), ("blend_h", [])):
+            if name != "blend" and (w > 32 if name == "blend_v" else h > 32):
+                continue
+            ref, got = dst0.copy(), dst0.copy()
+            getattr(o, "oracle_mc_" + name)(P(ref), ref.strides[0], P(tmp), w, h, *extra, bpc)
+            assert getattr(lib(), "mi_dsp_mc_" + name)(P(got), got.strides[0], P(tmp), w, h, *extra, bdmax) == 0
+            assert np.array_equal(got, ref), (name, w, h)
+        # emu_edge: blocks straddling every border of a small reference
+        iw, ih = int(rng.integers(8, 40)), int(rng.integers(8, 40))
+        refpic = make_texture(rng, iw, ih, bpc)
+        bw, bh = int(rng.integers(1, 48)), int(rng.integers(1, 48))
+        x, y = int(rng.integers(-bw - 4, iw + 4)), int(rng.integers(-bh - 4, ih + 4))
+        r = np.zeros((bh, bw), _dt(bpc))
+        g = np.zeros((bh, bw), _dt(bpc))
+        o.oracle_mc_emu_edge(bw, bh, iw, ih, x, y, P(r), r.strides[0], P(refpic), refpic.strides[0], bpc)
+        assert lib().mi_dsp_mc_emu_edge(bw, bh, iw, ih, x, y, P(g), g.strides[0], P(refpic), refpic.strides[0],
+                                        bdmax) == 0
+        assert np.array_equal(g, r), ("emu_edge", bw, bh, iw, ih, x, y)
