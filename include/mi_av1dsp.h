@@ -473,6 +473,14 @@ int mi_dsp_mc_blend_v(void *dst, ptrdiff_t dst_stride, const void *tmp, int w, i
 int mi_dsp_mc_blend_h(void *dst, ptrdiff_t dst_stride, const void *tmp, int w, int h, int bitdepth_max);
 int mi_dsp_mc_emu_edge(int bw, int bh, int iw, int ih, int x, int y, void *dst, ptrdiff_t dst_stride, const void *ref,
                        ptrdiff_t ref_stride, int bitdepth_max);
+/* warp8x8 (prep 0: pixels) / warp8x8t (prep 1: int16 intermediate, dst_stride in elements as
+ * the reference's tmp_stride) (src/mc.rs:885-1030); src at the 8x8 block origin, rows and
+ * columns -3 .. 11 readable; abcd = the block's warp steps. */
+int mi_dsp_mc_warp8x8(int prep, void *dst, ptrdiff_t dst_stride, const void *src, ptrdiff_t src_stride,
+                      const int16_t *abcd, int mx, int my, int bitdepth_max);
+/* resize (src/mc.rs:1114-1172): super-resolution upscaling of h rows. */
+int mi_dsp_mc_resize(void *dst, ptrdiff_t dst_stride, const void *src, ptrdiff_t src_stride, int dst_w, int h,
+                     int src_w, int dx, int mx0, int bitdepth_max);
 
 #ifdef __cplusplus
 }

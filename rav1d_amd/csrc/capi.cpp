@@ -1200,5 +1200,62 @@ int mi_dsp_mc_emu_edge(int bw, int bh, int iw, int ih, int x, int y, void *dst, 
     return win_out(dst, dst_stride, dout, 0, bh, 0, (ptrdiff_t)bw * px, s);
 }
 
+int mi_dsp_mc_warp8x8(int prep, void *dst, ptrdiff_t dst_stride, const void *src, ptrdiff_t src_stride,
+                      const int16_t *abcd, int mx, int my, int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || !dst || !src || !abcd) return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    const int px = bpc == 8 ? 1 : 2;
+    hipStream_t s = g_call.stream;
+    int16_t hb[4];
+    if (hipMemcpy(hb, abcd, sizeof(hb), hipMemcpyDefault) != hipSuccess) return -EIO;
+    uint8_t *win = g_call.scratch, *dout = win + 4096;
+    const int r0 = -3, r1 = 12;
+    const ptrdiff_t b0 = -3 * px, b1 = 12 * px;
+    if (int e = win_in(win, src, src_stride, r0, r1, b0, b1, s)) return e;
+    mi::McCallArgs a;
+    memset(&a, 0, sizeof(a));
+    a.src = win + (size_t)(-r0) * (b1 - b0) - b0;
+    a.src_stride = b1 - b0;
+    a.dst = dout;
+    a.dst_stride = 8 * px;
+    a.tmp1 = (int16_t *)dout;
+    a.prep = prep;
+    a.w = 8; a.h = 8; a.mx = mx; a.my = my;
+    for (int i = 0; i < 4; i++) a.abcd[i] = hb[i];
+    mc_call_bd(a, bpc, bitdepth_max);
+    if (mi::launch_mc_call(a, 3, s)) return -EIO;
+    // warp8x8t: dst is the int16 intermediate with stride dst_stride (in elements, as the
+    // reference's tmp_stride); warp8x8: pixels
+    if (prep) return win_out(dst, dst_stride * 2, dout, 0, 8, 0, 16, s);
+    return win_out(dst, dst_stride, dout, 0, 8, 0, 8 * px, s);
+}
+
+int mi_dsp_mc_resize(void *dst, ptrdiff_t dst_stride, const void *src, ptrdiff_t src_stride, int dst_w, int h,
+                     int src_w, int dx, int mx0, int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || !dst || !src || dst_w < 1 || h < 1 || src_w < 1 || dst_w > 8192 || src_w > 8192 || h > 64 ||
+        mx0 < 0 || mx0 >= (1 << 14))
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    const int px = bpc == 8 ? 1 : 2;
+    if ((size_t)(src_w + dst_w) * h * px > (1u << 20)) return -EINVAL;
+    hipStream_t s = g_call.stream;
+    uint8_t *win = g_call.scratch, *dout = win + (size_t)src_w * h * px;
+    if (int e = win_in(win, src, src_stride, 0, h, 0, (ptrdiff_t)src_w * px, s)) return e;
+    mi::McCallArgs a;
+    memset(&a, 0, sizeof(a));
+    a.src = win;
+    a.src_stride = (int64_t)src_w * px;
+    a.dst = dout;
+    a.dst_stride = (int64_t)dst_w * px;
+    a.w = dst_w; a.h = h; a.iw = src_w; a.mx = mx0; a.weight = dx;
+    mc_call_bd(a, bpc, bitdepth_max);
+    if (mi::launch_mc_call(a, 4, s)) return -EIO;
+    return win_out(dst, dst_stride, dout, 0, h, 0, (ptrdiff_t)dst_w * px, s);
+}
+
 }  // extern "C"
 } // extern "C"

@@ -1,6 +1,6 @@
 // mc_call.hip — single-call motion-compensation kernels behind the table-compatible entry
 // points (mi_dsp_mc_*): mc[10] / mct[10] (8-tap and bilinear put / prep), avg, w_avg, mask,
-// w_mask[3], blend, blend_v, blend_h and emu_edge of Rav1dMCDSPContext (rav1d src/mc.rs:
+// w_mask[3], blend, blend_v, blend_h, warp8x8 / warp8x8t, emu_edge and resize of Rav1dMCDSPContext (rav1d src/mc.rs:
 // 1174-1338; C src/mc_tmpl.c:52-845). One lane per output pixel (per mask sample for
 // w_mask); the per-call path exists for drop-in parity, the frame path is mc.hip.
 #include "common.h"
@@ -12,6 +12,12 @@ __constant__ int8_t k_subpel_c[6][15][8] = {
 };
 __constant__ uint8_t k_obmc_c[64] = {
 #include "tables/obmc_masks.inc"
+};
+__constant__ int8_t k_warp_c[193][8] = {
+#include "tables/mc_warp_filter.inc"
+};
+__constant__ int8_t k_resize_c[64][8] = {
+#include "tables/resize_filter.inc"
 };
 
 __device__ __forceinline__ int rnd_c(int v, int sh) { return (v + ((1 << sh) >> 1)) >> sh; }
@@ -154,9 +160,62 @@ __global__ __launch_bounds__(256) void mc_call_emu_kernel(McCallArgs a) {
     st<Px>(a.dst, a.dst_stride, yy, xx, ld<Px>(a.src, a.src_stride, sy, sx));
 }
 
+// warp8x8 / warp8x8t (mc_tmpl.c:714-796): 15 horizontally filtered rows of 8 in LDS (the
+// filter phase steps by abcd[0] along x and abcd[1] per row), then the vertical pass (abcd[2]
+// along x, abcd[3] per row). src at the block origin, rows / columns -3 .. 11 readable.
+template <typename Px>
+__global__ __launch_bounds__(64) void mc_call_warp_kernel(McCallArgs a) {
+    __shared__ int mid[15 * 8];
+    const int lane = threadIdx.x, ib = a.ib;
+    for (int i = lane; i < 15 * 8; i += 64) {
+        const int y = i >> 3, x = i & 7;
+        const int tmx = a.mx + y * a.abcd[1] + x * a.abcd[0];
+        const int8_t *F = k_warp_c[64 + ((tmx + 512) >> 10)];
+        int v = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) v += F[k] * ld<Px>(a.src, a.src_stride, y - 3, x + k - 3);
+        mid[i] = rnd_c(v, 7 - ib);
+    }
+    __syncthreads();
+    const int y = lane >> 3, x = lane & 7;
+    const int tmy = a.my + y * a.abcd[3] + x * a.abcd[2];
+    const int8_t *F = k_warp_c[64 + ((tmy + 512) >> 10)];
+    int v = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) v += F[k] * mid[(y + k) * 8 + x];
+    if (a.prep) a.tmp1[y * a.w + x] = (int16_t)(rnd_c(v, 7) - a.bias);
+    else st<Px>(a.dst, a.dst_stride, y, x, clip_c(rnd_c(v, 7 + ib), 0, a.bdmax));
+}
+
+// resize (mc_tmpl.c:847-875): output x reads source column -1 + ((mx0 + x * dx) >> 14) with
+// filter phase ((mx0 + x * dx) & 0x3fff) >> 8, columns clamped to [0, src_w)
+template <typename Px>
+__global__ __launch_bounds__(256) void mc_call_resize_kernel(McCallArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.w * a.h) return;
+    const int y = i / a.w, x = i % a.w;
+    const int64_t pos = (int64_t)a.mx + (int64_t)x * a.weight;   // weight: dx
+    const int sx = -1 + (int)(pos >> 14), ph = (int)(pos & 0x3fff) >> 8;
+    const int8_t *F = k_resize_c[ph];
+    int v = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) v += F[k] * ld<Px>(a.src, a.src_stride, y, clip_c(sx - 3 + k, 0, a.iw - 1));
+    st<Px>(a.dst, a.dst_stride, y, x, clip_c((-v + 64) >> 7, 0, a.bdmax));
+}
+
 int launch_mc_call(const McCallArgs &a, int kind, hipStream_t s) {
     const int n = kind == 1 && a.op == 3 ? (a.w >> a.ss_hor) * (a.h >> a.ss_ver) : a.w * a.h;
     const dim3 g((n + 255) / 256);
+    if (kind == 3) {
+        if (a.bpc == 8) mc_call_warp_kernel<uint8_t><<<1, 64, 0, s>>>(a);
+        else mc_call_warp_kernel<uint16_t><<<1, 64, 0, s>>>(a);
+        return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
+    if (kind == 4) {
+        if (a.bpc == 8) mc_call_resize_kernel<uint8_t><<<g, 256, 0, s>>>(a);
+        else mc_call_resize_kernel<uint16_t><<<g, 256, 0, s>>>(a);
+        return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
     if (a.bpc == 8) {
         if (kind == 0) mc_call_pp_kernel<uint8_t><<<g, 256, 0, s>>>(a);
         else if (kind == 1) mc_call_comb_kernel<uint8_t><<<g, 256, 0, s>>>(a);

@@ -241,3 +241,42 @@ def test_mc_combine_blend_emu(gpu, bpc):
         assert lib().mi_dsp_mc_emu_edge(bw, bh, iw, ih, x, y, P(g), g.strides[0], P(refpic), refpic.strides[0],
                                         bdmax) == 0
         assert np.array_equal(g, r), ("emu_edge", bw, bh, iw, ih, x, y)
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+def test_mc_warp8x8_resize(gpu, bpc):
+    o = _mc_sigs(_o())
+    I = ctypes.c_int
+    o.oracle_mc_warp8x8.argtypes = [I, _VP, _SS, _VP, _SS, _VP, _SS, _VP, I, I, I]
+    o.oracle_mc_warp8x8.restype = None
+    o.oracle_mc_resize.argtypes = [_VP, _SS, _VP, _SS, I, I, I, I, I, I]
+    o.oracle_mc_resize.restype = None
+    rng = np.random.default_rng(700 + bpc)
+    bdmax = (1 << bpc) - 1
+    for it in range(50):
+        src = make_texture(rng, 32, 32, bpc)
+        off = 8 * 32 + 8
+        abcd = rng.integers(-2000, 2001, size=4).astype(np.int16)
+        mx, my = int(rng.integers(-16384, 65537)), int(rng.integers(-16384, 65537))
+        ref = np.zeros((8, 8), _dt(bpc))
+        got = np.zeros((8, 8), _dt(bpc))
+        o.oracle_mc_warp8x8(0, P(ref), ref.strides[0], None, 0, P(src, off), src.strides[0], P(abcd), mx, my, bpc)
+        assert lib().mi_dsp_mc_warp8x8(0, P(got), got.strides[0], P(src, off), src.strides[0], P(abcd), mx, my,
+                                       bdmax) == 0
+        assert np.array_equal(got, ref), ("warp8x8", it)
+        rt = np.zeros((8, 12), np.int16)
+        gt = np.zeros((8, 12), np.int16)
+        o.oracle_mc_warp8x8(1, None, 0, P(rt), 12, P(src, off), src.strides[0], P(abcd), mx, my, bpc)
+        assert lib().mi_dsp_mc_warp8x8(1, P(gt), 12, P(src, off), src.strides[0], P(abcd), mx, my, bdmax) == 0
+        assert np.array_equal(gt, rt), ("warp8x8t", it)
+        # resize: a row band upscaled as superres does (dx = step, mx0 = initial phase)
+        src_w, h = int(rng.integers(16, 200)), int(rng.integers(1, 9))
+        dst_w = int(src_w * rng.uniform(1.0, 2.0))
+        dx = ((src_w << 14) + (dst_w >> 1)) // dst_w
+        mx0 = int(rng.integers(0, 1 << 14))
+        s = make_texture(rng, src_w, h, bpc)
+        r = np.zeros((h, dst_w), _dt(bpc))
+        g = np.zeros((h, dst_w), _dt(bpc))
+        o.oracle_mc_resize(P(r), r.strides[0], P(s), s.strides[0], dst_w, h, src_w, dx, mx0, bpc)
+        assert lib().mi_dsp_mc_resize(P(g), g.strides[0], P(s), s.strides[0], dst_w, h, src_w, dx, mx0, bdmax) == 0
+        assert np.array_equal(g, r), ("resize", src_w, dst_w, mx0)
