@@ -15,7 +15,8 @@
 
 namespace mi {
 
-constexpr int kLrWin = 72;             // LDS window row stride (int16), >= 64 + 6
+constexpr int kLrWin = 80;             // LDS window row stride (int16): columns x0-8 .. x0+71
+constexpr int kWX = 8;                 // window column of x0 (8-px aligned halo: vector staging)
 constexpr int kLrAB = 68;              // A/B row stride
 constexpr int kNY = 8;                 // waves (row groups) per workgroup
 constexpr int kNR = 64 / kNY;          // output rows per lane
@@ -46,7 +47,8 @@ __device__ __forceinline__ int ld_px(const uint8_t *base, int64_t stride, int y,
 // tx + 64 for the two extra columns) and a quarter of the rows, and slides a (2R+1)-row
 // window of horizontal sums down its column: 2R+1 LDS reads per position.
 template <int R>
-__device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, unsigned s, int bdm8) {
+__device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, unsigned s, int bdm8,
+                       const uint8_t *xbyx) {
     constexpr int n = (2 * R + 1) * (2 * R + 1);
     constexpr unsigned one_by_x = n == 25 ? 164 : 455;
     // 66 columns x kABG row groups, one column per lane
@@ -57,7 +59,7 @@ __device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, u
     const int y0 = -1 + g * per, y1 = min(-1 + (g + 1) * per, sh + 1);
     {
         const int x = c - 1;                          // position column (-1 .. tw)
-        const int16_t *col = win + x + 3;
+        const int16_t *col = win + x + kWX;
         int rs[2 * R + 1], rq[2 * R + 1];
 #pragma unroll
         for (int k = 0; k < 2 * R; k++) {             // rows y0-R .. y0+R-1
@@ -83,7 +85,7 @@ __device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, u
                 const int b = (sum + ((1 << bdm8) >> 1)) >> bdm8;
                 const unsigned p = (unsigned)max(a * n - b * b, 0);
                 const unsigned z = (p * s + (1u << 19)) >> 20;
-                const unsigned xv = sgr_x_by_x(z);
+                const unsigned xv = xbyx[min(z, 255u)];   // LDS table, not a divide per sample
                 A[(y + 1) * kLrAB + x + 1] = (int)((xv * (unsigned)sum * one_by_x + (1u << 11)) >> 12);
                 B[(y + 1) * kLrAB + x + 1] = (int16_t)xv;
             }
@@ -115,7 +117,7 @@ __device__ __forceinline__ void sgr_px(const int *A, const int16_t *B, int r0, i
         for (int q = 0; q < kNR; q++) {
             ld(r0 + q + 1, ca2, sa2, cb2, sb2);
             if (r0 + q < r1) {
-                const int src = win[(r0 + q + 3) * kLrWin + i + 3];
+                const int src = win[(r0 + q + 3) * kLrWin + i + kWX];
                 const int a = (cb1 + sb1 + cb0 + cb2) * 4 + (sb0 + sb2) * 3;
                 const int b = (ca1 + sa1 + ca0 + ca2) * 4 + (sa0 + sa2) * 3;
                 acc[q] += w * ((b - a * src + (1 << 8)) >> 9);
@@ -131,13 +133,13 @@ __device__ __forceinline__ void sgr_px(const int *A, const int16_t *B, int r0, i
         for (int q = 0; q < kNR; q += 2) {
             ld(r0 + q + 1, cad, sad, cbd, sbd);
             if (r0 + q < r1) {
-                const int src = win[(r0 + q + 3) * kLrWin + i + 3];
+                const int src = win[(r0 + q + 3) * kLrWin + i + kWX];
                 const int a = (cbu + cbd) * 6 + (sbu + sbd) * 5;
                 const int b = (cau + cad) * 6 + (sau + sad) * 5;
                 acc[q] += w * ((b - a * src + (1 << 8)) >> 9);
             }
             if (r0 + q + 1 < r1) {
-                const int src = win[(r0 + q + 4) * kLrWin + i + 3];
+                const int src = win[(r0 + q + 4) * kLrWin + i + kWX];
                 const int a = cbd * 6 + sbd * 5;
                 const int b = cad * 6 + sad * 5;
                 acc[q + 1] += w * ((b - a * src + (1 << 7)) >> 8);
@@ -147,14 +149,49 @@ __device__ __forceinline__ void sgr_px(const int *A, const int16_t *B, int r0, i
     }
 }
 
+// 8 pixels as int16 pairs in a uint4 (u16: one 16-B load; u8: one 8-B load widened)
+__device__ __forceinline__ uint32_t pk2(int lo, int hi) { return (uint32_t)(lo & 0xffff) | ((uint32_t)hi << 16); }
+template <typename Px>
+__device__ __forceinline__ uint4 load8(const Px *p) {
+    if constexpr (sizeof(Px) == 2) {
+        return *reinterpret_cast<const uint4 *>(p);
+    } else {
+        const uint2 d = *reinterpret_cast<const uint2 *>(p);
+        return make_uint4((d.x & 0xff) | ((d.x & 0xff00) << 8), ((d.x >> 16) & 0xff) | ((d.x >> 8) & 0xff0000),
+                          (d.y & 0xff) | ((d.y & 0xff00) << 8), ((d.y >> 16) & 0xff) | ((d.y >> 8) & 0xff0000));
+    }
+}
+template <typename Px>
+__device__ __forceinline__ void store8(Px *p, const uint4 &u) {
+    if constexpr (sizeof(Px) == 2) {
+        *reinterpret_cast<uint4 *>(p) = u;
+    } else {
+        uint2 d;
+        d.x = (u.x & 0xff) | ((u.x >> 8) & 0xff00) | ((u.y & 0xff) << 16) | ((u.y & 0xff0000) << 8);
+        d.y = (u.z & 0xff) | ((u.z >> 8) & 0xff00) | ((u.w & 0xff) << 16) | ((u.w & 0xff0000) << 8);
+        *reinterpret_cast<uint2 *>(p) = d;
+    }
+}
+// the finished sh x tw output tile (int16, row stride 64, in LDS) -> O with 8-pixel stores
+template <typename Px>
+__device__ __forceinline__ void store_tile(const int16_t *t, uint8_t *O, int64_t st, int S, int sh, int x0, int tw) {
+    for (int i = threadIdx.x; i < sh * 8; i += kNT) {
+        const int r = i >> 3, c = 8 * (i & 7);
+        if (c >= tw) continue;
+        Px *dp = reinterpret_cast<Px *>(O + (int64_t)(S + r) * st) + x0 + c;
+        if (c + 8 <= tw) store8<Px>(dp, *reinterpret_cast<const uint4 *>(t + r * 64 + c));
+        else for (int j = 0; j < tw - c; j++) dp[j] = (Px)t[r * 64 + c + j];
+    }
+}
+
 // Stripe (64 luma rows, offset 8 up; first stripe 56) -> plane rows.
 __device__ __forceinline__ int stripe_start(int k, int ssv) { return k ? (64 * k - 8) >> ssv : 0; }
 
 template <typename Px>
 __global__ __launch_bounds__(kNT) void lr_kernel(LrArgs a) {
-    __shared__ int16_t win[70 * kLrWin];
+    __shared__ __attribute__((aligned(16))) int16_t win[70 * kLrWin];
     __shared__ int A[66 * kLrAB];
-    __shared__ int16_t B[66 * kLrAB];
+    __shared__ __attribute__((aligned(16))) int16_t B[66 * kLrAB];
     int16_t *hor = reinterpret_cast<int16_t *>(A);    // Wiener: [70][64] aliases A
 
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -193,27 +230,30 @@ __global__ __launch_bounds__(kNT) void lr_kernel(LrArgs a) {
         u = &a.lr_mask[sbi].lr[p][ui];
         type = u->type;
     }
-    if (type == 0) {   // RESTORATION_NONE: O = C
-        if (tx < tw) {
-            int v[kNR];
-#pragma unroll
-            for (int q = 0; q < kNR; q++) v[q] = r0 + q < r1 ? ld_px<Px>(C, st, S + r0 + q, x0 + tx) : 0;
-#pragma unroll
-            for (int q = 0; q < kNR; q++)
-                if (r0 + q < r1) reinterpret_cast<Px *>(O + (int64_t)(S + r0 + q) * st)[x0 + tx] = (Px)v[q];
+    if (type == 0) {   // RESTORATION_NONE: O = C, 8-pixel vectors
+        for (int i = threadIdx.x; i < sh * 8; i += kNT) {
+            const int r = i >> 3, x = x0 + 8 * (i & 7);
+            if (x >= x0 + tw) continue;
+            const Px *sp = reinterpret_cast<const Px *>(C + (int64_t)(S + r) * st) + x;
+            Px *dp = reinterpret_cast<Px *>(O + (int64_t)(S + r) * st) + x;
+            if (x + 8 <= x0 + tw) store8<Px>(dp, load8<Px>(sp));   // O = C
+            else for (int j = 0; j < x0 + tw - x; j++) dp[j] = sp[j];
         }
         return;
     }
 
-    // ---- stage the (sh+6) x (tw+6) window (C inside the stripe, D across its edges) ----
+    // ---- stage the (sh+6)-row window, columns x0-8 .. x0+71 (C inside the stripe, D across
+    // its edges) as 8-pixel vectors; columns outside the plane replicate the edge pixel ----
     const bool have_top = k > 0, have_bottom = E < ph;
-    const int wr = sh + 6, wc = tw + 6;
-    // all row loads of this lane are issued before the first LDS store (latency overlap)
-    int16_t v0[kWL], v1[kWL];
+    const int wr = sh + 6;
+    constexpr int kNV = kLrWin / 8;                   // vectors per window row
+    constexpr int kSV = (70 * kNV + kNT - 1) / kNT;   // vectors per lane
+    uint4 sv[kSV];
 #pragma unroll
-    for (int q = 0; q < kWL; q++) {
-        const int rr = ty + kNY * q, r = rr - 3;
-        v0[q] = v1[q] = 0;
+    for (int q = 0; q < kSV; q++) {
+        sv[q] = make_uint4(0, 0, 0, 0);
+        const int i = threadIdx.x + q * kNT;
+        const int rr = i / kNV, x = x0 - 8 + 8 * (i % kNV), r = rr - 3;
         if (rr < wr) {
             int yy;
             const uint8_t *src;
@@ -221,17 +261,20 @@ __global__ __launch_bounds__(kNT) void lr_kernel(LrArgs a) {
             else if (r < 0) { src = have_top ? D : C; yy = have_top ? S - 2 + (r == -1) : S; }
             else { src = have_bottom ? D : C; yy = have_bottom ? min(E + (r > sh), ph - 1) : E - 1; }
             const Px *row = reinterpret_cast<const Px *>(src + (int64_t)yy * st);
-            v0[q] = (int16_t)row[min(max(x0 + tx - 3, 0), pw - 1)];
-            if (tx + 64 < wc) v1[q] = (int16_t)row[min(x0 + tx + 61, pw - 1)];
+            if (x >= 0 && x + 8 <= pw) sv[q] = load8<Px>(row + x);
+            else {
+                int e[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) e[j] = row[min(max(x + j, 0), pw - 1)];
+                sv[q] = make_uint4(pk2(e[0], e[1]), pk2(e[2], e[3]), pk2(e[4], e[5]), pk2(e[6], e[7]));
+            }
         }
     }
 #pragma unroll
-    for (int q = 0; q < kWL; q++) {
-        const int rr = ty + kNY * q;
-        if (rr < wr) {
-            win[rr * kLrWin + tx] = v0[q];
-            if (tx + 64 < wc) win[rr * kLrWin + tx + 64] = v1[q];
-        }
+    for (int q = 0; q < kSV; q++) {
+        const int i = threadIdx.x + q * kNT;
+        const int rr = i / kNV;
+        if (rr < wr) *reinterpret_cast<uint4 *>(&win[rr * kLrWin + 8 * (i % kNV)]) = sv[q];
     }
     __syncthreads();
 
@@ -247,7 +290,7 @@ __global__ __launch_bounds__(kNT) void lr_kernel(LrArgs a) {
         const int clip_h = (1 << (bd + 1 + 7 - rbh)) - 1;
         if (tx < tw) {
             for (int rr = ty; rr < wr; rr += kNY) {
-                const int16_t *row = win + rr * kLrWin + tx;
+                const int16_t *row = win + rr * kLrWin + tx + kWX - 3;
                 int sum = 1 << (bd + 6);
 #pragma unroll
                 for (int t = 0; t < 7; t++) sum += (int)row[t] * fh[t];
@@ -266,15 +309,19 @@ __global__ __launch_bounds__(kNT) void lr_kernel(LrArgs a) {
                     int sum = -off;
 #pragma unroll
                     for (int t = 0; t < 7; t++) sum += h[q + t] * fv[t];
-                    const int v = min(max((sum + (1 << (rbv - 1))) >> rbv, 0), bdmax);
-                    reinterpret_cast<Px *>(O + (int64_t)(S + r0 + q) * st)[x0 + tx] = (Px)v;
+                    B[(r0 + q) * 64 + tx] = (int16_t)min(max((sum + (1 << (rbv - 1))) >> rbv, 0), bdmax);
                 }
             }
         }
+        __syncthreads();
+        store_tile<Px>(B, O, st, S, sh, x0, tw);
         return;
     }
 
     // ---- self-guided (looprestoration.rs:566-912) ----
+    __shared__ uint8_t xbyx[256];
+    if (threadIdx.x < 256) xbyx[threadIdx.x] = (uint8_t)sgr_x_by_x(threadIdx.x);
+    __syncthreads();
     const int sidx = type - 3;
     const int s0 = k_sgr_params[sidx][0], s1 = k_sgr_params[sidx][1];
     const int w0 = u->sgr_weights[0];
@@ -284,26 +331,28 @@ __global__ __launch_bounds__(kNT) void lr_kernel(LrArgs a) {
 #pragma unroll
     for (int q = 0; q < kNR; q++) acc[q] = 0;
     if (s0) {
-        sgr_ab<2>(win, A, B, sh, tw, (unsigned)s0, bdm8);
+        sgr_ab<2>(win, A, B, sh, tw, (unsigned)s0, bdm8, xbyx);
         __syncthreads();
         if (tx < tw) sgr_px<2>(A, B, r0, r1, tx, win, w0, acc);
         __syncthreads();
     }
     if (s1) {
-        sgr_ab<1>(win, A, B, sh, tw, (unsigned)s1, bdm8);
+        sgr_ab<1>(win, A, B, sh, tw, (unsigned)s1, bdm8, xbyx);
         __syncthreads();
         if (tx < tw) sgr_px<1>(A, B, r0, r1, tx, win, w1, acc);
     }
+    __syncthreads();   // B (the A/B map) is free: it becomes the output tile
     if (tx < tw) {
 #pragma unroll
         for (int q = 0; q < kNR; q++) {
             if (r0 + q < r1) {
-                const int px = win[(r0 + q + 3) * kLrWin + tx + 3];
-                const int v = min(max(px + ((acc[q] + (1 << 10)) >> 11), 0), bdmax);
-                reinterpret_cast<Px *>(O + (int64_t)(S + r0 + q) * st)[x0 + tx] = (Px)v;
+                const int px = win[(r0 + q + 3) * kLrWin + tx + kWX];
+                B[(r0 + q) * 64 + tx] = (int16_t)min(max(px + ((acc[q] + (1 << 10)) >> 11), 0), bdmax);
             }
         }
     }
+    __syncthreads();
+    store_tile<Px>(B, O, st, S, sh, x0, tw);
 }
 
 int launch_lr(const LrArgs &a, int bpc, hipStream_t s) {
