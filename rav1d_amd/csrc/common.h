@@ -83,8 +83,11 @@ struct ItxArgs {
     int blk_start[20];  // block ranges per tx size (enum order, as the caller groups them)
     int large_wg0;      // first workgroup of the large-size launch
 };
-// launch order of tx sizes: every side <= 16 first, then sizes with a 32/64 side
-constexpr int kItxLaunchOrder[19] = { 0, 1, 2, 5, 6, 7, 8, 13, 14, 3, 4, 9, 10, 11, 12, 15, 16, 17, 18 };
+// launch order of tx sizes: every side <= 16 first (small launch), then the large launch with
+// the 64-point sizes at its front: their workgroups are few but the longest (a 64-point
+// transform per lane, ~14 us at 4K10), so they start first and the 32-class workgroups fill
+// the machine around them (large launch 20.2 -> see DESIGN.md §4)
+constexpr int kItxLaunchOrder[19] = { 0, 1, 2, 5, 6, 7, 8, 13, 14, 4, 11, 12, 17, 18, 3, 9, 10, 15, 16 };
 constexpr int kItxNumSmall = 9;
 int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start);
 

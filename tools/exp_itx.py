@@ -32,6 +32,10 @@ def run(mask, name, reps=20):
 tx, dc = allb["tx"], (allb["txtp"] == 0) & (allb["eob"] < 1)
 small = np.isin(tx, [0, 1, 2, 5, 6, 7, 8, 13, 14])
 run(np.ones(len(allb), bool), "all")
+run(np.isin(tx, [4, 11, 12, 17, 18]), "64-class sizes")
+run(np.isin(tx, [3, 9, 10, 15, 16]), "32-class sizes")
+if len(sys.argv) > 1:
+    sys.exit(0)
 run(small, "small sizes")
 run(~small, "large sizes")
 run((tx == 0) & dc, "4x4 dc-only")
