@@ -478,6 +478,11 @@ int mi_dsp_mc_emu_edge(int bw, int bh, int iw, int ih, int x, int y, void *dst, 
  * columns -3 .. 11 readable; abcd = the block's warp steps. */
 int mi_dsp_mc_warp8x8(int prep, void *dst, ptrdiff_t dst_stride, const void *src, ptrdiff_t src_stride,
                       const int16_t *abcd, int mx, int my, int bitdepth_max);
+/* mc_scaled[filter2d] (prep 0: pixels into dst) / mct_scaled[filter2d] (prep 1: w * h int16
+ * into dst, dst_stride ignored) (src/mc.rs:212, 351, 496, 608): mx, my in [0, 1024) (1/1024
+ * pel), dx / dy the steps. */
+int mi_dsp_mc_scaled(int prep, int filter2d, void *dst, ptrdiff_t dst_stride, const void *src, ptrdiff_t src_stride,
+                     int w, int h, int mx, int my, int dx, int dy, int bitdepth_max);
 /* resize (src/mc.rs:1114-1172): super-resolution upscaling of h rows. */
 int mi_dsp_mc_resize(void *dst, ptrdiff_t dst_stride, const void *src, ptrdiff_t src_stride, int dst_w, int h,
                      int src_w, int dx, int mx0, int bitdepth_max);

@@ -1257,5 +1257,39 @@ int mi_dsp_mc_resize(void *dst, ptrdiff_t dst_stride, const void *src, ptrdiff_t
     return win_out(dst, dst_stride, dout, 0, h, 0, (ptrdiff_t)dst_w * px, s);
 }
 
+int mi_dsp_mc_scaled(int prep, int filter2d, void *dst, ptrdiff_t dst_stride, const void *src, ptrdiff_t src_stride,
+                     int w, int h, int mx, int my, int dx, int dy, int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || !dst || !src || filter2d < 0 || filter2d > 9 || !mc_dims_ok(w, h) || mx < 0 || mx >= 1024 || my < 0 ||
+        my >= 1024 || dx < 1 || dy < 1 || dx > 2048 || dy > 2048)
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    const int px = bpc == 8 ? 1 : 2;
+    hipStream_t s = g_call.stream;
+    // source reach: rows -3 .. ((h-1)*dy + my >> 10) + 4, columns -3 .. ((w-1)*dx + mx >> 10) + 4
+    const int r0 = -3, r1 = (((h - 1) * dy + my) >> 10) + 5;
+    const ptrdiff_t b0 = -3 * px, b1 = (ptrdiff_t)((((w - 1) * dx + mx) >> 10) + 5) * px;
+    if ((size_t)(r1 - r0) * (b1 - b0) > (1u << 19)) return -EINVAL;
+    uint8_t *win = g_call.scratch, *dout = win + (1 << 19);
+    if (int e = win_in(win, src, src_stride, r0, r1, b0, b1, s)) return e;
+    mi::McCallArgs a;
+    memset(&a, 0, sizeof(a));
+    a.src = win + (size_t)(-r0) * (b1 - b0) - b0;
+    a.src_stride = b1 - b0;
+    a.dst = dout;
+    a.dst_stride = (int64_t)w * px;
+    a.tmp1 = (int16_t *)dout;
+    a.prep = prep;
+    a.w = w; a.h = h; a.mx = mx; a.my = my; a.dx = dx; a.dy = dy; a.filter2d = filter2d;
+    mc_call_bd(a, bpc, bitdepth_max);
+    if (mi::launch_mc_call(a, 5, s)) return -EIO;
+    if (prep) {
+        if (hipMemcpyAsync(dst, dout, (size_t)w * h * 2, hipMemcpyDefault, s) != hipSuccess) return -EIO;
+        return hipStreamSynchronize(s) == hipSuccess ? 0 : -EIO;
+    }
+    return win_out(dst, dst_stride, dout, 0, h, 0, (ptrdiff_t)w * px, s);
+}
+
 }  // extern "C"
 } // extern "C"

@@ -280,9 +280,10 @@ struct McCallArgs {
     int64_t dst_stride, src_stride;
     int w, h, mx, my, filter2d, prep, op, weight, sign, ss_hor, ss_ver, iw, ih;
     int abcd[4];                  // warp
+    int dx, dy;                   // scaled
     int bpc, ib, bias, bdmax;
 };
-// kind 0 put / prep, 1 combine (op), 2 emu_edge, 3 warp8x8(t), 4 resize (mc_call.hip)
+// kind 0 put / prep, 1 combine (op), 2 emu_edge, 3 warp8x8(t), 4 resize, 5 scaled (mc_call.hip)
 int launch_mc_call(const McCallArgs &a, int kind, hipStream_t s);
 
 } // namespace mi

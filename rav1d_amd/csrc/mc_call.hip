@@ -1,6 +1,7 @@
 // mc_call.hip — single-call motion-compensation kernels behind the table-compatible entry
 // points (mi_dsp_mc_*): mc[10] / mct[10] (8-tap and bilinear put / prep), avg, w_avg, mask,
-// w_mask[3], blend, blend_v, blend_h, warp8x8 / warp8x8t, emu_edge and resize of Rav1dMCDSPContext (rav1d src/mc.rs:
+// w_mask[3], blend, blend_v, blend_h, warp8x8 / warp8x8t, emu_edge, resize and mc_scaled /
+// mct_scaled of Rav1dMCDSPContext (rav1d src/mc.rs:
 // 1174-1338; C src/mc_tmpl.c:52-845). One lane per output pixel (per mask sample for
 // w_mask); the per-call path exists for drop-in parity, the frame path is mc.hip.
 #include "common.h"
@@ -160,6 +161,51 @@ __global__ __launch_bounds__(256) void mc_call_emu_kernel(McCallArgs a) {
     st<Px>(a.dst, a.dst_stride, yy, xx, ld<Px>(a.src, a.src_stride, sy, sx));
 }
 
+// put / prep scaled (mc_tmpl.c:201-227, 291-330, 445-470, 528-560): positions in 1/1024 pel,
+// step dx / dy; output (y, x) reads source row ((my + y*dy) >> 10) and column
+// ((mx + x*dx) >> 10) with filter phases from the low 10 bits (closed form of the reference's
+// running position; mx, my < 1024)
+template <typename Px>
+__global__ __launch_bounds__(256) void mc_call_scaled_kernel(McCallArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.w * a.h) return;
+    const int y = i / a.w, x = i % a.w, ib = a.ib, bias = a.bias;
+    const int px_ = a.mx + x * a.dx, py_ = a.my + y * a.dy;
+    const int ioff = px_ >> 10, imx = px_ & 0x3ff, row = py_ >> 10, imy = py_ & 0x3ff;
+    const uint8_t *s = a.src;
+    const int64_t ss = a.src_stride;
+    int out;
+    if (a.filter2d == 9) {
+        auto mid = [&](int r) {
+            const int p0 = ld<Px>(s, ss, r, ioff), p1 = ld<Px>(s, ss, r, ioff + 1);
+            return rnd_c(16 * p0 + (imx >> 6) * (p1 - p0), 4 - ib);
+        };
+        const int m0 = mid(row), m1 = mid(row + 1);
+        const int v = 16 * m0 + (imy >> 6) * (m1 - m0);
+        out = a.prep ? rnd_c(v, 4) - bias : clip_c(rnd_c(v, 4 + ib), 0, a.bdmax);
+    } else {
+        const int8_t *fh = sub_h(a.filter2d, imx >> 6, a.w), *fv = sub_v(a.filter2d, imy >> 6, a.h);
+        auto mid = [&](int r) {
+            if (!fh) return ld<Px>(s, ss, r, ioff) << ib;
+            int v = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) v += fh[k] * ld<Px>(s, ss, r, ioff + k - 3);
+            return rnd_c(v, 6 - ib);
+        };
+        if (fv) {
+            int v = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) v += fv[k] * mid(row + k - 3);
+            out = a.prep ? rnd_c(v, 6) - bias : clip_c(rnd_c(v, 6 + ib), 0, a.bdmax);
+        } else {
+            const int m = mid(row);
+            out = a.prep ? m - bias : clip_c((m + ((1 << ib) >> 1)) >> ib, 0, a.bdmax);
+        }
+    }
+    if (a.prep) a.tmp1[y * a.w + x] = (int16_t)out;
+    else st<Px>(a.dst, a.dst_stride, y, x, out);
+}
+
 // warp8x8 / warp8x8t (mc_tmpl.c:714-796): 15 horizontally filtered rows of 8 in LDS (the
 // filter phase steps by abcd[0] along x and abcd[1] per row), then the vertical pass (abcd[2]
 // along x, abcd[3] per row). src at the block origin, rows / columns -3 .. 11 readable.
@@ -209,6 +255,11 @@ int launch_mc_call(const McCallArgs &a, int kind, hipStream_t s) {
     if (kind == 3) {
         if (a.bpc == 8) mc_call_warp_kernel<uint8_t><<<1, 64, 0, s>>>(a);
         else mc_call_warp_kernel<uint16_t><<<1, 64, 0, s>>>(a);
+        return hipGetLastError() == hipSuccess ? 0 : -5;
+    }
+    if (kind == 5) {
+        if (a.bpc == 8) mc_call_scaled_kernel<uint8_t><<<g, 256, 0, s>>>(a);
+        else mc_call_scaled_kernel<uint16_t><<<g, 256, 0, s>>>(a);
         return hipGetLastError() == hipSuccess ? 0 : -5;
     }
     if (kind == 4) {

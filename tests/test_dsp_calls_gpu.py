@@ -280,3 +280,33 @@ def test_mc_warp8x8_resize(gpu, bpc):
         o.oracle_mc_resize(P(r), r.strides[0], P(s), s.strides[0], dst_w, h, src_w, dx, mx0, bpc)
         assert lib().mi_dsp_mc_resize(P(g), g.strides[0], P(s), s.strides[0], dst_w, h, src_w, dx, mx0, bdmax) == 0
         assert np.array_equal(g, r), ("resize", src_w, dst_w, mx0)
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+def test_mc_scaled(gpu, bpc):
+    o = _mc_sigs(_o())
+    I = ctypes.c_int
+    o.oracle_mc_scaled.argtypes = [I, I, _VP, _SS, _VP, _VP, _SS] + [I] * 7
+    o.oracle_mc_scaled.restype = None
+    rng = np.random.default_rng(800 + bpc)
+    bdmax = (1 << bpc) - 1
+    for it in range(60):
+        w, h = int(rng.choice(SIZES[:6])), int(rng.choice(SIZES[:6]))
+        f2d = int(rng.integers(0, 10))
+        mx, my = int(rng.integers(0, 1024)), int(rng.integers(0, 1024))
+        dx, dy = int(rng.integers(512, 2049)), int(rng.integers(512, 2049))
+        src = make_texture(rng, 160, 160, bpc)
+        off = 8 * 160 + 8
+        for prep in (0, 1):
+            if prep:
+                ref, got = np.zeros(w * h, np.int16), np.zeros(w * h, np.int16)
+                o.oracle_mc_scaled(f2d, 1, None, 0, P(ref), P(src, off), src.strides[0], w, h, mx, my, dx, dy, bpc)
+                rc = lib().mi_dsp_mc_scaled(1, f2d, P(got), 0, P(src, off), src.strides[0], w, h, mx, my, dx, dy, bdmax)
+            else:
+                ref, got = np.zeros((h, w), _dt(bpc)), np.zeros((h, w), _dt(bpc))
+                o.oracle_mc_scaled(f2d, 0, P(ref), ref.strides[0], None, P(src, off), src.strides[0], w, h, mx, my,
+                                   dx, dy, bpc)
+                rc = lib().mi_dsp_mc_scaled(0, f2d, P(got), got.strides[0], P(src, off), src.strides[0], w, h, mx, my,
+                                            dx, dy, bdmax)
+            assert rc == 0
+            assert np.array_equal(got, ref), ("scaled", prep, f2d, w, h, mx, my, dx, dy)
