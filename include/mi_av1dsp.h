@@ -487,6 +487,19 @@ int mi_dsp_mc_scaled(int prep, int filter2d, void *dst, ptrdiff_t dst_stride, co
 int mi_dsp_mc_resize(void *dst, ptrdiff_t dst_stride, const void *src, ptrdiff_t src_stride, int dst_w, int h,
                      int src_w, int dx, int mx0, int bitdepth_max);
 
+/* lr.wiener[0|1] (src/looprestoration.rs:91-107, 299-370): one restoration unit of w <= 384
+ * by h <= 64 filtered in place. left = LeftPixelRow [h][4] (read when edges & LR_HAVE_LEFT);
+ * lpf = the loop-filtered rows, 0 and 1 above the unit and 6 and 7 below it, at `stride`
+ * (read when LR_HAVE_TOP / LR_HAVE_BOTTOM, columns -3 .. w + 2 as the edges allow);
+ * params = LooprestorationParams.filter [2][8] int16 as the reference builds it
+ * (src/lr_apply.rs: 8-bit centre tap without its +128). */
+int mi_dsp_lr_wiener(void *p, ptrdiff_t stride, const void *left, const void *lpf, int w, int h, const void *params,
+                     int edges, int bitdepth_max);
+/* lr.sgr[kind] (src/looprestoration.rs:710-912): kind 0 = 5x5 (s0, w0), 1 = 3x3 (s1, w1),
+ * 2 = both; params = LooprestorationParams_sgr {u32 s0, s1; i16 w0, w1}; the rest as wiener. */
+int mi_dsp_lr_sgr(int kind, void *p, ptrdiff_t stride, const void *left, const void *lpf, int w, int h,
+                  const void *params, int edges, int bitdepth_max);
+
 #ifdef __cplusplus
 }
 #endif

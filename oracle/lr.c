@@ -451,3 +451,36 @@ void oracle_lr_frame(void *const dst[3], void *const cdef[3], void *const debloc
     for (int p = 0; p < 3; p++)
         if (f.lpf[p]) free(f.lpf[p] - 4 * f.lpf_stride[p]);
 }
+
+/* Per-call lr.wiener / lr.sgr[kind] (looprestoration.rs:91-107): the table slots' semantics on
+ * one unit. left: [h][4] pixels; lpf: rows 0, 1 (above) and 6, 7 (below) at stride `stride`;
+ * filter: LooprestorationParams.filter as the reference builds it (lr_apply.rs:59-82: the
+ * 8-bit centre without its +128, folded here as the restatement expects). */
+void oracle_lr_wiener(void *p, ptrdiff_t stride, const void *left_px, const void *lpf, int w, int h,
+                      const int16_t filter[2][8], int edges, int bdmax)
+{
+    PX px = { bdmax > 255, bdmax, bdmax == 255 ? 8 : bdmax == 1023 ? 10 : 12 };
+    const ptrdiff_t ps = stride / (px.hbd ? 2 : 1);
+    int left[64][4];
+    for (int j = 0; j < h; j++)
+        for (int k = 0; k < 4; k++) left[j][k] = RD(&px, left_px, j * 4 + k);
+    LrParams prm;
+    memset(&prm, 0, sizeof(prm));
+    memcpy(prm.filter, filter, sizeof(prm.filter));
+    if (px.bd == 8) prm.filter[0][3] += 128;
+    wiener(&px, p, ps, (const int (*)[4])left, lpf, w, h, &prm, edges);
+}
+
+void oracle_lr_sgr(int kind, void *p, ptrdiff_t stride, const void *left_px, const void *lpf, int w, int h,
+                   unsigned s0, unsigned s1, int w0, int w1, int edges, int bdmax)
+{
+    PX px = { bdmax > 255, bdmax, bdmax == 255 ? 8 : bdmax == 1023 ? 10 : 12 };
+    const ptrdiff_t ps = stride / (px.hbd ? 2 : 1);
+    int left[64][4];
+    for (int j = 0; j < h; j++)
+        for (int k = 0; k < 4; k++) left[j][k] = RD(&px, left_px, j * 4 + k);
+    LrParams prm;
+    memset(&prm, 0, sizeof(prm));
+    prm.s0 = (int)s0; prm.s1 = (int)s1; prm.w0 = w0; prm.w1 = w1;
+    sgr(&px, kind, p, ps, (const int (*)[4])left, lpf, w, h, &prm, edges);
+}

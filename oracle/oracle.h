@@ -97,6 +97,12 @@ int oracle_prepare_intra_edges(int x, int have_left, int y, int have_top, int ti
 void oracle_intra_blocks(void *const planes[3], const ptrdiff_t strides[2], int bpc, const void *blocks, int n,
                          const int16_t *ac, const uint8_t *idx, const void *pal);
 
+/* lr.c: per-call loop restoration (one unit, in place) */
+void oracle_lr_wiener(void *p, ptrdiff_t stride, const void *left_px, const void *lpf, int w, int h,
+                      const int16_t filter[2][8], int edges, int bdmax);
+void oracle_lr_sgr(int kind, void *p, ptrdiff_t stride, const void *left_px, const void *lpf, int w, int h,
+                   unsigned s0, unsigned s1, int w0, int w1, int edges, int bdmax);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1291,5 +1291,80 @@ int mi_dsp_mc_scaled(int prep, int filter2d, void *dst, ptrdiff_t dst_stride, co
     return win_out(dst, dst_stride, dout, 0, h, 0, (ptrdiff_t)w * px, s);
 }
 
+// ---- lr table (src/looprestoration.rs:91-107): wiener, sgr[kind] on one unit ----
+namespace {
+// Stage the unit's pixels (columns 0 .. w + 3*have_right), the lpf rows 0, 1, 6, 7 (columns
+// -3*have_left .. w + 3*have_right) and left[h][4] into one pitch-P buffer (column 3 = x 0),
+// filter, and write the w x h result back over p.
+int lr_call(mi::LrCallArgs &a, void *p, ptrdiff_t stride, const void *left, const void *lpf, int w, int h,
+            int edges, int bitdepth_max, int bpc) {
+    const int px = bpc == 8 ? 1 : 2;
+    const bool hl = edges & 1, hr = edges & 2, ht = edges & 4, hb = edges & 8;
+    if ((hl && !left) || ((ht || hb) && !lpf)) return -EINVAL;
+    hipStream_t s = g_call.stream;
+    const ptrdiff_t P = (ptrdiff_t)(w + 6) * px;
+    uint8_t *dp = g_call.scratch, *dlpf = dp + 64 * P, *dleft = dlpf + 8 * P, *dout = dleft + 64 * 4 * 2;
+    auto rows = [&](uint8_t *dst, const void *src, int r, ptrdiff_t c0, ptrdiff_t c1) -> int {
+        return hipMemcpyAsync(dst + r * P + 3 * px + c0, (const uint8_t *)src + r * stride + c0, c1 - c0,
+                              hipMemcpyDefault, s) == hipSuccess ? 0 : -EIO;
+    };
+    const ptrdiff_t c1 = (ptrdiff_t)(w + (hr ? 3 : 0)) * px, lc0 = hl ? -3 * px : 0;
+    int e = 0;
+    for (int r = 0; r < h && !e; r++) e = rows(dp, p, r, 0, c1);
+    if (ht) for (int r = 0; r < 2 && !e; r++) e = rows(dlpf, lpf, r, lc0, c1);
+    if (hb) for (int r = 6; r < 8 && !e; r++) e = rows(dlpf, lpf, r, lc0, c1);
+    if (!e && hl) e = copy_in(dleft, left, (size_t)h * 4 * px, s);
+    if (e) return e;
+    a.p = dp + 3 * px;
+    a.lpf = dlpf + 3 * px;
+    a.left = dleft;
+    a.out = dout;
+    a.ps = P / px;
+    a.w = w;
+    a.h = h;
+    a.edges = edges;
+    a.bd = bpc;
+    (void)bitdepth_max;
+    if (mi::launch_lr_call(a, bpc, s)) return -EIO;
+    return win_out(p, stride, dout, 0, h, 0, (ptrdiff_t)w * px, s);
+}
+bool lr_dims_ok(int w, int h) { return w >= 1 && w <= 384 && h >= 1 && h <= 64; }
+}  // namespace
+
+int mi_dsp_lr_wiener(void *p, ptrdiff_t stride, const void *left, const void *lpf, int w, int h, const void *params,
+                     int edges, int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || !p || !params || !lr_dims_ok(w, h) || edges < 0 || edges > 15) return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    int16_t f[2][8];
+    if (hipMemcpy(f, params, sizeof(f), hipMemcpyDefault) != hipSuccess) return -EIO;
+    mi::LrCallArgs a;
+    memset(&a, 0, sizeof(a));
+    a.tp.wiener = true;
+    for (int k = 0; k < 7; k++) { a.tp.fh[k] = f[0][k]; a.tp.fv[k] = f[1][k]; }
+    if (bpc == 8) a.tp.fh[3] += 128;   // the reference adds the 8-bit centre tap separately
+    return lr_call(a, p, stride, left, lpf, w, h, edges, bitdepth_max, bpc);
+}
+
+int mi_dsp_lr_sgr(int kind, void *p, ptrdiff_t stride, const void *left, const void *lpf, int w, int h,
+                  const void *params, int edges, int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || kind < 0 || kind > 2 || !p || !params || !lr_dims_ok(w, h) || edges < 0 || edges > 15) return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    struct { uint32_t s0, s1; int16_t w0, w1; } sp;   // LooprestorationParams_sgr
+    if (hipMemcpy(&sp, params, sizeof(sp), hipMemcpyDefault) != hipSuccess) return -EIO;
+    mi::LrCallArgs a;
+    memset(&a, 0, sizeof(a));
+    a.tp.wiener = false;
+    a.tp.s0 = kind != 1 ? (int)sp.s0 : 0;
+    a.tp.s1 = kind != 0 ? (int)sp.s1 : 0;
+    a.tp.w0 = sp.w0;
+    a.tp.w1 = sp.w1;
+    if ((kind != 1 && !a.tp.s0) || (kind != 0 && !a.tp.s1)) return -EINVAL;
+    return lr_call(a, p, stride, left, lpf, w, h, edges, bitdepth_max, bpc);
+}
+
 }  // extern "C"
 } // extern "C"

@@ -227,6 +227,21 @@ struct LrArgs {
 // launchers (lr.hip)
 int launch_lr(const LrArgs &a, int bpc, hipStream_t s);
 
+// Wiener taps (centre +128 folded for every bit depth) or self-guided strengths / weights
+struct LrTileParams {
+    bool wiener;
+    int fh[7], fv[7];
+    int s0, s1, w0, w1;
+};
+struct LrCallArgs {
+    const uint8_t *p, *lpf, *left;   // staged unit pixels (column 0 = unit column 0), lpf rows 0-7, left [h][4]
+    uint8_t *out;                     // packed w x h
+    int64_t ps;                       // pixel stride of p and lpf (elements)
+    int w, h, edges, bd;
+    LrTileParams tp;
+};
+int launch_lr_call(const LrCallArgs &a, int bpc, hipStream_t s);
+
 struct FgArgs {
     MiFilmGrainData data;
     const uint8_t *src[3];

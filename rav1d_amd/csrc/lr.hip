@@ -187,6 +187,76 @@ __device__ __forceinline__ void store_tile(const int16_t *t, uint8_t *O, int64_t
 // Stripe (64 luma rows, offset 8 up; first stripe 56) -> plane rows.
 __device__ __forceinline__ int stripe_start(int k, int ssv) { return k ? (64 * k - 8) >> ssv : 0; }
 
+// Filter the staged window (sh + 6 rows, window column kWX = tile column 0) of one tile of at
+// most 64 x 64 into the output tile B (int16, row stride 64): Wiener (looprestoration.rs:
+// 299-370) or self-guided (:566-912). Shared by the frame kernel and the per-call entries.
+__device__ void lr_filter_tile(const LrTileParams &tp, int16_t *win, int *A, int16_t *B, int16_t *hor, int sh,
+                               int tw, int bd) {
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int r0 = ty * kNR, r1 = min(r0 + kNR, sh);
+    const int wr = sh + 6, bdmax = (1 << bd) - 1;
+    if (tp.wiener) {
+        const int rbh = bd == 12 ? 5 : 3, rbv = bd == 12 ? 9 : 11;
+        const int clip_h = (1 << (bd + 1 + 7 - rbh)) - 1;
+        if (tx < tw) {
+            for (int rr = ty; rr < wr; rr += kNY) {
+                const int16_t *row = win + rr * kLrWin + tx + kWX - 3;
+                int sum = 1 << (bd + 6);
+#pragma unroll
+                for (int t = 0; t < 7; t++) sum += (int)row[t] * tp.fh[t];
+                hor[rr * 64 + tx] = (int16_t)min(max((sum + (1 << (rbh - 1))) >> rbh, 0), clip_h);
+            }
+        }
+        __syncthreads();
+        if (tx < tw && r0 < r1) {
+            const int off = 1 << (bd + rbv - 1);
+            int h[kNR + 6];
+#pragma unroll
+            for (int q = 0; q < kNR + 6; q++) h[q] = r0 + q < wr ? (int)(uint16_t)hor[(r0 + q) * 64 + tx] : 0;
+#pragma unroll
+            for (int q = 0; q < kNR; q++) {
+                if (r0 + q < r1) {
+                    int sum = -off;
+#pragma unroll
+                    for (int t = 0; t < 7; t++) sum += h[q + t] * tp.fv[t];
+                    B[(r0 + q) * 64 + tx] = (int16_t)min(max((sum + (1 << (rbv - 1))) >> rbv, 0), bdmax);
+                }
+            }
+        }
+        __syncthreads();
+        return;
+    }
+    __shared__ uint8_t xbyx[256];
+    if (threadIdx.x < 256) xbyx[threadIdx.x] = (uint8_t)sgr_x_by_x(threadIdx.x);
+    __syncthreads();
+    const int bdm8 = bd - 8;
+    int acc[kNR];
+#pragma unroll
+    for (int q = 0; q < kNR; q++) acc[q] = 0;
+    if (tp.s0) {
+        sgr_ab<2>(win, A, B, sh, tw, (unsigned)tp.s0, bdm8, xbyx);
+        __syncthreads();
+        if (tx < tw) sgr_px<2>(A, B, r0, r1, tx, win, tp.w0, acc);
+        __syncthreads();
+    }
+    if (tp.s1) {
+        sgr_ab<1>(win, A, B, sh, tw, (unsigned)tp.s1, bdm8, xbyx);
+        __syncthreads();
+        if (tx < tw) sgr_px<1>(A, B, r0, r1, tx, win, tp.w1, acc);
+    }
+    __syncthreads();   // B (the A/B map) is free: it becomes the output tile
+    if (tx < tw) {
+#pragma unroll
+        for (int q = 0; q < kNR; q++) {
+            if (r0 + q < r1) {
+                const int px = win[(r0 + q + 3) * kLrWin + tx + kWX];
+                B[(r0 + q) * 64 + tx] = (int16_t)min(max(px + ((acc[q] + (1 << 10)) >> 11), 0), bdmax);
+            }
+        }
+    }
+    __syncthreads();
+}
+
 template <typename Px>
 __global__ __launch_bounds__(kNT) void lr_kernel(LrArgs a) {
     __shared__ __attribute__((aligned(16))) int16_t win[70 * kLrWin];
@@ -278,81 +348,70 @@ __global__ __launch_bounds__(kNT) void lr_kernel(LrArgs a) {
     }
     __syncthreads();
 
-    const int bd = a.bd, bdmax = (1 << bd) - 1;
-    if (type == 2) {
-        // ---- Wiener (looprestoration.rs:299-370) ----
-        int fh[7], fv[7];
-        fh[0] = fh[6] = u->filter_h[0]; fh[1] = fh[5] = u->filter_h[1]; fh[2] = fh[4] = u->filter_h[2];
-        fh[3] = 128 - 2 * (fh[0] + fh[1] + fh[2]);
-        fv[0] = fv[6] = u->filter_v[0]; fv[1] = fv[5] = u->filter_v[1]; fv[2] = fv[4] = u->filter_v[2];
-        fv[3] = 128 - 2 * (fv[0] + fv[1] + fv[2]);
-        const int rbh = bd == 12 ? 5 : 3, rbv = bd == 12 ? 9 : 11;
-        const int clip_h = (1 << (bd + 1 + 7 - rbh)) - 1;
-        if (tx < tw) {
-            for (int rr = ty; rr < wr; rr += kNY) {
-                const int16_t *row = win + rr * kLrWin + tx + kWX - 3;
-                int sum = 1 << (bd + 6);
-#pragma unroll
-                for (int t = 0; t < 7; t++) sum += (int)row[t] * fh[t];
-                hor[rr * 64 + tx] = (int16_t)min(max((sum + (1 << (rbh - 1))) >> rbh, 0), clip_h);
-            }
-        }
-        __syncthreads();
-        if (tx < tw && r0 < r1) {
-            const int off = 1 << (bd + rbv - 1);
-            int h[kNR + 6];
-#pragma unroll
-            for (int q = 0; q < kNR + 6; q++) h[q] = r0 + q < wr ? (int)(uint16_t)hor[(r0 + q) * 64 + tx] : 0;
-#pragma unroll
-            for (int q = 0; q < kNR; q++) {
-                if (r0 + q < r1) {
-                    int sum = -off;
-#pragma unroll
-                    for (int t = 0; t < 7; t++) sum += h[q + t] * fv[t];
-                    B[(r0 + q) * 64 + tx] = (int16_t)min(max((sum + (1 << (rbv - 1))) >> rbv, 0), bdmax);
-                }
-            }
-        }
-        __syncthreads();
-        store_tile<Px>(B, O, st, S, sh, x0, tw);
-        return;
+    LrTileParams tp;
+    tp.wiener = type == 2;
+    if (tp.wiener) {
+        tp.fh[0] = tp.fh[6] = u->filter_h[0]; tp.fh[1] = tp.fh[5] = u->filter_h[1]; tp.fh[2] = tp.fh[4] = u->filter_h[2];
+        tp.fh[3] = 128 - 2 * (tp.fh[0] + tp.fh[1] + tp.fh[2]);
+        tp.fv[0] = tp.fv[6] = u->filter_v[0]; tp.fv[1] = tp.fv[5] = u->filter_v[1]; tp.fv[2] = tp.fv[4] = u->filter_v[2];
+        tp.fv[3] = 128 - 2 * (tp.fv[0] + tp.fv[1] + tp.fv[2]);
+    } else {
+        const int sidx = type - 3;
+        tp.s0 = k_sgr_params[sidx][0];
+        tp.s1 = k_sgr_params[sidx][1];
+        tp.w0 = u->sgr_weights[0];
+        tp.w1 = 128 - (u->sgr_weights[0] + u->sgr_weights[1]);
     }
-
-    // ---- self-guided (looprestoration.rs:566-912) ----
-    __shared__ uint8_t xbyx[256];
-    if (threadIdx.x < 256) xbyx[threadIdx.x] = (uint8_t)sgr_x_by_x(threadIdx.x);
-    __syncthreads();
-    const int sidx = type - 3;
-    const int s0 = k_sgr_params[sidx][0], s1 = k_sgr_params[sidx][1];
-    const int w0 = u->sgr_weights[0];
-    const int w1 = 128 - (u->sgr_weights[0] + u->sgr_weights[1]);
-    const int bdm8 = bd - 8;
-    int acc[kNR];
-#pragma unroll
-    for (int q = 0; q < kNR; q++) acc[q] = 0;
-    if (s0) {
-        sgr_ab<2>(win, A, B, sh, tw, (unsigned)s0, bdm8, xbyx);
-        __syncthreads();
-        if (tx < tw) sgr_px<2>(A, B, r0, r1, tx, win, w0, acc);
-        __syncthreads();
-    }
-    if (s1) {
-        sgr_ab<1>(win, A, B, sh, tw, (unsigned)s1, bdm8, xbyx);
-        __syncthreads();
-        if (tx < tw) sgr_px<1>(A, B, r0, r1, tx, win, w1, acc);
-    }
-    __syncthreads();   // B (the A/B map) is free: it becomes the output tile
-    if (tx < tw) {
-#pragma unroll
-        for (int q = 0; q < kNR; q++) {
-            if (r0 + q < r1) {
-                const int px = win[(r0 + q + 3) * kLrWin + tx + kWX];
-                B[(r0 + q) * 64 + tx] = (int16_t)min(max(px + ((acc[q] + (1 << 10)) >> 11), 0), bdmax);
-            }
-        }
-    }
-    __syncthreads();
+    lr_filter_tile(tp, win, A, B, hor, sh, tw, a.bd);
     store_tile<Px>(B, O, st, S, sh, x0, tw);
+}
+
+// ---- per-call lr.wiener / lr.sgr (looprestoration.rs:91-107, 139-912) ----
+// One 512-lane workgroup per 64-column tile of the unit (w <= 384, h <= 64). The window is
+// the reference's `padding` (looprestoration.rs:139-268) built in LDS from the staged inputs:
+// the unit's pixels (with 3 columns either side where HAVE_LEFT / HAVE_RIGHT), left[h][4],
+// and the lpf rows 0, 1 (above) and 6, 7 (below); missing sides replicate.
+template <typename Px>
+__global__ __launch_bounds__(kNT) void lr_call_kernel(LrCallArgs a) {
+    __shared__ __attribute__((aligned(16))) int16_t win[70 * kLrWin];
+    __shared__ int A[66 * kLrAB];
+    __shared__ __attribute__((aligned(16))) int16_t B[66 * kLrAB];
+    int16_t *hor = reinterpret_cast<int16_t *>(A);
+    const int x0 = blockIdx.x * 64, tw = min(64, a.w - x0), h = a.h;
+    const bool hl = a.edges & 1, hr = a.edges & 2, ht = a.edges & 4, hb = a.edges & 8;
+    const Px *p = reinterpret_cast<const Px *>(a.p), *lpf = reinterpret_cast<const Px *>(a.lpf);
+    const Px *left = reinterpret_cast<const Px *>(a.left);
+    for (int i = threadIdx.x; i < (h + 6) * kLrWin; i += kNT) {
+        const int rr = i / kLrWin, c = i % kLrWin;
+        int x = x0 - kWX + c;
+        int v = 0;
+        if (x >= -3 && x < a.w + 3) {
+            if (!hr && x >= a.w) x = a.w - 1;
+            if (!hl && x < 0) x = 0;
+            const int j = rr - 3;
+            if (rr < 3 && ht) v = lpf[(rr < 2 ? 0 : 1) * a.ps + x];
+            else if (j >= h && hb) v = lpf[(j == h ? 6 : 7) * a.ps + x];
+            else {
+                const int jj = min(max(j, 0), h - 1);   // rows above / below replicate when absent
+                v = x < 0 ? left[jj * 4 + 1 + (x + 3)] : p[jj * a.ps + x];
+            }
+        }
+        win[i] = (int16_t)v;
+    }
+    __syncthreads();
+    lr_filter_tile(a.tp, win, A, B, hor, h, tw, a.bd);
+    // output tile -> the packed w x h result
+    for (int i = threadIdx.x; i < h * 64; i += kNT) {
+        const int r = i >> 6, c = i & 63;
+        if (c < tw) reinterpret_cast<Px *>(a.out)[r * a.w + x0 + c] = (Px)B[r * 64 + c];
+    }
+}
+
+int launch_lr_call(const LrCallArgs &a, int bpc, hipStream_t s) {
+    const int n = (a.w + 63) / 64;
+    if (bpc == 8) hipLaunchKernelGGL(lr_call_kernel<uint8_t>, dim3(n), dim3(kNT), 0, s, a);
+    else hipLaunchKernelGGL(lr_call_kernel<uint16_t>, dim3(n), dim3(kNT), 0, s, a);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 int launch_lr(const LrArgs &a, int bpc, hipStream_t s) {

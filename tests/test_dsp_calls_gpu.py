@@ -310,3 +310,58 @@ def test_mc_scaled(gpu, bpc):
                                             dx, dy, bdmax)
             assert rc == 0
             assert np.array_equal(got, ref), ("scaled", prep, f2d, w, h, mx, my, dx, dy)
+
+
+_SGR = [(140, 3236), (112, 2158), (93, 1618), (80, 1438), (70, 1295), (58, 1177), (47, 1079), (37, 996),
+        (30, 925), (25, 863), (0, 2589), (0, 1618), (0, 1177), (0, 925), (56, 0), (22, 0)]
+
+
+def _lr_case(rng, bpc):
+    """One unit at (8, 8) of a 400 x 80 picture: random size (w <= 384, h <= 64), edges, and
+    left / lpf pixels independent of the picture as the reference's callers may pass them."""
+    w = int(rng.choice([384, 64, 65, int(rng.integers(1, 385))]))
+    h = int(rng.choice([64, int(rng.integers(1, 65))]))
+    pic = make_texture(rng, 400, 80, bpc)
+    left = make_texture(rng, 4, h, bpc)
+    lpf = make_texture(rng, 400, 8, bpc)
+    return w, h, int(rng.integers(0, 16)), pic, left, lpf
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+def test_lr_wiener_sgr(gpu, bpc):
+    o = _o()
+    I = ctypes.c_int
+    o.oracle_lr_wiener.argtypes = [_VP, _SS, _VP, _VP, I, I, _VP, I, I]
+    o.oracle_lr_wiener.restype = None
+    o.oracle_lr_sgr.argtypes = [I, _VP, _SS, _VP, _VP, I, I, ctypes.c_uint, ctypes.c_uint, I, I, I, I]
+    o.oracle_lr_sgr.restype = None
+    rng = np.random.default_rng(900 + bpc)
+    bdmax = (1 << bpc) - 1
+    off = 8 * 400 + 8
+    for it in range(30):
+        w, h, edges, pic, left, lpf = _lr_case(rng, bpc)
+        # LooprestorationParams.filter as lr_apply builds it: symmetric taps in the AV1 ranges
+        f = np.zeros((2, 8), np.int16)
+        for k in range(2):
+            t = [int(rng.integers(-5, 11)), int(rng.integers(-23, 9)), int(rng.integers(-17, 47))]
+            c = -2 * sum(t) + (128 if (k == 1 or bpc > 8) else 0)
+            f[k, :7] = [t[0], t[1], t[2], c, t[2], t[1], t[0]]
+        ref, got = pic.copy(), pic.copy()
+        o.oracle_lr_wiener(P(ref, off), ref.strides[0], P(left), P(lpf, 8), w, h, P(f), edges, bdmax)
+        rc = lib().mi_dsp_lr_wiener(P(got, off), got.strides[0], P(left), P(lpf, 8), w, h, P(f), edges, bdmax)
+        assert rc == 0
+        assert np.array_equal(got, ref), ("wiener", it, w, h, edges, np.argwhere(got != ref)[:4])
+    for it in range(45):
+        w, h, edges, pic, left, lpf = _lr_case(rng, bpc)
+        s0, s1 = _SGR[int(rng.integers(0, 16))]
+        kind = (s0 != 0) + 2 * (s1 != 0) - 1
+        wt0, wt1 = int(rng.integers(-96, 32)), int(rng.integers(-32, 96))
+        w0, w1 = wt0, 128 - (wt0 + wt1)
+        prm = np.zeros(6, np.int16)
+        prm.view(np.uint32)[:2] = [s0, s1]
+        prm[4:6] = [w0, w1]
+        ref, got = pic.copy(), pic.copy()
+        o.oracle_lr_sgr(kind, P(ref, off), ref.strides[0], P(left), P(lpf, 8), w, h, s0, s1, w0, w1, edges, bdmax)
+        rc = lib().mi_dsp_lr_sgr(kind, P(got, off), got.strides[0], P(left), P(lpf, 8), w, h, P(prm), edges, bdmax)
+        assert rc == 0
+        assert np.array_equal(got, ref), ("sgr", kind, it, w, h, edges, np.argwhere(got != ref)[:4])
