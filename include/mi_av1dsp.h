@@ -500,6 +500,27 @@ int mi_dsp_lr_wiener(void *p, ptrdiff_t stride, const void *left, const void *lp
 int mi_dsp_lr_sgr(int kind, void *p, ptrdiff_t stride, const void *left, const void *lpf, int w, int h,
                   const void *params, int edges, int bitdepth_max);
 
+/* Film-grain table (src/filmgrain.rs:41-198). data = Dav1dFilmGrainData (MiFilmGrainData is
+ * layout-identical); buf / buf_y / grain_lut = GrainLut<Entry>: rows of 82 entries, int8 at
+ * 8 bits and int16 above; layout 1 = I420, 2 = I422, 3 = I444 (the generate_grain_uv /
+ * fguv_32x32xn enum_map slot).
+ * generate_grain_y (:298-343): the 73 x 82 luma template. */
+int mi_dsp_fg_generate_grain_y(void *buf, const MiFilmGrainData *data, int bitdepth_max);
+/* generate_grain_uv[layout] (:345-474): the chroma template of plane 1 + uv (its 38/73 x 44/82
+ * corner), auto-regressed over the luma template buf_y. */
+int mi_dsp_fg_generate_grain_uv(int layout, void *buf, const void *buf_y, const MiFilmGrainData *data, int uv,
+                                int bitdepth_max);
+/* fgy_32x32xn (:549-676): grain onto one strip of bh <= 32 rows and pw <= 8192 columns,
+ * src_row -> dst_row (same stride); scaling = the plane's LUT (1 << bitdepth entries). */
+int mi_dsp_fgy_32x32xn(void *dst_row, const void *src_row, ptrdiff_t stride, const MiFilmGrainData *data, size_t pw,
+                       const uint8_t *scaling, const void *grain_lut, int bh, int row_num, int bitdepth_max);
+/* fguv_32x32xn[layout] (:678-830): chroma plane 1 + uv_pl, bh in chroma rows; luma_row holds
+ * the co-located luma (pw << ss_x columns, as the reference reads them). */
+int mi_dsp_fguv_32x32xn(int layout, void *dst_row, const void *src_row, ptrdiff_t stride,
+                        const MiFilmGrainData *data, size_t pw, const uint8_t *scaling, const void *grain_lut, int bh,
+                        int row_num, const void *luma_row, ptrdiff_t luma_stride, int uv_pl, int is_id,
+                        int bitdepth_max);
+
 #ifdef __cplusplus
 }
 #endif

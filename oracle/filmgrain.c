@@ -302,3 +302,16 @@ void oracle_fg_apply(void *const out[3], void *const in[3], const ptrdiff_t stri
     }
     free(luma_in);
 }
+
+/* Per-call fgy_32x32xn (pl 0) / fguv_32x32xn (pl 1 + uv) (filmgrain.rs:87-191, 549-830): one
+ * strip; strides in bytes; lut = the plane's template as int16 [73][82]; layout 1..3. */
+void oracle_fg_32x32xn(int pl, int layout, void *dst_row, const void *src_row, ptrdiff_t stride, const void *data,
+                       int pw, const uint8_t *scaling, const int16_t *lut, int bh, int row_num,
+                       const void *luma_row, ptrdiff_t luma_stride, int is_id, int bdmax)
+{
+    FPX px = { bdmax > 255, bdmax, bdmax == 255 ? 0 : bdmax == 1023 ? 2 : 4 };
+    const int pxb = px.hbd ? 2 : 1;
+    const int sx = pl && layout != 3, sy = pl && layout == 1;
+    fg_row(&px, dst_row, src_row, stride / pxb, data, pw, scaling, lut, bh, row_num,
+           pl ? luma_row : NULL, luma_stride / pxb, pl ? pl - 1 : 0, is_id, sx, sy);
+}

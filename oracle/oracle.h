@@ -103,6 +103,14 @@ void oracle_lr_wiener(void *p, ptrdiff_t stride, const void *left_px, const void
 void oracle_lr_sgr(int kind, void *p, ptrdiff_t stride, const void *left_px, const void *lpf, int w, int h,
                    unsigned s0, unsigned s1, int w0, int w1, int edges, int bdmax);
 
+/* filmgrain.c: per-call table entries */
+void oracle_fg_generate_grain_y(int16_t *buf, const void *data, int bdmax);
+void oracle_fg_generate_grain_uv(int16_t *buf, const int16_t *buf_y, const void *data, int uv,
+                                 int subx, int suby, int bdmax);
+void oracle_fg_32x32xn(int pl, int layout, void *dst_row, const void *src_row, ptrdiff_t stride, const void *data,
+                       int pw, const uint8_t *scaling, const int16_t *lut, int bh, int row_num,
+                       const void *luma_row, ptrdiff_t luma_stride, int is_id, int bdmax);
+
 #ifdef __cplusplus
 }
 #endif

@@ -163,6 +163,11 @@ def lib():
     _sig(L, "mi_dsp_mc_scaled", _I, [_I, _I, _VP, _SS, _VP, _SS] + [_I] * 7)
     _sig(L, "mi_dsp_lr_wiener", _I, [_VP, _SS, _VP, _VP, _I, _I, _VP, _I, _I])
     _sig(L, "mi_dsp_lr_sgr", _I, [_I, _VP, _SS, _VP, _VP, _I, _I, _VP, _I, _I])
+    _sig(L, "mi_dsp_fg_generate_grain_y", _I, [_VP, _VP, _I])
+    _sig(L, "mi_dsp_fg_generate_grain_uv", _I, [_I, _VP, _VP, _VP, _I, _I])
+    _sig(L, "mi_dsp_fgy_32x32xn", _I, [_VP, _VP, _SS, _VP, ctypes.c_size_t, _VP, _VP, _I, _I, _I])
+    _sig(L, "mi_dsp_fguv_32x32xn", _I, [_I, _VP, _VP, _SS, _VP, ctypes.c_size_t, _VP, _VP, _I, _I, _VP, _SS, _I, _I,
+                                        _I])
     _sig(L, "mi_deblock_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiLoopFilter), _VP])
     _sig(L, "mi_deblock_frame_to", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
                                                   ctypes.POINTER(MiLoopFilter), _VP])
@@ -187,7 +192,8 @@ EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error"
             "mi_dsp_loop_filter_sb", "mi_dsp_cdef_filter", "mi_dsp_cdef_dir", "mi_dsp_mc_put", "mi_dsp_mc_prep",
             "mi_dsp_mc_avg", "mi_dsp_mc_w_avg", "mi_dsp_mc_mask", "mi_dsp_mc_w_mask", "mi_dsp_mc_blend",
             "mi_dsp_mc_blend_v", "mi_dsp_mc_blend_h", "mi_dsp_mc_emu_edge", "mi_dsp_mc_warp8x8", "mi_dsp_mc_resize",
-            "mi_dsp_mc_scaled", "mi_dsp_lr_wiener", "mi_dsp_lr_sgr"]
+            "mi_dsp_mc_scaled", "mi_dsp_lr_wiener", "mi_dsp_lr_sgr",
+            "mi_dsp_fg_generate_grain_y", "mi_dsp_fg_generate_grain_uv", "mi_dsp_fgy_32x32xn", "mi_dsp_fguv_32x32xn"]
 
 
 def check(rc, what):

@@ -72,6 +72,19 @@ struct CallState {
         if (hipMalloc(&scratch, scratch_bytes) != hipSuccess) return err = -ENOMEM;
         return err = 0;
     }
+    int reserve(size_t n) {   // grow the scratch (only ever grows; callers hold mu)
+        if (n <= scratch_bytes) return 0;
+        if (hipStreamSynchronize(stream) != hipSuccess) return -EIO;
+        (void)hipFree(scratch);
+        scratch = nullptr;
+        scratch_bytes = 0;
+        if (hipMalloc(&scratch, n) != hipSuccess) {
+            if (hipMalloc(&scratch, 1 << 20) == hipSuccess) scratch_bytes = 1 << 20;
+            return -ENOMEM;
+        }
+        scratch_bytes = n;
+        return 0;
+    }
 };
 CallState g_call;
 
@@ -593,17 +606,23 @@ int mi_lr_frame(MiCtx *ctx, const MiPicture *cdef, const MiPicture *deblocked, c
     return r ? fail(ctx, -EIO) : 0;
 }
 
-static int fg_setup(MiCtx *ctx, const MiPicture *in, const MiPicture *out, const MiFilmGrainData *data,
-                    int is_id, mi::FgArgs &a) {
+static int fg_tables() {
     static std::once_flag once;
     static int tables_rc = 0;
     std::call_once(once, [] { tables_rc = mi::init_fg_tables(); });
-    if (tables_rc) return -EIO;
+    return tables_rc ? -EIO : 0;
+}
+static bool fg_data_ok(const MiFilmGrainData *data) {
+    return !(data->num_y_points < 0 || data->num_y_points > 14 || data->ar_coeff_lag < 0 || data->ar_coeff_lag > 3 ||
+             data->num_uv_points[0] < 0 || data->num_uv_points[0] > 10 || data->num_uv_points[1] < 0 ||
+             data->num_uv_points[1] > 10 || data->ar_coeff_shift < 6 || data->ar_coeff_shift > 9);
+}
+
+static int fg_setup(MiCtx *ctx, const MiPicture *in, const MiPicture *out, const MiFilmGrainData *data,
+                    int is_id, mi::FgArgs &a) {
+    if (int e = fg_tables()) return e;
     if (in->bpc != 8 && in->bpc != 10 && in->bpc != 12) return -EINVAL;
-    if (data->num_y_points < 0 || data->num_y_points > 14 || data->ar_coeff_lag < 0 || data->ar_coeff_lag > 3 ||
-        data->num_uv_points[0] < 0 || data->num_uv_points[0] > 10 || data->num_uv_points[1] < 0 ||
-        data->num_uv_points[1] > 10 || data->ar_coeff_shift < 6 || data->ar_coeff_shift > 9)
-        return -EINVAL;
+    if (!fg_data_ok(data)) return -EINVAL;
     memset(&a, 0, sizeof(a));
     a.data = *data;
     a.bpc = in->bpc;
@@ -1364,6 +1383,188 @@ int mi_dsp_lr_sgr(int kind, void *p, ptrdiff_t stride, const void *left, const v
     a.tp.w1 = sp.w1;
     if ((kind != 1 && !a.tp.s0) || (kind != 0 && !a.tp.s1)) return -EINVAL;
     return lr_call(a, p, stride, left, lpf, w, h, edges, bitdepth_max, bpc);
+}
+
+
+// ---- film-grain table (src/filmgrain.rs:41-198): generate_grain_y / _uv, fgy / fguv_32x32xn ----
+namespace {
+constexpr int kGW = 82, kGH = 73, kGP = 88;   // template width / height, device pitch (fg.hip)
+constexpr size_t kFgLutB = 3 * kGH * kGP * 2, kFgSclB = 3 * 4096;
+size_t al256(size_t n) { return (n + 255) & ~(size_t)255; }
+
+int fg_read_data(MiFilmGrainData &d, const MiFilmGrainData *data) {
+    if (hipMemcpy(&d, data, sizeof(d), hipMemcpyDefault) != hipSuccess) return -EIO;
+    return fg_data_ok(&d) ? 0 : -EINVAL;
+}
+// caller's GrainLut<Entry> rows (82 entries: int8 at 8 bits, int16 above) <-> int16 [73][82]
+int fg_lut_read(int16_t *t, const void *buf, int bpc) {
+    if (bpc == 8) {
+        int8_t b[kGH * kGW];
+        if (hipMemcpy(b, buf, sizeof(b), hipMemcpyDefault) != hipSuccess) return -EIO;
+        for (int i = 0; i < kGH * kGW; i++) t[i] = b[i];
+        return 0;
+    }
+    return hipMemcpy(t, buf, kGH * kGW * 2, hipMemcpyDefault) == hipSuccess ? 0 : -EIO;
+}
+int fg_lut_write(void *buf, const int16_t *t, int bpc) {
+    if (bpc == 8) {
+        int8_t b[kGH * kGW];
+        for (int i = 0; i < kGH * kGW; i++) b[i] = (int8_t)t[i];
+        return hipMemcpy(buf, b, sizeof(b), hipMemcpyDefault) == hipSuccess ? 0 : -EIO;
+    }
+    return hipMemcpy(buf, t, kGH * kGW * 2, hipMemcpyDefault) == hipSuccess ? 0 : -EIO;
+}
+// run the template generator and fetch plane pl's template into t [73][82]
+int fg_generate(mi::FgArgs &a, int pl, int16_t *t) {
+    hipStream_t s = g_call.stream;
+    a.lut = (int16_t *)g_call.scratch;
+    a.scaling = g_call.scratch + kFgLutB;
+    if (mi::launch_fg(a, s, true, false)) return -EIO;
+    static int16_t dev[kGH * kGP];
+    if (hipMemcpyAsync(dev, a.lut + pl * kGH * kGP, sizeof(dev), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    for (int r = 0; r < kGH; r++) memcpy(t + r * kGW, dev + r * kGP, kGW * 2);
+    return 0;
+}
+// the caller's template -> device slot pl (pitch 88)
+int fg_lut_in(int16_t *dlut, int pl, const void *grain_lut, int bpc, hipStream_t s) {
+    static int16_t t[kGH * kGW], dev[kGH * kGP];
+    if (int e = fg_lut_read(t, grain_lut, bpc)) return e;
+    memset(dev, 0, sizeof(dev));
+    for (int r = 0; r < kGH; r++) memcpy(dev + r * kGP, t + r * kGW, kGW * 2);
+    if (hipMemcpyAsync(dlut + pl * kGH * kGP, dev, sizeof(dev), hipMemcpyHostToDevice, s) != hipSuccess) return -EIO;
+    return hipStreamSynchronize(s) == hipSuccess ? 0 : -EIO;   // dev is reused
+}
+int layout_ok(int layout) { return layout >= 1 && layout <= 3; }
+
+// fgy (plane 0) / fguv (plane 1 + uv): one 32-row strip through the frame apply kernel
+int fg_strip(int pl, int layout, void *dst_row, const void *src_row, ptrdiff_t stride, const MiFilmGrainData *data,
+             size_t pw, const uint8_t *scaling, const void *grain_lut, int bh, int row_num, const void *luma_row,
+             ptrdiff_t luma_stride, int is_id, int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    const int sx = pl && layout != 3, sy = pl && layout == 1;
+    if (!bpc || !dst_row || !src_row || !data || !scaling || !grain_lut || (pl && (!luma_row || !layout_ok(layout))) ||
+        pw < 1 || pw > 8192 || bh < 1 || bh > (32 >> sy) || row_num < 0)
+        return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    if (int e = fg_tables()) return e;
+    mi::FgArgs a;
+    memset(&a, 0, sizeof(a));
+    if (int e = fg_read_data(a.data, data)) return e;
+    const int px = bpc == 8 ? 1 : 2;
+    const size_t P = al256(pw * px), lw = pw << sx, LP = al256(lw * px);
+    const int lrows = pl ? ((bh - 1) << sy) + 1 : 0;
+    const int nblocks = (int)((pw + (32 >> sx) - 1) / (32 >> sx));
+    const size_t o_scl = kFgLutB, o_off = o_scl + kFgSclB, o_src = o_off + al256(2 * nblocks),
+                 o_luma = o_src + P * bh, total = o_luma + LP * lrows;
+    if (int e = g_call.reserve(total)) return e;
+    hipStream_t s = g_call.stream;
+    uint8_t *S = g_call.scratch;
+    a.lut = (int16_t *)S;
+    a.scaling = S + o_scl;
+    a.offsets = S + o_off;
+    if (int e = fg_lut_in(a.lut, pl, grain_lut, bpc, s)) return e;
+    int e = copy_in(a.scaling + pl * 4096, scaling, (size_t)1 << bpc, s);
+    if (!e && pl) e = copy_in(a.scaling, scaling, (size_t)1 << bpc, s);   // the slot read under chroma_scaling_from_luma
+    for (int r = 0; r < bh && !e; r++)
+        if (hipMemcpyAsync(S + o_src + r * P, (const uint8_t *)src_row + r * stride, pw * px, hipMemcpyDefault, s) !=
+            hipSuccess)
+            e = -EIO;
+    for (int y = 0; pl && y < bh && !e; y++)
+        if (hipMemcpyAsync(S + o_luma + (size_t)(y << sy) * LP, (const uint8_t *)luma_row + (y << sy) * luma_stride,
+                           lw * px, hipMemcpyDefault, s) != hipSuccess)
+            e = -EIO;
+    if (e) return e;
+    a.bpc = bpc;
+    a.layout = pl ? layout : 0;
+    a.ss_x = pl && layout != 3;
+    a.ss_y = pl && layout == 1;
+    a.w = (int)lw;
+    a.h = bh << sy;
+    a.is_id = is_id;
+    const bool prev = a.data.overlap_flag && row_num > 0;
+    a.nrows = prev ? 2 : 1;
+    a.row0 = prev ? row_num - 1 : row_num;
+    a.row_off = prev ? 1 : 0;
+    a.nblocks = nblocks;
+    a.src[0] = S + (pl ? o_luma : o_src);
+    a.stride[0] = pl ? (int64_t)LP : (int64_t)P;
+    a.src[pl] = S + o_src;
+    a.dst[pl] = S + o_src;
+    a.stride[pl] = (int64_t)P;
+    a.pw[pl] = (int)pw;
+    a.ph[pl] = bh;
+    a.chunks[pl] = (int)((pw + 511) / 512);
+    a.grain[pl] = 1;
+    const int nb = (a.chunks[pl] * bh + 3) / 4;
+    for (int q = 0; q < 4; q++) a.blk_start[q] = q <= pl ? 0 : nb;
+    if (mi::launch_fg_call(a, s)) return -EIO;
+    for (int r = 0; r < bh && !e; r++)
+        if (hipMemcpyAsync((uint8_t *)dst_row + r * stride, S + o_src + r * P, pw * px, hipMemcpyDefault, s) != hipSuccess)
+            e = -EIO;
+    if (hipStreamSynchronize(s) != hipSuccess) return -EIO;
+    return e;
+}
+}  // namespace
+
+int mi_dsp_fg_generate_grain_y(void *buf, const MiFilmGrainData *data, int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || !buf || !data) return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    if (int e = fg_tables()) return e;
+    mi::FgArgs a;
+    memset(&a, 0, sizeof(a));
+    if (int e = fg_read_data(a.data, data)) return e;
+    a.bpc = bpc;
+    static int16_t t[kGH * kGW];
+    if (int e = fg_generate(a, 0, t)) return e;
+    return fg_lut_write(buf, t, bpc);
+}
+
+int mi_dsp_fg_generate_grain_uv(int layout, void *buf, const void *buf_y, const MiFilmGrainData *data, int uv,
+                                int bitdepth_max) {
+    const int bpc = bpc_of(bitdepth_max);
+    if (!bpc || !layout_ok(layout) || !buf || !buf_y || !data || uv < 0 || uv > 1) return -EINVAL;
+    std::lock_guard<std::mutex> lk(g_call.mu);
+    if (int e = g_call.init()) return e;
+    if (int e = fg_tables()) return e;
+    mi::FgArgs a;
+    memset(&a, 0, sizeof(a));
+    if (int e = fg_read_data(a.data, data)) return e;
+    static int16_t ty[kGH * kGW], t[kGH * kGW], out[kGH * kGW];
+    if (int e = fg_lut_read(ty, buf_y, bpc)) return e;
+    int16_t *dly = (int16_t *)(g_call.scratch + kFgLutB + kFgSclB);
+    if (hipMemcpy(dly, ty, sizeof(ty), hipMemcpyHostToDevice) != hipSuccess) return -EIO;
+    a.bpc = bpc;
+    a.layout = layout;
+    a.ss_x = layout != 3;
+    a.ss_y = layout == 1;
+    a.lut_y = dly;
+    a.uv_only = 1 + uv;
+    if (int e = fg_generate(a, 1 + uv, t)) return e;
+    // only the chroma template's own cw x chh corner is written, as the reference does
+    if (int e = fg_lut_read(out, buf, bpc)) return e;
+    const int cw = a.ss_x ? 44 : kGW, chh = a.ss_y ? 38 : kGH;
+    for (int r = 0; r < chh; r++) memcpy(out + r * kGW, t + r * kGW, cw * 2);
+    return fg_lut_write(buf, out, bpc);
+}
+
+int mi_dsp_fgy_32x32xn(void *dst_row, const void *src_row, ptrdiff_t stride, const MiFilmGrainData *data, size_t pw,
+                       const uint8_t *scaling, const void *grain_lut, int bh, int row_num, int bitdepth_max) {
+    return fg_strip(0, 0, dst_row, src_row, stride, data, pw, scaling, grain_lut, bh, row_num, nullptr, 0, 0,
+                    bitdepth_max);
+}
+
+int mi_dsp_fguv_32x32xn(int layout, void *dst_row, const void *src_row, ptrdiff_t stride,
+                        const MiFilmGrainData *data, size_t pw, const uint8_t *scaling, const void *grain_lut, int bh,
+                        int row_num, const void *luma_row, ptrdiff_t luma_stride, int uv_pl, int is_id,
+                        int bitdepth_max) {
+    if (uv_pl < 0 || uv_pl > 1) return -EINVAL;
+    return fg_strip(1 + uv_pl, layout, dst_row, src_row, stride, data, pw, scaling, grain_lut, bh, row_num, luma_row,
+                    luma_stride, is_id, bitdepth_max);
 }
 
 }  // extern "C"

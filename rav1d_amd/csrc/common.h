@@ -253,10 +253,16 @@ struct FgArgs {
     int bpc, layout, ss_x, ss_y, w, h, is_id, nrows, nblocks;
     int pw[3], ph[3], chunks[3], grain[3];
     int blk_start[4];
+    // per-call (table) mode; all zero for frames
+    const int16_t *lut_y;         // generate_grain_uv: the caller's luma template [73][82]; only plane uv_only
+    int uv_only;                  //   1 + uv
+    int row0;                     // block-row number of offsets row 0 (row seeds)
+    int row_off;                  // offsets row of image row 0 (1 when a previous block row overlaps)
 };
 // launchers (fg.hip)
 int init_fg_tables();
 int launch_fg(const FgArgs &a, hipStream_t s, bool prep, bool apply);
+int launch_fg_call(const FgArgs &a, hipStream_t s);
 
 // ---- per-call (table-compatible) entry points: single-block kernels ----
 struct LfCallArgs {

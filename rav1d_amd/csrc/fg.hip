@@ -35,10 +35,10 @@ __device__ __forceinline__ int round2i(int x, int sh) { return (x + ((1 << sh) >
 // Random fill of the grain templates (generate_grain_*: first loop), all planes at once: job j
 // is lane `j - first job of its plane` of that plane's draw sequence. The 24 LFSR states of a
 // job are stepped first, then the 24 table reads issue back to back.
-__device__ void grain_fill_all(int16_t (*lut)[kGH][kGW], unsigned seed, int shift, bool uv0, bool uv1,
+__device__ void grain_fill_all(int16_t (*lut)[kGH][kGW], unsigned seed, int shift, bool ly, bool uv0, bool uv1,
                                int cw, int chh) {
     const int nl = kGW * kGH, nc = cw * chh;
-    const int jl = (nl + kDrawsPerLane - 1) / kDrawsPerLane, jc = (nc + kDrawsPerLane - 1) / kDrawsPerLane;
+    const int jl = ly ? (nl + kDrawsPerLane - 1) / kDrawsPerLane : 0, jc = (nc + kDrawsPerLane - 1) / kDrawsPerLane;
     const int jobs = jl + (uv0 ? jc : 0) + (uv1 ? jc : 0);
     for (int j = threadIdx.x; j < jobs; j += kPrepThreads) {
         int pl, lane;
@@ -77,7 +77,7 @@ __device__ void grain_fill_all(int16_t (*lut)[kGH][kGW], unsigned seed, int shif
 // t0 = 1 + max over (r, c) of [last luma step it reads - its own step] steps after the luma
 // one, instead of after the whole luma template (8K10 4:2:0, lag 3: 353 steps, not 526).
 template <int LAG>
-__device__ void grain_ar_all(int16_t (*lut)[kGH][kGW], const MiFilmGrainData &d, bool uv0, bool uv1,
+__device__ void grain_ar_all(int16_t (*lut)[kGH][kGW], const MiFilmGrainData &d, bool ly, bool uv0, bool uv1,
                              int cw, int chh, int subx, int suby, int gmin, int gmax) {
     constexpr int NT = 2 * LAG * LAG + 2 * LAG, skew = LAG + 1;
     const int role = threadIdx.x >> 7, lane = threadIdx.x & 127;   // role: wave-uniform
@@ -86,7 +86,7 @@ __device__ void grain_ar_all(int16_t (*lut)[kGH][kGW], const MiFilmGrainData &d,
 #pragma unroll
     for (int i = 0; i <= NT; i++) coef[i] = cg[i];
     const int gw = role ? cw : kGW, gh = role ? chh : kGH;
-    const bool on = role == 0 || (role == 1 ? uv0 : uv1);
+    const bool on = role == 0 ? ly : role == 1 ? uv0 : uv1;
     const bool own = on && lane < gh - 3;
     const bool lterm = role && d.num_y_points;
     const int shift = (int)d.ar_coeff_shift;
@@ -152,17 +152,21 @@ __global__ __launch_bounds__(kPrepThreads) void fg_prep_kernel(FgArgs a) {
     const int bdm8 = a.bpc - 8;
     const int shift = 4 - bdm8 + d.grain_scale_shift;
     const int gctr = 128 << bdm8;
-    const bool uv0 = a.layout && (d.num_uv_points[0] || d.chroma_scaling_from_luma);
-    const bool uv1 = a.layout && (d.num_uv_points[1] || d.chroma_scaling_from_luma);
+    // per-call generate_grain_uv: one chroma template over the caller's luma template
+    const bool ly = !a.lut_y;
+    const bool uv0 = ly ? a.layout && (d.num_uv_points[0] || d.chroma_scaling_from_luma) : a.uv_only == 1;
+    const bool uv1 = ly ? a.layout && (d.num_uv_points[1] || d.chroma_scaling_from_luma) : a.uv_only == 2;
     const int cw = a.ss_x ? 44 : kGW, chh = a.ss_y ? 38 : kGH;
 
-    grain_fill_all(lut, d.seed, shift, uv0, uv1, cw, chh);
+    grain_fill_all(lut, d.seed, shift, ly, uv0, uv1, cw, chh);
+    if (!ly)
+        for (int i = threadIdx.x; i < kGH * kGW; i += kPrepThreads) (&lut[0][0][0])[i] = a.lut_y[i];
     __syncthreads();
     switch (d.ar_coeff_lag) {
-    case 0: grain_ar_all<0>(lut, d, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
-    case 1: grain_ar_all<1>(lut, d, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
-    case 2: grain_ar_all<2>(lut, d, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
-    default: grain_ar_all<3>(lut, d, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
+    case 0: grain_ar_all<0>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
+    case 1: grain_ar_all<1>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
+    case 2: grain_ar_all<2>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
+    default: grain_ar_all<3>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
     }
     // export templates
     for (int i = threadIdx.x; i < 3 * kGH * kGP; i += kPrepThreads) {
@@ -187,7 +191,7 @@ __global__ __launch_bounds__(kPrepThreads) void fg_prep_kernel(FgArgs a) {
 __global__ __launch_bounds__(256) void fg_offsets_kernel(FgArgs a) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= a.nrows * a.nblocks) return;
-    const int row = i / a.nblocks, b = i - row * a.nblocks;
+    const int b = i % a.nblocks, row = i / a.nblocks + a.row0;
     unsigned s = a.data.seed;
     s ^= (unsigned)(((row * 37 + 178) & 0xFF) << 8);
     s ^= (unsigned)((row * 173 + 105) & 0xFF);
@@ -410,7 +414,7 @@ __global__ __launch_bounds__(256) void fg_apply_kernel(FgArgs a) {
         GrainPos q;
         q.sx = sx; q.sy = sy;
         const int bsh = 32 >> sy, bsw = 32 >> sx;
-        const int row = y >> (5 - sy);
+        const int lrow = y >> (5 - sy), row = lrow + a.row_off;
         q.yy = y & (bsh - 1);
         q.bi = x0 >> (5 - sx);
         q.xx0 = x0 & (bsw - 1);
@@ -420,7 +424,7 @@ __global__ __launch_bounds__(256) void fg_apply_kernel(FgArgs a) {
         q.hx = q.vy = false;
         q.rl = q.rt = q.rtl = 0;
         if (d.overlap_flag) {
-            const int bh = p ? (min(a.h - row * 32, 32) + sy) >> sy : min(a.h - row * 32, 32);
+            const int bh = p ? (min(a.h - lrow * 32, 32) + sy) >> sy : min(a.h - lrow * 32, 32);
             const int ystart = row ? min(2 >> sy, bh) : 0;
             q.hx = q.bi > 0 && q.xx0 == 0;     // blocks are >= 1 px wide: xstart > 0 iff bi > 0
             q.vy = q.yy < ystart;
@@ -498,6 +502,18 @@ int launch_fg(const FgArgs &a, hipStream_t s, bool prep, bool apply) {
         if (nb > 0) hipLaunchKernelGGL(fg_offsets_kernel, dim3((nb + 255) / 256), dim3(256), 0, s, a);
     }
     if (apply && a.blk_start[3] > 0) {
+        if (a.bpc == 8) fg_apply_kernel<uint8_t><<<a.blk_start[3], 256, 0, s>>>(a);
+        else fg_apply_kernel<uint16_t><<<a.blk_start[3], 256, 0, s>>>(a);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// per-call fgy / fguv_32x32xn: the caller's templates and scaling are already in a.lut /
+// a.scaling; draw the block offsets of this row (and the one above) and apply
+int launch_fg_call(const FgArgs &a, hipStream_t s) {
+    const int nb = a.nrows * a.nblocks;
+    if (nb > 0) hipLaunchKernelGGL(fg_offsets_kernel, dim3((nb + 255) / 256), dim3(256), 0, s, a);
+    if (a.blk_start[3] > 0) {
         if (a.bpc == 8) fg_apply_kernel<uint8_t><<<a.blk_start[3], 256, 0, s>>>(a);
         else fg_apply_kernel<uint16_t><<<a.blk_start[3], 256, 0, s>>>(a);
     }

@@ -365,3 +365,81 @@ def test_lr_wiener_sgr(gpu, bpc):
         rc = lib().mi_dsp_lr_sgr(kind, P(got, off), got.strides[0], P(left), P(lpf, 8), w, h, P(prm), edges, bdmax)
         assert rc == 0
         assert np.array_equal(got, ref), ("sgr", kind, it, w, h, edges, np.argwhere(got != ref)[:4])
+
+
+def _fg_sigs(o):
+    I = ctypes.c_int
+    o.oracle_fg_generate_grain_y.argtypes = [_VP, _VP, I]
+    o.oracle_fg_generate_grain_y.restype = None
+    o.oracle_fg_generate_grain_uv.argtypes = [_VP, _VP, _VP, I, I, I, I]
+    o.oracle_fg_generate_grain_uv.restype = None
+    o.oracle_fg_32x32xn.argtypes = [I, I, _VP, _VP, _SS, _VP, I, _VP, _VP, I, I, _VP, _SS, I, I]
+    o.oracle_fg_32x32xn.restype = None
+    return o
+
+
+def _entry(bpc):
+    return np.int8 if bpc == 8 else np.int16
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+def test_fg_generate_grain(gpu, bpc):
+    from rav1d_amd.frame import film_grain_data
+    from rav1d_amd.synth import make_fg_params
+    o = _fg_sigs(_o())
+    rng = np.random.default_rng(1000 + bpc)
+    bdmax = (1 << bpc) - 1
+    for it in range(12):
+        layout = int(rng.integers(1, 4))
+        d = film_grain_data(make_fg_params(rng, layout))
+        ref_y = np.zeros((73, 82), np.int16)
+        o.oracle_fg_generate_grain_y(P(ref_y), ctypes.byref(d), bdmax)
+        got_y = np.zeros((74, 82), _entry(bpc))
+        assert lib().mi_dsp_fg_generate_grain_y(P(got_y), ctypes.byref(d), bdmax) == 0
+        assert np.array_equal(got_y[:73].astype(np.int16), ref_y), ("y", it)
+        sx, sy = int(layout != 3), int(layout == 1)
+        for uv in (0, 1):
+            fill = int(rng.integers(-100, 100))
+            ref = np.full((74, 82), fill, np.int16)
+            o.oracle_fg_generate_grain_uv(P(ref), P(ref_y), ctypes.byref(d), uv, sx, sy, bdmax)
+            got = np.full((74, 82), fill, _entry(bpc))
+            assert lib().mi_dsp_fg_generate_grain_uv(layout, P(got), P(got_y), ctypes.byref(d), uv, bdmax) == 0
+            assert np.array_equal(got.astype(np.int16), ref), ("uv", it, layout, uv)
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+def test_fg_32x32xn(gpu, bpc):
+    from rav1d_amd.frame import film_grain_data
+    from rav1d_amd.synth import make_fg_params
+    o = _fg_sigs(_o())
+    rng = np.random.default_rng(1100 + bpc)
+    bdmax = (1 << bpc) - 1
+    gctr = 128 << (bpc - 8)
+    for it in range(40):
+        layout = int(rng.integers(1, 4))
+        pl = int(rng.integers(0, 3))
+        sx, sy = (int(layout != 3), int(layout == 1)) if pl else (0, 0)
+        d = film_grain_data(make_fg_params(rng, layout))
+        pw = int(rng.choice([int(rng.integers(1, 300)), 1000, 32 >> sx, (32 >> sx) + 1]))
+        bh = int(rng.integers(1, (32 >> sy) + 1))
+        row_num = int(rng.integers(0, 6))
+        is_id = int(rng.integers(0, 2))
+        W = (pw + 63) // 32 * 32
+        src = make_texture(rng, W, bh, bpc)
+        luma = make_texture(rng, 2 * W, bh << sy, bpc)
+        lut = rng.integers(-gctr, gctr, size=(74, 82)).astype(np.int16)
+        scl = rng.integers(0, 256, size=1 << bpc).astype(np.uint8)
+        ref = np.zeros_like(src)
+        o.oracle_fg_32x32xn(pl, layout, P(ref), P(src), src.strides[0], ctypes.byref(d), pw, P(scl), P(lut), bh,
+                            row_num, P(luma), luma.strides[0], is_id, bdmax)
+        got = np.zeros_like(src)
+        glut = lut.astype(_entry(bpc))
+        if pl == 0:
+            rc = lib().mi_dsp_fgy_32x32xn(P(got), P(src), src.strides[0], ctypes.byref(d), pw, P(scl), P(glut), bh,
+                                          row_num, bdmax)
+        else:
+            rc = lib().mi_dsp_fguv_32x32xn(layout, P(got), P(src), src.strides[0], ctypes.byref(d), pw, P(scl),
+                                           P(glut), bh, row_num, P(luma), luma.strides[0], pl - 1, is_id, bdmax)
+        assert rc == 0
+        assert np.array_equal(got[:, :pw], ref[:, :pw]), ("fg", it, pl, layout, pw, bh, row_num,
+                                                           np.argwhere(got[:, :pw] != ref[:, :pw])[:4])
