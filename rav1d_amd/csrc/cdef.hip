@@ -27,6 +27,9 @@ __device__ __forceinline__ int dir_off(int dir, int k, int ts) {
     return k == 0 ? nib(DY0, dir) * ts + nib(DX0, dir) : nib(DY1, dir) * ts + nib(DX1, dir);
 }
 
+#ifndef MI_CDEF_EXP
+#define MI_CDEF_EXP 0
+#endif
 constexpr int kTY = 68, kTS = 72;          // luma tile rows / LDS row stride (int16)
 
 __device__ __forceinline__ int constrain(int diff, int thr, int shift) {
@@ -166,6 +169,72 @@ struct TileLoad {
                 t[r * ts + c] = v[k];
                 if (c) t1[r * ts + c - 1] = v[k];
             }
+        }
+    }
+};
+
+// Vector form of TileLoad: each row of the window is read as 8-sample aligned vectors from
+// x0 - 8 (one 16-B load at 16 bits, 8-B at 8 bits; per-sample checks only for a vector that
+// straddles the frame edge) and written to T as 4 aligned pairs and to T1 (shifted by one) as
+// 3 pairs plus the two end samples: 10 vectors per luma row instead of 68 scalar loads.
+template <typename Px, int ROWS, int COLS>
+struct VecTileLoad {
+    static constexpr int NV = (COLS + 6 + 7) / 8, N = ROWS * NV, IT = (N + 255) / 256;
+    uint32_t w[IT][4];
+    __device__ __forceinline__ void fetch(const uint8_t *src, int64_t stride, int x0, int y0, int fw, int fh) {
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            const int i = threadIdx.x + 256 * k;
+            const int r = i / NV, j = i - r * NV;
+            const int y = y0 - 2 + r, xs = x0 - 8 + 8 * j;
+#pragma unroll
+            for (int q = 0; q < 4; q++) w[k][q] = 0x80008000u;
+            if (i < N && y >= 0 && y < fh) {
+                const Px *row = reinterpret_cast<const Px *>(src + (int64_t)y * stride);
+                if (xs >= 0 && xs + 8 <= fw) {
+                    if constexpr (sizeof(Px) == 2) {
+                        const uint4 v = *reinterpret_cast<const uint4 *>(row + xs);
+                        w[k][0] = v.x; w[k][1] = v.y; w[k][2] = v.z; w[k][3] = v.w;
+                    } else {
+                        const uint2 v = *reinterpret_cast<const uint2 *>(row + xs);
+                        w[k][0] = (v.x & 0xffu) | ((v.x & 0xff00u) << 8);
+                        w[k][1] = ((v.x >> 16) & 0xffu) | ((v.x >> 8) & 0xff0000u);
+                        w[k][2] = (v.y & 0xffu) | ((v.y & 0xff00u) << 8);
+                        w[k][3] = ((v.y >> 16) & 0xffu) | ((v.y >> 8) & 0xff0000u);
+                    }
+                } else if (xs + 8 > 0 && xs < fw) {
+#pragma unroll
+                    for (int e = 0; e < 8; e++) {
+                        const int x = xs + e;
+                        const uint32_t v = x >= 0 && x < fw ? (uint32_t)row[x] : 0x8000u;
+                        w[k][e >> 1] = (w[k][e >> 1] & (e & 1 ? 0xffffu : 0xffff0000u)) | (v << (16 * (e & 1)));
+                    }
+                }
+            }
+        }
+    }
+    __device__ __forceinline__ void store(int16_t *t, int16_t *t1, int ts) const {
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+            const int i = threadIdx.x + 256 * k;
+            if (i >= N) continue;
+            const int r = i / NV, j = i - r * NV;
+            const int c0 = 8 * j - 6;          // window column of sample 0 (even)
+            int16_t *tr = t + r * ts, *t1r = t1 + r * ts;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int c = c0 + 2 * q;
+                if (c >= 0 && c < COLS) *reinterpret_cast<uint32_t *>(tr + c) = w[k][q];
+            }
+            // T1[c - 1] = T[c]: samples (1,2), (3,4), (5,6) as pairs, 0 and 7 alone
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const int c = c0 + 2 * q;
+                if (c >= 0 && c <= COLS - 2)
+                    *reinterpret_cast<uint32_t *>(t1r + c) = (w[k][q] >> 16) | (w[k][q + 1] << 16);
+            }
+            if (c0 - 1 >= 0 && c0 - 1 <= COLS - 2) t1r[c0 - 1] = (int16_t)(w[k][0] & 0xffffu);
+            if (c0 + 6 >= 0 && c0 + 6 <= COLS - 2) t1r[c0 + 6] = (int16_t)(w[k][3] >> 16);
         }
     }
 };
@@ -316,8 +385,11 @@ __device__ __forceinline__ void filter_plane(const int16_t *T, int lane, const i
 
 // One 64x64 luma unit (+ co-located chroma) per 256-lane workgroup. L = layout (0 I400,
 // 1 I420, 2 I422, 3 I444), compile-time so every tile index is a shift or a constant divide.
+#ifndef MI_CDEF_WAVES
+#define MI_CDEF_WAVES 1
+#endif
 template <typename Px, int L>
-__global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
+__global__ __launch_bounds__(256, MI_CDEF_WAVES) void cdef_kernel(CdefArgs a) {
     constexpr int SSH = L == 1 || L == 2, SSV = L == 1;
     constexpr int CW = 64 >> SSH, CH = 64 >> SSV, CTS = CW + 8;
     constexpr int UVW = 8 >> SSH, UVH = 8 >> SSV;
@@ -362,8 +434,16 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
     int uv_sec = uv_lvl & 3; uv_sec += uv_sec == 3; uv_sec <<= bdm8;
 
     {
+#ifndef MI_CDEF_VEC
+#define MI_CDEF_VEC 1
+#endif
+#if MI_CDEF_VEC
+        VecTileLoad<Px, 68, 68> ly;
+        VecTileLoad<Px, CH + 4, CW + 4> lu, lv;
+#else
         TileLoad<Px, 68, 68> ly;
         TileLoad<Px, CH + 4, CW + 4> lu, lv;
+#endif
         ly.fetch(a.src[0], a.stride[0], x0, y0, fwy, fhy);
         if (L && uv_lvl) {
             lu.fetch(a.src[1], a.stride[1], x0 >> SSH, y0 >> SSV, fwc, fhc);
@@ -386,7 +466,11 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
             const unsigned noskip = (unsigned)lf->noskip_mask[by_idx][1] << 16 | lf->noskip_mask[by_idx][0];
             if (noskip & (3u << (bx & 30))) {
                 unsigned var = 0;
+#if MI_CDEF_EXP == 1
+                var = 1000; dir = byl & 7;
+#else
                 if (y_pri || uv_pri) dir = find_dir(ty + (byl * 8 + 2) * kTS + bxl * 8 + 2, kTS, bdm8, &var);
+#endif
                 if (y_pri) {
                     pri = adjust_strength(y_pri, var);
                     if (pri || y_sec) flag |= 1;
@@ -402,6 +486,9 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
     }
     __syncthreads();
 
+#if MI_CDEF_EXP == 2
+    if (bflag[threadIdx.x & 63] != 77) return;
+#endif
     // luma: 2048 pairs, 8 rows of one 8x8 block per lane
     filter_plane<Px, 64, 64, 8, 8, 256, kTS, YN * 2, 1, true>(
         ty, threadIdx.x, bdir, bflag, bpri, y_pri != 0, y_pri, y_sec, a.damping, bdm8, false,

@@ -28,6 +28,9 @@ __constant__ uint8_t k_obmc[64] = {
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
+#ifndef MI_MC_EXP
+#define MI_MC_EXP 0
+#endif
 #ifndef MC_MAX_U
 #define MC_MAX_U 16
 #endif
@@ -154,7 +157,10 @@ __device__ __forceinline__ void predict(const McArgs &a, const int16_t *win, int
 }
 
 template <typename Px>
-__global__ __launch_bounds__(64) void mc_kernel(McArgs a, int g) {
+#ifndef MI_MC_WAVES
+#define MI_MC_WAVES 1
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MI_MC_WAVES))) void mc_kernel(McArgs a, int g) {
     __shared__ __attribute__((aligned(16))) int16_t win[2][kWinElems];
     const int lane = threadIdx.x;
 #ifndef MI_MC_XCD_CHUNK
@@ -256,6 +262,9 @@ __global__ __launch_bounds__(64) void mc_kernel(McArgs a, int g) {
                 const int yy = min(max(r.dy + rr, 0), r.ih - 1);
                 const int x0 = r.dx + 4 * qq;
                 const uint8_t *row = r.base + (int64_t)yy * r.stride;
+#if MI_MC_EXP == 1
+                if (true) { v0[k] = (uint32_t)ec; v1[k] = (uint32_t)rr; } else
+#endif
                 if (inside) {
                     if (sizeof(Px) == 2) {
                         const U2a q = *reinterpret_cast<const U2a *>(row + 2 * x0);
@@ -320,7 +329,11 @@ __global__ __launch_bounds__(64) void mc_kernel(McArgs a, int g) {
         }
 #pragma unroll
         for (int q = 0; q < 8; q++)
+#if MI_MC_EXP == 2
+            if (q < R && o0[q] == -12345) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];
+#else
             if (q < R) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];
+#endif
         return;
     }
     predict<true>(a, win[0] + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
@@ -375,7 +388,11 @@ __global__ __launch_bounds__(64) void mc_kernel(McArgs a, int g) {
     }
 #pragma unroll
     for (int q = 0; q < 8; q++)
+#if MI_MC_EXP == 2
+        if (q < R && o0[q] == -12345) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];
+#else
         if (q < R) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];
+#endif
 }
 
 // Waves per class for one plane group: packed small units or one wave per 64-lane tile.

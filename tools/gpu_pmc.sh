@@ -15,6 +15,8 @@ PASSES=("FETCH_SIZE" "WRITE_SIZE" \
         "SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES GRBM_GUI_ACTIVE")
 # TRAFFIC_ONLY=1: just the two HBM byte passes
 [ -n "$TRAFFIC_ONLY" ] && PASSES=("FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B")
+# SQ_ONLY=1: just the two issue/stall passes
+[ -n "$SQ_ONLY" ] && PASSES=("${PASSES[@]:2}") && i=2
 for P in "${PASSES[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $OUT/$TAG/p$i -o p -- \
