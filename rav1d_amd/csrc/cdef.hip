@@ -30,6 +30,9 @@ __device__ __forceinline__ int dir_off(int dir, int k, int ts) {
 #ifndef MI_CDEF_EXP
 #define MI_CDEF_EXP 0
 #endif
+#ifndef MI_CDEF_CPAD
+#define MI_CDEF_CPAD 8
+#endif
 constexpr int kTY = 68, kTS = 72;          // luma tile rows / LDS row stride (int16)
 
 __device__ __forceinline__ int constrain(int diff, int thr, int shift) {
@@ -98,6 +101,51 @@ __device__ int find_dir(const int16_t *t, int ts, int bdm8, unsigned *var) {
         if (cost[n] > bc) { bc = cost[n]; best = n; }
     *var = (bc - cost[best ^ 4]) >> 10;
     return best;
+}
+
+// find_dir split by direction pair over the workgroup's four waves (cdef.rs:921-1031): wave
+// PAIR takes directions 2 PAIR and 2 PAIR + 1 of the 64 blocks (lane = block), so each lane
+// keeps two partial-sum arrays instead of eight and all four waves share the search.
+template <int PAIR>
+__device__ __forceinline__ void dir_costs(const int16_t *t, int ts, int bdm8, unsigned &ca, unsigned &cb) {
+    constexpr int NA = PAIR == 1 || PAIR == 3 ? 8 : 15;
+    int a[NA] = {}, b[11] = {};
+#pragma unroll
+    for (int y = 0; y < 8; y++) {
+#pragma unroll
+        for (int x = 0; x < 8; x += 2) {
+            const uint32_t pr = *reinterpret_cast<const uint32_t *>(t + y * ts + x);
+            const int p0 = ((int)(int16_t)(pr & 0xffffu) >> bdm8) - 128, p1 = ((int)(int16_t)(pr >> 16) >> bdm8) - 128;
+            const int pp[2] = { p0, p1 };
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const int xx = x + e, p = pp[e];
+                if (PAIR == 0) { a[y + xx] += p; b[y + (xx >> 1)] += p; }
+                if (PAIR == 1) { a[y] += p; b[3 + y - (xx >> 1)] += p; }
+                if (PAIR == 2) { a[7 + y - xx] += p; b[3 - (y >> 1) + xx] += p; }
+                if (PAIR == 3) { a[xx] += p; b[(y >> 1) + xx] += p; }
+            }
+        }
+    }
+    const unsigned dv[7] = { 840, 420, 280, 210, 168, 140, 120 };
+    unsigned c = 0;
+    if (NA == 8) {
+#pragma unroll
+        for (int n = 0; n < 8; n++) c += (unsigned)(a[n] * a[n]);
+        c *= 105;
+    } else {
+#pragma unroll
+        for (int n = 0; n < 7; n++) c += (unsigned)(a[n] * a[n] + a[14 - n] * a[14 - n]) * dv[n];
+        c += (unsigned)(a[7] * a[7]) * 105;
+    }
+    ca = c;
+    c = 0;
+#pragma unroll
+    for (int m = 0; m < 5; m++) c += (unsigned)(b[3 + m] * b[3 + m]);
+    c *= 105;
+#pragma unroll
+    for (int m = 0; m < 3; m++) c += (unsigned)(b[m] * b[m] + b[10 - m] * b[10 - m]) * dv[2 * m + 1];
+    cb = c;
 }
 
 // Filter one pixel at LDS position (x, y); c = centre sample. Returns the new value.
@@ -391,7 +439,7 @@ __device__ __forceinline__ void filter_plane(const int16_t *T, int lane, const i
 template <typename Px, int L>
 __global__ __launch_bounds__(256, MI_CDEF_WAVES) void cdef_kernel(CdefArgs a) {
     constexpr int SSH = L == 1 || L == 2, SSV = L == 1;
-    constexpr int CW = 64 >> SSH, CH = 64 >> SSV, CTS = CW + 8;
+    constexpr int CW = 64 >> SSH, CH = 64 >> SSV, CTS = CW + MI_CDEF_CPAD;
     constexpr int UVW = 8 >> SSH, UVH = 8 >> SSV;
     constexpr int YN = kTY * kTS, CN = L ? (CH + 4) * CTS : 2;
     __shared__ int16_t ty[2 * YN];                 // T, T1
@@ -399,6 +447,7 @@ __global__ __launch_bounds__(256, MI_CDEF_WAVES) void cdef_kernel(CdefArgs a) {
     __shared__ int8_t bdir[64];
     __shared__ int8_t bflag[64];          // bit0 luma filtered, bit1 chroma filtered
     __shared__ int16_t bpri[64];
+    __shared__ unsigned dcost[8][64];     // find_dir costs per direction and block
 
     const int bid = xcd_block(blockIdx.x, gridDim.x);
     const int tx = bid % a.tiles_x, tyy = bid / a.tiles_x;
@@ -457,6 +506,24 @@ __global__ __launch_bounds__(256, MI_CDEF_WAVES) void cdef_kernel(CdefArgs a) {
     }
     __syncthreads();
 
+#ifndef MI_CDEF_DIR4
+#define MI_CDEF_DIR4 1
+#endif
+#if MI_CDEF_DIR4
+    if (y_pri || uv_pri) {
+        const int b = threadIdx.x & 63, w = threadIdx.x >> 6;   // wave-uniform direction pair
+        const int16_t *tb = ty + ((b >> 3) * 8 + 2) * kTS + (b & 7) * 8 + 2;
+        unsigned ca, cb;
+        if (w == 0) dir_costs<0>(tb, kTS, bdm8, ca, cb);
+        else if (w == 1) dir_costs<1>(tb, kTS, bdm8, ca, cb);
+        else if (w == 2) dir_costs<2>(tb, kTS, bdm8, ca, cb);
+        else dir_costs<3>(tb, kTS, bdm8, ca, cb);
+        dcost[2 * w][b] = ca;
+        dcost[2 * w + 1][b] = cb;
+        __syncthreads();
+    }
+#endif
+
     if (threadIdx.x < 64) {
         const int b = threadIdx.x, bxl = b & 7, byl = b >> 3;
         const int bx = (x0 >> 2) + bxl * 2, by = (y0 >> 2) + byl * 2;   // 4-px units
@@ -468,6 +535,14 @@ __global__ __launch_bounds__(256, MI_CDEF_WAVES) void cdef_kernel(CdefArgs a) {
                 unsigned var = 0;
 #if MI_CDEF_EXP == 1
                 var = 1000; dir = byl & 7;
+#elif MI_CDEF_DIR4
+                if (y_pri || uv_pri) {
+                    unsigned bc = dcost[0][b];
+#pragma unroll
+                    for (int n = 1; n < 8; n++)
+                        if (dcost[n][b] > bc) { bc = dcost[n][b]; dir = n; }
+                    var = (bc - dcost[dir ^ 4][b]) >> 10;
+                }
 #else
                 if (y_pri || uv_pri) dir = find_dir(ty + (byl * 8 + 2) * kTS + bxl * 8 + 2, kTS, bdm8, &var);
 #endif
