@@ -95,6 +95,72 @@ __device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, u
     }
 }
 
+#ifndef MI_LR_AB2
+#define MI_LR_AB2 1
+#endif
+#if MI_LR_AB2
+// Column-pair form of sgr_ab: lane (g, cp) owns positions x = 2cp - 2 and x + 1 (x even, so
+// the six window samples x-2 .. x+3 are three aligned 32-bit LDS reads per row serving both
+// columns' horizontal sums, instead of 2 x (2R+1) 16-bit reads). 34 pairs x 15 row groups.
+template <int R>
+__device__ void sgr_ab2(const int16_t *win, int *A, int16_t *B, int sh, int tw, unsigned s, int bdm8,
+                        const uint8_t *xbyx) {
+    constexpr int n = (2 * R + 1) * (2 * R + 1);
+    constexpr unsigned one_by_x = n == 25 ? 164 : 455;
+    constexpr int NP = 34, G = kNT / NP;
+    const int g = threadIdx.x / NP, cp = threadIdx.x - g * NP;
+    const int x = 2 * cp - 2;                          // positions x, x + 1 (valid: -1 .. tw)
+    if (g >= G || x > tw) return;
+    const int nrows = sh + 2;
+    const int per = (nrows + G - 1) / G;
+    const int y0 = -1 + g * per, y1 = min(-1 + (g + 1) * per, sh + 1);
+    if (y0 >= y1) return;
+    const uint32_t *col = reinterpret_cast<const uint32_t *>(win + x - 2 + kWX);
+    constexpr int W2 = kLrWin / 2;
+    auto hsum = [&](int yy, int &s0, int &q0, int &s1, int &q1) {
+        const uint32_t *r = col + (yy + 3) * W2;
+        const uint32_t w0 = r[0], w1 = r[1], w2 = r[2];
+        const int v0 = w0 & 0xffff, v1 = w0 >> 16, v2 = w1 & 0xffff, v3 = w1 >> 16, v4 = w2 & 0xffff, v5 = w2 >> 16;
+        if (R == 2) {
+            const int m = v1 + v2 + v3 + v4, mq = v1 * v1 + v2 * v2 + v3 * v3 + v4 * v4;
+            s0 = m + v0; q0 = mq + v0 * v0; s1 = m + v5; q1 = mq + v5 * v5;
+        } else {
+            const int m = v2 + v3, mq = v2 * v2 + v3 * v3;
+            s0 = m + v1; q0 = mq + v1 * v1; s1 = m + v4; q1 = mq + v4 * v4;
+        }
+    };
+    int rs0[2 * R + 1], rq0[2 * R + 1], rs1[2 * R + 1], rq1[2 * R + 1];
+#pragma unroll
+    for (int k = 0; k < 2 * R; k++) hsum(y0 - R + k, rs0[k], rq0[k], rs1[k], rq1[k]);
+    const bool c0 = x >= -1, c1 = x + 1 <= tw;
+    for (int y = y0; y < y1; y++) {
+        hsum(y + R, rs0[2 * R], rq0[2 * R], rs1[2 * R], rq1[2 * R]);
+        if (R == 1 || !((y + 1) & 1)) {
+            int sum0 = 0, sq0 = 0, sum1 = 0, sq1 = 0;
+#pragma unroll
+            for (int k = 0; k <= 2 * R; k++) { sum0 += rs0[k]; sq0 += rq0[k]; sum1 += rs1[k]; sq1 += rq1[k]; }
+            const int sums[2] = { sum0, sum1 }, sqs[2] = { sq0, sq1 };
+            const bool on[2] = { c0, c1 };
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const int a = (sqs[e] + ((1 << (2 * bdm8)) >> 1)) >> (2 * bdm8);
+                const int b = (sums[e] + ((1 << bdm8) >> 1)) >> bdm8;
+                const unsigned p = (unsigned)max(a * n - b * b, 0);
+                const unsigned z = (p * s + (1u << 19)) >> 20;
+                const unsigned xv = xbyx[min(z, 255u)];
+                if (on[e]) {
+                    A[(y + 1) * kLrAB + x + e + 1] = (int)((xv * (unsigned)sums[e] * one_by_x + (1u << 11)) >> 12);
+                    B[(y + 1) * kLrAB + x + e + 1] = (int16_t)xv;
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 2 * R; k++) { rs0[k] = rs0[k + 1]; rq0[k] = rq0[k + 1]; rs1[k] = rs1[k + 1]; rq1[k] = rq1[k + 1]; }
+    }
+}
+#define sgr_ab sgr_ab2
+#endif
+
 // Self-guided output terms for rows r0..r0+kNR-1 of column i (looprestoration.rs selfguided_filter
 // tail). The lane walks down its column keeping, per A/B row, the centre value c and the sum of
 // its two horizontal neighbours s in registers: 3 A + 3 B LDS reads per row instead of 9 + 9.
