@@ -215,6 +215,31 @@ __device__ __forceinline__ void sgr_px(const int *A, const int16_t *B, int r0, i
     }
 }
 
+// Wiener horizontal pass (looprestoration.rs:299-335) by column pairs: lane (rg, cp) filters
+// columns 2cp and 2cp + 1 of rows rg, rg + 16, ...: the ten samples x-4 .. x+5 are five aligned
+// 32-bit LDS reads (2.5 per output instead of 7) and the pair is one 32-bit store.
+__device__ __forceinline__ void wiener_hor(const int16_t *win, int16_t *hor, int wr, int tw, const int (&fh)[7],
+                                           int bd, int rbh, int clip_h) {
+    const int cp = threadIdx.x & 31, rg = threadIdx.x >> 5, x = 2 * cp;
+    if (x >= tw) return;
+    for (int rr = rg; rr < wr; rr += kNT / 32) {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(win + rr * kLrWin + x + kWX - 4);
+        int v[10];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const uint32_t q = w[k];
+            v[2 * k] = (int)(int16_t)(q & 0xffffu);
+            v[2 * k + 1] = (int)(int16_t)(q >> 16);
+        }
+        int s0 = 1 << (bd + 6), s1 = s0;
+#pragma unroll
+        for (int t = 0; t < 7; t++) { s0 += v[t + 1] * fh[t]; s1 += v[t + 2] * fh[t]; }
+        const int h0 = min(max((s0 + (1 << (rbh - 1))) >> rbh, 0), clip_h);
+        const int h1 = min(max((s1 + (1 << (rbh - 1))) >> rbh, 0), clip_h);
+        *reinterpret_cast<uint32_t *>(hor + rr * 64 + x) = (uint32_t)(h0 & 0xffff) | ((uint32_t)h1 << 16);
+    }
+}
+
 // 8 pixels as int16 pairs in a uint4 (u16: one 16-B load; u8: one 8-B load widened)
 __device__ __forceinline__ uint32_t pk2(int lo, int hi) { return (uint32_t)(lo & 0xffff) | ((uint32_t)hi << 16); }
 template <typename Px>
@@ -265,15 +290,7 @@ __device__ __forceinline__ void lr_wiener_tile(const int (&fh)[7], const int (&f
     {
         const int rbh = bd == 12 ? 5 : 3, rbv = bd == 12 ? 9 : 11;
         const int clip_h = (1 << (bd + 1 + 7 - rbh)) - 1;
-        if (tx < tw) {
-            for (int rr = ty; rr < wr; rr += kNY) {
-                const int16_t *row = win + rr * kLrWin + tx + kWX - 3;
-                int sum = 1 << (bd + 6);
-#pragma unroll
-                for (int t = 0; t < 7; t++) sum += (int)row[t] * fh[t];
-                hor[rr * 64 + tx] = (int16_t)min(max((sum + (1 << (rbh - 1))) >> rbh, 0), clip_h);
-            }
-        }
+        wiener_hor(win, hor, wr, tw, fh, bd, rbh, clip_h);
         __syncthreads();
         if (tx < tw && r0 < r1) {
             const int off = 1 << (bd + rbv - 1);
@@ -433,15 +450,7 @@ __global__ __launch_bounds__(kNT) void lr_kernel(LrArgs a) {
         fv[3] = 128 - 2 * (fv[0] + fv[1] + fv[2]);
         const int rbh = bd == 12 ? 5 : 3, rbv = bd == 12 ? 9 : 11;
         const int clip_h = (1 << (bd + 1 + 7 - rbh)) - 1;
-        if (tx < tw) {
-            for (int rr = ty; rr < wr; rr += kNY) {
-                const int16_t *row = win + rr * kLrWin + tx + kWX - 3;
-                int sum = 1 << (bd + 6);
-#pragma unroll
-                for (int t = 0; t < 7; t++) sum += (int)row[t] * fh[t];
-                hor[rr * 64 + tx] = (int16_t)min(max((sum + (1 << (rbh - 1))) >> rbh, 0), clip_h);
-            }
-        }
+        wiener_hor(win, hor, wr, tw, fh, bd, rbh, clip_h);
         __syncthreads();
         if (tx < tw && r0 < r1) {
             const int off = 1 << (bd + rbv - 1);
