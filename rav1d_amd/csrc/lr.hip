@@ -240,6 +240,109 @@ __device__ __forceinline__ void wiener_hor(const int16_t *win, int16_t *hor, int
     }
 }
 
+// Self-guided filter tail by column pairs (looprestoration.rs:566-912): lane (rg, cp) owns
+// columns 2cp, 2cp + 1 and rows 4rg .. 4rg + 3. Per A/B row the four entries x-1 .. x+2 are two
+// 32-bit reads of each map (A int, B int16: 3 reads) for both columns instead of 6 per column.
+// Runs both radii as the frame has them and leaves the finished tile in B (row stride 64).
+__device__ __forceinline__ void sgr_pairs(int *A, int16_t *B, const int16_t *win, int sh, int tw, int bdm8, int s0,
+                                          int s1, int w0, int w1, const uint8_t *xbyx, int bdmax) {
+    const int cp = threadIdx.x & 31, rg = threadIdx.x >> 5, x = 2 * cp;
+    const int r0 = rg * 4, r1 = min(r0 + 4, sh);
+    int acc[2][4] = {};
+    // c: centre, s: left + right neighbours, for columns x (e = 0) and x + 1 (e = 1)
+    auto ld = [&](int y, int (&ca)[2], int (&sa)[2], int (&cb)[2], int (&sb)[2]) {
+        const int *ar = A + (y + 1) * kLrAB + x;            // entries x-1 .. x+2 at ar[0..3]
+        const int16_t *br = B + (y + 1) * kLrAB + x;
+        const int2 a01 = *reinterpret_cast<const int2 *>(ar), a23 = *reinterpret_cast<const int2 *>(ar + 2);
+        const uint32_t b01 = *reinterpret_cast<const uint32_t *>(br), b23 = *reinterpret_cast<const uint32_t *>(br + 2);
+        const int bv0 = (int16_t)(b01 & 0xffff), bv1 = (int16_t)(b01 >> 16), bv2 = (int16_t)(b23 & 0xffff),
+                  bv3 = (int16_t)(b23 >> 16);
+        ca[0] = a01.y; sa[0] = a01.x + a23.x; ca[1] = a23.x; sa[1] = a01.y + a23.y;
+        cb[0] = bv1; sb[0] = bv0 + bv2; cb[1] = bv2; sb[1] = bv1 + bv3;
+    };
+    auto src2 = [&](int j, int (&v)[2]) {
+        const uint32_t q = *reinterpret_cast<const uint32_t *>(win + (j + 3) * kLrWin + x + kWX);
+        v[0] = (int16_t)(q & 0xffff); v[1] = (int16_t)(q >> 16);
+    };
+    const bool act = x < tw && r0 < r1;
+    if (s0) {
+        sgr_ab<2>(win, A, B, sh, tw, (unsigned)s0, bdm8, xbyx);
+        __syncthreads();
+        if (act) {
+            // A/B on odd rows: even j uses rows j-1 and j+1, odd j row j (r0 is even)
+            int cau[2], sau[2], cbu[2], sbu[2], cad[2], sad[2], cbd[2], sbd[2];
+            ld(r0 - 1, cau, sau, cbu, sbu);
+#pragma unroll
+            for (int q = 0; q < 4; q += 2) {
+                ld(r0 + q + 1, cad, sad, cbd, sbd);
+                int v[2];
+                if (r0 + q < r1) {
+                    src2(r0 + q, v);
+#pragma unroll
+                    for (int e = 0; e < 2; e++) {
+                        const int a = (cbu[e] + cbd[e]) * 6 + (sbu[e] + sbd[e]) * 5;
+                        const int b = (cau[e] + cad[e]) * 6 + (sau[e] + sad[e]) * 5;
+                        acc[e][q] += w0 * ((b - a * v[e] + (1 << 8)) >> 9);
+                    }
+                }
+                if (r0 + q + 1 < r1) {
+                    src2(r0 + q + 1, v);
+#pragma unroll
+                    for (int e = 0; e < 2; e++) {
+                        const int a = cbd[e] * 6 + sbd[e] * 5;
+                        const int b = cad[e] * 6 + sad[e] * 5;
+                        acc[e][q + 1] += w0 * ((b - a * v[e] + (1 << 7)) >> 8);
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < 2; e++) { cau[e] = cad[e]; sau[e] = sad[e]; cbu[e] = cbd[e]; sbu[e] = sbd[e]; }
+            }
+        }
+        __syncthreads();
+    }
+    if (s1) {
+        sgr_ab<1>(win, A, B, sh, tw, (unsigned)s1, bdm8, xbyx);
+        __syncthreads();
+        if (act) {
+            int c0[2], t0[2], d0[2], u0[2], c1[2], t1[2], d1[2], u1[2], c2[2], t2[2], d2[2], u2[2];
+            ld(r0 - 1, c0, t0, d0, u0);
+            ld(r0, c1, t1, d1, u1);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                ld(r0 + q + 1, c2, t2, d2, u2);
+                if (r0 + q < r1) {
+                    int v[2];
+                    src2(r0 + q, v);
+#pragma unroll
+                    for (int e = 0; e < 2; e++) {
+                        const int a = (d1[e] + u1[e] + d0[e] + d2[e]) * 4 + (u0[e] + u2[e]) * 3;
+                        const int b = (c1[e] + t1[e] + c0[e] + c2[e]) * 4 + (t0[e] + t2[e]) * 3;
+                        acc[e][q] += w1 * ((b - a * v[e] + (1 << 8)) >> 9);
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < 2; e++) {
+                    c0[e] = c1[e]; t0[e] = t1[e]; d0[e] = d1[e]; u0[e] = u1[e];
+                    c1[e] = c2[e]; t1[e] = t2[e]; d1[e] = d2[e]; u1[e] = u2[e];
+                }
+            }
+        }
+    }
+    __syncthreads();   // B (the A/B map) is free: it becomes the output tile
+    if (act) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (r0 + q < r1) {
+                int v[2];
+                src2(r0 + q, v);
+                const int o0 = min(max(v[0] + ((acc[0][q] + (1 << 10)) >> 11), 0), bdmax);
+                const int o1 = min(max(v[1] + ((acc[1][q] + (1 << 10)) >> 11), 0), bdmax);
+                *reinterpret_cast<uint32_t *>(B + (r0 + q) * 64 + x) = (uint32_t)(o0 & 0xffff) | ((uint32_t)o1 << 16);
+            }
+        }
+    }
+}
+
 // 8 pixels as int16 pairs in a uint4 (u16: one 16-B load; u8: one 8-B load widened)
 __device__ __forceinline__ uint32_t pk2(int lo, int hi) { return (uint32_t)(lo & 0xffff) | ((uint32_t)hi << 16); }
 template <typename Px>
@@ -318,37 +421,17 @@ __device__ __forceinline__ void lr_sgr_tile(int s0, int s1, int w0, int w1, int1
     if (threadIdx.x < 256) xbyx[threadIdx.x] = (uint8_t)sgr_x_by_x(threadIdx.x);
     __syncthreads();
     const int bdm8 = bd - 8;
-    int acc[kNR];
-#pragma unroll
-    for (int q = 0; q < kNR; q++) acc[q] = 0;
-    if (s0) {
-        sgr_ab<2>(win, A, B, sh, tw, (unsigned)s0, bdm8, xbyx);
-        __syncthreads();
-        if (tx < tw) sgr_px<2>(A, B, r0, r1, tx, win, w0, acc);
-        __syncthreads();
-    }
-    if (s1) {
-        sgr_ab<1>(win, A, B, sh, tw, (unsigned)s1, bdm8, xbyx);
-        __syncthreads();
-        if (tx < tw) sgr_px<1>(A, B, r0, r1, tx, win, w1, acc);
-    }
-    __syncthreads();   // B (the A/B map) is free: it becomes the output tile
-    if (tx < tw) {
-#pragma unroll
-        for (int q = 0; q < kNR; q++) {
-            if (r0 + q < r1) {
-                const int px = win[(r0 + q + 3) * kLrWin + tx + kWX];
-                B[(r0 + q) * 64 + tx] = (int16_t)min(max(px + ((acc[q] + (1 << 10)) >> 11), 0), bdmax);
-            }
-        }
-    }
+    sgr_pairs(A, B, win, sh, tw, bdm8, s0, s1, w0, w1, xbyx, bdmax);
     __syncthreads();
 }
 
+#ifndef MI_LR_WAVES
+#define MI_LR_WAVES 8   // 64 VGPRs: four 512-lane workgroups per CU (the LDS allows four)
+#endif
 template <typename Px>
-__global__ __launch_bounds__(kNT) void lr_kernel(LrArgs a) {
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES))) void lr_kernel(LrArgs a) {
     __shared__ __attribute__((aligned(16))) int16_t win[70 * kLrWin];
-    __shared__ int A[66 * kLrAB];
+    __shared__ __attribute__((aligned(16))) int A[66 * kLrAB];
     __shared__ __attribute__((aligned(16))) int16_t B[66 * kLrAB];
     int16_t *hor = reinterpret_cast<int16_t *>(A);    // Wiener: [70][64] aliases A
 
@@ -481,30 +564,7 @@ __global__ __launch_bounds__(kNT) void lr_kernel(LrArgs a) {
     const int w0 = u->sgr_weights[0];
     const int w1 = 128 - (u->sgr_weights[0] + u->sgr_weights[1]);
     const int bdm8 = bd - 8;
-    int acc[kNR];
-#pragma unroll
-    for (int q = 0; q < kNR; q++) acc[q] = 0;
-    if (s0) {
-        sgr_ab<2>(win, A, B, sh, tw, (unsigned)s0, bdm8, xbyx);
-        __syncthreads();
-        if (tx < tw) sgr_px<2>(A, B, r0, r1, tx, win, w0, acc);
-        __syncthreads();
-    }
-    if (s1) {
-        sgr_ab<1>(win, A, B, sh, tw, (unsigned)s1, bdm8, xbyx);
-        __syncthreads();
-        if (tx < tw) sgr_px<1>(A, B, r0, r1, tx, win, w1, acc);
-    }
-    __syncthreads();   // B (the A/B map) is free: it becomes the output tile
-    if (tx < tw) {
-#pragma unroll
-        for (int q = 0; q < kNR; q++) {
-            if (r0 + q < r1) {
-                const int px = win[(r0 + q + 3) * kLrWin + tx + kWX];
-                B[(r0 + q) * 64 + tx] = (int16_t)min(max(px + ((acc[q] + (1 << 10)) >> 11), 0), bdmax);
-            }
-        }
-    }
+    sgr_pairs(A, B, win, sh, tw, bdm8, s0, s1, w0, w1, xbyx, bdmax);
     __syncthreads();
     store_tile<Px>(B, O, st, S, sh, x0, tw);
 }
@@ -517,7 +577,7 @@ __global__ __launch_bounds__(kNT) void lr_kernel(LrArgs a) {
 template <typename Px>
 __global__ __launch_bounds__(kNT) void lr_call_kernel(LrCallArgs a) {
     __shared__ __attribute__((aligned(16))) int16_t win[70 * kLrWin];
-    __shared__ int A[66 * kLrAB];
+    __shared__ __attribute__((aligned(16))) int A[66 * kLrAB];
     __shared__ __attribute__((aligned(16))) int16_t B[66 * kLrAB];
     int16_t *hor = reinterpret_cast<int16_t *>(A);
     const int x0 = blockIdx.x * 64, tw = min(64, a.w - x0), h = a.h;
