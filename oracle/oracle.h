@@ -105,6 +105,7 @@ void oracle_lr_sgr(int kind, void *p, ptrdiff_t stride, const void *left_px, con
 
 /* filmgrain.c: per-call table entries */
 void oracle_fg_generate_grain_y(int16_t *buf, const void *data, int bdmax);
+void oracle_fg_generate_scaling(int bitdepth, const uint8_t (*points)[2], int num, uint8_t *scaling);
 void oracle_fg_generate_grain_uv(int16_t *buf, const int16_t *buf_y, const void *data, int uv,
                                  int subx, int suby, int bdmax);
 void oracle_fg_32x32xn(int pl, int layout, void *dst_row, const void *src_row, ptrdiff_t stride, const void *data,

@@ -44,3 +44,38 @@ def test_zero_scaling_is_copy():
     out = oracle_lib.film_grain(planes, bpc, layout, w, h, fg)
     for p in range(3):
         assert np.array_equal(out[p], planes[p])
+
+
+def test_per_call_strips_compose_the_frame():
+    """oracle_fg_32x32xn (the fgy_32x32xn table slot) over every 32-row strip of the luma plane,
+    with the frame's own template and scaling LUT, reproduces oracle_fg_apply's luma plane."""
+    import ctypes
+    from rav1d_amd.frame import film_grain_data
+    w, h, bpc, layout = 150, 90, 10, 1
+    rng = np.random.default_rng(3)
+    planes = pad_planes(planes_for(w, h, bpc, layout, rng), w, h, bpc, layout)
+    fg = make_fg_params(rng, layout)
+    fg.update(overlap_flag=1)
+    ref = oracle_lib.film_grain(planes, bpc, layout, w, h, fg)
+    o = oracle_lib.load_oracle()
+    VP, I = ctypes.c_void_p, ctypes.c_int
+    o.oracle_fg_generate_scaling.argtypes = [I, VP, I, VP]
+    o.oracle_fg_generate_scaling.restype = None
+    o.oracle_fg_32x32xn.argtypes = [I, I, VP, VP, ctypes.c_ssize_t, VP, I, VP, VP, I, I, VP, ctypes.c_ssize_t, I, I]
+    o.oracle_fg_32x32xn.restype = None
+    lut = np.zeros((74, 82), np.int16)
+    lut[:73] = oracle_lib.fg_grain_y(fg, bpc)
+    pts = np.zeros((14, 2), np.uint8)
+    pts[:fg["num_y_points"]] = fg["y_points"]
+    scl = np.zeros(4096, np.uint8)
+    o.oracle_fg_generate_scaling(bpc, oracle_lib.ptr(pts), fg["num_y_points"], oracle_lib.ptr(scl))
+    d = film_grain_data(fg)
+    src = np.ascontiguousarray(planes[0])
+    out = src.copy()
+    for row in range((h + 31) // 32):
+        bh = min(32, h - 32 * row)
+        off = row * 32 * src.shape[1]
+        o.oracle_fg_32x32xn(0, layout, ctypes.c_void_p(out.ctypes.data + 2 * off),
+                            ctypes.c_void_p(src.ctypes.data + 2 * off), src.strides[0], ctypes.byref(d), w,
+                            oracle_lib.ptr(scl), oracle_lib.ptr(lut), bh, row, None, 0, 0, (1 << bpc) - 1)
+    assert np.array_equal(out[:h, :w], ref[0][:h, :w])

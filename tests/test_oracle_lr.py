@@ -68,3 +68,36 @@ def test_restoration_changes_pixels_and_stays_in_range():
     out = oracle_lib.lr_frame(c, d, bpc, layout, w, h, lr)
     assert not np.array_equal(out[0], c[0])
     assert max(int(o.max()) for o in out) <= 1023
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+def test_per_call_identity_filters_leave_unit_unchanged(bpc):
+    """lr.wiener with the identity taps (centre 128, as lr_apply builds it: without the +128 at
+    8 bits) and lr.sgr with zero weights return the unit unchanged for every edge combination,
+    whatever the left / lpf neighbours hold."""
+    import ctypes
+    from rav1d_amd.synth import make_texture
+    o = oracle_lib.load_oracle()
+    VP, I, SS = ctypes.c_void_p, ctypes.c_int, ctypes.c_ssize_t
+    o.oracle_lr_wiener.argtypes = [VP, SS, VP, VP, I, I, VP, I, I]
+    o.oracle_lr_wiener.restype = None
+    o.oracle_lr_sgr.argtypes = [I, VP, SS, VP, VP, I, I, ctypes.c_uint, ctypes.c_uint, I, I, I, I]
+    o.oracle_lr_sgr.restype = None
+    rng = np.random.default_rng(40 + bpc)
+    bdmax = (1 << bpc) - 1
+    f = np.zeros((2, 8), np.int16)
+    f[0, 3] = 0 if bpc == 8 else 128
+    f[1, 3] = 128
+    for edges in range(16):
+        pic = make_texture(rng, 120, 40, bpc)
+        left = make_texture(rng, 4, 24, bpc)
+        lpf = make_texture(rng, 120, 8, bpc)
+        off = 8 * 120 + 8
+        p = ctypes.c_void_p(pic.ctypes.data + off * pic.itemsize)
+        lp = ctypes.c_void_p(lpf.ctypes.data + 8 * lpf.itemsize)
+        before = pic.copy()
+        o.oracle_lr_wiener(p, pic.strides[0], oracle_lib.ptr(left), lp, 97, 24, oracle_lib.ptr(f), edges, bdmax)
+        assert np.array_equal(pic, before), ("wiener", edges)
+        for kind, (s0, s1) in ((0, (140, 0)), (1, (0, 3236)), (2, (140, 3236))):
+            o.oracle_lr_sgr(kind, p, pic.strides[0], oracle_lib.ptr(left), lp, 97, 24, s0, s1, 0, 0, edges, bdmax)
+            assert np.array_equal(pic, before), ("sgr", kind, edges)
