@@ -169,6 +169,7 @@ int fill_mc_args(mi::McArgs &a, const MiPicture *cur, const MiPicture *refs, int
         a.ref_stride[r][0] = refs[r].stride[0];
         a.ref_stride[r][1] = refs[r].stride[1];
     }
+    a.nrefs = nrefs;
     a.bpc = cur->bpc;
     a.ib = cur->bpc == 8 ? 4 : 14 - cur->bpc;
     a.bias = cur->bpc == 8 ? 0 : 8192;

@@ -154,6 +154,7 @@ struct McArgs {
     uint8_t *masks;
     int16_t *tmp;                    // MI_MC_PREP arena
     int bpc, ib, bias, bdmax, layout;
+    int nrefs;                       // valid entries of ref / ref_stride / ref_w / ref_h
     int seg_ss_hor, seg_ss_ver;      // w_mask[chr_layout_idx] subsampling of the SEG mask
     uint32_t class_start[2 * MI_MC_NCLASS + 1];
     uint32_t first_wave[2][MI_MC_NCLASS + 1];
