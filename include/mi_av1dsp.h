@@ -232,6 +232,12 @@ typedef struct MiMcCombine {
 #define MI_INTRA_SMOOTH_NB  16u   /* sm_flag / sm_uv_flag of a neighbour (angle bit 9) */
 #define MI_INTRA_EDGE_FILTER 32u  /* seq_hdr.intra_edge_filter (angle bit 10) */
 #define MI_INTRA_II         64u   /* inter-intra: blend into the pixels with the mask at idx + aux_off */
+#define MI_INTRA_CFL_AC    128u   /* CfL with the AC computed on the device (cfl_ac, ipred.rs:1326-1432)
+                                     from the reconstructed luma under the block, instead of read
+                                     from ac + aux_off: reserved = w_pad | h_pad << 8 | ss_hor << 16 |
+                                     ss_ver << 17 (w, h = cw, ch of cfl_ac). The block's dependencies
+                                     (mi_intra_recon deps / its level) must include the luma blocks
+                                     that own the pixels it reads. */
 typedef struct MiIntraBlock {
     uint16_t x, y;          /* plane pixels */
     uint8_t  w, h;          /* transform size, pixels (4..64) */
@@ -247,7 +253,7 @@ typedef struct MiIntraBlock {
     uint16_t max_w, max_h;  /* intra_pred's max_width / max_height */
     uint32_t aux_off;       /* CfL: int16 index into ac; PAL: byte index into idx; II: mask byte index */
     uint32_t pal_off;       /* PAL: pixel index of the block's 8-entry palette in `pal` */
-    uint32_t reserved;
+    uint32_t reserved;      /* MI_INTRA_CFL_AC: w_pad | h_pad << 8 | ss_hor << 16 | ss_ver << 17; else 0 */
 } MiIntraBlock;
 
 #define MI_IPRED_II 128    /* mode flag: inter-intra, blend the prediction into the existing

@@ -517,7 +517,17 @@ void oracle_intra_blocks(void *const planes[3], const ptrdiff_t strides[2], int 
             const int m = oracle_prepare_intra_edges(b->x, b->flags & 1, b->y, (b->flags >> 1) & 1, b->tile_w, b->tile_h,
                                                      (b->flags >> 2) & 1, (b->flags >> 3) & 1, planes[b->plane], st,
                                                      cfl ? 0 : b->mode, &angle, b->w, b->h, (b->flags >> 5) & 1, tl, bpc);
-            if (cfl) {
+            if (cfl && (b->flags & 128)) {
+                /* MI_INTRA_CFL_AC: cfl_ac over the reconstructed luma under the block
+                 * (recon.rs:2735-2800: the AC is taken from the luma just reconstructed) */
+                int16_t acd[32 * 32];
+                const int ssh = (b->reserved >> 16) & 1, ssv = (b->reserved >> 17) & 1;
+                const uint8_t *yp = (const uint8_t *)planes[0] + (ptrdiff_t)(b->y << ssv) * strides[0] +
+                                    (ptrdiff_t)(b->x << ssh) * pb;
+                oracle_cfl_ac(acd, yp, strides[0], b->reserved & 0xff, (b->reserved >> 8) & 0xff, b->w, b->h, ssh, ssv,
+                              bpc);
+                oracle_cfl_pred(m, out, ost, tl, b->w, b->h, acd, b->alpha, bpc);
+            } else if (cfl) {
                 oracle_cfl_pred(m, out, ost, tl, b->w, b->h, ac + b->aux_off, b->alpha, bpc);
             } else {
                 const int aw = m == 13 ? b->filt_idx : angle | ((b->flags & 16) ? 512 : 0) | ((b->flags & 32) ? 1024 : 0);

@@ -83,7 +83,7 @@ INTRA_DTYPE = np.dtype([("x", "<u2"), ("y", "<u2"), ("w", "u1"), ("h", "u1"), ("
                         ("pal_off", "<u4"), ("reserved", "<u4")])
 assert INTRA_DTYPE.itemsize == 32
 INTRA_HAVE_LEFT, INTRA_HAVE_TOP, INTRA_TOP_RIGHT, INTRA_BOTTOM_LEFT = 1, 2, 4, 8
-INTRA_SMOOTH_NB, INTRA_EDGE_FILTER, INTRA_II = 16, 32, 64
+INTRA_SMOOTH_NB, INTRA_EDGE_FILTER, INTRA_II, INTRA_CFL_AC = 16, 32, 64, 128
 
 MC_AVG, MC_WAVG, MC_MASK, MC_SEG = 0, 1, 2, 3
 MC_OBMC_H, MC_OBMC_V, MC_PREP = 4, 5, 6

@@ -91,7 +91,7 @@ __device__ void upsample_edge_par(int *out, int hsz, const Px *in_, int from, in
 // scratch for the directional edge and the filter-intra image.
 template <typename Px, bool ToLds = false>
 __device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredBlock &b, const Px *tl, int *eb, Px *ft,
-                                              Px *lt = nullptr) {
+                                              Px *lt = nullptr, const int16_t *acl = nullptr) {
     const int lane = threadIdx.x;
     const int w = b.w, h = b.h, n = w * h;
     const int64_t st = a.stride[b.plane ? 1 : 0];
@@ -145,7 +145,7 @@ __device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredB
         if (!cfl) {
             for (int i = lane; i < n; i += 64) put(i / w, i % w, dc);
         } else {
-            const int16_t *ac = a.ac + b.aux_off;
+            const int16_t *ac = acl ? acl : a.ac + b.aux_off;
             const int alpha = b.alpha;
             for (int i = lane; i < n; i += 64) {
                 const int diff = alpha * ac[i];
@@ -351,13 +351,50 @@ __global__ __launch_bounds__(64) void ipred_kernel(IpredArgs a) {
 __constant__ uint8_t k_needs[14] = { 3, 2, 1, 1, 2, 0, 14, 7, 21, 3, 3, 3, 7, 7 };
 __constant__ uint8_t k_mode_angle[8] = { 90, 180, 45, 135, 113, 157, 203, 67 };
 
+// cfl_ac (ipred.rs:1326-1432; C ipred_tmpl.c:658-700) by one wave: each AC sample is the sum
+// of its 1/2/4 luma pixels scaled to <<3 in total, w_pad / h_pad 4-px groups replicate the last
+// real column / row, then the rounded mean is subtracted. Lane i % 64 owns sample i, so the
+// caller's reads of ac need no barrier. Sc1: the luma was stored during this launch (fused
+// reconstruction), read past L1.
+template <typename Px, bool Sc1>
+__device__ __forceinline__ void cfl_ac_wave(int16_t *ac, const uint8_t *ybase, int64_t stride, int w_pad, int h_pad,
+                                            int cw, int ch, int ss_hor, int ss_ver) {
+    const int lane = threadIdx.x & 63;
+    const int rw = cw - 4 * w_pad, rh = ch - 4 * h_pad;   // real (unpadded) extent
+    const int64_t ps = stride / (int64_t)sizeof(Px);
+    const Px *y = reinterpret_cast<const Px *>(ybase);
+    auto L = [&](int64_t o) -> int {
+        if constexpr (Sc1) return __hip_atomic_load(y + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else return y[o];
+    };
+    const int sh = 1 + !ss_ver + !ss_hor;
+    int sum = 0;
+    for (int i = lane; i < cw * ch; i += 64) {
+        const int r = min(i / cw, rh - 1), c = min(i % cw, rw - 1);
+        const int yy = r << ss_ver, xx = c << ss_hor;
+        int s = L(yy * ps + xx);
+        if (ss_hor) s += L(yy * ps + xx + 1);
+        if (ss_ver) {
+            s += L((yy + 1) * ps + xx);
+            if (ss_hor) s += L((yy + 1) * ps + xx + 1);
+        }
+        s <<= sh;
+        ac[i] = (int16_t)s;
+        sum += s;
+    }
+    sum = wave_sum(sum);
+    const int log2sz = __ffs(cw) - 1 + __ffs(ch) - 1;
+    const int mean = (sum + ((1 << log2sz) >> 1)) >> log2sz;
+    for (int i = lane; i < cw * ch; i += 64) ac[i] = (int16_t)(ac[i] - mean);
+}
+
 // Gather one block's edges from the picture (rav1d_prepare_intra_edges) and predict it, one
 // wave. Fused (the persistent reconstruction kernel): neighbour pixels were stored by other
 // CUs of this XCD during the launch, so every picture read is an L1-bypassing `sc1` load
 // (L2-served), and the prediction goes to the LDS tile lt.
 template <typename Px, bool Fused>
 __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlock &ib, int *eb, Px *ft, Px *edge,
-                                            Px *lt) {
+                                            Px *lt, int16_t *acl) {
     const int lane = threadIdx.x;
     const int w = ib.w, h = ib.h, x = ib.x, y = ib.y;
     const bool have_left = ib.flags & MI_INTRA_HAVE_LEFT, have_top = ib.flags & MI_INTRA_HAVE_TOP;
@@ -457,6 +494,14 @@ __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlo
     b.mode = (uint8_t)((cfl ? MI_IPRED_CFL + m : m) | ii);
     b.angle = (uint16_t)(angle | (ib.flags & MI_INTRA_SMOOTH_NB ? 512 : 0) | (ib.flags & MI_INTRA_EDGE_FILTER ? 1024 : 0));
     if (m == 13) b.angle = (uint16_t)ib.filt_idx;
+    if (cfl && (ib.flags & MI_INTRA_CFL_AC)) {
+        // the AC from the reconstructed luma under the block (its dependencies made it final)
+        const int ssh = (ib.reserved >> 16) & 1, ssv = (ib.reserved >> 17) & 1;
+        const uint8_t *yb = a.dst[0] + (int64_t)(y << ssv) * a.stride[0] + (int64_t)(x << ssh) * sizeof(Px);
+        cfl_ac_wave<Px, Fused>(acl, yb, a.stride[0], ib.reserved & 0xff, (ib.reserved >> 8) & 0xff, w, h, ssh, ssv);
+        predict_block<Px, Fused>(a, b, tl, eb, ft, lt, acl);
+        return;
+    }
     predict_block<Px, Fused>(a, b, tl, eb, ft, lt);
 }
 
@@ -465,7 +510,8 @@ __global__ __launch_bounds__(64) void intra_kernel(IpredArgs a) {
     __shared__ int eb[2 * 128 + 2];
     __shared__ Px ft[32 * 32];
     __shared__ Px edge[2 * 128 + 1];           // topleft at [128]
-    intra_block<Px, false>(a, a.iblocks[blockIdx.x], eb, ft, edge, nullptr);
+    __shared__ int16_t acl[32 * 32];           // MI_INTRA_CFL_AC
+    intra_block<Px, false>(a, a.iblocks[blockIdx.x], eb, ft, edge, nullptr, acl);
 }
 
 // ---- persistent fused intra reconstruction (mi_intra_recon) ----
@@ -586,6 +632,7 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
     __shared__ int eb[2 * 128 + 2];
     __shared__ Px ft[32 * 32];
     __shared__ Px edge[2 * 128 + 1];
+    __shared__ int16_t acl[32 * 32];           // MI_INTRA_CFL_AC
     __shared__ __attribute__((aligned(16))) Px lt[64 * 64];
     __shared__ Lt tmp[32 * 65];
     const unsigned xcc = xcc_id();
@@ -645,7 +692,7 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
         }
         __syncthreads();
         DBG(i, 2);
-        intra_block<Px, true>(fr.ip, ib, eb, ft, edge, lt);
+        intra_block<Px, true>(fr.ip, ib, eb, ft, edge, lt, acl);
         __syncthreads();
         DBG(i, 3);
         switch (tb.tx) {
@@ -700,29 +747,7 @@ int launch_intra_recon(const IntraReconArgs &a, int bpc, int wg_per_xcd, hipStre
 // column / row, then the rounded mean subtracted. One wave, the mean by a wave reduction.
 template <typename Px>
 __global__ __launch_bounds__(64) void cfl_ac_kernel(CflAcArgs a) {
-    const int lane = threadIdx.x, cw = a.cw, ch = a.ch;
-    const int rw = cw - 4 * a.w_pad, rh = ch - 4 * a.h_pad;   // real (unpadded) extent
-    const int64_t ps = a.stride / (int64_t)sizeof(Px);
-    const Px *y = reinterpret_cast<const Px *>(a.y);
-    const int sh = 1 + !a.ss_ver + !a.ss_hor;
-    int sum = 0;
-    for (int i = lane; i < cw * ch; i += 64) {
-        const int r = min(i / cw, rh - 1), c = min(i % cw, rw - 1);
-        const int yy = r << a.ss_ver, xx = c << a.ss_hor;
-        int s = y[yy * ps + xx];
-        if (a.ss_hor) s += y[yy * ps + xx + 1];
-        if (a.ss_ver) {
-            s += y[(yy + 1) * ps + xx];
-            if (a.ss_hor) s += y[(yy + 1) * ps + xx + 1];
-        }
-        s <<= sh;
-        a.ac[i] = (int16_t)s;
-        sum += s;
-    }
-    sum = wave_sum(sum);
-    const int log2sz = __ffs(cw) - 1 + __ffs(ch) - 1;
-    const int mean = (sum + ((1 << log2sz) >> 1)) >> log2sz;
-    for (int i = lane; i < cw * ch; i += 64) a.ac[i] = (int16_t)(a.ac[i] - mean);
+    cfl_ac_wave<Px, false>(a.ac, a.y, a.stride, a.w_pad, a.h_pad, a.cw, a.ch, a.ss_hor, a.ss_ver);
 }
 
 int launch_cfl_ac(const CflAcArgs &a, int bpc, hipStream_t s) {

@@ -66,7 +66,7 @@ def make_ipred_blocks(n, bpc, rng, sizes=SIZES, modes=None, plane_w=4096):
 
 
 def make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.5, pal_frac=0.05, cfl_frac=0.4,
-                     filter_frac=0.1, ii_frac=0.0, edge_filter=None):
+                     filter_frac=0.1, ii_frac=0.0, edge_filter=None, cfl_dev_frac=0.5):
     """A whole intra frame as MiIntraBlock transform blocks in decode order (blocks in quadtree
     z-order, luma then U then V per block, transform blocks raster within a block), with the
     edge-availability flags a decoder would pass (top-right / bottom-left only where those
@@ -74,7 +74,9 @@ def make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.5, pal_
     the blocks owning any pixel its edges may read). Returns dict(blocks (decode order),
     order (indices sorted by level), level_start, ac, idx, pal, deps (per block, decode-order
     indices of those owners)). Single tile; w, h multiples
-    of 64."""
+    of 64. A cfl_dev_frac share of the CfL blocks up to 32x32 take MI_INTRA_CFL_AC (the AC is
+    computed on the device from the reconstructed luma; its owners join the dependencies), with
+    random cfl_ac padding."""
     from . import (INTRA_BOTTOM_LEFT, INTRA_DTYPE, INTRA_EDGE_FILTER, INTRA_HAVE_LEFT, INTRA_HAVE_TOP, INTRA_II,
                    INTRA_SMOOTH_NB, INTRA_TOP_RIGHT)
     from .synth import partition_blocks
@@ -115,8 +117,22 @@ def make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.5, pal_
                     if tx > 0 and ty + th < ph and (own[ty + th:min(ty + 2 * th, ph), tx - 1] >= 0).all() \
                             and rng.random() < 0.85:
                         flags |= INTRA_BOTTOM_LEFT
+                    # CfL with the AC from the reconstructed luma (decided before the dependencies)
+                    r = rng.random()
+                    cfl_dev = bool(pl and pal_frac <= r < pal_frac + cfl_frac and tw <= 32 and th <= 32
+                                   and rng.random() < cfl_dev_frac)
+                    reserved = 0
                     # dependency level from every pixel the edge may read
                     deps = []
+                    if cfl_dev:
+                        wp = int(rng.integers(0, tw // 4)) if rng.random() < 0.3 else 0
+                        hp = int(rng.integers(0, th // 4)) if rng.random() < 0.3 else 0
+                        reserved = wp | (hp << 8) | (ss_h << 16) | (ss_v << 17)
+                        flags |= 128
+                        ly0, lx0 = ty << ss_v, tx << ss_h
+                        ly1 = ly0 + ((th - 4 * hp) << ss_v)
+                        lx1 = lx0 + ((tw - 4 * wp) << ss_h)
+                        deps.append(owner[0][ly0:ly1, lx0:lx1].ravel())
                     if tx > 0:
                         deps.append(own[ty:min(ty + 2 * th, ph), tx - 1])
                     if ty > 0:
@@ -128,7 +144,6 @@ def make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.5, pal_
                         lv = 1 + max(level_of[i] for i in dep_ids)
                     dep_lists.append(dep_ids)
                     mode, angle, filt, alpha, aux, poff = 0, 0, 0, 0, 0, 0
-                    r = rng.random()
                     if r < pal_frac:
                         mode = 64
                         pal.append(rng.integers(0, 1 << bpc, size=8).astype(dt))
@@ -152,7 +167,7 @@ def make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.5, pal_
                             aux, n_idx = n_idx, n_idx + tw * th
                     k = len(recs)
                     recs.append((tx, ty, tw, th, pl, mode, angle, flags, filt, alpha, pw, ph, pw - tx, ph - ty,
-                                 aux, poff, 0))
+                                 aux, poff, reserved))
                     level_of.append(lv)
                     own[ty:ty + th, tx:tx + tw] = k
     blocks = np.array(recs, dtype=INTRA_DTYPE)
