@@ -98,17 +98,42 @@ __device__ void grain_ar_all(int16_t (*lut)[kGH][kGW], const MiFilmGrainData &d,
     const int tstart = role ? t0 : 0;
     int16_t *buf = &lut[role][0][0];
     const int y = 3 + lane;
+    // The lane's neighbourhood slides one column per step: rows y-LAG .. y-1 over columns
+    // x-LAG .. x+LAG and its own row's last LAG outputs live in registers, so a step reads
+    // only the new column x+LAG of the rows above (final: those rows run skew = LAG+1 columns
+    // ahead) instead of all NT neighbours.
+    constexpr int WA = LAG ? LAG : 1, WC = 2 * LAG + 1;
+    int wv[WA][WC], cv[WA];
+    bool primed = false;
     for (int t = 0; t < steps; t++) {
         const int x = 3 + (t - tstart) - skew * lane;
         if (own && x >= 3 && x < gw - 3) {
             const int16_t *p = buf + y * kGW + x;
+            if constexpr (LAG > 0) {
+                if (!primed) {
+#pragma unroll
+                    for (int r = 0; r < LAG; r++)
+#pragma unroll
+                        for (int c = 0; c < WC; c++) wv[r][c] = p[(r - LAG) * kGW + c - LAG];
+#pragma unroll
+                    for (int c = 0; c < LAG; c++) cv[c] = p[c - LAG];
+                    primed = true;
+                } else {
+#pragma unroll
+                    for (int r = 0; r < LAG; r++) {
+#pragma unroll
+                        for (int c = 0; c < WC - 1; c++) wv[r][c] = wv[r][c + 1];
+                        wv[r][WC - 1] = p[(r - LAG) * kGW + LAG];
+                    }
+                }
+            }
             int sum = 0, ci = 0;
 #pragma unroll
             for (int dy = -LAG; dy <= 0; dy++)
 #pragma unroll
                 for (int dx = -LAG; dx <= LAG; dx++) {
                     if (dy == 0 && dx == 0) break;
-                    sum += coef[ci++] * p[dy * kGW + dx];
+                    sum += coef[ci++] * (dy < 0 ? wv[dy + LAG][dx + LAG] : cv[dx + LAG]);
                 }
             if (lterm) {
                 const int lx = ((x - 3) << subx) + 3, ly = ((y - 3) << suby) + 3;
@@ -118,8 +143,13 @@ __device__ void grain_ar_all(int16_t (*lut)[kGH][kGW], const MiFilmGrainData &d,
                 if (suby) { l += q[kGW]; if (subx) l += q[kGW + 1]; }
                 sum += round2i(l, subx + suby) * coef[NT];
             }
-            const int g = p[0] + round2i(sum, shift);
-            buf[y * kGW + x] = (int16_t)min(max(g, gmin), gmax);
+            const int g = min(max(p[0] + round2i(sum, shift), gmin), gmax);
+            buf[y * kGW + x] = (int16_t)g;
+            if constexpr (LAG > 0) {
+#pragma unroll
+                for (int c = 0; c < LAG - 1; c++) cv[c] = cv[c + 1];
+                cv[LAG - 1] = g;
+            }
         }
         __syncthreads();
     }
