@@ -19,11 +19,11 @@ from pmc_summary import collect  # noqa: E402
 CALIB_BYTES = 1 << 30
 # stage -> (kernel name prefixes, dominant read width, dominant write width in bytes)
 STAGES = {
-    "mc": (["mc_kernel"], 2, 2),                      # per-pixel u16 window gathers
-    "itx": (["itx_frame_kernel"], 8, 2),
+    "mc": (["mc_kernel"], 8, 2),                      # 4-sample (8-B) window quads, per-pixel stores
+    "itx": (["itx_frame_kernel"], 8, 8),              # 4-pixel chunks in and out
     "deblock": (["lf_tile_kernel"], 16, 16),           # uint4 tile staging and stores
-    "cdef": (["cdef_kernel"], 8, 8),                  # uint2 tile rows
-    "lr": (["lr_kernel"], 2, 2),
+    "cdef": (["cdef_kernel"], 16, 4),                 # 8-sample vectors in, pixel pairs out
+    "lr": (["lr_kernel"], 16, 16),                    # 8-pixel vectors in and out
 }
 FRAME_KERNEL = "cdef_kernel"                          # one dispatch per frame: counts the frames
 
