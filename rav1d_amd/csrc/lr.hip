@@ -343,6 +343,35 @@ __device__ __forceinline__ void sgr_pairs(int *A, int16_t *B, const int16_t *win
     }
 }
 
+// Wiener vertical pass (looprestoration.rs:337-370) by column pairs: lane (rg, cp) filters
+// columns 2cp, 2cp + 1 of rows 4rg .. 4rg + 3 from ten 32-bit reads of the horizontal output
+// (one per row, both columns) and stores each output pair as one 32-bit word.
+__device__ __forceinline__ void wiener_ver(const int16_t *hor, int16_t *B, int wr, int sh, int tw, const int (&fv)[7],
+                                           int bd, int rbv, int bdmax) {
+    const int cp = threadIdx.x & 31, rg = threadIdx.x >> 5, x = 2 * cp;
+    const int r0 = rg * 4, r1 = min(r0 + 4, sh);
+    if (x >= tw || r0 >= r1) return;
+    const int off = 1 << (bd + rbv - 1);
+    int h0[10], h1[10];
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+        const uint32_t w = r0 + q < wr ? *reinterpret_cast<const uint32_t *>(hor + (r0 + q) * 64 + x) : 0u;
+        h0[q] = (int)(w & 0xffffu);
+        h1[q] = (int)(w >> 16);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        if (r0 + q < r1) {
+            int s0 = -off, s1 = -off;
+#pragma unroll
+            for (int t = 0; t < 7; t++) { s0 += h0[q + t] * fv[t]; s1 += h1[q + t] * fv[t]; }
+            const int o0 = min(max((s0 + (1 << (rbv - 1))) >> rbv, 0), bdmax);
+            const int o1 = min(max((s1 + (1 << (rbv - 1))) >> rbv, 0), bdmax);
+            *reinterpret_cast<uint32_t *>(B + (r0 + q) * 64 + x) = (uint32_t)(o0 & 0xffff) | ((uint32_t)o1 << 16);
+        }
+    }
+}
+
 // 8 pixels as int16 pairs in a uint4 (u16: one 16-B load; u8: one 8-B load widened)
 __device__ __forceinline__ uint32_t pk2(int lo, int hi) { return (uint32_t)(lo & 0xffff) | ((uint32_t)hi << 16); }
 template <typename Px>
@@ -395,21 +424,7 @@ __device__ __forceinline__ void lr_wiener_tile(const int (&fh)[7], const int (&f
         const int clip_h = (1 << (bd + 1 + 7 - rbh)) - 1;
         wiener_hor(win, hor, wr, tw, fh, bd, rbh, clip_h);
         __syncthreads();
-        if (tx < tw && r0 < r1) {
-            const int off = 1 << (bd + rbv - 1);
-            int h[kNR + 6];
-#pragma unroll
-            for (int q = 0; q < kNR + 6; q++) h[q] = r0 + q < wr ? (int)(uint16_t)hor[(r0 + q) * 64 + tx] : 0;
-#pragma unroll
-            for (int q = 0; q < kNR; q++) {
-                if (r0 + q < r1) {
-                    int sum = -off;
-#pragma unroll
-                    for (int t = 0; t < 7; t++) sum += h[q + t] * fv[t];
-                    B[(r0 + q) * 64 + tx] = (int16_t)min(max((sum + (1 << (rbv - 1))) >> rbv, 0), bdmax);
-                }
-            }
-        }
+        wiener_ver(hor, B, wr, sh, tw, fv, bd, rbv, bdmax);
         __syncthreads();
     }
 }
@@ -535,21 +550,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
         const int clip_h = (1 << (bd + 1 + 7 - rbh)) - 1;
         wiener_hor(win, hor, wr, tw, fh, bd, rbh, clip_h);
         __syncthreads();
-        if (tx < tw && r0 < r1) {
-            const int off = 1 << (bd + rbv - 1);
-            int h[kNR + 6];
-#pragma unroll
-            for (int q = 0; q < kNR + 6; q++) h[q] = r0 + q < wr ? (int)(uint16_t)hor[(r0 + q) * 64 + tx] : 0;
-#pragma unroll
-            for (int q = 0; q < kNR; q++) {
-                if (r0 + q < r1) {
-                    int sum = -off;
-#pragma unroll
-                    for (int t = 0; t < 7; t++) sum += h[q + t] * fv[t];
-                    B[(r0 + q) * 64 + tx] = (int16_t)min(max((sum + (1 << (rbv - 1))) >> rbv, 0), bdmax);
-                }
-            }
-        }
+        wiener_ver(hor, B, wr, sh, tw, fv, bd, rbv, bdmax);
         __syncthreads();
         store_tile<Px>(B, O, st, S, sh, x0, tw);
         return;
