@@ -79,3 +79,40 @@ def test_per_call_strips_compose_the_frame():
                             ctypes.c_void_p(src.ctypes.data + 2 * off), src.strides[0], ctypes.byref(d), w,
                             oracle_lib.ptr(scl), oracle_lib.ptr(lut), bh, row, None, 0, 0, (1 << bpc) - 1)
     assert np.array_equal(out[:h, :w], ref[0][:h, :w])
+
+
+TABLES = {"dr_intra_derivative": 44, "filter_intra_taps": 320, "mc_subpel_filters": 720, "mc_warp_filter": 1544,
+          "obmc_masks": 64, "resize_filter": 512, "sm_weights": 128}
+
+
+@pytest.mark.skipif(not os.path.exists(REF_TABLES), reason="reference not mounted")
+@pytest.mark.parametrize("name", sorted(TABLES))
+def test_kernel_tables_match_reference(name):
+    """Every constant table the HIP kernels and the oracle compile in equals the reference's
+    dav1d_<name> (src/tables.c; the generic-C layout of the filter-intra F() macro,
+    tables.c:753-757), parsed by tools/gen_tables.py, value for value."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gen_tables
+    txt = open(REF_TABLES).read()
+    key = next(k for k in re.findall(r"dav1d_" + name + r"\[[^=]*", txt))
+    fn = gen_tables.filter_intra if name == "filter_intra_taps" else gen_tables.numbers
+    ref = fn(gen_tables.body_of(txt, key.strip()))
+    ours = open(os.path.join(ROOT, "rav1d_amd", "csrc", "tables", f"{name}.inc")).read()
+    ours = [int(v) for v in re.findall(r"-?\d+", re.sub(r"/\*.*?\*/", "", ours, flags=re.S))]
+    assert len(ref) == TABLES[name] and ref == ours
+
+
+@pytest.mark.skipif(not os.path.exists(REF_TABLES), reason="reference not mounted")
+def test_sgr_params_match_reference():
+    """k_sgr_params in lr.hip (and the per-call tests' copy) equal dav1d_sgr_params."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gen_tables
+    ref = gen_tables.numbers(gen_tables.body_of(open(REF_TABLES).read(), "dav1d_sgr_params[16][2]"))
+    src = open(os.path.join(ROOT, "rav1d_amd", "csrc", "lr.hip")).read()
+    i = src.index("k_sgr_params[16][2] = {")
+    ours = [int(v) for v in re.findall(r"-?\d+", src[i + len("k_sgr_params[16][2] = {"): src.index("};", i)])]
+    assert ref == ours and len(ours) == 32
+    from tests.test_dsp_calls_gpu import _SGR
+    assert [v for pr in _SGR for v in pr] == ref
