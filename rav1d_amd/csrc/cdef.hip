@@ -27,12 +27,6 @@ __device__ __forceinline__ int dir_off(int dir, int k, int ts) {
     return k == 0 ? nib(DY0, dir) * ts + nib(DX0, dir) : nib(DY1, dir) * ts + nib(DX1, dir);
 }
 
-#ifndef MI_CDEF_EXP
-#define MI_CDEF_EXP 0
-#endif
-#ifndef MI_CDEF_CPAD
-#define MI_CDEF_CPAD 8
-#endif
 constexpr int kTY = 68, kTS = 72;          // luma tile rows / LDS row stride (int16)
 
 __device__ __forceinline__ int constrain(int diff, int thr, int shift) {
@@ -191,37 +185,8 @@ __device__ __forceinline__ int cdef_px(const int16_t *t, int ts, int x, int y, i
 
 // Tile loader: the (ROWS x COLS) window at (x0-2, y0-2) as int16, i16::MIN outside the frame,
 // written twice: T[r][c] and T1[r][c-1] (T shifted left by one sample), so that any horizontal
-// sample pair (c, c+1) is one aligned 32-bit LDS word in T (c even) or T1 (c odd). All loads of
-// the calling lane are issued before the first LDS store (unrolled, constant divisors).
-template <typename Px, int ROWS, int COLS>
-struct TileLoad {
-    static constexpr int N = ROWS * COLS, IT = (N + 255) / 256;
-    int16_t v[IT];
-    __device__ __forceinline__ void fetch(const uint8_t *src, int64_t stride, int x0, int y0, int fw, int fh) {
-#pragma unroll
-        for (int k = 0; k < IT; k++) {
-            const int i = threadIdx.x + 256 * k;
-            const int r = i / COLS, c = i - r * COLS;
-            const int x = x0 - 2 + c, y = y0 - 2 + r;
-            v[k] = INT16_MIN;
-            if (i < N && x >= 0 && y >= 0 && x < fw && y < fh)
-                v[k] = (int16_t) reinterpret_cast<const Px *>(src + (int64_t)y * stride)[x];
-        }
-    }
-    __device__ __forceinline__ void store(int16_t *t, int16_t *t1, int ts) const {
-#pragma unroll
-        for (int k = 0; k < IT; k++) {
-            const int i = threadIdx.x + 256 * k;
-            const int r = i / COLS, c = i - r * COLS;
-            if (i < N) {
-                t[r * ts + c] = v[k];
-                if (c) t1[r * ts + c - 1] = v[k];
-            }
-        }
-    }
-};
-
-// Vector form of TileLoad: each row of the window is read as 8-sample aligned vectors from
+// sample pair (c, c+1) is one aligned 32-bit LDS word in T (c even) or T1 (c odd). Each row of
+// the window is read as 8-sample aligned vectors from
 // x0 - 8 (one 16-B load at 16 bits, 8-B at 8 bits; per-sample checks only for a vector that
 // straddles the frame edge) and written to T as 4 aligned pairs and to T1 (shifted by one) as
 // 3 pairs plus the two end samples: 10 vectors per luma row instead of 68 scalar loads.
@@ -433,13 +398,10 @@ __device__ __forceinline__ void filter_plane(const int16_t *T, int lane, const i
 
 // One 64x64 luma unit (+ co-located chroma) per 256-lane workgroup. L = layout (0 I400,
 // 1 I420, 2 I422, 3 I444), compile-time so every tile index is a shift or a constant divide.
-#ifndef MI_CDEF_WAVES
-#define MI_CDEF_WAVES 1
-#endif
 template <typename Px, int L>
-__global__ __launch_bounds__(256, MI_CDEF_WAVES) void cdef_kernel(CdefArgs a) {
+__global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
     constexpr int SSH = L == 1 || L == 2, SSV = L == 1;
-    constexpr int CW = 64 >> SSH, CH = 64 >> SSV, CTS = CW + MI_CDEF_CPAD;
+    constexpr int CW = 64 >> SSH, CH = 64 >> SSV, CTS = CW + 8;
     constexpr int UVW = 8 >> SSH, UVH = 8 >> SSV;
     constexpr int YN = kTY * kTS, CN = L ? (CH + 4) * CTS : 2;
     __shared__ int16_t ty[2 * YN];                 // T, T1
@@ -483,16 +445,8 @@ __global__ __launch_bounds__(256, MI_CDEF_WAVES) void cdef_kernel(CdefArgs a) {
     int uv_sec = uv_lvl & 3; uv_sec += uv_sec == 3; uv_sec <<= bdm8;
 
     {
-#ifndef MI_CDEF_VEC
-#define MI_CDEF_VEC 1
-#endif
-#if MI_CDEF_VEC
         VecTileLoad<Px, 68, 68> ly;
         VecTileLoad<Px, CH + 4, CW + 4> lu, lv;
-#else
-        TileLoad<Px, 68, 68> ly;
-        TileLoad<Px, CH + 4, CW + 4> lu, lv;
-#endif
         ly.fetch(a.src[0], a.stride[0], x0, y0, fwy, fhy);
         if (L && uv_lvl) {
             lu.fetch(a.src[1], a.stride[1], x0 >> SSH, y0 >> SSV, fwc, fhc);
@@ -506,10 +460,6 @@ __global__ __launch_bounds__(256, MI_CDEF_WAVES) void cdef_kernel(CdefArgs a) {
     }
     __syncthreads();
 
-#ifndef MI_CDEF_DIR4
-#define MI_CDEF_DIR4 1
-#endif
-#if MI_CDEF_DIR4
     if (y_pri || uv_pri) {
         const int b = threadIdx.x & 63, w = threadIdx.x >> 6;   // wave-uniform direction pair
         const int16_t *tb = ty + ((b >> 3) * 8 + 2) * kTS + (b & 7) * 8 + 2;
@@ -522,7 +472,6 @@ __global__ __launch_bounds__(256, MI_CDEF_WAVES) void cdef_kernel(CdefArgs a) {
         dcost[2 * w + 1][b] = cb;
         __syncthreads();
     }
-#endif
 
     if (threadIdx.x < 64) {
         const int b = threadIdx.x, bxl = b & 7, byl = b >> 3;
@@ -533,9 +482,6 @@ __global__ __launch_bounds__(256, MI_CDEF_WAVES) void cdef_kernel(CdefArgs a) {
             const unsigned noskip = (unsigned)lf->noskip_mask[by_idx][1] << 16 | lf->noskip_mask[by_idx][0];
             if (noskip & (3u << (bx & 30))) {
                 unsigned var = 0;
-#if MI_CDEF_EXP == 1
-                var = 1000; dir = byl & 7;
-#elif MI_CDEF_DIR4
                 if (y_pri || uv_pri) {
                     unsigned bc = dcost[0][b];
 #pragma unroll
@@ -543,9 +489,6 @@ __global__ __launch_bounds__(256, MI_CDEF_WAVES) void cdef_kernel(CdefArgs a) {
                         if (dcost[n][b] > bc) { bc = dcost[n][b]; dir = n; }
                     var = (bc - dcost[dir ^ 4][b]) >> 10;
                 }
-#else
-                if (y_pri || uv_pri) dir = find_dir(ty + (byl * 8 + 2) * kTS + bxl * 8 + 2, kTS, bdm8, &var);
-#endif
                 if (y_pri) {
                     pri = adjust_strength(y_pri, var);
                     if (pri || y_sec) flag |= 1;
@@ -561,9 +504,6 @@ __global__ __launch_bounds__(256, MI_CDEF_WAVES) void cdef_kernel(CdefArgs a) {
     }
     __syncthreads();
 
-#if MI_CDEF_EXP == 2
-    if (bflag[threadIdx.x & 63] != 77) return;
-#endif
     // luma: 2048 pairs, 8 rows of one 8x8 block per lane
     filter_plane<Px, 64, 64, 8, 8, 256, kTS, YN * 2, 1, true>(
         ty, threadIdx.x, bdir, bflag, bpri, y_pri != 0, y_pri, y_sec, a.damping, bdm8, false,

@@ -22,7 +22,6 @@ constexpr int kNY = 8;                 // waves (row groups) per workgroup
 constexpr int kNR = 64 / kNY;          // output rows per lane
 constexpr int kNT = 64 * kNY;          // lanes per workgroup
 constexpr int kWL = (70 + kNY - 1) / kNY;   // window rows loaded per lane
-constexpr int kABG = kNT / 66;         // A/B row groups (66 columns each)
 
 __constant__ uint16_t k_sgr_params[16][2] = {
     { 140, 3236 }, { 112, 2158 }, { 93, 1618 }, { 80, 1438 }, { 70, 1295 }, { 58, 1177 },
@@ -42,68 +41,12 @@ __device__ __forceinline__ int ld_px(const uint8_t *base, int64_t stride, int y,
     return reinterpret_cast<const Px *>(base + (int64_t)y * stride)[x];
 }
 
-// Self-guided A/B maps (looprestoration.rs selfguided_filter, first half) for radius R over
-// rows -1..sh (every other row for R = 2) and cols -1..tw. Lane (tx, ty) owns column tx (and
-// tx + 64 for the two extra columns) and a quarter of the rows, and slides a (2R+1)-row
-// window of horizontal sums down its column: 2R+1 LDS reads per position.
-template <int R>
-__device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, unsigned s, int bdm8,
-                       const uint8_t *xbyx) {
-    constexpr int n = (2 * R + 1) * (2 * R + 1);
-    constexpr unsigned one_by_x = n == 25 ? 164 : 455;
-    // 66 columns x kABG row groups, one column per lane
-    const int g = threadIdx.x / 66, c = threadIdx.x - g * 66;
-    if (g >= kABG || c >= tw + 2) return;
-    const int nrows = sh + 2;                         // y = -1 .. sh
-    const int per = (nrows + kABG - 1) / kABG;
-    const int y0 = -1 + g * per, y1 = min(-1 + (g + 1) * per, sh + 1);
-    {
-        const int x = c - 1;                          // position column (-1 .. tw)
-        const int16_t *col = win + x + kWX;
-        int rs[2 * R + 1], rq[2 * R + 1];
-#pragma unroll
-        for (int k = 0; k < 2 * R; k++) {             // rows y0-R .. y0+R-1
-            const int16_t *row = col + (y0 - R + k + 3) * kLrWin;
-            int s1 = 0, q1 = 0;
-#pragma unroll
-            for (int dx = -R; dx <= R; dx++) { const int v = row[dx]; s1 += v; q1 += v * v; }
-            rs[k] = s1; rq[k] = q1;
-        }
-        for (int y = y0; y < y1; y++) {
-            {
-                const int16_t *row = col + (y + R + 3) * kLrWin;
-                int s1 = 0, q1 = 0;
-#pragma unroll
-                for (int dx = -R; dx <= R; dx++) { const int v = row[dx]; s1 += v; q1 += v * v; }
-                rs[2 * R] = s1; rq[2 * R] = q1;
-            }
-            if (R == 1 || !((y + 1) & 1)) {
-                int sum = 0, sq = 0;
-#pragma unroll
-                for (int k = 0; k <= 2 * R; k++) { sum += rs[k]; sq += rq[k]; }
-                const int a = (sq + ((1 << (2 * bdm8)) >> 1)) >> (2 * bdm8);
-                const int b = (sum + ((1 << bdm8) >> 1)) >> bdm8;
-                const unsigned p = (unsigned)max(a * n - b * b, 0);
-                const unsigned z = (p * s + (1u << 19)) >> 20;
-                const unsigned xv = xbyx[min(z, 255u)];   // LDS table, not a divide per sample
-                A[(y + 1) * kLrAB + x + 1] = (int)((xv * (unsigned)sum * one_by_x + (1u << 11)) >> 12);
-                B[(y + 1) * kLrAB + x + 1] = (int16_t)xv;
-            }
-#pragma unroll
-            for (int k = 0; k < 2 * R; k++) { rs[k] = rs[k + 1]; rq[k] = rq[k + 1]; }
-        }
-    }
-}
-
-#ifndef MI_LR_AB2
-#define MI_LR_AB2 1
-#endif
-#if MI_LR_AB2
-// Column-pair form of sgr_ab: lane (g, cp) owns positions x = 2cp - 2 and x + 1 (x even, so
+// Self-guided A/B maps (looprestoration.rs selfguided_filter, first half) by column pairs:
+// lane (g, cp) owns positions x = 2cp - 2 and x + 1 (x even, so
 // the six window samples x-2 .. x+3 are three aligned 32-bit LDS reads per row serving both
 // columns' horizontal sums, instead of 2 x (2R+1) 16-bit reads). 34 pairs x 15 row groups.
 template <int R>
-__device__ void sgr_ab2(const int16_t *win, int *A, int16_t *B, int sh, int tw, unsigned s, int bdm8,
+__device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, unsigned s, int bdm8,
                         const uint8_t *xbyx) {
     constexpr int n = (2 * R + 1) * (2 * R + 1);
     constexpr unsigned one_by_x = n == 25 ? 164 : 455;
@@ -158,8 +101,6 @@ __device__ void sgr_ab2(const int16_t *win, int *A, int16_t *B, int sh, int tw, 
         for (int k = 0; k < 2 * R; k++) { rs0[k] = rs0[k + 1]; rq0[k] = rq0[k + 1]; rs1[k] = rs1[k + 1]; rq1[k] = rq1[k + 1]; }
     }
 }
-#define sgr_ab sgr_ab2
-#endif
 
 // Self-guided output terms for rows r0..r0+kNR-1 of column i (looprestoration.rs selfguided_filter
 // tail). The lane walks down its column keeping, per A/B row, the centre value c and the sum of

@@ -28,9 +28,6 @@ __constant__ uint8_t k_obmc[64] = {
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
-#ifndef MI_MC_EXP
-#define MI_MC_EXP 0
-#endif
 #ifndef MC_MAX_U
 #define MC_MAX_U 16
 #endif
@@ -157,44 +154,19 @@ __device__ __forceinline__ void predict(const McArgs &a, const int16_t *win, int
 }
 
 template <typename Px>
-#ifndef MI_MC_WAVES
-#define MI_MC_WAVES 1
-#endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MI_MC_WAVES))) void mc_kernel(McArgs a, int g) {
+__global__ __launch_bounds__(64) void mc_kernel(McArgs a, int g) {
     __shared__ __attribute__((aligned(16))) int16_t win[2][kWinElems];
     const int lane = threadIdx.x;
 #ifndef MI_MC_XCD_CHUNK
 #define MI_MC_XCD_CHUNK 1
 #endif
     const uint32_t *fw = a.first_wave[g];
-#ifndef MI_MC_XCD_BAND
-#define MI_MC_XCD_BAND 0
-#endif
-#if MI_MC_XCD_BAND
-    // XCD-banded order: workgroups are dealt round-robin to the 8 XCDs, so XCD k = blockIdx % 8
-    // takes the k-th eighth of every class's waves. Units within a class are in raster order, so
-    // each XCD's L2 sees one band of the frame and the reference rows under it (neighbouring
-    // windows share lines) instead of every XCD pulling the whole reference through its L2.
-    // Measured at 4K10 (units band-sorted within classes): 103 us vs 84 us round-robin: with all
-    // XCDs on neighbouring waves the duplicated lines come from the MALL, while a band per XCD
-    // re-streams its whole band once per class. Kept as an option, off.
-    const uint32_t k = blockIdx.x & 7, j = blockIdx.x >> 3;
-    int c = -1, item = 0;
-    uint32_t acc = 0;
-    for (int cc = 0; cc < MI_MC_NCLASS; cc++) {
-        const uint32_t W = fw[cc + 1] - fw[cc], lo = (k * W) >> 3, n = (((k + 1) * W) >> 3) - lo;
-        if (c < 0 && j < acc + n) { c = cc; item = (int)(lo + j - acc); }
-        acc += n;
-    }
-    if (c < 0) return;   // this XCD's share is shorter than the grid's per-XCD depth
-#else
     const int wave = xcd_chunk(blockIdx.x, gridDim.x, MI_MC_XCD_CHUNK);
     // class of this wave: last class whose first wave <= wave (wave-uniform scan)
     int c = 0;
     for (int k = 1; k < MI_MC_NCLASS; k++)
         if (fw[k] <= (uint32_t)wave) c = k;
     const int item = wave - (int)fw[c];
-#endif
     const ClassGeom G = class_geom(c);
     const uint32_t cls_begin = a.class_start[g * MI_MC_NCLASS + c], cls_end = a.class_start[g * MI_MC_NCLASS + c + 1];
 
@@ -262,9 +234,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MI_MC_WAVES)
                 const int yy = min(max(r.dy + rr, 0), r.ih - 1);
                 const int x0 = r.dx + 4 * qq;
                 const uint8_t *row = r.base + (int64_t)yy * r.stride;
-#if MI_MC_EXP == 1
-                if (true) { v0[k] = (uint32_t)ec; v1[k] = (uint32_t)rr; } else
-#endif
                 if (inside) {
                     if (sizeof(Px) == 2) {
                         const U2a q = *reinterpret_cast<const U2a *>(row + 2 * x0);
@@ -329,11 +298,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MI_MC_WAVES)
         }
 #pragma unroll
         for (int q = 0; q < 8; q++)
-#if MI_MC_EXP == 2
-            if (q < R && o0[q] == -12345) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];
-#else
             if (q < R) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];
-#endif
         return;
     }
     predict<true>(a, win[0] + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
@@ -388,11 +353,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MI_MC_WAVES)
     }
 #pragma unroll
     for (int q = 0; q < 8; q++)
-#if MI_MC_EXP == 2
-        if (q < R && o0[q] == -12345) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];
-#else
         if (q < R) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];
-#endif
 }
 
 // Waves per class for one plane group: packed small units or one wave per 64-lane tile.
@@ -422,18 +383,6 @@ int mc_plan(McArgs &a, int g) {
 
 int launch_mc(const McArgs &a, int g, int waves, hipStream_t s) {
     if (waves <= 0) return 0;
-#if MI_MC_XCD_BAND
-    uint32_t depth = 0;   // the longest XCD share
-    for (uint32_t k = 0; k < 8; k++) {
-        uint32_t n = 0;
-        for (int c = 0; c < MI_MC_NCLASS; c++) {
-            const uint32_t W = a.first_wave[g][c + 1] - a.first_wave[g][c];
-            n += (((k + 1) * W) >> 3) - ((k * W) >> 3);
-        }
-        depth = n > depth ? n : depth;
-    }
-    waves = (int)(8 * depth);
-#endif
     if (a.bpc == 8) mc_kernel<uint8_t><<<waves, 64, 0, s>>>(a, g);
     else mc_kernel<uint16_t><<<waves, 64, 0, s>>>(a, g);
     return hipGetLastError() == hipSuccess ? 0 : -5;
