@@ -256,6 +256,13 @@ typedef struct MiIntraBlock {
     uint32_t reserved;      /* MI_INTRA_CFL_AC: w_pad | h_pad << 8 | ss_hor << 16 | ss_ver << 17; else 0 */
 } MiIntraBlock;
 
+#define MI_INTRA_IBC 96    /* MiIntraBlock.mode: intra block copy, the bilinear put (mc[FILTER_2D_BILINEAR],
+                              mc.rs:1322-1338) from the current picture as recon's mc() does with
+                              the frame itself as reference (recon.rs:3236-3290): reserved =
+                              (uint16)mv.x | mv.y << 16 (luma 1/8 pel as coded), filt_idx = ss_hor |
+                              ss_ver << 1 of the block's plane; the block's dependencies must cover
+                              the source rectangle (plus one column / row when the chroma phase is
+                              half-pel) */
 #define MI_IPRED_II 128    /* mode flag: inter-intra, blend the prediction into the existing
                               (inter) pixels with the mask at idx + aux_off (mc.blend,
                               recon.rs:3524-3543): only with slots 0-12 */

@@ -508,7 +508,15 @@ void oracle_intra_blocks(void *const planes[3], const ptrdiff_t strides[2], int 
         const int ii = b->flags & 64;
         uint8_t *out = ii ? tmp : dst;
         const ptrdiff_t ost = ii ? b->w * pb : st;
-        if (b->mode == 64) {
+        if (b->mode == 96) {
+            /* intra block copy: mc() with the current picture as reference, bilinear (recon.rs) */
+            const int mvx = (int16_t)(b->reserved & 0xffff), mvy = (int16_t)(b->reserved >> 16);
+            const int ssh = b->filt_idx & 1, ssv = (b->filt_idx >> 1) & 1;
+            const uint8_t *src = (const uint8_t *)planes[b->plane] + (ptrdiff_t)(b->y + (mvy >> (3 + ssv))) * st +
+                                 (ptrdiff_t)(b->x + (mvx >> (3 + ssh))) * pb;
+            oracle_mc_put(9, out, ost, src, st, b->w, b->h, (mvx & (15 >> !ssh)) << !ssh, (mvy & (15 >> !ssv)) << !ssv,
+                          bpc);
+        } else if (b->mode == 64) {
             oracle_pal_pred(out, ost, (const uint8_t *)pal + (size_t)b->pal_off * pb, idx + b->aux_off, b->w, b->h, bpc);
         } else {
             const int cfl = b->mode == 32;

@@ -411,6 +411,37 @@ __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlo
             for (int i = lane; i < w * h; i += 64) lt[i] = (Px)P(y + i / w, x + i % w);
     }
     const int bd = a.bpc;
+    if (ib.mode == MI_INTRA_IBC) {
+        // intra block copy: bilinear put_bilin_c (mc_tmpl.c) from the already reconstructed
+        // source rectangle of this picture (its owners are this block's dependencies)
+        const int mvx = (int16_t)(ib.reserved & 0xffff), mvy = (int16_t)(ib.reserved >> 16);
+        const int ssh = ib.filt_idx & 1, ssv = (ib.filt_idx >> 1) & 1;
+        const int sx = x + (mvx >> (3 + ssh)), sy = y + (mvy >> (3 + ssv));
+        const int mx = (mvx & (15 >> !ssh)) << !ssh, my = (mvy & (15 >> !ssv)) << !ssv;
+        const int ibits = bd == 8 ? 4 : 14 - bd, bdmax = (1 << bd) - 1;
+        auto rnd = [](int v, int sh) { return (v + ((1 << sh) >> 1)) >> sh; };
+        for (int i = lane; i < w * h; i += 64) {
+            const int yy = i / w, xx = i % w, py = sy + yy, px = sx + xx;
+            const int s00 = P(py, px);
+            int v;
+            if (mx && my) {
+                const int m0 = rnd(16 * s00 + mx * (P(py, px + 1) - s00), 4 - ibits);
+                const int s10 = P(py + 1, px);
+                const int m1 = rnd(16 * s10 + mx * (P(py + 1, px + 1) - s10), 4 - ibits);
+                v = rnd(16 * m0 + my * (m1 - m0), 4 + ibits);
+            } else if (mx) {
+                v = (rnd(16 * s00 + mx * (P(py, px + 1) - s00), 4 - ibits) + ((1 << ibits) >> 1)) >> ibits;
+            } else if (my) {
+                v = rnd(16 * s00 + my * (P(py + 1, px) - s00), 4);
+            } else {
+                v = s00;
+            }
+            v = min(max(v, 0), bdmax);
+            if constexpr (Fused) lt[i] = (Px)v;
+            else reinterpret_cast<Px *>(a.dst[ib.plane] + (int64_t)(y + yy) * st)[x + xx] = (Px)v;
+        }
+        return;
+    }
 
     MiIpredBlock b;
     b.edge_off = 0;

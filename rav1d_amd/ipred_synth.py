@@ -66,7 +66,7 @@ def make_ipred_blocks(n, bpc, rng, sizes=SIZES, modes=None, plane_w=4096):
 
 
 def make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.5, pal_frac=0.05, cfl_frac=0.4,
-                     filter_frac=0.1, ii_frac=0.0, edge_filter=None, cfl_dev_frac=0.5):
+                     filter_frac=0.1, ii_frac=0.0, edge_filter=None, cfl_dev_frac=0.5, ibc_frac=0.05):
     """A whole intra frame as MiIntraBlock transform blocks in decode order (blocks in quadtree
     z-order, luma then U then V per block, transform blocks raster within a block), with the
     edge-availability flags a decoder would pass (top-right / bottom-left only where those
@@ -122,8 +122,24 @@ def make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.5, pal_
                     cfl_dev = bool(pl and pal_frac <= r < pal_frac + cfl_frac and tw <= 32 and th <= 32
                                    and rng.random() < cfl_dev_frac)
                     reserved = 0
+                    # intra block copy: a luma-integer displacement up / left onto pixels already
+                    # reconstructed (half-pel in subsampled chroma for odd displacements)
+                    ibc = None
+                    if not cfl_dev and rng.random() < ibc_frac:
+                        for _ in range(8):
+                            lx, lyd = -int(rng.integers(0, 65)), -int(rng.integers(0, 65))
+                            mvx, mvy = 8 * lx, 8 * lyd
+                            sx, sy = tx + (mvx >> (3 + sh)), ty + (mvy >> (3 + sv))
+                            mxp = (mvx & (15 >> (1 - sh))) << (1 - sh)
+                            myp = (mvy & (15 >> (1 - sv))) << (1 - sv)
+                            ex, ey = sx + tw + (mxp > 0), sy + th + (myp > 0)
+                            if sx >= 0 and sy >= 0 and ex <= pw and ey <= ph and (own[sy:ey, sx:ex] >= 0).all():
+                                ibc = (mvx, mvy, own[sy:ey, sx:ex].ravel())
+                                break
                     # dependency level from every pixel the edge may read
                     deps = []
+                    if ibc is not None:
+                        deps.append(ibc[2])
                     if cfl_dev:
                         wp = int(rng.integers(0, tw // 4)) if rng.random() < 0.3 else 0
                         hp = int(rng.integers(0, th // 4)) if rng.random() < 0.3 else 0
@@ -144,7 +160,11 @@ def make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.5, pal_
                         lv = 1 + max(level_of[i] for i in dep_ids)
                     dep_lists.append(dep_ids)
                     mode, angle, filt, alpha, aux, poff = 0, 0, 0, 0, 0, 0
-                    if r < pal_frac:
+                    if ibc is not None:
+                        mode, filt = 96, sh | (sv << 1)
+                        reserved = (ibc[0] & 0xFFFF) | ((ibc[1] & 0xFFFF) << 16)
+                        flags &= ~INTRA_II
+                    elif r < pal_frac:
                         mode = 64
                         pal.append(rng.integers(0, 1 << bpc, size=8).astype(dt))
                         poff, n_pal = n_pal, n_pal + 8
