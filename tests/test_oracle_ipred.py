@@ -94,3 +94,29 @@ def test_oracle_cfl_and_palette():
     pal = rng.integers(0, 1024, size=8)
     idx = rng.integers(0, 8, size=32).astype(np.uint8)
     assert np.array_equal(oracle_lib.pal_pred(pal, idx, 8, 4, 10), pal[idx].reshape(4, 8))
+
+
+@pytest.mark.parametrize("bpc", [8, 10])
+def test_oracle_intra_block_copy(bpc):
+    """MI_INTRA_IBC in the oracle: an integer luma displacement copies the source rectangle; a
+    half-pel chroma phase (odd luma displacement, 4:2:0) averages neighbours as put_bilin does."""
+    from rav1d_amd import INTRA_DTYPE
+    rng = np.random.default_rng(5 + bpc)
+    dt = np.uint8 if bpc == 8 else np.uint16
+    luma = rng.integers(0, 1 << bpc, size=(64, 64)).astype(dt)
+    chroma = rng.integers(0, 1 << bpc, size=(32, 32)).astype(dt)
+    mv = lambda lx, ly: (lx * 8 & 0xFFFF) | ((ly * 8 & 0xFFFF) << 16)  # noqa: E731
+    blk = np.zeros(2, INTRA_DTYPE)
+    blk[0] = (32, 32, 16, 8, 0, 96, 0, 0, 0, 0, 64, 64, 32, 32, 0, 0, mv(-20, -24))
+    blk[1] = (16, 16, 8, 8, 1, 96, 0, 0, 3, 0, 32, 32, 16, 16, 0, 0, mv(-9, -20))
+    z = np.zeros(1, np.int16)
+    out = oracle_lib.intra_blocks([luma, chroma, chroma.copy()], bpc, blk, z, np.zeros(1, np.uint8), np.zeros(8, dt))
+    assert np.array_equal(out[0][32:40, 32:48], luma[8:16, 12:28])
+    # chroma: x offset floor(-9 / 2) = -5 with phase 8/16, y offset -10 exactly (source and
+    # destination disjoint, as the block-copy constraints guarantee)
+    src = chroma.astype(np.int64)
+    a, b = src[6:14, 11:19], src[6:14, 12:20]
+    ib = 4 if bpc == 8 else 14 - bpc
+    px = (16 * a + 8 * (b - a) + ((1 << (4 - ib)) >> 1)) >> (4 - ib)
+    exp = np.clip((px + ((1 << ib) >> 1)) >> ib, 0, (1 << bpc) - 1)
+    assert np.array_equal(out[1][16:24, 16:24].astype(np.int64), exp)
