@@ -29,7 +29,6 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from rav1d_amd import ITX_KEEP_COEFS  # noqa: E402
 from rav1d_amd import frame as F  # noqa: E402
 from rav1d_amd.synth import frame_bytes, itx_algorithmic_bytes, make_frame, mc_algorithmic_bytes  # noqa: E402
 
@@ -71,7 +70,7 @@ class Pipeline:
         lvl_bytes = ((w + 3) >> 2) * ((h + 3) >> 2) * 4
         mask_bytes = fr["lf"]["masks"].nbytes
         self.algo = {
-            "itx": itx_algorithmic_bytes(fr["blocks"], bpc, zero_coefs=False),
+            "itx": itx_algorithmic_bytes(fr["blocks"], bpc, zero_coefs=True),
             "deblock": 2 * fb + lvl_bytes + mask_bytes,
             "cdef": 2 * fb + mask_bytes,
             "lr": 2 * fb + fb * 4 // 64 + fr["lr"]["lr_mask"].nbytes,
@@ -118,7 +117,7 @@ class Pipeline:
                                                         ctypes.c_void_p(self.mc.masks.data_ptr()), None, sp), "mc"))
         ss = (ctypes.c_uint32 * 20)(*[int(v) for v in self.fr["size_start"]])
         timed("itx", lambda: F.check(lib.mi_itx_frame(ctx, ctypes.byref(pa), ctypes.c_void_p(self.blocks.data_ptr()),
-                                                      ss, ctypes.c_void_p(self.coef.data_ptr()), ITX_KEEP_COEFS, sp), "itx"))
+                                                      ss, ctypes.c_void_p(self.coef.data_ptr()), 0, sp), "itx"))
         timed("deblock", lambda: F.check(lib.mi_deblock_frame_to(ctx, ctypes.byref(pa), ctypes.byref(pd),
                                                                  ctypes.byref(self.lf.s), sp), "lf"))
         timed("cdef", lambda: F.check(lib.mi_cdef_frame(ctx, ctypes.byref(pd), ctypes.byref(pb),
@@ -194,12 +193,14 @@ def intra_1080p8(ctx, reps=5, nframes=24, ndesc=4):
     from rav1d_amd.intra import IntraFrame, device_status, intra_recon, make_intra_residuals
     from rav1d_amd.ipred_synth import make_intra_frame
     w, h, bpc = 1920, 1080, 8
-    descs = []
+    frs = []
     for k in range(ndesc):
         rng = np.random.default_rng(0x1A7A0001 + k)
-        descs.append(IntraFrame(ctx, make_intra_residuals(make_intra_frame(w, h, bpc, 1, rng), bpc, rng)))
+        frs.append(make_intra_residuals(make_intra_frame(w, h, bpc, 1, rng), bpc, rng))
+    # one descriptor set (and coefficient arena: itxfm_add zeroes what it consumes) per frame
+    descs = [IntraFrame(ctx, frs[f % ndesc]) for f in range(nframes)]
     curs = [F.Frame(w, h, bpc, 1) for _ in range(nframes)]
-    batch = [(descs[f % ndesc], curs[f].picture()) for f in range(nframes)]
+    batch = [(descs[f], curs[f].picture()) for f in range(nframes)]
     s = torch.cuda.Stream()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 
@@ -214,14 +215,14 @@ def intra_1080p8(ctx, reps=5, nframes=24, ndesc=4):
         return ev[0].elapsed_time(ev[1]) / reps
 
     with torch.cuda.stream(s):
-        one_ms = timed(lambda: intra_recon(ctx, batch[:1], s))
-        batch_ms = timed(lambda: intra_recon(ctx, batch, s))
+        one_ms = timed(lambda: intra_recon(ctx, batch[:1], s, keep_coefs=False))
+        batch_ms = timed(lambda: intra_recon(ctx, batch, s, keep_coefs=False))
         device_status(ctx, s)
         intra, pic = descs[0], batch[0][1]
         g = torch.cuda.CUDAGraph()
-        intra.step(pic, s)
+        intra.step(pic, s, keep_coefs=False)
         with torch.cuda.graph(g, stream=s):
-            intra.step(pic, s)
+            intra.step(pic, s, keep_coefs=False)
         level_ms = timed(g.replay)
     fr = descs[0].fr
     return dict(mpx_per_s=round(nframes * w * h / (batch_ms / 1e3) / 1e6, 1),

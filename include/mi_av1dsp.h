@@ -260,9 +260,11 @@ typedef struct MiIntraBlock {
                               mc.rs:1322-1338) from the current picture as recon's mc() does with
                               the frame itself as reference (recon.rs:3236-3290): reserved =
                               (uint16)mv.x | mv.y << 16 (luma 1/8 pel as coded), filt_idx = ss_hor |
-                              ss_ver << 1 of the block's plane; the block's dependencies must cover
-                              the source rectangle (plus one column / row when the chroma phase is
-                              half-pel) */
+                              ss_ver << 1 of the block's plane; max_w / max_h = the reference area
+                              mc() clamps to for intrabc (f.bw * 4 >> ss_hor, f.bh * 4 >> ss_ver,
+                              recon.rs:2052-2083: reads outside it replicate its border, as
+                              emu_edge); the block's dependencies must cover the source rectangle
+                              (plus one column / row when the chroma phase is half-pel) */
 #define MI_IPRED_II 128    /* mode flag: inter-intra, blend the prediction into the existing
                               (inter) pixels with the mask at idx + aux_off (mc.blend,
                               recon.rs:3524-3543): only with slots 0-12 */

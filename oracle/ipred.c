@@ -512,10 +512,22 @@ void oracle_intra_blocks(void *const planes[3], const ptrdiff_t strides[2], int 
             /* intra block copy: mc() with the current picture as reference, bilinear (recon.rs) */
             const int mvx = (int16_t)(b->reserved & 0xffff), mvy = (int16_t)(b->reserved >> 16);
             const int ssh = b->filt_idx & 1, ssv = (b->filt_idx >> 1) & 1;
-            const uint8_t *src = (const uint8_t *)planes[b->plane] + (ptrdiff_t)(b->y + (mvy >> (3 + ssv))) * st +
-                                 (ptrdiff_t)(b->x + (mvx >> (3 + ssh))) * pb;
-            oracle_mc_put(9, out, ost, src, st, b->w, b->h, (mvx & (15 >> !ssh)) << !ssh, (mvy & (15 >> !ssv)) << !ssv,
-                          bpc);
+            const int dx = b->x + (mvx >> (3 + ssh)), dy = b->y + (mvy >> (3 + ssv));
+            const int mx = (mvx & (15 >> !ssh)) << !ssh, my = (mvy & (15 >> !ssv)) << !ssv;
+            const uint8_t *src = (const uint8_t *)planes[b->plane] + (ptrdiff_t)dy * st + (ptrdiff_t)dx * pb;
+            ptrdiff_t sst = st;
+            /* recon.rs:2052-2083 (C recon_tmpl.c mc()): the intrabc reference area is
+             * f.bw*4 >> ss_hor by f.bh*4 >> ss_ver (max_w x max_h here); a footprint leaving it
+             * goes through emu_edge into a (bw+7) x (bh+7) scratch with the block at (3, 3) */
+            static uint8_t emu[(128 + 7) * (128 + 7) * 2];
+            if (dx < !!mx * 3 || dy < !!my * 3 || dx + b->w + !!mx * 4 > b->max_w || dy + b->h + !!my * 4 > b->max_h) {
+                const ptrdiff_t es = (ptrdiff_t)(b->w + 7) * pb;
+                oracle_mc_emu_edge(b->w + 7, b->h + 7, b->max_w, b->max_h, dx - 3, dy - 3, emu, es, planes[b->plane], st,
+                                   bpc);
+                src = emu + 3 * es + 3 * pb;
+                sst = es;
+            }
+            oracle_mc_put(9, out, ost, src, sst, b->w, b->h, mx, my, bpc);
         } else if (b->mode == 64) {
             oracle_pal_pred(out, ost, (const uint8_t *)pal + (size_t)b->pal_off * pb, idx + b->aux_off, b->w, b->h, bpc);
         } else {
@@ -550,5 +562,19 @@ void oracle_intra_blocks(void *const planes[3], const ptrdiff_t strides[2], int 
                     D(dst, st, y, x, (a * (64 - mm) + t * mm + 32) >> 6, bpc);
                 }
         }
+    }
+}
+
+/* Interleaved intra reconstruction in decode order (recon.rs:2402-3160: for every transform
+ * block, prepare_intra_edges + intra_pred / cfl_pred / pal_pred, then itxfm_add before the next
+ * block reads its edges). tx_blocks[k] is the residual (MiTxBlock) of blocks[k]; the arena is
+ * zeroed as the blocks consume it (itx.rs:152-158). */
+void oracle_intra_recon(void *const planes[3], const ptrdiff_t strides[2], int bpc, const void *blocks,
+                        const void *tx_blocks, int n, const int16_t *ac, const uint8_t *idx, const void *pal,
+                        void *coef) {
+    const ptrdiff_t st3[3] = {strides[0], strides[1], strides[1]};
+    for (int k = 0; k < n; k++) {
+        oracle_intra_blocks(planes, strides, bpc, (const IntraBlock *)blocks + k, 1, ac, idx, pal);
+        oracle_itx_frame(planes, st3, (const uint8_t *)tx_blocks + 16 * k, 1, coef, (1 << bpc) - 1);
     }
 }

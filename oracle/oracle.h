@@ -96,6 +96,9 @@ int oracle_prepare_intra_edges(int x, int have_left, int y, int have_top, int ti
                                int mode, int *angle, int w, int h, int filter_edge, void *topleft, int bpc);
 void oracle_intra_blocks(void *const planes[3], const ptrdiff_t strides[2], int bpc, const void *blocks, int n,
                          const int16_t *ac, const uint8_t *idx, const void *pal);
+void oracle_intra_recon(void *const planes[3], const ptrdiff_t strides[2], int bpc, const void *blocks,
+                        const void *tx_blocks, int n, const int16_t *ac, const uint8_t *idx, const void *pal,
+                        void *coef);
 
 /* lr.c: per-call loop restoration (one unit, in place) */
 void oracle_lr_wiener(void *p, ptrdiff_t stride, const void *left_px, const void *lpf, int w, int h,

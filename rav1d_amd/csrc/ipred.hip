@@ -420,19 +420,24 @@ __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlo
         const int mx = (mvx & (15 >> !ssh)) << !ssh, my = (mvy & (15 >> !ssv)) << !ssv;
         const int ibits = bd == 8 ? 4 : 14 - bd, bdmax = (1 << bd) - 1;
         auto rnd = [](int v, int sh) { return (v + ((1 << sh) >> 1)) >> sh; };
+        // emu_edge (recon.rs:2052-2083, intrabc: the frame's 8-aligned coded size f.bw*4 >> ss_hor
+        // by f.bh*4 >> ss_ver, carried in max_w / max_h) replicates the border: clamping every
+        // tap coordinate is the same read
+        const int cw = ib.max_w - 1, chh = ib.max_h - 1;
+        auto Q = [&](int yy, int xx) { return P(min(max(yy, 0), chh), min(max(xx, 0), cw)); };
         for (int i = lane; i < w * h; i += 64) {
             const int yy = i / w, xx = i % w, py = sy + yy, px = sx + xx;
-            const int s00 = P(py, px);
+            const int s00 = Q(py, px);
             int v;
             if (mx && my) {
-                const int m0 = rnd(16 * s00 + mx * (P(py, px + 1) - s00), 4 - ibits);
-                const int s10 = P(py + 1, px);
-                const int m1 = rnd(16 * s10 + mx * (P(py + 1, px + 1) - s10), 4 - ibits);
+                const int m0 = rnd(16 * s00 + mx * (Q(py, px + 1) - s00), 4 - ibits);
+                const int s10 = Q(py + 1, px);
+                const int m1 = rnd(16 * s10 + mx * (Q(py + 1, px + 1) - s10), 4 - ibits);
                 v = rnd(16 * m0 + my * (m1 - m0), 4 + ibits);
             } else if (mx) {
-                v = (rnd(16 * s00 + mx * (P(py, px + 1) - s00), 4 - ibits) + ((1 << ibits) >> 1)) >> ibits;
+                v = (rnd(16 * s00 + mx * (Q(py, px + 1) - s00), 4 - ibits) + ((1 << ibits) >> 1)) >> ibits;
             } else if (my) {
-                v = rnd(16 * s00 + my * (P(py + 1, px) - s00), 4);
+                v = rnd(16 * s00 + my * (Q(py + 1, px) - s00), 4);
             } else {
                 v = s00;
             }

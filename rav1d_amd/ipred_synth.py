@@ -126,14 +126,19 @@ def make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.5, pal_
                     # reconstructed (half-pel in subsampled chroma for odd displacements)
                     ibc = None
                     if not cfl_dev and rng.random() < ibc_frac:
-                        for _ in range(8):
+                        for t_ in range(8):
                             lx, lyd = -int(rng.integers(0, 65)), -int(rng.integers(0, 65))
+                            if t_ & 1:
+                                # a source hugging the right / bottom border: the half-pel chroma
+                                # tap reads one column / row past the reference area (emu_edge)
+                                lx, lyd = (-int(rng.integers(0, 2)), lyd) if t_ & 2 else (lx, -int(rng.integers(0, 2)))
                             mvx, mvy = 8 * lx, 8 * lyd
                             sx, sy = tx + (mvx >> (3 + sh)), ty + (mvy >> (3 + sv))
                             mxp = (mvx & (15 >> (1 - sh))) << (1 - sh)
                             myp = (mvy & (15 >> (1 - sv))) << (1 - sv)
-                            ex, ey = sx + tw + (mxp > 0), sy + th + (myp > 0)
-                            if sx >= 0 and sy >= 0 and ex <= pw and ey <= ph and (own[sy:ey, sx:ex] >= 0).all():
+                            ex, ey = min(sx + tw + (mxp > 0), pw), min(sy + th + (myp > 0), ph)
+                            if sx >= 0 and sy >= 0 and sx + tw <= pw and sy + th <= ph and \
+                                    (own[sy:ey, sx:ex] >= 0).all():
                                 ibc = (mvx, mvy, own[sy:ey, sx:ex].ravel())
                                 break
                     # dependency level from every pixel the edge may read
@@ -186,7 +191,9 @@ def make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.5, pal_
                             idx.append(rng.integers(0, 65, size=tw * th).astype(np.uint8))
                             aux, n_idx = n_idx, n_idx + tw * th
                     k = len(recs)
-                    recs.append((tx, ty, tw, th, pl, mode, angle, flags, filt, alpha, pw, ph, pw - tx, ph - ty,
+                    # intrabc: max_w / max_h = the reference area mc() clamps to (the plane)
+                    mw, mh = (pw, ph) if mode == 96 else (pw - tx, ph - ty)
+                    recs.append((tx, ty, tw, th, pl, mode, angle, flags, filt, alpha, pw, ph, mw, mh,
                                  aux, poff, reserved))
                     level_of.append(lv)
                     own[ty:ty + th, tx:tx + tw] = k

@@ -330,3 +330,24 @@ def intra_blocks(planes, bpc, blocks, ac, idx, pal):
     a_, i_, p_ = (np.ascontiguousarray(x) for x in (ac, idx, pal))
     o.oracle_intra_blocks(pp, ps, bpc, ptr(b), len(b), ptr(a_), ptr(i_), ptr(p_))
     return pl[:len(planes)]
+
+
+def intra_recon(planes, bpc, blocks, tx_blocks, ac, idx, pal, coef):
+    """Oracle decode-order intra reconstruction: per block prediction then its residual
+    (tx_blocks[k] belongs to blocks[k]); returns (planes, arena after zeroing), copies."""
+    o = load_oracle()
+    _ipred_sigs(o)
+    f = o.oracle_intra_recon
+    f.restype = None
+    f.argtypes = [_VP, _VP, ctypes.c_int, _VP, _VP, ctypes.c_int, _VP, _VP, _VP, _VP]
+    pl = [np.ascontiguousarray(p).copy() for p in planes]
+    while len(pl) < 3:
+        pl.append(pl[0])
+    pp = (ctypes.c_void_p * 3)(*[a.ctypes.data for a in pl])
+    ps = (ctypes.c_ssize_t * 2)(pl[0].strides[0], pl[1].strides[0])
+    b, t = np.ascontiguousarray(blocks), np.ascontiguousarray(tx_blocks)
+    assert len(b) == len(t)
+    a_, i_, p_ = (np.ascontiguousarray(x) for x in (ac, idx, pal))
+    c = np.ascontiguousarray(coef).copy()
+    f(pp, ps, bpc, ptr(b), ptr(t), len(b), ptr(a_), ptr(i_), ptr(p_), ptr(c))
+    return pl[:len(planes)], c

@@ -154,3 +154,69 @@ def test_intra_recon_fused_multi_frame(gpu, nframes):
         for p in range(3):
             assert np.array_equal(curs[f].buffer_np(p), exp[p]), f"frame {f} plane {p}"
         assert int(torch.count_nonzero(frames[f].coef)) == 0, f"frame {f}: coefficients not zeroed"
+
+
+def test_intra_recon_bench_1080p8(gpu):
+    """The exact workload bench.py times for configs[1]: 1080p 8-bit 4:2:0 intra frames from the
+    four bench descriptor seeds (0x1A7A0001 + k), cycled through a 24-frame batch in one
+    persistent launch, coefficients zeroed as consumed (itxfm_add contract). Every frame is
+    compared with the oracle's decode-order reconstruction, and the device status must be 0."""
+    from rav1d_amd.intra import IntraFrame, device_status, intra_recon, make_intra_residuals
+    w, h, bpc, nframes, ndesc = 1920, 1080, 8, 24, 4
+    frs = []
+    for k in range(ndesc):
+        rng = np.random.default_rng(0x1A7A0001 + k)
+        frs.append(make_intra_residuals(make_intra_frame(w, h, bpc, 1, rng), bpc, rng))
+    intras = [IntraFrame(gpu, frs[f % ndesc]) for f in range(nframes)]   # one coefficient arena per frame
+    curs = [Frame(w, h, bpc, 1) for _ in range(nframes)]
+    init = [curs[0].buffer_np(p) for p in range(3)]
+    intra_recon(gpu, [(intras[f], curs[f].picture()) for f in range(nframes)], keep_coefs=False)
+    device_status(gpu)
+    for k in range(ndesc):
+        fr = frs[k]
+        exp, arena = oracle_lib.intra_recon(init, bpc, fr["blocks"], fr["tx_blocks"][fr["tx_of_block"]], fr["ac"],
+                                            fr["idx"], fr["pal"], fr["coef"])
+        assert not arena.any()
+        for f in range(k, nframes, ndesc):
+            for p in range(3):
+                got = curs[f].buffer_np(p)
+                if not np.array_equal(got, exp[p]):
+                    bad = np.argwhere(got != exp[p])
+                    raise AssertionError(f"frame {f} plane {p}: {len(bad)} mismatches, first at {bad[0]}")
+            assert int(torch.count_nonzero(intras[f].coef)) == 0, f"frame {f}: coefficients not zeroed"
+
+
+@pytest.mark.parametrize("bpc,layout", [(8, 1), (10, 2), (12, 3)])
+def test_intra_recon_block_copy_heavy(gpu, bpc, layout):
+    """Intra block copy at a high rate, with sources hugging the right / bottom border (the
+    half-pel chroma tap past the reference area replicates its border, as emu_edge): both the
+    per-level and the persistent path against the oracle, and the frame must hold block copies
+    with both chroma phases non-zero."""
+    from rav1d_amd.intra import IntraFrame, device_status, make_intra_residuals
+    w, h = 256, 192
+    rng = np.random.default_rng(4242 + bpc + layout)
+    fr = make_intra_residuals(make_intra_frame(w, h, bpc, layout, rng, ibc_frac=0.6, cfl_dev_frac=0.2), bpc, rng)
+    b = fr["blocks"]
+    ibc = b[b["mode"] == 96]
+    assert len(ibc) > 20
+    if layout != 3:
+        mvx = (ibc["reserved"] & 0xFFFF).astype(np.int16)
+        assert ((ibc["plane"] > 0) & ((mvx & 15) != 0)).any(), "no half-pel chroma block copy"
+    init_cur = Frame(w, h, bpc, layout)
+    init = [init_cur.buffer_np(p) for p in range(len(init_cur.planes))]
+    exp, _ = oracle_lib.intra_recon(init, bpc, b, fr["tx_blocks"][fr["tx_of_block"]], fr["ac"], fr["idx"], fr["pal"],
+                                    fr["coef"])
+    intra = IntraFrame(gpu, fr)
+    for fused in (False, True):
+        cur = Frame(w, h, bpc, layout)
+        if fused:
+            intra.recon(cur.picture())
+            device_status(gpu)
+        else:
+            intra.step(cur.picture())
+            torch.cuda.synchronize()
+        for p in range(len(cur.planes)):
+            got = cur.buffer_np(p)
+            if not np.array_equal(got, exp[p]):
+                bad = np.argwhere(got != exp[p])
+                raise AssertionError(f"fused={fused} plane {p}: {len(bad)} mismatches, first at {bad[0]}")

@@ -107,8 +107,8 @@ def test_oracle_intra_block_copy(bpc):
     chroma = rng.integers(0, 1 << bpc, size=(32, 32)).astype(dt)
     mv = lambda lx, ly: (lx * 8 & 0xFFFF) | ((ly * 8 & 0xFFFF) << 16)  # noqa: E731
     blk = np.zeros(2, INTRA_DTYPE)
-    blk[0] = (32, 32, 16, 8, 0, 96, 0, 0, 0, 0, 64, 64, 32, 32, 0, 0, mv(-20, -24))
-    blk[1] = (16, 16, 8, 8, 1, 96, 0, 0, 3, 0, 32, 32, 16, 16, 0, 0, mv(-9, -20))
+    blk[0] = (32, 32, 16, 8, 0, 96, 0, 0, 0, 0, 64, 64, 64, 64, 0, 0, mv(-20, -24))
+    blk[1] = (16, 16, 8, 8, 1, 96, 0, 0, 3, 0, 32, 32, 32, 32, 0, 0, mv(-9, -20))
     z = np.zeros(1, np.int16)
     out = oracle_lib.intra_blocks([luma, chroma, chroma.copy()], bpc, blk, z, np.zeros(1, np.uint8), np.zeros(8, dt))
     assert np.array_equal(out[0][32:40, 32:48], luma[8:16, 12:28])
@@ -120,3 +120,30 @@ def test_oracle_intra_block_copy(bpc):
     px = (16 * a + 8 * (b - a) + ((1 << (4 - ib)) >> 1)) >> (4 - ib)
     exp = np.clip((px + ((1 << ib) >> 1)) >> ib, 0, (1 << bpc) - 1)
     assert np.array_equal(out[1][16:24, 16:24].astype(np.int64), exp)
+
+
+@pytest.mark.parametrize("bpc", [8, 10])
+def test_oracle_intra_block_copy_edge(bpc):
+    """A half-pel chroma block copy whose source ends at the reference area's right / bottom
+    border (max_w x max_h = f.bw*4 >> ss_hor by f.bh*4 >> ss_ver): the tap past the border reads
+    the replicated last column / row (emu_edge, recon.rs:2052-2083), not the padding."""
+    from rav1d_amd import INTRA_DTYPE
+    rng = np.random.default_rng(17 + bpc)
+    dt = np.uint8 if bpc == 8 else np.uint16
+    luma = rng.integers(0, 1 << bpc, size=(64, 64)).astype(dt)
+    chroma = rng.integers(0, 1 << bpc, size=(32, 48)).astype(dt)   # 8 columns of padding beyond max_w=40
+    mv = lambda lx, ly: (lx * 8 & 0xFFFF) | ((ly * 8 & 0xFFFF) << 16)  # noqa: E731
+    blk = np.zeros(1, INTRA_DTYPE)
+    # chroma 8x8 at (32, 24) in a 40x32 area; luma mv (-1, -1): offset (-1, -1), phases 8/16
+    blk[0] = (32, 24, 8, 8, 1, 96, 0, 0, 3, 0, 40, 32, 40, 32, 0, 0, mv(-1, -1))
+    z = np.zeros(1, np.int16)
+    out = oracle_lib.intra_blocks([luma, chroma, chroma.copy()], bpc, blk, z, np.zeros(1, np.uint8), np.zeros(8, dt))
+    src = chroma.astype(np.int64)[:32, :40]
+    src = np.pad(src, ((0, 1), (0, 1)), mode="edge")
+    ib = 4 if bpc == 8 else 14 - bpc
+    rnd = lambda v, s: (v + ((1 << s) >> 1)) >> s  # noqa: E731
+    a, b = src[23:32, 31:39], src[23:32, 32:40]
+    hm = rnd(16 * a + 8 * (b - a), 4 - ib)
+    v = rnd(16 * hm[:-1] + 8 * (hm[1:] - hm[:-1]), 4 + ib)
+    exp = np.clip(v, 0, (1 << bpc) - 1)
+    assert np.array_equal(out[1][24:32, 32:40].astype(np.int64), exp)
