@@ -1,0 +1,96 @@
+/*
+ * mi_av1dec.h — C-ABI of the host front-end: AV1 OBUs in, pass-2 work lists out.
+ *
+ * This is the CPU side north_star keeps on the host (rav1d's OBU / msac / mode and
+ * coefficient decoding: src/obu.rs:2662, src/msac.rs, src/decode.rs:1131-4067,
+ * src/recon.rs:478-2023, src/lf_mask.rs:380-723), restated in C++ (rav1d_amd/host/) and built
+ * as rav1d_amd/libmi_av1dec.so. Instead of reconstructing pixels it emits, per frame, the
+ * descriptor lists of mi_av1dsp.h (MiIntraBlock / MiTxBlock, coefficient arena, Av1Filter
+ * masks and levels, Av1Restoration units, film-grain data) that the gfx950 kernels execute.
+ *
+ * Threading: one MiDec per stream; calls on one MiDec are serialised by the caller.
+ * Errors: 0 / positive counts, or a negative errno (-EINVAL bitstream error, -ENOMEM,
+ * -ENOTSUP for a coding tool this front-end does not decode yet); mi_dec_error() explains.
+ */
+#ifndef MI_AV1DEC_H
+#define MI_AV1DEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mi_av1dsp.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MI_AV1DEC_ABI_VERSION 1
+
+/* The pass-2 work of one decoded frame. All pointers stay valid until the next
+ * mi_dec_next() / mi_dec_destroy() on the same decoder. */
+typedef struct MiDecFrame {
+    int32_t w, h;                 /* coded luma size (frame_hdr.width[0], height) */
+    int32_t up_w;                 /* luma width after super-resolution (width[1]); == w without */
+    int32_t render_w, render_h;
+    int32_t bpc, layout, sb128;
+    /* intra path, decode order: blocks[i] predicted then tx[i] added (eob < 0: no residual);
+     * deps[dep_start[i] .. dep_start[i + 1]) = earlier blocks owning pixels blocks[i] reads */
+    const MiIntraBlock *intra;
+    const MiTxBlock *intra_tx;
+    int32_t n_intra;
+    const int32_t *dep_start;     /* n_intra + 1 entries */
+    const int32_t *deps;
+    int32_t n_deps;
+    /* residuals of inter blocks (added after motion compensation, before the intra path) */
+    const MiTxBlock *inter_tx;
+    int32_t n_inter_tx;
+    /* coefficient arena: int16_t (8 bpc) or int32_t (10/12 bpc), ncoef entries */
+    const void *coef;
+    size_t ncoef;
+    const uint8_t *idx;           /* palette indices (MI_IPRED_PAL aux_off) */
+    size_t nidx;
+    const void *pal;              /* palette colours, pixels of bpc (MI_IPRED_PAL pal_off) */
+    size_t npal;
+    /* deblocking (MiLoopFilter inputs) */
+    int32_t filter_y, filter_uv;
+    const uint8_t *lf_level;      /* [rows][b4_stride][4] */
+    int32_t b4_stride;
+    const MiAv1Filter *lf_masks;  /* [sb128h][sb128w], tile fixups applied */
+    int32_t sb128w, sb128h;
+    uint8_t lim_e[64], lim_i[64];
+    /* CDEF (seq_hdr.cdef) */
+    int32_t cdef_on, cdef_damping;
+    uint8_t cdef_y[8], cdef_uv[8];
+    /* loop restoration */
+    const MiAv1Restoration *lr_mask;   /* [sb128h][lr_sb128w] */
+    int32_t lr_sb128w, restore_planes, lr_unit_size[2];
+} MiDecFrame;
+
+/* One decoder event: a frame to reconstruct into picture `pic_id` (frame != NULL; its inter
+ * prediction reads pictures ref_pic[]), and/or a picture to output (show_pic >= 0, with film
+ * grain when fg_present). Pictures listed in release[] are no longer referenced. */
+typedef struct MiDecEvent {
+    const MiDecFrame *frame;
+    int32_t pic_id;
+    int32_t ref_pic[7];
+    int32_t show_pic;
+    int32_t fg_present;
+    MiFilmGrainData fg;
+    const int32_t *release;
+    int32_t n_release;
+} MiDecEvent;
+
+typedef struct MiDec MiDec;
+
+int  mi_dec_create(MiDec **out);
+void mi_dec_destroy(MiDec *d);
+/* Feed one temporal unit (any whole number of OBUs). */
+int  mi_dec_send(MiDec *d, const uint8_t *data, size_t size);
+/* Next event: 1 and *ev filled, 0 when none is pending, or -errno. */
+int  mi_dec_next(MiDec *d, MiDecEvent *ev);
+const char *mi_dec_error(const MiDec *d);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MI_AV1DEC_H */

@@ -1,0 +1,71 @@
+/*
+ * decode.c — the oracle's frame reconstruction driver: runs one front-end work list
+ * (MiDecFrame, include/mi_av1dec.h) through the CPU restatement in the reference's order.
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * Order, as rav1d decodes a frame with one thread (decode.rs decode_frame_main ->
+ * decode_tile_sbrow + filter_sbrow; recon.rs:4019-4211 filter_sbrow):
+ *   reconstruction of every block in decode order (recon_b_intra: prediction, then itxfm_add
+ *   per transform block) -> deblock (lf_apply.rs, sbrow order, in place) -> CDEF
+ *   (cdef_apply.rs, reads the deblocked picture) -> loop restoration (lr_apply.rs, reads the
+ *   CDEF output and the deblocked rows across stripe edges).
+ * Film grain is applied by the caller to output pictures only (fg_apply.rs).
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "mi_av1dec.h"
+#include "oracle.h"
+
+void oracle_cdef_frame(void *const dst[3], void *const src[3], const ptrdiff_t strides[3], int w,
+                       int h, int layout, int bpc, const void *masks_, int sb128w, int damping_hdr,
+                       const uint8_t *y_strength, const uint8_t *uv_strength);
+void oracle_deblock_frame(void *const planes[3], const ptrdiff_t strides[3], int w, int h,
+                          int layout, int bpc, const uint8_t *level, ptrdiff_t b4_stride,
+                          const void *masks_, int sb128w, int sb128, const uint8_t *lut_e,
+                          const uint8_t *lut_i, int filter_y, int filter_uv);
+void oracle_lr_frame(void *const dst[3], void *const cdef[3], void *const deblocked[3],
+                     const ptrdiff_t strides[3], int w, int h, int layout, int bpc, int sb128,
+                     int restore_planes, const int unit_size_log2[2], const void *lr_mask,
+                     int sb128w);
+
+/* pic: the picture to reconstruct (128-aligned planes, cleared or not); scratch1/2: two more
+ * pictures of the same geometry. On return the final (reference) picture is in out[], which
+ * points at one of the three. */
+void oracle_decode_frame(const MiDecFrame *f, void *const pic[3], void *const scratch1[3],
+                         void *const scratch2[3], const ptrdiff_t strides[3], void **out)
+{
+    const int bpc = f->bpc, layout = f->layout;
+    const int ss_ver = layout == 1;
+    const int nplanes = layout ? 3 : 1;
+    const size_t cb = bpc == 8 ? 2 : 4;
+
+    /* 1. intra path in decode order (the arena is consumed: work on a copy) */
+    if (f->n_intra) {
+        void *coef = malloc(f->ncoef * cb + 16);
+        memcpy(coef, f->coef, f->ncoef * cb);
+        const ptrdiff_t st2[2] = { strides[0], strides[1] };
+        oracle_intra_recon(pic, st2, bpc, f->intra, f->intra_tx, f->n_intra, NULL, f->idx, f->pal, coef);
+        free(coef);
+    }
+    /* 2. deblocking, in place */
+    if (f->filter_y)
+        oracle_deblock_frame(pic, strides, f->w, f->h, layout, bpc, f->lf_level, f->b4_stride, f->lf_masks,
+                             f->sb128w, f->sb128, f->lim_e, f->lim_i, f->filter_y, f->filter_uv);
+    /* 3. CDEF: deblocked -> scratch1 */
+    void *const *cdef_out = pic;
+    if (f->cdef_on) {
+        oracle_cdef_frame(scratch1, pic, strides, f->w, f->h, layout, bpc, f->lf_masks, f->sb128w,
+                          f->cdef_damping, f->cdef_y, f->cdef_uv);
+        cdef_out = scratch1;
+    }
+    /* 4. loop restoration: (CDEF output, deblocked) -> scratch2 */
+    void *const *final = cdef_out;
+    if (f->restore_planes) {
+        oracle_lr_frame(scratch2, (void *const *)cdef_out, pic, strides, f->w, f->h, layout, bpc, f->sb128,
+                        f->restore_planes, f->lr_unit_size, f->lr_mask, f->lr_sb128w);
+        final = scratch2;
+    }
+    (void)ss_ver;
+    for (int p = 0; p < 3; p++) out[p] = p < nplanes ? final[p] : NULL;
+}

@@ -1,0 +1,114 @@
+"""Host front-end binding: IVF demux (tools/input/ivf.rs) and the C-ABI of
+rav1d_amd/libmi_av1dec.so (include/mi_av1dec.h), which parses AV1 OBUs into per-frame work
+lists for the gfx950 kernels. No pixels are produced here."""
+import ctypes
+import os
+import struct
+import subprocess
+
+from . import MiFilmGrainData
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+DEC_PATH = os.environ.get("MI_DEC_LIB") or os.path.join(HERE, "libmi_av1dec.so")
+
+_dec = None
+
+
+class MiDecFrame(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_int32), ("h", ctypes.c_int32), ("up_w", ctypes.c_int32),
+                ("render_w", ctypes.c_int32), ("render_h", ctypes.c_int32),
+                ("bpc", ctypes.c_int32), ("layout", ctypes.c_int32), ("sb128", ctypes.c_int32),
+                ("intra", ctypes.c_void_p), ("intra_tx", ctypes.c_void_p), ("n_intra", ctypes.c_int32),
+                ("dep_start", ctypes.c_void_p), ("deps", ctypes.c_void_p), ("n_deps", ctypes.c_int32),
+                ("inter_tx", ctypes.c_void_p), ("n_inter_tx", ctypes.c_int32),
+                ("coef", ctypes.c_void_p), ("ncoef", ctypes.c_size_t),
+                ("idx", ctypes.c_void_p), ("nidx", ctypes.c_size_t),
+                ("pal", ctypes.c_void_p), ("npal", ctypes.c_size_t),
+                ("filter_y", ctypes.c_int32), ("filter_uv", ctypes.c_int32),
+                ("lf_level", ctypes.c_void_p), ("b4_stride", ctypes.c_int32),
+                ("lf_masks", ctypes.c_void_p), ("sb128w", ctypes.c_int32), ("sb128h", ctypes.c_int32),
+                ("lim_e", ctypes.c_uint8 * 64), ("lim_i", ctypes.c_uint8 * 64),
+                ("cdef_on", ctypes.c_int32), ("cdef_damping", ctypes.c_int32),
+                ("cdef_y", ctypes.c_uint8 * 8), ("cdef_uv", ctypes.c_uint8 * 8),
+                ("lr_mask", ctypes.c_void_p), ("lr_sb128w", ctypes.c_int32), ("restore_planes", ctypes.c_int32),
+                ("lr_unit_size", ctypes.c_int32 * 2)]
+
+
+class MiDecEvent(ctypes.Structure):
+    _fields_ = [("frame", ctypes.POINTER(MiDecFrame)), ("pic_id", ctypes.c_int32),
+                ("ref_pic", ctypes.c_int32 * 7), ("show_pic", ctypes.c_int32),
+                ("fg_present", ctypes.c_int32), ("fg", MiFilmGrainData),
+                ("release", ctypes.POINTER(ctypes.c_int32)), ("n_release", ctypes.c_int32)]
+
+
+def build_dec():
+    subprocess.run(["make", "-s", "-C", os.path.join(HERE, "host")], check=True)
+
+
+def dec_lib():
+    global _dec
+    if _dec is None:
+        if not os.path.exists(DEC_PATH):
+            raise RuntimeError(f"{DEC_PATH} missing: build it with `make -C rav1d_amd/host`")
+        d = ctypes.CDLL(DEC_PATH)
+        d.mi_dec_create.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        d.mi_dec_destroy.argtypes = [ctypes.c_void_p]
+        d.mi_dec_destroy.restype = None
+        d.mi_dec_send.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
+        d.mi_dec_next.argtypes = [ctypes.c_void_p, ctypes.POINTER(MiDecEvent)]
+        d.mi_dec_error.argtypes = [ctypes.c_void_p]
+        d.mi_dec_error.restype = ctypes.c_char_p
+        _dec = d
+    return _dec
+
+
+def ivf_frames(path_or_bytes):
+    """Yield the frame payloads of an IVF file (32-byte header, then 12-byte frame headers:
+    u32 size, u64 timestamp; tools/input/ivf.rs:224)."""
+    data = path_or_bytes if isinstance(path_or_bytes, (bytes, bytearray)) else open(path_or_bytes, "rb").read()
+    if data[:4] != b"DKIF":
+        raise ValueError("not an IVF file")
+    hdr_len = struct.unpack_from("<H", data, 6)[0]
+    off = hdr_len
+    while off + 12 <= len(data):
+        size = struct.unpack_from("<I", data, off)[0]
+        off += 12
+        if off + size > len(data):
+            break
+        yield bytes(data[off:off + size])
+        off += size
+
+
+class Av1Decoder:
+    """One stream. send() one temporal unit, then drain events()."""
+
+    def __init__(self):
+        self.lib = dec_lib()
+        self.h = ctypes.c_void_p()
+        r = self.lib.mi_dec_create(ctypes.byref(self.h))
+        if r:
+            raise RuntimeError(f"mi_dec_create: {r}")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.mi_dec_destroy(self.h)
+            self.h = None
+
+    def error(self):
+        return self.lib.mi_dec_error(self.h).decode()
+
+    def send(self, data):
+        r = self.lib.mi_dec_send(self.h, data, len(data))
+        if r < 0:
+            raise RuntimeError(f"mi_dec_send: {r} ({self.error()})")
+
+    def events(self):
+        """Yield MiDecEvent structs; each is valid only until the next one is requested."""
+        ev = MiDecEvent()
+        while True:
+            r = self.lib.mi_dec_next(self.h, ctypes.byref(ev))
+            if r < 0:
+                raise RuntimeError(f"mi_dec_next: {r} ({self.error()})")
+            if r == 0:
+                return
+            yield ev
