@@ -44,7 +44,9 @@ typedef struct MiDecFrame {
     /* residuals of inter blocks (added after motion compensation, before the intra path) */
     const MiTxBlock *inter_tx;
     int32_t n_inter_tx;
-    /* coefficient arena: int16_t (8 bpc) or int32_t (10/12 bpc), ncoef entries */
+    /* coefficient arena: int16_t (8 bpc) or int32_t (10/12 bpc), ncoef entries. Entries
+     * 0..15 are a reserved zero block: a transform block without residual (skip, or an
+     * all-zero block) has eob < 0 and coef_off 0, so any consumer adds nothing. */
     const void *coef;
     size_t ncoef;
     const uint8_t *idx;           /* palette indices (MI_IPRED_PAL aux_off) */
@@ -79,6 +81,31 @@ typedef struct MiDecEvent {
     const int32_t *release;
     int32_t n_release;
 } MiDecEvent;
+
+/* ---- device execution of a decoded frame (these two live in librav1d_amd.so) ----
+ *
+ * The pictures one frame's pass 2 writes (device planes, all of one geometry):
+ * recon = prediction + residual, deblocked (recon -> deblocked), cdef (deblocked -> cdef),
+ * restored ((cdef, deblocked) -> restored). Stages the frame header switches off are skipped,
+ * not copied: *final receives the index (0 recon .. 3 restored) of the picture holding the
+ * frame's reference-quality output (the picture rav1d leaves in f.sr_cur after
+ * filter_sbrow: recon.rs:4019-4211). */
+typedef struct MiFramePictures {
+    MiPicture recon, deblocked, cdef, restored;
+} MiFramePictures;
+
+/* Enqueue one frame's reconstruction and in-loop filters on `stream` (recon_b_intra over the
+ * intra work list in one persistent launch, blocks reordered by dependency level; then
+ * mi_deblock_frame_to / mi_cdef_frame / mi_lr_frame). The host arrays of `f` are copied during
+ * the call (pinned staging + async upload), so `f` may be released on return. Calls on one
+ * context must use one stream. 0 or -errno (-EINVAL malformed work list, -ENOMEM, -EIO). */
+int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int *final, void *stream);
+
+/* Wait for the work enqueued on `stream` and report device-side failures of the frame(s):
+ * 0, or -EIO when a block's dependency wait gave up or a block was never reconstructed (the
+ * pictures are then not valid). rav1d reports such a frame as a decode error (Dav1dResult,
+ * src/error.rs). */
+int mi_frame_end(MiCtx *ctx, void *stream);
 
 typedef struct MiDec MiDec;
 

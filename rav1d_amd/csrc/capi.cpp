@@ -13,29 +13,8 @@
 #include <string>
 #include <vector>
 #include "common.h"
+#include "ctx.h"
 
-struct MiCtx {
-    int device = 0;
-    int last_error = 0;
-    // film-grain scratch (grain templates, scaling LUTs, block offsets)
-    int16_t *fg_lut = nullptr;
-    uint8_t *fg_scaling = nullptr;
-    uint8_t *fg_offsets = nullptr;
-    size_t fg_offsets_bytes = 0;
-    // persistent intra reconstruction: per-block done epochs, queue heads, error word
-    uint32_t *ir_done = nullptr;
-    size_t ir_done_n = 0;
-    int *ir_words = nullptr;      // [0..63] queue heads, [64] error, [72..79] XCD worker ranks
-    uint32_t ir_epoch = 0;
-    int ir_last_n[mi::kIrMaxFrames] = {0}, ir_last_frames = 0;
-    ~MiCtx() {
-        if (ir_done) (void)hipFree(ir_done);
-        if (ir_words) (void)hipFree(ir_words);
-        if (fg_lut) (void)hipFree(fg_lut);
-        if (fg_scaling) (void)hipFree(fg_scaling);
-        if (fg_offsets) (void)hipFree(fg_offsets);
-    }
-};
 
 namespace {
 

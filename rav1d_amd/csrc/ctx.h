@@ -1,0 +1,36 @@
+// ctx.h — MiCtx, the per-stream device context behind include/mi_av1dsp.h (one per decoder
+// frame context; calls on one context are serialised by the caller and use one stream).
+#pragma once
+#include "common.h"
+
+struct MiCtx {
+    int device = 0;
+    int last_error = 0;
+    // film-grain scratch (grain templates, scaling LUTs, block offsets)
+    int16_t *fg_lut = nullptr;
+    uint8_t *fg_scaling = nullptr;
+    uint8_t *fg_offsets = nullptr;
+    size_t fg_offsets_bytes = 0;
+    // persistent intra reconstruction: per-block done epochs, queue heads, error word
+    uint32_t *ir_done = nullptr;
+    size_t ir_done_n = 0;
+    int *ir_words = nullptr;      // [0..63] queue heads, [64] error, [72..79] XCD worker ranks
+    uint32_t ir_epoch = 0;
+    int ir_last_n[mi::kIrMaxFrames] = {0}, ir_last_frames = 0;
+    // frame executor (frame_exec.cpp): device copy of one frame's descriptors, staged through
+    // pinned host memory; `fx_ev` marks when the staging buffer may be rewritten
+    uint8_t *fx_dev = nullptr, *fx_host = nullptr;
+    size_t fx_dev_bytes = 0, fx_host_bytes = 0;
+    hipEvent_t fx_ev = nullptr;
+    bool fx_ev_pending = false;
+    ~MiCtx() {
+        if (fx_ev) (void)hipEventDestroy(fx_ev);
+        if (fx_dev) (void)hipFree(fx_dev);
+        if (fx_host) (void)hipHostFree(fx_host);
+        if (ir_done) (void)hipFree(ir_done);
+        if (ir_words) (void)hipFree(ir_words);
+        if (fg_lut) (void)hipFree(fg_lut);
+        if (fg_scaling) (void)hipFree(fg_scaling);
+        if (fg_offsets) (void)hipFree(fg_offsets);
+    }
+};

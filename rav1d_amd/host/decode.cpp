@@ -1638,8 +1638,9 @@ int FrameDec::run(FrameResult &res, std::string &err) {
     fw.ss_ver = ss_ver;
     fw.sb128 = s.sb128;
     fw.intra_only = 1;
-    fw.ncoef = 0;
-    fw.coef.clear();
+    // arena entries 0..15: the reserved zero block that residual-free records point at
+    fw.ncoef = 16;
+    fw.coef.assign((size_t)16 * (s.bpc == 8 ? 2 : 4), 0);
     fw.b4_stride = b4_stride;
     fw.sb128w = sb128w;
     fw.sb128h = sb128h;

@@ -1,0 +1,61 @@
+"""Stream decode on the device: the front-end's per-frame work lists (rav1d_amd/libmi_av1dec.so,
+include/mi_av1dec.h) executed by librav1d_amd.so's frame executor (mi_frame_run / mi_frame_end).
+
+This is the host loop rav1d runs in decode.rs:4526-4550 (decode_tile_sbrow, then filter_sbrow)
+with the pixel work moved to the GPU: for every decoder event, the frame's reconstruction and
+in-loop filters are enqueued on one stream into device pictures; shown pictures are handed to
+the caller (on the device). There is no CPU pixel path here.
+"""
+import ctypes
+
+from . import MiFramePictures, check, lib
+from . import frame as F
+from .av1dec import Av1Decoder, ivf_frames
+
+
+class DevicePictureSet:
+    """The four pictures one frame's pass 2 writes (recon, deblocked, cdef, restored)."""
+
+    def __init__(self, w, h, bpc, layout):
+        self.frames = [F.Frame(w, h, bpc, layout) for _ in range(4)]
+        self.pics = MiFramePictures()
+        for i, fr in enumerate(self.frames):
+            self.pics.pics[i] = fr.picture()
+        self.final = 0
+
+    def output(self):
+        return self.frames[self.final]
+
+
+def run_frame(ctx, fr, stream=None):
+    """Enqueue one MiDecFrame on the device; returns its DevicePictureSet (output() = the
+    reference-quality picture once the stream reaches it)."""
+    ps = DevicePictureSet(fr.w, fr.h, fr.bpc, fr.layout)
+    final = ctypes.c_int(-1)
+    check(lib().mi_frame_run(ctx.h, ctypes.byref(fr), ctypes.byref(ps.pics), ctypes.byref(final),
+                             F._stream_ptr(stream)), "mi_frame_run")
+    ps.final = final.value
+    return ps
+
+
+def frame_end(ctx, stream=None):
+    check(lib().mi_frame_end(ctx.h, F._stream_ptr(stream)), "mi_frame_end")
+
+
+def decode_ivf(ctx, data, stream=None, sync_each=True):
+    """Decode an IVF stream on the device; yields the shown pictures (Frame, device planes) in
+    output order. With sync_each, every frame is checked with mi_frame_end before it is shown."""
+    dec = Av1Decoder()
+    pics = {}
+    for tu in ivf_frames(data):
+        dec.send(tu)
+        for ev in dec.events():
+            if ev.frame:
+                pics[ev.pic_id] = run_frame(ctx, ev.frame.contents, stream)
+                if sync_each:
+                    frame_end(ctx, stream)
+            if ev.show_pic >= 0:
+                yield pics[ev.show_pic].output()
+            for i in range(ev.n_release):
+                pics.pop(ev.release[i], None)
+    frame_end(ctx, stream)

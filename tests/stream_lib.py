@@ -1,0 +1,86 @@
+"""Whole-stream decode through the front-end (rav1d_amd/libmi_av1dec.so) and the oracle's frame
+driver (oracle/decode.c), hashed like the reference's md5 muxer (tools/output/md5.rs:541-637).
+
+TEST INFRASTRUCTURE ONLY: this is the checker that pins the CPU restatement (and, through it,
+the GPU path) to the reference's own MD5 vectors (tests/dav1d-test-data/**/meson.build).
+"""
+import ctypes
+import hashlib
+
+import numpy as np
+
+from rav1d_amd.av1dec import Av1Decoder, MiDecFrame, ivf_frames
+from tests import oracle_lib
+
+
+def _bind(o):
+    if getattr(o, "_dec_bound", False):
+        return o
+    vp = ctypes.c_void_p
+    o.oracle_decode_frame.argtypes = [ctypes.POINTER(MiDecFrame), vp, vp, vp, vp, vp]
+    o.oracle_decode_frame.restype = None
+    o._dec_bound = True
+    return o
+
+
+def alloc_picture(w, h, bpc, layout):
+    """dav1d default-allocator geometry (src/picture.rs:98-115): 128-aligned planes."""
+    aw, ah = (w + 127) & ~127, (h + 127) & ~127
+    ss_hor, ss_ver = int(layout in (1, 2)), int(layout == 1)
+    dt = np.uint8 if bpc == 8 else np.uint16
+    planes = [np.zeros((ah, aw), dt)]
+    if layout:
+        planes += [np.zeros((ah >> ss_ver, aw >> ss_hor), dt) for _ in range(2)]
+    return planes
+
+
+def md5_update_picture(md5, planes, w, h, layout):
+    """md5_write (tools/output/md5.rs:541-576): visible rows of every plane, pixel bytes LE."""
+    md5.update(np.ascontiguousarray(planes[0][:h, :w]).tobytes())
+    if layout:
+        ss_hor, ss_ver = int(layout in (1, 2)), int(layout == 1)
+        cw, ch = (w + ss_hor) >> ss_hor, (h + ss_ver) >> ss_ver
+        for p in (1, 2):
+            md5.update(np.ascontiguousarray(planes[p][:ch, :cw]).tobytes())
+
+
+def oracle_frame(fr):
+    """Reconstruct one MiDecFrame through the oracle; returns the final planes (1 or 3)."""
+    o = _bind(oracle_lib.load_oracle())
+    pics = [alloc_picture(fr.w, fr.h, fr.bpc, fr.layout) for _ in range(3)]
+    for p in pics:
+        while len(p) < 3:
+            p.append(p[0])
+    arr = [(ctypes.c_void_p * 3)(*[a.ctypes.data for a in p]) for p in pics]
+    st = (ctypes.c_ssize_t * 3)(*[a.strides[0] for a in pics[0]])
+    out = (ctypes.c_void_p * 3)()
+    o.oracle_decode_frame(ctypes.byref(fr), arr[0], arr[1], arr[2], st, out)
+    by_addr = {a.ctypes.data: a for p in pics for a in p}
+    n = 3 if fr.layout else 1
+    return [by_addr[out[i]] for i in range(n)]
+
+
+def decode_stream(data, recon=oracle_frame, max_frames=None):
+    """Decode an IVF stream; returns (md5 hex, frames output). `recon(frame) -> planes` runs the
+    pixel path (oracle by default; the GPU path in the -m gpu tests)."""
+    dec = Av1Decoder()
+    pics = {}
+    md5 = hashlib.md5()
+    shown = 0
+    for tu in ivf_frames(data):
+        dec.send(tu)
+        for ev in dec.events():
+            if ev.frame:
+                fr = ev.frame.contents
+                if fr.up_w != fr.w:
+                    raise NotImplementedError("super-resolution stream")
+                pics[ev.pic_id] = (recon(fr), fr.w, fr.h, fr.layout)
+            if ev.show_pic >= 0:
+                planes, w, h, layout = pics[ev.show_pic]
+                md5_update_picture(md5, planes, w, h, layout)
+                shown += 1
+            for i in range(ev.n_release):
+                pics.pop(ev.release[i], None)
+        if max_frames and shown >= max_frames:
+            break
+    return md5.hexdigest(), shown

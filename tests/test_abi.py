@@ -8,9 +8,25 @@ from rav1d_amd import EXPORTED, LIB_PATH, lib
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _decl(name):
+    txt = open(os.path.join(ROOT, "include", name)).read()
+    return set(re.findall(r"\b(mi_[a-z0-9_]+)\s*\(", txt))
+
+
 def header_symbols():
-    txt = open(os.path.join(ROOT, "include", "mi_av1dsp.h")).read()
-    return sorted(set(re.findall(r"\b(mi_[a-z0-9_]+)\s*\(", txt)))
+    """librav1d_amd.so: every mi_av1dsp.h entry plus mi_av1dec.h's device executor."""
+    dec = _decl("mi_av1dec.h")
+    return sorted(_decl("mi_av1dsp.h") | {s for s in dec if s.startswith("mi_frame_")})
+
+
+def test_front_end_exports_header_symbols():
+    """libmi_av1dec.so (host front-end, no GPU code) exports mi_av1dec.h's mi_dec_* entries."""
+    from rav1d_amd.av1dec import dec_lib
+    L = dec_lib()
+    syms = sorted(s for s in _decl("mi_av1dec.h") if s.startswith("mi_dec_"))
+    assert len(syms) >= 5
+    for s in syms:
+        assert hasattr(L, s), f"{s} missing from libmi_av1dec.so"
 
 
 def test_library_exports_header_symbols():
