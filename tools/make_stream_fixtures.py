@@ -15,10 +15,12 @@ PINNED = [
     ("av1-1-b8-02-allintra", "8-bit/intra/av1-1-b8-02-allintra.ivf"),
     ("issue_320", "8-bit/issues/320_tennis.ivf"),
     ("issue_321", "8-bit/issues/321_tennis.ivf"),
+    ("issue_322", "8-bit/issues/322_tennis.ivf"),
     ("issue_324", "8-bit/issues/324_tennis.ivf"),
     ("issue_325", "8-bit/issues/325_tennis.ivf"),
     ("itut_t35", "8-bit/features/itut_t35.ivf"),
     ("long_leb", "8-bit/features/long_leb.ivf"),
+    ("00000791", "12-bit/data/00000791.ivf"),
 ]
 
 if __name__ == "__main__":
