@@ -19,6 +19,7 @@ import argparse
 import ctypes
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -60,6 +61,8 @@ class Pipeline:
             self.ref_pics = (F.MiPicture * len(self.refs))(*[r.picture() for r in self.refs])
         self.blocks = torch.from_numpy(fr["blocks"].view(np.uint8).copy()).cuda()
         self.coef = torch.from_numpy(fr["coef"].copy()).cuda()
+        self.coef0 = self.coef.clone()               # itx zeroes the arena it consumes
+        self.A0 = [t.clone() for t in self.A.planes]
         self.lf = F.LoopFilterMeta(fr["lf"])
         self.cdef = F.CdefMeta(fr["lf"]["masks"], fr["cdef"], masks_dev=self.lf.masks)
         self.lr = F.LrMeta(fr["lr"])
@@ -129,6 +132,54 @@ class Pipeline:
             stream.wait_event(prep_done)
             timed("fg", lambda: F.check(lib.mi_film_grain_apply(ctx, ctypes.byref(po), ctypes.byref(pg),
                                                                 ctypes.byref(self.fgd), 0, sp), "fg"))
+
+
+    def restore(self):
+        """Pass-2 inputs back to their initial state (coefficient arena, prediction picture),
+        so that one more step reproduces the oracle's single-pass output."""
+        self.coef.copy_(self.coef0)
+        for t, t0 in zip(self.A.planes, self.A0):
+            t.copy_(t0)
+
+    def output_digest(self):
+        """sha256 over the visible pixels of the reference picture O (every plane)."""
+        import hashlib
+        h = hashlib.sha256()
+        for p in range(len(self.O.planes)):
+            h.update(np.ascontiguousarray(self.O.plane_np(p)).tobytes())
+        return h.hexdigest()
+
+
+def oracle_digest(fr):
+    """The same digest over the oracle's output for the same descriptors (CPU restatement)."""
+    import hashlib
+    from tests.pipeline import oracle_pipeline
+    out = oracle_pipeline(fr)["lr"]
+    ss_hor, ss_ver = int(fr["layout"] in (1, 2)), int(fr["layout"] == 1)
+    h = hashlib.sha256()
+    for p, a in enumerate(out):
+        w = fr["w"] if p == 0 else (fr["w"] + ss_hor) >> ss_hor
+        hh = fr["h"] if p == 0 else (fr["h"] + ss_ver) >> ss_ver
+        h.update(np.ascontiguousarray(a[:hh, :w]).tobytes())
+    return h.hexdigest()
+
+
+def broadcast_config(cfg, world):
+    """rank 0's run configuration / seed table, broadcast to every rank."""
+    if world == 1:
+        return cfg
+    box = [cfg]
+    dist.broadcast_object_list(box, src=0)
+    return box[0]
+
+
+def gather_results(local, world):
+    """every rank's {rank, frames, ns, sha256, verified} gathered to all ranks."""
+    if world == 1:
+        return [local]
+    out = [None] * world
+    dist.all_gather_object(out, local)
+    return out
 
 
 def film_grain_8k(ctx, stream, reps=20):
@@ -233,20 +284,41 @@ def intra_1080p8(ctx, reps=5, nframes=24, ndesc=4):
                 kernel="intra_recon_kernel (persistent, one-wave workers, 3 frames per XCD)")
 
 
-def cpu_baseline(fr, budget_s=20.0):
-    """The oracle (single-threaded C restatement, oracle/) on a bounded sample of the same
-    workload: whole 4K10 inter frames through all stages until ~budget_s. Luma Mpixels/s."""
-    from tests.pipeline import oracle_pipeline
-    n, t0 = 0, time.perf_counter()
-    while True:
-        oracle_pipeline(fr)
-        n += 1
-        el = time.perf_counter() - t0
-        if el > budget_s or n >= 20:
-            break
-    return dict(value=round(n * fr["w"] * fr["h"] / el / 1e6, 3), unit="Mpixels/s", cores=1, kind="port",
-                sample=f"{n} frame(s) of the same synthetic 4K10 inter descriptors through oracle/ "
-                       f"(mc+itx+deblock+cdef+lr), 1 thread, {el:.1f}s")
+def host_cpu():
+    """lscpu model / sockets / cores of the host the baseline runs on."""
+    info = {}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "Socket(s)", "Core(s) per socket", "CPU(s)", "Thread(s) per core"):
+                info[k.strip()] = v.strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return info
+
+
+def cpu_baseline(fr, reps=5):
+    """The oracle (the C restatement in oracle/, driven from C by oracle/cpu_bench.c: no Python
+    in the timed loop) on a bounded sample of the same workload: whole 4K10 inter frames through
+    MC + itx + deblock + CDEF + LR. Single thread, and N threads each decoding its own frame
+    (independent streams, as the GPU replicas); best of `reps`. Luma Mpixels/s."""
+    from tests.pipeline import oracle_bench
+    # the box exports OMP_NUM_THREADS as this job's CPU share; nproc counts the whole machine
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    res, t_total = {}, 0.0
+    for th in sorted({1, n}):
+        best = None
+        for _ in range(reps):
+            t = oracle_bench(fr, th, 1)
+            t_total += t
+            best = t if best is None else min(best, t)
+        res[th] = th * fr["w"] * fr["h"] / best / 1e6
+    return dict(value=round(res[n], 3), unit="Mpixels/s", cores=n, kind="port",
+                threads={str(k): round(v, 3) for k, v in res.items()}, host=host_cpu(),
+                sample=f"1 whole synthetic 4K10 inter frame per thread (the bench's own descriptors) through "
+                       f"oracle/ (mc+itx+deblock+cdef+lr) from C, best of {reps}, at 1 and {n} threads "
+                       f"(independent frames per thread); {t_total:.1f}s of CPU-timed work")
 
 
 def timed_region(step, steps, sync, world, device):
@@ -276,6 +348,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fg", action="store_true", help="skip the separate 8K10 film-grain measurement")
     ap.add_argument("--no-intra", action="store_true", help="skip the separate 1080p8 intra measurement")
+    ap.add_argument("--no-verify", action="store_true", help="skip the per-rank oracle check of the output")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -286,7 +359,10 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     stream = torch.cuda.current_stream()
 
-    fr = make_frame(W, H, BPC, LAYOUT, seed=0x4C100001 + rank, with_fg=False, with_mc=True)
+    cfg = broadcast_config({"w": W, "h": H, "bpc": BPC, "layout": LAYOUT,
+                            "seeds": [0x4C100001 + r for r in range(world)]}, world)
+    fr = make_frame(cfg["w"], cfg["h"], cfg["bpc"], cfg["layout"], seed=cfg["seeds"][rank], with_fg=False,
+                    with_mc=True)
     ctx = F.Context(local)
     pipe = Pipeline(ctx, fr)
     torch.cuda.synchronize()
@@ -303,6 +379,16 @@ def main():
     stage_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
 
     elapsed = timed_region(lambda: pipe.step(stream), args.steps, torch.cuda.synchronize, world, "cuda")
+
+    # per-rank correctness: one more step from the initial inputs, digest of the output
+    # picture, checked against the oracle on this rank's host cores (outside the timed region)
+    pipe.restore()
+    pipe.step(stream)
+    torch.cuda.synchronize()
+    digest = pipe.output_digest()
+    verified = digest == oracle_digest(fr) if not args.no_verify else None
+    ranks = gather_results({"rank": rank, "frames": args.steps, "ns": int(elapsed * 1e9),
+                            "sha256": digest, "verified": verified}, world)
 
     dom = max(stage_ms, key=stage_ms.get)
     achieved = pipe.algo[dom] / (stage_ms[dom] / 1e3) / 1e9
@@ -322,10 +408,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u16",
-            "data": "synthetic (seeded inter-frame descriptors per SURVEY.md §8d config 3; no CPU front-end yet)",
+            "data": "synthetic (seeded inter-frame descriptors per SURVEY.md §8d config 3; the front-end decodes intra-only streams so far)",
             "config": {"workload": f"4K10 4:2:0 {W}x{H} inter frame: mc (2 refs, 30% compound) + itx residual "
                                    f"+ deblock + cdef + lr",
                        "parallelism": f"replicas{world} (one independent stream per GPU)"},
+            "verified": all(r["verified"] for r in ranks) if not args.no_verify else None,
+            "per_rank": ranks,
             "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
             "stage_gbs": {k: round(pipe.algo[k] / (stage_ms[k] / 1e3) / 1e9, 1) for k in stage_ms if k in pipe.algo},
             # per launch: algorithmic bytes / mean launch duration (the stage's events span its

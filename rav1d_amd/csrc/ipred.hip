@@ -356,6 +356,18 @@ __constant__ uint8_t k_mode_angle[8] = { 90, 180, 45, 135, 113, 157, 203, 67 };
 // real column / row, then the rounded mean is subtracted. Lane i % 64 owns sample i, so the
 // caller's reads of ac need no barrier. Sc1: the luma was stored during this launch (fused
 // reconstruction), read past L1.
+// A pixel read of the persistent kernel's hand-off: the aligned 4-byte word holding it, loaded
+// `sc1` (L1-bypassing, agent scope), and the pixel extracted. MI355X_MICROARCH.md's hand-off
+// table (row 1) covers 4-, 8- and 16-B `sc1` loads of bytes stored `sc1`, not 1-/2-B loads.
+template <typename Px>
+__device__ __forceinline__ int ld_px_sc1(const Px *q) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(q);
+    const uint32_t w = __hip_atomic_load(reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (sizeof(Px) == 1) return (w >> (8 * (a & 3))) & 0xff;
+    else return (w >> (8 * (a & 2))) & 0xffff;
+}
+
 template <typename Px, bool Sc1>
 __device__ __forceinline__ void cfl_ac_wave(int16_t *ac, const uint8_t *ybase, int64_t stride, int w_pad, int h_pad,
                                             int cw, int ch, int ss_hor, int ss_ver) {
@@ -364,7 +376,7 @@ __device__ __forceinline__ void cfl_ac_wave(int16_t *ac, const uint8_t *ybase, i
     const int64_t ps = stride / (int64_t)sizeof(Px);
     const Px *y = reinterpret_cast<const Px *>(ybase);
     auto L = [&](int64_t o) -> int {
-        if constexpr (Sc1) return __hip_atomic_load(y + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (Sc1) return ld_px_sc1(y + o);
         else return y[o];
     };
     const int sh = 1 + !ss_ver + !ss_hor;
@@ -402,7 +414,7 @@ __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlo
     const Px *pic = reinterpret_cast<const Px *>(a.dst[ib.plane]);
     auto P = [&](int yy, int xx) -> int {
         const Px *q = reinterpret_cast<const Px *>(reinterpret_cast<const uint8_t *>(pic) + (int64_t)yy * st) + xx;
-        if constexpr (Fused) return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (Fused) return ld_px_sc1(q);
         else return *q;
     };
     if constexpr (Fused) {
@@ -555,9 +567,10 @@ __global__ __launch_bounds__(64) void intra_kernel(IpredArgs a) {
 // One launch reconstructs whole intra frames: prediction (intra_block) and the residual
 // (inverse transform + add) of every transform block, in dependency order, without a launch
 // per wavefront step. Frame f is worked on only by the workgroups the dispatcher placed on
-// XCD f (HW_REG_XCC_ID): those share one L2, so a block's pixels, stored plainly (the
-// vector L1 writes through), are visible to every other worker of the frame once the
-// storing wave has drained its stores; readers bypass L1 with `sc1` loads. Each worker wave
+// XCD f (HW_REG_XCC_ID), for L2 locality only: correctness does not depend on it. A block's
+// pixels are published with the hand-off of MI355X_MICROARCH.md's table row 1: 4-/8-B `sc1`
+// stores, the storing wave's vmcnt(0), then one lane's `sc1` done-flag store; readers poll the
+// flag and read pixels with 4-B `sc1` loads only. Each worker wave
 // takes the next block from the frame's queue (an atomic head over blocks in dependency
 // order), waits until every block its edges read has been marked done with this launch's
 // epoch, predicts into an LDS tile, adds the residual there and stores the tile. Deadlock-free:
@@ -741,7 +754,7 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
         DBG(i, 5);
         __syncthreads();
         DBG(i, 6);
-        // store the reconstructed tile: 4-pixel chunks
+        // store the reconstructed tile: 4-pixel chunks, 4-B (8 bpc) / 8-B (hbd) `sc1` stores
         {
             const int w = ib.w, h = ib.h, cpr = w >> 2;
             const int64_t st = fr.ip.stride[ib.plane ? 1 : 0];
@@ -750,22 +763,27 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
                 const int yy = c / cpr, xx = (c % cpr) * 4;
                 const Px *src = lt + yy * w + xx;
                 if constexpr (sizeof(Px) == 2)
-                    *reinterpret_cast<uint2 *>(base + yy * st + xx * 2) =
-                        make_uint2(src[0] | ((uint32_t)src[1] << 16), src[2] | ((uint32_t)src[3] << 16));
+                    __hip_atomic_store(reinterpret_cast<uint64_t *>(base + yy * st + xx * 2),
+                                       (uint64_t)(src[0] | ((uint32_t)src[1] << 16)) |
+                                           ((uint64_t)(src[2] | ((uint32_t)src[3] << 16)) << 32),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 else
-                    *reinterpret_cast<uint32_t *>(base + yy * st + xx) =
-                        src[0] | ((uint32_t)src[1] << 8) | ((uint32_t)src[2] << 16) | ((uint32_t)src[3] << 24);
+                    __hip_atomic_store(reinterpret_cast<uint32_t *>(base + yy * st + xx),
+                                       src[0] | ((uint32_t)src[1] << 8) | ((uint32_t)src[2] << 16) |
+                                           ((uint32_t)src[3] << 24),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         DBG(i, 7);
+        // hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1): every byte
+        // stored `sc1`, the storing wave drains its stores, then ONE lane stores the flag `sc1`
+        // (agent scope); consumers poll it with `sc1` loads and read the pixels with 4-B `sc1`
+        // loads (ld_px_sc1). Each worker workgroup is one wave.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         DBG(i, 8);
         __syncthreads();
         DBG(i, 4);
-        // the flag: a plain store (all lanes, same word) keeps its line in this XCD's L2, where
-        // the consumers' L1-bypassing polls read it (an agent-scope store would write the line
-        // through and drop it, making every poll a fabric round trip)
-        __hip_atomic_store(fr.done + i, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) __hip_atomic_store(fr.done + i, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
