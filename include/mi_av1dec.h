@@ -102,8 +102,9 @@ typedef struct MiFramePictures {
 int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int *final, void *stream);
 
 /* Wait for the work enqueued on `stream` and report device-side failures of the frame(s):
- * 0, or -EIO when a block's dependency wait gave up or a block was never reconstructed (the
- * pictures are then not valid). rav1d reports such a frame as a decode error (Dav1dResult,
+ * 0; -EINVAL when a kernel rejected (skipped) a descriptor no valid stream produces; -EIO
+ * when a block's dependency wait gave up or a block was never reconstructed (the pictures
+ * are then not valid). rav1d reports such a frame as a decode error (Dav1dResult,
  * src/error.rs). */
 int mi_frame_end(MiCtx *ctx, void *stream);
 

@@ -339,8 +339,11 @@ typedef struct MiIntraFrame {
 } MiIntraFrame;
 int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned flags, void *stream);
 
-/* Synchronise `stream` and report device-side failures of the context's persistent
- * launches since the last call: 0, or -ETIMEDOUT (a dependency wait gave up). */
+/* Synchronise `stream` and report device-side failures of the context's launches since the
+ * last call: 0; -EINVAL when a kernel skipped device descriptors the reference could never
+ * issue (mi_itx_frame / mi_intra_recon: a transform type the size's table slot lacks, a size
+ * outside its group, a rectangle outside its plane); -ETIMEDOUT when a dependency wait gave up;
+ * -EIO when a block was never taken. */
 int mi_ctx_device_status(MiCtx *ctx, void *stream);
 
 /* Deblock a whole frame in place: all column edges (every plane), then all row edges.

@@ -67,6 +67,15 @@ struct CallState {
 };
 CallState g_call;
 
+// The context's device words ([0..63] queue heads, [64] dependency-wait give-up, [65]
+// rejected descriptors, [72..79] XCD worker ranks), allocated zeroed on first use.
+int ctx_words(MiCtx *c) {
+    if (c->ir_words) return 0;
+    if (hipMalloc(&c->ir_words, 128 * sizeof(int)) != hipSuccess) return -ENOMEM;
+    if (hipMemset(c->ir_words, 0, 128 * sizeof(int)) != hipSuccess) return -EIO;
+    return 0;
+}
+
 bool same_geometry(const MiPicture *a, const MiPicture *b) {
     return a->bpc == b->bpc && a->w == b->w && a->h == b->h && a->layout == b->layout &&
            a->stride[0] == b->stride[0] && a->stride[1] == b->stride[1];
@@ -108,6 +117,16 @@ int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
     a.coef = (uint8_t *)coef;
     a.bdmax = (1 << pic->bpc) - 1;
     a.zero_coefs = (flags & MI_ITX_KEEP_COEFS) ? 0 : 1;
+    {
+        const int sh = pic->layout == 1 || pic->layout == 2, sv = pic->layout == 1;
+        const int aw = (pic->w + 127) & ~127, ah = (pic->h + 127) & ~127;
+        for (int p = 0; p < (pic->layout ? 3 : 1); p++) {
+            a.pw[p] = p ? aw >> sh : aw;
+            a.ph[p] = p ? ah >> sv : ah;
+        }
+    }
+    if (int e = ctx_words(ctx)) return fail(ctx, e);
+    a.err = ctx->ir_words + 65;
     for (int k = 0; k < MI_N_RECT_TX_SIZES; k++)
         if (size_start[k + 1] < size_start[k]) return fail(ctx, -EINVAL);
     const int wg = mi::itx_fill_schedule(a, size_start);
@@ -310,10 +329,7 @@ int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned
             return fail(ctx, -EINVAL);
         total += (size_t)fr.n;
     }
-    if (!ctx->ir_words) {
-        if (hipMalloc(&ctx->ir_words, 128 * sizeof(int)) != hipSuccess) return fail(ctx, -ENOMEM);
-        if (hipMemset(ctx->ir_words, 0, 128 * sizeof(int)) != hipSuccess) return fail(ctx, -EIO);
-    }
+    if (int e = ctx_words(ctx)) return fail(ctx, e);
     if (total > ctx->ir_done_n) {
         if (ctx->ir_done) (void)hipFree(ctx->ir_done);
         ctx->ir_done = nullptr;
@@ -347,6 +363,11 @@ int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned
         d.done = ctx->ir_done + off;
         d.head = ctx->ir_words + f;
         d.n = fr.n;
+        d.pw = (uint16_t)((fr.pic.w + 127) & ~127);
+        d.ph = (uint16_t)((fr.pic.h + 127) & ~127);
+        d.ss_hor = fr.pic.layout == 1 || fr.pic.layout == 2;
+        d.ss_ver = fr.pic.layout == 1;
+        d.nplanes = fr.pic.layout ? 3 : 1;
         off += (size_t)fr.n;
     }
     // queue heads and XCD worker ranks start from 0 in stream order
@@ -355,6 +376,7 @@ int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned
         return fail(ctx, -EIO);
     a.xcd_rank = ctx->ir_words + 72;
     a.err = ctx->ir_words + 64;
+    a.desc_err = ctx->ir_words + 65;
 #ifdef MI_IR_DEBUG
     static int *dbg = nullptr;
     if (!dbg && hipHostMalloc((void **)&dbg, 65536 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
@@ -382,8 +404,12 @@ int mi_ctx_device_status(MiCtx *ctx, void *stream) {
     if (!ctx) return -EINVAL;
     if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(ctx, -EIO);
     if (!ctx->ir_words) return 0;
-    int w[65];
+    int w[66];
     if (hipMemcpy(w, ctx->ir_words, sizeof(w), hipMemcpyDeviceToHost) != hipSuccess) return fail(ctx, -EIO);
+    if (w[65]) {   // a kernel rejected (skipped) descriptors
+        (void)hipMemset(ctx->ir_words + 65, 0, sizeof(int));
+        return fail(ctx, -EINVAL);
+    }
     if (getenv("MI_DEBUG"))
         fprintf(stderr, "mi_ctx_device_status: heads %d %d %d %d %d %d %d %d err %d\n", w[0], w[1], w[2], w[3], w[4],
                 w[5], w[6], w[7], w[64]);
@@ -722,6 +748,9 @@ int mi_dsp_itxfm_add(int tx, int txtp, void *dst, ptrdiff_t stride, void *coeff,
     a.coef = dcoef;
     a.bdmax = bitdepth_max;
     a.zero_coefs = 1;
+    a.pw[0] = d.w;
+    a.ph[0] = d.h;
+    a.err = (int *)(dblk + 1);   // scratch word: the host checked tx / txtp above
     uint32_t ss1[MI_N_RECT_TX_SIZES + 1];
     for (int k = 0; k <= MI_N_RECT_TX_SIZES; k++) ss1[k] = k > tx ? 1 : 0;
     const int nwg = mi::itx_fill_schedule(a, ss1);

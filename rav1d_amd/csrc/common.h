@@ -82,7 +82,18 @@ struct ItxArgs {
     int wg_size[19];    // tx size launched i-th
     int blk_start[20];  // block ranges per tx size (enum order, as the caller groups them)
     int large_wg0;      // first workgroup of the large-size launch
+    int pw[3], ph[3];   // plane extents (128-aligned picture area; 0 = no such plane)
+    int *err;           // device error word: set when a descriptor is rejected
 };
+
+// Legal TxfmType values of a RectTxfmSize (itx.rs:400-457, 1072-1110): bit t set when the
+// reference's itxfm_add[tx][t] slot is filled.
+__host__ __device__ constexpr uint32_t itx_legal_types(int tx) {
+    return tx == 0 ? 0x1ffffu
+         : imax_c(tx_dim(tx).w, tx_dim(tx).h) == 64 ? 0x1u
+         : imax_c(tx_dim(tx).w, tx_dim(tx).h) == 32 ? 0x201u
+         : (tx_dim(tx).w == 16 && tx_dim(tx).h == 16) ? 0xfffu : 0xffffu;
+}
 // launch order of tx sizes: every side <= 16 first (small launch), then the large launch with
 // the 64-point sizes at its front: their workgroups are few but the longest (a 64-point
 // transform per lane, ~14 us at 4K10), so they start first and the 32-class workgroups fill
@@ -199,6 +210,8 @@ struct IntraReconFrame {
     uint32_t *done;               // per block: epoch when reconstructed
     int *head;                    // queue head
     int n;
+    uint16_t pw, ph;              // luma plane extent (128-aligned picture area)
+    uint8_t ss_hor, ss_ver, nplanes, pad_;
 };
 constexpr int kIrMaxFrames = 24;     // descriptors travel as kernel arguments (4 KB limit)
 struct IntraReconArgs {
@@ -206,9 +219,11 @@ struct IntraReconArgs {
     int *xcd_rank;                // [8] worker counters (zeroed per launch)
     int *err;
     int *dbg;                     // MI_IR_DEBUG builds: host-mapped progress words
+    int *desc_err;                // rejected descriptors (skipped; reported as -EINVAL)
     uint32_t epoch;
     int nframes, zero_coefs;
 };
+static_assert(sizeof(IntraReconArgs) <= 4096, "kernel argument limit");
 int launch_intra_recon(const IntraReconArgs &a, int bpc, int wg_per_xcd, hipStream_t s);
 // launchers (ipred.hip)
 int launch_ipred(const IpredArgs &a, int n, hipStream_t s);

@@ -270,7 +270,8 @@ int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, i
 int mi_frame_end(MiCtx *ctx, void *stream) {
     if (!ctx) return -EINVAL;
     const int r = mi_ctx_device_status(ctx, stream);
-    return r ? (ctx->last_error = -EIO) : 0;
+    // a kernel rejected descriptors: -EINVAL; a stalled or untaken block: -EIO
+    return r ? (ctx->last_error = r == -EINVAL ? -EINVAL : -EIO) : 0;
 }
 
 }  // extern "C"

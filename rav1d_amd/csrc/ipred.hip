@@ -713,6 +713,24 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
         DBG(i, 1);
         const MiIntraBlock ib = fr.ip.iblocks[i];
         const MiTxBlock tb = fr.tx[i];
+        {
+            // a descriptor the reference could never issue (plane / rectangle outside the
+            // picture, a residual of another size or position, an illegal transform type) is
+            // skipped, reported, and still marked done so that no worker waits on it forever
+            const int sh = ib.plane ? fr.ss_hor : 0, sv = ib.plane ? fr.ss_ver : 0;
+            const TxDim td = tx_dim(tb.tx < 19 ? tb.tx : 0);
+            const bool ok_ = ib.plane < fr.nplanes && ib.x + ib.w <= (fr.pw >> sh) && ib.y + ib.h <= (fr.ph >> sv) &&
+                            tb.tx < 19 && td.w == ib.w && td.h == ib.h && tb.x == ib.x && tb.y == ib.y &&
+                            tb.plane == ib.plane && (tb.eob < 0 || (tb.txtp < 17 && ((itx_legal_types(tb.tx) >> tb.txtp) & 1)));
+            const bool ok = __builtin_amdgcn_readfirstlane((int)ok_) != 0;
+            if (!ok) {
+                if (lane == 0) {
+                    atomicOr(a.desc_err, 2);
+                    __hip_atomic_store(fr.done + i, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                continue;
+            }
+        }
         // the residual's row pass needs only the coefficients: before the dependency wait
         Cf *cf = reinterpret_cast<Cf *>(fr.coef) + tb.coef_off;
         int dc = 0;

@@ -84,10 +84,20 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     const int t = threadIdx.x;
     const int lb = t / TPB, j = t % TPB;
     const int bi = a.blk_start[TX] + lwg * BPW + lb;
-    const bool valid = bi < a.blk_start[TX + 1];
+    bool valid = bi < a.blk_start[TX + 1];
 
     MiTxBlock b{};
-    if (valid) b = a.blocks[bi];
+    if (valid) {
+        b = a.blocks[bi];
+        // a descriptor the reference could never issue (wrong size group, a type the size's
+        // table slot lacks, a rectangle outside its plane) is skipped and reported
+        const bool ok = b.tx == TX && b.txtp < 17 && ((itx_legal_types(TX) >> b.txtp) & 1) && b.plane < 3 &&
+                        b.x + Wd <= a.pw[b.plane] && b.y + Ht <= a.ph[b.plane];
+        if (!ok) {
+            valid = false;
+            if (j == 0) atomicOr(a.err, 2);
+        }
+    }
     const int bdmax = a.bdmax;
     Cf *cf = reinterpret_cast<Cf *>(a.coef) + b.coef_off;
     const bool wht = (TX == 0) && b.txtp == 16;
