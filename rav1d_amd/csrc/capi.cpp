@@ -132,12 +132,11 @@ int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
     const int wg = mi::itx_fill_schedule(a, size_start);
     if (wg == 0) return 0;
     if (!blocks || !coef) return fail(ctx, -EINVAL);
-    // The two launches stay serialised on the caller's stream: running the large sizes on a
-    // side stream (event fork/join) measured slower (4K10 itx 56 -> 74 us, 1080p8 intra
-    // 22.6 -> 33.2 ms) than the cross-queue dependency saves.
+    // One launch (itx.hip): the large sizes' workgroups first, the small ones fill in around
+    // them. A side stream for the large sizes (event fork/join) measured slower (4K10 itx
+    // 56 -> 74 us) than the cross-queue dependency saves.
     hipStream_t s = (hipStream_t)stream;
-    const int small_wg = a.large_wg0, large_wg = wg - a.large_wg0;
-    const int r = mi::launch_itx_frame(a, small_wg, large_wg, pic->bpc, s);
+    const int r = mi::launch_itx_frame(a, wg, pic->bpc, s);
     return r ? fail(ctx, -EIO) : 0;
 }
 
@@ -754,7 +753,7 @@ int mi_dsp_itxfm_add(int tx, int txtp, void *dst, ptrdiff_t stride, void *coeff,
     uint32_t ss1[MI_N_RECT_TX_SIZES + 1];
     for (int k = 0; k <= MI_N_RECT_TX_SIZES; k++) ss1[k] = k > tx ? 1 : 0;
     const int nwg = mi::itx_fill_schedule(a, ss1);
-    if (mi::launch_itx_frame(a, a.large_wg0, nwg - a.large_wg0, bpc, s)) return -EIO;
+    if (mi::launch_itx_frame(a, nwg, bpc, s)) return -EIO;
 
     if (dst_dev) {
         for (int y = 0; y < d.h; y++)

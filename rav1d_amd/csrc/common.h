@@ -78,10 +78,9 @@ struct ItxArgs {
     uint8_t *coef;
     int bdmax;
     int zero_coefs;
-    int wg_start[20];   // first workgroup of the i-th size in launch order (small sizes first)
-    int wg_size[19];    // tx size launched i-th
+    int wg_start[20];   // first workgroup of the i-th size in grid order (kItxLaunchOrder)
+    int wg_size[19];    // tx size of the i-th range
     int blk_start[20];  // block ranges per tx size (enum order, as the caller groups them)
-    int large_wg0;      // first workgroup of the large-size launch
     int pw[3], ph[3];   // plane extents (128-aligned picture area; 0 = no such plane)
     int *err;           // device error word: set when a descriptor is rejected
 };
@@ -94,17 +93,14 @@ __host__ __device__ constexpr uint32_t itx_legal_types(int tx) {
          : imax_c(tx_dim(tx).w, tx_dim(tx).h) == 32 ? 0x201u
          : (tx_dim(tx).w == 16 && tx_dim(tx).h == 16) ? 0xfffu : 0xffffu;
 }
-// launch order of tx sizes: every side <= 16 first (small launch), then the large launch with
-// the 64-point sizes at its front: their workgroups are few but the longest (a 64-point
-// transform per lane, ~14 us at 4K10), so they start first and the 32-class workgroups fill
-// the machine around them (large launch 20.2 -> see DESIGN.md §4)
-constexpr int kItxLaunchOrder[19] = { 0, 1, 2, 5, 6, 7, 8, 13, 14, 4, 11, 12, 17, 18, 3, 9, 10, 15, 16 };
-constexpr int kItxNumSmall = 9;
+// order of the tx sizes in the itx grid: the 64-point sizes first (few workgroups, the longest),
+// then the 32-point sizes, then every size with both sides <= 16
+constexpr int kItxLaunchOrder[19] = { 4, 11, 12, 17, 18, 3, 9, 10, 15, 16, 0, 1, 2, 5, 6, 7, 8, 13, 14 };
+// fills wg_start / wg_size / blk_start; returns the grid size
 int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start);
 
-// launchers (itx.hip)
-// small_wg / large_wg: workgroups of the two launches (either may be 0)
-int launch_itx_frame(const ItxArgs &a, int small_wg, int large_wg, int bpc, hipStream_t s);
+// launcher (itx.hip)
+int launch_itx_frame(const ItxArgs &a, int nwg, int bpc, hipStream_t s);
 
 struct LfArgs {
     uint8_t *plane[3];

@@ -4,11 +4,9 @@
 // 1781-1788, 2674-2682, 3116, 4013). Semantics per block are inv_txfm_add_rust
 // (src/itx.rs:64-188; C src/itx_tmpl.c:40-100) and the lossless WHT (src/itx.rs:475-526).
 //
-// Mapping. Blocks arrive grouped by tx size (and by type / DC-only inside a size, so control
-// flow is wave-uniform almost everywhere). Two launches per frame: sizes whose sides are all
-// <= 16 (about 97 % of blocks in real frames; small register and LDS footprint, so many
-// workgroups per CU hide the descriptor -> coefficient -> pixel latency chain) and sizes with
-// a 32- or 64-point side. A 256-lane workgroup takes BPW blocks of one size:
+// Mapping. Blocks arrive grouped by tx size (inside a size, DC-only blocks first and then by
+// position keeps control flow wave-uniform and lets neighbouring blocks of a workgroup share
+// pixel lines). One launch per frame; a 256-lane workgroup takes BPW blocks of one size:
 //   1. every lane reads its block descriptor and immediately issues the loads of the
 //      destination pixels it will own in step 4 (4-pixel row chunks, 4/8-byte vector loads),
 //      so they are in flight during the transforms;
@@ -231,44 +229,33 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     if (valid && dconly && j == 0 && a.zero_coefs) cf[0] = 0;
 }
 
-template <typename Px, typename Cf, typename Lt, bool Wide, bool Large>
+// One launch for every size. The workgroups of the 64- and 32-point sizes come first in the
+// grid: they are few but the longest (a 64-point transform per lane, ~15 us at 4K10), so they
+// start first and the small sizes fill the machine around them. Measured against two launches
+// (sides <= 16, then the rest, each with its own register budget: 66 / 127 VGPRs): 56.3 ->
+// 46.4 us at 4K10; the small sizes lose little from the larger register budget, the large
+// ones stop being a serial tail.
+template <typename Px, typename Cf, typename Lt, bool Wide>
 __global__ __launch_bounds__(kItxThreads) void itx_frame_kernel(ItxArgs a) {
-    __shared__ Lt lds[itx_lds_max(Large)];
-    const int wg = blockIdx.x + (Large ? a.large_wg0 : 0);
-    int i = Large ? kItxNumSmall : 0;
+    __shared__ Lt lds[itx_lds_max(true) > itx_lds_max(false) ? itx_lds_max(true) : itx_lds_max(false)];
+    const int wg = blockIdx.x;
+    int i = 0;
     while (i < 18 && wg >= a.wg_start[i + 1]) i++;
     const int s = a.wg_size[i];
     const int lwg = wg - a.wg_start[i];
-    if constexpr (!Large) {
-        switch (s) {
+    switch (s) {
 #define CASE(n) case n: itx_size<n, Px, Cf, Lt, Wide>(a, lwg, lds); break;
-            CASE(0) CASE(1) CASE(2) CASE(5) CASE(6) CASE(7) CASE(8) CASE(13) CASE(14)
+        CASE(0) CASE(1) CASE(2) CASE(5) CASE(6) CASE(7) CASE(8) CASE(13) CASE(14)
+        CASE(3) CASE(4) CASE(9) CASE(10) CASE(11) CASE(12) CASE(15) CASE(16) CASE(17) CASE(18)
 #undef CASE
-        default: break;
-        }
-    } else {
-        switch (s) {
-#define CASE(n) case n: itx_size<n, Px, Cf, Lt, Wide>(a, lwg, lds); break;
-            CASE(3) CASE(4) CASE(9) CASE(10) CASE(11) CASE(12) CASE(15) CASE(16) CASE(17) CASE(18)
-#undef CASE
-        default: break;
-        }
+    default: break;
     }
-}
-
-template <typename Px, typename Cf, typename Lt, bool Wide>
-static void launch2(const ItxArgs &a, int small_wg, int large_wg, hipStream_t s) {
-    if (small_wg)
-        hipLaunchKernelGGL((itx_frame_kernel<Px, Cf, Lt, Wide, false>), dim3(small_wg), dim3(kItxThreads), 0, s, a);
-    if (large_wg)
-        hipLaunchKernelGGL((itx_frame_kernel<Px, Cf, Lt, Wide, true>), dim3(large_wg), dim3(kItxThreads), 0, s, a);
 }
 
 int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start) {
     int wg = 0;
     for (int i = 0; i < 19; i++) {
         const int sz = kItxLaunchOrder[i];
-        if (i == kItxNumSmall) a.large_wg0 = wg;
         a.wg_start[i] = wg;
         a.wg_size[i] = sz;
         const int n = (int)(size_start[sz + 1] - size_start[sz]);
@@ -279,11 +266,11 @@ int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start) {
     return wg;
 }
 
-int launch_itx_frame(const ItxArgs &a, int small_wg, int large_wg, int bpc, hipStream_t s) {
-    // workgroup ranges are laid out size by size; small sizes first (itx_fill_schedule)
-    if (bpc == 8) launch2<uint8_t, int16_t, int16_t, false>(a, small_wg, large_wg, s);
-    else if (bpc == 10) launch2<uint16_t, int32_t, int16_t, false>(a, small_wg, large_wg, s);
-    else launch2<uint16_t, int32_t, int32_t, true>(a, small_wg, large_wg, s);
+int launch_itx_frame(const ItxArgs &a, int nwg, int bpc, hipStream_t s) {
+    if (nwg <= 0) return 0;
+    if (bpc == 8) hipLaunchKernelGGL((itx_frame_kernel<uint8_t, int16_t, int16_t, false>), dim3(nwg), dim3(kItxThreads), 0, s, a);
+    else if (bpc == 10) hipLaunchKernelGGL((itx_frame_kernel<uint16_t, int32_t, int16_t, false>), dim3(nwg), dim3(kItxThreads), 0, s, a);
+    else hipLaunchKernelGGL((itx_frame_kernel<uint16_t, int32_t, int32_t, true>), dim3(nwg), dim3(kItxThreads), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -159,6 +159,16 @@ def make_itx_frame(w, h, bpc=10, layout=1, seed=0x1D1C0001, dc_frac=0.6, full_fr
                 bpc=bpc, layout=layout)
 
 
+def itx_device_order(blocks):
+    """mi_itx_frame order: grouped by tx size (required); inside a size DC-only blocks first,
+    then by plane and raster position (neighbouring blocks of a workgroup share pixel lines:
+    4K10 itx 46.4 -> 43.5 us against type order). Returns (blocks, size_start)."""
+    dc = (blocks["txtp"] == 0) & (blocks["eob"] < 1)
+    order = np.lexsort((blocks["x"], blocks["y"], blocks["plane"], ~dc, blocks["tx"]))
+    blocks = blocks[order]
+    return blocks, np.searchsorted(blocks["tx"], np.arange(N_RECT_TX_SIZES + 1)).astype(np.uint32)
+
+
 def itx_algorithmic_bytes(blocks, bpc, zero_coefs=True):
     """sum over blocks of coefB*n_coef (+ the zeroing write) + 2*pixB*w*h,
     plus the 16-byte descriptor."""
@@ -415,9 +425,7 @@ def itx_blocks_from_tilings(tilings, bpc, rng, dc_frac=0.6, full_frac=0.1):
             off += c.size
     blocks = np.array(recs, dtype=TXBLOCK_DTYPE)
     coef = np.concatenate(chunks).astype(np.int16 if bpc == 8 else np.int32)
-    order = np.lexsort((blocks["coef_off"], blocks["eob"] > 0, blocks["txtp"], blocks["tx"]))
-    blocks = blocks[order]
-    size_start = np.searchsorted(blocks["tx"], np.arange(N_RECT_TX_SIZES + 1)).astype(np.uint32)
+    blocks, size_start = itx_device_order(blocks)
     return blocks, size_start, coef
 
 
