@@ -1,7 +1,7 @@
 """Debug: fused intra recon on a small frame, short spin limit, host-mapped progress words."""
 import sys, os, time, ctypes
 import numpy as np, torch
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from rav1d_amd.frame import Frame, Context
 from rav1d_amd.ipred_synth import make_intra_frame
 from rav1d_amd.intra import IntraFrame, make_intra_residuals, intra_recon

@@ -1,7 +1,7 @@
 """Film-grain apply timing experiments on a synthetic 4K10 frame (diagnostic, not a test)."""
 import sys, os, ctypes, copy
 import numpy as np, torch
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from rav1d_amd import frame as F
 from rav1d_amd.synth import make_frame
 

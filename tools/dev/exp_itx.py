@@ -1,7 +1,7 @@
 """itx timing experiments on subsets of a synthetic 4K10 frame (diagnostic, not a test)."""
 import sys, os, ctypes
 import numpy as np, torch
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from rav1d_amd import frame as F, ITX_KEEP_COEFS, N_RECT_TX_SIZES
 from rav1d_amd.synth import make_frame, itx_algorithmic_bytes
 

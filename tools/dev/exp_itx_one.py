@@ -2,7 +2,7 @@
 REPS times, for PMC passes (diagnostic)."""
 import os, sys
 import numpy as np, torch
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from rav1d_amd import frame as F  # noqa: E402
 from rav1d_amd.synth import make_frame, itx_region_sort  # noqa: E402
 fr = make_frame(3840, 2160, 10)

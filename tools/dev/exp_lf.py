@@ -2,7 +2,7 @@
 usage: python tools/exp_lf.py [tiles|inplace|both] [noedges]"""
 import sys, os
 import numpy as np, torch
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from rav1d_amd import frame as F
 from rav1d_amd.synth import make_frame, frame_bytes
 

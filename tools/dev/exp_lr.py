@@ -1,7 +1,7 @@
 """Loop-restoration timing on a synthetic 4K10 frame by unit-type mix (diagnostic, not a test)."""
 import sys, os
 import numpy as np, torch
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from rav1d_amd import frame as F
 from rav1d_amd.synth import make_lr_meta, make_texture, frame_bytes
 

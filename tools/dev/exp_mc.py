@@ -1,7 +1,7 @@
 """MC timing on subsets of a synthetic 4K10 inter frame (diagnostic, not a test)."""
 import sys, os, ctypes
 import numpy as np, torch
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from rav1d_amd import frame as F
 from rav1d_amd.synth import make_mc_units, make_texture, mc_sort_units, mc_class_of, mc_algorithmic_bytes
 
