@@ -165,6 +165,9 @@ int fill_mc_args(mi::McArgs &a, const MiPicture *cur, const MiPicture *refs, int
         }
         a.ref_stride[r][0] = refs[r].stride[0];
         a.ref_stride[r][1] = refs[r].stride[1];
+        // mc_kernel forms reference row offsets with 24-bit multiplies
+        for (int k = 0; k < 2; k++)
+            if (refs[r].stride[k] <= 0 || refs[r].stride[k] >= (1 << 24)) return -EINVAL;
     }
     a.nrefs = nrefs;
     a.bpc = cur->bpc;

@@ -19,7 +19,7 @@
 
 namespace mi {
 
-__constant__ int8_t k_subpel[6][15][8] = {
+__constant__ __attribute__((aligned(8))) int8_t k_subpel[6][15][8] = {
 #include "tables/mc_subpel_filters.inc"
 };
 __constant__ uint8_t k_obmc[64] = {
@@ -103,16 +103,20 @@ __device__ __forceinline__ void predict(const McArgs &a, const int16_t *win, int
     const bool bilin = f2d == 9;
     const int SH = bilin ? 4 : 6, ib = a.ib, one = 1 << SH;
     const int th = f2d_type_h(f2d), tv = f2d_type_v(f2d);
-    const int8_t *ph = k_subpel[w > 4 ? th : 3 + (th & 1)][max(s.mx, 1) - 1];
-    const int8_t *pv = k_subpel[h > 4 ? tv : 3 + (tv & 1)][max(s.my, 1) - 1];
+    // the 8 taps of a subpel filter are one aligned 8-byte row of k_subpel: two loads per
+    // direction instead of eight byte loads
+    const uint2 qh = *reinterpret_cast<const uint2 *>(k_subpel[w > 4 ? th : 3 + (th & 1)][max(s.mx, 1) - 1]);
+    const uint2 qv = *reinterpret_cast<const uint2 *>(k_subpel[h > 4 ? tv : 3 + (tv & 1)][max(s.my, 1) - 1]);
     int fh[8], fv[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
         const int id = k == 3 ? one : 0;
         const int bh = k == 3 ? 16 - s.mx : k == 4 ? s.mx : 0;
         const int bv = k == 3 ? 16 - s.my : k == 4 ? s.my : 0;
-        fh[k] = bilin ? bh : s.mx ? (int)ph[k] : id;
-        fv[k] = bilin ? bv : s.my ? (int)pv[k] : id;
+        const int th8 = (int)(int8_t)(((k < 4 ? qh.x : qh.y) >> (8 * (k & 3))) & 0xff);
+        const int tv8 = (int)(int8_t)(((k < 4 ? qv.x : qv.y) >> (8 * (k & 3))) & 0xff);
+        fh[k] = bilin ? bh : s.mx ? th8 : id;
+        fv[k] = bilin ? bv : s.my ? tv8 : id;
     }
     // horizontal taps as 5 aligned pairs: even column (f0,f1)..(f6,f7),(0,0); odd column
     // starts one sample left: (0,f0),(f1,f2),..,(f7,0)
@@ -145,7 +149,7 @@ __device__ __forceinline__ void predict(const McArgs &a, const int16_t *win, int
             v[7] = hmid(q + 7);
             int sum = vrnd;
 #pragma unroll
-            for (int t = 0; t < 8; t++) sum += fv[t] * v[t];
+            for (int t = 0; t < 8; t++) sum += __mul24(fv[t], v[t]);   // |tap| < 2^7, |mid| < 2^16
             out[q] = PREP ? (sum >> vsh) - a.bias : min(max(sum >> vsh, 0), a.bdmax);
 #pragma unroll
             for (int t = 0; t < 7; t++) v[t] = v[t + 1];
@@ -153,9 +157,12 @@ __device__ __forceinline__ void predict(const McArgs &a, const int16_t *win, int
     }
 }
 
+#ifndef MC_MIN_WAVES
+#define MC_MIN_WAVES 1
+#endif
 template <typename Px>
-__global__ __launch_bounds__(64) void mc_kernel(McArgs a, int g) {
-    __shared__ __attribute__((aligned(16))) int16_t win[2][kWinElems];
+__global__ __launch_bounds__(64, MC_MIN_WAVES) void mc_kernel(McArgs a, int g) {
+    __shared__ __attribute__((aligned(16))) int16_t win[kWinElems];
     const int lane = threadIdx.x;
 #ifndef MI_MC_XCD_CHUNK
 #define MI_MC_XCD_CHUNK 1
@@ -233,7 +240,7 @@ __global__ __launch_bounds__(64) void mc_kernel(McArgs a, int g) {
                 const int rr = (int)(((uint32_t)ec * inv) >> 20), qq = ec - rr * Q;
                 const int yy = min(max(r.dy + rr, 0), r.ih - 1);
                 const int x0 = r.dx + 4 * qq;
-                const uint8_t *row = r.base + (int64_t)yy * r.stride;
+                const uint8_t *row = r.base + (uint32_t)__umul24((unsigned)yy, (unsigned)r.stride);
                 if (inside) {
                     if (sizeof(Px) == 2) {
                         const U2a q = *reinterpret_cast<const U2a *>(row + 2 * x0);
@@ -259,27 +266,38 @@ __global__ __launch_bounds__(64) void mc_kernel(McArgs a, int g) {
                 if (o[k] >= 0) *reinterpret_cast<uint2 *>(wdst + o[k]) = make_uint2(v0[k], v1[k]);
         }
     };
-    stage(rs[0], win[0]);
-    if (nref == 2) stage(rs[1], win[1]);
+    // One window buffer: a compound unit's references are staged and filtered one after the
+    // other (half the LDS of staging both, so twice the waves fit a CU).
+    const bool any2 = __any(active && nref == 2);
+    stage(rs[0], win);
     __syncthreads();
-    if (!active) return;
 
     const int r0 = rg * G.R, R = G.R;
     int o0[8], o1[8];
     const int64_t ds = a.dst_stride[p ? 1 : 0];
     uint8_t *dst = a.dst[p] + (int64_t)(b.y + ty0 + r0) * ds;
     const int x = b.x + tx0 + col;
+    const bool prep0 = nref == 2 || b.comp == MI_MC_PREP;
+    if (active) {
+        if (prep0) predict<true>(a, win + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
+        else predict<false>(a, win + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
+    }
+    if (any2) {
+        __syncthreads();                 // every lane is done reading reference 0
+        if (nref == 2) stage(rs[1], win);
+        __syncthreads();
+        if (active && nref == 2) predict<true>(a, win + uu * WN, WS, rs[1], b.filter2d, b.w, b.h, col, r0, R, o1);
+    }
+    if (!active) return;
     if (nref == 1) {
         if (b.comp == MI_MC_PREP) {
             // one side of a compound combined later (mi_mc_combine): the mct intermediate
-            predict<true>(a, win[0] + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
             int16_t *t = a.tmp + b.mask_off + (ty0 + r0) * b.w + tx0 + col;
 #pragma unroll
             for (int q = 0; q < 8; q++)
                 if (q < R) t[q * b.w] = (int16_t)o0[q];
             return;
         }
-        predict<false>(a, win[0] + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
         if (b.comp == MI_MC_OBMC_H || b.comp == MI_MC_OBMC_V) {
             // OBMC lap blended into the block's prediction (blend_h / blend_v, mc_tmpl.c:636-660)
             const bool above = b.comp == MI_MC_OBMC_H;
@@ -301,8 +319,6 @@ __global__ __launch_bounds__(64) void mc_kernel(McArgs a, int g) {
             if (q < R) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];
         return;
     }
-    predict<true>(a, win[0] + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
-    predict<true>(a, win[1] + uu * WN, WS, rs[1], b.filter2d, b.w, b.h, col, r0, R, o1);
     const int ib = a.ib, sign = b.param >> 7;
     if (b.comp == MI_MC_SEG) {
         // w_mask (mc_tmpl.c:661-712): per-pixel weight from |t1 - t2|, t1 = tmp[sign]
