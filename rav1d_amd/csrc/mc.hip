@@ -16,6 +16,7 @@
 // set shifted by one), feeds the vertical 8-tap through a register window, and blends the
 // two predictions in registers (avg / w_avg / mask / w_mask) before the store.
 #include "common.h"
+#include <type_traits>
 
 namespace mi {
 
@@ -97,9 +98,9 @@ struct RefSel {
 // v only, copy) run as the 2-D filter: a missing direction gets the identity tap 1 << SH at
 // the centre, and every shift on the identity side is exact, e.g. h only, put:
 // ((mid << SH) + 2^(SH+ib-1)) >> (SH+ib) == (mid + 2^(ib-1)) >> ib. No lane diverges.
-template <bool PREP>
+template <bool PREP, int R>
 __device__ __forceinline__ void predict(const McArgs &a, const int16_t *win, int WS, const RefSel &s, int f2d,
-                                        int w, int h, int col, int r0, int R, int out[8]) {
+                                        int w, int h, int col, int r0, int out[8]) {
     const bool bilin = f2d == 9;
     const int SH = bilin ? 4 : 6, ib = a.ib, one = 1 << SH;
     const int th = f2d_type_h(f2d), tv = f2d_type_v(f2d);
@@ -272,104 +273,113 @@ __global__ __launch_bounds__(64, MC_MIN_WAVES) void mc_kernel(McArgs a, int g) {
     stage(rs[0], win);
     __syncthreads();
 
-    const int r0 = rg * G.R, R = G.R;
-    int o0[8], o1[8];
-    const int64_t ds = a.dst_stride[p ? 1 : 0];
-    uint8_t *dst = a.dst[p] + (int64_t)(b.y + ty0 + r0) * ds;
-    const int x = b.x + tx0 + col;
-    const bool prep0 = nref == 2 || b.comp == MI_MC_PREP;
-    if (active) {
-        if (prep0) predict<true>(a, win + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
-        else predict<false>(a, win + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, R, o0);
-    }
-    if (any2) {
-        __syncthreads();                 // every lane is done reading reference 0
-        if (nref == 2) stage(rs[1], win);
-        __syncthreads();
-        if (active && nref == 2) predict<true>(a, win + uu * WN, WS, rs[1], b.filter2d, b.w, b.h, col, r0, R, o1);
-    }
-    if (!active) return;
-    if (nref == 1) {
-        if (b.comp == MI_MC_PREP) {
-            // one side of a compound combined later (mi_mc_combine): the mct intermediate
-            int16_t *t = a.tmp + b.mask_off + (ty0 + r0) * b.w + tx0 + col;
-#pragma unroll
+    // everything after staging runs with the rows per lane R as a compile-time constant
+    // (min(h, 8) is wave-uniform): no per-row exec masking in the filters and epilogues
+    auto finish = [&](auto RC) {
+        constexpr int R = decltype(RC)::value;
+        const int r0 = rg * R;
+        int o0[8], o1[8];
+        const int64_t ds = a.dst_stride[p ? 1 : 0];
+        uint8_t *dst = a.dst[p] + (int64_t)(b.y + ty0 + r0) * ds;
+        const int x = b.x + tx0 + col;
+        const bool prep0 = nref == 2 || b.comp == MI_MC_PREP;
+        if (active) {
+            if (prep0) predict<true, R>(a, win + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, o0);
+            else predict<false, R>(a, win + uu * WN, WS, rs[0], b.filter2d, b.w, b.h, col, r0, o0);
+        }
+        if (any2) {
+            __syncthreads();                 // every lane is done reading reference 0
+            if (nref == 2) stage(rs[1], win);
+            __syncthreads();
+            if (active && nref == 2) predict<true, R>(a, win + uu * WN, WS, rs[1], b.filter2d, b.w, b.h, col, r0, o1);
+        }
+        if (!active) return;
+        if (nref == 1) {
+            if (b.comp == MI_MC_PREP) {
+                // one side of a compound combined later (mi_mc_combine): the mct intermediate
+                int16_t *t = a.tmp + b.mask_off + (ty0 + r0) * b.w + tx0 + col;
+    #pragma unroll
+                for (int q = 0; q < 8; q++)
+                    if (q < R) t[q * b.w] = (int16_t)o0[q];
+                return;
+            }
+            if (b.comp == MI_MC_OBMC_H || b.comp == MI_MC_OBMC_V) {
+                // OBMC lap blended into the block's prediction (blend_h / blend_v, mc_tmpl.c:636-660)
+                const bool above = b.comp == MI_MC_OBMC_H;
+                const int yb = ty0 + r0, xb = tx0 + col;
+    #pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    const int y = yb + q;
+                    const bool on = q < R && (above ? y < ((b.param * 3) >> 2) : xb < ((b.w * 3) >> 2));
+                    if (on) {
+                        const int m = k_obmc[above ? b.param + y : b.w + xb];
+                        Px *d = reinterpret_cast<Px *>(dst + (int64_t)q * ds) + x;
+                        *d = (Px)((*d * (64 - m) + o0[q] * m + 32) >> 6);
+                    }
+                }
+                return;
+            }
+    #pragma unroll
             for (int q = 0; q < 8; q++)
-                if (q < R) t[q * b.w] = (int16_t)o0[q];
+                if (q < R) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];
             return;
         }
-        if (b.comp == MI_MC_OBMC_H || b.comp == MI_MC_OBMC_V) {
-            // OBMC lap blended into the block's prediction (blend_h / blend_v, mc_tmpl.c:636-660)
-            const bool above = b.comp == MI_MC_OBMC_H;
+        const int ib = a.ib, sign = b.param >> 7;
+        if (b.comp == MI_MC_SEG) {
+            // w_mask (mc_tmpl.c:661-712): per-pixel weight from |t1 - t2|, t1 = tmp[sign]
+            const int mask_sh = a.bpc + ib - 4, mask_rnd = 1 << (mask_sh - 5);
+            const int sh = ib + 6, rnd = (32 << ib) + a.bias * 64;
+            const int msh = a.seg_ss_hor, msv = a.seg_ss_ver, mstride = b.w >> msh;
             const int yb = ty0 + r0, xb = tx0 + col;
-#pragma unroll
+            uint8_t *mo = a.masks + b.mask_off;
+            int mprev = 0;
+    #pragma unroll
             for (int q = 0; q < 8; q++) {
-                const int y = yb + q;
-                const bool on = q < R && (above ? y < ((b.param * 3) >> 2) : xb < ((b.w * 3) >> 2));
-                if (on) {
-                    const int m = k_obmc[above ? b.param + y : b.w + xb];
-                    Px *d = reinterpret_cast<Px *>(dst + (int64_t)q * ds) + x;
-                    *d = (Px)((*d * (64 - m) + o0[q] * m + 32) >> 6);
+                if (q < R) {
+                    const int t1 = sign ? o1[q] : o0[q], t2 = sign ? o0[q] : o1[q];
+                    const int m = min(38 + ((abs(t1 - t2) + mask_rnd) >> mask_sh), 64);
+                    o0[q] = min(max((t1 * m + t2 * (64 - m) + rnd) >> sh, 0), a.bdmax);
+                    // neighbour column (lane ^ 1 holds column ^ 1 of the same rows)
+                    const int mn = msh ? __shfl_xor(m, 1) : 0;
+                    if (!msh) {
+                        mo[(yb + q) * mstride + xb] = (uint8_t)m;
+                    } else if (!msv) {
+                        if (!(col & 1)) mo[(yb + q) * mstride + (xb >> 1)] = (uint8_t)((m + mn + 1 - sign) >> 1);
+                    } else if (q & 1) {
+                        if (!(col & 1)) mo[((yb + q) >> 1) * mstride + (xb >> 1)] = (uint8_t)((mprev + m + mn + 2 - sign) >> 2);
+                    } else {
+                        mprev = m + mn;
+                    }
                 }
             }
-            return;
+        } else {
+            const uint8_t *mk = a.masks + b.mask_off;
+    #pragma unroll
+            for (int q = 0; q < 8; q++) {
+                if (q < R) {
+                    int v;
+                    if (b.comp == MI_MC_AVG) {
+                        v = (o0[q] + o1[q] + (1 << ib) + a.bias * 2) >> (ib + 1);
+                    } else if (b.comp == MI_MC_WAVG) {
+                        const int wt = b.param & 31;
+                        v = (o0[q] * wt + o1[q] * (16 - wt) + (8 << ib) + a.bias * 16) >> (ib + 4);
+                    } else {
+                        const int m = mk[(ty0 + r0 + q) * b.w + tx0 + col];
+                        const int t1 = sign ? o1[q] : o0[q], t2 = sign ? o0[q] : o1[q];
+                        v = (t1 * m + t2 * (64 - m) + (32 << ib) + a.bias * 64) >> (ib + 6);
+                    }
+                    o0[q] = min(max(v, 0), a.bdmax);
+                }
+            }
         }
-#pragma unroll
+    #pragma unroll
         for (int q = 0; q < 8; q++)
             if (q < R) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];
-        return;
-    }
-    const int ib = a.ib, sign = b.param >> 7;
-    if (b.comp == MI_MC_SEG) {
-        // w_mask (mc_tmpl.c:661-712): per-pixel weight from |t1 - t2|, t1 = tmp[sign]
-        const int mask_sh = a.bpc + ib - 4, mask_rnd = 1 << (mask_sh - 5);
-        const int sh = ib + 6, rnd = (32 << ib) + a.bias * 64;
-        const int msh = a.seg_ss_hor, msv = a.seg_ss_ver, mstride = b.w >> msh;
-        const int yb = ty0 + r0, xb = tx0 + col;
-        uint8_t *mo = a.masks + b.mask_off;
-        int mprev = 0;
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            if (q < R) {
-                const int t1 = sign ? o1[q] : o0[q], t2 = sign ? o0[q] : o1[q];
-                const int m = min(38 + ((abs(t1 - t2) + mask_rnd) >> mask_sh), 64);
-                o0[q] = min(max((t1 * m + t2 * (64 - m) + rnd) >> sh, 0), a.bdmax);
-                // neighbour column (lane ^ 1 holds column ^ 1 of the same rows)
-                const int mn = msh ? __shfl_xor(m, 1) : 0;
-                if (!msh) {
-                    mo[(yb + q) * mstride + xb] = (uint8_t)m;
-                } else if (!msv) {
-                    if (!(col & 1)) mo[(yb + q) * mstride + (xb >> 1)] = (uint8_t)((m + mn + 1 - sign) >> 1);
-                } else if (q & 1) {
-                    if (!(col & 1)) mo[((yb + q) >> 1) * mstride + (xb >> 1)] = (uint8_t)((mprev + m + mn + 2 - sign) >> 2);
-                } else {
-                    mprev = m + mn;
-                }
-            }
-        }
-    } else {
-        const uint8_t *mk = a.masks + b.mask_off;
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            if (q < R) {
-                int v;
-                if (b.comp == MI_MC_AVG) {
-                    v = (o0[q] + o1[q] + (1 << ib) + a.bias * 2) >> (ib + 1);
-                } else if (b.comp == MI_MC_WAVG) {
-                    const int wt = b.param & 31;
-                    v = (o0[q] * wt + o1[q] * (16 - wt) + (8 << ib) + a.bias * 16) >> (ib + 4);
-                } else {
-                    const int m = mk[(ty0 + r0 + q) * b.w + tx0 + col];
-                    const int t1 = sign ? o1[q] : o0[q], t2 = sign ? o0[q] : o1[q];
-                    v = (t1 * m + t2 * (64 - m) + (32 << ib) + a.bias * 64) >> (ib + 6);
-                }
-                o0[q] = min(max(v, 0), a.bdmax);
-            }
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < 8; q++)
-        if (q < R) reinterpret_cast<Px *>(dst + (int64_t)q * ds)[x] = (Px)o0[q];
+
+    };
+    if (G.R == 8) finish(std::integral_constant<int, 8>{});
+    else if (G.R == 4) finish(std::integral_constant<int, 4>{});
+    else finish(std::integral_constant<int, 2>{});
 }
 
 // Waves per class for one plane group: packed small units or one wave per 64-lane tile.
