@@ -27,7 +27,16 @@ __device__ __forceinline__ int dir_off(int dir, int k, int ts) {
     return k == 0 ? nib(DY0, dir) * ts + nib(DX0, dir) : nib(DY1, dir) * ts + nib(DX1, dir);
 }
 
-constexpr int kTY = 68, kTS = 72;          // luma tile rows / LDS row stride (int16)
+#ifndef MI_CDEF_T1
+#define MI_CDEF_T1 1     // 0: no shifted copy, odd taps read unaligned words
+#endif
+#ifndef MI_CDEF_DIAG
+#define MI_CDEF_DIAG 0   // experiment builds only: 1 no filtering, 2 no filtering or direction search, 3 no tile fetch
+#endif
+// Luma tile: 68 rows (2-row halo) x 88 int16 (frame columns x0-8 .. x0+79; interior at column 8).
+// 88 = 44 dwords per row: a 32-lane group's 8 rows x 4 dwords fall on 32 distinct banks, and
+// every 8-px block row is 16-B aligned for ds_read_b128.
+constexpr int kTY = 68, kTS = 88;
 
 __device__ __forceinline__ int constrain(int diff, int thr, int shift) {
     const int ad = abs(diff);
@@ -142,6 +151,55 @@ __device__ __forceinline__ void dir_costs(const int16_t *t, int ts, int bdm8, un
     cb = c;
 }
 
+// find_dir's cost of one direction D for the 8x8 block at t (cdef.rs:921-1031): the partial
+// sums of that direction only (index didx<D>), the pixel bias of -128 folded into their start
+// values. One wave per direction, lane = block.
+template <int D> __device__ __host__ constexpr int didx(int y, int x) {
+    return D == 0 ? y + x : D == 1 ? y + (x >> 1) : D == 2 ? y : D == 3 ? 3 + y - (x >> 1)
+         : D == 4 ? 7 + y - x : D == 5 ? 3 - (y >> 1) + x : D == 6 ? x : (y >> 1) + x;
+}
+template <int D> __device__ __host__ constexpr int dcount(int k) {
+    int n = 0;
+    for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) n += didx<D>(y, x) == k;
+    return n;
+}
+template <int D>
+__device__ __forceinline__ unsigned dir_cost1(const int16_t *t, int ts, int bdm8) {
+    constexpr int NA = D == 2 || D == 6 ? 8 : (D & 1) ? 11 : 15;
+    int a[NA];
+#pragma unroll
+    for (int k = 0; k < NA; k++) a[k] = -128 * dcount<D>(k);
+#pragma unroll
+    for (int y = 0; y < 8; y++) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(t + y * ts);   // one 8-px row, ds_read_b128
+        const uint32_t w[4] = { v.x, v.y, v.z, v.w };
+#pragma unroll
+        for (int x = 0; x < 8; x += 2) {
+            a[didx<D>(y, x)] += (int)(int16_t)(w[x >> 1] & 0xffffu) >> bdm8;
+            a[didx<D>(y, x + 1)] += (int)(int16_t)(w[x >> 1] >> 16) >> bdm8;
+        }
+    }
+    const unsigned dv[7] = { 840, 420, 280, 210, 168, 140, 120 };
+    unsigned c = 0;
+    if constexpr (NA == 8) {
+#pragma unroll
+        for (int n = 0; n < 8; n++) c += (unsigned)(a[n] * a[n]);
+        c *= 105;
+    } else if constexpr (NA == 15) {
+#pragma unroll
+        for (int n = 0; n < 7; n++) c += (unsigned)(a[n] * a[n] + a[14 - n] * a[14 - n]) * dv[n];
+        c += (unsigned)(a[7] * a[7]) * 105;
+    } else {
+#pragma unroll
+        for (int m = 0; m < 5; m++) c += (unsigned)(a[3 + m] * a[3 + m]);
+        c *= 105;
+#pragma unroll
+        for (int m = 0; m < 3; m++) c += (unsigned)(a[m] * a[m] + a[10 - m] * a[10 - m]) * dv[2 * m + 1];
+    }
+    return c;
+}
+
 // Filter one pixel at LDS position (x, y); c = centre sample. Returns the new value.
 __device__ __forceinline__ int cdef_px(const int16_t *t, int ts, int x, int y, int pri, int sec,
                                        int dir, int damping, int bdm8) {
@@ -190,14 +248,14 @@ __device__ __forceinline__ int cdef_px(const int16_t *t, int ts, int x, int y, i
 // x0 - 8 (one 16-B load at 16 bits, 8-B at 8 bits; per-sample checks only for a vector that
 // straddles the frame edge) and written to T as 4 aligned pairs and to T1 (shifted by one) as
 // 3 pairs plus the two end samples: 10 vectors per luma row instead of 68 scalar loads.
-template <typename Px, int ROWS, int COLS>
+template <typename Px, int ROWS, int COLS, int NTH>
 struct VecTileLoad {
-    static constexpr int NV = (COLS + 6 + 7) / 8, N = ROWS * NV, IT = (N + 255) / 256;
+    static constexpr int NV = (COLS + 6 + 7) / 8, N = ROWS * NV, IT = (N + NTH - 1) / NTH;
     uint32_t w[IT][4];
     __device__ __forceinline__ void fetch(const uint8_t *src, int64_t stride, int x0, int y0, int fw, int fh) {
 #pragma unroll
         for (int k = 0; k < IT; k++) {
-            const int i = threadIdx.x + 256 * k;
+            const int i = threadIdx.x + NTH * k;
             const int r = i / NV, j = i - r * NV;
             const int y = y0 - 2 + r, xs = x0 - 8 + 8 * j;
 #pragma unroll
@@ -226,28 +284,23 @@ struct VecTileLoad {
             }
         }
     }
+    // T column c holds frame column x0 - 8 + c, so vector j lands 16-B aligned at column 8j
+    // (one ds_write_b128) and the tile interior starts at column 8. T1[c] = T[c + 1]: samples
+    // (1,2) (3,4) (5,6) as one 12-B store at column 8j, samples 0 and 7 alone.
     __device__ __forceinline__ void store(int16_t *t, int16_t *t1, int ts) const {
 #pragma unroll
         for (int k = 0; k < IT; k++) {
-            const int i = threadIdx.x + 256 * k;
+            const int i = threadIdx.x + NTH * k;
             if (i >= N) continue;
             const int r = i / NV, j = i - r * NV;
-            const int c0 = 8 * j - 6;          // window column of sample 0 (even)
-            int16_t *tr = t + r * ts, *t1r = t1 + r * ts;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int c = c0 + 2 * q;
-                if (c >= 0 && c < COLS) *reinterpret_cast<uint32_t *>(tr + c) = w[k][q];
-            }
-            // T1[c - 1] = T[c]: samples (1,2), (3,4), (5,6) as pairs, 0 and 7 alone
-#pragma unroll
-            for (int q = 0; q < 3; q++) {
-                const int c = c0 + 2 * q;
-                if (c >= 0 && c <= COLS - 2)
-                    *reinterpret_cast<uint32_t *>(t1r + c) = (w[k][q] >> 16) | (w[k][q + 1] << 16);
-            }
-            if (c0 - 1 >= 0 && c0 - 1 <= COLS - 2) t1r[c0 - 1] = (int16_t)(w[k][0] & 0xffffu);
-            if (c0 + 6 >= 0 && c0 + 6 <= COLS - 2) t1r[c0 + 6] = (int16_t)(w[k][3] >> 16);
+            int16_t *tr = t + r * ts + 8 * j, *t1r = t1 + r * ts + 8 * j;
+            *reinterpret_cast<uint4 *>(tr) = make_uint4(w[k][0], w[k][1], w[k][2], w[k][3]);
+            if (!MI_CDEF_T1) continue;
+            *reinterpret_cast<uint3 *>(t1r) = make_uint3((w[k][0] >> 16) | (w[k][1] << 16),
+                                                         (w[k][1] >> 16) | (w[k][2] << 16),
+                                                         (w[k][2] >> 16) | (w[k][3] << 16));
+            if (j) t1r[-1] = (int16_t)(w[k][0] & 0xffffu);
+            t1r[6] = (int16_t)(w[k][3] >> 16);
         }
     }
 };
@@ -257,10 +310,11 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 // constrain() (cdef.rs:545) on two samples at once. d = sat(p - c): a sentinel tap gives
 // d = -32768 and |d| = 32767 (saturated), so its contribution is 0 exactly as in 32-bit.
-__device__ __forceinline__ s16x2 constrain2(s16x2 d, s16x2 thr, s16x2 shift) {
+__device__ __forceinline__ s16x2 constrain2(s16x2 d, u16x2 thr, u16x2 shift) {
     const s16x2 zero = { 0, 0 };
     const s16x2 ad = __builtin_elementwise_max(d, __builtin_elementwise_sub_sat(zero, d));
-    const s16x2 m = __builtin_elementwise_max(zero, thr - (ad >> shift));
+    // max(0, thr - (|d| >> shift)) as one unsigned saturating subtract
+    const s16x2 m = __builtin_bit_cast(s16x2, __builtin_elementwise_sub_sat(thr, __builtin_bit_cast(u16x2, ad) >> shift));
     return __builtin_elementwise_max(__builtin_elementwise_min(d, m), zero - m);
 }
 
@@ -301,8 +355,8 @@ __device__ __forceinline__ s16x2 cdef_pair(const char *P, const PairTaps &t, int
     s16x2 sum = { 0, 0 }, mx = c;
     u16x2 mn = __builtin_bit_cast(u16x2, c);
     if (pri) {
-        const short sh = (short)max(0, damping - ulog2i(pri));
-        const s16x2 thr = { (short)pri, (short)pri }, shv = { sh, sh };
+        const unsigned short sh = (unsigned short)max(0, damping - ulog2i(pri));
+        const u16x2 thr = { (unsigned short)pri, (unsigned short)pri }, shv = { sh, sh };
         const short tap0 = (short)(4 - ((pri >> bdm8) & 1)), tap1 = (short)((tap0 & 3) | 2);
 #pragma unroll
         for (int k = 0; k < 2; k++) {
@@ -319,8 +373,8 @@ __device__ __forceinline__ s16x2 cdef_pair(const char *P, const PairTaps &t, int
         }
     }
     if (sec) {
-        const short sh = (short)(damping - ulog2i(sec));
-        const s16x2 thr = { (short)sec, (short)sec }, shv = { sh, sh };
+        const unsigned short sh = (unsigned short)(damping - ulog2i(sec));
+        const u16x2 thr = { (unsigned short)sec, (unsigned short)sec }, shv = { sh, sh };
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             s16x2 v = { 0, 0 };
@@ -380,7 +434,7 @@ __device__ __forceinline__ void filter_plane(const int16_t *T, int lane, const i
 #pragma unroll
             for (int i = 0; i < RB; i++) {
                 const int r = r0 + i;
-                const char *P = reinterpret_cast<const char *>(T + (r + 2) * TS + x + 2);
+                const char *P = reinterpret_cast<const char *>(T + (r + 2) * TS + x + 8);
                 const s16x2 v = cdef_pair(P, t, pri, sec, damping, bdm8);
                 store_pair<Px>(reinterpret_cast<Px *>(dst + (int64_t)(gy0 + r) * stride) + gx, v);
             }
@@ -389,27 +443,70 @@ __device__ __forceinline__ void filter_plane(const int16_t *T, int lane, const i
             for (int i = 0; i < RB; i++) {
                 const int r = r0 + i, gy = gy0 + r;
                 Px *dp = reinterpret_cast<Px *>(dst + (int64_t)gy * stride) + gx;
-                if (TILE_COPY && gx < fw && gy < fh) store_pair<Px>(dp, ld2(reinterpret_cast<const char *>(T + (r + 2) * TS + x + 2)));
+                if (TILE_COPY && gx < fw && gy < fh) store_pair<Px>(dp, ld2(reinterpret_cast<const char *>(T + (r + 2) * TS + x + 8)));
                 else copy_pair<Px>(dp, reinterpret_cast<const Px *>(src + (int64_t)gy * stride) + gx);
             }
         }
     }
 }
 
-// One 64x64 luma unit (+ co-located chroma) per 256-lane workgroup. L = layout (0 I400,
+// Luma of one 64x64 unit, one 8x8 block per 32-lane group at a time: lane l of group g takes
+// row g*8 + l/4 and pair column l%4 of the blocks (g, 0..7) in turn. Every lane of a group then
+// shares the block's direction, so a tap read touches 8 rows x 4 consecutive dwords: with the
+// 36-dword row stride those are 32 distinct banks (no bank conflicts for any direction), where a
+// row-major mapping mixed eight directions per group. Per-block state is one broadcast LDS word
+// (flag | dir << 8 | pri << 16) and the direction's tap deltas three broadcast 16-B reads.
+template <typename Px, int TS>
+__device__ __forceinline__ void filter_luma(const int16_t *T, const int4 (*taps)[3], const int *bstate,
+                                            int sec, int damping, int bdm8, const uint8_t *src, uint8_t *dst,
+                                            int64_t stride, int gx0, int gy0, int fw, int fh) {
+    const int g = threadIdx.x >> 5, l = threadIdx.x & 31;     // 16 groups: block row g / 2, columns 4 (g & 1) ..
+    const int r = (g >> 1) * 8 + (l >> 2), gy = gy0 + r, c0 = (g & 1) * 4;
+    const char *prow = reinterpret_cast<const char *>(T + (r + 2) * TS + 2 * (l & 3) + 8);
+    Px *drow = reinterpret_cast<Px *>(dst + (int64_t)gy * stride) + gx0 + 2 * (l & 3);
+    const Px *srow = reinterpret_cast<const Px *>(src + (int64_t)gy * stride) + gx0 + 2 * (l & 3);
+#pragma unroll
+    for (int i = c0; i < c0 + 4; i++) {
+        const int st = bstate[(g >> 1) * 8 + i];
+        const char *P = prow + 16 * i;
+        if (st & 1) {
+            const int dir = (st >> 8) & 7, pri = st >> 16;
+            PairTaps t;
+            const int4 q0 = taps[dir][0], q1 = taps[dir][1], q2 = taps[dir][2];
+            t.pri[0] = q0.x; t.pri[1] = q0.y; t.pri[2] = q0.z; t.pri[3] = q0.w;
+            t.sec[0] = q1.x; t.sec[1] = q1.y; t.sec[2] = q1.z; t.sec[3] = q1.w;
+            t.sec[4] = q2.x; t.sec[5] = q2.y; t.sec[6] = q2.z; t.sec[7] = q2.w;
+            store_pair<Px>(drow + 8 * i, cdef_pair(P, t, pri, sec, damping, bdm8));
+        } else if (gx0 + 8 * i + 2 * (l & 3) < fw && gy < fh) {
+            store_pair<Px>(drow + 8 * i, ld2(P));
+        } else {
+            copy_pair<Px>(drow + 8 * i, srow + 8 * i);
+        }
+    }
+}
+
+// One 64x64 luma unit (+ co-located chroma) per 512-lane workgroup (eight waves: one per
+// direction in the search, 34 KB of LDS for four workgroups = 32 waves per CU). L = layout (0 I400,
 // 1 I420, 2 I422, 3 I444), compile-time so every tile index is a shift or a constant divide.
 template <typename Px, int L>
-__global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
+#ifndef MI_CDEF_MINW
+#define MI_CDEF_MINW 8
+#endif
+__global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
+    constexpr int NTH = 512;
     constexpr int SSH = L == 1 || L == 2, SSV = L == 1;
-    constexpr int CW = 64 >> SSH, CH = 64 >> SSV, CTS = CW + 8;
+    constexpr int CW = 64 >> SSH, CH = 64 >> SSV, CTS = CW == 64 ? 88 : 48;   // 24-dword rows: two rows 2 apart are 16 banks apart
     constexpr int UVW = 8 >> SSH, UVH = 8 >> SSV;
     constexpr int YN = kTY * kTS, CN = L ? (CH + 4) * CTS : 2;
-    __shared__ int16_t ty[2 * YN];                 // T, T1
-    __shared__ int16_t tuv[2][2 * CN];             // per chroma plane: T, T1
+    constexpr int NT = MI_CDEF_T1 ? 2 : 1;
+    __shared__ __align__(16) int16_t ty[NT * YN];              // T, T1
+    __shared__ __align__(16) int16_t tuv[2][NT * CN];          // per chroma plane: T, T1
     __shared__ int8_t bdir[64];
     __shared__ int8_t bflag[64];          // bit0 luma filtered, bit1 chroma filtered
     __shared__ int16_t bpri[64];
     __shared__ unsigned dcost[8][64];     // find_dir costs per direction and block
+    __shared__ int bstate[64];            // luma: filtered | dir << 8 | adjusted pri << 16
+    __shared__ int4 ytaps[8][3];          // luma tap byte deltas per direction (PairTaps order)
 
     const int bid = xcd_block(blockIdx.x, gridDim.x);
     const int tx = bid % a.tiles_x, tyy = bid / a.tiles_x;
@@ -429,7 +526,7 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
             const int pw = p ? CW : 64, ph = p ? CH : 64;
             const int px0 = p ? x0 >> SSH : x0, py0 = p ? y0 >> SSV : y0;
             const int cpr = pw / PX8;   // 8-byte chunks per row
-            for (int i = threadIdx.x; i < cpr * ph; i += 256) {
+            for (int i = threadIdx.x; i < cpr * ph; i += NTH) {
                 const int r = i / cpr, c = i - r * cpr;
                 const int64_t off = (int64_t)(py0 + r) * a.stride[p] + (int64_t)(px0 + c * PX8) * sizeof(Px);
                 *reinterpret_cast<uint2 *>(a.dst[p] + off) = *reinterpret_cast<const uint2 *>(a.src[p] + off);
@@ -444,11 +541,22 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
     const int uv_pri = (uv_lvl >> 2) << bdm8;
     int uv_sec = uv_lvl & 3; uv_sec += uv_sec == 3; uv_sec <<= bdm8;
 
+    if (threadIdx.x < 8) {
+        PairTaps t;
+        make_taps<kTS, MI_CDEF_T1 ? YN * 2 : 2>(t, threadIdx.x);
+        ytaps[threadIdx.x][0] = make_int4(t.pri[0], t.pri[1], t.pri[2], t.pri[3]);
+        ytaps[threadIdx.x][1] = make_int4(t.sec[0], t.sec[1], t.sec[2], t.sec[3]);
+        ytaps[threadIdx.x][2] = make_int4(t.sec[4], t.sec[5], t.sec[6], t.sec[7]);
+    }
     {
-        VecTileLoad<Px, 68, 68> ly;
-        VecTileLoad<Px, CH + 4, CW + 4> lu, lv;
+        VecTileLoad<Px, 68, 68, NTH> ly;
+        VecTileLoad<Px, CH + 4, CW + 4, NTH> lu, lv;
+#if MI_CDEF_DIAG != 3
         ly.fetch(a.src[0], a.stride[0], x0, y0, fwy, fhy);
         if (L && uv_lvl) {
+#else
+        if (false) {
+#endif
             lu.fetch(a.src[1], a.stride[1], x0 >> SSH, y0 >> SSV, fwc, fhc);
             lv.fetch(a.src[2], a.stride[2], x0 >> SSH, y0 >> SSV, fwc, fhc);
         }
@@ -460,16 +568,21 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
     }
     __syncthreads();
 
-    if (y_pri || uv_pri) {
-        const int b = threadIdx.x & 63, w = threadIdx.x >> 6;   // wave-uniform direction pair
-        const int16_t *tb = ty + ((b >> 3) * 8 + 2) * kTS + (b & 7) * 8 + 2;
-        unsigned ca, cb;
-        if (w == 0) dir_costs<0>(tb, kTS, bdm8, ca, cb);
-        else if (w == 1) dir_costs<1>(tb, kTS, bdm8, ca, cb);
-        else if (w == 2) dir_costs<2>(tb, kTS, bdm8, ca, cb);
-        else dir_costs<3>(tb, kTS, bdm8, ca, cb);
-        dcost[2 * w][b] = ca;
-        dcost[2 * w + 1][b] = cb;
+    if (MI_CDEF_DIAG != 2 && (y_pri || uv_pri)) {
+        const int b = threadIdx.x & 63, w = threadIdx.x >> 6;   // wave-uniform direction
+        const int16_t *tb = ty + ((b >> 3) * 8 + 2) * kTS + (b & 7) * 8 + 8;
+        unsigned c;
+        switch (w) {
+        case 0: c = dir_cost1<0>(tb, kTS, bdm8); break;
+        case 1: c = dir_cost1<1>(tb, kTS, bdm8); break;
+        case 2: c = dir_cost1<2>(tb, kTS, bdm8); break;
+        case 3: c = dir_cost1<3>(tb, kTS, bdm8); break;
+        case 4: c = dir_cost1<4>(tb, kTS, bdm8); break;
+        case 5: c = dir_cost1<5>(tb, kTS, bdm8); break;
+        case 6: c = dir_cost1<6>(tb, kTS, bdm8); break;
+        default: c = dir_cost1<7>(tb, kTS, bdm8); break;
+        }
+        dcost[w][b] = c;
         __syncthreads();
     }
 
@@ -498,22 +611,23 @@ __global__ __launch_bounds__(256) void cdef_kernel(CdefArgs a) {
                 if (uv_lvl) flag |= 2;
             }
         }
+        if (MI_CDEF_DIAG == 1 || MI_CDEF_DIAG == 2) flag = 0;
         bdir[b] = (int8_t)dir;
         bflag[b] = (int8_t)flag;
         bpri[b] = (int16_t)pri;
+        bstate[b] = (flag & 1) | (y_pri ? dir : 0) << 8 | (y_pri ? pri : 0) << 16;
     }
     __syncthreads();
 
-    // luma: 2048 pairs, 8 rows of one 8x8 block per lane
-    filter_plane<Px, 64, 64, 8, 8, 256, kTS, YN * 2, 1, true>(
-        ty, threadIdx.x, bdir, bflag, bpri, y_pri != 0, y_pri, y_sec, a.damping, bdm8, false,
-        a.src[0], a.dst[0], a.stride[0], x0, y0, fwy, fhy);
+    // luma: 2048 pairs, one 8x8 block per 32-lane group at a time
+    filter_luma<Px, kTS>(ty, ytaps, bstate, y_sec, a.damping, bdm8, a.src[0], a.dst[0], a.stride[0],
+                         x0, y0, fwy, fhy);
     if (L) {
-        // chroma: lanes 0..127 U, 128..255 V (damping - 1, cdef_apply.rs)
-        const int p = 1 + (threadIdx.x >> 7);
+        // chroma: lanes 0..255 U, 256..511 V (damping - 1, cdef_apply.rs)
+        const int p = 1 + (threadIdx.x >> 8);
         // (the chroma tile is only staged when uv_lvl != 0: unfiltered chroma copies from D)
-        filter_plane<Px, CW, CH, UVW, UVH, 128, CTS, CN * 2, 2, false>(
-            tuv[p - 1], threadIdx.x & 127, bdir, bflag, bpri, false, uv_pri, uv_sec, a.damping - 1, bdm8,
+        filter_plane<Px, CW, CH, UVW, UVH, 256, CTS, MI_CDEF_T1 ? CN * 2 : 2, 2, false>(
+            tuv[p - 1], threadIdx.x & 255, bdir, bflag, bpri, false, uv_pri, uv_sec, a.damping - 1, bdm8,
             L == 2, a.src[p], a.dst[p], a.stride[p], x0 >> SSH, y0 >> SSV, fwc, fhc);
     }
 }
@@ -584,8 +698,8 @@ int launch_cdef(const CdefArgs &a, int tiles, int bpc, hipStream_t s) {
     if (tiles <= 0) return 0;
 #define MI_CDEF_LAUNCH(L)                                                                            \
     do {                                                                                             \
-        if (bpc == 8) cdef_kernel<uint8_t, L><<<tiles, 256, 0, s>>>(a);                               \
-        else cdef_kernel<uint16_t, L><<<tiles, 256, 0, s>>>(a);                                       \
+        if (bpc == 8) cdef_kernel<uint8_t, L><<<tiles, 512, 0, s>>>(a);                               \
+        else cdef_kernel<uint16_t, L><<<tiles, 512, 0, s>>>(a);                                       \
     } while (0)
     switch (a.layout) {
     case 0: MI_CDEF_LAUNCH(0); break;

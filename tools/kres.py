@@ -4,7 +4,7 @@ import re, subprocess, sys, os
 src = os.path.abspath(sys.argv[1])
 inc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "include")
 r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-I" + inc, "-c", src,
-                    "-o", "/tmp/kres.o", "-Rpass-analysis=kernel-resource-usage"] + (["-xhip"] if src.endswith(".cpp") else []),
+                    "-o", "/tmp/kres.o", "-Rpass-analysis=kernel-resource-usage"] + os.environ.get("MI_EXTRA_FLAGS", "").split() + (["-xhip"] if src.endswith(".cpp") else []),
                    capture_output=True, text=True, cwd="/tmp")
 cur, rows = None, []
 for line in r.stderr.splitlines():
