@@ -186,6 +186,11 @@ def lib():
     _sig(L, "mi_film_grain_prep", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiFilmGrainData), _VP])
     _sig(L, "mi_frame_run", ctypes.c_int, [_VP, _VP, ctypes.POINTER(MiFramePictures), ctypes.POINTER(ctypes.c_int), _VP])
     _sig(L, "mi_frame_end", ctypes.c_int, [_VP, _VP])
+    # output side (include/mi_av1out.h)
+    _sig(L, "mi_host_picture_alloc", ctypes.c_int, [_I, _I, _I, _I, ctypes.POINTER(MiPicture)])
+    _sig(L, "mi_host_picture_free", None, [ctypes.POINTER(MiPicture)])
+    _sig(L, "mi_output_picture", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
+                                                ctypes.POINTER(MiFilmGrainData), ctypes.c_int, _VP])
     _lib = L
     return L
 
@@ -200,7 +205,8 @@ EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error"
             "mi_dsp_mc_avg", "mi_dsp_mc_w_avg", "mi_dsp_mc_mask", "mi_dsp_mc_w_mask", "mi_dsp_mc_blend",
             "mi_dsp_mc_blend_v", "mi_dsp_mc_blend_h", "mi_dsp_mc_emu_edge", "mi_dsp_mc_warp8x8", "mi_dsp_mc_resize",
             "mi_dsp_mc_scaled", "mi_dsp_lr_wiener", "mi_dsp_lr_sgr",
-            "mi_dsp_fg_generate_grain_y", "mi_dsp_fg_generate_grain_uv", "mi_dsp_fgy_32x32xn", "mi_dsp_fguv_32x32xn"]
+            "mi_dsp_fg_generate_grain_y", "mi_dsp_fg_generate_grain_uv", "mi_dsp_fgy_32x32xn", "mi_dsp_fguv_32x32xn",
+            "mi_host_picture_alloc", "mi_host_picture_free", "mi_output_picture"]
 
 
 def check(rc, what):

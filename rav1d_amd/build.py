@@ -32,7 +32,7 @@ def _stale(obj, src):
         return True
     t = os.path.getmtime(obj)
     deps = [src] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
-    deps += [os.path.join(HERE, "..", "include", h) for h in ("mi_av1dsp.h", "mi_av1dec.h")]
+    deps += [os.path.join(HERE, "..", "include", h) for h in ("mi_av1dsp.h", "mi_av1dec.h", "mi_av1out.h")]
     return any(os.path.getmtime(d) > t for d in deps)
 
 

@@ -59,3 +59,37 @@ def decode_ivf(ctx, data, stream=None, sync_each=True):
             for i in range(ev.n_release):
                 pics.pop(ev.release[i], None)
     frame_end(ctx, stream)
+
+
+def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True):
+    """Decode an IVF stream on the device and write every shown picture through `muxer`
+    (rav1d_amd.output.Muxer): the picture leaves HBM once, via mi_output_picture into pinned
+    host memory, with film grain applied in that same pass when the frame carries grain and
+    apply_grain is set (Dav1dSettings.apply_grain, src/lib.rs). Returns the pictures written."""
+    from .output import HostPicture, output_picture
+    import torch
+    dec = Av1Decoder()
+    pics, host, n = {}, None, 0
+    for tu in ivf_frames(data):
+        dec.send(tu)
+        for ev in dec.events():
+            if ev.frame:
+                pics[ev.pic_id] = run_frame(ctx, ev.frame.contents, stream)
+                frame_end(ctx, stream)
+            if ev.show_pic >= 0:
+                out = pics[ev.show_pic].output()
+                if host is None or (host.pic.w, host.pic.h, host.pic.bpc, host.pic.layout) != \
+                        (out.w, out.h, out.bpc, out.layout):
+                    host = HostPicture(out.w, out.h, out.bpc, out.layout)
+                fg = ev.fg if (ev.fg_present and apply_grain) else None
+                output_picture(ctx, out, host, fg, 0, stream)
+                if stream is not None:
+                    stream.synchronize()
+                else:
+                    torch.cuda.synchronize()
+                muxer.write(host.pic)
+                n += 1
+            for i in range(ev.n_release):
+                pics.pop(ev.release[i], None)
+    frame_end(ctx, stream)
+    return n

@@ -63,9 +63,11 @@ def oracle_frame(fr):
 def decode_stream(data, recon=oracle_frame, max_frames=None):
     """Decode an IVF stream; returns (md5 hex, frames output). `recon(frame) -> planes` runs the
     pixel path (oracle by default; the GPU path in the -m gpu tests)."""
+    from rav1d_amd.output import Muxer, host_picture_np
     dec = Av1Decoder()
     pics = {}
     md5 = hashlib.md5()
+    mux = Muxer("md5")           # the product md5 muxer (libmi_av1dec.so), checked against hashlib
     shown = 0
     for tu in ivf_frames(data):
         dec.send(tu)
@@ -74,13 +76,18 @@ def decode_stream(data, recon=oracle_frame, max_frames=None):
                 fr = ev.frame.contents
                 if fr.up_w != fr.w:
                     raise NotImplementedError("super-resolution stream")
-                pics[ev.pic_id] = (recon(fr), fr.w, fr.h, fr.layout)
+                pics[ev.pic_id] = (recon(fr), fr.w, fr.h, fr.layout, fr.bpc)
             if ev.show_pic >= 0:
-                planes, w, h, layout = pics[ev.show_pic]
+                planes, w, h, layout, bpc = pics[ev.show_pic]
                 md5_update_picture(md5, planes, w, h, layout)
+                mux.write(host_picture_np(planes, w, h, bpc, layout))
                 shown += 1
             for i in range(ev.n_release):
                 pics.pop(ev.release[i], None)
         if max_frames and shown >= max_frames:
             break
-    return md5.hexdigest(), shown
+    digest = mux.digest()
+    mux.close()
+    if shown:
+        assert digest == md5.hexdigest(), "md5 muxer disagrees with hashlib"
+    return digest if shown else md5.hexdigest(), shown

@@ -14,9 +14,11 @@ def _decl(name):
 
 
 def header_symbols():
-    """librav1d_amd.so: every mi_av1dsp.h entry plus mi_av1dec.h's device executor."""
-    dec = _decl("mi_av1dec.h")
-    return sorted(_decl("mi_av1dsp.h") | {s for s in dec if s.startswith("mi_frame_")})
+    """librav1d_amd.so: every mi_av1dsp.h entry plus mi_av1dec.h's device executor and
+    mi_av1out.h's device-to-host output."""
+    dec, out = _decl("mi_av1dec.h"), _decl("mi_av1out.h")
+    return sorted(_decl("mi_av1dsp.h") | {s for s in dec if s.startswith("mi_frame_")} |
+                  {s for s in out if not s.startswith("mi_muxer_")})
 
 
 def test_front_end_exports_header_symbols():
@@ -25,6 +27,7 @@ def test_front_end_exports_header_symbols():
     L = dec_lib()
     syms = sorted(s for s in _decl("mi_av1dec.h") if s.startswith("mi_dec_"))
     assert len(syms) >= 5
+    syms += sorted(s for s in _decl("mi_av1out.h") if s.startswith("mi_muxer_"))
     for s in syms:
         assert hasattr(L, s), f"{s} missing from libmi_av1dec.so"
 
