@@ -218,16 +218,90 @@ def film_grain_8k(ctx, stream, reps=20):
                 prep_ms=round(prep_ms, 4), apply_gbs=round(2 * fb / (apply_ms / 1e3) / 1e9, 1))
 
 
+def mc_coherent(ctx, stream, reps=20):
+    """MC alone on a 4K10 inter frame whose motion is spatially coherent (one motion per 64x64
+    superblock and reference + noise of +-2 px per block: rav1d_amd.synth mv_mode "coherent"),
+    beside the headline's uniformly random MVs (the worst case for
+    reference-window reuse). Same block shapes, filters and compound mix."""
+    fr = make_frame(W, H, BPC, LAYOUT, seed=0x4C100001, with_fg=False, with_mc=True, mv_mode="coherent")
+    cur = F.Frame(W, H, BPC, LAYOUT)
+    refs = []
+    for planes in fr["refs"]:
+        r = F.Frame(W, H, BPC, LAYOUT)
+        for p, a in enumerate(planes):
+            r.set_plane_np(p, a)
+        refs.append(r)
+    meta = F.McMeta(*fr["mc"])
+    lib, pc = F.lib(), cur.picture()
+    pics = (F.MiPicture * len(refs))(*[r.picture() for r in refs])
+    blocks, masks, sp = ctypes.c_void_p(meta.blocks.data_ptr()), ctypes.c_void_p(meta.masks.data_ptr()), F._stream_ptr(stream)
+    fn = lambda: F.check(lib.mi_mc_frame(ctx.h, ctypes.byref(pc), pics, len(refs), blocks, meta.class_start,
+                                         masks, None, sp), "mc")
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    algo = mc_algorithmic_bytes(fr["mc"][0], BPC) + fr["mc"][2].nbytes
+    gbs = algo / (ms / 1e3) / 1e9
+    return dict(ms=round(ms, 4), algo_bytes=int(algo), gbs=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4),
+                traffic_per_step=pmc_traffic("mc", "r02_traffic_coherent.json"),
+                mv_field="coherent: per-64x64 motion per reference uniform in +-64 px, +-2 px noise per block")
+
+
+def output_4k10(ctx, stream, reps=10):
+    """The output side at 4K10 (include/mi_av1out.h): the displayed picture written into pinned
+    host memory by mi_output_picture, as a DMA copy of the visible area and with film grain
+    stored by the grain kernel straight into host memory (one pass). PCIe-bound: this is the
+    host-buffer rate DESIGN.md §5 quotes, never the headline value."""
+    from rav1d_amd.output import HostPicture, output_picture
+    from rav1d_amd.synth import make_fg_params, make_texture
+    rng = np.random.default_rng(0x0F7E0001)
+    src = F.Frame(W, H, BPC, LAYOUT)
+    for p in range(3):
+        pw, ph = src.dims(p)
+        src.set_plane_np(p, make_texture(rng, pw, ph, BPC))
+    host = HostPicture(W, H, BPC, LAYOUT)
+    fg = F.film_grain_data(make_fg_params(rng, LAYOUT))
+    fb = frame_bytes(W, H, BPC, LAYOUT)
+    res = {}
+    for name, g in (("copy", None), ("grain_fused", fg)):
+        fn = lambda: output_picture(ctx, src, host, g, 0, stream)
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        res[name] = dict(ms=round(ms, 3), fps=round(1e3 / ms, 1), host_gbs=round(fb / (ms / 1e3) / 1e9, 1))
+    host.free()
+    return res
+
+
 def per_launch(v, launches):
     return None if v is None else int(v // launches)
 
 
-def pmc_traffic(stage):
-    """HBM bytes per step of `stage` from the committed PMC run (profiles/r01_traffic.json,
+def pmc_traffic(stage, name=None):
+    """HBM bytes per step of `stage` from the committed PMC run (profiles/r02_traffic.json,
     written by tools/traffic_json.py from tools/gpu_pmc.sh's FETCH_SIZE / WRITE_SIZE passes of
-    this same bench command, calibrated per access width by tools/pmc_calib). None if absent."""
-    path = os.path.join(ROOT, "profiles", "r01_traffic.json")
-    if not os.path.exists(path):
+    this same bench command, calibrated per access width by tools/pmc_calib; the round-1 file
+    when this round's is absent). None if absent."""
+    path = None
+    for n in ([name] if name else ["r02_traffic.json", "r01_traffic.json"]):
+        if os.path.exists(os.path.join(ROOT, "profiles", n)):
+            path = os.path.join(ROOT, "profiles", n)
+            break
+    if path is None:
         return None
     ent = json.load(open(path)).get("stages", {}).get(stage)
     return None if ent is None else ent.get("hbm_bytes_per_step")
@@ -349,6 +423,9 @@ def main():
     ap.add_argument("--no-fg", action="store_true", help="skip the separate 8K10 film-grain measurement")
     ap.add_argument("--no-intra", action="store_true", help="skip the separate 1080p8 intra measurement")
     ap.add_argument("--no-verify", action="store_true", help="skip the per-rank oracle check of the output")
+    ap.add_argument("--no-extra", action="store_true", help="skip the coherent-motion MC and output-side measurements")
+    ap.add_argument("--mv", choices=["uniform", "coherent"], default="uniform",
+                    help="motion field of the timed frame (uniform: SURVEY.md 8(d) config 3)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -362,7 +439,7 @@ def main():
     cfg = broadcast_config({"w": W, "h": H, "bpc": BPC, "layout": LAYOUT,
                             "seeds": [0x4C100001 + r for r in range(world)]}, world)
     fr = make_frame(cfg["w"], cfg["h"], cfg["bpc"], cfg["layout"], seed=cfg["seeds"][rank], with_fg=False,
-                    with_mc=True)
+                    with_mc=True, mv_mode=args.mv)
     ctx = F.Context(local)
     pipe = Pipeline(ctx, fr)
     torch.cuda.synchronize()
@@ -425,11 +502,22 @@ def main():
                          "algo_bytes_per_launch": pipe.algo[dom] // pipe.launches[dom],
                          "launch_us": round(stage_ms[dom] * 1e3 / pipe.launches[dom], 2),
                          "launches_per_step": pipe.launches[dom]},
+            # the same figures for every stage's kernel (north_star sets >= 0.5 on itx and deblock)
+            "stage_roofline": {k: {"kernel": pipe.kernels[k], "achieved": round(pipe.algo[k] / (stage_ms[k] / 1e3) / 1e9, 1),
+                                   "frac": round(pipe.algo[k] / (stage_ms[k] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                   "traffic": per_launch(pmc_traffic(k), pipe.launches[k]),
+                                   "algo_bytes_per_launch": pipe.algo[k] // pipe.launches[k],
+                                   "launch_us": round(stage_ms[k] * 1e3 / pipe.launches[k], 2)}
+                               for k in stage_ms if k in pipe.algo},
+            "mv_field": args.mv,
         }
         if world == 1 and not args.no_fg:
             out["film_grain_8k10"] = film_grain_8k(ctx, stream)
         if world == 1 and not args.no_intra:
             out["intra_1080p8"] = intra_1080p8(ctx)
+        if world == 1 and not args.no_extra:
+            out["mc_coherent_4k10"] = mc_coherent(ctx, stream)
+            out["output_4k10"] = output_4k10(ctx, stream)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(fr)
         print(json.dumps(out))

@@ -429,7 +429,8 @@ def itx_blocks_from_tilings(tilings, bpc, rng, dc_frac=0.6, full_frac=0.1):
     return blocks, size_start, coef
 
 
-def make_frame(w, h, bpc=10, layout=1, seed=0x4C100001, sb128=1, with_fg=True, with_mc=False, nrefs=2):
+def make_frame(w, h, bpc=10, layout=1, seed=0x4C100001, sb128=1, with_fg=True, with_mc=False, nrefs=2,
+               mv_mode="uniform"):
     """One synthetic frame's worth of post-entropy descriptors for every implemented stage,
     all derived from one transform tiling: prediction planes, itx blocks + coefficient arena,
     deblock masks/levels, CDEF indices/strengths, LR units, film-grain parameters.
@@ -454,7 +455,7 @@ def make_frame(w, h, bpc=10, layout=1, seed=0x4C100001, sb128=1, with_fg=True, w
         fr["refs"] = [[make_texture(rng, w, h, bpc)] +
                       ([make_texture(rng, cw, ch, bpc) for _ in range(2)] if layout else [])
                       for _ in range(nrefs)]
-        fr["mc"] = make_mc_units(w, h, layout, rng, nrefs=nrefs)
+        fr["mc"] = make_mc_units(w, h, layout, rng, nrefs=nrefs, mv_mode=mv_mode)
     return fr
 
 
@@ -506,21 +507,35 @@ def _mc_record(x, y, bw, bh, plane, f2d, mvs, refs, comp, param, mask_off):
     return (x, y, bw, bh, plane, f2d, (mvs[0][0], mvs[1][0]), (mvs[0][1], mvs[1][1]), refs, comp, param, mask_off)
 
 
-def make_mc_units(w, h, layout, rng, nrefs=2, compound_frac=0.3, mv_px=64, sb=64, min_bs=8, blocks=None):
+def make_mc_units(w, h, layout, rng, nrefs=2, compound_frac=0.3, mv_px=64, sb=64, min_bs=8, blocks=None,
+                  mv_mode="uniform", mv_noise_px=2):
     """Inter prediction units for one frame: every block predicted from one reference (put)
     or two (compound: avg / w_avg / mask / seg, uniformly), filters uniform over the nine
-    8-tap pairs and bilinear, MVs uniform in +-mv_px at 1/8 pel. Returns (units bucketed by
-    plane group and shape class, class_start[2 * MC_NCLASS + 1], mask buffer)."""
+    8-tap pairs and bilinear. MVs at 1/8 pel: mv_mode "uniform" draws each block's MVs
+    uniformly in +-mv_px (SURVEY.md §8(d) config 3, the worst case for reference reuse);
+    "coherent" gives every 64x64 superblock one motion per reference (uniform in +-mv_px) and
+    each block that motion plus noise uniform in +-mv_noise_px, as real streams' spatially
+    correlated motion fields look. Returns (units bucketed by plane group and shape class,
+    class_start[2 * MC_NCLASS + 1], mask buffer)."""
     ss_h = 1 if layout in (1, 2) else 0
     ss_v = 1 if layout == 1 else 0
     seg_h, seg_v = (ss_h, ss_v) if layout else (0, 0)
     if blocks is None:
         blocks = partition_blocks(w, h, rng, sb=sb, min_bs=min_bs)
     luma, chroma, masks, moff = [], [], [], 0
+    sb_mv = {}
     for (x, y, bw, bh) in blocks:
         f2d = int(rng.integers(0, 10))
-        mvs = [(int(rng.integers(-8 * mv_px, 8 * mv_px + 1)), int(rng.integers(-8 * mv_px, 8 * mv_px + 1)))
-               for _ in range(2)]
+        if mv_mode == "coherent":
+            key = (x // 64, y // 64)
+            if key not in sb_mv:
+                sb_mv[key] = [(int(rng.integers(-8 * mv_px, 8 * mv_px + 1)), int(rng.integers(-8 * mv_px, 8 * mv_px + 1)))
+                              for _ in range(2)]
+            n8 = 8 * mv_noise_px
+            mvs = [(m[0] + int(rng.integers(-n8, n8 + 1)), m[1] + int(rng.integers(-n8, n8 + 1))) for m in sb_mv[key]]
+        else:
+            mvs = [(int(rng.integers(-8 * mv_px, 8 * mv_px + 1)), int(rng.integers(-8 * mv_px, 8 * mv_px + 1)))
+                   for _ in range(2)]
         cmp_ = nrefs > 1 and rng.random() < compound_frac
         if cmp_:
             r = rng.choice(nrefs, 2, replace=False)
