@@ -414,6 +414,36 @@ def timed_region(step, steps, sync, world, device):
     return float(t.item())
 
 
+def single_stream(args, world, rank, local):
+    """One stream, frame-pipelined over the ranks: every rank builds the same
+    synthetic GOP (descriptor sets shared by reference count), prepares its own frames, and the
+    timed region decodes the whole stream `steps` times; value = frames decoded / wall time."""
+    from rav1d_amd.sstream import DeviceExecutor, PipelinedStream, make_stream_specs
+    specs = make_stream_specs(W, H, BPC, LAYOUT, args.single_stream, 0x55400001, reuse=True)
+    ctx = F.Context(local)
+    ex = DeviceExecutor(ctx)
+    for s in specs:
+        if s.idx % world == rank:
+            ex.prepare(s)
+    ps = PipelinedStream(ex, ex.alloc, rank, world, "cuda")
+    for _ in range(max(1, args.warmup)):
+        ps.run(specs)
+    torch.cuda.synchronize()
+    elapsed = timed_region(lambda: ps.run(specs), args.steps, torch.cuda.synchronize, world, "cuda")
+    frames = args.steps * len(specs)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "decoded Mpixels/s (one 4K 10-bit 4:2:0 stream, frames pipelined over the GPUs)",
+            "value": round(frames * W * H / elapsed / 1e6, 2), "unit": "Mpixels/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "fps": round(frames / elapsed, 2), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "u16", "data": "synthetic hierarchical GOP (rav1d_amd.sstream)",
+            "config": {"workload": f"one 4K10 stream of {len(specs)} frames per step, frame k on rank k % N, "
+                                   f"references sent point to point", "parallelism": f"frame-pipelined x{world}"}}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -424,6 +454,9 @@ def main():
     ap.add_argument("--no-intra", action="store_true", help="skip the separate 1080p8 intra measurement")
     ap.add_argument("--no-verify", action="store_true", help="skip the per-rank oracle check of the output")
     ap.add_argument("--no-extra", action="store_true", help="skip the coherent-motion MC and output-side measurements")
+    ap.add_argument("--single-stream", type=int, default=0, metavar="FRAMES",
+                    help="instead of replicas: one 4K10 stream of FRAMES frames (hierarchical GOP of 8), frame k "
+                         "reconstructed on rank k %% N, references exchanged point to point (rav1d_amd.sstream)")
     ap.add_argument("--mv", choices=["uniform", "coherent"], default="uniform",
                     help="motion field of the timed frame (uniform: SURVEY.md 8(d) config 3)")
     args = ap.parse_args()
@@ -435,6 +468,9 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     stream = torch.cuda.current_stream()
+
+    if args.single_stream:
+        return single_stream(args, world, rank, local)
 
     cfg = broadcast_config({"w": W, "h": H, "bpc": BPC, "layout": LAYOUT,
                             "seeds": [0x4C100001 + r for r in range(world)]}, world)
