@@ -57,6 +57,15 @@ __host__ __device__ constexpr int itx_lanes(int tx) {
 }
 constexpr int kItxThreads = 256;
 __host__ __device__ constexpr int itx_blocks_per_wg(int tx) { return kItxThreads / itx_lanes(tx); }
+// Rounds of itx_blocks_per_wg blocks per workgroup: the small sizes' loads of all rounds are in
+// flight together (4-lane blocks: 4 rounds, 8-lane: 2).
+#ifndef MI_ITX_ROUNDS4
+#define MI_ITX_ROUNDS4 4
+#endif
+#ifndef MI_ITX_ROUNDS8
+#define MI_ITX_ROUNDS8 2
+#endif
+__host__ __device__ constexpr int itx_rounds(int tx) { return itx_lanes(tx) <= 4 ? MI_ITX_ROUNDS4 : itx_lanes(tx) <= 8 ? MI_ITX_ROUNDS8 : 1; }
 
 // Which transform types are legal for a size (src/itx.rs:400-457): 16 types for sizes up to
 // 16 on both sides except 16x16 (12 types), DCT_DCT + IDTX when a side is 32, DCT_DCT only

@@ -19,6 +19,7 @@
 // integer networks, not contractions).
 #include "common.h"
 #include "itx_1d.h"
+#include <type_traits>
 
 namespace mi {
 
@@ -67,11 +68,15 @@ __device__ __forceinline__ typename Vec4<Px>::T pack4(const int *o) {
     }
 }
 
+// a[i] for i in 0..2 as selects (a dynamic index into the kernel-argument struct would make
+// the compiler copy the whole struct to scratch)
+template <typename T> __device__ __forceinline__ T sel3(const T (&v)[3], int i) { return i == 0 ? v[0] : i == 1 ? v[1] : v[2]; }
+
 template <int TX, typename Px, typename Cf, typename Lt, bool Wide>
 __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     constexpr TxDim D = tx_dim(TX);
     constexpr int Wd = D.w, Ht = D.h, SH = imin_c(Ht, 32), SW = imin_c(Wd, 32);
-    constexpr int TPB = itx_lanes(TX), BPW = kItxThreads / TPB;
+    constexpr int TPB = itx_lanes(TX), BPW = kItxThreads / TPB, ROUNDS = itx_rounds(TX);
     constexpr int LS = Wd + 1;                        // padded LDS row stride
     constexpr bool Rect2 = (Wd == 2 * Ht) || (Ht == 2 * Wd);
     constexpr int Shift = D.shift, Rnd = (1 << Shift) >> 1;
@@ -81,36 +86,47 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
 
     const int t = threadIdx.x;
     const int lb = t / TPB, j = t % TPB;
-    const int bi = a.blk_start[TX] + lwg * BPW + lb;
-    bool valid = bi < a.blk_start[TX + 1];
-
-    MiTxBlock b{};
-    if (valid) {
-        b = a.blocks[bi];
-        // a descriptor the reference could never issue (wrong size group, a type the size's
-        // table slot lacks, a rectangle outside its plane) is skipped and reported
-        const bool ok = b.tx == TX && b.txtp < 17 && ((itx_legal_types(TX) >> b.txtp) & 1) && b.plane < 3 &&
-                        b.x + Wd <= a.pw[b.plane] && b.y + Ht <= a.ph[b.plane];
-        if (!ok) {
-            valid = false;
-            if (j == 0) atomicOr(a.err, 2);
-        }
-    }
+    // per-plane arguments as locals (selected by value, never by address into the kernarg)
+    uint8_t *const plane3[3] = { a.plane[0], a.plane[1], a.plane[2] };
+    const int64_t stride3[3] = { a.stride[0], a.stride[1], a.stride[2] };
+    const int pw3[3] = { a.pw[0], a.pw[1], a.pw[2] }, ph3[3] = { a.ph[0], a.ph[1], a.ph[2] };
     const int bdmax = a.bdmax;
-    Cf *cf = reinterpret_cast<Cf *>(a.coef) + b.coef_off;
-    const bool wht = (TX == 0) && b.txtp == 16;
-    const bool dconly = b.txtp == 0 && b.eob < 1;
     Lt *tmp = lds + lb * SH * LS;
 
-    // ---- 1. prefetch destination chunks ----
-    uint8_t *pbase = a.plane[b.plane] + (int64_t)b.y * a.stride[b.plane] + (int64_t)b.x * sizeof(Px);
-    const int64_t st = a.stride[b.plane];
-    V pix[NCH];
+    // ---- 1. every round's descriptor, destination chunks and DC coefficient in flight at
+    // once: small blocks carry little work per load, so a workgroup takes ROUNDS x BPW of
+    // them and overlaps their memory latency instead of paying it once per round ----
+    MiTxBlock bk[ROUNDS];
+    bool vk[ROUNDS];
+    int dk[ROUNDS];
+    V pk[ROUNDS][NCH];
 #pragma unroll
-    for (int k = 0; k < NCH; k++) {
-        const int c = j + k * TPB;
-        if (valid && c < Ht * CPR)
-            pix[k] = *reinterpret_cast<const V *>(pbase + (int64_t)(c / CPR) * st + (c % CPR) * 4 * sizeof(Px));
+    for (int rd = 0; rd < ROUNDS; rd++) {
+        const int bi = a.blk_start[TX] + (lwg * ROUNDS + rd) * BPW + lb;
+        bool valid = bi < a.blk_start[TX + 1];
+        MiTxBlock b{};
+        if (valid) {
+            b = a.blocks[bi];
+            // a descriptor the reference could never issue (wrong size group, a type the
+            // size's table slot lacks, a rectangle outside its plane) is skipped and reported
+            const bool ok = b.tx == TX && b.txtp < 17 && ((itx_legal_types(TX) >> b.txtp) & 1) &&
+                            b.plane < 3 && b.x + Wd <= sel3(pw3, b.plane) && b.y + Ht <= sel3(ph3, b.plane);
+            if (!ok) {
+                valid = false;
+                if (j == 0) atomicOr(a.err, 2);
+            }
+        }
+        const uint8_t *pbase = sel3(plane3, b.plane) + (int64_t)b.y * sel3(stride3, b.plane) + (int64_t)b.x * sizeof(Px);
+        const int64_t st = sel3(stride3, b.plane);
+#pragma unroll
+        for (int c4 = 0; c4 < NCH; c4++) {
+            const int c = j + c4 * TPB;
+            if (valid && c < Ht * CPR)
+                pk[rd][c4] = *reinterpret_cast<const V *>(pbase + (int64_t)(c / CPR) * st + (c % CPR) * 4 * sizeof(Px));
+        }
+        dk[rd] = valid && b.txtp == 0 && b.eob < 1 ? (int)(reinterpret_cast<const Cf *>(a.coef) + b.coef_off)[0] : 0;
+        bk[rd] = b;
+        vk[rd] = valid;
     }
 
     int row_lo, col_lo;
@@ -118,15 +134,27 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     else { row_lo = (int)((unsigned)~bdmax << 7); col_lo = (int)((unsigned)~bdmax << 5); }
     const int row_hi = ~row_lo, col_hi = ~col_lo;
 
+#pragma unroll
+    for (int rd = 0; rd < ROUNDS; rd++) {
+    const MiTxBlock b = bk[rd];
+    const bool valid = vk[rd];
+    V pix[NCH];
+#pragma unroll
+    for (int c4 = 0; c4 < NCH; c4++) pix[c4] = pk[rd][c4];
+    Cf *cf = reinterpret_cast<Cf *>(a.coef) + b.coef_off;
+    const bool wht = (TX == 0) && b.txtp == 16;
+    const bool dconly = b.txtp == 0 && b.eob < 1;
+    uint8_t *pbase = sel3(plane3, b.plane) + (int64_t)b.y * sel3(stride3, b.plane) + (int64_t)b.x * sizeof(Px);
+    const int64_t st = sel3(stride3, b.plane);
+
     int dc = 0;
     if (valid && dconly) {
-        dc = (int)cf[0];
+        dc = dk[rd];
         if (Rect2) dc = (dc * 181 + 128) >> 8;
         dc = (dc * 181 + 128) >> 8;
         dc = (dc + Rnd) >> Shift;
         dc = (dc * 181 + 128 + 2048) >> 12;
     }
-
     // ---- 2. row pass ----
     if (valid && !dconly && j < SH) {
         int r[Wd];
@@ -227,6 +255,8 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
         }
     }
     if (valid && dconly && j == 0 && a.zero_coefs) cf[0] = 0;
+    if (ROUNDS > 1) __syncthreads();     // the next round reuses this block's LDS rows
+    }
 }
 
 // One launch for every size. The workgroups of the 64- and 32-point sizes come first in the
@@ -236,13 +266,19 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
 // 46.4 us at 4K10; the small sizes lose little from the larger register budget, the large
 // ones stop being a serial tail.
 template <typename Px, typename Cf, typename Lt, bool Wide>
-__global__ __launch_bounds__(kItxThreads) void itx_frame_kernel(ItxArgs a) {
+#ifndef MI_ITX_MINW
+#define MI_ITX_MINW 4
+#endif
+__global__ __launch_bounds__(kItxThreads, MI_ITX_MINW) void itx_frame_kernel(ItxArgs a) {
     __shared__ Lt lds[itx_lds_max(true) > itx_lds_max(false) ? itx_lds_max(true) : itx_lds_max(false)];
     const int wg = blockIdx.x;
-    int i = 0;
-    while (i < 18 && wg >= a.wg_start[i + 1]) i++;
-    const int s = a.wg_size[i];
-    const int lwg = wg - a.wg_start[i];
+    // the size range holding this workgroup, with compile-time indices only (a runtime index
+    // into the kernel-argument struct makes the compiler copy it to scratch)
+    int s = a.wg_size[0], base = a.wg_start[0];
+#pragma unroll
+    for (int k = 1; k < 19; k++)
+        if (wg >= a.wg_start[k]) { s = a.wg_size[k]; base = a.wg_start[k]; }
+    const int lwg = wg - base;
     switch (s) {
 #define CASE(n) case n: itx_size<n, Px, Cf, Lt, Wide>(a, lwg, lds); break;
         CASE(0) CASE(1) CASE(2) CASE(5) CASE(6) CASE(7) CASE(8) CASE(13) CASE(14)
@@ -259,7 +295,8 @@ int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start) {
         a.wg_start[i] = wg;
         a.wg_size[i] = sz;
         const int n = (int)(size_start[sz + 1] - size_start[sz]);
-        wg += (n + itx_blocks_per_wg(sz) - 1) / itx_blocks_per_wg(sz);
+        const int per_wg = itx_blocks_per_wg(sz) * itx_rounds(sz);
+        wg += (n + per_wg - 1) / per_wg;
     }
     a.wg_start[19] = wg;
     for (int k = 0; k <= 19; k++) a.blk_start[k] = (int)size_start[k];
