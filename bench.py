@@ -287,6 +287,63 @@ def output_4k10(ctx, stream, reps=10):
     return res
 
 
+def real_streams(ctx, reps=3):
+    """configs[0]/[1] on the reference's own streams (tests/golden/streams, MD5s from its meson
+    files): `8-bit/features/itut_t35` (1920x1080 8-bit intra) and `8-bit/intra/av1-1-b8-02-allintra`
+    (352x288, 39 frames), end to end: host front-end (libmi_av1dec.so) -> device
+    reconstruction + in-loop filters (mi_frame_run, one frame at a time, mi_frame_end after each)
+    -> mi_output_picture into host memory -> product md5 muxer, verified against the vector's
+    MD5. Beside it: the front-end alone, and the CPU restatement (oracle/, single thread) decoding
+    the same stream from the same front-end (kind "port": rav1d's own CLI cannot be built here)."""
+    from rav1d_amd.av1dec import Av1Decoder, ivf_frames
+    from rav1d_amd.output import Muxer
+    from rav1d_amd.stream import decode_to_muxer
+    from tests.stream_lib import decode_stream
+    gold = os.path.join(ROOT, "tests", "golden", "streams")
+    vecs = {v["name"]: v for v in json.load(open(os.path.join(gold, "vectors.json")))}
+    out = {}
+    for name in ("itut_t35", "av1-1-b8-02-allintra"):
+        v = vecs[name]
+        data = open(os.path.join(gold, v["file"]), "rb").read()
+        m = Muxer("md5")
+        n = decode_to_muxer(ctx, data, m)
+        ok = m.verify(v["md5"]) == 0
+        m.close()
+        best = 1e9
+        for _ in range(reps):
+            m = Muxer("md5")
+            t0 = time.perf_counter()
+            decode_to_muxer(ctx, data, m)
+            best = min(best, time.perf_counter() - t0)
+            m.close()
+        fe = 1e9
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            dec = Av1Decoder()
+            for tu in ivf_frames(data):
+                dec.send(tu)
+                for _ev in dec.events():
+                    pass
+            fe = min(fe, time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        cmd5, _ = decode_stream(data)
+        cpu = time.perf_counter() - t0
+        fr = None
+        dec = Av1Decoder()
+        for tu in ivf_frames(data):
+            dec.send(tu)
+            for ev in dec.events():
+                if ev.frame:
+                    fr = (ev.frame.contents.w, ev.frame.contents.h)
+        px = n * fr[0] * fr[1]
+        out[name] = dict(frames=n, size=f"{fr[0]}x{fr[1]} 8-bit 4:2:0", md5_verified=ok,
+                         gpu_end_to_end_ms=round(best * 1e3, 3), gpu_fps=round(n / best, 1),
+                         gpu_mpx_per_s=round(px / best / 1e6, 2), front_end_ms=round(fe * 1e3, 3),
+                         cpu_oracle_ms=round(cpu * 1e3, 1), cpu_oracle_mpx_per_s=round(px / cpu / 1e6, 2),
+                         cpu_oracle_md5_verified=cmd5 == v["md5"])
+    return out
+
+
 def per_launch(v, launches):
     return None if v is None else int(v // launches)
 
@@ -554,6 +611,7 @@ def main():
         if world == 1 and not args.no_extra:
             out["mc_coherent_4k10"] = mc_coherent(ctx, stream)
             out["output_4k10"] = output_4k10(ctx, stream)
+            out["real_streams"] = real_streams(ctx)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(fr)
         print(json.dumps(out))

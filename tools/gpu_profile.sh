@@ -23,3 +23,6 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/s
 echo "kernel stats done"; cat $OUT/bench_stats.json
 TRAFFIC_ONLY=1 bash $R/tools/gpu_pmc.sh $TAG/pmc > /dev/null || { echo "pmc failed"; exit 1; }
 python3 $R/tools/traffic_json.py $OUT > $OUT/traffic.json && cat $OUT/traffic.json
+# the same passes on the coherent motion field (bench --mv coherent): MC traffic beside the uniform one
+BENCH_ARGS="--mv coherent" TRAFFIC_ONLY=1 bash $R/tools/gpu_pmc.sh $TAG/pmc_coh > /dev/null || { echo "pmc (coherent) failed"; exit 1; }
+python3 $R/tools/traffic_json.py $OUT pmc_coh > $OUT/traffic_coherent.json && echo "coherent traffic done"

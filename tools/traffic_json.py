@@ -55,10 +55,11 @@ def sized_bytes(d):
 
 def main():
     root = sys.argv[1]
+    sub = sys.argv[2] if len(sys.argv) > 2 else "pmc"     # the PMC passes' subdirectory
     fac = calib(root)
-    fetch = collect(os.path.join(root, "pmc", "p1"))
-    write = collect(os.path.join(root, "pmc", "p2"))
-    req = collect(os.path.join(root, "pmc", "p3"))
+    fetch = collect(os.path.join(root, sub, "p1"))
+    write = collect(os.path.join(root, sub, "p2"))
+    req = collect(os.path.join(root, sub, "p3"))
     creq = collect(os.path.join(root, "calib_TCC_EA0_RDREQ"))
     # calibration of the sized count: true bytes / sized bytes per read width (expect 1.0)
     sized_cal = {}
@@ -66,7 +67,7 @@ def main():
         if k.startswith("rd<") and sized_bytes(d):
             sized_cal[k[3:-1].strip()] = round(CALIB_BYTES / sized_bytes(d), 4)
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over "
-                     "`bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-fg`; counters in KB",
+                     "`bench.py --steps 5 --warmup 2` (pipeline only); counters in KB",
            "calibration": {f"{c}@{w}B": round(v, 4) for (c, w), v in sorted(fac.items())},
            "sized_read_calibration": sized_cal,
            "kernels": {}, "stages": {}}
