@@ -670,7 +670,7 @@ static int fg_setup(MiCtx *ctx, const MiPicture *in, const MiPicture *out, const
             a.chunks[p] = (a.pw[p] + 511) / 512;   // 64-lane waves per row, 8 contiguous px per lane
             a.grain[p] = p == 0 ? data->num_y_points != 0
                                 : (data->chroma_scaling_from_luma || data->num_uv_points[p - 1]);
-            nb += (int)(((int64_t)a.chunks[p] * a.ph[p] + 3) / 4);
+            nb += (int)(((int64_t)a.chunks[p] * a.ph[p] + 4 * mi::kFgItems - 1) / (4 * mi::kFgItems));
         }
         a.blk_start[3] = nb;
     }
@@ -1509,7 +1509,7 @@ int fg_strip(int pl, int layout, void *dst_row, const void *src_row, ptrdiff_t s
     a.ph[pl] = bh;
     a.chunks[pl] = (int)((pw + 511) / 512);
     a.grain[pl] = 1;
-    const int nb = (a.chunks[pl] * bh + 3) / 4;
+    const int nb = (a.chunks[pl] * bh + 4 * mi::kFgItems - 1) / (4 * mi::kFgItems);
     for (int q = 0; q < 4; q++) a.blk_start[q] = q <= pl ? 0 : nb;
     if (mi::launch_fg_call(a, s)) return -EIO;
     for (int r = 0; r < bh && !e; r++)

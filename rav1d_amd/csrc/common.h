@@ -263,6 +263,11 @@ struct LrCallArgs {
 };
 int launch_lr_call(const LrCallArgs &a, int bpc, hipStream_t s);
 
+#ifndef MI_FG_ITEMS
+#define MI_FG_ITEMS 1
+#endif
+constexpr int kFgItems = MI_FG_ITEMS;   // wave-items (512-px row segments) per wave in fg_apply_kernel (8K10 apply: 1 -> 72.5 us, 4 -> 75.7, 8 -> 78.4)
+
 struct FgArgs {
     MiFilmGrainData data;
     const uint8_t *src[3];

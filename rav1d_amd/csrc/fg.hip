@@ -372,127 +372,126 @@ __global__ __launch_bounds__(256) void fg_apply_kernel(FgArgs a) {
     const MiFilmGrainData &d = a.data;
     const bool grain = a.grain[p];
     const int wpr = a.chunks[p];   // waves per plane row
-    const int t = (b - a.blk_start[p]) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int y = t / wpr, seg = t - y * wpr;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int pw = a.pw[p], ph = a.ph[p];
-    const int x0 = (seg * 64 + (threadIdx.x & 63)) * 8;
-    const bool active = y < ph && x0 < pw;
-    const int n = active ? min(8, pw - x0) : 0;
     const int64_t st = a.stride[p];
-    const Px *src = reinterpret_cast<const Px *>(a.src[p] + (int64_t)y * st) + x0;
-    Px *dst = reinterpret_cast<Px *>(a.dst[p] + (int64_t)y * st) + x0;
-    if (!grain) {   // uniform per workgroup: plain copy, no staging
-        if (active) {
-            int e[8];
-            load8(e, src, n);
-            store8(dst, e, n);
-        }
-        return;
-    }
-
-    // scaling LUT (1 << bpc entries) -> registers; written to LDS after the pixel loads issue
-    const int nw = (1 << a.bpc) >> 2;
-    uint32_t lutw[4];
-    {
-        const uint32_t *g = reinterpret_cast<const uint32_t *>(
-            a.scaling + (p && !d.chroma_scaling_from_luma ? p : 0) * 4096);
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int i = threadIdx.x + 256 * k;
-            lutw[k] = i < nw ? g[i] : 0;
-        }
-    }
-    int sv[8];
-    if (active) load8(sv, src, n);
     const int sx = p ? a.ss_x : 0, sy = p ? a.ss_y : 0;
-
-    // co-located luma (chroma planes): 8 << sx samples from x0 << sx, clamped at w - 1
-    int lum[8];
-    if (p && active) {
-        const int lx0 = x0 << sx;
-        const Px *luma = reinterpret_cast<const Px *>(a.src[0] + (int64_t)(y << sy) * a.stride[0]);
-        if (sx) {
-            int l0[8], l1[8];
-            if (lx0 + 16 <= a.w) {
-                load8(l0, luma + lx0, 8);
-                load8(l1, luma + lx0 + 8, 8);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    l0[j] = luma[min(lx0 + j, a.w - 1)];
-                    l1[j] = luma[min(lx0 + 8 + j, a.w - 1)];
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                lum[j] = (l0[2 * j] + l0[2 * j + 1] + 1) >> 1;
-                lum[4 + j] = (l1[2 * j] + l1[2 * j + 1] + 1) >> 1;
-            }
-        } else if (n == 8) {
-            load8(lum, luma + lx0, 8);
-        } else {
-#pragma unroll
-            for (int j = 0; j < 8; j++) lum[j] = luma[min(lx0 + j, a.w - 1)];
-        }
-    }
-
-    // grain samples of this chunk's block
     const int bdm8 = a.bpc - 8, bdmax = (1 << a.bpc) - 1;
     const int gctr = 128 << bdm8, gmin = -gctr, gmax = gctr - 1;
-    int g[8];
-    if (active) {
-        GrainPos q;
-        q.sx = sx; q.sy = sy;
-        const int bsh = 32 >> sy, bsw = 32 >> sx;
-        const int lrow = y >> (5 - sy), row = lrow + a.row_off;
-        q.yy = y & (bsh - 1);
-        q.bi = x0 >> (5 - sx);
-        q.xx0 = x0 & (bsw - 1);
-        const uint8_t *offr = a.offsets + row * a.nblocks;
-        const uint8_t *offp = row ? offr - a.nblocks : offr;
-        q.rc = offr[q.bi];
-        q.hx = q.vy = false;
-        q.rl = q.rt = q.rtl = 0;
-        if (d.overlap_flag) {
-            const int bh = p ? (min(a.h - lrow * 32, 32) + sy) >> sy : min(a.h - lrow * 32, 32);
-            const int ystart = row ? min(2 >> sy, bh) : 0;
-            q.hx = q.bi > 0 && q.xx0 == 0;     // blocks are >= 1 px wide: xstart > 0 iff bi > 0
-            q.vy = q.yy < ystart;
-            if (q.hx) q.rl = offr[q.bi - 1];
-            if (q.vy) q.rt = offp[q.bi];
-            if (q.hx && q.vy) q.rtl = offp[q.bi - 1];
-        }
-        grain8(a.lut + p * kGH * kGP, q, gmin, gmax, g);
-    }
-
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int i = threadIdx.x + 256 * k;
-        if (i < nw) scl32[i] = lutw[k];
-    }
-    __syncthreads();
-    if (!active) return;
-
     int minv = 0, maxv = bdmax;
     if (d.clip_to_restricted_range) {
         minv = 16 << bdm8;
         maxv = (p == 0 || a.is_id ? 235 : 240) << bdm8;
     }
-    int ov[8];
+
+    // the scaling LUT (1 << bpc entries) staged once per workgroup, for kFgItems wave-items
+    // per wave (a workgroup per single row segment spent as many loads on the LUT as on pixels)
+    if (grain) {
+        const int nw = (1 << a.bpc) >> 2;
+        const uint32_t *g = reinterpret_cast<const uint32_t *>(
+            a.scaling + (p && !d.chroma_scaling_from_luma ? p : 0) * 4096);
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-        int val = sv[j];
+        for (int k = 0; k < 4; k++) {
+            const int i = threadIdx.x + 256 * k;
+            if (i < nw) scl32[i] = g[i];
+        }
+        __syncthreads();
+    }
+
+    for (int it = 0; it < kFgItems; it++) {
+        const int t = ((b - a.blk_start[p]) * kFgItems + it) * 4 + wave;
+        const int y = t / wpr, seg = t - y * wpr;
+        const int x0 = (seg * 64 + (threadIdx.x & 63)) * 8;
+        const bool active = y < ph && x0 < pw;
+        if (!__builtin_amdgcn_readfirstlane((int)(y < ph))) break;    // past the plane: wave-uniform
+        const int n = active ? min(8, pw - x0) : 0;
+        const Px *src = reinterpret_cast<const Px *>(a.src[p] + (int64_t)y * st) + x0;
+        Px *dst = reinterpret_cast<Px *>(a.dst[p] + (int64_t)y * st) + x0;
+        if (!grain) {   // uniform per workgroup: plain copy
+            if (active) {
+                int e[8];
+                load8(e, src, n);
+                store8(dst, e, n);
+            }
+            continue;
+        }
+        if (!active) continue;
+        int sv[8];
+        load8(sv, src, n);
+
+        // co-located luma (chroma planes): 8 << sx samples from x0 << sx, clamped at w - 1
+        int lum[8];
         if (p) {
-            val = lum[j];
-            if (!d.chroma_scaling_from_luma) {
-                const int comb = lum[j] * d.uv_luma_mult[p - 1] + sv[j] * d.uv_mult[p - 1];
-                val = min(max((comb >> 6) + d.uv_offset[p - 1] * (1 << bdm8), 0), bdmax);
+            const int lx0 = x0 << sx;
+            const Px *luma = reinterpret_cast<const Px *>(a.src[0] + (int64_t)(y << sy) * a.stride[0]);
+            if (sx) {
+                int l0[8], l1[8];
+                if (lx0 + 16 <= a.w) {
+                    load8(l0, luma + lx0, 8);
+                    load8(l1, luma + lx0 + 8, 8);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        l0[j] = luma[min(lx0 + j, a.w - 1)];
+                        l1[j] = luma[min(lx0 + 8 + j, a.w - 1)];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    lum[j] = (l0[2 * j] + l0[2 * j + 1] + 1) >> 1;
+                    lum[4 + j] = (l1[2 * j] + l1[2 * j + 1] + 1) >> 1;
+                }
+            } else if (n == 8) {
+                load8(lum, luma + lx0, 8);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; j++) lum[j] = luma[min(lx0 + j, a.w - 1)];
             }
         }
-        const int noise = round2i(scl[val] * g[j], d.scaling_shift);
-        ov[j] = min(max(sv[j] + noise, minv), maxv);
+
+        // grain samples of this chunk's block
+        int g[8];
+        {
+            GrainPos q;
+            q.sx = sx; q.sy = sy;
+            const int bsh = 32 >> sy, bsw = 32 >> sx;
+            const int lrow = y >> (5 - sy), row = lrow + a.row_off;
+            q.yy = y & (bsh - 1);
+            q.bi = x0 >> (5 - sx);
+            q.xx0 = x0 & (bsw - 1);
+            const uint8_t *offr = a.offsets + row * a.nblocks;
+            const uint8_t *offp = row ? offr - a.nblocks : offr;
+            q.rc = offr[q.bi];
+            q.hx = q.vy = false;
+            q.rl = q.rt = q.rtl = 0;
+            if (d.overlap_flag) {
+                const int bh = p ? (min(a.h - lrow * 32, 32) + sy) >> sy : min(a.h - lrow * 32, 32);
+                const int ystart = row ? min(2 >> sy, bh) : 0;
+                q.hx = q.bi > 0 && q.xx0 == 0;     // blocks are >= 1 px wide: xstart > 0 iff bi > 0
+                q.vy = q.yy < ystart;
+                if (q.hx) q.rl = offr[q.bi - 1];
+                if (q.vy) q.rt = offp[q.bi];
+                if (q.hx && q.vy) q.rtl = offp[q.bi - 1];
+            }
+            grain8(a.lut + p * kGH * kGP, q, gmin, gmax, g);
+        }
+
+        int ov[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            int val = sv[j];
+            if (p) {
+                val = lum[j];
+                if (!d.chroma_scaling_from_luma) {
+                    const int comb = lum[j] * d.uv_luma_mult[p - 1] + sv[j] * d.uv_mult[p - 1];
+                    val = min(max((comb >> 6) + d.uv_offset[p - 1] * (1 << bdm8), 0), bdmax);
+                }
+            }
+            const int noise = round2i(scl[val] * g[j], d.scaling_shift);
+            ov[j] = min(max(sv[j] + noise, minv), maxv);
+        }
+        store8(dst, ov, n);
     }
-    store8(dst, ov, n);
 }
 
 int init_fg_tables() {
