@@ -59,12 +59,41 @@ void oracle_decode_frame(const MiDecFrame *f, void *const pic[3], void *const sc
                           f->cdef_damping, f->cdef_y, f->cdef_uv);
         cdef_out = scratch1;
     }
-    /* 4. loop restoration: (CDEF output, deblocked) -> scratch2 */
+    void *const *deblocked = pic;
+    /* 3b. super-resolution (recon.rs:4215-4285 filter_sbrow_resize; lf_apply.rs backup_lpf
+     * resizes the deblocked rows loop restoration reads the same way): every picture has the
+     * upscaled geometry; the CDEF output goes to scratch2, the deblocked picture to scratch1
+     * (the CDEF output at coded width is no longer read), and LR writes into pic. */
+    if (f->up_w != f->w) {
+        const int ss_hor = layout == 1 || layout == 2;
+        const int in_cw = (f->w + ss_hor) >> ss_hor, out_cw = (f->up_w + ss_hor) >> ss_hor;
+        int step[2], start[2];
+        step[0] = ((f->w << 14) + (f->up_w >> 1)) / f->up_w;          /* scale_fac, decode.rs:4644 */
+        step[1] = ((in_cw << 14) + (out_cw >> 1)) / out_cw;
+        for (int k = 0; k < 2; k++) {                                  /* get_upscale_x0, :4776 */
+            const int iw = k ? in_cw : f->w, ow = k ? out_cw : f->up_w;
+            const int err = ow * step[k] - (iw << 14);
+            start[k] = ((-((ow - iw) << 13) + (ow >> 1)) / ow + 128 - err / 2) & 0x3fff;
+        }
+        const int bw4 = ((f->w + 7) >> 3) << 1;
+        void *const *src_sets[2] = { cdef_out, pic };
+        void *const *dst_sets[2] = { scratch2, scratch1 };
+        for (int s2 = 0; s2 < (f->restore_planes ? 2 : 1); s2++)
+            for (int p = 0; p < nplanes; p++) {
+                const int sh = p ? ss_hor : 0, sv = p ? ss_ver : 0;
+                oracle_mc_resize(dst_sets[s2][p], strides[p], src_sets[s2][p], strides[p], (f->up_w + sh) >> sh,
+                                 (f->h + sv) >> sv, (4 * bw4 + sh) >> sh, step[p != 0], start[p != 0], bpc);
+            }
+        cdef_out = scratch2;
+        deblocked = f->restore_planes ? scratch1 : scratch2;
+    }
+    /* 4. loop restoration: (CDEF output, deblocked) -> scratch2 (pic with super-resolution) */
     void *const *final = cdef_out;
     if (f->restore_planes) {
-        oracle_lr_frame(scratch2, (void *const *)cdef_out, pic, strides, f->w, f->h, layout, bpc, f->sb128,
+        void *const *lr_out = f->up_w != f->w ? pic : scratch2;
+        oracle_lr_frame(lr_out, (void *const *)cdef_out, deblocked, strides, f->up_w, f->h, layout, bpc, f->sb128,
                         f->restore_planes, f->lr_unit_size, f->lr_mask, f->lr_sb128w);
-        final = scratch2;
+        final = lr_out;
     }
     (void)ss_ver;
     for (int p = 0; p < 3; p++) out[p] = p < nplanes ? final[p] : NULL;

@@ -53,17 +53,20 @@ struct Section {
 int validate(const MiDecFrame *f, const MiFramePictures *p) {
     if (f->bpc != 8 && f->bpc != 10 && f->bpc != 12) return -EINVAL;
     if (f->layout < 0 || f->layout > 3 || f->w <= 0 || f->h <= 0) return -EINVAL;
+    // super-resolution (up_w > w): every picture has the upscaled geometry
+    if (f->up_w < f->w || f->up_w > 2 * f->w + 16) return -EINVAL;
     const MiPicture *pics[4] = { &p->recon, &p->deblocked, &p->cdef, &p->restored };
     for (const MiPicture *q : pics)
-        if (q->bpc != f->bpc || q->layout != f->layout || q->w != f->w || q->h != f->h || !q->data[0] ||
-            (f->layout && (!q->data[1] || !q->data[2])))
+        if (q->bpc != f->bpc || q->layout != f->layout || q->w != f->up_w || q->h != f->h || !q->data[0] ||
+            (f->layout && (!q->data[1] || !q->data[2])) || q->stride[0] != p->recon.stride[0] ||
+            q->stride[1] != p->recon.stride[1])
             return -EINVAL;
     const int ss_hor = f->layout == 1 || f->layout == 2, ss_ver = f->layout == 1;
     const int nplanes = f->layout ? 3 : 1;
-    const int aw = (f->w + 127) & ~127, ah = (f->h + 127) & ~127;
+    const int aw = (f->w + 127) & ~127, ah = (f->h + 127) & ~127, aw_up = (f->up_w + 127) & ~127;
     const size_t pb = f->bpc == 8 ? 1 : 2;
     for (int pl = 0; pl < nplanes; pl++)
-        if ((size_t)std::abs(p->recon.stride[pl ? 1 : 0]) < (size_t)(aw >> (pl ? ss_hor : 0)) * pb) return -EINVAL;
+        if ((size_t)std::abs(p->recon.stride[pl ? 1 : 0]) < (size_t)(aw_up >> (pl ? ss_hor : 0)) * pb) return -EINVAL;
     if (f->n_intra < 0 || (f->n_intra && (!f->intra || !f->intra_tx || !f->dep_start))) return -EINVAL;
     if (f->n_intra && f->ncoef < 16) return -EINVAL;
     if (f->dep_start && (f->dep_start[0] != 0 || f->dep_start[f->n_intra] != f->n_deps)) return -EINVAL;
@@ -86,7 +89,10 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
         if (mode == MI_IPRED_PAL) {
             if ((size_t)b.aux_off + (size_t)b.w * b.h > f->nidx || (size_t)b.pal_off + 8 > f->npal) return -EINVAL;
         } else if (mode == MI_INTRA_IBC) {
-            return -EINVAL;   // intra block copy: not produced by the front-end yet
+            // the reference area the copy clamps its taps to lies inside the picture
+            if (b.filt_idx != (sh | (sv << 1)) || !b.max_w || !b.max_h || b.max_w > (aw >> sh) ||
+                b.max_h > (ah >> sv) || (b.mode & MI_IPRED_II))
+                return -EINVAL;
         } else if (mode != MI_IPRED_CFL && mode > 13) {
             return -EINVAL;
         }
@@ -209,6 +215,7 @@ int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, i
         MiIntraFrame fr;
         memset(&fr, 0, sizeof(fr));
         fr.pic = pics->recon;
+        fr.pic.w = f->w;                 // coded width (super-resolution upscales after CDEF)
         fr.blocks = (const MiIntraBlock *)D(0);
         fr.tx = (const MiTxBlock *)D(1);
         fr.dep_start = (const int32_t *)D(2);
@@ -219,7 +226,10 @@ int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, i
         fr.n = n;
         if ((r = mi_intra_recon(ctx, &fr, 1, 0, stream))) return r;
     }
-    const MiPicture *cur = &pics->recon;
+    // the coded-width views of the pictures (stages before super-resolution)
+    MiPicture cp[4] = { pics->recon, pics->deblocked, pics->cdef, pics->restored };
+    for (MiPicture &q : cp) q.w = f->w;
+    const MiPicture *cur = &cp[0];
     int idx = 0;
     // 2. deblocking (lf_apply.rs:597-834), recon -> deblocked
     if (f->filter_y) {
@@ -233,11 +243,12 @@ int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, i
         lf.filter_uv = f->filter_uv;
         memcpy(lf.lim_e, f->lim_e, 64);
         memcpy(lf.lim_i, f->lim_i, 64);
-        if ((r = mi_deblock_frame_to(ctx, cur, &pics->deblocked, &lf, stream))) return r;
-        cur = &pics->deblocked;
+        if ((r = mi_deblock_frame_to(ctx, cur, &cp[1], &lf, stream))) return r;
+        cur = &cp[1];
         idx = 1;
     }
     const MiPicture *deblocked = cur;
+    int dbl_idx = idx;
     // 3. CDEF (cdef_apply.rs:159-507), deblocked -> cdef
     if (f->cdef_on) {
         MiCdef cd;
@@ -247,9 +258,33 @@ int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, i
         cd.damping = f->cdef_damping;
         memcpy(cd.y_strength, f->cdef_y, 8);
         memcpy(cd.uv_strength, f->cdef_uv, 8);
-        if ((r = mi_cdef_frame(ctx, cur, &pics->cdef, &cd, stream))) return r;
-        cur = &pics->cdef;
+        if ((r = mi_cdef_frame(ctx, cur, &cp[2], &cd, stream))) return r;
+        cur = &cp[2];
         idx = 2;
+    }
+    // 3b. super-resolution (recon.rs:4215-4285 filter_sbrow_resize for the CDEF output;
+    // lf_apply.rs backup_lpf resizes the deblocked rows loop restoration reads across stripe
+    // edges the same way): both upscaled into pictures no later stage still reads at coded width
+    const MiPicture *slot[4] = { &pics->recon, &pics->deblocked, &pics->cdef, &pics->restored };
+    if (f->up_w != f->w) {
+        // free slots: everything except cur (C) and deblocked (D)
+        int fr_[4], nf = 0;
+        for (int k = 0; k < 4; k++)
+            if (k != idx && k != dbl_idx) fr_[nf++] = k;
+        const int cu = fr_[0];
+        if ((r = mi_superres_frame(ctx, cur, slot[cu], stream))) return r;
+        int du = cu;
+        if (f->restore_planes) {
+            du = fr_[1];
+            if (deblocked != cur && (r = mi_superres_frame(ctx, deblocked, slot[du], stream))) return r;
+            if (deblocked == cur) du = cu;
+        }
+        // loop restoration writes into a slot holding neither input: the coded-width CDEF output
+        // (or, without CDEF, the coded-width deblocked picture) is no longer read
+        cur = slot[cu];
+        deblocked = slot[du];
+        idx = cu;
+        dbl_idx = du;
     }
     // 4. loop restoration (lr_apply.rs:261-329), (cdef, deblocked) -> restored
     if (f->restore_planes) {
@@ -260,8 +295,12 @@ int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, i
         lr.restore_planes = f->restore_planes;
         lr.unit_size_log2[0] = f->lr_unit_size[0];
         lr.unit_size_log2[1] = f->lr_unit_size[1];
-        if ((r = mi_lr_frame(ctx, cur, deblocked, &pics->restored, &lr, stream))) return r;
-        idx = 3;
+        int out = 3;
+        if (f->up_w != f->w)
+            for (int k = 0; k < 4; k++)
+                if (k != idx && k != dbl_idx) { out = k; break; }
+        if ((r = mi_lr_frame(ctx, cur, deblocked, slot[out], &lr, stream))) return r;
+        idx = out;
     }
     *final = idx;
     return 0;

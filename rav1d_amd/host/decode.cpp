@@ -127,6 +127,23 @@ private:
                            uint16_t (*masks)[32][2][2]);
     void create_lf_mask_intra(const Block &b, int has_chroma);
     void tile_fixups();
+
+    // intra block copy (decode.rs:1988-2135): the frame's refmvs blocks (per 4x4, padded by
+    // 8 units on each side), the DV candidate search, mv residual, var-tx tree and the
+    // inter-style residual walk that emits MI_INTRA_IBC work
+    std::vector<RefMvBlock> rmv;
+    int rmv_stride = 0;
+    RefMvBlock &rmv_at(int y4, int x4) { return rmv[(size_t)(y4 + 8) * rmv_stride + (x4 + 8)]; }
+    void splat_rmv(int bs, int bw4, int bh4, Mv mv, bool valid);
+    void find_dv(int bs, int edge_flags, Mv stack[2]);
+    int read_mv_comp(CdfMvComp &c);
+    void read_mv_residual(Mv &mv, CdfMv &cdf);
+    void read_tx_tree(int from, int depth, uint16_t *masks, int x_off, int y_off, int tbx, int tby);
+    void ibc_residual_tree(const Block &b, Mv mv, int tx, int depth, const uint16_t *split, int x_off, int y_off,
+                           int tbx, int tby, uint8_t (*txtp_map)[32]);
+    void push_ibc(const Block &b, Mv mv, int plane, int tx, int tbx, int tby, int px, int py, int eob_txtp_read,
+                  uint8_t *actx, uint8_t *lctx, int nact, int nlct, int *txtp);
+    int decode_ibc(Block &b, int bs, int edge_flags, int has_chroma);
 };
 
 // ------------------------------------------------------------------------------------------
@@ -1000,6 +1017,371 @@ void FrameDec::emit_intra(const Block &b, int edge_flags, const uint8_t *pal_idx
 // ------------------------------------------------------------------------------------------
 // blocks (decode.rs decode_b; C decode.c:723-2116), intra frames
 
+// ---- intra block copy ----------------------------------------------------------------------
+
+static const Mv kInvalidMv = { INT16_MIN, INT16_MIN };   // refmvs INVALID_MV: an intra block
+
+// refmvs splat_mv (refmvs.rs): the block's entry over its bw4 x bh4 units
+void FrameDec::splat_rmv(int bs, int bw4, int bh4, Mv mv, bool valid) {
+    RefMvBlock r{};
+    r.mv[0] = valid ? mv : kInvalidMv;
+    r.mv[1] = Mv{ 0, 0 };
+    r.ref[0] = 0;
+    r.ref[1] = -1;
+    r.bs = (uint8_t)bs;
+    r.mf = 0;
+    for (int y = 0; y < bh4; y++)
+        for (int x = 0; x < bw4; x++) rmv_at(by + y, bx + x) = r;
+}
+
+// rav1d_refmvs_find (refmvs.rs; C refmvs.c dav1d_refmvs_find) for ref = {INTRA_FRAME, none}:
+// the spatial candidates only (intra frames carry no temporal MVs), weights, the two-stage sort
+// and the clamp; stack[0..1] are the first two candidates (zero where there are fewer).
+void FrameDec::find_dv(int bs, int edge_flags, Mv stack[2]) {
+    struct Cand { Mv mv; int weight; } st[9];
+    int cnt = 0;
+    const int bw4 = k_bdim[bs].w4, bh4 = k_bdim[bs].h4;
+    const int w4c = imin(imin(bw4, 16), ts->col_end - bx), h4c = imin(imin(bh4, 16), ts->row_end - by);
+    auto add = [&](const RefMvBlock &c, int weight, int *have_refmv) {
+        if (c.mv[0] == kInvalidMv) return;             // intra block (no block copy)
+        if (c.ref[0] != 0) return;
+        *have_refmv = 1;
+        for (int m = 0; m < cnt; m++)
+            if (st[m].mv == c.mv[0]) {
+                st[m].weight += weight;
+                return;
+            }
+        if (cnt < 8) st[cnt++] = { c.mv[0], weight };
+    };
+    // scan_row / scan_col: weights by the first candidate's extent, then per candidate
+    auto scan_row = [&](int y4, int x4, int max_rows, int step, int *have) -> int {
+        const RefMvBlock *b0 = &rmv_at(y4, x4);
+        const int cbw = k_bdim[b0->bs].w4;
+        int len = imax(step, imin(bw4, cbw));
+        if (bw4 <= cbw) {
+            const int weight = bw4 == 1 ? 2 : imax(2, imin(2 * max_rows, (int)k_bdim[b0->bs].h4));
+            add(*b0, len * weight, have);
+            return weight >> 1;
+        }
+        for (int x = 0;;) {
+            add(rmv_at(y4, x4 + x), len * 2, have);
+            x += len;
+            if (x >= w4c) return 1;
+            len = imax(step, (int)k_bdim[rmv_at(y4, x4 + x).bs].w4);
+        }
+    };
+    auto scan_col = [&](int y4, int x4, int max_cols, int step, int *have) -> int {
+        const RefMvBlock *b0 = &rmv_at(y4, x4);
+        const int cbh = k_bdim[b0->bs].h4;
+        int len = imax(step, imin(bh4, cbh));
+        if (bh4 <= cbh) {
+            const int weight = bh4 == 1 ? 2 : imax(2, imin(2 * max_cols, (int)k_bdim[b0->bs].w4));
+            add(*b0, len * weight, have);
+            return weight >> 1;
+        }
+        for (int y = 0;;) {
+            add(rmv_at(y4 + y, x4), len * 2, have);
+            y += len;
+            if (y >= h4c) return 1;
+            len = imax(step, (int)k_bdim[rmv_at(y4 + y, x4).bs].h4);
+        }
+    };
+    int have_row = 0, have_col = 0, dummy = 0;
+    unsigned max_rows = 0, n_rows = ~0u, max_cols = 0, n_cols = ~0u;
+    if (by > ts->row_start) {
+        max_rows = imin((by - ts->row_start + 1) >> 1, 2 + (bh4 > 1));
+        n_rows = scan_row(by - 1, bx, max_rows, bw4 >= 16 ? 4 : 1, &have_row);
+    }
+    if (bx > ts->col_start) {
+        max_cols = imin((bx - ts->col_start + 1) >> 1, 2 + (bw4 > 1));
+        n_cols = scan_col(by, bx - 1, max_cols, bh4 >= 16 ? 4 : 1, &have_col);
+    }
+    if (n_rows != ~0u && (edge_flags & E444_TR) && imax(bw4, bh4) <= 16 && bw4 + bx < ts->col_end)
+        add(rmv_at(by - 1, bx + bw4), 4, &have_row);
+    const int nearest_cnt = cnt;
+    for (int n = 0; n < nearest_cnt; n++) st[n].weight += 640;
+    if ((n_rows | n_cols) != ~0u) add(rmv_at(by - 1, bx - 1), 4, &have_row);
+    for (int n = 2; n <= 3; n++) {
+        if ((unsigned)n > n_rows && (unsigned)n <= max_rows)
+            n_rows += scan_row(((by - 2 * n + 1) | 1), bx | 1, 1 + max_rows - n, bw4 >= 16 ? 4 : 2, &have_row);
+        if ((unsigned)n > n_cols && (unsigned)n <= max_cols)
+            n_cols += scan_col(by | 1, (bx - n * 2 + 1) | 1, 1 + max_cols - n, bh4 >= 16 ? 4 : 2, &have_col);
+    }
+    (void)dummy;
+    // bubble sorts: the nearest candidates, then the rest (stable for equal weights)
+    for (int len = nearest_cnt; len;) {
+        int last = 0;
+        for (int n = 1; n < len; n++)
+            if (st[n - 1].weight < st[n].weight) { std::swap(st[n - 1], st[n]); last = n; }
+        len = last;
+    }
+    for (int len = cnt; len > nearest_cnt;) {
+        int last = nearest_cnt;
+        for (int n = nearest_cnt + 1; n < len; n++)
+            if (st[n - 1].weight < st[n].weight) { std::swap(st[n - 1], st[n]); last = n; }
+        len = last;
+    }
+    // clamp to the frame plus a 4-unit margin
+    const int left = -(bx + bw4 + 4) * 4 * 8, right = (w4 - bx + 4) * 4 * 8;
+    const int top = -(by + bh4 + 4) * 4 * 8, bottom = (h4 - by + 4) * 4 * 8;
+    for (int n = 0; n < cnt; n++) {
+        st[n].mv.x = (int16_t)iclip(st[n].mv.x, left, right);
+        st[n].mv.y = (int16_t)iclip(st[n].mv.y, top, bottom);
+    }
+    for (int n = 0; n < 2; n++) stack[n] = n < cnt ? st[n].mv : Mv{ 0, 0 };
+}
+
+// read_mv_component_diff / read_mv_residual (decode.rs:224-311) without fractional bits
+int FrameDec::read_mv_comp(CdfMvComp &c) {
+    Msac &m = ts->msac;
+    const int sign = m.bool_adapt(c.sign);
+    const int cl = m.symbol(c.classes, 10);
+    int up;
+    if (!cl) {
+        up = m.bool_adapt(c.class0);
+    } else {
+        up = 1 << cl;
+        for (int n = 0; n < cl; n++) up |= m.bool_adapt(c.classN[n]) << n;
+    }
+    const int diff = ((up << 3) | (3 << 1) | 1) + 1;
+    return sign ? -diff : diff;
+}
+
+void FrameDec::read_mv_residual(Mv &mv, CdfMv &cdf) {
+    switch (ts->msac.symbol(ts->cdf.mv.joint, 3)) {   // the joint always comes from cdf.mv
+    case 3: mv.y = (int16_t)(mv.y + read_mv_comp(cdf.comp[0])); mv.x = (int16_t)(mv.x + read_mv_comp(cdf.comp[1])); break;
+    case 1: mv.x = (int16_t)(mv.x + read_mv_comp(cdf.comp[1])); break;
+    case 2: mv.y = (int16_t)(mv.y + read_mv_comp(cdf.comp[0])); break;
+    default: break;
+    }
+}
+
+// read_tx_tree (decode.rs:313-372): split flags of the var-tx tree, contexts a.tx / l.tx
+void FrameDec::read_tx_tree(int from, int depth, uint16_t *masks, int x_off, int y_off, int tbx, int tby) {
+    const TxDim &t = k_txdim[from];
+    const int txw = t.lw, txh = t.lh;
+    const int tby4 = tby & 31;
+    int is_split = 0;
+    if (depth < 2 && from > TX_4X4) {
+        const int cat = 2 * (TX_64X64 - t.max) - depth;
+        const int ac = a.tx[tbx] < txw, lc = l.tx[tby4] < txh;
+        is_split = ts->msac.bool_adapt(ts->cdf.m.txpart[cat][ac + lc]);
+        if (is_split) masks[depth] |= (uint16_t)(1 << (y_off * 4 + x_off));
+    }
+    if (is_split && t.max > TX_8X8) {
+        const int sub = t.sub;
+        const int sw = k_txdim[sub].w, sh = k_txdim[sub].h;
+        read_tx_tree(sub, depth + 1, masks, x_off * 2, y_off * 2, tbx, tby);
+        if (txw >= txh && tbx + sw < bw) read_tx_tree(sub, depth + 1, masks, x_off * 2 + 1, y_off * 2, tbx + sw, tby);
+        if (txh >= txw && tby + sh < bh) {
+            read_tx_tree(sub, depth + 1, masks, x_off * 2, y_off * 2 + 1, tbx, tby + sh);
+            if (txw >= txh && tbx + sw < bw)
+                read_tx_tree(sub, depth + 1, masks, x_off * 2 + 1, y_off * 2 + 1, tbx + sw, tby + sh);
+        }
+    } else {
+        setn(a.tx, tbx, t.w, is_split ? TX_4X4 : txw);
+        setn(l.tx, tby4, t.h, is_split ? TX_4X4 : txh);
+    }
+}
+
+// One MI_INTRA_IBC work item: the block copy of one transform-sized piece (plane pixels px, py)
+// and, unless the block is skipped, the residual read here (inter transform types)
+void FrameDec::push_ibc(const Block &b, Mv mv, int plane, int tx, int tbx, int tby, int px, int py, int read,
+                        uint8_t *actx, uint8_t *lctx, int nact, int nlct, int *txtp) {
+    const TxDim &t = k_txdim[tx];
+    const int sh = plane ? ss_hor : 0, sv = plane ? ss_ver : 0;
+    MiIntraBlock ib{};
+    ib.x = (uint16_t)px;
+    ib.y = (uint16_t)py;
+    ib.w = (uint8_t)(t.w * 4);
+    ib.h = (uint8_t)(t.h * 4);
+    ib.plane = (uint8_t)plane;
+    ib.mode = MI_INTRA_IBC;
+    ib.filt_idx = (uint8_t)(sh | (sv << 1));
+    ib.reserved = (uint32_t)(uint16_t)mv.x | ((uint32_t)(uint16_t)mv.y << 16);
+    ib.max_w = (uint16_t)((bw * 4) >> sh);
+    ib.max_h = (uint16_t)((bh * 4) >> sv);
+    ib.tile_w = (uint16_t)((ts->col_end >> sh) * 4);
+    ib.tile_h = (uint16_t)((ts->row_end >> sv) * 4);
+    // dependencies: the source rectangle (plus the second bilinear tap of a half-pel chroma
+    // phase), clamped to the reference area as mc() replicates its border
+    const int mx = (mv.x & (15 >> !sh)) << !sh, my = (mv.y & (15 >> !sv)) << !sv;
+    const int dx = px + (mv.x >> (3 + sh)), dy = py + (mv.y >> (3 + sv));
+    const int x0 = iclip(dx, 0, ib.max_w - 1), x1 = iclip(dx + ib.w + (mx != 0), 1, ib.max_w);
+    const int y0 = iclip(dy, 0, ib.max_h - 1), y1 = iclip(dy + ib.h + (my != 0), 1, ib.max_h);
+    std::vector<int32_t> deps;
+    add_deps(plane, x0, y0, imax(x1, x0 + 1), imax(y1, y0 + 1), deps);
+    const int k = (int)fw.intra.size();
+    fw.intra.push_back(ib);
+    fw.dep_start.push_back((int32_t)fw.deps.size());
+    for (int32_t d : deps) fw.deps.push_back(d);
+    MiTxBlock tb{};
+    tb.x = ib.x;
+    tb.y = ib.y;
+    tb.plane = (uint8_t)plane;
+    tb.tx = (uint8_t)tx;
+    tb.eob = -1;
+    if (read) {
+        int32_t cf[32 * 32];
+        memset(cf, 0, sizeof(cf));
+        uint8_t res;
+        const int eob = decode_coefs(actx, lctx, tx, b.bs, b, 0, plane, cf, txtp, &res);
+        memset(actx, res, nact);
+        memset(lctx, res, nlct);
+        tb.txtp = (uint8_t)*txtp;
+        tb.eob = eob;
+        if (eob >= 0) tb.coef_off = store_coefs(cf, tx);
+    }
+    fw.intra_tx.push_back(tb);
+    std::vector<int32_t> &o = owner[plane];
+    for (int yy = py >> 2; yy < (py + ib.h) >> 2; yy++)
+        for (int xx = px >> 2; xx < (px + ib.w) >> 2; xx++) {
+            const size_t q = (size_t)yy * owner_stride + xx;
+            if (xx < owner_stride && q < o.size()) o[q] = k;
+        }
+    (void)tbx; (void)tby;
+}
+
+// read_coef_tree (recon.rs:1597-1800) for a block copy: the leaves of the var-tx tree
+void FrameDec::ibc_residual_tree(const Block &b, Mv mv, int tx, int depth, const uint16_t *split, int x_off,
+                                 int y_off, int tbx, int tby, uint8_t (*txtp_map)[32]) {
+    const TxDim &t = k_txdim[tx];
+    if (depth < 2 && split[depth] && (split[depth] & (1 << (y_off * 4 + x_off)))) {
+        const int sub = t.sub, sw = k_txdim[sub].w, sh = k_txdim[sub].h;
+        ibc_residual_tree(b, mv, sub, depth + 1, split, x_off * 2, y_off * 2, tbx, tby, txtp_map);
+        if (t.w >= t.h && tbx + sw < bw)
+            ibc_residual_tree(b, mv, sub, depth + 1, split, x_off * 2 + 1, y_off * 2, tbx + sw, tby, txtp_map);
+        if (t.h >= t.w && tby + sh < bh) {
+            ibc_residual_tree(b, mv, sub, depth + 1, split, x_off * 2, y_off * 2 + 1, tbx, tby + sh, txtp_map);
+            if (t.w >= t.h && tbx + sw < bw)
+                ibc_residual_tree(b, mv, sub, depth + 1, split, x_off * 2 + 1, y_off * 2 + 1, tbx + sw, tby + sh, txtp_map);
+        }
+        return;
+    }
+    const int tby4 = tby & 31, tbx4 = tbx & 31;
+    int txtp = 0;
+    push_ibc(b, mv, 0, tx, tbx, tby, tbx * 4, tby * 4, 1, &a.lcoef[tbx], &l.lcoef[tby4], imin(t.w, bw - tbx),
+             imin(t.h, bh - tby), &txtp);
+    for (int y = 0; y < t.h && tby4 + y < 32; y++)
+        for (int x = 0; x < t.w && tbx4 + x < 32; x++) txtp_map[tby4 + y][tbx4 + x] = (uint8_t)txtp;
+}
+
+// decode.rs:1988-2135 (intra block copy) + rav1d_read_coef_blocks' inter walk (recon.rs:1803-2010)
+int FrameDec::decode_ibc(Block &b, int bs, int edge_flags, int has_chroma) {
+    const BlockDim &bd = k_bdim[bs];
+    const int bw4 = bd.w4, bh4 = bd.h4;
+    const int bx4 = bx & 31, by4 = by & 31;
+    // DV prediction and residual
+    Mv stack[2];
+    find_dv(bs, edge_flags, stack);
+    Mv mv;
+    if (!(stack[0] == Mv{ 0, 0 })) mv = stack[0];
+    else if (!(stack[1] == Mv{ 0, 0 })) mv = stack[1];
+    else if (by - (16 << s.sb128) < ts->row_start) mv = Mv{ 0, (int16_t)(-(512 << s.sb128) - 2048) };
+    else mv = Mv{ (int16_t)(-(512 << s.sb128)), 0 };
+    read_mv_residual(mv, ts->cdf.dmv);
+    // keep the source inside the decoded part of the tile, outside the current superblock
+    int border_left = ts->col_start * 4, border_top = ts->row_start * 4;
+    if (has_chroma) {
+        if (bw4 < 2 && ss_hor) border_left += 4;
+        if (bh4 < 2 && ss_ver) border_top += 4;
+    }
+    int src_left = bx * 4 + (mv.x >> 3), src_top = by * 4 + (mv.y >> 3);
+    int src_right = src_left + bw4 * 4, src_bottom = src_top + bh4 * 4;
+    const int border_right = ((ts->col_end + (bw4 - 1)) & ~(bw4 - 1)) * 4;
+    if (src_left < border_left) { src_right += border_left - src_left; src_left = border_left; }
+    else if (src_right > border_right) { src_left -= src_right - border_right; src_right = border_right; }
+    if (src_top < border_top) { src_bottom += border_top - src_top; src_top = border_top; }
+    const int sbx = (bx >> (4 + s.sb128)) << (6 + s.sb128), sby = (by >> (4 + s.sb128)) << (6 + s.sb128);
+    const int sb_size = 1 << (6 + s.sb128);
+    if (src_bottom > sby && src_right > sbx) {
+        if (src_top - border_top >= src_bottom - sby) { src_top -= src_bottom - sby; src_bottom = sby; }
+        else if (src_left - border_left >= src_right - sbx) { src_left -= src_right - sbx; src_right = sbx; }
+    }
+    if (src_bottom > sby + sb_size) { src_top -= src_bottom - (sby + sb_size); src_bottom = sby + sb_size; }
+    if (src_bottom > sby && src_right > sbx) return fail("intra block copy vector overlaps the current superblock");
+    mv.x = (int16_t)((src_left - bx * 4) * 8);
+    mv.y = (int16_t)((src_top - by * 4) * 8);
+
+    // var-tx tree (decode.rs read_vartx_tree:770-851)
+    uint16_t split[2] = { 0, 0 };
+    int max_ytx = k_max_tx_for_bs[bs][0];
+    if (!b.skip && (h.seg.lossless[b.seg_id] || max_ytx == TX_4X4)) {
+        b.uvtx = max_ytx = TX_4X4;
+        if (h.txfm_mode == TXMODE_SWITCHABLE) {
+            setn(a.tx, bx, bw4, TX_4X4);
+            setn(l.tx, by4, bh4, TX_4X4);
+        }
+    } else if (h.txfm_mode != TXMODE_SWITCHABLE || b.skip) {
+        if (h.txfm_mode == TXMODE_SWITCHABLE) {
+            setn(a.tx, bx, bw4, bd.lw4);
+            setn(l.tx, by4, bh4, bd.lh4);
+        }
+        b.uvtx = k_max_tx_for_bs[bs][layout];
+    } else {
+        const TxDim &yt = k_txdim[max_ytx];
+        for (int yo = 0; yo < bh4 / yt.h; yo++)
+            for (int xo = 0; xo < bw4 / yt.w; xo++)
+                read_tx_tree(max_ytx, 0, split, xo, yo, bx + xo * yt.w, by + yo * yt.h);
+        b.uvtx = k_max_tx_for_bs[bs][layout];
+    }
+
+    // prediction + residual work in the reference's coefficient order
+    const int w4b = imin(bw4, bw - bx), h4b = imin(bh4, bh - by);
+    const int cw4 = (w4b + ss_hor) >> ss_hor, ch4 = (h4b + ss_ver) >> ss_ver;
+    const int cbw4 = (bw4 + ss_hor) >> ss_hor, cbh4 = (bh4 + ss_ver) >> ss_ver;
+    const TxDim &ut = k_txdim[b.uvtx];
+    const TxDim &yt = k_txdim[max_ytx];
+    uint8_t txtp_map[32][32];
+    memset(txtp_map, 0, sizeof(txtp_map));
+    if (b.skip) {
+        for (int y = 0; y < h4b; y += yt.h)
+            for (int x = 0; x < w4b; x += yt.w)
+                push_ibc(b, mv, 0, max_ytx, bx + x, by + y, (bx + x) * 4, (by + y) * 4, 0, nullptr, nullptr, 0, 0, nullptr);
+        if (has_chroma)
+            for (int pl = 1; pl <= 2; pl++)
+                for (int y = 0; y < ch4; y += ut.h)
+                    for (int x = 0; x < cw4; x += ut.w)
+                        push_ibc(b, mv, pl, b.uvtx, bx, by, ((bx >> ss_hor) + x) * 4, ((by >> ss_ver) + y) * 4, 0,
+                                 nullptr, nullptr, 0, 0, nullptr);
+        setn(a.lcoef, bx, bw4, 0x40);
+        setn(l.lcoef, by4, bh4, 0x40);
+        if (has_chroma)
+            for (int pl = 0; pl < 2; pl++) {
+                setn(a.ccoef[pl], bx >> ss_hor, cbw4, 0x40);
+                setn(l.ccoef[pl], by4 >> ss_ver, cbh4, 0x40);
+            }
+    } else {
+        for (int init_y = 0; init_y < h4b; init_y += 16) {
+            const int sub_h4 = imin(h4b, 16 + init_y);
+            for (int init_x = 0; init_x < w4b; init_x += 16) {
+                const int sub_w4 = imin(w4b, init_x + 16);
+                int y_off = init_y != 0;
+                for (int y = init_y; y < sub_h4; y += yt.h, y_off++) {
+                    int x_off = init_x != 0;
+                    for (int x = init_x; x < sub_w4; x += yt.w, x_off++)
+                        ibc_residual_tree(b, mv, max_ytx, 0, split, x_off, y_off, bx + x, by + y, txtp_map);
+                }
+                if (!has_chroma) continue;
+                const int sub_ch4 = imin(ch4, (init_y + 16) >> ss_ver), sub_cw4 = imin(cw4, (init_x + 16) >> ss_hor);
+                for (int pl = 0; pl < 2; pl++)
+                    for (int y = init_y >> ss_ver; y < sub_ch4; y += ut.h)
+                        for (int x = init_x >> ss_hor; x < sub_cw4; x += ut.w) {
+                            int txtp = txtp_map[by4 + (y << ss_ver)][bx4 + (x << ss_hor)];
+                            const int tby = by + (y << ss_ver), tbx = bx + (x << ss_hor);
+                            const int cx = (bx >> ss_hor) + x;
+                            push_ibc(b, mv, 1 + pl, b.uvtx, tbx, tby, cx * 4, ((by >> ss_ver) + y) * 4, 1,
+                                     &a.ccoef[pl][cx], &l.ccoef[pl][(by4 >> ss_ver) + y],
+                                     imin(ut.w, (bw - tbx + ss_hor) >> ss_hor), imin(ut.h, (bh - tby + ss_ver) >> ss_ver),
+                                     &txtp);
+                        }
+            }
+        }
+    }
+    splat_rmv(bs, bw4, bh4, mv, true);
+    return 0;
+}
+
 static int neg_deinterleave(int diff, int ref, int max) {
     if (!ref) return diff;
     if (ref >= max - 1) return max - diff - 1;
@@ -1142,7 +1524,35 @@ int FrameDec::decode_b(int bl, int bs, int bp, int edge_flags) {
 
     if (h.allow_intrabc) {
         b.intra = !m.bool_adapt(ts->cdf.m.intrabc);
-        if (!b.intra) return fail("intra block copy is not supported by this front-end yet");
+        if (!b.intra) {
+            if (int e = decode_ibc(b, bs, edge_flags, has_chroma)) return e;
+            // contexts of a block copy (decode.rs:2104-2135)
+            setn(a.tx_intra, bx, bw4, bd.lw4);
+            setn(l.tx_intra, by4, bh4, bd.lh4);
+            setn(a.mode, bx, bw4, DC_PRED);
+            setn(l.mode, by4, bh4, DC_PRED);
+            setn(a.pal_sz, bx, bw4, 0);
+            setn(l.pal_sz, by4, bh4, 0);
+            for (int i = 0; i < bw4; i++) pal_sz_uv[0][bx4 + i] = 0;
+            for (int i = 0; i < bh4; i++) pal_sz_uv[1][by4 + i] = 0;
+            setn(a.seg_pred, bx, bw4, seg_pred);
+            setn(l.seg_pred, by4, bh4, seg_pred);
+            setn(a.skip_mode, bx, bw4, 0);
+            setn(l.skip_mode, by4, bh4, 0);
+            setn(a.intra, bx, bw4, 0);
+            setn(l.intra, by4, bh4, 0);
+            setn(a.skip, bx, bw4, b.skip);
+            setn(l.skip, by4, bh4, b.skip);
+            if (has_chroma) {
+                setn(a.uvmode, cbx, cbw4, DC_PRED);
+                setn(l.uvmode, cby4, cbh4, DC_PRED);
+            }
+            if (h.seg.enabled && h.seg.update_map)
+                for (int y = 0; y < bh4; y++)
+                    if (by + y < (int)(segmap.size() / b4_stride))
+                        memset(&segmap[(size_t)(by + y) * b4_stride + bx], b.seg_id, bw4);
+            return 0;
+        }
     } else {
         b.intra = 1;
     }
@@ -1262,6 +1672,7 @@ int FrameDec::decode_b(int bl, int bs, int bp, int edge_flags) {
         for (int y = 0; y < bh4; y++)
             if (by + y < (int)(segmap.size() / b4_stride))
                 memset(&segmap[(size_t)(by + y) * b4_stride + bx], b.seg_id, bw4);
+    if (h.allow_intrabc) splat_rmv(bs, bw4, bh4, Mv{ 0, 0 }, false);
     if (!b.skip) {
         uint16_t (*ns)[2] = &lf_mask->noskip_mask[by4 >> 1];
         const unsigned mask = (~0u >> (32 - bw4)) << (bx4 & 15);
@@ -1686,6 +2097,14 @@ int FrameDec::run(FrameResult &res, std::string &err) {
     a_tx_lpf_end[1].resize(h.tiling.rows);
     owner_stride = (b4_stride + 32);
     for (int p = 0; p < 3; p++) owner[p].assign((size_t)owner_stride * (sb128h * 32 + 32), -1);
+    if (h.allow_intrabc) {
+        RefMvBlock none{};
+        none.mv[0] = kInvalidMv;
+        none.ref[0] = -1;
+        none.ref[1] = -1;
+        rmv_stride = b4_stride + 16;
+        rmv.assign((size_t)rmv_stride * (sb128h * 32 + 16), none);
+    }
     a.alloc(b4_stride + 64);
     l.alloc(64);
     memset(al_pal, 0, sizeof(al_pal));

@@ -30,7 +30,7 @@ class DevicePictureSet:
 def run_frame(ctx, fr, stream=None):
     """Enqueue one MiDecFrame on the device; returns its DevicePictureSet (output() = the
     reference-quality picture once the stream reaches it)."""
-    ps = DevicePictureSet(fr.w, fr.h, fr.bpc, fr.layout)
+    ps = DevicePictureSet(fr.up_w, fr.h, fr.bpc, fr.layout)   # upscaled geometry with super-resolution
     final = ctypes.c_int(-1)
     check(lib().mi_frame_run(ctx.h, ctypes.byref(fr), ctypes.byref(ps.pics), ctypes.byref(final),
                              F._stream_ptr(stream)), "mi_frame_run")

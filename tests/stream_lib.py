@@ -47,7 +47,8 @@ def md5_update_picture(md5, planes, w, h, layout):
 def oracle_frame(fr):
     """Reconstruct one MiDecFrame through the oracle; returns the final planes (1 or 3)."""
     o = _bind(oracle_lib.load_oracle())
-    pics = [alloc_picture(fr.w, fr.h, fr.bpc, fr.layout) for _ in range(3)]
+    # super-resolution: every picture has the upscaled geometry (the coded width is a prefix)
+    pics = [alloc_picture(fr.up_w, fr.h, fr.bpc, fr.layout) for _ in range(3)]
     for p in pics:
         while len(p) < 3:
             p.append(p[0])
@@ -74,9 +75,7 @@ def decode_stream(data, recon=oracle_frame, max_frames=None):
         for ev in dec.events():
             if ev.frame:
                 fr = ev.frame.contents
-                if fr.up_w != fr.w:
-                    raise NotImplementedError("super-resolution stream")
-                pics[ev.pic_id] = (recon(fr), fr.w, fr.h, fr.layout, fr.bpc)
+                pics[ev.pic_id] = (recon(fr), fr.up_w, fr.h, fr.layout, fr.bpc)
             if ev.show_pic >= 0:
                 planes, w, h, layout, bpc = pics[ev.show_pic]
                 md5_update_picture(md5, planes, w, h, layout)

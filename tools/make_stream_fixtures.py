@@ -21,6 +21,7 @@ PINNED = [
     ("itut_t35", "8-bit/features/itut_t35.ivf"),
     ("long_leb", "8-bit/features/long_leb.ivf"),
     ("00000791", "12-bit/data/00000791.ivf"),
+    ("itut_t35", "10-bit/features/itut_t35.ivf", "itut_t35_10bit"),   # 4K 10-bit, intra block copy
 ]
 
 if __name__ == "__main__":
@@ -28,9 +29,10 @@ if __name__ == "__main__":
     os.makedirs(out, exist_ok=True)
     by_path = {os.path.relpath(p, "/root/reference/tests/dav1d-test-data"): (n, m) for n, p, m in vectors()}
     table = []
-    for name, rel in PINNED:
+    for name, rel, *alias in PINNED:
         n, md5 = by_path[rel]
         assert n == name, (n, name)
+        name = alias[0] if alias else name
         dst = rel.replace("/", "__")
         shutil.copyfile(os.path.join("/root/reference/tests/dav1d-test-data", rel), os.path.join(out, dst))
         table.append({"name": name, "file": dst, "md5": md5, "source": f"tests/dav1d-test-data/{rel}"})
