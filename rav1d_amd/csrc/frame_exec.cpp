@@ -107,7 +107,6 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
         return -EINVAL;
     if (f->cdef_on && (!f->lf_masks || f->sb128w != sb128w || f->sb128h != sb128h)) return -EINVAL;
     if (f->restore_planes && (!f->lr_mask || f->lr_sb128w != ((f->up_w + 127) >> 7))) return -EINVAL;
-    if (f->up_w != f->w) return -EINVAL;   // super-resolution: not wired into the executor yet
     if (f->n_inter_tx) return -EINVAL;     // inter frames: not produced by the front-end yet
     return 0;
 }

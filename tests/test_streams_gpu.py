@@ -125,3 +125,65 @@ def test_unsatisfiable_dependency_reports_eio(gpu):
     assert L.mi_intra_recon(gpu.h, ctypes.byref(d), 1, 0, None) == 0
     assert L.mi_frame_end(gpu.h, None) == -5   # -EIO
     assert L.mi_frame_end(gpu.h, None) == 0    # reported once
+
+
+def _superres_frames(name, n_frames, up_num, up_den, keep_lr):
+    """Front-end frames of an intra vector turned into super-resolution frames: the coded
+    width stays, up_w = w * up_num / up_den (a width the frame header could carry, denominator
+    9..16 over 8), and the loop-restoration units are re-laid over the upscaled width (unit x
+    clamped into the coded frame's units) or switched off. Yields (frame, keepalive)."""
+    import ctypes
+
+    from rav1d_amd.av1dec import Av1Decoder, MiDecFrame, ivf_frames
+    v = next(x for x in VECTORS if x["name"] == name)
+    dec = Av1Decoder()
+    got = 0
+    for tu in ivf_frames(open(os.path.join(GOLDEN, v["file"]), "rb").read()):
+        dec.send(tu)
+        for ev in dec.events():
+            if not ev.frame or got >= n_frames:
+                continue
+            src = ev.frame.contents
+            fr = MiDecFrame.from_buffer_copy(src)
+            fr.up_w = src.w * up_num // up_den
+            keep = []
+            if keep_lr and src.restore_planes:
+                old = np.frombuffer((ctypes.c_uint8 * (108 * src.sb128h * src.lr_sb128w)).from_address(src.lr_mask),
+                                    np.uint8).reshape(src.sb128h, src.lr_sb128w, 108)
+                nw = (fr.up_w + 127) >> 7
+                cols = np.minimum(np.arange(nw) * src.lr_sb128w // nw, src.lr_sb128w - 1)
+                new = np.ascontiguousarray(old[:, cols])
+                keep.append(new)
+                fr.lr_mask, fr.lr_sb128w = new.ctypes.data, nw
+            else:
+                fr.restore_planes = 0
+            got += 1
+            yield fr, (keep, ev)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("keep_lr", [False, True])
+def test_superres_frames_match_oracle(gpu, keep_lr):
+    """Super-resolution through the frame executor (CDEF output upscaled by mi_superres_frame,
+    then LR over the upscaled width reading the upscaled deblocked picture, recon.rs:4211-4283)
+    equals the oracle's frame driver on the same work lists. No intra-only reference vector
+    uses super-resolution, so the frames are the allintra vector's with a widened up_w: parity
+    unpinned by reference outputs, pinned to the oracle (whose resize step follows
+    decode.rs:4640-4660 / mc.rs resize)."""
+    import torch
+
+    from rav1d_amd.stream import run_frame
+    from tests.stream_lib import oracle_frame
+    for fr, _keep in _superres_frames("av1-1-b8-02-allintra", 3, 3, 2, keep_lr):
+        ps = run_frame(gpu, fr)
+        torch.cuda.synchronize()
+        from rav1d_amd.stream import frame_end
+        frame_end(gpu)
+        want = oracle_frame(fr)
+        out = ps.output()
+        ss_h, ss_v = int(fr.layout in (1, 2)), int(fr.layout == 1)
+        for p in range(len(want)):
+            h = fr.h if p == 0 else (fr.h + ss_v) >> ss_v
+            w = fr.up_w if p == 0 else (fr.up_w + ss_h) >> ss_h
+            got = out.buffer_np(p)[:h, :w]
+            assert np.array_equal(got, want[p][:h, :w]), f"plane {p} keep_lr={keep_lr}"
