@@ -86,8 +86,9 @@ class Pipeline:
         self.kernels = {"mc": "mc_kernel", "itx": "itx_frame_kernel", "deblock": "lf_tile_kernel",
                         "cdef": "cdef_kernel", "lr": "lr_kernel", "fg": "fg_apply_kernel"}
 
-    def step(self, stream, ev=None):
-        """Enqueue one frame. ev: optional dict stage -> list of (start, end) events."""
+    def step(self, stream, ev=None, mark=None):
+        """Enqueue one frame. ev: optional dict stage -> list of (start, end) events; mark:
+        optional event recorded on `stream` once the frame's motion compensation is done."""
         lib = F.lib()
         ctx = self.ctx.h
         sp = F._stream_ptr(stream)
@@ -118,6 +119,8 @@ class Pipeline:
             timed("mc", lambda: F.check(lib.mi_mc_frame(ctx, ctypes.byref(pa), self.ref_pics, len(self.refs),
                                                         ctypes.c_void_p(self.mc.blocks.data_ptr()), self.mc.class_start,
                                                         ctypes.c_void_p(self.mc.masks.data_ptr()), None, sp), "mc"))
+        if mark is not None:
+            mark.record(stream)
         ss = (ctypes.c_uint32 * 20)(*[int(v) for v in self.fr["size_start"]])
         timed("itx", lambda: F.check(lib.mi_itx_frame(ctx, ctypes.byref(pa), ctypes.c_void_p(self.blocks.data_ptr()),
                                                       ss, ctypes.c_void_p(self.coef.data_ptr()), 0, sp), "itx"))
@@ -302,7 +305,7 @@ def real_streams(ctx, reps=3):
     gold = os.path.join(ROOT, "tests", "golden", "streams")
     vecs = {v["name"]: v for v in json.load(open(os.path.join(gold, "vectors.json")))}
     out = {}
-    for name in ("itut_t35", "av1-1-b8-02-allintra"):
+    for name in ("itut_t35", "av1-1-b8-02-allintra", "itut_t35_10bit"):
         v = vecs[name]
         data = open(os.path.join(gold, v["file"]), "rb").read()
         m = Muxer("md5")
@@ -335,8 +338,9 @@ def real_streams(ctx, reps=3):
             for ev in dec.events():
                 if ev.frame:
                     fr = (ev.frame.contents.w, ev.frame.contents.h)
+                    bits = ev.frame.contents.bpc
         px = n * fr[0] * fr[1]
-        out[name] = dict(frames=n, size=f"{fr[0]}x{fr[1]} 8-bit 4:2:0", md5_verified=ok,
+        out[name] = dict(frames=n, size=f"{fr[0]}x{fr[1]} {bits}-bit 4:2:0", md5_verified=ok,
                          gpu_end_to_end_ms=round(best * 1e3, 3), gpu_fps=round(n / best, 1),
                          gpu_mpx_per_s=round(px / best / 1e6, 2), front_end_ms=round(fe * 1e3, 3),
                          cpu_oracle_ms=round(cpu * 1e3, 1), cpu_oracle_mpx_per_s=round(px / cpu / 1e6, 2),
@@ -514,6 +518,10 @@ def main():
     ap.add_argument("--single-stream", type=int, default=0, metavar="FRAMES",
                     help="instead of replicas: one 4K10 stream of FRAMES frames (hierarchical GOP of 8), frame k "
                          "reconstructed on rank k %% N, references exchanged point to point (rav1d_amd.sstream)")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="frames reconstructed concurrently per GPU, each on its own HIP stream and context "
+                         "(rav1d's frame threads, n_fc): a step is then that many frames")
+    ap.add_argument("--stagger", type=int, default=0, help="with --inflight > 1: frame k's MC waits for frame k-1's")
     ap.add_argument("--mv", choices=["uniform", "coherent"], default="uniform",
                     help="motion field of the timed frame (uniform: SURVEY.md 8(d) config 3)")
     args = ap.parse_args()
@@ -548,7 +556,33 @@ def main():
     torch.cuda.synchronize()
     stage_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
 
-    elapsed = timed_region(lambda: pipe.step(stream), args.steps, torch.cuda.synchronize, world, "cuda")
+    # frames in flight: independent frames on their own streams (and contexts: a context's
+    # scratch belongs to one stream), the first on the default stream. The headline runs
+    # --inflight frames per step (default 1: every launch has the GPU to itself, so the event
+    # durations above are the kernels' own); with the extras, two frames in flight (rav1d's
+    # frame threads) are measured beside it.
+    n_pipes = max(args.inflight, 1 if args.no_extra else 2)
+    pipes = [(pipe, stream)]
+    for _ in range(n_pipes - 1):
+        pk = Pipeline(F.Context(local), fr)
+        pipes.append((pk, torch.cuda.Stream()))
+    for pk, sk in pipes[1:]:
+        for _ in range(args.warmup):
+            pk.step(sk)
+    torch.cuda.synchronize()
+    marks = [torch.cuda.Event() for _ in pipes]
+
+    def step_k(k):
+        def run():
+            # staggered: frame i starts its motion compensation once frame i-1's is done
+            for i, (pk, sk) in enumerate(pipes[:k]):
+                if args.stagger and i:
+                    sk.wait_event(marks[i - 1])
+                pk.step(sk, mark=marks[i] if args.stagger else None)
+        return run
+    elapsed = timed_region(step_k(args.inflight), args.steps, torch.cuda.synchronize, world, "cuda")
+    elapsed2 = timed_region(step_k(2), args.steps, torch.cuda.synchronize, world, "cuda") \
+        if args.inflight == 1 and n_pipes >= 2 else None
 
     # per-rank correctness: one more step from the initial inputs, digest of the output
     # picture, checked against the oracle on this rank's host cores (outside the timed region)
@@ -557,12 +591,19 @@ def main():
     torch.cuda.synchronize()
     digest = pipe.output_digest()
     verified = digest == oracle_digest(fr) if not args.no_verify else None
-    ranks = gather_results({"rank": rank, "frames": args.steps, "ns": int(elapsed * 1e9),
+    # the other in-flight frames (own buffers, streams and contexts) produce the same picture
+    for pk, sk in pipes[1:]:
+        pk.restore()
+        pk.step(sk)
+        torch.cuda.synchronize()
+        if verified is not None:
+            verified = verified and pk.output_digest() == digest
+    ranks = gather_results({"rank": rank, "frames": args.steps * args.inflight, "ns": int(elapsed * 1e9),
                             "sha256": digest, "verified": verified}, world)
 
     dom = max(stage_ms, key=stage_ms.get)
     achieved = pipe.algo[dom] / (stage_ms[dom] / 1e3) / 1e9
-    frames = args.steps * world
+    frames = args.steps * world * args.inflight
     value = frames * W * H / elapsed / 1e6
     if rank == 0:
         out = {
@@ -574,6 +615,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "fps": round(frames / elapsed, 2),
+            "frames_in_flight": args.inflight,
+            "two_frames_in_flight": None if elapsed2 is None else {
+                "value": round(2 * args.steps * world * W * H / elapsed2 / 1e6, 2),
+                "ms_per_step": round(elapsed2 / args.steps * 1e3, 4),
+                "note": "two independent frames per step on two HIP streams / contexts (frame threading); "
+                        "outputs verified identical"},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
