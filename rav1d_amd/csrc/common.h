@@ -227,6 +227,7 @@ struct IntraReconArgs {
     int *desc_err;                // rejected descriptors (skipped; reported as -EINVAL)
     uint32_t epoch;
     int nframes, zero_coefs;
+    int spread;                   // fewer frames than XCDs: XCD x works on frame x % nframes
 };
 static_assert(sizeof(IntraReconArgs) <= 4096, "kernel argument limit");
 int launch_intra_recon(const IntraReconArgs &a, int bpc, int wg_per_xcd, hipStream_t s);

@@ -566,8 +566,9 @@ __global__ __launch_bounds__(64) void intra_kernel(IpredArgs a) {
 //
 // One launch reconstructs whole intra frames: prediction (intra_block) and the residual
 // (inverse transform + add) of every transform block, in dependency order, without a launch
-// per wavefront step. Frame f is worked on only by the workgroups the dispatcher placed on
-// XCD f (HW_REG_XCC_ID), for L2 locality only: correctness does not depend on it. A block's
+// per wavefront step. Frame f is worked on by the workgroups the dispatcher placed on XCD f
+// (HW_REG_XCC_ID), and with fewer than 8 frames XCD x joins frame x % nframes; the placement
+// is for L2 locality only: correctness does not depend on it. A block's
 // pixels are published with the hand-off of MI355X_MICROARCH.md's table row 1: 4-/8-B `sc1`
 // stores, the storing wave's vmcnt(0), then one lane's `sc1` done-flag store; readers poll the
 // flag and read pixels with 4-B `sc1` loads only. Each worker wave
@@ -694,12 +695,20 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
 #else
 #define DBG(i, v) do {} while (0)
 #endif
-    // frames xcc, xcc + 8, ... belong to this XCD; its workers are dealt over them round robin
-    const int nper = (a.nframes - (int)xcc + 7) >> 3;
-    if (nper <= 0) return;
+    // frames xcc, xcc + 8, ... belong to this XCD; its workers are dealt over them round robin.
+    // With fewer frames than XCDs (spread), XCD x helps frame x % nframes: the hand-off below is
+    // valid across XCDs, placement only buys L2 locality.
     const int lane = threadIdx.x;
-    const int rank = __builtin_amdgcn_readfirstlane(atomicAdd(a.xcd_rank + xcc, lane == 0 ? 1 : 0));
-    const IntraReconFrame &fr = a.fr[xcc + 8 * (rank % nper)];
+    int fidx;
+    if (a.spread) {
+        fidx = (int)xcc % a.nframes;
+    } else {
+        const int nper = (a.nframes - (int)xcc + 7) >> 3;
+        if (nper <= 0) return;
+        const int rank = __builtin_amdgcn_readfirstlane(atomicAdd(a.xcd_rank + xcc, lane == 0 ? 1 : 0));
+        fidx = xcc + 8 * (rank % nper);
+    }
+    const IntraReconFrame &fr = a.fr[fidx];
     for (;;) {
         // The block index must be provably wave-uniform and the loop free of lane-divergent
         // branches: otherwise the structurizer may run lanes 1..63 into the next iteration

@@ -69,7 +69,6 @@ int Bits::subexp(int ref, int n) {
 }
 
 // ---------------------------------------------------------------------- msac
-static constexpr int kWin = 64;
 
 void Msac::init(const uint8_t *data, size_t sz, bool disable_update) {
     pos = data;
@@ -90,75 +89,6 @@ void Msac::refill() {
     }
     dif = d;
     cnt = kWin - c - 24;
-}
-
-void Msac::norm(uint64_t d, unsigned r) {
-    const int s = 15 ^ (31 ^ __builtin_clz(r));
-    cnt -= s;
-    dif = ((d + 1) << s) - 1;   // ones shifted into the low bits
-    rng = r << s;
-    if (cnt < 0) refill();
-}
-
-unsigned Msac::bool_equi() {
-    unsigned v = ((rng >> 8) << 7) + 4;
-    const uint64_t vw = (uint64_t)v << (kWin - 16);
-    const unsigned ret = dif >= vw;
-    uint64_t d = dif - ret * vw;
-    v += ret * (rng - 2 * v);
-    norm(d, v);
-    return !ret;
-}
-
-unsigned Msac::bool_prob(unsigned f) {
-    unsigned v = ((rng >> 8) * (f >> 6) >> 1) + 4;
-    const uint64_t vw = (uint64_t)v << (kWin - 16);
-    const unsigned ret = dif >= vw;
-    uint64_t d = dif - ret * vw;
-    v += ret * (rng - 2 * v);
-    norm(d, v);
-    return !ret;
-}
-
-unsigned Msac::symbol(uint16_t *cdf, unsigned n) {
-    const unsigned c = (unsigned)(dif >> (kWin - 16)), r = rng >> 8;
-    unsigned u, v = rng, val = (unsigned)-1;
-    do {
-        val++;
-        u = v;
-        v = (r * (cdf[val] >> 6) >> 1) + 4 * (n - val);
-    } while (c < v);
-    norm(dif - ((uint64_t)v << (kWin - 16)), u - v);
-    if (adapt) {
-        const unsigned count = cdf[n];
-        const unsigned rate = 4 + (count >> 4) + (n > 2);
-        unsigned i = 0;
-        for (; i < val; i++) cdf[i] += (32768 - cdf[i]) >> rate;
-        for (; i < n; i++) cdf[i] -= cdf[i] >> rate;
-        cdf[n] = count + (count < 32);
-    }
-    return val;
-}
-
-unsigned Msac::bool_adapt(uint16_t *cdf) {
-    const unsigned b = bool_prob(cdf[0]);
-    if (adapt) {
-        const unsigned count = cdf[1];
-        const int rate = 4 + (count >> 4);
-        if (b) cdf[0] += (32768 - cdf[0]) >> rate;
-        else cdf[0] -= cdf[0] >> rate;
-        cdf[1] = count + (count < 32);
-    }
-    return b;
-}
-
-unsigned Msac::hi_tok(uint16_t *cdf) {
-    unsigned tok = 3, br;
-    do {
-        br = symbol(cdf, 3);
-        tok += br;
-    } while (br == 3 && tok < 15);
-    return tok;
 }
 
 int Msac::uniform(unsigned n) {
