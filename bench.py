@@ -521,6 +521,8 @@ def main():
     ap.add_argument("--inflight", type=int, default=1,
                     help="frames reconstructed concurrently per GPU, each on its own HIP stream and context "
                          "(rav1d's frame threads, n_fc): a step is then that many frames")
+    ap.add_argument("--two-in-flight", action="store_true",
+                    help="also time two independent frames per step on two streams (two_frames_in_flight)")
     ap.add_argument("--stagger", type=int, default=0, help="with --inflight > 1: frame k's MC waits for frame k-1's")
     ap.add_argument("--mv", choices=["uniform", "coherent"], default="uniform",
                     help="motion field of the timed frame (uniform: SURVEY.md 8(d) config 3)")
@@ -559,9 +561,10 @@ def main():
     # frames in flight: independent frames on their own streams (and contexts: a context's
     # scratch belongs to one stream), the first on the default stream. The headline runs
     # --inflight frames per step (default 1: every launch has the GPU to itself, so the event
-    # durations above are the kernels' own); with the extras, two frames in flight (rav1d's
-    # frame threads) are measured beside it.
-    n_pipes = max(args.inflight, 1 if args.no_extra else 2)
+    # durations above are the kernels' own); with --two-in-flight, two frames in flight (rav1d's
+    # frame threads) are measured beside it (not in the default run: its concurrent launches
+    # would mix into a profiler's per-kernel averages of this command).
+    n_pipes = max(args.inflight, 2 if args.two_in_flight else 1)
     pipes = [(pipe, stream)]
     for _ in range(n_pipes - 1):
         pk = Pipeline(F.Context(local), fr)
