@@ -61,35 +61,61 @@ def decode_ivf(ctx, data, stream=None, sync_each=True):
     frame_end(ctx, stream)
 
 
-def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True):
+def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=True):
     """Decode an IVF stream on the device and write every shown picture through `muxer`
     (rav1d_amd.output.Muxer): the picture leaves HBM once, via mi_output_picture into pinned
     host memory, with film grain applied in that same pass when the frame carries grain and
-    apply_grain is set (Dav1dSettings.apply_grain, src/lib.rs). Returns the pictures written."""
+    apply_grain is set (Dav1dSettings.apply_grain, src/lib.rs). Returns the pictures written.
+
+    pipelined: the host front-end parses temporal unit t + 1 while the device reconstructs
+    frame t (rav1d overlaps its entropy pass with reconstruction the same way with frame
+    threads, src/thread_task.rs): a shown picture is handed to the muxer once its output copy
+    (an event, not a stream sync) has landed, one picture behind; two host pictures alternate.
+    Device failures of any frame are reported by the mi_frame_end at the end of the stream.
+    Without it every frame is checked by mi_frame_end before it is shown."""
     from .output import HostPicture, output_picture
     import torch
     dec = Av1Decoder()
-    pics, host, n = {}, None, 0
+    pics, n = {}, 0
+    hosts = [None, None]
+    pending = None                      # (slot, event) of the picture awaiting the muxer
+
+    def flush():
+        nonlocal pending, n
+        if pending is None:
+            return
+        slot, ev = pending
+        ev.synchronize()
+        muxer.write(hosts[slot].pic)
+        n += 1
+        pending = None
+
+    slot = 0
     for tu in ivf_frames(data):
         dec.send(tu)
         for ev in dec.events():
             if ev.frame:
                 pics[ev.pic_id] = run_frame(ctx, ev.frame.contents, stream)
-                frame_end(ctx, stream)
+                if not pipelined:
+                    frame_end(ctx, stream)
             if ev.show_pic >= 0:
                 out = pics[ev.show_pic].output()
-                if host is None or (host.pic.w, host.pic.h, host.pic.bpc, host.pic.layout) != \
-                        (out.w, out.h, out.bpc, out.layout):
-                    host = HostPicture(out.w, out.h, out.bpc, out.layout)
+                h = hosts[slot]
+                if h is None or (h.pic.w, h.pic.h, h.pic.bpc, h.pic.layout) != (out.w, out.h, out.bpc, out.layout):
+                    if pending is not None and pending[0] == slot:
+                        flush()
+                    hosts[slot] = h = HostPicture(out.w, out.h, out.bpc, out.layout)
                 fg = ev.fg if (ev.fg_present and apply_grain) else None
-                output_picture(ctx, out, host, fg, 0, stream)
-                if stream is not None:
-                    stream.synchronize()
-                else:
-                    torch.cuda.synchronize()
-                muxer.write(host.pic)
-                n += 1
+                output_picture(ctx, out, h, fg, 0, stream)
+                done = torch.cuda.Event()
+                done.record(stream if stream is not None else torch.cuda.current_stream())
+                flush()                  # the previous picture, while this one is on the device
+                pending = (slot, done)
+                if not pipelined:
+                    flush()
+                slot ^= 1
             for i in range(ev.n_release):
                 pics.pop(ev.release[i], None)
+    flush()
     frame_end(ctx, stream)
     return n

@@ -81,3 +81,15 @@ def test_stream_to_md5_muxer_matches_reference(gpu, v):
     assert n > 0
     assert m.verify(v["md5"]) == 0, f"{v['name']}: {m.digest()} != {v['md5']}"
     m.close()
+
+
+def test_stream_to_md5_muxer_unpipelined_matches_reference(gpu):
+    """The same chain with every frame checked by mi_frame_end before it is shown (no overlap of
+    the front-end with the device)."""
+    from rav1d_amd.stream import decode_to_muxer
+    v = next(x for x in VECTORS if x["name"] == "av1-1-b8-02-allintra")
+    data = open(os.path.join(GOLDEN, v["file"]), "rb").read()
+    m = Muxer("md5")
+    assert decode_to_muxer(gpu, data, m, pipelined=False) == 39
+    assert m.verify(v["md5"]) == 0
+    m.close()
