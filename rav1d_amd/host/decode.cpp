@@ -133,6 +133,7 @@ private:
     // inter-style residual walk that emits MI_INTRA_IBC work
     std::vector<RefMvBlock> rmv;
     int rmv_stride = 0;
+    std::vector<int32_t> dep_tmp;     // one block's dependency list (reused)
     RefMvBlock &rmv_at(int y4, int x4) { return rmv[(size_t)(y4 + 8) * rmv_stride + (x4 + 8)]; }
     void splat_rmv(int bs, int bw4, int bh4, Mv mv, bool valid);
     void find_dv(int bs, int edge_flags, Mv stack[2]);
@@ -848,7 +849,8 @@ void FrameDec::emit_intra(const Block &b, int edge_flags, const uint8_t *pal_idx
         (void)intra_tx_eob_plane_bs;
         // dependencies: every already reconstructed pixel the prediction may read
         const int k = (int)fw.intra.size();
-        std::vector<int32_t> deps;
+        std::vector<int32_t> &deps = dep_tmp;
+        deps.clear();
         const int x = ib.x, y = ib.y, w = ib.w, hh = ib.h;
         const int tile_w = ib.tile_w, tile_h = ib.tile_h;
         if (ib.mode == MI_IPRED_PAL) {
@@ -875,7 +877,8 @@ void FrameDec::emit_intra(const Block &b, int edge_flags, const uint8_t *pal_idx
         if (!skip) {
             int txtp = 0;
             uint8_t res;
-            memset(cf, 0, sizeof(cf));
+            // decode_coefs writes scan positions of the transform's coded area only
+            memset(cf, 0, sizeof(int32_t) * imin(k_txdim[txs].w * 4, 32) * imin(k_txdim[txs].h * 4, 32));
             const int eob = decode_coefs(actx, lctx, txs, b.bs, b, 1, plane, cf, &txtp, &res);
             memset(actx, res, nact);
             memset(lctx, res, nlct);
@@ -1209,7 +1212,8 @@ void FrameDec::push_ibc(const Block &b, Mv mv, int plane, int tx, int tbx, int t
     const int dx = px + (mv.x >> (3 + sh)), dy = py + (mv.y >> (3 + sv));
     const int x0 = iclip(dx, 0, ib.max_w - 1), x1 = iclip(dx + ib.w + (mx != 0), 1, ib.max_w);
     const int y0 = iclip(dy, 0, ib.max_h - 1), y1 = iclip(dy + ib.h + (my != 0), 1, ib.max_h);
-    std::vector<int32_t> deps;
+    std::vector<int32_t> &deps = dep_tmp;
+    deps.clear();
     add_deps(plane, x0, y0, imax(x1, x0 + 1), imax(y1, y0 + 1), deps);
     const int k = (int)fw.intra.size();
     fw.intra.push_back(ib);
@@ -1223,7 +1227,7 @@ void FrameDec::push_ibc(const Block &b, Mv mv, int plane, int tx, int tbx, int t
     tb.eob = -1;
     if (read) {
         int32_t cf[32 * 32];
-        memset(cf, 0, sizeof(cf));
+        memset(cf, 0, sizeof(int32_t) * imin(t.w * 4, 32) * imin(t.h * 4, 32));
         uint8_t res;
         const int eob = decode_coefs(actx, lctx, tx, b.bs, b, 0, plane, cf, txtp, &res);
         memset(actx, res, nact);
