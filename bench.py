@@ -529,6 +529,7 @@ def main():
     ap.add_argument("--inflight", type=int, default=1,
                     help="frames reconstructed concurrently per GPU, each on its own HIP stream and context "
                          "(rav1d's frame threads, n_fc): a step is then that many frames")
+    ap.add_argument("--graph", type=int, default=0, help="1: replay the step as one captured HIP graph")
     ap.add_argument("--two-in-flight", action="store_true",
                     help="also time two independent frames per step on two streams (two_frames_in_flight)")
     ap.add_argument("--stagger", type=int, default=0, help="with --inflight > 1: frame k's MC waits for frame k-1's")
@@ -591,7 +592,21 @@ def main():
                     sk.wait_event(marks[i - 1])
                 pk.step(sk, mark=marks[i] if args.stagger else None)
         return run
-    elapsed = timed_region(step_k(args.inflight), args.steps, torch.cuda.synchronize, world, "cuda")
+    step_fn = step_k(args.inflight)
+    if args.graph:
+        # the step's launches captured once into a HIP graph (the C-ABI calls only enqueue
+        # kernels on the stream they are given), replayed per step
+        graph, cap = torch.cuda.CUDAGraph(), torch.cuda.Stream()
+        cap.wait_stream(stream)
+        with torch.cuda.graph(graph, stream=cap):
+            for pk, _ in pipes[:args.inflight]:
+                pk.step(cap)
+        torch.cuda.synchronize()
+        step_fn = graph.replay
+        for _ in range(args.warmup):
+            step_fn()
+        torch.cuda.synchronize()
+    elapsed = timed_region(step_fn, args.steps, torch.cuda.synchronize, world, "cuda")
     elapsed2 = timed_region(step_k(2), args.steps, torch.cuda.synchronize, world, "cuda") \
         if args.inflight == 1 and n_pipes >= 2 else None
 
