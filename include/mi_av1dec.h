@@ -112,6 +112,12 @@ typedef struct MiDec MiDec;
 
 int  mi_dec_create(MiDec **out);
 void mi_dec_destroy(MiDec *d);
+/* Frame threads (rav1d's Dav1dSettings.n_frame_threads, src/lib.rs): with n > 1, intra frames
+ * are entropy-decoded on up to n worker threads while mi_dec_send parses on; mi_dec_next
+ * still returns events in decode order and waits for the oldest frame's worker, so a caller
+ * that wants the overlap sends a few temporal units ahead before draining. A worker's failure
+ * is returned by the mi_dec_next of its frame. Default 1 (synchronous). 0 or -EINVAL. */
+int  mi_dec_set_threads(MiDec *d, int n);
 /* Feed one temporal unit (any whole number of OBUs). */
 int  mi_dec_send(MiDec *d, const uint8_t *data, size_t size);
 /* Next event: 1 and *ev filled, 0 when none is pending, or -errno. */

@@ -56,6 +56,7 @@ def dec_lib():
         d.mi_dec_destroy.restype = None
         d.mi_dec_send.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
         d.mi_dec_next.argtypes = [ctypes.c_void_p, ctypes.POINTER(MiDecEvent)]
+        d.mi_dec_set_threads.argtypes = [ctypes.c_void_p, ctypes.c_int]
         d.mi_dec_error.argtypes = [ctypes.c_void_p]
         d.mi_dec_error.restype = ctypes.c_char_p
         _dec = d
@@ -82,12 +83,16 @@ def ivf_frames(path_or_bytes):
 class Av1Decoder:
     """One stream. send() one temporal unit, then drain events()."""
 
-    def __init__(self):
+    def __init__(self, threads=1):
+        """threads > 1: intra frames are decoded on that many worker threads (mi_dec_set_threads);
+        send a few temporal units ahead of draining events() to overlap them."""
         self.lib = dec_lib()
         self.h = ctypes.c_void_p()
         r = self.lib.mi_dec_create(ctypes.byref(self.h))
         if r:
             raise RuntimeError(f"mi_dec_create: {r}")
+        if threads > 1:
+            self.lib.mi_dec_set_threads(self.h, threads)
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -112,3 +117,26 @@ class Av1Decoder:
             if r == 0:
                 return
             yield ev
+
+
+def stream_events(data, threads=1, lookahead=None):
+    """Decoder events of an IVF stream in decode order. With threads > 1 the front-end keeps
+    `lookahead` (default 2 * threads) temporal units ahead of the events handed out, so that
+    frames decode on the worker threads while the caller consumes earlier ones. Each event is
+    valid until the next one is requested."""
+    dec = Av1Decoder(threads)
+    la = 0 if threads <= 1 else (lookahead if lookahead is not None else 2 * threads)
+    sent = 0
+    for tu in ivf_frames(data):
+        dec.send(tu)
+        sent += 1
+        if sent <= la:
+            continue
+        gen = dec.events()
+        if la:
+            ev = next(gen, None)     # one event per temporal unit sent: the queue stays `la` deep
+            if ev is not None:
+                yield ev
+        else:
+            yield from gen
+    yield from dec.events()

@@ -25,6 +25,12 @@ int mi_dec_create(MiDec **out) {
 
 void mi_dec_destroy(MiDec *d) { delete d; }
 
+int mi_dec_set_threads(MiDec *d, int n) {
+    if (!d || n < 1) return -EINVAL;
+    d->dec.set_threads(n);
+    return 0;
+}
+
 const char *mi_dec_error(const MiDec *d) { return d ? d->dec.error.c_str() : "null decoder"; }
 
 int mi_dec_send(MiDec *d, const uint8_t *data, size_t size) {
@@ -40,7 +46,11 @@ int mi_dec_send(MiDec *d, const uint8_t *data, size_t size) {
 
 int mi_dec_next(MiDec *d, MiDecEvent *ev) {
     if (!d || !ev) return -EINVAL;
-    if (!d->dec.pop(d->cur)) return 0;
+    const int r = d->dec.pop(d->cur);
+    if (r <= 0) {
+        if (r < 0 && d->dec.error.find("not supported") != std::string::npos) return -ENOTSUP;
+        return r;
+    }
     const av1::DecEvent &e = d->cur;
     memset(ev, 0, sizeof(*ev));
     ev->pic_id = e.pic_id;

@@ -2,6 +2,7 @@
 // per-frame block decoder that turns a frame's tile data into a FrameWork.
 #pragma once
 #include <deque>
+#include <thread>
 #include <memory>
 #include <string>
 #include <vector>
@@ -13,8 +14,14 @@ namespace av1 {
 
 // What a reference slot remembers of a decoded frame (picture identity, header, entropy and
 // motion state for later frames: decode.rs submit_frame / refs[]).
+struct FrameJob;
+
 struct RefSlot {
     int pic_id = -1;
+    // set while the frame that refreshed this slot is still being decoded on a worker thread:
+    // cdf (when cdf_from_job), segmap and mvs come from the job's result (Decoder::resolve)
+    std::shared_ptr<FrameJob> job;
+    bool cdf_from_job = false, mvs_from_job = false;
     std::shared_ptr<const FrameHdr> hdr;
     std::shared_ptr<const Cdf> cdf;
     std::shared_ptr<const std::vector<uint8_t>> segmap;
@@ -28,6 +35,7 @@ struct RefSlot {
 // picture to output (show_pic >= 0).
 struct DecEvent {
     std::shared_ptr<FrameWork> work;
+    std::shared_ptr<FrameJob> job;   // the worker decoding `work` (threads > 1), joined by pop()
     int pic_id = -1;                 // id of the picture `work` reconstructs
     int ref_pic[7] = {-1, -1, -1, -1, -1, -1, -1};   // pictures its inter prediction reads
     int show_pic = -1;               // picture to output after this event (-1: none)
@@ -41,7 +49,13 @@ public:
     Decoder();
     // Feed one temporal unit (or any whole number of OBUs). Returns 0 or -errno.
     int send(const uint8_t *data, size_t size);
-    bool pop(DecEvent &ev);
+    // 1 and ev filled, 0 when no event is queued, or -errno (a frame decoded on a worker
+    // thread failed; error explains). Waits for the oldest frame's worker.
+    int pop(DecEvent &ev);
+    // Frame threads (rav1d's n_fc): intra frames are decoded on up to n worker threads while
+    // send() parses on; events still come out in decode order. 1 (default): synchronous.
+    void set_threads(int n) { threads_ = n < 1 ? 1 : n > 64 ? 64 : n; }
+    ~Decoder();
     std::string error;
 
 private:
@@ -54,13 +68,17 @@ private:
                      const std::shared_ptr<const Cdf> &cdf, const std::shared_ptr<const std::vector<uint8_t>> &segmap,
                      const std::shared_ptr<const std::vector<RefMvBlock>> &mvs, const int *refpoc, int bw, int bh);
     void release_unused(DecEvent &ev, const int *old_ids);
+    void resolve(RefSlot &r);
+    void resolve_all();
 
     std::unique_ptr<SeqHdr> seq_;
     std::shared_ptr<FrameHdr> frame_hdr_;
     RefSlot refs_[8];
     struct TileData { const uint8_t *data; size_t size; int start, end; };
     std::vector<TileData> tiles_;
-    std::vector<std::vector<uint8_t>> tile_bufs_;
+    std::vector<std::shared_ptr<std::vector<uint8_t>>> tile_bufs_;
+    int threads_ = 1;
+    std::deque<std::shared_ptr<FrameJob>> running_;
     int n_tiles_ = 0;
     int next_pic_ = 0;
     std::deque<DecEvent> out_;
@@ -83,5 +101,24 @@ struct FrameInputs {
     std::vector<Tile> tiles;                                // in tile order
 };
 int decode_frame(const FrameInputs &in, FrameWork &work, FrameResult &res, std::string &err);
+
+// One frame decoded on a worker thread: copies of everything the decoder may replace while
+// it runs (sequence header, frame header, input CDFs, the temporal unit bytes).
+struct FrameJob {
+    SeqHdr seq;
+    std::shared_ptr<const FrameHdr> hdr;
+    std::shared_ptr<const Cdf> in_cdf;
+    std::vector<std::shared_ptr<std::vector<uint8_t>>> bufs;
+    FrameInputs in;
+    std::shared_ptr<FrameWork> work;
+    FrameResult res;
+    std::string err;
+    int rc = 0;
+    std::thread th;
+    void wait() {
+        if (th.joinable()) th.join();
+    }
+    ~FrameJob() { wait(); }
+};
 
 }  // namespace av1

@@ -773,6 +773,7 @@ int Decoder::parse_obu(const uint8_t *data, size_t size, size_t *used) {
         if (frame_hdr_->show_existing_frame) {
             if (type == 6) return -EINVAL;
             const int idx = frame_hdr_->existing_frame_idx;
+            resolve(refs_[idx]);
             const RefSlot &rs = refs_[idx];
             if (!rs.hdr || rs.pic_id < 0) return -EINVAL;
             DecEvent ev;
@@ -873,6 +874,8 @@ int Decoder::submit_frame() {
     in.hdr = &h;
     in.in_cdf = nullptr;
     for (int i = 0; i < 7; i++) in.refs[i] = nullptr;
+    if (!is_intra_frame(h)) resolve_all();
+    if (h.primary_ref_frame != 7) resolve(refs_[h.refidx[h.primary_ref_frame]]);
     if (!is_intra_frame(h)) {
         for (int i = 0; i < 7; i++) {
             const RefSlot &r = refs_[h.refidx[i]];
@@ -916,11 +919,34 @@ int Decoder::submit_frame() {
     }
     auto work = std::make_shared<FrameWork>();
     FrameResult res;
-    const int r = decode_frame(in, *work, res, error);
-    if (r < 0) return r;
+    std::shared_ptr<FrameJob> job;
+    if (threads_ > 1 && is_intra_frame(h)) {
+        // frame thread: the job owns copies of what the decoder may replace meanwhile
+        while ((int)running_.size() >= threads_) {
+            running_.front()->wait();
+            running_.pop_front();
+        }
+        job = std::make_shared<FrameJob>();
+        job->seq = s;
+        job->hdr = frame_hdr_;
+        if (in.in_cdf) job->in_cdf = refs_[h.refidx[h.primary_ref_frame]].cdf;
+        job->bufs = tile_bufs_;
+        job->in = in;
+        job->in.seq = &job->seq;
+        job->in.hdr = job->hdr.get();
+        job->in.in_cdf = job->in_cdf.get();
+        job->work = work;
+        FrameJob *j = job.get();
+        job->th = std::thread([j] { j->rc = decode_frame(j->in, *j->work, j->res, j->err); });
+        running_.push_back(job);
+    } else {
+        const int r = decode_frame(in, *work, res, error);
+        if (r < 0) return r;
+    }
 
     DecEvent ev;
     ev.work = work;
+    ev.job = job;
     ev.pic_id = next_pic_++;
     if (!is_intra_frame(h))
         for (int i = 0; i < 7; i++) ev.ref_pic[i] = in.refs[i]->pic_id;
@@ -955,6 +981,9 @@ int Decoder::submit_frame() {
         rs.cdf = slot_cdf;
         rs.segmap = res.segmap;
         rs.mvs = h.allow_intrabc ? nullptr : res.mvs;
+        rs.job = job;
+        rs.cdf_from_job = job && h.refresh_context;
+        rs.mvs_from_job = job && !h.allow_intrabc;
         memcpy(rs.refpoc, refpoc, sizeof(refpoc));
         rs.bw = bw;
         rs.bh = bh;
@@ -971,8 +1000,8 @@ int Decoder::submit_frame() {
 
 int Decoder::send(const uint8_t *data, size_t size) {
     // keep the bytes alive for the tiles of a frame that spans several calls
-    tile_bufs_.emplace_back(data, data + size);
-    const uint8_t *p = tile_bufs_.back().data();
+    tile_bufs_.push_back(std::make_shared<std::vector<uint8_t>>(data, data + size));
+    const uint8_t *p = tile_bufs_.back()->data();
     size_t off = 0;
     while (off < size) {
         size_t used = 0;
@@ -988,11 +1017,39 @@ int Decoder::send(const uint8_t *data, size_t size) {
     return 0;
 }
 
-bool Decoder::pop(DecEvent &ev) {
-    if (out_.empty()) return false;
+int Decoder::pop(DecEvent &ev) {
+    if (out_.empty()) return 0;
     ev = std::move(out_.front());
     out_.pop_front();
-    return true;
+    if (ev.job) {
+        ev.job->wait();
+        if (ev.job->rc < 0) {
+            error = ev.job->err.empty() ? "frame decode failed" : ev.job->err;
+            const int rc = ev.job->rc;
+            ev.job.reset();
+            return rc;
+        }
+        ev.job.reset();
+    }
+    return 1;
+}
+
+void Decoder::resolve(RefSlot &r) {
+    if (!r.job) return;
+    r.job->wait();
+    if (r.cdf_from_job) r.cdf = r.job->res.out_cdf;
+    r.segmap = r.job->res.segmap;
+    r.mvs = r.mvs_from_job ? r.job->res.mvs : nullptr;
+    r.job.reset();
+    r.cdf_from_job = r.mvs_from_job = false;
+}
+
+void Decoder::resolve_all() {
+    for (RefSlot &r : refs_) resolve(r);
+}
+
+Decoder::~Decoder() {
+    for (auto &j : running_) j->wait();
 }
 
 }  // namespace av1

@@ -23,12 +23,12 @@ def frames(data):
         off += size
 
 
-def main(d):
+def main(d, threads):
     resource.setrlimit(resource.RLIMIT_AS, (8 << 30, 8 << 30))
     from rav1d_amd.av1dec import Av1Decoder
     for name in sorted(os.listdir(d)):
         data = open(os.path.join(d, name), "rb").read()
-        dec, nev, nerr = Av1Decoder(), 0, 0
+        dec, nev, nerr = Av1Decoder(threads), 0, 0
         for f in frames(data):
             try:
                 dec.send(f)
@@ -36,9 +36,9 @@ def main(d):
                     nev += 1
             except RuntimeError:
                 nerr += 1          # a rejected temporal unit: the stream restarts, as the fuzzer's
-                dec = Av1Decoder() # dav1d_flush / new context would
+                dec = Av1Decoder(threads)   # dav1d_flush / a new context would
         print(name, nev, nerr, flush=True)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 1)

@@ -9,7 +9,7 @@ import hashlib
 
 import numpy as np
 
-from rav1d_amd.av1dec import Av1Decoder, MiDecFrame, ivf_frames
+from rav1d_amd.av1dec import MiDecFrame
 from tests import oracle_lib
 
 
@@ -61,28 +61,27 @@ def oracle_frame(fr):
     return [by_addr[out[i]] for i in range(n)]
 
 
-def decode_stream(data, recon=oracle_frame, max_frames=None):
+def decode_stream(data, recon=oracle_frame, max_frames=None, threads=1):
     """Decode an IVF stream; returns (md5 hex, frames output). `recon(frame) -> planes` runs the
-    pixel path (oracle by default; the GPU path in the -m gpu tests)."""
+    pixel path (oracle by default; the GPU path in the -m gpu tests). threads > 1: the
+    front-end's frame threads (mi_dec_set_threads)."""
+    from rav1d_amd.av1dec import stream_events
     from rav1d_amd.output import Muxer, host_picture_np
-    dec = Av1Decoder()
     pics = {}
     md5 = hashlib.md5()
     mux = Muxer("md5")           # the product md5 muxer (libmi_av1dec.so), checked against hashlib
     shown = 0
-    for tu in ivf_frames(data):
-        dec.send(tu)
-        for ev in dec.events():
-            if ev.frame:
-                fr = ev.frame.contents
-                pics[ev.pic_id] = (recon(fr), fr.up_w, fr.h, fr.layout, fr.bpc)
-            if ev.show_pic >= 0:
-                planes, w, h, layout, bpc = pics[ev.show_pic]
-                md5_update_picture(md5, planes, w, h, layout)
-                mux.write(host_picture_np(planes, w, h, bpc, layout))
-                shown += 1
-            for i in range(ev.n_release):
-                pics.pop(ev.release[i], None)
+    for ev in stream_events(data, threads):
+        if ev.frame:
+            fr = ev.frame.contents
+            pics[ev.pic_id] = (recon(fr), fr.up_w, fr.h, fr.layout, fr.bpc)
+        if ev.show_pic >= 0:
+            planes, w, h, layout, bpc = pics[ev.show_pic]
+            md5_update_picture(md5, planes, w, h, layout)
+            mux.write(host_picture_np(planes, w, h, bpc, layout))
+            shown += 1
+        for i in range(ev.n_release):
+            pics.pop(ev.release[i], None)
         if max_frames and shown >= max_frames:
             break
     digest = mux.digest()

@@ -7,14 +7,18 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 CORPUS = os.path.join(HERE, "golden", "oss_fuzz")
 
 
-def test_fuzz_corpus_never_crashes():
+@pytest.mark.parametrize("threads", [1, 4])
+def test_fuzz_corpus_never_crashes(threads):
+    """threads 4: the front-end's frame threads, failures surfacing from worker threads."""
     names = sorted(os.listdir(CORPUS))
     assert len(names) >= 100
-    r = subprocess.run([sys.executable, os.path.join(HERE, "fuzz_child.py"), CORPUS],
+    r = subprocess.run([sys.executable, os.path.join(HERE, "fuzz_child.py"), CORPUS, str(threads)],
                        capture_output=True, text=True, timeout=600)
     done = [ln.split()[0] for ln in r.stdout.splitlines() if ln.strip()]
     assert r.returncode == 0, f"front-end died (rc {r.returncode}) after {done[-1:]}: {r.stderr[-500:]}"

@@ -34,3 +34,14 @@ def test_front_end_rejects_garbage():
     with pytest.raises(RuntimeError):
         dec.send(bytes([0x12, 0x00, 0x0a, 0x0b, 0x00, 0x00, 0x00, 0x24, 0xff, 0xff, 0xff, 0xff, 0xff]))
         list(dec.events())
+
+
+@pytest.mark.parametrize("threads", [2, 5])
+def test_frame_threads_match_reference_md5(threads):
+    """The front-end's frame threads (mi_dec_set_threads): intra frames decoded on worker
+    threads, events in decode order, MD5 unchanged."""
+    for name in ("av1-1-b8-02-allintra", "itut_t35", "00000791"):
+        v = next(x for x in VECTORS if x["name"] == name)
+        data = open(os.path.join(GOLDEN, v["file"]), "rb").read()
+        md5, n = decode_stream(data, threads=threads)
+        assert md5 == v["md5"], name
