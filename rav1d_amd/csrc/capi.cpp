@@ -392,9 +392,11 @@ int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned
     a.epoch = ctx->ir_epoch;
     a.nframes = nframes;
     a.zero_coefs = (flags & MI_ITX_KEEP_COEFS) ? 0 : 1;
-    // fewer frames than XCDs: the idle XCDs' workers join the frames (1080p8 single frame
-    // 7.22 -> 6.54 ms); MI_IR_SPREAD=0 keeps one XCD per frame
-    static const int spread_env = getenv("MI_IR_SPREAD") ? atoi(getenv("MI_IR_SPREAD")) : 1;
+    // MI_IR_SPREAD=1 (experiment only): with fewer frames than XCDs the idle XCDs' workers join
+    // the frames (1080p8 single frame 7.22 -> 6.54 ms) -- but a worker on another XCD can hit a
+    // 128-B line its own L2 cached before a neighbouring block was written (sc1 loads are
+    // L2-served): observed as wrong pixels with two frames in flight. Off: one XCD per frame.
+    static const int spread_env = getenv("MI_IR_SPREAD") ? atoi(getenv("MI_IR_SPREAD")) : 0;
     a.spread = spread_env && nframes < 8;
     ctx->ir_last_frames = nframes;
     for (int f = 0; f < nframes; f++) ctx->ir_last_n[f] = frames[f].n;

@@ -566,9 +566,10 @@ __global__ __launch_bounds__(64) void intra_kernel(IpredArgs a) {
 //
 // One launch reconstructs whole intra frames: prediction (intra_block) and the residual
 // (inverse transform + add) of every transform block, in dependency order, without a launch
-// per wavefront step. Frame f is worked on by the workgroups the dispatcher placed on XCD f
-// (HW_REG_XCC_ID), and with fewer than 8 frames XCD x joins frame x % nframes; the placement
-// is for L2 locality only: correctness does not depend on it. A block's
+// per wavefront step. Frame f is worked on only by the workgroups the dispatcher placed on
+// XCD f (HW_REG_XCC_ID): the `sc1` loads below are served by the reading XCD's L2, which may
+// hold a line cached before a neighbouring block sharing it was written, so readers and
+// writers of one frame share one L2 (the `spread` experiment breaks this and is off). A block's
 // pixels are published with the hand-off of MI355X_MICROARCH.md's table row 1: 4-/8-B `sc1`
 // stores, the storing wave's vmcnt(0), then one lane's `sc1` done-flag store; readers poll the
 // flag and read pixels with 4-B `sc1` loads only. Each worker wave

@@ -33,12 +33,14 @@ struct Md5 {
         // RFC 1321 section 3.4: four rounds of 16 steps; per-step shift amounts and the
         // constants floor(|sin(i + 1)| * 2^32)
         static const int R[4][4] = { { 7, 12, 17, 22 }, { 5, 9, 14, 20 }, { 4, 11, 16, 23 }, { 6, 10, 15, 21 } };
-        static uint32_t K[64];
-        static bool init = false;
-        if (!init) {
-            for (int i = 0; i < 64; i++) K[i] = (uint32_t)(std::fabs(std::sin((double)(i + 1))) * 4294967296.0);
-            init = true;
-        }
+        struct KT {
+            uint32_t v[64];
+            KT() {
+                for (int i = 0; i < 64; i++) v[i] = (uint32_t)(std::fabs(std::sin((double)(i + 1))) * 4294967296.0);
+            }
+        };
+        static const KT kt;   // thread-safe one-time initialisation
+        const uint32_t *K = kt.v;
         uint32_t x[16];
         for (int i = 0; i < 16; i++)
             x[i] = (uint32_t)p[4 * i] | (uint32_t)p[4 * i + 1] << 8 | (uint32_t)p[4 * i + 2] << 16 | (uint32_t)p[4 * i + 3] << 24;
