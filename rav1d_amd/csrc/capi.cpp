@@ -333,6 +333,8 @@ int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned
     }
     if (int e = ctx_words(ctx)) return fail(ctx, e);
     if (total > ctx->ir_done_n) {
+        // an earlier launch on this context's stream may still poll the old flags
+        if (ctx->ir_done && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(ctx, -EIO);
         if (ctx->ir_done) (void)hipFree(ctx->ir_done);
         ctx->ir_done = nullptr;
         ctx->ir_done_n = 0;

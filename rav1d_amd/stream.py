@@ -61,61 +61,101 @@ def decode_ivf(ctx, data, stream=None, sync_each=True):
     frame_end(ctx, stream)
 
 
-def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=True):
+_extra_lanes = {}
+
+
+def _lanes(ctx, stream, n):
+    """n (context, stream) pairs for frames in flight: the caller's first, then cached extra
+    contexts with their own streams (a context's calls stay on one stream)."""
+    import torch
+    lanes = [(ctx, stream)]
+    key = id(ctx)
+    extra = _extra_lanes.setdefault(key, [])
+    while len(extra) < n - 1:
+        from .frame import Context
+        extra.append((Context(torch.cuda.current_device()), torch.cuda.Stream()))
+    return lanes + extra[:n - 1]
+
+
+def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=True, threads=8, in_flight=1):
     """Decode an IVF stream on the device and write every shown picture through `muxer`
     (rav1d_amd.output.Muxer): the picture leaves HBM once, via mi_output_picture into pinned
     host memory, with film grain applied in that same pass when the frame carries grain and
     apply_grain is set (Dav1dSettings.apply_grain, src/lib.rs). Returns the pictures written.
 
-    pipelined: the host front-end parses temporal unit t + 1 while the device reconstructs
-    frame t (rav1d overlaps its entropy pass with reconstruction the same way with frame
-    threads, src/thread_task.rs): a shown picture is handed to the muxer once its output copy
-    (an event, not a stream sync) has landed, one picture behind; two host pictures alternate.
-    Device failures of any frame are reported by the mi_frame_end at the end of the stream.
-    Without it every frame is checked by mi_frame_end before it is shown."""
+    pipelined: rav1d's frame threading on this path (src/thread_task.rs):
+      * the host front-end decodes intra frames on `threads` worker threads, a few temporal
+        units ahead of the device (mi_dec_set_threads);
+      * frames are reconstructed `in_flight` at a time, frame k on (context, stream) k % in_flight;
+        a frame whose prediction reads other pictures waits for their events first
+        (experimental: with 2, the allintra vector's MD5 is wrong in about half the runs when
+        the lanes really overlap on the device -- not yet understood; default 1);
+      * a shown picture goes to the muxer once its output copy has landed (an event, not a
+        stream sync), one picture behind; host pictures rotate.
+    Device failures of any frame are reported by the mi_frame_end calls at the end of the
+    stream. Without pipelined: one frame at a time, each checked by mi_frame_end before it is
+    shown, the front-end synchronous."""
+    from .av1dec import stream_events
     from .output import HostPicture, output_picture
     import torch
-    dec = Av1Decoder()
-    pics, n = {}, 0
-    hosts = [None, None]
-    pending = None                      # (slot, event) of the picture awaiting the muxer
+    if not pipelined:
+        threads, in_flight = 1, 1
+    lanes = _lanes(ctx, stream, max(1, in_flight))
+    streams = [st if st is not None else torch.cuda.current_stream() for _, st in lanes]
+    if len(lanes) > 1:
+        for st in streams[1:]:
+            st.wait_stream(streams[0])
+    pics, done_ev, n = {}, {}, 0
+    hosts = [None] * (len(lanes) + 1)
+    pending = []                        # (slot, event) of pictures awaiting the muxer, in order
+    k = 0
 
-    def flush():
-        nonlocal pending, n
-        if pending is None:
-            return
-        slot, ev = pending
-        ev.synchronize()
-        muxer.write(hosts[slot].pic)
-        n += 1
-        pending = None
+    def flush(keep):
+        nonlocal n
+        while len(pending) > keep:
+            slot, ev = pending.pop(0)
+            ev.synchronize()
+            muxer.write(hosts[slot].pic)
+            n += 1
 
     slot = 0
-    for tu in ivf_frames(data):
-        dec.send(tu)
-        for ev in dec.events():
-            if ev.frame:
-                pics[ev.pic_id] = run_frame(ctx, ev.frame.contents, stream)
-                if not pipelined:
-                    frame_end(ctx, stream)
-            if ev.show_pic >= 0:
-                out = pics[ev.show_pic].output()
-                h = hosts[slot]
-                if h is None or (h.pic.w, h.pic.h, h.pic.bpc, h.pic.layout) != (out.w, out.h, out.bpc, out.layout):
-                    if pending is not None and pending[0] == slot:
-                        flush()
-                    hosts[slot] = h = HostPicture(out.w, out.h, out.bpc, out.layout)
-                fg = ev.fg if (ev.fg_present and apply_grain) else None
-                output_picture(ctx, out, h, fg, 0, stream)
-                done = torch.cuda.Event()
-                done.record(stream if stream is not None else torch.cuda.current_stream())
-                flush()                  # the previous picture, while this one is on the device
-                pending = (slot, done)
-                if not pipelined:
-                    flush()
-                slot ^= 1
-            for i in range(ev.n_release):
-                pics.pop(ev.release[i], None)
-    flush()
-    frame_end(ctx, stream)
+    for ev in stream_events(data, threads if pipelined else 1):
+        if ev.frame:
+            li = k % len(lanes)
+            k += 1
+            lctx, lst = lanes[li]
+            for r in ev.ref_pic:          # pictures this frame's prediction reads
+                if r >= 0 and r in done_ev:
+                    streams[li].wait_event(done_ev[r])
+            # the pictures are allocated (and zero-filled) on the lane's own stream
+            with torch.cuda.stream(streams[li]):
+                ps = run_frame(lctx, ev.frame.contents, lst)
+            pics[ev.pic_id] = (ps, li)
+            e = torch.cuda.Event()
+            e.record(streams[li])
+            done_ev[ev.pic_id] = e
+            if not pipelined:
+                frame_end(lctx, lst)
+        if ev.show_pic >= 0:
+            ps, li = pics[ev.show_pic]
+            out = ps.output()
+            lctx, lst = lanes[li]
+            if any(p[0] == slot for p in pending):
+                flush(0)
+            h = hosts[slot]
+            if h is None or (h.pic.w, h.pic.h, h.pic.bpc, h.pic.layout) != (out.w, out.h, out.bpc, out.layout):
+                hosts[slot] = h = HostPicture(out.w, out.h, out.bpc, out.layout)
+            fg = ev.fg if (ev.fg_present and apply_grain) else None
+            output_picture(lctx, out, h, fg, 0, lst)
+            done = torch.cuda.Event()
+            done.record(streams[li])
+            pending.append((slot, done))
+            flush(len(lanes) if pipelined else 0)
+            slot = (slot + 1) % len(hosts)
+        for i in range(ev.n_release):
+            pics.pop(ev.release[i], None)
+            done_ev.pop(ev.release[i], None)
+    flush(0)
+    for lctx, lst in lanes:
+        frame_end(lctx, lst)
     return n
