@@ -373,6 +373,16 @@ int mi_deblock_frame_to(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, 
 int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
                 const MiMcBlock *blocks, const uint32_t class_start[2 * MI_MC_NCLASS + 1],
                 uint8_t *masks, int16_t *tmp, void *stream);
+/* mi_mc_frame with flags. MI_MC_ONE_GRID: both plane groups run in one grid, so the small
+ * chroma units fill the luma tail (4K10 synthetic frame: 62 us against 75 for the two
+ * launches). The caller promises that no chroma unit of the call reads a mask written by a SEG
+ * unit of the same call. For a frame without chroma MASK units this is a pure gain; when they
+ * exist, moving them into a second call cost more than it saved (82-85 us), so the caller
+ * keeps mi_mc_frame there. Unknown flags: -EINVAL. */
+#define MI_MC_ONE_GRID 1u
+int mi_mc_frame_ex(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
+                   const MiMcBlock *blocks, const uint32_t class_start[2 * MI_MC_NCLASS + 1],
+                   uint8_t *masks, int16_t *tmp, unsigned flags, void *stream);
 /* OBMC: the caller runs mi_mc_frame a second time with the above-neighbour laps
  * (MI_MC_OBMC_H units) and a third time with the left-neighbour laps (MI_MC_OBMC_V), as
  * obmc() blends above before left. `tmp` (device, int16) receives MI_MC_PREP units; may be

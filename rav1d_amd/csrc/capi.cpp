@@ -186,7 +186,13 @@ extern "C" {
 int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
                 const MiMcBlock *blocks, const uint32_t class_start[2 * MI_MC_NCLASS + 1], uint8_t *masks,
                 int16_t *tmp, void *stream) {
-    if (!ctx || !cur || !class_start) return fail(ctx, -EINVAL);
+    return mi_mc_frame_ex(ctx, cur, refs, nrefs, blocks, class_start, masks, tmp, 0, stream);
+}
+
+int mi_mc_frame_ex(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
+                   const MiMcBlock *blocks, const uint32_t class_start[2 * MI_MC_NCLASS + 1], uint8_t *masks,
+                   int16_t *tmp, unsigned flags, void *stream) {
+    if (!ctx || !cur || !class_start || (flags & ~MI_MC_ONE_GRID)) return fail(ctx, -EINVAL);
     for (int k = 0; k < 2 * MI_MC_NCLASS; k++)
         if (class_start[k] > class_start[k + 1]) return fail(ctx, -EINVAL);
     mi::McArgs a;
@@ -201,9 +207,15 @@ int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nre
     const int w0 = mi::mc_plan(a, 0), w1 = mi::mc_plan(a, 1);
     if (w0 < 0 || w1 < 0) return fail(ctx, -EINVAL);
     hipStream_t s = (hipStream_t)stream;
-    // luma first: chroma units of SEG blocks read the mask their luma unit writes
-    int r = mi::launch_mc(a, 0, w0, s);
-    if (!r) r = mi::launch_mc(a, 1, w1, s);
+    // luma first: chroma units of SEG blocks read the mask their luma unit writes (one grid
+    // only when the caller says no chroma unit of this call does)
+    int r;
+    if ((flags & MI_MC_ONE_GRID) && w0 && w1) {
+        r = mi::launch_mc(a, 2, w0 + w1, s);
+    } else {
+        r = mi::launch_mc(a, 0, w0, s);
+        if (!r) r = mi::launch_mc(a, 1, w1, s);
+    }
     return r ? fail(ctx, -EIO) : 0;
 }
 

@@ -162,14 +162,21 @@ __device__ __forceinline__ void predict(const McArgs &a, const int16_t *win, int
 #define MC_MIN_WAVES 1
 #endif
 template <typename Px>
+// g: 0 / 1 = the waves of plane group 0 / 1; 2 = both groups in one grid (group 0's waves,
+// then group 1's; mi_mc_frame_ex with MI_MC_ONE_GRID: no chroma unit reads a mask written
+// in the same grid), so the small chroma units fill the luma tail.
 __global__ __launch_bounds__(64, MC_MIN_WAVES) void mc_kernel(McArgs a, int g) {
     __shared__ __attribute__((aligned(16))) int16_t win[kWinElems];
     const int lane = threadIdx.x;
 #ifndef MI_MC_XCD_CHUNK
 #define MI_MC_XCD_CHUNK 1
 #endif
+    int wave = xcd_chunk(blockIdx.x, gridDim.x, MI_MC_XCD_CHUNK);
+    if (g == 2) {
+        g = wave >= (int)a.first_wave[0][MI_MC_NCLASS];
+        if (g) wave -= (int)a.first_wave[0][MI_MC_NCLASS];
+    }
     const uint32_t *fw = a.first_wave[g];
-    const int wave = xcd_chunk(blockIdx.x, gridDim.x, MI_MC_XCD_CHUNK);
     // class of this wave: last class whose first wave <= wave (wave-uniform scan)
     int c = 0;
     for (int k = 1; k < MI_MC_NCLASS; k++)

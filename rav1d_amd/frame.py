@@ -143,6 +143,36 @@ class McMeta:
         self.class_start = (ctypes.c_uint32 * (2 * MC_NCLASS + 1))(*[int(v) for v in class_start])
 
 
+class McSplitMeta:
+    """A frame's MC units split for mi_mc_frame_ex(MI_MC_ONE_GRID) (synth.mc_split_one_grid):
+    `a` runs luma and most chroma in one grid, `b` the chroma MASK units after it; both use
+    one device mask buffer."""
+
+    def __init__(self, units, masks):
+        from .synth import mc_split_one_grid
+        ua, ca, ub, cb = mc_split_one_grid(units)
+        self.n = len(units)
+        self.a = McMeta(ua, ca, masks)
+        self.b = McMeta(ub, cb, masks[:0])
+        self.masks = self.b.masks = self.a.masks
+
+
+def mc_frame_one_grid(ctx, cur, refs, split, stream=None, tmp=None):
+    """mi_mc_frame_ex(MI_MC_ONE_GRID) over split.a, then mi_mc_frame over split.b."""
+    pics = (MiPicture * len(refs))(*[r.picture() for r in refs])
+    L, pc, sp = lib(), ctypes.byref(cur.picture()), _stream_ptr(stream)
+    check(L.mi_mc_frame_ex(ctx.h, pc, pics, len(refs), ctypes.c_void_p(split.a.blocks.data_ptr()),
+                           split.a.class_start, ctypes.c_void_p(split.masks.data_ptr()), _dptr(tmp),
+                           MI_MC_ONE_GRID, sp), "mi_mc_frame_ex")
+    if split.b.n:
+        check(L.mi_mc_frame(ctx.h, pc, pics, len(refs), ctypes.c_void_p(split.b.blocks.data_ptr()),
+                            split.b.class_start, ctypes.c_void_p(split.masks.data_ptr()), _dptr(tmp), sp),
+              "mi_mc_frame")
+
+
+MI_MC_ONE_GRID = 1
+
+
 def _dptr(t):
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
 

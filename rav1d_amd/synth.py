@@ -587,6 +587,17 @@ def mc_sort_units(units):
     return units[order], cs
 
 
+def mc_split_one_grid(units):
+    """Split a frame's units for mi_mc_frame_ex(MI_MC_ONE_GRID): (a) luma and every chroma unit
+    that reads no mask written in the same call, one grid; (b) the chroma MASK compound units
+    (chroma of SEG blocks, and wedges, which cannot be told apart from the record), a second
+    call. Returns (units_a, class_start_a, units_b, class_start_b)."""
+    later = (units["plane"] > 0) & (units["ref"][:, 1] >= 0) & (units["comp"] == 2)   # MI_MC_MASK
+    ua, ca = mc_sort_units(units[~later])
+    ub, cb = mc_sort_units(units[later])
+    return ua, ca, ub, cb
+
+
 def make_mc_grid_units(pw, ph, uw, uh, plane, rng, nrefs=2, compound_frac=0.5, mv_px=24):
     """A plane tiled with uw x uh units (any size 2..128, including the 4-tap w/h <= 4 cases),
     for kernel-shape coverage. Compound only where uw, uh >= 8 (as AV1); no SEG/MASK here.

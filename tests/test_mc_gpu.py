@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 import torch
 
-from rav1d_amd.frame import Frame, McMeta, mc_frame
+from rav1d_amd.frame import Frame, McMeta, McSplitMeta, mc_frame, mc_frame_one_grid
 from rav1d_amd.synth import make_mc_grid_units, make_mc_units, make_texture
 from tests import oracle_lib
 
@@ -23,13 +23,18 @@ def make_refs(w, h, bpc, layout, n, rng):
     return refs
 
 
-def run_case(gpu, w, h, bpc, layout, units, class_start, masks, refs, rng):
+def run_case(gpu, w, h, bpc, layout, units, class_start, masks, refs, rng, one_grid=False):
     cur = Frame(w, h, bpc, layout)
     init = [rng.integers(0, 1 << bpc, size=cur.buffer_np(p).shape) for p in range(len(cur.planes))]
     for p, a in enumerate(init):
         cur.set_buffer_np(p, a)
-    meta = McMeta(units, class_start, masks)
-    mc_frame(gpu, cur, refs, meta)
+    if one_grid:
+        # mi_mc_frame_ex(MI_MC_ONE_GRID) + the chroma MASK units in a second call
+        meta = McSplitMeta(units, masks)
+        mc_frame_one_grid(gpu, cur, refs, meta)
+    else:
+        meta = McMeta(units, class_start, masks)
+        mc_frame(gpu, cur, refs, meta)
     torch.cuda.synchronize()
     ref_np = [[r.buffer_np(p) for p in range(len(r.planes))] for r in refs]
     dt = np.uint8 if bpc == 8 else np.uint16
@@ -52,6 +57,29 @@ def test_mc_frame_matches_oracle(gpu, bpc, layout, size):
     refs = make_refs(w, h, bpc, layout, 3, rng)
     units, ps, masks = make_mc_units(w, h, layout, rng, nrefs=3, compound_frac=0.5, mv_px=40)
     run_case(gpu, w, h, bpc, layout, units, ps, masks, refs, rng)
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+@pytest.mark.parametrize("layout", [1, 2, 3, 0])
+def test_mc_frame_one_grid_matches_oracle(gpu, bpc, layout):
+    w, h = 256, 192
+    rng = np.random.default_rng(bpc * 5 + layout * 11 + 1)
+    refs = make_refs(w, h, bpc, layout, 3, rng)
+    units, ps, masks = make_mc_units(w, h, layout, rng, nrefs=3, compound_frac=0.5, mv_px=40)
+    if layout:
+        assert ((units["plane"] > 0) & (units["comp"] == 2) & (units["ref"][:, 1] >= 0)).any()
+    run_case(gpu, w, h, bpc, layout, units, ps, masks, refs, rng, one_grid=True)
+
+
+def test_mc_frame_ex_rejects_unknown_flags(gpu):
+    from rav1d_amd import lib
+    from rav1d_amd.frame import MiPicture
+    import ctypes
+    cur = Frame(64, 64, 8, 1)
+    cs = (ctypes.c_uint32 * 129)()
+    rc = lib().mi_mc_frame_ex(gpu.h, ctypes.byref(cur.picture()), (MiPicture * 1)(cur.picture()), 1,
+                              None, cs, None, None, 2, None)
+    assert rc == -22
 
 
 UNIT_SHAPES = [(2, 2), (2, 4), (4, 2), (4, 4), (4, 8), (8, 4), (4, 16), (16, 4), (8, 8), (8, 16), (16, 8),
