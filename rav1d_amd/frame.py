@@ -138,6 +138,9 @@ class McMeta:
 
     def __init__(self, units, class_start, masks):
         self.n = len(units)
+        # no chroma MASK unit (which may read a mask a SEG luma unit of the call writes): both
+        # plane groups can run in one grid (mi_mc_frame_ex, MI_MC_ONE_GRID)
+        self.one_grid = not bool(((units["plane"] > 0) & (units["ref"][:, 1] >= 0) & (units["comp"] == 2)).any())
         self.blocks = torch.from_numpy(np.ascontiguousarray(units).view(np.uint8).copy()).cuda()
         self.masks = torch.from_numpy(np.ascontiguousarray(masks).copy()).cuda()
         self.class_start = (ctypes.c_uint32 * (2 * MC_NCLASS + 1))(*[int(v) for v in class_start])
@@ -181,10 +184,11 @@ def mc_frame(ctx, cur, refs, meta, stream=None, tmp=None):
     """mi_mc_frame: inter prediction of every unit into `cur` from the reference Frames.
     tmp: optional int16 device tensor (arena for MI_MC_PREP units)."""
     pics = (MiPicture * len(refs))(*[r.picture() for r in refs])
-    rc = lib().mi_mc_frame(ctx.h, ctypes.byref(cur.picture()), pics, len(refs),
-                           ctypes.c_void_p(meta.blocks.data_ptr()), meta.class_start,
-                           ctypes.c_void_p(meta.masks.data_ptr()), _dptr(tmp), _stream_ptr(stream))
-    check(rc, "mi_mc_frame")
+    rc = lib().mi_mc_frame_ex(ctx.h, ctypes.byref(cur.picture()), pics, len(refs),
+                              ctypes.c_void_p(meta.blocks.data_ptr()), meta.class_start,
+                              ctypes.c_void_p(meta.masks.data_ptr()), _dptr(tmp),
+                              MI_MC_ONE_GRID if meta.one_grid else 0, _stream_ptr(stream))
+    check(rc, "mi_mc_frame_ex")
 
 
 def _dev(a):
