@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define MI_AV1DEC_ABI_VERSION 1
+#define MI_AV1DEC_ABI_VERSION 2
 
 /* The pass-2 work of one decoded frame. All pointers stay valid until the next
  * mi_dec_next() / mi_dec_destroy() on the same decoder. */
@@ -66,6 +66,26 @@ typedef struct MiDecFrame {
     /* loop restoration */
     const MiAv1Restoration *lr_mask;   /* [sb128h][lr_sb128w] */
     int32_t lr_sb128w, restore_planes, lr_unit_size[2];
+    /* inter prediction (recon_b_inter, recon.rs:3162-4045), run before the residuals: every count
+     * is 0 in an intra frame. MiMcBlock / MiWarpBlock refs index the frame's seven references
+     * (LAST .. ALTREF = MiDecEvent.ref_pic[0..6]). */
+    const MiMcBlock *mc;              /* put / compound / MI_MC_PREP units, any order */
+    int32_t n_mc;
+    const MiMcBlock *obmc_h;          /* OBMC laps of above neighbours (blended first) */
+    int32_t n_obmc_h;
+    const MiMcBlock *obmc_v;          /* OBMC laps of left neighbours */
+    int32_t n_obmc_v;
+    const MiWarpBlock *warp;          /* warp8x8 / warp8x8t blocks */
+    int32_t n_warp;
+    const MiMcBlock *scaled;          /* units whose reference differs in size (put or MI_MC_PREP) */
+    int32_t n_scaled;
+    const MiMcCombine *combine_y;     /* compounds with a warped / scaled side: luma ... */
+    int32_t n_combine_y;
+    const MiMcCombine *combine_uv;    /* ... then chroma (its MASK units read what luma SEG wrote) */
+    int32_t n_combine_uv;
+    const uint8_t *masks;             /* wedge masks (MASK inputs) and room for SEG outputs */
+    size_t nmasks;
+    size_t ntmp;                      /* int16 elements of the arena the prep sides write */
 } MiDecFrame;
 
 /* One decoder event: a frame to reconstruct into picture `pic_id` (frame != NULL; its inter
@@ -80,6 +100,7 @@ typedef struct MiDecEvent {
     MiFilmGrainData fg;
     const int32_t *release;
     int32_t n_release;
+    int32_t mtrx_identity;   /* seq_hdr.mtrx == DAV1D_MC_IDENTITY (the grain's chroma clip, fg_apply.rs) */
 } MiDecEvent;
 
 /* ---- device execution of a decoded frame (these two live in librav1d_amd.so) ----
@@ -92,6 +113,8 @@ typedef struct MiDecEvent {
  * filter_sbrow: recon.rs:4019-4211). */
 typedef struct MiFramePictures {
     MiPicture recon, deblocked, cdef, restored;
+    MiPicture refs[7];    /* the reference pictures of an inter frame (MiDecEvent.ref_pic order,
+                             each the reference's final picture); unused for intra frames */
 } MiFramePictures;
 
 /* Enqueue one frame's reconstruction and in-loop filters on `stream` (recon_b_intra over the

@@ -265,6 +265,10 @@ typedef struct MiIntraBlock {
                               recon.rs:2052-2083: reads outside it replicate its border, as
                               emu_edge); the block's dependencies must cover the source rectangle
                               (plus one column / row when the chroma phase is half-pel) */
+#define MI_INTRA_RESID 97  /* MiIntraBlock.mode: no prediction, the residual of a transform block of an
+                              inter-intra block (recon_b_inter's itxfm_add after the blend,
+                              recon.rs:3940-4045) added to the pixels already there; its dependencies
+                              must cover its own rectangle (the MI_INTRA_II block) */
 #define MI_IPRED_II 128    /* mode flag: inter-intra, blend the prediction into the existing
                               (inter) pixels with the mask at idx + aux_off (mc.blend,
                               recon.rs:3524-3543): only with slots 0-12 */

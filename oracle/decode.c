@@ -5,8 +5,10 @@
  *
  * Order, as rav1d decodes a frame with one thread (decode.rs decode_frame_main ->
  * decode_tile_sbrow + filter_sbrow; recon.rs:4019-4211 filter_sbrow):
- *   reconstruction of every block in decode order (recon_b_intra: prediction, then itxfm_add
- *   per transform block) -> deblock (lf_apply.rs, sbrow order, in place) -> CDEF
+ *   reconstruction of every block (inter prediction of all inter blocks and their residuals --
+ *   they read only reference pictures, so doing them first changes no pixel -- then the intra
+ *   blocks in decode order: recon_b_intra's prediction, then itxfm_add per transform block)
+ *   -> deblock (lf_apply.rs, sbrow order, in place) -> CDEF
  *   (cdef_apply.rs, reads the deblocked picture) -> loop restoration (lr_apply.rs, reads the
  *   CDEF output and the deblocked rows across stripe edges).
  * Film grain is applied by the caller to output pictures only (fg_apply.rs).
@@ -32,22 +34,54 @@ void oracle_lr_frame(void *const dst[3], void *const cdef[3], void *const debloc
 /* pic: the picture to reconstruct (128-aligned planes, cleared or not); scratch1/2: two more
  * pictures of the same geometry. On return the final (reference) picture is in out[], which
  * points at one of the three. */
-void oracle_decode_frame(const MiDecFrame *f, void *const pic[3], void *const scratch1[3],
-                         void *const scratch2[3], const ptrdiff_t strides[3], void **out)
+void oracle_decode_frame_refs(const MiDecFrame *f, void *const pic[3], void *const scratch1[3],
+                              void *const scratch2[3], const ptrdiff_t strides[3], void *const *refs,
+                              const ptrdiff_t *ref_strides, const int *ref_wh, void **out)
 {
     const int bpc = f->bpc, layout = f->layout;
     const int ss_ver = layout == 1;
     const int nplanes = layout ? 3 : 1;
     const size_t cb = bpc == 8 ? 2 : 4;
+    const ptrdiff_t st2[2] = { strides[0], strides[1] };
+    /* the arena is consumed by the transforms: work on a copy */
+    void *coef = malloc(f->ncoef * cb + 16);
+    memcpy(coef, f->coef, f->ncoef * cb);
 
-    /* 1. intra path in decode order (the arena is consumed: work on a copy) */
-    if (f->n_intra) {
-        void *coef = malloc(f->ncoef * cb + 16);
-        memcpy(coef, f->coef, f->ncoef * cb);
-        const ptrdiff_t st2[2] = { strides[0], strides[1] };
-        oracle_intra_recon(pic, st2, bpc, f->intra, f->intra_tx, f->n_intra, NULL, f->idx, f->pal, coef);
-        free(coef);
+    /* 1. inter prediction of every inter block (recon_b_inter, recon.rs:3162-3940): the units
+     * read only reference pictures, so they run before any residual. Within a compound block
+     * the luma SEG unit precedes the chroma units that read its mask. */
+    if (f->n_mc || f->n_warp || f->n_scaled || f->n_combine_y || f->n_obmc_h || f->n_obmc_v) {
+        int16_t *tmp = malloc(sizeof(int16_t) * (f->ntmp + 1));
+        uint8_t *masks = malloc(f->nmasks + 1);
+        if (f->nmasks) memcpy(masks, f->masks, f->nmasks);
+        oracle_mc_frame(pic, st2, layout, bpc, refs, ref_strides, ref_wh, f->mc, f->n_mc, masks, tmp);
+        oracle_mc_warp_frame(pic, st2, layout, bpc, refs, ref_strides, ref_wh, f->warp, f->n_warp, tmp);
+        oracle_mc_scaled_frame(pic, st2, layout, bpc, f->w, f->h, refs, ref_strides, ref_wh, f->scaled, f->n_scaled,
+                               tmp);
+        oracle_mc_combine_frame(pic, st2, layout, bpc, f->combine_y, f->n_combine_y, tmp, masks);
+        oracle_mc_combine_frame(pic, st2, layout, bpc, f->combine_uv, f->n_combine_uv, tmp, masks);
+        /* obmc(): the above laps, then the left laps (recon.rs:2205-2309); a lap whose
+         * reference differs in size goes through the scaled path */
+        for (int k = 0; k < 2; k++) {
+            const MiMcBlock *u = k ? f->obmc_v : f->obmc_h;
+            const int n = k ? f->n_obmc_v : f->n_obmc_h;
+            for (int i = 0; i < n; i++) {
+                const int r = u[i].ref[0];
+                if (ref_wh[r * 2] != f->w || ref_wh[r * 2 + 1] != f->h)
+                    oracle_mc_scaled_frame(pic, st2, layout, bpc, f->w, f->h, refs, ref_strides, ref_wh, &u[i], 1, tmp);
+                else
+                    oracle_mc_frame(pic, st2, layout, bpc, refs, ref_strides, ref_wh, &u[i], 1, masks, tmp);
+            }
+        }
+        free(tmp);
+        free(masks);
     }
+    /* 2. the residuals of inter blocks (read_coef_tree / recon_b_inter's chroma itxfm_add) */
+    if (f->n_inter_tx) oracle_itx_frame(pic, strides, f->inter_tx, f->n_inter_tx, coef, (1 << bpc) - 1);
+    /* 3. intra path in decode order (intra blocks of the frame, inter-intra blends) */
+    if (f->n_intra)
+        oracle_intra_recon(pic, st2, bpc, f->intra, f->intra_tx, f->n_intra, NULL, f->idx, f->pal, coef);
+    free(coef);
     /* 2. deblocking, in place */
     if (f->filter_y)
         oracle_deblock_frame(pic, strides, f->w, f->h, layout, bpc, f->lf_level, f->b4_stride, f->lf_masks,
@@ -97,4 +131,11 @@ void oracle_decode_frame(const MiDecFrame *f, void *const pic[3], void *const sc
     }
     (void)ss_ver;
     for (int p = 0; p < 3; p++) out[p] = p < nplanes ? final[p] : NULL;
+}
+
+/* An intra frame (no references). */
+void oracle_decode_frame(const MiDecFrame *f, void *const pic[3], void *const scratch1[3],
+                         void *const scratch2[3], const ptrdiff_t strides[3], void **out)
+{
+    oracle_decode_frame_refs(f, pic, scratch1, scratch2, strides, NULL, NULL, NULL, out);
 }

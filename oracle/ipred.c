@@ -503,6 +503,7 @@ void oracle_intra_blocks(void *const planes[3], const ptrdiff_t strides[2], int 
     uint8_t edge[(2 * 128 + 1) * 2], tmp[64 * 64 * 2];
     for (int k = 0; k < n; k++) {
         const IntraBlock *b = &bl[k];
+        if (b->mode == 97) continue;   /* MI_INTRA_RESID: the residual only (no prediction) */
         const ptrdiff_t st = strides[b->plane ? 1 : 0];
         uint8_t *dst = (uint8_t *)planes[b->plane] + b->y * st + b->x * pb;
         const int ii = b->flags & 64;

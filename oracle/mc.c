@@ -509,13 +509,17 @@ void oracle_mc_scaled_frame(void *const cur[3], const ptrdiff_t cur_stride[2], i
         const int sx = scale_fac(ref_wh[r * 2], cur_w), sy = scale_fac(ref_wh[r * 2 + 1], cur_h);
         const int stx = (sx + 8) >> 4, sty = (sy + 8) >> 4;
         const int mvx = bk->mvx[0], mvy = bk->mvy[0];
+        /* an OBMC lap (comp 4 above / 5 left) from a scaled reference: mc() into the lap buffer
+         * at the reference's own lap geometry, then blend_h / blend_v (recon.rs:2205-2309) */
+        const int v_mul = 4 >> ss_ver;
+        const int bh_ = bk->comp == 4 ? (((bk->param / v_mul) * 3 + 3) >> 2) * v_mul : bk->h;
         const int opy = (bk->y << 4) + mvy * (1 << !ss_ver), opx = (bk->x << 4) + mvx * (1 << !ss_hor);
         const int64_t tx = (int64_t)opx * sx + (int64_t)(sx - 0x4000) * 8;
         const int64_t ty = (int64_t)opy * sy + (int64_t)(sy - 0x4000) * 8;
         const int pos_x = (int)(tx < 0 ? -((-tx + 128) >> 8) : (tx + 128) >> 8) + 32;
         const int pos_y = (int)(ty < 0 ? -((-ty + 128) >> 8) : (ty + 128) >> 8) + 32;
         const int left = pos_x >> 10, top = pos_y >> 10;
-        const int right = ((pos_x + (bk->w - 1) * stx) >> 10) + 1, bottom = ((pos_y + (bk->h - 1) * sty) >> 10) + 1;
+        const int right = ((pos_x + (bk->w - 1) * stx) >> 10) + 1, bottom = ((pos_y + (bh_ - 1) * sty) >> 10) + 1;
         const int w = (ref_wh[r * 2] + ss_hor) >> ss_hor, h = (ref_wh[r * 2 + 1] + ss_ver) >> ss_ver;
         const void *rp = refs[r * 3 + p];
         ptrdiff_t rs = ref_strides[r * 2 + (p ? 1 : 0)];
@@ -532,8 +536,17 @@ void oracle_mc_scaled_frame(void *const cur[3], const ptrdiff_t cur_stride[2], i
         const ptrdiff_t ds = cur_stride[p ? 1 : 0];
         uint8_t *dst = (uint8_t *)cur[p] + bk->y * ds + bk->x * pb;
         const int prep = bk->comp == 6;
-        oracle_mc_scaled(bk->filter2d, prep, dst, ds, prep ? tmp_arena + bk->mask_off : NULL, ref, rs, bk->w, bk->h,
-                         pos_x & 0x3ff, pos_y & 0x3ff, stx, sty, bpc);
+        if (bk->comp == 4 || bk->comp == 5) {
+            uint8_t *lap = malloc((size_t)128 * 128 * pb);
+            oracle_mc_scaled(bk->filter2d, 0, lap, bk->w * pb, NULL, ref, rs, bk->w, bh_, pos_x & 0x3ff, pos_y & 0x3ff,
+                             stx, sty, bpc);
+            if (bk->comp == 4) oracle_mc_blend_h(dst, ds, lap, bk->w, bk->param, bpc);
+            else oracle_mc_blend_v(dst, ds, lap, bk->w, bk->h, bpc);
+            free(lap);
+        } else {
+            oracle_mc_scaled(bk->filter2d, prep, dst, ds, prep ? tmp_arena + bk->mask_off : NULL, ref, rs, bk->w, bk->h,
+                             pos_x & 0x3ff, pos_y & 0x3ff, stx, sty, bpc);
+        }
         free(emu);
     }
 }

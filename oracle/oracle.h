@@ -80,6 +80,13 @@ void oracle_mc_combine_frame(void *const cur[3], const ptrdiff_t cur_stride[2], 
 void oracle_superres_frame(void *const src[3], const ptrdiff_t src_stride[2], void *const dst[3],
                            const ptrdiff_t dst_stride[2], int layout, int bpc, int src_w, int dst_w, int h);
 
+/* ---- frame driver (decode.c) ---- */
+/* refs: 7 x 3 plane pointers (LAST .. ALTREF), ref_strides 7 x 2, ref_wh 7 x 2 (luma w, h) */
+struct MiDecFrame;
+void oracle_decode_frame_refs(const struct MiDecFrame *f, void *const pic[3], void *const scratch1[3],
+                              void *const scratch2[3], const ptrdiff_t strides[3], void *const *refs,
+                              const ptrdiff_t *ref_strides, const int *ref_wh, void **out);
+
 /* ---- ipred (src/ipred.rs; C twin src/ipred_tmpl.c) ---- */
 /* mode = intra_pred[] slot: 0 DC,1 V,2 H,3 LEFT_DC,4 TOP_DC,5 DC_128,6 Z1,7 Z2,8 Z3,9 SMOOTH,
  * 10 SMOOTH_V,11 SMOOTH_H,12 PAETH,13 FILTER; `angle` carries is_sm (bit 9) and the edge-filter

@@ -31,7 +31,7 @@ class MiPicture(ctypes.Structure):
 
 class MiFramePictures(ctypes.Structure):
     """include/mi_av1dec.h: the pictures of one frame's pass 2 (recon, deblocked, cdef, restored)."""
-    _fields_ = [("pics", MiPicture * 4)]
+    _fields_ = [("pics", MiPicture * 4), ("refs", MiPicture * 7)]
 
 
 class MiIntraFrame(ctypes.Structure):

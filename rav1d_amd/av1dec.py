@@ -31,14 +31,24 @@ class MiDecFrame(ctypes.Structure):
                 ("cdef_on", ctypes.c_int32), ("cdef_damping", ctypes.c_int32),
                 ("cdef_y", ctypes.c_uint8 * 8), ("cdef_uv", ctypes.c_uint8 * 8),
                 ("lr_mask", ctypes.c_void_p), ("lr_sb128w", ctypes.c_int32), ("restore_planes", ctypes.c_int32),
-                ("lr_unit_size", ctypes.c_int32 * 2)]
+                ("lr_unit_size", ctypes.c_int32 * 2),
+                ("mc", ctypes.c_void_p), ("n_mc", ctypes.c_int32),
+                ("obmc_h", ctypes.c_void_p), ("n_obmc_h", ctypes.c_int32),
+                ("obmc_v", ctypes.c_void_p), ("n_obmc_v", ctypes.c_int32),
+                ("warp", ctypes.c_void_p), ("n_warp", ctypes.c_int32),
+                ("scaled", ctypes.c_void_p), ("n_scaled", ctypes.c_int32),
+                ("combine_y", ctypes.c_void_p), ("n_combine_y", ctypes.c_int32),
+                ("combine_uv", ctypes.c_void_p), ("n_combine_uv", ctypes.c_int32),
+                ("masks", ctypes.c_void_p), ("nmasks", ctypes.c_size_t),
+                ("ntmp", ctypes.c_size_t)]
 
 
 class MiDecEvent(ctypes.Structure):
     _fields_ = [("frame", ctypes.POINTER(MiDecFrame)), ("pic_id", ctypes.c_int32),
                 ("ref_pic", ctypes.c_int32 * 7), ("show_pic", ctypes.c_int32),
                 ("fg_present", ctypes.c_int32), ("fg", MiFilmGrainData),
-                ("release", ctypes.POINTER(ctypes.c_int32)), ("n_release", ctypes.c_int32)]
+                ("release", ctypes.POINTER(ctypes.c_int32)), ("n_release", ctypes.c_int32),
+                ("mtrx_identity", ctypes.c_int32)]
 
 
 def build_dec():
@@ -78,6 +88,84 @@ def ivf_frames(path_or_bytes):
             break
         yield bytes(data[off:off + size])
         off += size
+
+
+def _leb128(data, off):
+    v, n = 0, 0
+    while True:
+        if off + n >= len(data) or n >= 8:
+            raise ValueError("truncated leb128")
+        b = data[off + n]
+        v |= (b & 0x7f) << (7 * n)
+        n += 1
+        if not b & 0x80:
+            return v, n
+
+
+def _obu_type(b):
+    return (b >> 3) & 0xf
+
+
+def _is_annexb(data):
+    """annexb_probe (tools/input/annexb.rs; C tools/input/annexb.c): temporal unit, frame unit and
+    OBU sizes nest, and the first OBU is an empty temporal delimiter."""
+    try:
+        tu, n0 = _leb128(data, 0)
+        fu, n1 = _leb128(data, n0)
+        ou, n2 = _leb128(data, n0 + n1)
+    except ValueError:
+        return False
+    o = n0 + n1 + n2
+    if fu + n1 > tu or ou + n2 >= fu or o >= len(data):
+        return False
+    return _obu_type(data[o]) == 2
+
+
+def annexb_units(data):
+    """Annex B demuxer (tools/input/annexb.rs): temporal_unit(size) > frame_unit(size) >
+    obu_length + OBU; yields one OBU at a time, as the reference hands each to the decoder."""
+    off = 0
+    while off < len(data):
+        tu, n = _leb128(data, off)
+        off += n
+        end_tu = off + tu
+        while off < end_tu:
+            fu, n = _leb128(data, off)
+            off += n
+            end_fu = off + fu
+            while off < end_fu:
+                ln, n = _leb128(data, off)
+                off += n
+                yield bytes(data[off:off + ln])
+                off += ln
+
+
+def section5_units(data):
+    """Low-overhead OBU stream (section 5; tools/input/section5.rs): temporal units split at
+    temporal delimiters, every OBU carrying its size field."""
+    off, start = 0, 0
+    while off < len(data):
+        h = data[off]
+        if not h & 0x2:
+            raise ValueError("section 5 OBU without a size field")
+        if _obu_type(h) == 2 and off > start:
+            yield bytes(data[start:off])
+            start = off
+        ext = 1 if h & 0x4 else 0
+        ln, n = _leb128(data, off + 1 + ext)
+        off += 1 + ext + n + ln
+    if off > start:
+        yield bytes(data[start:off])
+
+
+def stream_units(data):
+    """The decoder inputs of a file in any of the reference CLI's demuxer formats (IVF, Annex B,
+    section 5; tools/input/input.rs probes them in that order)."""
+    if data[:4] == b"DKIF":
+        return ivf_frames(data)
+    if _is_annexb(data):
+        return annexb_units(data)
+    return section5_units(data)
 
 
 class Av1Decoder:
@@ -120,14 +208,14 @@ class Av1Decoder:
 
 
 def stream_events(data, threads=1, lookahead=None):
-    """Decoder events of an IVF stream in decode order. With threads > 1 the front-end keeps
+    """Decoder events of a stream (IVF, Annex B or section 5) in decode order. With threads > 1 the front-end keeps
     `lookahead` (default 2 * threads) temporal units ahead of the events handed out, so that
     frames decode on the worker threads while the caller consumes earlier ones. Each event is
     valid until the next one is requested."""
     dec = Av1Decoder(threads)
     la = 0 if threads <= 1 else (lookahead if lookahead is not None else 2 * threads)
     sent = 0
-    for tu in ivf_frames(data):
+    for tu in stream_units(data):
         dec.send(tu)
         sent += 1
         if sent <= la:

@@ -296,7 +296,9 @@ def lr_frame(ctx, cdef, deblocked, dst, meta, stream=None):
 
 
 def film_grain_data(fg):
-    """dict (rav1d_amd.synth.make_fg_params) -> MiFilmGrainData"""
+    """dict (rav1d_amd.synth.make_fg_params) -> MiFilmGrainData (a MiFilmGrainData is returned as is)"""
+    if isinstance(fg, MiFilmGrainData):
+        return fg
     d = MiFilmGrainData()
     d.seed = fg["seed"]
     d.num_y_points = fg["num_y_points"]

@@ -40,13 +40,25 @@ int mi_dec_send(MiDec *d, const uint8_t *data, size_t size) {
         if (r < 0 && d->dec.error.find("not supported") != std::string::npos) return -ENOTSUP;
         return r;
     } catch (const std::bad_alloc &) {
+        d->dec.error = "out of memory";
         return -ENOMEM;
+    } catch (const std::exception &e) {
+        // e.g. std::system_error from a frame thread that could not be started: no C++
+        // exception crosses the C ABI
+        d->dec.error = e.what();
+        return -EAGAIN;
     }
 }
 
 int mi_dec_next(MiDec *d, MiDecEvent *ev) {
     if (!d || !ev) return -EINVAL;
-    const int r = d->dec.pop(d->cur);
+    int r;
+    try {
+        r = d->dec.pop(d->cur);
+    } catch (const std::exception &e) {
+        d->dec.error = e.what();
+        return -EAGAIN;
+    }
     if (r <= 0) {
         if (r < 0 && d->dec.error.find("not supported") != std::string::npos) return -ENOTSUP;
         return r;
@@ -58,6 +70,7 @@ int mi_dec_next(MiDec *d, MiDecEvent *ev) {
     ev->show_pic = e.show_pic;
     ev->fg_present = e.fg_present;
     ev->fg = e.fg;
+    ev->mtrx_identity = e.mtrx_identity;
     d->release.assign(e.release.begin(), e.release.end());
     ev->release = d->release.data();
     ev->n_release = (int32_t)d->release.size();
@@ -105,6 +118,23 @@ int mi_dec_next(MiDec *d, MiDecEvent *ev) {
         f.restore_planes = w.restore_planes;
         f.lr_unit_size[0] = w.lr_unit_size[0];
         f.lr_unit_size[1] = w.lr_unit_size[1];
+        f.mc = w.mc.data();
+        f.n_mc = (int32_t)w.mc.size();
+        f.obmc_h = w.obmc_h.data();
+        f.n_obmc_h = (int32_t)w.obmc_h.size();
+        f.obmc_v = w.obmc_v.data();
+        f.n_obmc_v = (int32_t)w.obmc_v.size();
+        f.warp = w.warp.data();
+        f.n_warp = (int32_t)w.warp.size();
+        f.scaled = w.scaled.data();
+        f.n_scaled = (int32_t)w.scaled.size();
+        f.combine_y = w.combine_y.data();
+        f.n_combine_y = (int32_t)w.combine_y.size();
+        f.combine_uv = w.combine_uv.data();
+        f.n_combine_uv = (int32_t)w.combine_uv.size();
+        f.masks = w.masks.data();
+        f.nmasks = w.masks.size();
+        f.ntmp = w.ntmp;
         ev->frame = &f;
     }
     return 1;

@@ -13,7 +13,7 @@
 #include <cstdio>
 #include <string>
 
-#include "decoder.h"
+#include "framedec.h"
 
 namespace av1 {
 
@@ -51,101 +51,7 @@ void BlockCtx::reset(bool keyframe) {
     std::fill(pal_sz.begin(), pal_sz.end(), 0);
 }
 
-namespace {
-
-template <typename T>
-inline void setn(std::vector<T> &v, int off, int n, int val) {
-    for (int i = 0; i < n; i++) v[off + i] = (T)val;
-}
-
-struct Block {
-    int bl, bs, bp, intra, seg_id, skip_mode, skip;
-    int y_mode, uv_mode, tx, uvtx, pal_sz[2], y_angle, uv_angle, cfl_alpha[2];
-};
-
-struct TileState {
-    Cdf cdf;
-    Msac msac;
-    int col_start, col_end, row_start, row_end;   // 4x4 units
-    int last_qidx;
-    int8_t last_delta_lf[4];
-    uint16_t dq[8][3][2];
-    LfLvl lflvl;
-    MiAv1RestorationUnit *lr_ref[3];
-};
-
-class FrameDec {
-public:
-    FrameDec(const FrameInputs &in, FrameWork &fw) : in_(in), s(*in.seq), h(*in.hdr), fw(fw) {}
-    int run(FrameResult &res, std::string &err);
-
-private:
-    const FrameInputs &in_;
-    const SeqHdr &s;
-    const FrameHdr &h;
-    FrameWork &fw;
-
-    int bw, bh, w4, h4, sb128w, sb128h, sb_shift, sb_step, sbh, b4_stride, layout, ss_hor, ss_ver, hbd_idx;
-    uint16_t dq_frame[8][3][2];
-    LfLvl lflvl_frame;
-    std::vector<TileState> ts_;
-    TileState *ts = nullptr;
-    BlockCtx a, l;
-    int bx = 0, by = 0;
-    int8_t *cur_cdef_idx = nullptr;
-    MiAv1Filter *lf_mask = nullptr;
-    uint16_t al_pal[2][32][3][8];            // [above / left][pos][plane][entry]
-    uint8_t pal_sz_uv[2][32];
-    std::vector<uint8_t> segmap;
-    std::vector<uint8_t> tx_lpf_right[2];    // per tile column: left context at the tile's right edge
-    std::vector<std::vector<uint8_t>> a_tx_lpf_end[2];   // above context at the end of each tile row
-    std::vector<int32_t> owner[3];           // per plane, per 4x4: index of the intra block there
-    int owner_stride;
-    std::string *err_ = nullptr;
-
-    int fail(const char *m) {
-        if (err_) *err_ = m;
-        return -EINVAL;
-    }
-    void init_quant(int qidx, uint16_t (*dq)[3][2]);
-    void calc_lf_values(LfLvl &out, const int8_t delta[4]);
-    void setup_tile(TileState &t, const uint8_t *data, size_t sz, int row, int col);
-    int decode_tile_sbrow(int tile_row, int tile_col);
-    void read_lr(MiAv1RestorationUnit *lr, int p, int frame_type);
-    int decode_sb(int bl, bool tr, bool lb);
-    int decode_b(int bl, int bs, int bp, int edge_flags);
-    void read_pal_plane(Block &b, int pl, int sz_ctx, int bx4, int by4, uint16_t *pal);
-    void read_pal_uv(Block &b, int sz_ctx, int bx4, int by4, uint16_t (*pal)[8]);
-    void read_pal_indices(uint8_t *idx, const Block &b, int pl, int w4, int h4, int bw4, int bh4);
-    int decode_coefs(uint8_t *actx, uint8_t *lctx, int tx, int bs, const Block &b, int intra, int plane, int32_t *cf,
-                     int *txtp, uint8_t *res_ctx);
-    void emit_intra(const Block &b, int edge_flags, const uint8_t *pal_idx, const uint16_t (*pal)[8]);
-    uint32_t store_coefs(const int32_t *cf, int tx);
-    void add_deps(int plane, int x0, int y0, int x1, int y1, std::vector<int32_t> &out);
-    void mask_edges_intra(int by4, int bx4, int w4_, int h4_, int tx, uint8_t *actx, uint8_t *lctx, uint16_t (*masks)[32][3][2]);
-    void mask_edges_chroma(int cby4, int cbx4, int cw4, int ch4, int skip_inter, int tx, uint8_t *actx, uint8_t *lctx,
-                           uint16_t (*masks)[32][2][2]);
-    void create_lf_mask_intra(const Block &b, int has_chroma);
-    void tile_fixups();
-
-    // intra block copy (decode.rs:1988-2135): the frame's refmvs blocks (per 4x4, padded by
-    // 8 units on each side), the DV candidate search, mv residual, var-tx tree and the
-    // inter-style residual walk that emits MI_INTRA_IBC work
-    std::vector<RefMvBlock> rmv;
-    int rmv_stride = 0;
-    std::vector<int32_t> dep_tmp;     // one block's dependency list (reused)
-    RefMvBlock &rmv_at(int y4, int x4) { return rmv[(size_t)(y4 + 8) * rmv_stride + (x4 + 8)]; }
-    void splat_rmv(int bs, int bw4, int bh4, Mv mv, bool valid);
-    void find_dv(int bs, int edge_flags, Mv stack[2]);
-    int read_mv_comp(CdfMvComp &c);
-    void read_mv_residual(Mv &mv, CdfMv &cdf);
-    void read_tx_tree(int from, int depth, uint16_t *masks, int x_off, int y_off, int tbx, int tby);
-    void ibc_residual_tree(const Block &b, Mv mv, int tx, int depth, const uint16_t *split, int x_off, int y_off,
-                           int tbx, int tby, uint8_t (*txtp_map)[32]);
-    void push_ibc(const Block &b, Mv mv, int plane, int tx, int tbx, int tby, int px, int py, int eob_txtp_read,
-                  uint8_t *actx, uint8_t *lctx, int nact, int nlct, int *txtp);
-    int decode_ibc(Block &b, int bs, int edge_flags, int has_chroma);
-};
+namespace fd {
 
 // ------------------------------------------------------------------------------------------
 // frame-level setup (decode.rs decode_frame_init; C decode.c:54-75, 2776-3155; lf_mask.c
@@ -1024,7 +930,15 @@ void FrameDec::emit_intra(const Block &b, int edge_flags, const uint8_t *pal_idx
 
 static const Mv kInvalidMv = { INT16_MIN, INT16_MIN };   // refmvs INVALID_MV: an intra block
 
-// refmvs splat_mv (refmvs.rs): the block's entry over its bw4 x bh4 units
+// refmvs splat_mv (refmvs.rs; C refmvs.c:909-917): the block's entry over its bw4 x bh4 units
+void FrameDec::splat(const RefMvBlock &r, int bw4, int bh4) {
+    for (int y = 0; y < bh4; y++) {
+        RefMvBlock *row = &rmv_at(by + y, bx);
+        for (int x = 0; x < bw4; x++) row[x] = r;
+    }
+}
+
+// splat_intrabc_mv / splat_intraref (decode.rs; C decode.c:570-614)
 void FrameDec::splat_rmv(int bs, int bw4, int bh4, Mv mv, bool valid) {
     RefMvBlock r{};
     r.mv[0] = valid ? mv : kInvalidMv;
@@ -1033,8 +947,7 @@ void FrameDec::splat_rmv(int bs, int bw4, int bh4, Mv mv, bool valid) {
     r.ref[1] = -1;
     r.bs = (uint8_t)bs;
     r.mf = 0;
-    for (int y = 0; y < bh4; y++)
-        for (int x = 0; x < bw4; x++) rmv_at(by + y, bx + x) = r;
+    splat(r, bw4, bh4);
 }
 
 // rav1d_refmvs_find (refmvs.rs; C refmvs.c dav1d_refmvs_find) for ref = {INTRA_FRAME, none}:
@@ -1134,27 +1047,39 @@ void FrameDec::find_dv(int bs, int edge_flags, Mv stack[2]) {
     for (int n = 0; n < 2; n++) stack[n] = n < cnt ? st[n].mv : Mv{ 0, 0 };
 }
 
-// read_mv_component_diff / read_mv_residual (decode.rs:224-311) without fractional bits
-int FrameDec::read_mv_comp(CdfMvComp &c) {
+// read_mv_component_diff / read_mv_residual (decode.rs:224-311; C decode.c:76-139): have_fp = 0
+// for block copies and force_integer_mv (fp = 3, hp = 1)
+int FrameDec::read_mv_comp(CdfMvComp &c, int have_fp) {
     Msac &m = ts->msac;
     const int sign = m.bool_adapt(c.sign);
     const int cl = m.symbol(c.classes, 10);
-    int up;
+    int up, fp = 3, hp = 1;
     if (!cl) {
         up = m.bool_adapt(c.class0);
+        if (have_fp) {
+            fp = m.symbol(c.class0_fp[up], 3);
+            hp = h.hp ? m.bool_adapt(c.class0_hp) : 1;
+        }
     } else {
         up = 1 << cl;
         for (int n = 0; n < cl; n++) up |= m.bool_adapt(c.classN[n]) << n;
+        if (have_fp) {
+            fp = m.symbol(c.classN_fp, 3);
+            hp = h.hp ? m.bool_adapt(c.classN_hp) : 1;
+        }
     }
-    const int diff = ((up << 3) | (3 << 1) | 1) + 1;
+    const int diff = ((up << 3) | (fp << 1) | hp) + 1;
     return sign ? -diff : diff;
 }
 
-void FrameDec::read_mv_residual(Mv &mv, CdfMv &cdf) {
+void FrameDec::read_mv_residual(Mv &mv, CdfMv &cdf, int have_fp) {
     switch (ts->msac.symbol(ts->cdf.mv.joint, 3)) {   // the joint always comes from cdf.mv
-    case 3: mv.y = (int16_t)(mv.y + read_mv_comp(cdf.comp[0])); mv.x = (int16_t)(mv.x + read_mv_comp(cdf.comp[1])); break;
-    case 1: mv.x = (int16_t)(mv.x + read_mv_comp(cdf.comp[1])); break;
-    case 2: mv.y = (int16_t)(mv.y + read_mv_comp(cdf.comp[0])); break;
+    case 3:
+        mv.y = (int16_t)(mv.y + read_mv_comp(cdf.comp[0], have_fp));
+        mv.x = (int16_t)(mv.x + read_mv_comp(cdf.comp[1], have_fp));
+        break;
+    case 1: mv.x = (int16_t)(mv.x + read_mv_comp(cdf.comp[1], have_fp)); break;
+    case 2: mv.y = (int16_t)(mv.y + read_mv_comp(cdf.comp[0], have_fp)); break;
     default: break;
     }
 }
@@ -1184,6 +1109,34 @@ void FrameDec::read_tx_tree(int from, int depth, uint16_t *masks, int x_off, int
     } else {
         setn(a.tx, tbx, t.w, is_split ? TX_4X4 : txw);
         setn(l.tx, tby4, t.h, is_split ? TX_4X4 : txh);
+    }
+}
+
+// read_vartx_tree (decode.rs:770-851; C decode.c:479-532): max_ytx, uvtx and the split masks of
+// an inter (or block copy) block
+void FrameDec::read_vartx_tree(Block &b, int bs) {
+    const BlockDim &bd = k_bdim[bs];
+    const int bw4 = bd.w4, bh4 = bd.h4, by4 = by & 31;
+    b.tx_split[0] = b.tx_split[1] = 0;
+    b.max_ytx = k_max_tx_for_bs[bs][0];
+    if (!b.skip && (h.seg.lossless[b.seg_id] || b.max_ytx == TX_4X4)) {
+        b.max_ytx = b.uvtx = TX_4X4;
+        if (h.txfm_mode == TXMODE_SWITCHABLE) {
+            setn(a.tx, bx, bw4, TX_4X4);
+            setn(l.tx, by4, bh4, TX_4X4);
+        }
+    } else if (h.txfm_mode != TXMODE_SWITCHABLE || b.skip) {
+        if (h.txfm_mode == TXMODE_SWITCHABLE) {
+            setn(a.tx, bx, bw4, bd.lw4);
+            setn(l.tx, by4, bh4, bd.lh4);
+        }
+        b.uvtx = k_max_tx_for_bs[bs][layout];
+    } else {
+        const TxDim &yt = k_txdim[b.max_ytx];
+        for (int yo = 0; yo < bh4 / yt.h; yo++)
+            for (int xo = 0; xo < bw4 / yt.w; xo++)
+                read_tx_tree(b.max_ytx, 0, b.tx_split, xo, yo, bx + xo * yt.w, by + yo * yt.h);
+        b.uvtx = k_max_tx_for_bs[bs][layout];
     }
 }
 
@@ -1283,7 +1236,7 @@ int FrameDec::decode_ibc(Block &b, int bs, int edge_flags, int has_chroma) {
     else if (!(stack[1] == Mv{ 0, 0 })) mv = stack[1];
     else if (by - (16 << s.sb128) < ts->row_start) mv = Mv{ 0, (int16_t)(-(512 << s.sb128) - 2048) };
     else mv = Mv{ (int16_t)(-(512 << s.sb128)), 0 };
-    read_mv_residual(mv, ts->cdf.dmv);
+    read_mv_residual(mv, ts->cdf.dmv, 0);
     // keep the source inside the decoded part of the tile, outside the current superblock
     int border_left = ts->col_start * 4, border_top = ts->row_start * 4;
     if (has_chroma) {
@@ -1307,28 +1260,9 @@ int FrameDec::decode_ibc(Block &b, int bs, int edge_flags, int has_chroma) {
     mv.x = (int16_t)((src_left - bx * 4) * 8);
     mv.y = (int16_t)((src_top - by * 4) * 8);
 
-    // var-tx tree (decode.rs read_vartx_tree:770-851)
-    uint16_t split[2] = { 0, 0 };
-    int max_ytx = k_max_tx_for_bs[bs][0];
-    if (!b.skip && (h.seg.lossless[b.seg_id] || max_ytx == TX_4X4)) {
-        b.uvtx = max_ytx = TX_4X4;
-        if (h.txfm_mode == TXMODE_SWITCHABLE) {
-            setn(a.tx, bx, bw4, TX_4X4);
-            setn(l.tx, by4, bh4, TX_4X4);
-        }
-    } else if (h.txfm_mode != TXMODE_SWITCHABLE || b.skip) {
-        if (h.txfm_mode == TXMODE_SWITCHABLE) {
-            setn(a.tx, bx, bw4, bd.lw4);
-            setn(l.tx, by4, bh4, bd.lh4);
-        }
-        b.uvtx = k_max_tx_for_bs[bs][layout];
-    } else {
-        const TxDim &yt = k_txdim[max_ytx];
-        for (int yo = 0; yo < bh4 / yt.h; yo++)
-            for (int xo = 0; xo < bw4 / yt.w; xo++)
-                read_tx_tree(max_ytx, 0, split, xo, yo, bx + xo * yt.w, by + yo * yt.h);
-        b.uvtx = k_max_tx_for_bs[bs][layout];
-    }
+    read_vartx_tree(b, bs);
+    const uint16_t *split = b.tx_split;
+    const int max_ytx = b.max_ytx;
 
     // prediction + residual work in the reference's coefficient order
     const int w4b = imin(bw4, bw - bx), h4b = imin(bh4, bh - by);
@@ -1452,9 +1386,11 @@ int FrameDec::decode_b(int bl, int bs, int bp, int edge_flags) {
             seg = &h.seg.d[b.seg_id];
         }
     }
-    // skip mode never applies in intra frames; skip
+    // skip_mode (inter frames with skip_mode_present), skip
     b.skip_mode = 0;
-    if (seg && seg->skip) b.skip = 1;
+    if ((!seg || (!seg->globalmv && seg->ref == -1 && !seg->skip)) && h.skip_mode_enabled && imin(bw4, bh4) > 1)
+        b.skip_mode = m.bool_adapt(ts->cdf.m.skip_mode[a.skip_mode[bx] + l.skip_mode[by4]]);
+    if (b.skip_mode || (seg && seg->skip)) b.skip = 1;
     else b.skip = m.bool_adapt(ts->cdf.m.skip[a.skip[bx] + l.skip[by4]]);
     if (h.seg.enabled && h.seg.update_map && !h.seg.preskip) {
         if (!b.skip && h.seg.temporal &&
@@ -1526,9 +1462,35 @@ int FrameDec::decode_b(int bl, int bs, int bp, int edge_flags) {
         else if (memcmp(ts->last_delta_lf, prev_dlf, 4)) calc_lf_values(ts->lflvl, ts->last_delta_lf);
     }
 
-    if (h.allow_intrabc) {
+    if (b.skip_mode) {
+        b.intra = 0;
+    } else if (inter_frame) {
+        if (seg && (seg->ref >= 0 || seg->globalmv)) {
+            b.intra = !seg->ref;
+        } else {
+            // get_intra_ctx (env.rs; C env.h:59-73)
+            int ictx = 0;
+            if (have_left) {
+                if (have_top) {
+                    ictx = l.intra[by4] + a.intra[bx];
+                    ictx += ictx == 2;
+                } else {
+                    ictx = l.intra[by4] * 2;
+                }
+            } else if (have_top) {
+                ictx = a.intra[bx] * 2;
+            }
+            b.intra = !m.bool_adapt(ts->cdf.m.intra[ictx]);
+        }
+    } else if (h.allow_intrabc) {
         b.intra = !m.bool_adapt(ts->cdf.m.intrabc);
-        if (!b.intra) {
+    } else {
+        b.intra = 1;
+    }
+    if (!b.intra && inter_frame) {
+        if (int e = decode_inter(b, bs, edge_flags, has_chroma, have_left, have_top, seg, seg_pred)) return e;
+    } else if (!b.intra) {
+        {
             if (int e = decode_ibc(b, bs, edge_flags, has_chroma)) return e;
             // contexts of a block copy (decode.rs:2104-2135)
             setn(a.tx_intra, bx, bw4, bd.lw4);
@@ -1551,18 +1513,12 @@ int FrameDec::decode_b(int bl, int bs, int bp, int edge_flags) {
                 setn(a.uvmode, cbx, cbw4, DC_PRED);
                 setn(l.uvmode, cby4, cbh4, DC_PRED);
             }
-            if (h.seg.enabled && h.seg.update_map)
-                for (int y = 0; y < bh4; y++)
-                    if (by + y < (int)(segmap.size() / b4_stride))
-                        memset(&segmap[(size_t)(by + y) * b4_stride + bx], b.seg_id, bw4);
-            return 0;
         }
     } else {
-        b.intra = 1;
-    }
 
     // intra modes
-    uint16_t *ycdf = ts->cdf.kfym[k_intra_mode_ctx[a.mode[bx]]][k_intra_mode_ctx[l.mode[by4]]];
+    uint16_t *ycdf = inter_frame ? ts->cdf.m.y_mode[k_ymode_size_ctx[bs]]
+                                 : ts->cdf.kfym[k_intra_mode_ctx[a.mode[bx]]][k_intra_mode_ctx[l.mode[by4]]];
     b.y_mode = m.symbol(ycdf, 12);
     if (bd.lw4 + bd.lh4 >= 2 && b.y_mode >= V_PRED && b.y_mode <= D67_PRED)
         b.y_angle = (int)m.symbol(ts->cdf.m.angle_delta[b.y_mode - V_PRED], 6) - 3;
@@ -1671,12 +1627,26 @@ int FrameDec::decode_b(int bl, int bs, int bp, int edge_flags) {
                 for (int y = 0; y < bh4; y++) memcpy(al_pal[1][by4 + y][pl], pal[pl], 16);
             }
     }
+    if (inter_frame) {
+        setn(a.comp_type, bx, bw4, COMP_NONE);
+        setn(l.comp_type, by4, bh4, COMP_NONE);
+        setn(a.ref[0], bx, bw4, -1);
+        setn(l.ref[0], by4, bh4, -1);
+        setn(a.ref[1], bx, bw4, -1);
+        setn(l.ref[1], by4, bh4, -1);
+        setn(a.filter[0], bx, bw4, 3);
+        setn(l.filter[0], by4, bh4, 3);
+        setn(a.filter[1], bx, bw4, 3);
+        setn(l.filter[1], by4, bh4, 3);
+    }
+    if (h.allow_intrabc || inter_frame) splat_rmv(bs, bw4, bh4, Mv{ 0, 0 }, false);
+    }   // intra
+
     // segmentation map, CDEF skip mask
     if (h.seg.enabled && h.seg.update_map)
         for (int y = 0; y < bh4; y++)
             if (by + y < (int)(segmap.size() / b4_stride))
                 memset(&segmap[(size_t)(by + y) * b4_stride + bx], b.seg_id, bw4);
-    if (h.allow_intrabc) splat_rmv(bs, bw4, bh4, Mv{ 0, 0 }, false);
     if (!b.skip) {
         uint16_t (*ns)[2] = &lf_mask->noskip_mask[by4 >> 1];
         const unsigned mask = (~0u >> (32 - bw4)) << (bx4 & 15);
@@ -2026,7 +1996,7 @@ void FrameDec::tile_fixups() {
 
 int FrameDec::run(FrameResult &res, std::string &err) {
     err_ = &err;
-    if (!is_intra_frame(h)) return fail("inter frames are not supported by this front-end yet");
+    inter_frame = !is_intra_frame(h);
     layout = s.layout;
     ss_hor = layout == 1 || layout == 2;
     ss_ver = layout == 1;
@@ -2052,7 +2022,7 @@ int FrameDec::run(FrameResult &res, std::string &err) {
     fw.ss_hor = ss_hor;
     fw.ss_ver = ss_ver;
     fw.sb128 = s.sb128;
-    fw.intra_only = 1;
+    fw.intra_only = !inter_frame;
     // arena entries 0..15: the reserved zero block that residual-free records point at
     fw.ncoef = 16;
     fw.coef.assign((size_t)16 * (s.bpc == 8 ? 2 : 4), 0);
@@ -2101,13 +2071,18 @@ int FrameDec::run(FrameResult &res, std::string &err) {
     a_tx_lpf_end[1].resize(h.tiling.rows);
     owner_stride = (b4_stride + 32);
     for (int p = 0; p < 3; p++) owner[p].assign((size_t)owner_stride * (sb128h * 32 + 32), -1);
-    if (h.allow_intrabc) {
+    if (h.allow_intrabc || inter_frame) {
         RefMvBlock none{};
         none.mv[0] = kInvalidMv;
         none.ref[0] = -1;
         none.ref[1] = -1;
         rmv_stride = b4_stride + 16;
         rmv.assign((size_t)rmv_stride * (sb128h * 32 + 16), none);
+        f2d_map.assign(rmv.size(), 0);
+    }
+    if (inter_frame) {
+        refmvs_init_frame();
+        inter_frame_init();
     }
     a.alloc(b4_stride + 64);
     l.alloc(64);
@@ -2127,12 +2102,16 @@ int FrameDec::run(FrameResult &res, std::string &err) {
         const int sb_end = imin(h.tiling.row_start_sb[tr + 1], sbh);
         for (int sby = h.tiling.row_start_sb[tr]; sby < sb_end; sby++) {
             by = sby << sb_shift;
+            // decode.rs decode_frame_main (C decode.c:3225-3244): temporal MVs projected per
+            // sbrow before its tiles, this frame's MVs saved after them
+            if (inter_frame && h.use_ref_frame_mvs) load_tmvs(by >> 1, (by + sb_step) >> 1);
             for (int tc = 0; tc < h.tiling.cols; tc++) {
                 ts = &ts_[tr * h.tiling.cols + tc];
                 if (ts->msac.cnt < -15) return fail("symbol decoder overread");
                 const int r = decode_tile_sbrow(tr, tc);
                 if (r) return r;
             }
+            if (inter_frame) save_tmvs(by >> 1, (by + sb_step) >> 1);
         }
         a_tx_lpf_end[0][tr] = a.tx_lpf_y;
         a_tx_lpf_end[1][tr] = a.tx_lpf_uv;
@@ -2146,6 +2125,7 @@ int FrameDec::run(FrameResult &res, std::string &err) {
         else cdf_init_default(*res.out_cdf, h.quant.yac);
         cdf_update_frame(*res.out_cdf, ts_[h.tiling.update].cdf, is_intra_frame(h));
     }
+    if (inter_frame) res.mvs = rp;
     if (h.seg.enabled) {
         if (h.seg.update_map) res.segmap = std::make_shared<std::vector<uint8_t>>(std::move(segmap));
         else if (in_.prev_segmap) res.segmap = std::make_shared<std::vector<uint8_t>>(*in_.prev_segmap);
@@ -2154,10 +2134,10 @@ int FrameDec::run(FrameResult &res, std::string &err) {
     return 0;
 }
 
-}  // namespace
+}  // namespace fd
 
 int decode_frame(const FrameInputs &in, FrameWork &work, FrameResult &res, std::string &err) {
-    FrameDec d(in, work);
+    fd::FrameDec d(in, work);
     return d.run(res, err);
 }
 

@@ -25,7 +25,7 @@ struct RefSlot {
     std::shared_ptr<const FrameHdr> hdr;
     std::shared_ptr<const Cdf> cdf;
     std::shared_ptr<const std::vector<uint8_t>> segmap;
-    std::shared_ptr<const std::vector<RefMvBlock>> mvs;   // 8x8-subsampled temporal MVs
+    std::shared_ptr<const std::vector<TmvBlock>> mvs;   // 8x8-subsampled temporal MVs (save_tmvs)
     int refpoc[7];
     int bw, bh;   // 4x4-unit frame size the segmap / mvs belong to
     int showable;
@@ -41,6 +41,7 @@ struct DecEvent {
     int show_pic = -1;               // picture to output after this event (-1: none)
     MiFilmGrainData fg{};            // grain of the shown picture (if fg_present)
     int fg_present = 0;
+    int mtrx_identity = 0;           // the grain's chroma clip (seq_hdr.mtrx == MC_IDENTITY)
     std::vector<int> release;        // pictures no slot references any more
 };
 
@@ -66,7 +67,7 @@ private:
     int submit_frame();
     void update_refs(int pic_id, const std::shared_ptr<const FrameHdr> &hdr,
                      const std::shared_ptr<const Cdf> &cdf, const std::shared_ptr<const std::vector<uint8_t>> &segmap,
-                     const std::shared_ptr<const std::vector<RefMvBlock>> &mvs, const int *refpoc, int bw, int bh);
+                     const std::shared_ptr<const std::vector<TmvBlock>> &mvs, const int *refpoc, int bw, int bh);
     void release_unused(DecEvent &ev, const int *old_ids);
     void resolve(RefSlot &r);
     void resolve_all();
@@ -89,7 +90,7 @@ private:
 struct FrameResult {
     std::shared_ptr<Cdf> out_cdf;                           // refresh_context
     std::shared_ptr<std::vector<uint8_t>> segmap;
-    std::shared_ptr<std::vector<RefMvBlock>> mvs;
+    std::shared_ptr<std::vector<TmvBlock>> mvs;
 };
 struct FrameInputs {
     const SeqHdr *seq;

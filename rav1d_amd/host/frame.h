@@ -24,7 +24,13 @@ inline bool operator==(Mv a, Mv b) { return a.y == b.y && a.x == b.x; }
 struct RefMvBlock {
     Mv mv[2];
     int8_t ref[2];     // 0 intra, 1..7 = LAST..ALTREF, -1 none
-    uint8_t bs, mf;
+    uint8_t bs, mf;    // mf: 1 = globalmv with a warped global model, 2 = newmv
+};
+// One saved motion vector per 8x8 for later frames' temporal prediction (refmvs.rs
+// refmvs_temporal_block; C refmvs.h): ref 0 = none
+struct TmvBlock {
+    Mv mv;
+    int8_t ref;
 };
 
 struct LfLvl { uint8_t v[8][4][8][2]; };   // [seg][plane/dir][ref][mode] (lf_mask.rs lflvl)
@@ -39,6 +45,16 @@ struct FrameWork {
     std::vector<int32_t> dep_start, deps;
     // residuals of inter blocks (no intra dependency)
     std::vector<MiTxBlock> inter_tx;
+    // inter prediction (recon_b_inter's mc / obmc / warp_affine / compound calls as descriptors,
+    // run before the residuals): main units (put, compound, MI_MC_PREP sides), OBMC laps (all
+    // above laps, then all left laps), warped 8x8s, scaled-reference units, compound combines
+    // (all luma, then all chroma), the mask arena (MASK inputs, SEG outputs) and the int16
+    // elements of the tmp arena the prep sides write
+    std::vector<MiMcBlock> mc, obmc_h, obmc_v, scaled;
+    std::vector<MiWarpBlock> warp;
+    std::vector<MiMcCombine> combine_y, combine_uv;
+    std::vector<uint8_t> masks;
+    size_t ntmp = 0;
     // coefficient arena: int16 (8 bpc) or int32 (10/12 bpc) values, as bytes
     std::vector<uint8_t> coef;
     size_t ncoef;

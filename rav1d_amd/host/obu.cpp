@@ -780,6 +780,7 @@ int Decoder::parse_obu(const uint8_t *data, size_t size, size_t *used) {
             ev.show_pic = rs.pic_id;
             ev.fg_present = rs.hdr->fg.present;
             ev.fg = rs.hdr->fg.data;
+            ev.mtrx_identity = seq_->mtrx == 0;
             if (rs.hdr->frame_type == FRAME_KEY) {
                 // a shown key frame refreshes every slot (obu.rs show_existing_frame)
                 int old_ids[8];
@@ -954,6 +955,7 @@ int Decoder::submit_frame() {
         ev.show_pic = ev.pic_id;
         ev.fg_present = h.fg.present;
         ev.fg = h.fg.data;
+        ev.mtrx_identity = s.mtrx == 0;
     }
     // reference slots (decode.rs submit_frame: refresh_frame_flags)
     std::shared_ptr<const Cdf> slot_cdf;

@@ -19,6 +19,8 @@ def _bind(o):
     vp = ctypes.c_void_p
     o.oracle_decode_frame.argtypes = [ctypes.POINTER(MiDecFrame), vp, vp, vp, vp, vp]
     o.oracle_decode_frame.restype = None
+    o.oracle_decode_frame_refs.argtypes = [ctypes.POINTER(MiDecFrame), vp, vp, vp, vp, vp, vp, vp, vp]
+    o.oracle_decode_frame_refs.restype = None
     o._dec_bound = True
     return o
 
@@ -44,8 +46,9 @@ def md5_update_picture(md5, planes, w, h, layout):
             md5.update(np.ascontiguousarray(planes[p][:ch, :cw]).tobytes())
 
 
-def oracle_frame(fr):
-    """Reconstruct one MiDecFrame through the oracle; returns the final planes (1 or 3)."""
+def oracle_frame(fr, refs=None):
+    """Reconstruct one MiDecFrame through the oracle; returns the final planes (1 or 3).
+    refs: the seven reference pictures of an inter frame, (planes, w, h) each (None: unused)."""
     o = _bind(oracle_lib.load_oracle())
     # super-resolution: every picture has the upscaled geometry (the coded width is a prefix)
     pics = [alloc_picture(fr.up_w, fr.h, fr.bpc, fr.layout) for _ in range(3)]
@@ -55,15 +58,30 @@ def oracle_frame(fr):
     arr = [(ctypes.c_void_p * 3)(*[a.ctypes.data for a in p]) for p in pics]
     st = (ctypes.c_ssize_t * 3)(*[a.strides[0] for a in pics[0]])
     out = (ctypes.c_void_p * 3)()
-    o.oracle_decode_frame(ctypes.byref(fr), arr[0], arr[1], arr[2], st, out)
+    rp = (ctypes.c_void_p * 21)()
+    rs = (ctypes.c_ssize_t * 14)()
+    rwh = (ctypes.c_int * 14)()
+    for i, r in enumerate(refs or []):
+        if r is None:
+            continue
+        planes, w, h = r
+        for p in range(3):
+            a = planes[p] if p < len(planes) else planes[0]
+            rp[i * 3 + p] = a.ctypes.data
+        rs[i * 2] = planes[0].strides[0]
+        rs[i * 2 + 1] = (planes[1] if len(planes) > 1 else planes[0]).strides[0]
+        rwh[i * 2], rwh[i * 2 + 1] = w, h
+    o.oracle_decode_frame_refs(ctypes.byref(fr), arr[0], arr[1], arr[2], st, rp, rs, rwh, out)
     by_addr = {a.ctypes.data: a for p in pics for a in p}
     n = 3 if fr.layout else 1
     return [by_addr[out[i]] for i in range(n)]
 
 
-def decode_stream(data, recon=oracle_frame, max_frames=None, threads=1):
-    """Decode an IVF stream; returns (md5 hex, frames output). `recon(frame) -> planes` runs the
-    pixel path (oracle by default; the GPU path in the -m gpu tests). threads > 1: the
+def decode_stream(data, recon=oracle_frame, max_frames=None, threads=1, apply_grain=False):
+    """Decode an IVF stream; returns (md5 hex, frames output). `recon(frame, refs) -> planes` runs
+    the pixel path (refs: the reference pictures, (planes, w, h) or None, in ref_pic order).
+    apply_grain: the reference CLI's --filmgrain 1 (Dav1dSettings.apply_grain, src/lib.rs): shown
+    pictures that carry grain get it (the oracle's rav1d_apply_grain) before hashing (oracle by default; the GPU path in the -m gpu tests). threads > 1: the
     front-end's frame threads (mi_dec_set_threads)."""
     from rav1d_amd.av1dec import stream_events
     from rav1d_amd.output import Muxer, host_picture_np
@@ -74,9 +92,17 @@ def decode_stream(data, recon=oracle_frame, max_frames=None, threads=1):
     for ev in stream_events(data, threads):
         if ev.frame:
             fr = ev.frame.contents
-            pics[ev.pic_id] = (recon(fr), fr.up_w, fr.h, fr.layout, fr.bpc)
+            refs = [None] * 7
+            for i in range(7):
+                r = ev.ref_pic[i]
+                if r >= 0:
+                    planes, w, h = pics[r][0], pics[r][1], pics[r][2]
+                    refs[i] = (planes, w, h)
+            pics[ev.pic_id] = (recon(fr, refs), fr.up_w, fr.h, fr.layout, fr.bpc)
         if ev.show_pic >= 0:
             planes, w, h, layout, bpc = pics[ev.show_pic]
+            if apply_grain and ev.fg_present:
+                planes = oracle_lib.film_grain(planes, bpc, layout, w, h, ev.fg, ev.mtrx_identity)
             md5_update_picture(md5, planes, w, h, layout)
             mux.write(host_picture_np(planes, w, h, bpc, layout))
             shown += 1

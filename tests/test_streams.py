@@ -4,7 +4,10 @@ The vectors and their MD5s are the reference's own (tests/dav1d-test-data/**/mes
 into tests/golden/streams/ by tools/make_stream_fixtures.py); the MD5 is taken over the shown
 frames exactly as the md5 muxer does (tools/output/md5.rs:541-637). A match pins the whole
 oracle chain used by these streams — intra prediction (all modes, CfL, palette, filter intra,
-edge filter / upsampling), itx, deblocking, CDEF and loop restoration — bit for bit to rav1d.
+edge filter / upsampling), inter prediction (single / compound / wedge / segmentation masks,
+OBMC, local and global warp, inter-intra, scaled references, sub-8x8 chroma), itx, deblocking,
+CDEF, loop restoration and (for the reference's --filmgrain 1 vectors) film grain — bit for bit
+to rav1d. Inputs are IVF, Annex B or section-5 OBU streams, demuxed as the reference CLI does.
 """
 import json
 import os
@@ -23,7 +26,7 @@ def load(v):
 
 @pytest.mark.parametrize("v", VECTORS, ids=[v["name"] for v in VECTORS])
 def test_oracle_matches_reference_md5(v):
-    md5, n = decode_stream(load(v))
+    md5, n = decode_stream(load(v), apply_grain=bool(v.get("filmgrain")))
     assert n > 0
     assert md5 == v["md5"], f"{v['name']}: {n} frames, md5 {md5} != {v['md5']}"
 

@@ -22,6 +22,46 @@ PINNED = [
     ("long_leb", "8-bit/features/long_leb.ivf"),
     ("00000791", "12-bit/data/00000791.ivf"),
     ("itut_t35", "10-bit/features/itut_t35.ivf", "itut_t35_10bit"),   # 4K 10-bit, intra block copy
+    # inter frames: the smallest vectors that together use every inter tool at 8, 10 and 12 bit
+    # and every layout (compound avg / w_avg / wedge / seg, OBMC, local and global warp,
+    # inter-intra, scaled references, sub-8x8 chroma), from tools/dev feature counts
+    ("av1-1-b8-01-size-18x16", "8-bit/size/av1-1-b8-01-size-18x16.ivf"),
+    ("av1-1-b8-01-size-18x18", "8-bit/size/av1-1-b8-01-size-18x18.ivf"),
+    ("av1-1-b8-01-size-18x34", "8-bit/size/av1-1-b8-01-size-18x34.ivf"),
+    ("00000623", "8-bit/data/00000623.ivf"),
+    ("00000706", "8-bit/data/00000706.ivf"),
+    ("00000711", "8-bit/data/00000711.ivf"),
+    ("00000862", "8-bit/data/00000862.ivf"),
+    ("00001105", "8-bit/data/00001105.ivf"),
+    ("00001132", "8-bit/data/00001132.ivf"),
+    ("00001137", "8-bit/data/00001137.ivf"),
+    ("00001138", "8-bit/data/00001138.ivf"),
+    ("00000716", "10-bit/data/00000716.ivf", "00000716_10bit"),
+    ("00000721", "10-bit/data/00000721.ivf", "00000721_10bit"),
+    ("00000726", "10-bit/data/00000726.ivf", "00000726_10bit"),
+    ("00000831", "10-bit/data/00000831.ivf", "00000831_10bit"),
+    ("00000943", "10-bit/data/00000943.ivf", "00000943_10bit"),
+    ("av1-1-b10-00-quantizer-61", "10-bit/quantizer/av1-1-b10-00-quantizer-61.ivf"),
+    ("av1-1-b10-00-quantizer-62", "10-bit/quantizer/av1-1-b10-00-quantizer-62.ivf"),
+    ("av1-1-b10-00-quantizer-63", "10-bit/quantizer/av1-1-b10-00-quantizer-63.ivf"),
+    ("test185_302", "10-bit/argon/test185_302.obu"),                  # Annex B, scaled refs
+    ("00000732", "12-bit/data/00000732.ivf", "00000732_12bit"),
+    ("00000736", "12-bit/data/00000736.ivf", "00000736_12bit"),
+    ("00000741", "12-bit/data/00000741.ivf", "00000741_12bit"),
+    ("test15240", "12-bit/argon/test15240.obu"),                      # 4:0:0, scaled refs
+    ("annexb", "8-bit/features/annexb.obu"),
+    ("section5", "8-bit/features/section5.obu"),
+]
+
+# the reference's --filmgrain 1 tests (explicit test() entries in the meson files: film grain
+# applied to the shown pictures before hashing)
+GRAIN = [
+    ("av1-1-b8-23-film_grain-50", "8-bit/film_grain/av1-1-b8-23-film_grain-50.ivf", "392a4adc567fa05b210eebe15bcbb491"),
+    ("ccvb_film_grain-fg", "8-bit/features/ccvb_film_grain.ivf", "a934b6263b7009746cce5f5bd33224f1"),
+    ("309_odd_width", "8-bit/issues/309_odd_width.ivf", "30d31f7c74575e58366898534a87841d"),
+    ("av1-1-b10-23-film_grain-50", "10-bit/film_grain/av1-1-b10-23-film_grain-50.ivf",
+     "be596f5921854b9a9a5be81c302a5327"),
+    ("test5606", "10-bit/argon/test5606.obu", "0888c66e9ad2f6ebc7f6d6fd8b464dd8"),
 ]
 
 if __name__ == "__main__":
@@ -36,5 +76,10 @@ if __name__ == "__main__":
         dst = rel.replace("/", "__")
         shutil.copyfile(os.path.join("/root/reference/tests/dav1d-test-data", rel), os.path.join(out, dst))
         table.append({"name": name, "file": dst, "md5": md5, "source": f"tests/dav1d-test-data/{rel}"})
+    for name, rel, md5 in GRAIN:
+        dst = rel.replace("/", "__")
+        shutil.copyfile(os.path.join("/root/reference/tests/dav1d-test-data", rel), os.path.join(out, dst))
+        table.append({"name": name, "file": dst, "md5": md5, "filmgrain": 1,
+                      "source": f"tests/dav1d-test-data/{rel} --filmgrain 1"})
     json.dump(table, open(os.path.join(out, "vectors.json"), "w"), indent=1)
     print(len(table), "vectors")
