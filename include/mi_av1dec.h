@@ -124,6 +124,10 @@ typedef struct MiFramePictures {
  * context must use one stream. 0 or -errno (-EINVAL malformed work list, -ENOMEM, -EIO). */
 int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int *final, void *stream);
 
+/* The host-side checks mi_frame_run applies before enqueuing anything, without a device: 0, or
+ * -EINVAL with *why (if non-NULL) naming the failed check. */
+int mi_frame_validate(const MiDecFrame *f, const MiFramePictures *pics, const char **why);
+
 /* Wait for the work enqueued on `stream` and report device-side failures of the frame(s):
  * 0; -EINVAL when a kernel rejected (skipped) a descriptor no valid stream produces; -EIO
  * when a block's dependency wait gave up or a block was never reconstructed (the pictures

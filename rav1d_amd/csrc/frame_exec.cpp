@@ -3,11 +3,13 @@
 //
 // The reference reconstructs a frame superblock row by superblock row, interleaving
 // decode_tile_sbrow and filter_sbrow (decode.rs:4526-4550; recon.rs:4019-4211). With the
-// whole frame's work list known up front the device runs it as four whole-frame stages on
-// one stream: intra reconstruction (one persistent launch over the blocks in dependency-level
-// order), deblocking recon -> deblocked, CDEF deblocked -> cdef, loop restoration
-// (cdef, deblocked) -> restored (out-of-place buffers stand in for the
-// reference's line backups).
+// whole frame's work list known up front the device runs it as whole-frame stages on one
+// stream: inter prediction of every inter block (MC, warp, scaled references, compound
+// combines, OBMC laps: they read only reference pictures) and the inter residuals, then intra
+// reconstruction (one persistent launch over the intra and inter-intra blocks in
+// dependency-level order), deblocking recon -> deblocked, CDEF deblocked -> cdef, loop
+// restoration (cdef, deblocked) -> restored (out-of-place buffers stand in for
+// the reference's line backups).
 //
 // The work list is validated on the host before anything is enqueued (-EINVAL, never a
 // device fault), then copied into one pinned staging blob and uploaded with a single async
@@ -45,69 +47,225 @@ int tx_of(int w, int h) {
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 struct Section {
-    const void *src;
+    const void *src;      // nullptr: device scratch, not uploaded (after every uploaded section)
     size_t bytes;
     size_t off;
 };
 
+int ilog2(int v) { return 31 - __builtin_clz((unsigned)v); }
+
+// MiMcBlock units bucketed as mi_mc_frame takes them: plane group (luma, chroma), then shape
+// class log2(w) * 8 + log2(h)
+void bucket_mc(const MiMcBlock *u, int n, std::vector<MiMcBlock> &out, uint32_t cs[2 * MI_MC_NCLASS + 1]) {
+    std::vector<uint32_t> cnt(2 * MI_MC_NCLASS + 1, 0);
+    auto key = [](const MiMcBlock &b) { return (b.plane ? MI_MC_NCLASS : 0) + ilog2(b.w) * 8 + ilog2(b.h); };
+    for (int i = 0; i < n; i++) cnt[key(u[i]) + 1]++;
+    for (int k = 0; k < 2 * MI_MC_NCLASS; k++) cnt[k + 1] += cnt[k];
+    for (int k = 0; k <= 2 * MI_MC_NCLASS; k++) cs[k] = cnt[k];
+    out.resize(n);
+    for (int i = 0; i < n; i++) out[cnt[key(u[i])]++] = u[i];
+}
+
+// the check a rejected work list failed (mi_frame_validate's `why`)
+thread_local const char *g_why = nullptr;
+#define STR2(x) #x
+#define STR(x) STR2(x)
+#define BAD() (g_why = "frame_exec.cpp:" STR(__LINE__), -EINVAL)
+#define BADF() (g_why = "frame_exec.cpp:" STR(__LINE__), false)
+
+bool pow2_in(int v, int lo, int hi) { return v >= lo && v <= hi && !(v & (v - 1)); }
+
+bool inter_present(const MiDecFrame *f) {
+    return f->n_mc || f->n_obmc_h || f->n_obmc_v || f->n_warp || f->n_scaled || f->n_combine_y || f->n_combine_uv;
+}
+
+// The reference pictures an inter frame's units read (same bit depth and layout, planes present)
+// and which of them differ in size from the frame (the scaled-reference path).
+int validate_refs(const MiDecFrame *f, const MiFramePictures *p, bool scaled[7]) {
+    for (int r = 0; r < 7; r++) {
+        const MiPicture &q = p->refs[r];
+        scaled[r] = false;
+        if (!q.data[0]) continue;
+        if (q.bpc != f->bpc || q.layout != f->layout || q.w <= 0 || q.h <= 0 || (f->layout && (!q.data[1] || !q.data[2])))
+            return BAD();
+        // svc scale factors (decode.rs:4776): 2x down to 1/16 x
+        if (2 * f->w < q.w || 2 * f->h < q.h || f->w > 16 * q.w || f->h > 16 * q.h) return BAD();
+        scaled[r] = q.w != f->w || q.h != f->h || q.stride[0] != p->recon.stride[0] || q.stride[1] != p->recon.stride[1];
+    }
+    return 0;
+}
+
+int validate_inter(const MiDecFrame *f, const MiFramePictures *p, const bool scaled[7]) {
+    const int ss_hor = f->layout == 1 || f->layout == 2, ss_ver = f->layout == 1;
+    const int nplanes = f->layout ? 3 : 1;
+    const int aw = (f->w + 127) & ~127, ah = (f->h + 127) & ~127;
+    auto ref_ok = [&](int r) { return r >= 0 && r < 7 && p->refs[r].data[0]; };
+    // a unit's rectangle, references, and the mask / tmp bytes it touches
+    auto unit_ok = [&](const MiMcBlock &u, bool allow_scaled, bool lap) {
+        if (u.plane >= nplanes || !pow2_in(u.w, 2, 128) || !pow2_in(u.h, 2, 128)) return BADF();
+        const int sh = u.plane ? ss_hor : 0, sv = u.plane ? ss_ver : 0;
+        if (u.x + u.w > (aw >> sh) || u.y + u.h > (ah >> sv)) return BADF();
+        if (u.filter2d > 9 || !ref_ok(u.ref[0]) || (!allow_scaled && scaled[u.ref[0]])) return BADF();
+        if (lap) return (u.comp == MI_MC_OBMC_H || u.comp == MI_MC_OBMC_V) && u.ref[1] < 0 &&
+                        (u.comp == MI_MC_OBMC_V || (u.param >= 2 && u.param <= u.h * 2 && u.param <= 64));
+        if (u.ref[1] >= 0) {
+            if (!ref_ok(u.ref[1]) || scaled[u.ref[1]] || u.comp > MI_MC_SEG) return BADF();
+            if (u.comp == MI_MC_MASK && (size_t)u.mask_off + (size_t)u.w * u.h > f->nmasks) return BADF();
+            if (u.comp == MI_MC_SEG) {
+                const int ms = f->layout ? ss_hor : 0, mv = f->layout ? ss_ver : 0;
+                if ((size_t)u.mask_off + (size_t)(u.w >> ms) * (u.h >> mv) > f->nmasks) return BADF();
+            }
+            if (u.comp == MI_MC_WAVG && (u.param & 31) > 16) return BADF();
+            return true;
+        }
+        if (u.comp == MI_MC_PREP) return (size_t)u.mask_off + (size_t)u.w * u.h <= f->ntmp;
+        return u.comp == 0;
+    };
+    struct L { const MiMcBlock *u; int n; bool scaled_ok, lap; };
+    const L lists[4] = { { f->mc, f->n_mc, false, false }, { f->scaled, f->n_scaled, true, false },
+                         { f->obmc_h, f->n_obmc_h, true, true }, { f->obmc_v, f->n_obmc_v, true, true } };
+    for (const L &l : lists) {
+        if (l.n < 0 || (l.n && !l.u)) return BAD();
+        for (int i = 0; i < l.n; i++) {
+            if (!unit_ok(l.u[i], l.scaled_ok, l.lap)) return BAD();
+            if (l.scaled_ok && !l.lap && (l.u[i].ref[1] >= 0 || (l.u[i].comp != 0 && l.u[i].comp != MI_MC_PREP)))
+                return BAD();
+        }
+    }
+    if (f->n_warp < 0 || (f->n_warp && !f->warp)) return BAD();
+    for (int i = 0; i < f->n_warp; i++) {
+        const MiWarpBlock &w = f->warp[i];
+        const int sh = w.plane ? ss_hor : 0, sv = w.plane ? ss_ver : 0;
+        if (w.plane >= nplanes || !ref_ok(w.ref) || scaled[w.ref] || w.prep > 1) return BAD();
+        if (w.x + 8 > (aw >> sh) || w.y + 8 > (ah >> sv)) return BAD();
+        // every filter phase warp8x8 forms (mx + y * beta + x * alpha over the 15 x 8 intermediate
+        // samples, my + y * delta + x * gamma over the 8 x 8 outputs) indexes the 193-entry table
+        auto phases_ok = [](int64_t m, int64_t sy, int ny, int64_t sx) {
+            for (int cy = 0; cy < 2; cy++)
+                for (int cx = 0; cx < 2; cx++) {
+                    const int64_t t = m + (cy ? ny : 0) * sy + (cx ? 7 : 0) * sx;
+                    const int64_t i = 64 + ((t + 512) >> 10);
+                    if (i < 0 || i > 192) return false;
+                }
+            return true;
+        };
+        if (!phases_ok(w.mx, w.abcd[1], 14, w.abcd[0]) || !phases_ok(w.my, w.abcd[3], 7, w.abcd[2])) return BAD();
+        if (w.prep && (w.tmp_stride < 8 || (size_t)w.tmp_off + (size_t)7 * w.tmp_stride + 8 > f->ntmp)) return BAD();
+    }
+    for (int k = 0; k < 2; k++) {
+        const MiMcCombine *c = k ? f->combine_uv : f->combine_y;
+        const int n = k ? f->n_combine_uv : f->n_combine_y;
+        if (n < 0 || (n && !c)) return BAD();
+        for (int i = 0; i < n; i++) {
+            const MiMcCombine &u = c[i];
+            const int sh = u.plane ? ss_hor : 0, sv = u.plane ? ss_ver : 0;
+            if (u.plane >= nplanes || (k == 0) != (u.plane == 0) || !pow2_in(u.w, 2, 128) || !pow2_in(u.h, 2, 128) ||
+                u.comp > MI_MC_SEG || u.x + u.w > (aw >> sh) || u.y + u.h > (ah >> sv))
+                return BAD();
+            for (int t = 0; t < 2; t++)
+                if ((size_t)u.tmp_off[t] + (size_t)u.w * u.h > f->ntmp) return BAD();
+            if (u.comp == MI_MC_MASK && (size_t)u.mask_off + (size_t)u.w * u.h > f->nmasks) return BAD();
+            if (u.comp == MI_MC_SEG) {
+                const int ms = f->layout ? ss_hor : 0, mv = f->layout ? ss_ver : 0;
+                if ((size_t)u.mask_off + (size_t)(u.w >> ms) * (u.h >> mv) > f->nmasks) return BAD();
+            }
+        }
+    }
+    if ((f->nmasks && !f->masks) || f->ntmp > ((size_t)1 << 28)) return BAD();
+    if (f->n_inter_tx < 0 || (f->n_inter_tx && !f->inter_tx)) return BAD();
+    for (int i = 0; i < f->n_inter_tx; i++) {
+        const MiTxBlock &t = f->inter_tx[i];
+        if (t.plane >= nplanes || t.tx >= MI_N_RECT_TX_SIZES || t.eob < 0 || !legal_txtp(t.tx, t.txtp)) return BAD();
+        const mi::TxDim d = mi::tx_dim(t.tx);
+        const int sh = t.plane ? ss_hor : 0, sv = t.plane ? ss_ver : 0;
+        if (t.x + d.w > (aw >> sh) || t.y + d.h > (ah >> sv)) return BAD();
+        if ((size_t)t.coef_off + (size_t)std::min(d.w, 32) * std::min(d.h, 32) > f->ncoef) return BAD();
+    }
+    return 0;
+}
+
 int validate(const MiDecFrame *f, const MiFramePictures *p) {
-    if (f->bpc != 8 && f->bpc != 10 && f->bpc != 12) return -EINVAL;
-    if (f->layout < 0 || f->layout > 3 || f->w <= 0 || f->h <= 0) return -EINVAL;
+    if (f->bpc != 8 && f->bpc != 10 && f->bpc != 12) return BAD();
+    if (f->layout < 0 || f->layout > 3 || f->w <= 0 || f->h <= 0) return BAD();
     // super-resolution (up_w > w): every picture has the upscaled geometry
-    if (f->up_w < f->w || f->up_w > 2 * f->w + 16) return -EINVAL;
+    if (f->up_w < f->w || f->up_w > 2 * f->w + 16) return BAD();
     const MiPicture *pics[4] = { &p->recon, &p->deblocked, &p->cdef, &p->restored };
     for (const MiPicture *q : pics)
         if (q->bpc != f->bpc || q->layout != f->layout || q->w != f->up_w || q->h != f->h || !q->data[0] ||
             (f->layout && (!q->data[1] || !q->data[2])) || q->stride[0] != p->recon.stride[0] ||
             q->stride[1] != p->recon.stride[1])
-            return -EINVAL;
+            return BAD();
     const int ss_hor = f->layout == 1 || f->layout == 2, ss_ver = f->layout == 1;
     const int nplanes = f->layout ? 3 : 1;
     const int aw = (f->w + 127) & ~127, ah = (f->h + 127) & ~127, aw_up = (f->up_w + 127) & ~127;
     const size_t pb = f->bpc == 8 ? 1 : 2;
     for (int pl = 0; pl < nplanes; pl++)
-        if ((size_t)std::abs(p->recon.stride[pl ? 1 : 0]) < (size_t)(aw_up >> (pl ? ss_hor : 0)) * pb) return -EINVAL;
-    if (f->n_intra < 0 || (f->n_intra && (!f->intra || !f->intra_tx || !f->dep_start))) return -EINVAL;
-    if (f->n_intra && f->ncoef < 16) return -EINVAL;
-    if (f->dep_start && (f->dep_start[0] != 0 || f->dep_start[f->n_intra] != f->n_deps)) return -EINVAL;
+        if ((size_t)std::abs(p->recon.stride[pl ? 1 : 0]) < (size_t)(aw_up >> (pl ? ss_hor : 0)) * pb) return BAD();
+    // every array a count refers to is present (they are copied from during the call)
+    if (f->n_intra < 0 || (f->n_intra && (!f->intra || !f->intra_tx || !f->dep_start))) return BAD();
+    if (f->n_deps < 0 || (f->n_deps && !f->deps) || (f->ncoef && !f->coef) || (f->nidx && !f->idx) ||
+        (f->npal && !f->pal))
+        return BAD();
+    if ((f->n_intra || f->n_inter_tx) && f->ncoef < 16) return BAD();
+    if (f->dep_start && (f->dep_start[0] != 0 || f->dep_start[f->n_intra] != f->n_deps)) return BAD();
+    const bool inter = inter_present(f);
     for (int i = 0; i < f->n_intra; i++) {
         const MiIntraBlock &b = f->intra[i];
         const MiTxBlock &t = f->intra_tx[i];
-        if (b.plane >= nplanes || t.plane != b.plane || t.x != b.x || t.y != b.y) return -EINVAL;
+        if (b.plane >= nplanes || t.plane != b.plane || t.x != b.x || t.y != b.y) return BAD();
         const int tx = tx_of(b.w, b.h);
-        if (tx < 0 || t.tx != tx) return -EINVAL;
+        if (tx < 0 || t.tx != tx) return BAD();
         const int sh = b.plane ? ss_hor : 0, sv = b.plane ? ss_ver : 0;
-        if (b.x + b.w > (aw >> sh) || b.y + b.h > (ah >> sv)) return -EINVAL;
+        if (b.x + b.w > (aw >> sh) || b.y + b.h > (ah >> sv)) return BAD();
         if (t.eob >= 0) {
-            if (!legal_txtp(tx, t.txtp)) return -EINVAL;
+            if (!legal_txtp(tx, t.txtp)) return BAD();
             const mi::TxDim d = mi::tx_dim(tx);
-            if ((size_t)t.coef_off + (size_t)std::min(d.w, 32) * std::min(d.h, 32) > f->ncoef) return -EINVAL;
-        } else if (t.coef_off + 16 > f->ncoef || t.txtp != 0) {
-            return -EINVAL;
+            if ((size_t)t.coef_off + (size_t)std::min(d.w, 32) * std::min(d.h, 32) > f->ncoef) return BAD();
+        } else if (t.coef_off + 16 > f->ncoef || (t.txtp != 0 && t.txtp != 16)) {
+            return BAD();
         }
-        const int mode = b.mode & ~MI_IPRED_II;
+        // edge availability: no left / top neighbour at the plane's first column / row; the
+        // tile limits inside the plane
+        if (((b.flags & MI_INTRA_HAVE_LEFT) && !b.x) || ((b.flags & MI_INTRA_HAVE_TOP) && !b.y)) return BAD();
+        if (b.mode != MI_INTRA_RESID && b.mode != MI_IPRED_PAL &&
+            (b.tile_w > (aw >> sh) || b.tile_h > (ah >> sv) || b.tile_w <= b.x || b.tile_h <= b.y))
+            return BAD();
+        const int mode = b.mode;
         if (mode == MI_IPRED_PAL) {
-            if ((size_t)b.aux_off + (size_t)b.w * b.h > f->nidx || (size_t)b.pal_off + 8 > f->npal) return -EINVAL;
+            if ((size_t)b.aux_off + (size_t)b.w * b.h > f->nidx || (size_t)b.pal_off + 8 > f->npal) return BAD();
         } else if (mode == MI_INTRA_IBC) {
             // the reference area the copy clamps its taps to lies inside the picture
-            if (b.filt_idx != (sh | (sv << 1)) || !b.max_w || !b.max_h || b.max_w > (aw >> sh) ||
-                b.max_h > (ah >> sv) || (b.mode & MI_IPRED_II))
-                return -EINVAL;
-        } else if (mode != MI_IPRED_CFL && mode > 13) {
-            return -EINVAL;
+            if (b.filt_idx != (sh | (sv << 1)) || !b.max_w || !b.max_h || b.max_w > (aw >> sh) || b.max_h > (ah >> sv))
+                return BAD();
+        } else if (mode == MI_IPRED_CFL) {
+            // CfL (chroma only; the executor has no ac array: the AC comes from the luma under
+            // the block) with padded sizes inside the block and the layout's subsampling
+            if (!(b.flags & MI_INTRA_CFL_AC) || !b.plane) return BAD();
+            const unsigned wp = b.reserved & 0xff, hp = (b.reserved >> 8) & 0xff;
+            if (((b.reserved >> 16) & 1) != (unsigned)ss_hor || ((b.reserved >> 17) & 1) != (unsigned)ss_ver ||
+                wp * 4 > b.w || hp * 4 > b.h || (b.reserved >> 18))
+                return BAD();
+        } else if (mode == 13) {
+            if (b.filt_idx >= 5 || b.w > 32 || b.h > 32) return BAD();   // filter intra: 5 taps sets, <= 32x32
+        } else if (mode >= 1 && mode <= 8) {
+            if (b.angle < -3 || b.angle > 3) return BAD();
+        } else if (mode != MI_INTRA_RESID && mode > 12) {
+            return BAD();
         }
-        if ((b.mode & MI_IPRED_II) || (b.flags & MI_INTRA_II)) return -EINVAL;   // inter-intra: inter frames
+        if (b.flags & MI_INTRA_II) {
+            // inter-intra: slots 0-12 with the blend mask in idx, in an inter frame
+            if (mode > 12 || (size_t)b.aux_off + (size_t)b.w * b.h > f->nidx || !inter) return BAD();
+        }
         for (int d = f->dep_start[i]; d < f->dep_start[i + 1]; d++)
-            if (d < 0 || d >= f->n_deps || f->deps[d] < 0 || f->deps[d] >= i) return -EINVAL;
-        if (f->dep_start[i + 1] < f->dep_start[i]) return -EINVAL;
+            if (d < 0 || d >= f->n_deps || f->deps[d] < 0 || f->deps[d] >= i) return BAD();
+        if (f->dep_start[i + 1] < f->dep_start[i]) return BAD();
     }
     const int sb128w = (f->w + 127) >> 7, sb128h = (f->h + 127) >> 7;
     if (f->filter_y && (!f->lf_level || !f->lf_masks || f->sb128w != sb128w || f->sb128h != sb128h ||
                         f->b4_stride < sb128w * 32))
-        return -EINVAL;
-    if (f->cdef_on && (!f->lf_masks || f->sb128w != sb128w || f->sb128h != sb128h)) return -EINVAL;
-    if (f->restore_planes && (!f->lr_mask || f->lr_sb128w != ((f->up_w + 127) >> 7))) return -EINVAL;
-    if (f->n_inter_tx) return -EINVAL;     // inter frames: not produced by the front-end yet
+        return BAD();
+    if (f->cdef_on && (!f->lf_masks || f->sb128w != sb128w || f->sb128h != sb128h)) return BAD();
+    if (f->restore_planes && (!f->lr_mask || f->lr_sb128w != ((f->up_w + 127) >> 7))) return BAD();
     return 0;
 }
 
@@ -141,10 +299,15 @@ int stage_upload(MiCtx *ctx, std::vector<Section> &secs, hipStream_t s) {
         if (hipMalloc((void **)&ctx->fx_dev, n) != hipSuccess) return -ENOMEM;
         ctx->fx_dev_bytes = n;
     }
+    size_t upload = 0;
     for (const Section &x : secs)
-        if (x.bytes) memcpy(ctx->fx_host + x.off, x.src, x.bytes);
+        if (x.bytes && x.src) {
+            memcpy(ctx->fx_host + x.off, x.src, x.bytes);
+            upload = std::max(upload, x.off + x.bytes);
+        }
     if (!ctx->fx_ev && hipEventCreateWithFlags(&ctx->fx_ev, hipEventDisableTiming) != hipSuccess) return -EIO;
-    if (hipMemcpyAsync(ctx->fx_dev, ctx->fx_host, total, hipMemcpyHostToDevice, s) != hipSuccess) return -EIO;
+    if (upload && hipMemcpyAsync(ctx->fx_dev, ctx->fx_host, upload, hipMemcpyHostToDevice, s) != hipSuccess)
+        return -EIO;
     if (hipEventRecord(ctx->fx_ev, s) != hipSuccess) return -EIO;
     ctx->fx_ev_pending = true;
     return 0;
@@ -192,6 +355,31 @@ int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, i
         }
         dep_start[n] = nd;
     }
+    // inter frames: the references, units bucketed for mi_mc_frame (OBMC laps split by whether
+    // their reference is scaled), residuals grouped by transform size for mi_itx_frame
+    const bool inter = inter_present(f) || f->n_inter_tx;
+    bool scaled[7] = {};
+    if (inter) {
+        if ((r = validate_refs(f, pics, scaled)) || (r = validate_inter(f, pics, scaled))) return ctx->last_error = r;
+    }
+    std::vector<MiMcBlock> mc_b, lap_b[2], lap_s[2];
+    uint32_t mc_cs[2 * MI_MC_NCLASS + 1], lap_cs[2][2 * MI_MC_NCLASS + 1];
+    bucket_mc(f->mc, f->n_mc, mc_b, mc_cs);
+    for (int k = 0; k < 2; k++) {
+        const MiMcBlock *u = k ? f->obmc_v : f->obmc_h;
+        std::vector<MiMcBlock> plain;
+        for (int i = 0; i < (k ? f->n_obmc_v : f->n_obmc_h); i++) (scaled[u[i].ref[0]] ? lap_s[k] : plain).push_back(u[i]);
+        bucket_mc(plain.data(), (int)plain.size(), lap_b[k], lap_cs[k]);
+    }
+    std::vector<MiTxBlock> itx_b(f->n_inter_tx);
+    uint32_t itx_ss[MI_N_RECT_TX_SIZES + 1] = {};
+    {
+        for (int i = 0; i < f->n_inter_tx; i++) itx_ss[f->inter_tx[i].tx + 1]++;
+        for (int t = 0; t < MI_N_RECT_TX_SIZES; t++) itx_ss[t + 1] += itx_ss[t];
+        uint32_t pos[MI_N_RECT_TX_SIZES];
+        memcpy(pos, itx_ss, sizeof(pos));
+        for (int i = 0; i < f->n_inter_tx; i++) itx_b[pos[f->inter_tx[i].tx]++] = f->inter_tx[i];
+    }
     const int sb128h = (f->h + 127) >> 7;
     std::vector<Section> secs = {
         { blocks.data(), blocks.size() * sizeof(MiIntraBlock), 0 },
@@ -204,10 +392,65 @@ int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, i
         { f->lf_level, f->filter_y ? (size_t)f->b4_stride * sb128h * 32 * 4 : 0, 0 },
         { f->lf_masks, (f->filter_y || f->cdef_on) ? (size_t)f->sb128w * sb128h * sizeof(MiAv1Filter) : 0, 0 },
         { f->lr_mask, f->restore_planes ? (size_t)f->lr_sb128w * sb128h * sizeof(MiAv1Restoration) : 0, 0 },
+        { mc_b.data(), mc_b.size() * sizeof(MiMcBlock), 0 },                       // 10
+        { lap_b[0].data(), lap_b[0].size() * sizeof(MiMcBlock), 0 },               // 11
+        { lap_s[0].data(), lap_s[0].size() * sizeof(MiMcBlock), 0 },               // 12
+        { lap_b[1].data(), lap_b[1].size() * sizeof(MiMcBlock), 0 },               // 13
+        { lap_s[1].data(), lap_s[1].size() * sizeof(MiMcBlock), 0 },               // 14
+        { f->warp, (size_t)f->n_warp * sizeof(MiWarpBlock), 0 },                  // 15
+        { f->scaled, (size_t)f->n_scaled * sizeof(MiMcBlock), 0 },                // 16
+        { f->combine_y, (size_t)f->n_combine_y * sizeof(MiMcCombine), 0 },        // 17
+        { f->combine_uv, (size_t)f->n_combine_uv * sizeof(MiMcCombine), 0 },      // 18
+        { f->masks, f->nmasks, 0 },                                                 // 19
+        { itx_b.data(), itx_b.size() * sizeof(MiTxBlock), 0 },                     // 20
+        { nullptr, f->ntmp * 2, 0 },                                                // 21: tmp arena
     };
     if ((r = stage_upload(ctx, secs, s))) return ctx->last_error = r;
     uint8_t *dev = ctx->fx_dev;
     auto D = [&](int i) -> void * { return secs[i].bytes ? dev + secs[i].off : nullptr; };
+
+    // 0. inter prediction (recon_b_inter's mc / warp_affine / compound / obmc calls over the
+    // whole frame: they read reference pictures only), then the inter residuals
+    if (inter) {
+        MiPicture cur = pics->recon;
+        cur.w = f->w;
+        MiPicture same[7], any[7];
+        for (int k = 0; k < 7; k++) {
+            // references the units never read (absent, or scaled for the same-size paths) are
+            // stood in for by the current picture: the entry points check every slot's geometry
+            const bool have = pics->refs[k].data[0] != nullptr;
+            same[k] = have && !scaled[k] ? pics->refs[k] : cur;
+            any[k] = have ? pics->refs[k] : cur;
+        }
+        uint8_t *masks = (uint8_t *)D(19);
+        int16_t *tmp = (int16_t *)D(21);
+        if (f->n_mc && (r = mi_mc_frame(ctx, &cur, same, 7, (const MiMcBlock *)D(10), mc_cs, masks, tmp, stream)))
+            return r;
+        if (f->n_warp && (r = mi_mc_warp(ctx, &cur, same, 7, (const MiWarpBlock *)D(15), f->n_warp, tmp, stream)))
+            return r;
+        if (f->n_scaled && (r = mi_mc_scaled(ctx, &cur, any, 7, (const MiMcBlock *)D(16), f->n_scaled, tmp, stream)))
+            return r;
+        // compounds with a warped / scaled side: luma, then chroma (a chroma MASK unit reads the
+        // mask its luma SEG unit wrote)
+        if (f->n_combine_y &&
+            (r = mi_mc_combine(ctx, &cur, (const MiMcCombine *)D(17), f->n_combine_y, tmp, masks, stream)))
+            return r;
+        if (f->n_combine_uv &&
+            (r = mi_mc_combine(ctx, &cur, (const MiMcCombine *)D(18), f->n_combine_uv, tmp, masks, stream)))
+            return r;
+        // obmc(): every above lap, then every left lap (recon.rs:2205-2309)
+        for (int k = 0; k < 2; k++) {
+            if (!lap_b[k].empty() &&
+                (r = mi_mc_frame(ctx, &cur, same, 7, (const MiMcBlock *)D(11 + 2 * k), lap_cs[k], masks, tmp, stream)))
+                return r;
+            if (!lap_s[k].empty() && (r = mi_mc_scaled(ctx, &cur, any, 7, (const MiMcBlock *)D(12 + 2 * k),
+                                                       (int)lap_s[k].size(), tmp, stream)))
+                return r;
+        }
+        if (f->n_inter_tx &&
+            (r = mi_itx_frame(ctx, &cur, (const MiTxBlock *)D(20), itx_ss, D(4), 0, stream)))
+            return r;
+    }
 
     // 1. intra reconstruction (prediction + residual per transform block)
     if (n) {
@@ -303,6 +546,19 @@ int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, i
     }
     *final = idx;
     return 0;
+}
+
+int mi_frame_validate(const MiDecFrame *f, const MiFramePictures *pics, const char **why) {
+    if (!f || !pics) return -EINVAL;
+    g_why = nullptr;
+    int r = validate(f, pics);
+    bool scaled[7] = {};
+    if (!r && (inter_present(f) || f->n_inter_tx)) {
+        r = validate_refs(f, pics, scaled);
+        if (!r) r = validate_inter(f, pics, scaled);
+    }
+    if (why) *why = r ? (g_why ? g_why : "?") : nullptr;
+    return r;
 }
 
 int mi_frame_end(MiCtx *ctx, void *stream) {

@@ -418,10 +418,12 @@ __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlo
         else return *q;
     };
     if constexpr (Fused) {
-        // inter-intra blends into the block's existing (inter) pixels: start the tile from them
-        if (ib.flags & MI_INTRA_II)
+        // inter-intra blends into the block's existing (inter) pixels, and the residual of an
+        // inter-intra block (MI_INTRA_RESID) adds to them: start the tile from them
+        if ((ib.flags & MI_INTRA_II) || ib.mode == MI_INTRA_RESID)
             for (int i = lane; i < w * h; i += 64) lt[i] = (Px)P(y + i / w, x + i % w);
     }
+    if (ib.mode == MI_INTRA_RESID) return;
     const int bd = a.bpc;
     if (ib.mode == MI_INTRA_IBC) {
         // intra block copy: bilinear put_bilin_c (mc_tmpl.c) from the already reconstructed

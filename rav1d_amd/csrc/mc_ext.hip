@@ -11,7 +11,8 @@
 // These paths are rare in streams (reference scaling, global/local warp, superres), so the
 // kernels favour one simple, divergence-free shape each over the main path's packing:
 //   scaled:  one 64-lane workgroup per unit, one lane per output pixel, the 8 intermediate
-//            rows it needs filtered in registers (8 x 8 taps + 8 taps);
+//            rows it needs filtered in registers (8 x 8 taps + 8 taps); also OBMC laps whose
+//            neighbour's reference is scaled (blended like mc_kernel's laps);
 //   warp:    four 8x8 blocks per 256-lane workgroup; the 15x15 window and the warp filter
 //            table staged in LDS, lane (r, c) filters intermediate rows r and r + 8, then
 //            output (r, c);
@@ -29,6 +30,9 @@ __constant__ int8_t k_warp[193][8] = {
 };
 __constant__ int8_t k_resize[64][8] = {
 #include "tables/resize_filter.inc"
+};
+__constant__ uint8_t k_obmc_s[64] = {
+#include "tables/obmc_masks.inc"
 };
 
 __device__ __forceinline__ int rnd2(int v, int sh) { return (v + ((1 << sh) >> 1)) >> sh; }
@@ -111,8 +115,19 @@ __global__ __launch_bounds__(64) void mc_scaled_kernel(McArgs a, const MiMcBlock
                 v = prep ? mid[3] - a.bias : min(max((mid[3] + ((1 << ib) >> 1)) >> ib, 0), a.bdmax);
             }
         }
-        if (prep) a.tmp[b.mask_off + i] = (int16_t)v;
-        else reinterpret_cast<Px *>(a.dst[p] + (int64_t)(b.y + y) * ds)[b.x + x] = (Px)v;
+        Px *d = reinterpret_cast<Px *>(a.dst[p] + (int64_t)(b.y + y) * ds) + b.x + x;
+        if (prep) {
+            a.tmp[b.mask_off + i] = (int16_t)v;
+        } else if (b.comp == MI_MC_OBMC_H || b.comp == MI_MC_OBMC_V) {
+            // an OBMC lap from a scaled reference, blended as blend_h / blend_v (mc_tmpl.c)
+            const bool above = b.comp == MI_MC_OBMC_H;
+            if (above ? y < ((b.param * 3) >> 2) : x < ((w * 3) >> 2)) {
+                const int m = k_obmc_s[above ? b.param + y : w + x];
+                *d = (Px)((*d * (64 - m) + v * m + 32) >> 6);
+            }
+        } else {
+            *d = (Px)v;
+        }
     }
 }
 

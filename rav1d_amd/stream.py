@@ -10,7 +10,7 @@ import ctypes
 
 from . import MiFramePictures, check, lib
 from . import frame as F
-from .av1dec import Av1Decoder, ivf_frames
+from .av1dec import Av1Decoder, stream_units
 
 
 class DevicePictureSet:
@@ -27,10 +27,15 @@ class DevicePictureSet:
         return self.frames[self.final]
 
 
-def run_frame(ctx, fr, stream=None):
+def run_frame(ctx, fr, stream=None, refs=None):
     """Enqueue one MiDecFrame on the device; returns its DevicePictureSet (output() = the
-    reference-quality picture once the stream reaches it)."""
+    reference-quality picture once the stream reaches it). refs: the frame's seven reference
+    pictures (Frame or None, in MiDecEvent.ref_pic order) for an inter frame."""
     ps = DevicePictureSet(fr.up_w, fr.h, fr.bpc, fr.layout)   # upscaled geometry with super-resolution
+    for i, r in enumerate(refs or []):
+        if r is not None:
+            ps.pics.refs[i] = r.picture()
+    ps.refs = [r for r in (refs or []) if r is not None]       # keep the reference tensors alive
     final = ctypes.c_int(-1)
     check(lib().mi_frame_run(ctx.h, ctypes.byref(fr), ctypes.byref(ps.pics), ctypes.byref(final),
                              F._stream_ptr(stream)), "mi_frame_run")
@@ -42,16 +47,24 @@ def frame_end(ctx, stream=None):
     check(lib().mi_frame_end(ctx.h, F._stream_ptr(stream)), "mi_frame_end")
 
 
+def _refs(pics, ev, key=lambda p: p):
+    """The reference pictures (final Frames) of an event's frame, in ref_pic order."""
+    out = []
+    for r in ev.ref_pic:
+        out.append(key(pics[r]).output() if r >= 0 and r in pics else None)
+    return out
+
+
 def decode_ivf(ctx, data, stream=None, sync_each=True):
-    """Decode an IVF stream on the device; yields the shown pictures (Frame, device planes) in
+    """Decode a stream (IVF, Annex B or section 5) on the device; yields the shown pictures (Frame, device planes) in
     output order. With sync_each, every frame is checked with mi_frame_end before it is shown."""
     dec = Av1Decoder()
     pics = {}
-    for tu in ivf_frames(data):
+    for tu in stream_units(data):
         dec.send(tu)
         for ev in dec.events():
             if ev.frame:
-                pics[ev.pic_id] = run_frame(ctx, ev.frame.contents, stream)
+                pics[ev.pic_id] = run_frame(ctx, ev.frame.contents, stream, _refs(pics, ev))
                 if sync_each:
                     frame_end(ctx, stream)
             if ev.show_pic >= 0:
@@ -129,7 +142,7 @@ def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=T
                     streams[li].wait_event(done_ev[r])
             # the pictures are allocated (and zero-filled) on the lane's own stream
             with torch.cuda.stream(streams[li]):
-                ps = run_frame(lctx, ev.frame.contents, lst)
+                ps = run_frame(lctx, ev.frame.contents, lst, _refs(pics, ev, key=lambda p: p[0]))
             pics[ev.pic_id] = (ps, li)
             e = torch.cuda.Event()
             e.record(streams[li])
@@ -146,7 +159,7 @@ def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=T
             if h is None or (h.pic.w, h.pic.h, h.pic.bpc, h.pic.layout) != (out.w, out.h, out.bpc, out.layout):
                 hosts[slot] = h = HostPicture(out.w, out.h, out.bpc, out.layout)
             fg = ev.fg if (ev.fg_present and apply_grain) else None
-            output_picture(lctx, out, h, fg, 0, lst)
+            output_picture(lctx, out, h, fg, ev.mtrx_identity, lst)
             done = torch.cuda.Event()
             done.record(streams[li])
             pending.append((slot, done))

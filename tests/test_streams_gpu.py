@@ -1,6 +1,8 @@
 """Reference MD5 vectors decoded on the MI355X: front-end work lists executed by
-librav1d_amd.so's frame executor (mi_frame_run: persistent intra reconstruction, deblocking,
-CDEF, loop restoration), shown pictures hashed as the md5 muxer does
+librav1d_amd.so's frame executor (mi_frame_run: inter prediction -- MC, OBMC, warp, scaled
+references, compound masks -- and inter residuals, persistent intra reconstruction incl.
+inter-intra, deblocking, CDEF, loop restoration; film grain at output for the --filmgrain 1
+vectors), shown pictures hashed as the md5 muxer does
 (tools/output/md5.rs:541-637). Expected MD5s are the reference's (tests/golden/streams)."""
 import hashlib
 import json
@@ -30,7 +32,16 @@ def gpu_md5(ctx, data):
 @pytest.mark.parametrize("v", VECTORS, ids=[v["name"] for v in VECTORS])
 def test_gpu_decode_matches_reference_md5(gpu, v):
     data = open(os.path.join(GOLDEN, v["file"]), "rb").read()
-    md5, n = gpu_md5(gpu, data)
+    if v.get("filmgrain"):
+        # --filmgrain 1: the grain is applied on the device as the picture is output
+        from rav1d_amd.output import Muxer
+        from rav1d_amd.stream import decode_to_muxer
+        m = Muxer("md5")
+        n = decode_to_muxer(gpu, data, m, apply_grain=True, pipelined=False)
+        md5 = m.digest()
+        m.close()
+    else:
+        md5, n = gpu_md5(gpu, data)
     assert n > 0
     assert md5 == v["md5"], f"{v['name']}: {n} frames, md5 {md5} != {v['md5']}"
 
