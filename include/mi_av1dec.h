@@ -135,6 +135,24 @@ int mi_frame_validate(const MiDecFrame *f, const MiFramePictures *pics, const ch
  * src/error.rs). */
 int mi_frame_end(MiCtx *ctx, void *stream);
 
+/* Per-stage timing of mi_frame_run on one context (the §8(d) breakdown of a stream decode).
+ * With timing on, every mi_frame_run records five HIP events on its stream; mi_ctx_timing
+ * waits for them, sums the stages over the frames run since the last read, and resets.
+ * Timing adds no synchronisation to mi_frame_run itself. */
+typedef struct MiFrameTiming {
+    int32_t frames;        /* frames run since the last read */
+    int32_t reserved;
+    double host_ms;        /* host time inside mi_frame_run: checks, dependency-level sort,
+                              bucketing, staging copy (and any wait for the staging buffer) */
+    double upload_ms;      /* device time of the descriptor + coefficient upload (H2D) */
+    double inter_ms;       /* MC, warp, scaled, combine, OBMC laps, inter residuals */
+    double intra_ms;       /* the persistent intra reconstruction launch */
+    double filter_ms;      /* deblock, CDEF, super-resolution, loop restoration */
+    int64_t upload_bytes;  /* bytes uploaded */
+} MiFrameTiming;
+int mi_ctx_set_timing(MiCtx *ctx, int on);
+int mi_ctx_timing(MiCtx *ctx, MiFrameTiming *out);
+
 typedef struct MiDec MiDec;
 
 int  mi_dec_create(MiDec **out);
@@ -145,6 +163,18 @@ void mi_dec_destroy(MiDec *d);
  * that wants the overlap sends a few temporal units ahead before draining. A worker's failure
  * is returned by the mi_dec_next of its frame. Default 1 (synchronous). 0 or -EINVAL. */
 int  mi_dec_set_threads(MiDec *d, int n);
+/* Dav1dSettings.inloop_filters (include/dav1d/dav1d.rs:17-35, src/lib.rs:136,218; the CLI's
+ * --inloopfilters): the in-loop filters the frames this decoder emits ask mi_frame_run to
+ * apply. A filter left out is skipped as rav1d's filter_sbrow_* skip it (recon.rs:4054, 4162,
+ * 4178, 4290): the frame's filter_y / cdef_on / restore_planes are cleared, super-resolution
+ * still runs, and the unfiltered picture is the reference later frames predict from. The bit
+ * values are rav1d's. Default MI_INLOOPFILTER_ALL. 0 or -EINVAL. */
+#define MI_INLOOPFILTER_NONE 0
+#define MI_INLOOPFILTER_DEBLOCK (1 << 1)
+#define MI_INLOOPFILTER_CDEF (1 << 2)
+#define MI_INLOOPFILTER_RESTORATION (1 << 3)
+#define MI_INLOOPFILTER_ALL (MI_INLOOPFILTER_DEBLOCK | MI_INLOOPFILTER_CDEF | MI_INLOOPFILTER_RESTORATION)
+int  mi_dec_set_inloop_filters(MiDec *d, int flags);
 /* Feed one temporal unit (any whole number of OBUs). */
 int  mi_dec_send(MiDec *d, const uint8_t *data, size_t size);
 /* Next event: 1 and *ev filled, 0 when none is pending, or -errno. */

@@ -34,6 +34,13 @@ class MiFramePictures(ctypes.Structure):
     _fields_ = [("pics", MiPicture * 4), ("refs", MiPicture * 7)]
 
 
+class MiFrameTiming(ctypes.Structure):
+    """include/mi_av1dec.h: per-stage timing of mi_frame_run (mi_ctx_set_timing / mi_ctx_timing)."""
+    _fields_ = [("frames", ctypes.c_int32), ("reserved", ctypes.c_int32), ("host_ms", ctypes.c_double),
+                ("upload_ms", ctypes.c_double), ("inter_ms", ctypes.c_double), ("intra_ms", ctypes.c_double),
+                ("filter_ms", ctypes.c_double), ("upload_bytes", ctypes.c_int64)]
+
+
 class MiIntraFrame(ctypes.Structure):
     _fields_ = [("pic", MiPicture), ("blocks", ctypes.c_void_p), ("tx", ctypes.c_void_p),
                 ("dep_start", ctypes.c_void_p), ("deps", ctypes.c_void_p), ("ac", ctypes.c_void_p),
@@ -189,6 +196,8 @@ def lib():
     _sig(L, "mi_frame_run", ctypes.c_int, [_VP, _VP, ctypes.POINTER(MiFramePictures), ctypes.POINTER(ctypes.c_int), _VP])
     _sig(L, "mi_frame_end", ctypes.c_int, [_VP, _VP])
     _sig(L, "mi_frame_validate", ctypes.c_int, [_VP, ctypes.POINTER(MiFramePictures), ctypes.POINTER(ctypes.c_char_p)])
+    _sig(L, "mi_ctx_set_timing", ctypes.c_int, [_VP, ctypes.c_int])
+    _sig(L, "mi_ctx_timing", ctypes.c_int, [_VP, ctypes.POINTER(MiFrameTiming)])
     # output side (include/mi_av1out.h)
     _sig(L, "mi_host_picture_alloc", ctypes.c_int, [_I, _I, _I, _I, ctypes.POINTER(MiPicture)])
     _sig(L, "mi_host_picture_free", None, [ctypes.POINTER(MiPicture)])
@@ -203,6 +212,7 @@ EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error"
             "mi_itx_frame", "mi_mc_frame", "mi_mc_frame_ex", "mi_mc_scaled", "mi_mc_warp", "mi_mc_combine", "mi_superres_frame",
             "mi_ipred_blocks", "mi_intra_blocks", "mi_intra_recon", "mi_ctx_device_status", "mi_deblock_frame", "mi_deblock_frame_to", "mi_cdef_frame", "mi_lr_frame",
             "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply", "mi_frame_run", "mi_frame_end", "mi_frame_validate",
+            "mi_ctx_set_timing", "mi_ctx_timing",
             "mi_dsp_itxfm_add", "mi_dsp_intra_pred", "mi_dsp_cfl_pred", "mi_dsp_pal_pred", "mi_dsp_cfl_ac",
             "mi_dsp_loop_filter_sb", "mi_dsp_cdef_filter", "mi_dsp_cdef_dir", "mi_dsp_mc_put", "mi_dsp_mc_prep",
             "mi_dsp_mc_avg", "mi_dsp_mc_w_avg", "mi_dsp_mc_mask", "mi_dsp_mc_w_mask", "mi_dsp_mc_blend",

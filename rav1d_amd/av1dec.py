@@ -67,6 +67,7 @@ def dec_lib():
         d.mi_dec_send.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
         d.mi_dec_next.argtypes = [ctypes.c_void_p, ctypes.POINTER(MiDecEvent)]
         d.mi_dec_set_threads.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        d.mi_dec_set_inloop_filters.argtypes = [ctypes.c_void_p, ctypes.c_int]
         d.mi_dec_error.argtypes = [ctypes.c_void_p]
         d.mi_dec_error.restype = ctypes.c_char_p
         _dec = d
@@ -168,12 +169,21 @@ def stream_units(data):
     return section5_units(data)
 
 
+# Dav1dSettings.inloop_filters bits (include/dav1d/dav1d.rs:28-35; include/mi_av1dec.h)
+INLOOPFILTER_NONE, INLOOPFILTER_DEBLOCK, INLOOPFILTER_CDEF, INLOOPFILTER_RESTORATION = 0, 2, 4, 8
+INLOOPFILTER_ALL = INLOOPFILTER_DEBLOCK | INLOOPFILTER_CDEF | INLOOPFILTER_RESTORATION
+# the CLI's --inloopfilters values (inloop_filters_tbl, tools/dav1d_cli_parse.rs:479-530)
+INLOOPFILTER_NAMES = {"none": 0, "deblock": 2, "nodeblock": 12, "cdef": 4, "nocdef": 10,
+                      "restoration": 8, "norestoration": 6, "all": 14}
+
+
 class Av1Decoder:
     """One stream. send() one temporal unit, then drain events()."""
 
-    def __init__(self, threads=1):
+    def __init__(self, threads=1, inloop_filters=INLOOPFILTER_ALL):
         """threads > 1: intra frames are decoded on that many worker threads (mi_dec_set_threads);
-        send a few temporal units ahead of draining events() to overlap them."""
+        send a few temporal units ahead of draining events() to overlap them. inloop_filters:
+        Dav1dSettings.inloop_filters (an int of INLOOPFILTER_* bits or a CLI name)."""
         self.lib = dec_lib()
         self.h = ctypes.c_void_p()
         r = self.lib.mi_dec_create(ctypes.byref(self.h))
@@ -181,6 +191,12 @@ class Av1Decoder:
             raise RuntimeError(f"mi_dec_create: {r}")
         if threads > 1:
             self.lib.mi_dec_set_threads(self.h, threads)
+        if isinstance(inloop_filters, str):
+            inloop_filters = INLOOPFILTER_NAMES[inloop_filters]
+        if inloop_filters != INLOOPFILTER_ALL:
+            r = self.lib.mi_dec_set_inloop_filters(self.h, int(inloop_filters))
+            if r:
+                raise ValueError(f"mi_dec_set_inloop_filters({inloop_filters}): {r}")
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -207,12 +223,12 @@ class Av1Decoder:
             yield ev
 
 
-def stream_events(data, threads=1, lookahead=None):
+def stream_events(data, threads=1, lookahead=None, inloop_filters=INLOOPFILTER_ALL):
     """Decoder events of a stream (IVF, Annex B or section 5) in decode order. With threads > 1 the front-end keeps
     `lookahead` (default 2 * threads) temporal units ahead of the events handed out, so that
     frames decode on the worker threads while the caller consumes earlier ones. Each event is
     valid until the next one is requested."""
-    dec = Av1Decoder(threads)
+    dec = Av1Decoder(threads, inloop_filters)
     la = 0 if threads <= 1 else (lookahead if lookahead is not None else 2 * threads)
     sent = 0
     for tu in stream_units(data):

@@ -67,12 +67,16 @@ struct CallState {
 };
 CallState g_call;
 
-// The context's device words ([0..63] queue heads, [64] dependency-wait give-up, [65]
-// rejected descriptors, [72..79] XCD worker ranks), allocated zeroed on first use.
-int ctx_words(MiCtx *c) {
+// The context's device words ([0..63] queue heads, [64] dependency-wait give-up / untaken
+// blocks, [65] rejected descriptors, [72..79] XCD worker ranks), allocated zeroed on first use.
+// Zeroed on the context's own stream: a null-stream hipMemset is not ordered with a
+// non-blocking stream and may land after (or during) the first kernel that uses the words --
+// with two contexts whose streams overlap, it reset the queue heads of a running persistent
+// intra launch, which then re-ran blocks whose coefficients it had already consumed.
+int ctx_words(MiCtx *c, hipStream_t s) {
     if (c->ir_words) return 0;
     if (hipMalloc(&c->ir_words, 128 * sizeof(int)) != hipSuccess) return -ENOMEM;
-    if (hipMemset(c->ir_words, 0, 128 * sizeof(int)) != hipSuccess) return -EIO;
+    if (hipMemsetAsync(c->ir_words, 0, 128 * sizeof(int), s) != hipSuccess) return -EIO;
     return 0;
 }
 
@@ -125,7 +129,7 @@ int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
             a.ph[p] = p ? ah >> sv : ah;
         }
     }
-    if (int e = ctx_words(ctx)) return fail(ctx, e);
+    if (int e = ctx_words(ctx, (hipStream_t)stream)) return fail(ctx, e);
     a.err = ctx->ir_words + 65;
     for (int k = 0; k < MI_N_RECT_TX_SIZES; k++)
         if (size_start[k + 1] < size_start[k]) return fail(ctx, -EINVAL);
@@ -343,7 +347,7 @@ int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned
             return fail(ctx, -EINVAL);
         total += (size_t)fr.n;
     }
-    if (int e = ctx_words(ctx)) return fail(ctx, e);
+    if (int e = ctx_words(ctx, (hipStream_t)stream)) return fail(ctx, e);
     if (total > ctx->ir_done_n) {
         // an earlier launch on this context's stream may still poll the old flags
         if (ctx->ir_done && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(ctx, -EIO);
@@ -351,7 +355,9 @@ int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned
         ctx->ir_done = nullptr;
         ctx->ir_done_n = 0;
         if (hipMalloc(&ctx->ir_done, total * sizeof(uint32_t)) != hipSuccess) return fail(ctx, -ENOMEM);
-        if (hipMemset(ctx->ir_done, 0, total * sizeof(uint32_t)) != hipSuccess) return fail(ctx, -EIO);
+        // stream-ordered, as ctx_words
+        if (hipMemsetAsync(ctx->ir_done, 0, total * sizeof(uint32_t), (hipStream_t)stream) != hipSuccess)
+            return fail(ctx, -EIO);
         ctx->ir_done_n = total;
         ctx->ir_epoch = 0;
     }
@@ -412,8 +418,6 @@ int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned
     // L2-served): observed as wrong pixels with two frames in flight. Off: one XCD per frame.
     static const int spread_env = getenv("MI_IR_SPREAD") ? atoi(getenv("MI_IR_SPREAD")) : 0;
     a.spread = spread_env && nframes < 8;
-    ctx->ir_last_frames = nframes;
-    for (int f = 0; f < nframes; f++) ctx->ir_last_n[f] = frames[f].n;
     // one-wave workers per XCD (occupancy allows 3 per SIMD = 384 per XCD): 128, plus 64 per
     // extra frame the XCD serves
     const int per_xcd = (nframes + 7) / 8;
@@ -429,20 +433,22 @@ int mi_ctx_device_status(MiCtx *ctx, void *stream) {
     int w[66];
     if (hipMemcpy(w, ctx->ir_words, sizeof(w), hipMemcpyDeviceToHost) != hipSuccess) return fail(ctx, -EIO);
     if (w[65]) {   // a kernel rejected (skipped) descriptors
-        (void)hipMemset(ctx->ir_words + 65, 0, sizeof(int));
+        if (hipMemsetAsync(ctx->ir_words + 65, 0, sizeof(int), (hipStream_t)stream) != hipSuccess ||
+            hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+            return fail(ctx, -EIO);
         return fail(ctx, -EINVAL);
     }
     if (getenv("MI_DEBUG"))
         fprintf(stderr, "mi_ctx_device_status: heads %d %d %d %d %d %d %d %d err %d\n", w[0], w[1], w[2], w[3], w[4],
                 w[5], w[6], w[7], w[64]);
+    // [64]: bit 0 a dependency wait gave up, bit 2 a launch left blocks untaken (a frame
+    // whose XCD received no workgroup): set on the device by every launch, sticky until read
     if (w[64]) {
-        (void)hipMemset(ctx->ir_words + 64, 0, sizeof(int));
-        return fail(ctx, -ETIMEDOUT);
+        if (hipMemsetAsync(ctx->ir_words + 64, 0, sizeof(int), (hipStream_t)stream) != hipSuccess ||
+            hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+            return fail(ctx, -EIO);
+        return fail(ctx, (w[64] & 1) ? -ETIMEDOUT : -EIO);
     }
-    // every block of the last launch was taken by a worker (a frame whose XCD received no
-    // workgroup would be left untouched)
-    for (int f = 0; f < ctx->ir_last_frames; f++)
-        if (w[f] < ctx->ir_last_n[f]) return fail(ctx, -EIO);
     return 0;
 }
 

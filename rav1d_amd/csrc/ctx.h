@@ -3,6 +3,8 @@
 #pragma once
 #include "common.h"
 
+#include <vector>
+
 struct MiCtx {
     int device = 0;
     int last_error = 0;
@@ -16,14 +18,28 @@ struct MiCtx {
     size_t ir_done_n = 0;
     int *ir_words = nullptr;      // [0..63] queue heads, [64] error, [72..79] XCD worker ranks
     uint32_t ir_epoch = 0;
-    int ir_last_n[mi::kIrMaxFrames] = {0}, ir_last_frames = 0;
     // frame executor (frame_exec.cpp): device copy of one frame's descriptors, staged through
     // pinned host memory; `fx_ev` marks when the staging buffer may be rewritten
     uint8_t *fx_dev = nullptr, *fx_host = nullptr;
     size_t fx_dev_bytes = 0, fx_host_bytes = 0;
     hipEvent_t fx_ev = nullptr;
     bool fx_ev_pending = false;
+    // per-stage timing of mi_frame_run (mi_ctx_set_timing): 5 events per frame (before the
+    // upload, after it, after inter prediction + residuals, after intra, at the end)
+    bool tm_on = false;
+    std::vector<hipEvent_t> tm_ev;
+    double tm_host_ms = 0;
+    int64_t tm_bytes = 0;
+    int tm_frames = 0;
+    void tm_clear() {
+        for (hipEvent_t e : tm_ev) (void)hipEventDestroy(e);
+        tm_ev.clear();
+        tm_host_ms = 0;
+        tm_bytes = 0;
+        tm_frames = 0;
+    }
     ~MiCtx() {
+        tm_clear();
         if (fx_ev) (void)hipEventDestroy(fx_ev);
         if (fx_dev) (void)hipFree(fx_dev);
         if (fx_host) (void)hipHostFree(fx_host);

@@ -17,6 +17,7 @@
 #include <errno.h>
 #include <string.h>
 #include <algorithm>
+#include <chrono>
 #include <vector>
 
 #include "ctx.h"
@@ -269,7 +270,8 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
     return 0;
 }
 
-int stage_upload(MiCtx *ctx, std::vector<Section> &secs, hipStream_t s) {
+int stage_upload(MiCtx *ctx, std::vector<Section> &secs, hipStream_t s, hipEvent_t before = nullptr,
+                 int64_t *bytes = nullptr) {
     size_t total = 0;
     for (Section &x : secs) {
         x.off = total;
@@ -306,6 +308,8 @@ int stage_upload(MiCtx *ctx, std::vector<Section> &secs, hipStream_t s) {
             upload = std::max(upload, x.off + x.bytes);
         }
     if (!ctx->fx_ev && hipEventCreateWithFlags(&ctx->fx_ev, hipEventDisableTiming) != hipSuccess) return -EIO;
+    if (before && hipEventRecord(before, s) != hipSuccess) return -EIO;
+    if (bytes) *bytes = (int64_t)upload;
     if (upload && hipMemcpyAsync(ctx->fx_dev, ctx->fx_host, upload, hipMemcpyHostToDevice, s) != hipSuccess)
         return -EIO;
     if (hipEventRecord(ctx->fx_ev, s) != hipSuccess) return -EIO;
@@ -315,10 +319,95 @@ int stage_upload(MiCtx *ctx, std::vector<Section> &secs, hipStream_t s) {
 
 } // namespace
 
+namespace {
+
+// the five stage events of one timed frame (mi_ctx_set_timing); released unless committed
+struct StageEvents {
+    hipEvent_t ev[5] = {};
+    bool on = false;
+    explicit StageEvents(bool timing) : on(timing) {
+        if (on)
+            for (hipEvent_t &e : ev)
+                if (hipEventCreate(&e) != hipSuccess) e = nullptr;
+    }
+    void mark(int k, hipStream_t s) {
+        if (ev[k]) (void)hipEventRecord(ev[k], s);
+    }
+    ~StageEvents() {
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+};
+
+int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int *final, void *stream,
+              StageEvents &tev, int64_t *bytes);
+
+}  // namespace
+
 extern "C" {
 
 int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int *final, void *stream) {
     if (!ctx || !f || !pics || !final) return -EINVAL;
+    const auto t0 = std::chrono::steady_clock::now();
+    StageEvents tev(ctx->tm_on);
+    int64_t bytes = 0;
+    const int r = frame_run(ctx, f, pics, final, stream, tev, &bytes);
+    if (r == 0 && ctx->tm_on) {
+        bool all = true;
+        for (hipEvent_t e : tev.ev) all = all && e;
+        if (all) {
+            for (hipEvent_t &e : tev.ev) {
+                ctx->tm_ev.push_back(e);
+                e = nullptr;
+            }
+            ctx->tm_frames++;
+            ctx->tm_bytes += bytes;
+            ctx->tm_host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        }
+    }
+    return r;
+}
+
+int mi_ctx_set_timing(MiCtx *ctx, int on) {
+    if (!ctx) return -EINVAL;
+    ctx->tm_clear();
+    ctx->tm_on = on != 0;
+    return 0;
+}
+
+int mi_ctx_timing(MiCtx *ctx, MiFrameTiming *out) {
+    if (!ctx || !out) return -EINVAL;
+    memset(out, 0, sizeof(*out));
+    double st[4] = {0, 0, 0, 0};
+    for (size_t i = 0; i + 5 <= ctx->tm_ev.size(); i += 5) {
+        if (hipEventSynchronize(ctx->tm_ev[i + 4]) != hipSuccess) {
+            ctx->tm_clear();
+            return -EIO;
+        }
+        for (int k = 0; k < 4; k++) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, ctx->tm_ev[i + k], ctx->tm_ev[i + k + 1]) == hipSuccess) st[k] += ms;
+        }
+    }
+    out->frames = ctx->tm_frames;
+    out->host_ms = ctx->tm_host_ms;
+    out->upload_ms = st[0];
+    out->inter_ms = st[1];
+    out->intra_ms = st[2];
+    out->filter_ms = st[3];
+    out->upload_bytes = ctx->tm_bytes;
+    const bool on = ctx->tm_on;
+    ctx->tm_clear();
+    ctx->tm_on = on;
+    return 0;
+}
+
+}  // extern "C"
+
+namespace {
+
+int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int *final, void *stream,
+              StageEvents &tev, int64_t *bytes) {
     int r = validate(f, pics);
     if (r) return ctx->last_error = r;
     hipStream_t s = (hipStream_t)stream;
@@ -405,7 +494,8 @@ int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, i
         { itx_b.data(), itx_b.size() * sizeof(MiTxBlock), 0 },                     // 20
         { nullptr, f->ntmp * 2, 0 },                                                // 21: tmp arena
     };
-    if ((r = stage_upload(ctx, secs, s))) return ctx->last_error = r;
+    if ((r = stage_upload(ctx, secs, s, tev.ev[0], bytes))) return ctx->last_error = r;
+    tev.mark(1, s);
     uint8_t *dev = ctx->fx_dev;
     auto D = [&](int i) -> void * { return secs[i].bytes ? dev + secs[i].off : nullptr; };
 
@@ -452,6 +542,7 @@ int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, i
             return r;
     }
 
+    tev.mark(2, s);
     // 1. intra reconstruction (prediction + residual per transform block)
     if (n) {
         MiIntraFrame fr;
@@ -468,6 +559,7 @@ int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, i
         fr.n = n;
         if ((r = mi_intra_recon(ctx, &fr, 1, 0, stream))) return r;
     }
+    tev.mark(3, s);
     // the coded-width views of the pictures (stages before super-resolution)
     MiPicture cp[4] = { pics->recon, pics->deblocked, pics->cdef, pics->restored };
     for (MiPicture &q : cp) q.w = f->w;
@@ -544,9 +636,14 @@ int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, i
         if ((r = mi_lr_frame(ctx, cur, deblocked, slot[out], &lr, stream))) return r;
         idx = out;
     }
+    tev.mark(4, s);
     *final = idx;
     return 0;
 }
+
+}  // namespace
+
+extern "C" {
 
 int mi_frame_validate(const MiDecFrame *f, const MiFramePictures *pics, const char **why) {
     if (!f || !pics) return -EINVAL;

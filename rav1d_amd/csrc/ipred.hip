@@ -817,11 +817,21 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
     }
 }
 
+// After the persistent launch, in stream order: every frame's queue head must have passed its
+// block count (a frame whose XCD received no workgroup would be left untouched). Sets bit 2 of
+// the sticky error word mi_frame_end reports, so a failure of any launch is seen, not only of
+// the last one.
+__global__ __launch_bounds__(64) void intra_recon_check_kernel(IntraReconArgs a) {
+    const int f = threadIdx.x;
+    if (f < a.nframes && *a.fr[f].head < a.fr[f].n) atomicOr(a.err, 4);
+}
+
 int launch_intra_recon(const IntraReconArgs &a, int bpc, int wg_per_xcd, hipStream_t s) {
     const int n = 8 * wg_per_xcd;
     if (bpc == 8) intra_recon_kernel<uint8_t, int16_t, int16_t, false><<<n, 64, 0, s>>>(a);
     else if (bpc == 10) intra_recon_kernel<uint16_t, int32_t, int16_t, false><<<n, 64, 0, s>>>(a);
     else intra_recon_kernel<uint16_t, int32_t, int32_t, true><<<n, 64, 0, s>>>(a);
+    intra_recon_check_kernel<<<1, 64, 0, s>>>(a);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -11,6 +11,7 @@ struct MiDec {
     MiDecFrame frame;
     std::vector<int32_t> release;
     std::string err;
+    int inloop = MI_INLOOPFILTER_ALL;
 };
 
 extern "C" {
@@ -28,6 +29,12 @@ void mi_dec_destroy(MiDec *d) { delete d; }
 int mi_dec_set_threads(MiDec *d, int n) {
     if (!d || n < 1) return -EINVAL;
     d->dec.set_threads(n);
+    return 0;
+}
+
+int mi_dec_set_inloop_filters(MiDec *d, int flags) {
+    if (!d || (flags & ~MI_INLOOPFILTER_ALL)) return -EINVAL;
+    d->inloop = flags;
     return 0;
 }
 
@@ -100,8 +107,10 @@ int mi_dec_next(MiDec *d, MiDecEvent *ev) {
         f.nidx = w.idx.size();
         f.pal = w.pal.data();
         f.npal = w.pal.size() / (w.bpc == 8 ? 1 : 2);
-        f.filter_y = w.filter_y;
-        f.filter_uv = w.filter_uv;
+        // Dav1dSettings.inloop_filters: a filter switched off is skipped for the whole frame
+        const bool dbl = d->inloop & MI_INLOOPFILTER_DEBLOCK;
+        f.filter_y = dbl ? w.filter_y : 0;
+        f.filter_uv = dbl ? w.filter_uv : 0;
         f.lf_level = w.lf_level.data();
         f.b4_stride = w.b4_stride;
         f.lf_masks = w.lf_masks.data();
@@ -109,13 +118,13 @@ int mi_dec_next(MiDec *d, MiDecEvent *ev) {
         f.sb128h = w.sb128h;
         memcpy(f.lim_e, w.lim_e, 64);
         memcpy(f.lim_i, w.lim_i, 64);
-        f.cdef_on = w.cdef_on;
+        f.cdef_on = (d->inloop & MI_INLOOPFILTER_CDEF) ? w.cdef_on : 0;
         f.cdef_damping = w.cdef_damping;
         memcpy(f.cdef_y, w.cdef_y, 8);
         memcpy(f.cdef_uv, w.cdef_uv, 8);
         f.lr_mask = w.lr_mask.data();
         f.lr_sb128w = w.sr_sb128w;
-        f.restore_planes = w.restore_planes;
+        f.restore_planes = (d->inloop & MI_INLOOPFILTER_RESTORATION) ? w.restore_planes : 0;
         f.lr_unit_size[0] = w.lr_unit_size[0];
         f.lr_unit_size[1] = w.lr_unit_size[1];
         f.mc = w.mc.data();

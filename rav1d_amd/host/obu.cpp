@@ -205,7 +205,7 @@ int Decoder::parse_frame_hdr(Bits &gb, FrameHdr &h) {
         }
         return 0;
     }
-    h.frame_type = s.reduced_still ? FRAME_KEY : gb.bits(2);
+    h.frame_type = s.reduced_still ? (int)FRAME_KEY : (int)gb.bits(2);
     h.show_frame = s.reduced_still || gb.bit();
     if (h.show_frame) {
         if (s.decoder_model_info_present && !s.equal_picture_interval) gb.bits(s.frame_presentation_delay_len);
@@ -315,7 +315,7 @@ int Decoder::parse_frame_hdr(Bits &gb, FrameHdr &h) {
         }
         if (read_frame_size(gb, h, !h.error_resilient && h.frame_size_override) < 0) return -EINVAL;
         h.hp = !h.force_integer_mv && gb.bit();
-        h.subpel_filter_mode = gb.bit() ? FILTER_SWITCHABLE : gb.bits(2);
+        h.subpel_filter_mode = gb.bit() ? (int)FILTER_SWITCHABLE : (int)gb.bits(2);
         h.switchable_motion_mode = gb.bit();
         h.use_ref_frame_mvs = !h.error_resilient && s.ref_frame_mvs && s.order_hint && gb.bit();
     }

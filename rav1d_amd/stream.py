@@ -55,10 +55,11 @@ def _refs(pics, ev, key=lambda p: p):
     return out
 
 
-def decode_ivf(ctx, data, stream=None, sync_each=True):
+def decode_ivf(ctx, data, stream=None, sync_each=True, inloop_filters=14):
     """Decode a stream (IVF, Annex B or section 5) on the device; yields the shown pictures (Frame, device planes) in
-    output order. With sync_each, every frame is checked with mi_frame_end before it is shown."""
-    dec = Av1Decoder()
+    output order. With sync_each, every frame is checked with mi_frame_end before it is shown.
+    inloop_filters: Dav1dSettings.inloop_filters (rav1d_amd.av1dec.INLOOPFILTER_*)."""
+    dec = Av1Decoder(inloop_filters=inloop_filters)
     pics = {}
     for tu in stream_units(data):
         dec.send(tu)
@@ -90,7 +91,8 @@ def _lanes(ctx, stream, n):
     return lanes + extra[:n - 1]
 
 
-def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=True, threads=8, in_flight=1):
+def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=True, threads=8, in_flight=2,
+                    inloop_filters=14, stats=None):
     """Decode an IVF stream on the device and write every shown picture through `muxer`
     (rav1d_amd.output.Muxer): the picture leaves HBM once, via mi_output_picture into pinned
     host memory, with film grain applied in that same pass when the frame carries grain and
@@ -100,14 +102,22 @@ def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=T
       * the host front-end decodes intra frames on `threads` worker threads, a few temporal
         units ahead of the device (mi_dec_set_threads);
       * frames are reconstructed `in_flight` at a time, frame k on (context, stream) k % in_flight;
-        a frame whose prediction reads other pictures waits for their events first
-        (experimental: with 2, the allintra vector's MD5 is wrong in about half the runs when
-        the lanes really overlap on the device -- not yet understood; default 1);
+        a frame whose prediction reads other pictures waits for their events first (allintra:
+        80 -> 49 ms with 2 lanes; inter streams whose front-end is the bound: unchanged);
       * a shown picture goes to the muxer once its output copy has landed (an event, not a
         stream sync), one picture behind; host pictures rotate.
     Device failures of any frame are reported by the mi_frame_end calls at the end of the
     stream. Without pipelined: one frame at a time, each checked by mi_frame_end before it is
-    shown, the front-end synchronous."""
+    shown, the front-end synchronous.
+
+    stats: a dict to receive the per-stage breakdown: host time waiting for the
+    front-end's events (front_end_ms), host time inside mi_frame_run (run_host_ms), the device
+    stages of every frame from mi_ctx_timing (upload_ms / inter_ms / intra_ms / filter_ms,
+    upload_bytes), the output copies into host memory (d2h_ms, HIP events) and the muxer's host
+    time (mux_ms)."""
+    import time
+
+    from . import MiFrameTiming
     from .av1dec import stream_events
     from .output import HostPicture, output_picture
     import torch
@@ -122,17 +132,31 @@ def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=T
     hosts = [None] * (len(lanes) + 1)
     pending = []                        # (slot, event) of pictures awaiting the muxer, in order
     k = 0
+    clock = time.perf_counter
+    acc = dict(front_end_ms=0.0, mux_ms=0.0, d2h_ms=0.0)
+    out_ev = []
+    if stats is not None:
+        for lctx, _ in lanes:
+            check(lib().mi_ctx_set_timing(lctx.h, 1), "mi_ctx_set_timing")
 
     def flush(keep):
         nonlocal n
         while len(pending) > keep:
             slot, ev = pending.pop(0)
             ev.synchronize()
+            t = clock()
             muxer.write(hosts[slot].pic)
+            acc["mux_ms"] += (clock() - t) * 1e3
             n += 1
 
     slot = 0
-    for ev in stream_events(data, threads if pipelined else 1):
+    events = iter(stream_events(data, threads if pipelined else 1, inloop_filters=inloop_filters))
+    while True:
+        t = clock()
+        ev = next(events, None)
+        acc["front_end_ms"] += (clock() - t) * 1e3
+        if ev is None:
+            break
         if ev.frame:
             li = k % len(lanes)
             k += 1
@@ -159,7 +183,13 @@ def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=T
             if h is None or (h.pic.w, h.pic.h, h.pic.bpc, h.pic.layout) != (out.w, out.h, out.bpc, out.layout):
                 hosts[slot] = h = HostPicture(out.w, out.h, out.bpc, out.layout)
             fg = ev.fg if (ev.fg_present and apply_grain) else None
+            if stats is not None:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(streams[li])
             output_picture(lctx, out, h, fg, ev.mtrx_identity, lst)
+            if stats is not None:
+                b.record(streams[li])
+                out_ev.append((a, b))
             done = torch.cuda.Event()
             done.record(streams[li])
             pending.append((slot, done))
@@ -171,4 +201,18 @@ def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=T
     flush(0)
     for lctx, lst in lanes:
         frame_end(lctx, lst)
+    if stats is not None:
+        tot = dict(frames=0, run_host_ms=0.0, upload_ms=0.0, inter_ms=0.0, intra_ms=0.0, filter_ms=0.0,
+                   upload_bytes=0)
+        for lctx, _ in lanes:
+            tm = MiFrameTiming()
+            check(lib().mi_ctx_timing(lctx.h, ctypes.byref(tm)), "mi_ctx_timing")
+            check(lib().mi_ctx_set_timing(lctx.h, 0), "mi_ctx_set_timing")
+            tot["frames"] += tm.frames
+            tot["run_host_ms"] += tm.host_ms
+            for f in ("upload_ms", "inter_ms", "intra_ms", "filter_ms", "upload_bytes"):
+                tot[f] += getattr(tm, f)
+        acc["d2h_ms"] = sum(a.elapsed_time(b) for a, b in out_ev)
+        stats.update(tot)
+        stats.update(acc)
     return n

@@ -77,19 +77,22 @@ def oracle_frame(fr, refs=None):
     return [by_addr[out[i]] for i in range(n)]
 
 
-def decode_stream(data, recon=oracle_frame, max_frames=None, threads=1, apply_grain=False):
+def decode_stream(data, recon=oracle_frame, max_frames=None, threads=1, apply_grain=False, inloop_filters=14,
+                  hash_output=True):
     """Decode an IVF stream; returns (md5 hex, frames output). `recon(frame, refs) -> planes` runs
     the pixel path (refs: the reference pictures, (planes, w, h) or None, in ref_pic order).
     apply_grain: the reference CLI's --filmgrain 1 (Dav1dSettings.apply_grain, src/lib.rs): shown
     pictures that carry grain get it (the oracle's rav1d_apply_grain) before hashing (oracle by default; the GPU path in the -m gpu tests). threads > 1: the
-    front-end's frame threads (mi_dec_set_threads)."""
+    front-end's frame threads (mi_dec_set_threads). inloop_filters: Dav1dSettings.inloop_filters
+    (mi_dec_set_inloop_filters). hash_output=False: no hashing (returns (None, frames)), the
+    reference CLI's --muxer null."""
     from rav1d_amd.av1dec import stream_events
     from rav1d_amd.output import Muxer, host_picture_np
     pics = {}
     md5 = hashlib.md5()
     mux = Muxer("md5")           # the product md5 muxer (libmi_av1dec.so), checked against hashlib
     shown = 0
-    for ev in stream_events(data, threads):
+    for ev in stream_events(data, threads, inloop_filters=inloop_filters):
         if ev.frame:
             fr = ev.frame.contents
             refs = [None] * 7
@@ -103,8 +106,9 @@ def decode_stream(data, recon=oracle_frame, max_frames=None, threads=1, apply_gr
             planes, w, h, layout, bpc = pics[ev.show_pic]
             if apply_grain and ev.fg_present:
                 planes = oracle_lib.film_grain(planes, bpc, layout, w, h, ev.fg, ev.mtrx_identity)
-            md5_update_picture(md5, planes, w, h, layout)
-            mux.write(host_picture_np(planes, w, h, bpc, layout))
+            if hash_output:
+                md5_update_picture(md5, planes, w, h, layout)
+                mux.write(host_picture_np(planes, w, h, bpc, layout))
             shown += 1
         for i in range(ev.n_release):
             pics.pop(ev.release[i], None)
@@ -112,6 +116,8 @@ def decode_stream(data, recon=oracle_frame, max_frames=None, threads=1, apply_gr
             break
     digest = mux.digest()
     mux.close()
+    if not hash_output:
+        return None, shown
     if shown:
         assert digest == md5.hexdigest(), "md5 muxer disagrees with hashlib"
     return digest if shown else md5.hexdigest(), shown

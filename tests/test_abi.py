@@ -17,7 +17,7 @@ def header_symbols():
     """librav1d_amd.so: every mi_av1dsp.h entry plus mi_av1dec.h's device executor and
     mi_av1out.h's device-to-host output."""
     dec, out = _decl("mi_av1dec.h"), _decl("mi_av1out.h")
-    return sorted(_decl("mi_av1dsp.h") | {s for s in dec if s.startswith("mi_frame_")} |
+    return sorted(_decl("mi_av1dsp.h") | {s for s in dec if s.startswith(("mi_frame_", "mi_ctx_"))} |
                   {s for s in out if not s.startswith("mi_muxer_")})
 
 

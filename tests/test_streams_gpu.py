@@ -198,3 +198,59 @@ def test_superres_frames_match_oracle(gpu, keep_lr):
             w = fr.up_w if p == 0 else (fr.up_w + ss_h) >> ss_h
             got = out.buffer_np(p)[:h, :w]
             assert np.array_equal(got, want[p][:h, :w]), f"plane {p} keep_lr={keep_lr}"
+
+
+class _Collect:
+    """A muxer that keeps a copy of every picture handed to it (host pictures, visible area)."""
+
+    def __init__(self):
+        self.frames = []
+
+    def write(self, pic):
+        from rav1d_amd.output import HostPicture
+        h = HostPicture.__new__(HostPicture)
+        h.pic = pic
+        self.frames.append([h.plane_np(p) for p in range(3 if pic.layout else 1)])
+
+
+def _oracle_frames(data):
+    """Every shown picture of the oracle's decode (visible area per plane)."""
+    from rav1d_amd.av1dec import stream_events
+    from tests.stream_lib import oracle_frame
+    pics, out = {}, []
+    for ev in stream_events(data):
+        if ev.frame:
+            fr = ev.frame.contents
+            refs = [None if r < 0 else pics[r][:3] for r in ev.ref_pic]
+            pics[ev.pic_id] = (oracle_frame(fr, refs), fr.up_w, fr.h, fr.layout)
+        if ev.show_pic >= 0:
+            planes, w, h, lay = pics[ev.show_pic]
+            ss_hor, ss_ver = int(lay in (1, 2)), int(lay == 1)
+            dims = [(w, h)] + [((w + ss_hor) >> ss_hor, (h + ss_ver) >> ss_ver)] * 2
+            out.append([planes[p][:dims[p][1], :dims[p][0]] for p in range(len(planes))])
+        for i in range(ev.n_release):
+            pics.pop(ev.release[i], None)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["av1-1-b8-02-allintra", "00000623"])
+def test_two_device_lanes_match_oracle_per_frame(gpu, name):
+    """Frames alternating over two (context, stream) lanes that overlap on the device (rav1d's
+    frame threads, decode_to_muxer in_flight=2), each lane's context fresh so that its
+    first-use initialisation happens while the other lane's work is queued: every shown picture
+    equals the oracle's. Before the fix this failed in about one run in four: the contexts'
+    device words were zeroed by a null-stream hipMemset, unordered with the lanes' non-blocking
+    streams, and it could land in the middle of the other lane's persistent intra launch."""
+    from rav1d_amd import stream as S
+    from rav1d_amd.frame import Context
+    data = open(os.path.join(GOLDEN, next(v for v in VECTORS if v["name"] == name)["file"]), "rb").read()
+    want = _oracle_frames(data)
+    for rep in range(2):
+        S._extra_lanes.clear()                     # fresh contexts and streams for the extra lane
+        m = _Collect()
+        n = S.decode_to_muxer(Context(0), data, m, apply_grain=False, in_flight=2)
+        assert n == len(want)
+        for k, (got, exp) in enumerate(zip(m.frames, want)):
+            for p in range(len(exp)):
+                assert np.array_equal(got[p], exp[p]), f"{name} rep {rep} frame {k} plane {p}"

@@ -51,6 +51,10 @@ PINNED = [
     ("test15240", "12-bit/argon/test15240.obu"),                      # 4:0:0, scaled refs
     ("annexb", "8-bit/features/annexb.obu"),
     ("section5", "8-bit/features/section5.obu"),
+    # the largest inter vectors: bench.py's real-stream entries
+    ("issue_318", "10-bit/issues/318_tx_4x4.ivf"),                    # 1920x1080 10-bit, 35 frames
+    ("00001141", "8-bit/data/00001141.ivf"),                          # 3840x2160 8-bit, 3 frames
+    ("issue_295", "8-bit/issues/295_adst_precision.ivf"),             # 2780x2136 8-bit, 25 frames
 ]
 
 # the reference's --filmgrain 1 tests (explicit test() entries in the meson files: film grain
