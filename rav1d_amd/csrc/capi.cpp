@@ -337,93 +337,7 @@ int mi_intra_blocks(MiCtx *ctx, const MiPicture *pic, const MiIntraBlock *blocks
 }
 
 int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned flags, void *stream) {
-    if (!ctx || !frames || nframes < 1 || nframes > mi::kIrMaxFrames) return fail(ctx, -EINVAL);
-    const int bpc = frames[0].pic.bpc;
-    if (bpc != 8 && bpc != 10 && bpc != 12) return fail(ctx, -EINVAL);
-    size_t total = 0;
-    for (int f = 0; f < nframes; f++) {
-        const MiIntraFrame &fr = frames[f];
-        if (fr.pic.bpc != bpc || fr.n < 0 || (fr.n && (!fr.blocks || !fr.tx || !fr.dep_start || !fr.coef)))
-            return fail(ctx, -EINVAL);
-        total += (size_t)fr.n;
-    }
-    if (int e = ctx_words(ctx, (hipStream_t)stream)) return fail(ctx, e);
-    if (total > ctx->ir_done_n) {
-        // an earlier launch on this context's stream may still poll the old flags
-        if (ctx->ir_done && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(ctx, -EIO);
-        if (ctx->ir_done) (void)hipFree(ctx->ir_done);
-        ctx->ir_done = nullptr;
-        ctx->ir_done_n = 0;
-        if (hipMalloc(&ctx->ir_done, total * sizeof(uint32_t)) != hipSuccess) return fail(ctx, -ENOMEM);
-        // stream-ordered, as ctx_words
-        if (hipMemsetAsync(ctx->ir_done, 0, total * sizeof(uint32_t), (hipStream_t)stream) != hipSuccess)
-            return fail(ctx, -EIO);
-        ctx->ir_done_n = total;
-        ctx->ir_epoch = 0;
-    }
-    if (++ctx->ir_epoch == 0) ctx->ir_epoch = 1;   // done words hold the epoch of the last call
-    hipStream_t s = (hipStream_t)stream;
-    mi::IntraReconArgs a;
-    memset(&a, 0, sizeof(a));
-    size_t off = 0;
-    for (int f = 0; f < nframes; f++) {
-        const MiIntraFrame &fr = frames[f];
-        mi::IntraReconFrame &d = a.fr[f];
-        for (int p = 0; p < 3; p++) d.ip.dst[p] = (uint8_t *)fr.pic.data[p];
-        d.ip.stride[0] = fr.pic.stride[0];
-        d.ip.stride[1] = fr.pic.stride[1];
-        d.ip.iblocks = fr.blocks;
-        d.ip.ac = fr.ac;
-        d.ip.idx = fr.idx;
-        d.ip.pal = (const uint8_t *)fr.pal;
-        d.ip.bpc = bpc;
-        d.ip.bdmax = (1 << bpc) - 1;
-        d.tx = fr.tx;
-        d.coef = (uint8_t *)fr.coef;
-        d.dep_start = fr.dep_start;
-        d.deps = fr.deps;
-        d.done = ctx->ir_done + off;
-        d.head = ctx->ir_words + f;
-        d.n = fr.n;
-        d.pw = (uint16_t)((fr.pic.w + 127) & ~127);
-        d.ph = (uint16_t)((fr.pic.h + 127) & ~127);
-        d.ss_hor = fr.pic.layout == 1 || fr.pic.layout == 2;
-        d.ss_ver = fr.pic.layout == 1;
-        d.nplanes = fr.pic.layout ? 3 : 1;
-        off += (size_t)fr.n;
-    }
-    // queue heads and XCD worker ranks start from 0 in stream order
-    if (hipMemsetAsync(ctx->ir_words, 0, 64 * sizeof(int), s) != hipSuccess ||
-        hipMemsetAsync(ctx->ir_words + 72, 0, 8 * sizeof(int), s) != hipSuccess)
-        return fail(ctx, -EIO);
-    a.xcd_rank = ctx->ir_words + 72;
-    a.err = ctx->ir_words + 64;
-    a.desc_err = ctx->ir_words + 65;
-#ifdef MI_IR_DEBUG
-    static int *dbg = nullptr;
-    if (!dbg && hipHostMalloc((void **)&dbg, 65536 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
-        return fail(ctx, -ENOMEM);
-    memset(dbg, 0, 65536 * sizeof(int));
-    int *ddbg = nullptr;
-    (void)hipHostGetDevicePointer((void **)&ddbg, dbg, 0);
-    a.dbg = ddbg;
-    setenv("MI_IR_DBG_PTR", std::to_string((uintptr_t)dbg).c_str(), 1);
-#endif
-    a.epoch = ctx->ir_epoch;
-    a.nframes = nframes;
-    a.zero_coefs = (flags & MI_ITX_KEEP_COEFS) ? 0 : 1;
-    // MI_IR_SPREAD=1 (experiment only): with fewer frames than XCDs the idle XCDs' workers join
-    // the frames (1080p8 single frame 7.22 -> 6.54 ms) -- but a worker on another XCD can hit a
-    // 128-B line its own L2 cached before a neighbouring block was written (sc1 loads are
-    // L2-served): observed as wrong pixels with two frames in flight. Off: one XCD per frame.
-    static const int spread_env = getenv("MI_IR_SPREAD") ? atoi(getenv("MI_IR_SPREAD")) : 0;
-    a.spread = spread_env && nframes < 8;
-    // one-wave workers per XCD (occupancy allows 3 per SIMD = 384 per XCD): 128, plus 64 per
-    // extra frame the XCD serves
-    const int per_xcd = (nframes + 7) / 8;
-    static const int wenv = getenv("MI_IR_WORKERS") ? atoi(getenv("MI_IR_WORKERS")) : 0;
-    const int wpx = wenv ? wenv : std::min(384, 128 + 64 * (per_xcd - 1));
-    return mi::launch_intra_recon(a, bpc, wpx, s) ? fail(ctx, -EIO) : 0;
+    return mi_internal::intra_recon(ctx, frames, nframes, nullptr, 1, flags, stream);
 }
 
 int mi_ctx_device_status(MiCtx *ctx, void *stream) {
@@ -1606,3 +1520,103 @@ int mi_dsp_fguv_32x32xn(int layout, void *dst_row, const void *src_row, ptrdiff_
 
 }  // extern "C"
 } // extern "C"
+
+namespace mi_internal {
+
+// mi_intra_recon, and the strip form frame_exec.cpp uses for a single frame: with nstrips > 1
+// the frame's blocks are grouped by strip (strip q = blocks [strip_start[q], strip_start[q+1]),
+// each in dependency order), deps index the whole frame, and queue q (strip q) runs on XCD q.
+int intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, const int32_t *strip_start, int nstrips,
+                unsigned flags, void *stream) {
+    if (!ctx || !frames || nframes < 1 || nframes > mi::kIrMaxFrames) return fail(ctx, -EINVAL);
+    if (nstrips > 1 && (nframes != 1 || nstrips > 8 || !strip_start)) return fail(ctx, -EINVAL);
+    const int bpc = frames[0].pic.bpc;
+    if (bpc != 8 && bpc != 10 && bpc != 12) return fail(ctx, -EINVAL);
+    size_t total = 0;
+    for (int f = 0; f < nframes; f++) {
+        const MiIntraFrame &fr = frames[f];
+        if (fr.pic.bpc != bpc || fr.n < 0 || (fr.n && (!fr.blocks || !fr.tx || !fr.dep_start || !fr.coef)))
+            return fail(ctx, -EINVAL);
+        total += (size_t)fr.n;
+    }
+    if (nstrips > 1)
+        for (int q = 0; q < nstrips; q++)
+            if (strip_start[0] != 0 || strip_start[q + 1] < strip_start[q] || strip_start[nstrips] != frames[0].n)
+                return fail(ctx, -EINVAL);
+    if (int e = ctx_words(ctx, (hipStream_t)stream)) return fail(ctx, e);
+    if (total > ctx->ir_done_n) {
+        // an earlier launch on this context's stream may still poll the old flags
+        if (ctx->ir_done && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(ctx, -EIO);
+        if (ctx->ir_done) (void)hipFree(ctx->ir_done);
+        ctx->ir_done = nullptr;
+        ctx->ir_done_n = 0;
+        if (hipMalloc(&ctx->ir_done, total * sizeof(uint32_t)) != hipSuccess) return fail(ctx, -ENOMEM);
+        // stream-ordered, as ctx_words
+        if (hipMemsetAsync(ctx->ir_done, 0, total * sizeof(uint32_t), (hipStream_t)stream) != hipSuccess)
+            return fail(ctx, -EIO);
+        ctx->ir_done_n = total;
+        ctx->ir_epoch = 0;
+    }
+    if (++ctx->ir_epoch == 0) ctx->ir_epoch = 1;   // done words hold the epoch of the last call
+    hipStream_t s = (hipStream_t)stream;
+    mi::IntraReconArgs a;
+    memset(&a, 0, sizeof(a));
+    const int nq = nstrips > 1 ? nstrips : nframes;
+    size_t off = 0;
+    for (int q = 0; q < nq; q++) {
+        const MiIntraFrame &fr = frames[nstrips > 1 ? 0 : q];
+        const int s0 = nstrips > 1 ? strip_start[q] : 0;
+        mi::IntraReconFrame &d = a.fr[q];
+        for (int p = 0; p < 3; p++) d.ip.dst[p] = (uint8_t *)fr.pic.data[p];
+        d.ip.stride[0] = fr.pic.stride[0];
+        d.ip.stride[1] = fr.pic.stride[1];
+        d.ip.iblocks = fr.blocks + s0;
+        d.ip.ac = fr.ac;
+        d.ip.idx = fr.idx;
+        d.ip.pal = (const uint8_t *)fr.pal;
+        d.ip.bpc = bpc;
+        d.ip.bdmax = (1 << bpc) - 1;
+        d.tx = fr.tx + s0;
+        d.coef = (uint8_t *)fr.coef;
+        d.dep_start = fr.dep_start + s0;
+        d.deps = fr.deps;
+        d.done = ctx->ir_done + off;
+        d.base = s0;
+        d.head = ctx->ir_words + q;
+        d.n = nstrips > 1 ? strip_start[q + 1] - s0 : fr.n;
+        d.pw = (uint16_t)((fr.pic.w + 127) & ~127);
+        d.ph = (uint16_t)((fr.pic.h + 127) & ~127);
+        d.ss_hor = fr.pic.layout == 1 || fr.pic.layout == 2;
+        d.ss_ver = fr.pic.layout == 1;
+        d.nplanes = fr.pic.layout ? 3 : 1;
+        if (nstrips <= 1) off += (size_t)fr.n;
+    }
+    // queue heads and XCD worker ranks start from 0 in stream order
+    if (hipMemsetAsync(ctx->ir_words, 0, 64 * sizeof(int), s) != hipSuccess ||
+        hipMemsetAsync(ctx->ir_words + 72, 0, 8 * sizeof(int), s) != hipSuccess)
+        return fail(ctx, -EIO);
+    a.xcd_rank = ctx->ir_words + 72;
+    a.err = ctx->ir_words + 64;
+    a.desc_err = ctx->ir_words + 65;
+#ifdef MI_IR_DEBUG
+    static int *dbg = nullptr;
+    if (!dbg && hipHostMalloc((void **)&dbg, 65536 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return fail(ctx, -ENOMEM);
+    memset(dbg, 0, 65536 * sizeof(int));
+    int *ddbg = nullptr;
+    (void)hipHostGetDevicePointer((void **)&ddbg, dbg, 0);
+    a.dbg = ddbg;
+    setenv("MI_IR_DBG_PTR", std::to_string((uintptr_t)dbg).c_str(), 1);
+#endif
+    a.epoch = ctx->ir_epoch;
+    a.nframes = nq;
+    a.zero_coefs = (flags & MI_ITX_KEEP_COEFS) ? 0 : 1;
+    // one-wave workers per XCD (occupancy allows 3 per SIMD = 384 per XCD): 128 per queue, plus
+    // 64 per extra queue the XCD serves
+    const int per_xcd = (nq + 7) / 8;
+    static const int wenv = getenv("MI_IR_WORKERS") ? atoi(getenv("MI_IR_WORKERS")) : 0;
+    const int wpx = wenv ? wenv : std::min(384, 128 + 64 * (per_xcd - 1));
+    return mi::launch_intra_recon(a, bpc, wpx, s) ? fail(ctx, -EIO) : 0;
+}
+
+}  // namespace mi_internal

@@ -212,22 +212,22 @@ struct IntraReconFrame {
     const MiTxBlock *tx;
     uint8_t *coef;
     const int32_t *dep_start, *deps;
-    uint32_t *done;               // per block: epoch when reconstructed
+    uint32_t *done;               // epoch when reconstructed: block i's flag is done[base + i],
+                                  // dependency d's is done[d] (a strip's deps index its frame)
     int *head;                    // queue head
-    int n;
+    int n, base;
     uint16_t pw, ph;              // luma plane extent (128-aligned picture area)
     uint8_t ss_hor, ss_ver, nplanes, pad_;
 };
 constexpr int kIrMaxFrames = 24;     // descriptors travel as kernel arguments (4 KB limit)
 struct IntraReconArgs {
-    IntraReconFrame fr[kIrMaxFrames];   // frame f on XCD f % 8
+    IntraReconFrame fr[kIrMaxFrames];   // queue f (a frame, or a strip of one) on XCD f % 8
     int *xcd_rank;                // [8] worker counters (zeroed per launch)
     int *err;
     int *dbg;                     // MI_IR_DEBUG builds: host-mapped progress words
     int *desc_err;                // rejected descriptors (skipped; reported as -EINVAL)
     uint32_t epoch;
     int nframes, zero_coefs;
-    int spread;                   // fewer frames than XCDs: XCD x works on frame x % nframes
 };
 static_assert(sizeof(IntraReconArgs) <= 4096, "kernel argument limit");
 int launch_intra_recon(const IntraReconArgs &a, int bpc, int wg_per_xcd, hipStream_t s);

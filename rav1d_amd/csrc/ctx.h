@@ -50,3 +50,11 @@ struct MiCtx {
         if (fg_offsets) (void)hipFree(fg_offsets);
     }
 };
+
+struct MiIntraFrame;
+namespace mi_internal {
+// mi_intra_recon over frames, or (nstrips > 1, one frame) over the frame's strips: queue q =
+// blocks [strip_start[q], strip_start[q + 1]) on XCD q (capi.cpp)
+int intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, const int32_t *strip_start, int nstrips,
+                unsigned flags, void *stream);
+}

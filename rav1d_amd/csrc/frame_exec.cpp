@@ -17,6 +17,7 @@
 #include <errno.h>
 #include <string.h>
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <vector>
 
@@ -270,6 +271,99 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
     return 0;
 }
 
+// ---- one frame's intra blocks over every XCD (mi_internal::intra_recon strips) ----
+//
+// The persistent reconstruction hands pixels from block to block through the reading XCD's L2
+// (ipred.hip), so a line must never be read on an XCD while another XCD may still write it.
+// The frame is cut into up to 8 vertical strips, strip q reconstructed on XCD q, with every
+// boundary a 128-B line boundary in every plane (and a multiple of 64 luma px). A block that
+// reads pixels of another strip (its left column, top-left and top-right edges at a strip
+// boundary) gets, besides the owners of those pixels, every block writing the lines they lie
+// in: when it first reads such a line on its XCD, the line is final. All those writers precede
+// the block in decode order (the lines lie in superblocks decoded before it: the left
+// neighbour superblock or the superblock row above; an intra block copy source lies a
+// superblock row above or 256 px left of the current superblock, spec 7.11.2 / rav1d
+// decode.rs); if one did not, the frame stays on one XCD. Returns the number of strips (1: no
+// split); strip[i] per block, extra deps as CSR.
+int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<int32_t> &xs,
+                 std::vector<int32_t> &xd) {
+    static const int env = getenv("MI_IR_STRIPS") ? atoi(getenv("MI_IR_STRIPS")) : 8;
+    const int n = f->n_intra;
+    const int maxs = std::min(8, env);
+    if (maxs < 2 || n < 64) return 1;
+    const int pxb = f->bpc == 8 ? 1 : 2;
+    const int ssh = f->layout == 1 || f->layout == 2, ssv = f->layout == 1;
+    const int nplanes = f->layout ? 3 : 1;
+    const int unit = (128 / pxb) << (f->layout ? ssh : 0);   // luma px per line of the widest plane
+    const int units = (f->w + unit - 1) / unit;
+    const int ns = std::min(maxs, units);
+    if (ns < 2) return 1;
+    std::vector<int> sx(ns + 1);
+    for (int q = 0; q <= ns; q++) sx[q] = (int)((int64_t)q * units / ns) * unit;
+    // strip of every block (by its luma column) and the owner of every 4x4 unit of each plane
+    strip.resize(n);
+    const int aw = (f->w + 127) & ~127, ah = (f->h + 127) & ~127;
+    int pw4[3], ph4[3];
+    std::vector<int32_t> own[3];
+    for (int p = 0; p < nplanes; p++) {
+        pw4[p] = (p ? aw >> ssh : aw) >> 2;
+        ph4[p] = (p ? ah >> ssv : ah) >> 2;
+        own[p].assign((size_t)pw4[p] * ph4[p], -1);
+    }
+    for (int i = 0; i < n; i++) {
+        const MiIntraBlock &b = f->intra[i];
+        const int xl = b.plane ? b.x << ssh : b.x;
+        strip[i] = (int8_t)(std::upper_bound(sx.begin(), sx.end(), xl) - sx.begin() - 1);
+        for (int y = b.y >> 2; y < (b.y + b.h) >> 2; y++)
+            for (int x = b.x >> 2; x < (b.x + b.w) >> 2; x++) own[b.plane][(size_t)y * pw4[b.plane] + x] = i;
+    }
+    xs.assign(n + 1, 0);
+    xd.clear();
+    const int lpx = 128 / pxb;                                // plane px per line
+    std::vector<int32_t> add;
+    for (int i = 0; i < n; i++) {
+        xs[i] = (int32_t)xd.size();
+        const MiIntraBlock &b = f->intra[i];
+        const int p = b.plane;
+        add.clear();
+        // the pixels this block may read: its edges (rows y-1 .. y+2h-1, columns x-1 .. x+2w-1),
+        // or for intra block copy the source rectangle (+1 for the bilinear phase, +-1 margin)
+        int bx0 = std::max(0, (int)b.x - 1), by0 = std::max(0, (int)b.y - 1);
+        int bx1 = b.x + 2 * b.w, by1 = b.y + 2 * b.h;
+        if (b.mode == MI_INTRA_IBC) {
+            const int mvx = (int16_t)(b.reserved & 0xffff), mvy = (int16_t)(b.reserved >> 16);
+            const int sh = b.filt_idx & 1, sv = (b.filt_idx >> 1) & 1;
+            const int sx = b.x + (mvx >> (3 + sh)), sy = b.y + (mvy >> (3 + sv));
+            bx0 = std::max(0, sx - 1);
+            by0 = std::max(0, sy - 1);
+            bx1 = sx + b.w + 2;
+            by1 = sy + b.h + 2;
+        }
+        for (int d = f->dep_start[i]; d < f->dep_start[i + 1]; d++) {
+            const int j = f->deps[d];
+            if (strip[j] == strip[i]) continue;
+            const MiIntraBlock &o = f->intra[j];
+            if (o.plane != p) return 1;                       // (CfL luma: same strip by construction)
+            const int x0 = std::max(bx0, (int)o.x), x1 = std::min(bx1, o.x + o.w);
+            const int y0 = std::max(by0, (int)o.y), y1 = std::min(by1, o.y + o.h);
+            if (x0 >= x1 || y0 >= y1) continue;
+            const int l0 = x0 / lpx, l1 = (x1 - 1) / lpx;     // lines of those rows
+            for (int y = y0 >> 2; y <= (y1 - 1) >> 2; y++)
+                for (int u = (l0 * lpx) >> 2; u < std::min(pw4[p], ((l1 + 1) * lpx) >> 2); u++) {
+                    const int w = own[p][(size_t)y * pw4[p] + u];
+                    if (w < 0 || w == j) continue;
+                    if (w >= i) return 1;                     // a later writer: no split
+                    add.push_back(w);
+                }
+        }
+        std::sort(add.begin(), add.end());
+        add.erase(std::unique(add.begin(), add.end()), add.end());
+        xd.insert(xd.end(), add.begin(), add.end());
+    }
+    xs[n] = (int32_t)xd.size();
+    return ns;
+}
+
 int stage_upload(MiCtx *ctx, std::vector<Section> &secs, hipStream_t s, hipEvent_t before = nullptr,
                  int64_t *bytes = nullptr) {
     size_t total = 0;
@@ -415,35 +509,53 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
     const int n = f->n_intra;
 
     // dependency levels (deps always point backwards): level order lets the persistent
-    // kernel's workers run every block of a level side by side
+    // kernel's workers run every block of a level side by side. A single frame is split into
+    // vertical strips, one per XCD (intra_strips), each strip's blocks in level order.
     std::vector<MiIntraBlock> blocks(n);
     std::vector<MiTxBlock> tx(n);
-    std::vector<int32_t> dep_start(n + 1), deps(std::max(1, f->n_deps));
+    std::vector<int32_t> dep_start(n + 1), deps;
+    std::vector<int32_t> strip_start;
     if (n) {
+        std::vector<int32_t> xs, xd;          // extra dependencies of the strip split (CSR)
+        std::vector<int8_t> strip;
+        const int nstrips = intra_strips(f, strip, xs, xd);
+        auto each_dep = [&](int i, auto &&fn) {
+            for (int d = f->dep_start[i]; d < f->dep_start[i + 1]; d++) fn(f->deps[d]);
+            if (nstrips > 1)
+                for (int d = xs[i]; d < xs[i + 1]; d++) fn(xd[d]);
+        };
         std::vector<int32_t> level(n), pos(n);
         int maxl = 0;
         for (int i = 0; i < n; i++) {
             int l = 0;
-            for (int d = f->dep_start[i]; d < f->dep_start[i + 1]; d++) l = std::max(l, level[f->deps[d]] + 1);
+            each_dep(i, [&](int d) { l = std::max(l, level[d] + 1); });
             level[i] = l;
             maxl = std::max(maxl, l);
         }
-        std::vector<int32_t> cnt(maxl + 2, 0);
-        for (int i = 0; i < n; i++) cnt[level[i] + 1]++;
-        for (int l = 0; l <= maxl; l++) cnt[l + 1] += cnt[l];
-        for (int i = 0; i < n; i++) pos[i] = cnt[level[i]]++;
+        // counting sort by (strip, level), decode order within
+        const int nkeys = nstrips * (maxl + 1);
+        auto key = [&](int i) { return (nstrips > 1 ? strip[i] * (maxl + 1) : 0) + level[i]; };
+        std::vector<int32_t> cnt(nkeys + 1, 0);
+        for (int i = 0; i < n; i++) cnt[key(i) + 1]++;
+        for (int k = 0; k < nkeys; k++) cnt[k + 1] += cnt[k];
+        if (nstrips > 1) {
+            strip_start.resize(nstrips + 1);
+            for (int q = 0; q <= nstrips; q++) strip_start[q] = cnt[q * (maxl + 1)];
+        }
+        for (int i = 0; i < n; i++) pos[i] = cnt[key(i)]++;
         std::vector<int32_t> inv(n);
         for (int i = 0; i < n; i++) inv[pos[i]] = i;
-        int nd = 0;
+        deps.reserve(f->n_deps + xd.size() + 1);
         for (int k = 0; k < n; k++) {
             const int i = inv[k];
             blocks[k] = f->intra[i];
             tx[k] = f->intra_tx[i];
-            dep_start[k] = nd;
-            for (int d = f->dep_start[i]; d < f->dep_start[i + 1]; d++) deps[nd++] = pos[f->deps[d]];
+            dep_start[k] = (int32_t)deps.size();
+            each_dep(i, [&](int d) { deps.push_back(pos[d]); });
         }
-        dep_start[n] = nd;
+        dep_start[n] = (int32_t)deps.size();
     }
+    if (deps.empty()) deps.push_back(0);
     // inter frames: the references, units bucketed for mi_mc_frame (OBMC laps split by whether
     // their reference is scaled), residuals grouped by transform size for mi_itx_frame
     const bool inter = inter_present(f) || f->n_inter_tx;
@@ -557,7 +669,9 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         fr.idx = (const uint8_t *)D(5);
         fr.pal = D(6);
         fr.n = n;
-        if ((r = mi_intra_recon(ctx, &fr, 1, 0, stream))) return r;
+        if ((r = mi_internal::intra_recon(ctx, &fr, 1, strip_start.empty() ? nullptr : strip_start.data(),
+                                          (int)strip_start.size() - 1, 0, stream)))
+            return r;
     }
     tev.mark(3, s);
     // the coded-width views of the pictures (stages before super-resolution)

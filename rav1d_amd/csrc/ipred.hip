@@ -568,10 +568,13 @@ __global__ __launch_bounds__(64) void intra_kernel(IpredArgs a) {
 //
 // One launch reconstructs whole intra frames: prediction (intra_block) and the residual
 // (inverse transform + add) of every transform block, in dependency order, without a launch
-// per wavefront step. Frame f is worked on only by the workgroups the dispatcher placed on
-// XCD f (HW_REG_XCC_ID): the `sc1` loads below are served by the reading XCD's L2, which may
-// hold a line cached before a neighbouring block sharing it was written, so readers and
-// writers of one frame share one L2 (the `spread` experiment breaks this and is off). A block's
+// per wavefront step. Queue f -- a frame, or one vertical strip of a single frame
+// (frame_exec.cpp) -- is worked on only by the workgroups the dispatcher placed on XCD f
+// (HW_REG_XCC_ID): the `sc1` loads below are served by the reading XCD's L2, which may hold a
+// line cached before a neighbouring block sharing it was written, so the readers and writers
+// of a line share one L2. Strips keep that true: their boundaries are 128-B line boundaries in
+// every plane, and a block that reads a line of another strip also depends on every block
+// writing that line, so the first read of such a line on this XCD finds it final. A block's
 // pixels are published with the hand-off of MI355X_MICROARCH.md's table row 1: 4-/8-B `sc1`
 // stores, the storing wave's vmcnt(0), then one lane's `sc1` done-flag store; readers poll the
 // flag and read pixels with 4-B `sc1` loads only. Each worker wave
@@ -698,19 +701,13 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
 #else
 #define DBG(i, v) do {} while (0)
 #endif
-    // frames xcc, xcc + 8, ... belong to this XCD; its workers are dealt over them round robin.
-    // With fewer frames than XCDs (spread), XCD x helps frame x % nframes: the hand-off below is
-    // valid across XCDs, placement only buys L2 locality.
+    // queues xcc, xcc + 8, ... (frames, or the strips of one frame) belong to this XCD; its
+    // workers are dealt over them round robin
     const int lane = threadIdx.x;
-    int fidx;
-    if (a.spread) {
-        fidx = (int)xcc % a.nframes;
-    } else {
-        const int nper = (a.nframes - (int)xcc + 7) >> 3;
-        if (nper <= 0) return;
-        const int rank = __builtin_amdgcn_readfirstlane(atomicAdd(a.xcd_rank + xcc, lane == 0 ? 1 : 0));
-        fidx = xcc + 8 * (rank % nper);
-    }
+    const int nper = (a.nframes - (int)xcc + 7) >> 3;
+    if (nper <= 0) return;
+    const int rank = __builtin_amdgcn_readfirstlane(atomicAdd(a.xcd_rank + xcc, lane == 0 ? 1 : 0));
+    const int fidx = xcc + 8 * (rank % nper);
     const IntraReconFrame &fr = a.fr[fidx];
     for (;;) {
         // The block index must be provably wave-uniform and the loop free of lane-divergent
@@ -738,7 +735,7 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
             if (!ok) {
                 if (lane == 0) {
                     atomicOr(a.desc_err, 2);
-                    __hip_atomic_store(fr.done + i, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(fr.done + fr.base + i, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 continue;
             }
@@ -813,7 +810,7 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
         DBG(i, 8);
         __syncthreads();
         DBG(i, 4);
-        if (lane == 0) __hip_atomic_store(fr.done + i, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(fr.done + fr.base + i, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
