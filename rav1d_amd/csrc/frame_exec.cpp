@@ -73,6 +73,12 @@ thread_local const char *g_why = nullptr;
 #define STR2(x) #x
 #define STR(x) STR2(x)
 #define BAD() (g_why = "frame_exec.cpp:" STR(__LINE__), -EINVAL)
+
+// the coefficients a transform block reads from the arena: a DC-only block (DCT_DCT, eob < 1)
+// its DC alone (the front-end stores only that), any other the min(w,32) x min(h,32) run
+size_t coef_span(const mi::TxDim &d, int txtp, int eob) {
+    return txtp == 0 && eob < 1 ? 1 : (size_t)std::min(d.w, 32) * std::min(d.h, 32);
+}
 #define BADF() (g_why = "frame_exec.cpp:" STR(__LINE__), false)
 
 bool pow2_in(int v, int lo, int hi) { return v >= lo && v <= hi && !(v & (v - 1)); }
@@ -181,7 +187,7 @@ int validate_inter(const MiDecFrame *f, const MiFramePictures *p, const bool sca
         const mi::TxDim d = mi::tx_dim(t.tx);
         const int sh = t.plane ? ss_hor : 0, sv = t.plane ? ss_ver : 0;
         if (t.x + d.w > (aw >> sh) || t.y + d.h > (ah >> sv)) return BAD();
-        if ((size_t)t.coef_off + (size_t)std::min(d.w, 32) * std::min(d.h, 32) > f->ncoef) return BAD();
+        if ((size_t)t.coef_off + coef_span(d, t.txtp, t.eob) > f->ncoef) return BAD();
     }
     return 0;
 }
@@ -222,7 +228,7 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
         if (t.eob >= 0) {
             if (!legal_txtp(tx, t.txtp)) return BAD();
             const mi::TxDim d = mi::tx_dim(tx);
-            if ((size_t)t.coef_off + (size_t)std::min(d.w, 32) * std::min(d.h, 32) > f->ncoef) return BAD();
+            if ((size_t)t.coef_off + coef_span(d, t.txtp, t.eob) > f->ncoef) return BAD();
         } else if (t.coef_off + 16 > f->ncoef || (t.txtp != 0 && t.txtp != 16)) {
             return BAD();
         }

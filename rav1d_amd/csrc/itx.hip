@@ -100,6 +100,10 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     bool vk[ROUNDS];
     int dk[ROUNDS];
     V pk[ROUNDS][NCH];
+    // multi-round sizes: every round's coefficient row too, so that later rounds do not pay a
+    // load latency each (lane j < SH reads row j: SW coefficients)
+    constexpr int CR = ROUNDS > 1 ? ROUNDS : 1, CW = ROUNDS > 1 ? SW : 1;
+    int ck[CR][CW];
 #pragma unroll
     for (int rd = 0; rd < ROUNDS; rd++) {
         const int bi = a.blk_start[TX] + (lwg * ROUNDS + rd) * BPW + lb;
@@ -125,6 +129,12 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
                 pk[rd][c4] = *reinterpret_cast<const V *>(pbase + (int64_t)(c / CPR) * st + (c % CPR) * 4 * sizeof(Px));
         }
         dk[rd] = valid && b.txtp == 0 && b.eob < 1 ? (int)(reinterpret_cast<const Cf *>(a.coef) + b.coef_off)[0] : 0;
+        if constexpr (ROUNDS > 1) {
+            const Cf *cq = reinterpret_cast<const Cf *>(a.coef) + b.coef_off;
+            const bool need = valid && !(b.txtp == 0 && b.eob < 1) && j < SH;
+#pragma unroll
+            for (int x = 0; x < CW; x++) ck[rd][x] = need ? (int)cq[j + x * SH] : 0;
+        }
         bk[rd] = b;
         vk[rd] = valid;
     }
@@ -162,7 +172,9 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
         for (int x = 0; x < Wd; x++) r[x] = 0;
 #pragma unroll
         for (int x = 0; x < SW; x++) {
-            const int v = (int)cf[j + x * SH];
+            int v;
+            if constexpr (ROUNDS > 1) v = ck[rd][x];
+            else v = (int)cf[j + x * SH];
             if constexpr (Rect2) r[x] = (v * 181 + 128) >> 8;
             else r[x] = v;
         }

@@ -449,10 +449,12 @@ int FrameDec::decode_coefs(uint8_t *actx, uint8_t *lctx, int tx, int bs, const B
 }
 
 // copy a decoded block into the frame's coefficient arena (itxfm_add layout, min(w,32) x
-// min(h,32) column-major), return its offset in coefficients
-uint32_t FrameDec::store_coefs(const int32_t *cf, int tx) {
+// min(h,32) column-major), return its offset in coefficients. A DC-only block (DCT_DCT with
+// eob 0: itxfm_add's dc-only path reads and clears coefficient 0 alone) keeps only its DC,
+// which shrinks the arena the device path uploads.
+uint32_t FrameDec::store_coefs(const int32_t *cf, int tx, int txtp, int eob) {
     const TxDim &t = k_txdim[tx];
-    const int n = imin(t.w * 4, 32) * imin(t.h * 4, 32);
+    const int n = txtp == 0 && eob < 1 ? 1 : imin(t.w * 4, 32) * imin(t.h * 4, 32);
     const uint32_t off = (uint32_t)fw.ncoef;
     const int cb = s.bpc == 8 ? 2 : 4;
     fw.coef.resize((fw.ncoef + n) * cb);
@@ -790,7 +792,7 @@ void FrameDec::emit_intra(const Block &b, int edge_flags, const uint8_t *pal_idx
             memset(lctx, res, nlct);
             tb.txtp = (uint8_t)txtp;
             tb.eob = eob;
-            if (eob >= 0) tb.coef_off = store_coefs(cf, txs);
+            if (eob >= 0) tb.coef_off = store_coefs(cf, txs, txtp, eob);
         } else {
             memset(actx, 0x40, nact);
             memset(lctx, 0x40, nlct);
@@ -1187,7 +1189,7 @@ void FrameDec::push_ibc(const Block &b, Mv mv, int plane, int tx, int tbx, int t
         memset(lctx, res, nlct);
         tb.txtp = (uint8_t)*txtp;
         tb.eob = eob;
-        if (eob >= 0) tb.coef_off = store_coefs(cf, tx);
+        if (eob >= 0) tb.coef_off = store_coefs(cf, tx, *txtp, eob);
     }
     fw.intra_tx.push_back(tb);
     std::vector<int32_t> &o = owner[plane];

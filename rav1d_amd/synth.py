@@ -145,6 +145,8 @@ def make_itx_frame(w, h, bpc=10, layout=1, seed=0x1D1C0001, dc_frac=0.6, full_fr
             c, eob = make_coefs(rng, tx, txtp, regime, bpc)
             if txtp == 16:
                 c = np.clip(c // 64, -(1 << (bpc + 2)), (1 << (bpc + 2)))
+            if txtp == 0 and eob < 1:
+                c = c.reshape(-1)[:1]     # a DC-only block keeps its DC alone (as the front-end stores it)
             recs.append((off, x, y, p, tx, txtp, 0, eob))
             coef_chunks.append(c)
             off += c.size
@@ -420,6 +422,8 @@ def itx_blocks_from_tilings(tilings, bpc, rng, dc_frac=0.6, full_frac=0.1):
                 txtp = types[int(rng.integers(len(types)))]
                 regime = 2 if rng.random() < full_frac / (1 - dc_frac) else 1
             c, eob = make_coefs(rng, tx, txtp, regime, bpc)
+            if txtp == 0 and eob < 1:
+                c = c.reshape(-1)[:1]     # a DC-only block keeps its DC alone (as the front-end stores it)
             recs.append((off, x, y, p, tx, txtp, 0, eob))
             chunks.append(c)
             off += c.size
