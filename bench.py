@@ -463,8 +463,9 @@ def real_streams(ctx, reps=3, oracle_reps=5, oracle_budget_s=25.0):
             frames=n, size=f"{size[0]}x{size[1]} {bits}-bit", md5_verified=ok, muxer="null (md5 verified in a separate pass)",
             gpu_ms=round(best * 1e3, 3), gpu_fps=round(n / best, 1), gpu_mpx_per_s=round(px / best / 1e6, 2),
             gpu_unpipelined_ms=round(best_seq * 1e3, 3),
-            stages_ms={k: round(st[k], 3) for k in ("front_end_ms", "run_host_ms", "upload_ms", "inter_ms", "intra_ms",
-                                                     "filter_ms", "d2h_ms", "mux_ms")},
+            stages_ms={k: round(st[k], 3) for k in ("front_end_ms", "run_host_ms", "run_levels_ms", "run_stage_ms",
+                                                     "upload_ms", "inter_ms", "intra_ms", "filter_ms", "d2h_ms",
+                                                     "mux_ms")},
             upload_mb=round(st["upload_bytes"] / 1e6, 2),
             front_end_only_ms=round(fe * 1e3, 3),
             cpu_oracle_ms=round(cpu * 1e3, 1), cpu_oracle_reps=creps, cpu_oracle_mpx_per_s=round(px / cpu / 1e6, 2))

@@ -149,6 +149,9 @@ typedef struct MiFrameTiming {
     double intra_ms;       /* the persistent intra reconstruction launch */
     double filter_ms;      /* deblock, CDEF, super-resolution, loop restoration */
     int64_t upload_bytes;  /* bytes uploaded */
+    double stage_ms;       /* of host_ms: the staging copy into pinned memory, with any wait for
+                              the previous frame's upload to leave the staging buffer */
+    double strips_ms;      /* of host_ms: the dependency levels and the XCD strip split */
 } MiFrameTiming;
 int mi_ctx_set_timing(MiCtx *ctx, int on);
 int mi_ctx_timing(MiCtx *ctx, MiFrameTiming *out);

@@ -38,7 +38,8 @@ class MiFrameTiming(ctypes.Structure):
     """include/mi_av1dec.h: per-stage timing of mi_frame_run (mi_ctx_set_timing / mi_ctx_timing)."""
     _fields_ = [("frames", ctypes.c_int32), ("reserved", ctypes.c_int32), ("host_ms", ctypes.c_double),
                 ("upload_ms", ctypes.c_double), ("inter_ms", ctypes.c_double), ("intra_ms", ctypes.c_double),
-                ("filter_ms", ctypes.c_double), ("upload_bytes", ctypes.c_int64)]
+                ("filter_ms", ctypes.c_double), ("upload_bytes", ctypes.c_int64), ("stage_ms", ctypes.c_double),
+                ("strips_ms", ctypes.c_double)]
 
 
 class MiIntraFrame(ctypes.Structure):

@@ -28,13 +28,13 @@ struct MiCtx {
     // upload, after it, after inter prediction + residuals, after intra, at the end)
     bool tm_on = false;
     std::vector<hipEvent_t> tm_ev;
-    double tm_host_ms = 0;
+    double tm_host_ms = 0, tm_stage_ms = 0, tm_strips_ms = 0;
     int64_t tm_bytes = 0;
     int tm_frames = 0;
     void tm_clear() {
         for (hipEvent_t e : tm_ev) (void)hipEventDestroy(e);
         tm_ev.clear();
-        tm_host_ms = 0;
+        tm_host_ms = tm_stage_ms = tm_strips_ms = 0;
         tm_bytes = 0;
         tm_frames = 0;
     }

@@ -496,6 +496,8 @@ int mi_ctx_timing(MiCtx *ctx, MiFrameTiming *out) {
     out->intra_ms = st[2];
     out->filter_ms = st[3];
     out->upload_bytes = ctx->tm_bytes;
+    out->stage_ms = ctx->tm_stage_ms;
+    out->strips_ms = ctx->tm_strips_ms;
     const bool on = ctx->tm_on;
     ctx->tm_clear();
     ctx->tm_on = on;
@@ -521,6 +523,8 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
     std::vector<MiTxBlock> tx(n);
     std::vector<int32_t> dep_start(n + 1), deps;
     std::vector<int32_t> strip_start;
+    using clk = std::chrono::steady_clock;
+    const auto t_lv = clk::now();
     if (n) {
         std::vector<int32_t> xs, xd;          // extra dependencies of the strip split (CSR)
         std::vector<int8_t> strip;
@@ -562,6 +566,7 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         dep_start[n] = (int32_t)deps.size();
     }
     if (deps.empty()) deps.push_back(0);
+    if (ctx->tm_on) ctx->tm_strips_ms += std::chrono::duration<double, std::milli>(clk::now() - t_lv).count();
     // inter frames: the references, units bucketed for mi_mc_frame (OBMC laps split by whether
     // their reference is scaled), residuals grouped by transform size for mi_itx_frame
     const bool inter = inter_present(f) || f->n_inter_tx;
@@ -612,7 +617,9 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         { itx_b.data(), itx_b.size() * sizeof(MiTxBlock), 0 },                     // 20
         { nullptr, f->ntmp * 2, 0 },                                                // 21: tmp arena
     };
+    const auto t_st = clk::now();
     if ((r = stage_upload(ctx, secs, s, tev.ev[0], bytes))) return ctx->last_error = r;
+    if (ctx->tm_on) ctx->tm_stage_ms += std::chrono::duration<double, std::milli>(clk::now() - t_st).count();
     tev.mark(1, s);
     uint8_t *dev = ctx->fx_dev;
     auto D = [&](int i) -> void * { return secs[i].bytes ? dev + secs[i].off : nullptr; };

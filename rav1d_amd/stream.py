@@ -203,13 +203,15 @@ def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=T
         frame_end(lctx, lst)
     if stats is not None:
         tot = dict(frames=0, run_host_ms=0.0, upload_ms=0.0, inter_ms=0.0, intra_ms=0.0, filter_ms=0.0,
-                   upload_bytes=0)
+                   upload_bytes=0, run_stage_ms=0.0, run_levels_ms=0.0)
         for lctx, _ in lanes:
             tm = MiFrameTiming()
             check(lib().mi_ctx_timing(lctx.h, ctypes.byref(tm)), "mi_ctx_timing")
             check(lib().mi_ctx_set_timing(lctx.h, 0), "mi_ctx_set_timing")
             tot["frames"] += tm.frames
             tot["run_host_ms"] += tm.host_ms
+            tot["run_stage_ms"] += tm.stage_ms
+            tot["run_levels_ms"] += tm.strips_ms
             for f in ("upload_ms", "inter_ms", "intra_ms", "filter_ms", "upload_bytes"):
                 tot[f] += getattr(tm, f)
         acc["d2h_ms"] = sum(a.elapsed_time(b) for a, b in out_ev)
