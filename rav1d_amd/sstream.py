@@ -15,7 +15,15 @@ Transfer protocol, deadlock-free by construction:
     producer);
   * a consumer receives the pictures coming from one peer strictly in increasing r (the order
     the peer sends them), buffering any it does not need yet, so the per-pair message order
-    always matches.
+    always matches;
+  * the two directions of a pair travel on two communicators (one process group carries every
+    lower -> higher rank message, another every higher -> lower one). RCCL / NCCL put a
+    pair's unbatched sends and receives of one communicator on one stream, where A's send to
+    B queued before A's receive from B, and B's send to A before B's receive from A, would
+    wait on each other for large pictures; with one communicator per direction a send never
+    sits in front of the receive its peer's send needs.
+The "nccl" (RCCL over xGMI) path is experimental: the tests exercise this scheduler over gloo
+(tests/test_sstream_dist.py) and on one GPU; the round-end driver owns the 8-GPU node.
 The per-frame work is an `executor(spec, ref_pictures) -> picture` callable: the device
 executor below runs the batched C-ABI kernels (mi_mc_frame -> mi_itx_frame ->
 mi_deblock_frame_to -> mi_cdef_frame -> mi_lr_frame); tests drive the same scheduler with
@@ -98,21 +106,31 @@ class PipelinedStream:
         self.executor, self.alloc = executor, alloc
         self.rank, self.world, self.device = rank, world, device
         self.gloo = dist.is_initialized() and dist.get_backend() == "gloo"
+        # one communicator per direction (every rank creates both, in the same order)
+        self.up = self.down = None
+        if dist.is_initialized() and world > 1:
+            self.up, self.down = dist.new_group(), dist.new_group()
+
+    def _group(self, peer, sending):
+        """lower -> higher rank messages on `up`, higher -> lower on `down`"""
+        return self.up if (peer > self.rank) == sending else self.down
 
     def _send(self, pic, dst, pending):
+        g = self._group(dst, True)
         for t in pic.planes:
             src = t.cpu() if self.gloo and t.is_cuda else t
-            pending.append((dist.isend(src, dst), src))
+            pending.append((dist.isend(src, dst, group=g), src))
 
     def _recv(self, spec_of, r, src):
         pic = self.alloc(spec_of[r])
+        g = self._group(src, False)
         for t in pic.planes:
             if self.gloo and t.is_cuda:
                 h = torch.empty_like(t, device="cpu")
-                dist.recv(h, src)
+                dist.recv(h, src, group=g)
                 t.copy_(h)
             else:
-                dist.recv(t, src)
+                dist.recv(t, src, group=g)
         return pic
 
     def run(self, specs):

@@ -24,19 +24,30 @@ def frames(data):
 
 
 def main(d, threads):
-    resource.setrlimit(resource.RLIMIT_AS, (8 << 30, 8 << 30))
+    if not os.environ.get("FUZZ_NO_AS_LIMIT"):     # (AddressSanitizer reserves terabytes of shadow)
+        resource.setrlimit(resource.RLIMIT_AS, (8 << 30, 8 << 30))
     from rav1d_amd.av1dec import Av1Decoder
     for name in sorted(os.listdir(d)):
         data = open(os.path.join(d, name), "rb").read()
+        # one decoder for the whole input, fed on after every rejected temporal unit, as the
+        # reference fuzzer keeps its context after a dav1d_send_data / dav1d_get_picture error
+        # (tests/libfuzzer/dav1d_fuzzer.c:165-181): the front-end's recovery state is exercised
         dec, nev, nerr = Av1Decoder(threads), 0, 0
         for f in frames(data):
             try:
                 dec.send(f)
+            except RuntimeError:
+                nerr += 1
+            try:
                 for _ in dec.events():
                     nev += 1
             except RuntimeError:
-                nerr += 1          # a rejected temporal unit: the stream restarts, as the fuzzer's
-                dec = Av1Decoder(threads)   # dav1d_flush / a new context would
+                nerr += 1
+        try:
+            for _ in dec.events():
+                nev += 1
+        except RuntimeError:
+            nerr += 1
         print(name, nev, nerr, flush=True)
 
 
