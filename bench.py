@@ -274,7 +274,7 @@ def mc_coherent(ctx, stream, reps=20):
     algo = mc_algorithmic_bytes(fr["mc"][0], BPC) + fr["mc"][2].nbytes
     gbs = algo / (ms / 1e3) / 1e9
     return dict(ms=round(ms, 4), algo_bytes=int(algo), gbs=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4),
-                traffic_per_step=pmc_traffic("mc", "r02_traffic_coherent.json"),
+                traffic_per_step=pmc_traffic("mc", "r03_traffic_coherent.json"),
                 mv_field="coherent: per-64x64 motion per reference uniform in +-64 px, +-2 px noise per block")
 
 
@@ -477,12 +477,12 @@ def per_launch(v, launches):
 
 
 def pmc_traffic(stage, name=None):
-    """HBM bytes per step of `stage` from the committed PMC run (profiles/r02_traffic.json,
+    """HBM bytes per step of `stage` from the committed PMC run (profiles/r03_traffic.json,
     written by tools/traffic_json.py from tools/gpu_pmc.sh's FETCH_SIZE / WRITE_SIZE passes of
     this same bench command, calibrated per access width by tools/pmc_calib; the round-1 file
     when this round's is absent). None if absent."""
     path = None
-    for n in ([name] if name else ["r02_traffic.json", "r01_traffic.json"]):
+    for n in ([name] if name else ["r03_traffic.json", "r02_traffic.json", "r01_traffic.json"]):
         if os.path.exists(os.path.join(ROOT, "profiles", n)):
             path = os.path.join(ROOT, "profiles", n)
             break

@@ -17,8 +17,10 @@ for C in FETCH_SIZE WRITE_SIZE "TCC_EA0_RDREQ TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64
       $R/tools/pmc_calib > $OUT/calib_$D.log 2>&1 || { echo "calib $D failed"; tail -20 $OUT/calib_$D.log; exit 1; }
 done
 echo "calibration done"
+# the headline command alone (no real-stream / intra / grain legs), so that the per-kernel averages
+# are the headline's launches, comparable with the bench's event-timed launch_us
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o p -- \
-    python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench_stats.json 2> $OUT/bench_stats.err \
+    python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-fg --no-intra --no-extra > $OUT/bench_stats.json 2> $OUT/bench_stats.err \
     || { echo "stats run failed"; tail -20 $OUT/bench_stats.err; exit 1; }
 echo "kernel stats done"; cat $OUT/bench_stats.json
 TRAFFIC_ONLY=1 bash $R/tools/gpu_pmc.sh $TAG/pmc > /dev/null || { echo "pmc failed"; exit 1; }
