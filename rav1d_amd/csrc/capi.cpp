@@ -1527,7 +1527,7 @@ namespace mi_internal {
 // the frame's blocks are grouped by strip (strip q = blocks [strip_start[q], strip_start[q+1]),
 // each in dependency order), deps index the whole frame, and queue q (strip q) runs on XCD q.
 int intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, const int32_t *strip_start, int nstrips,
-                unsigned flags, void *stream) {
+                unsigned flags, void *stream, bool granules) {
     if (!ctx || !frames || nframes < 1 || nframes > mi::kIrMaxFrames) return fail(ctx, -EINVAL);
     if (nstrips > 1 && (nframes != 1 || nstrips > 8 || !strip_start)) return fail(ctx, -EINVAL);
     const int bpc = frames[0].pic.bpc;
@@ -1555,12 +1555,33 @@ int intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, const int32
         if (hipMemsetAsync(ctx->ir_done, 0, total * sizeof(uint32_t), (hipStream_t)stream) != hipSuccess)
             return fail(ctx, -EIO);
         ctx->ir_done_n = total;
-        ctx->ir_epoch = 0;
     }
     if (++ctx->ir_epoch == 0) ctx->ir_epoch = 1;   // done words hold the epoch of the last call
     hipStream_t s = (hipStream_t)stream;
     mi::IntraReconArgs a;
     memset(&a, 0, sizeof(a));
+    // edge granules: one region per frame (mi::gran_count), zeroed once when (re)allocated
+    std::vector<uint32_t> goff(nframes, 0);
+    if (granules) {
+        size_t ng = 0;
+        for (int f = 0; f < nframes; f++) {
+            const MiPicture &pic = frames[f].pic;
+            goff[f] = (uint32_t)ng;
+            ng += mi::gran_count((pic.w + 127) & ~127, (pic.h + 127) & ~127, pic.layout == 1 || pic.layout == 2,
+                                 pic.layout == 1, pic.layout ? 3 : 1);
+        }
+        if (ng > 0xffffffffull) return fail(ctx, -EINVAL);
+        if (ng > ctx->ir_gran_n) {
+            if (ctx->ir_gran && hipStreamSynchronize(s) != hipSuccess) return fail(ctx, -EIO);
+            if (ctx->ir_gran) (void)hipFree(ctx->ir_gran);
+            ctx->ir_gran = nullptr;
+            ctx->ir_gran_n = 0;
+            if (hipMalloc((void **)&ctx->ir_gran, ng * 8) != hipSuccess) return fail(ctx, -ENOMEM);
+            if (hipMemsetAsync(ctx->ir_gran, 0, ng * 8, s) != hipSuccess) return fail(ctx, -EIO);
+            ctx->ir_gran_n = ng;
+        }
+        a.gran = ctx->ir_gran;
+    }
     const int nq = nstrips > 1 ? nstrips : nframes;
     size_t off = 0;
     for (int q = 0; q < nq; q++) {
@@ -1589,6 +1610,7 @@ int intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, const int32
         d.ss_hor = fr.pic.layout == 1 || fr.pic.layout == 2;
         d.ss_ver = fr.pic.layout == 1;
         d.nplanes = fr.pic.layout ? 3 : 1;
+        d.goff = goff[nstrips > 1 ? 0 : q];
         if (nstrips <= 1) off += (size_t)fr.n;
     }
     // queue heads and XCD worker ranks start from 0 in stream order

@@ -207,6 +207,17 @@ struct IpredArgs {
     int bpc, bdmax;
 };
 // persistent fused intra reconstruction (ipred.hip): frame f is worked on by XCD f % 8
+// edge granules per frame (ipred.hip GranCtx: per plane, a column-boundary array then a
+// row-boundary array of 8-B {two pixels, epoch} records); host: the allocation
+__host__ __device__ inline size_t gran_count(int pw, int ph, int ss_hor, int ss_ver, int nplanes) {
+    size_t n = 0;
+    for (int p = 0; p < nplanes; p++) {
+        const int w = p ? pw >> ss_hor : pw, h = p ? ph >> ss_ver : ph;
+        n += (size_t)((w >> 2) + 1) * (h >> 1) + (size_t)((h >> 2) + 1) * (w >> 1);
+    }
+    return n;
+}
+
 struct IntraReconFrame {
     IpredArgs ip;                 // picture planes / strides, iblocks, ac, idx, pal, bpc, bdmax
     const MiTxBlock *tx;
@@ -218,6 +229,7 @@ struct IntraReconFrame {
     int n, base;
     uint16_t pw, ph;              // luma plane extent (128-aligned picture area)
     uint8_t ss_hor, ss_ver, nplanes, pad_;
+    uint32_t goff;                // edge granules (IntraReconArgs::gran): this frame's first one
 };
 constexpr int kIrMaxFrames = 24;     // descriptors travel as kernel arguments (4 KB limit)
 struct IntraReconArgs {
@@ -226,6 +238,10 @@ struct IntraReconArgs {
     int *err;
     int *dbg;                     // MI_IR_DEBUG builds: host-mapped progress words
     int *desc_err;                // rejected descriptors (skipped; reported as -EINVAL)
+    // edge granules (null: off): per frame and plane, the right column of every block at its
+    // 4-px column boundary and its bottom row at its row boundary, as 8-B {two pixels, epoch}
+    // records a consumer polls instead of a done flag plus pixel loads (ipred.hip)
+    unsigned long long *gran;
     uint32_t epoch;
     int nframes, zero_coefs;
 };

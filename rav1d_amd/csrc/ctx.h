@@ -17,7 +17,9 @@ struct MiCtx {
     uint32_t *ir_done = nullptr;
     size_t ir_done_n = 0;
     int *ir_words = nullptr;      // [0..63] queue heads, [64] error, [72..79] XCD worker ranks
-    uint32_t ir_epoch = 0;
+    uint32_t ir_epoch = 0;        // never reset: done words and edge granules hold old epochs
+    unsigned long long *ir_gran = nullptr;   // edge granules (ipred.hip GranCtx), zeroed when allocated
+    size_t ir_gran_n = 0;
     // frame executor (frame_exec.cpp): device copy of one frame's descriptors, staged through
     // pinned host memory; `fx_ev` marks when the staging buffer may be rewritten
     uint8_t *fx_dev = nullptr, *fx_host = nullptr;
@@ -45,6 +47,7 @@ struct MiCtx {
         if (fx_host) (void)hipHostFree(fx_host);
         if (ir_done) (void)hipFree(ir_done);
         if (ir_words) (void)hipFree(ir_words);
+        if (ir_gran) (void)hipFree(ir_gran);
         if (fg_lut) (void)hipFree(fg_lut);
         if (fg_scaling) (void)hipFree(fg_scaling);
         if (fg_offsets) (void)hipFree(fg_offsets);
@@ -55,6 +58,8 @@ struct MiIntraFrame;
 namespace mi_internal {
 // mi_intra_recon over frames, or (nstrips > 1, one frame) over the frame's strips: queue q =
 // blocks [strip_start[q], strip_start[q + 1]) on XCD q (capi.cpp)
+// granules: edges handed over as data-tagged granules (ipred.hip); then deps need list only the
+// blocks whose pixels are read beyond the edges (CfL luma, intra block copy sources)
 int intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, const int32_t *strip_start, int nstrips,
-                unsigned flags, void *stream);
+                unsigned flags, void *stream, bool granules = false);
 }

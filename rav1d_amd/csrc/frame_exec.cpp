@@ -525,6 +525,18 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
     std::vector<int32_t> strip_start;
     using clk = std::chrono::steady_clock;
     const auto t_lv = clk::now();
+    // edge granules (ipred.hip gran_fetch) when every pixel an intra edge reads is written in the
+    // same launch: no inter units, no inter-intra blends or inter residuals. A block then waits
+    // on flags only for the pixels it reads beyond its edges (CfL's luma, intra block copy's
+    // source); the levels still follow every dependency. MI_IR_GRANULES=0 turns them off.
+    static const bool gran_env = [] {
+        const char *e = getenv("MI_IR_GRANULES");
+        return !(e && e[0] == '0');
+    }();
+    const bool inter = inter_present(f) || f->n_inter_tx;
+    bool granules = gran_env && !inter && n > 0;
+    for (int i = 0; granules && i < n; i++)
+        if ((f->intra[i].flags & MI_INTRA_II) || f->intra[i].mode == MI_INTRA_RESID) granules = false;
     if (n) {
         std::vector<int32_t> xs, xd;          // extra dependencies of the strip split (CSR)
         std::vector<int8_t> strip;
@@ -561,7 +573,13 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
             blocks[k] = f->intra[i];
             tx[k] = f->intra_tx[i];
             dep_start[k] = (int32_t)deps.size();
-            each_dep(i, [&](int d) { deps.push_back(pos[d]); });
+            const MiIntraBlock &b = f->intra[i];
+            if (!granules || b.mode == MI_INTRA_IBC || b.mode == MI_IPRED_CFL) {
+                each_dep(i, [&](int d) { deps.push_back(pos[d]); });
+            } else {
+                for (int d = f->dep_start[i]; d < f->dep_start[i + 1]; d++)
+                    if (f->intra[f->deps[d]].plane != b.plane) deps.push_back(pos[f->deps[d]]);
+            }
         }
         dep_start[n] = (int32_t)deps.size();
     }
@@ -569,7 +587,6 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
     if (ctx->tm_on) ctx->tm_strips_ms += std::chrono::duration<double, std::milli>(clk::now() - t_lv).count();
     // inter frames: the references, units bucketed for mi_mc_frame (OBMC laps split by whether
     // their reference is scaled), residuals grouped by transform size for mi_itx_frame
-    const bool inter = inter_present(f) || f->n_inter_tx;
     bool scaled[7] = {};
     if (inter) {
         if ((r = validate_refs(f, pics, scaled)) || (r = validate_inter(f, pics, scaled))) return ctx->last_error = r;
@@ -683,7 +700,7 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         fr.pal = D(6);
         fr.n = n;
         if ((r = mi_internal::intra_recon(ctx, &fr, 1, strip_start.empty() ? nullptr : strip_start.data(),
-                                          (int)strip_start.size() - 1, 0, stream)))
+                                          (int)strip_start.size() - 1, 0, stream, granules)))
             return r;
     }
     tev.mark(3, s);

@@ -400,13 +400,103 @@ __device__ __forceinline__ void cfl_ac_wave(int16_t *ac, const uint8_t *ybase, i
     for (int i = lane; i < cw * ch; i += 64) ac[i] = (int16_t)(ac[i] - mean);
 }
 
+// Edge granules of the persistent reconstruction (IntraReconArgs::gran): for one plane, the
+// right column of every block at its 4-px column boundary (col[bx * colp + y / 2]: pixels y and
+// y + 1 of column 4 * bx - 1) and its bottom row at its row boundary (row[by * rowp + x / 2]:
+// pixels x and x + 1 of row 4 * by - 1), each an 8-B {pixel, pixel << 16, epoch << 32} record
+// stored by one `sc1` 8-B store: the hand-off of MI355X_MICROARCH.md's data-tagged granules (no
+// flag, no second load: a consumer polls the record itself and finds the data with the tag).
+#ifndef MI_IR_GRAN_SPIN_LOG2
+#define MI_IR_GRAN_SPIN_LOG2 22
+#endif
+struct GranCtx {
+    unsigned long long *col, *row;
+    int colp, rowp;
+    uint32_t epoch;
+    int *err;
+};
+__device__ __forceinline__ GranCtx gran_ctx(unsigned long long *base, int pw, int ph, int ss_hor, int ss_ver,
+                                             int nplanes, int plane, uint32_t epoch, int *err) {
+    GranCtx g;
+    unsigned long long *q = base;
+    for (int p = 0; p < nplanes; p++) {
+        const int w = p ? pw >> ss_hor : pw, h = p ? ph >> ss_ver : ph;
+        const int colp = h >> 1, rowp = w >> 1;
+        if (p == plane) {
+            g.col = q;
+            g.row = q + (size_t)((w >> 2) + 1) * colp;
+            g.colp = colp;
+            g.rowp = rowp;
+        }
+        q += (size_t)((w >> 2) + 1) * colp + (size_t)((h >> 2) + 1) * rowp;
+    }
+    g.epoch = epoch;
+    g.err = err;
+    return g;
+}
+// The edge pixels (yy[k], xx[k]) (use[k]) of the block at (x, y) from the granules: a left-column
+// pixel from the column boundary x, a top-row pixel from the row boundary y, the top-left corner
+// from whichever of the two its block wrote. Every lane polls its records until each carries this
+// launch's epoch (one round of loads in the common case); bounded like the flag wait.
+template <int K>
+__device__ __forceinline__ void gran_fetch(const GranCtx &g, int x, int y, const int (&yy)[K], const int (&xx)[K],
+                                           const bool (&use)[K], int (&out)[K]) {
+    const unsigned long long *pa[K], *pb[K];
+    int sa[K], sb[K];
+    bool ok[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        ok[k] = !use[k];
+        pb[k] = nullptr;
+        sa[k] = sb[k] = 0;
+        if (xx[k] == x - 1 && yy[k] == y - 1) {
+            pa[k] = g.col + (x >> 2) * g.colp + ((y - 1) >> 1);
+            sa[k] = ((y - 1) & 1) * 16;
+            pb[k] = g.row + (y >> 2) * g.rowp + ((x - 1) >> 1);
+            sb[k] = ((x - 1) & 1) * 16;
+        } else if (xx[k] == x - 1) {
+            pa[k] = g.col + (x >> 2) * g.colp + (yy[k] >> 1);
+            sa[k] = (yy[k] & 1) * 16;
+        } else {
+            pa[k] = g.row + (y >> 2) * g.rowp + (xx[k] >> 1);
+            sa[k] = (xx[k] & 1) * 16;
+        }
+    }
+    for (unsigned spins = 0;; spins++) {
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            if (ok[k]) continue;
+            unsigned long long v = __hip_atomic_load(pa[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(v >> 32) == g.epoch) {
+                out[k] = (int)((v >> sa[k]) & 0xffff);
+                ok[k] = true;
+            } else if (pb[k]) {
+                v = __hip_atomic_load(pb[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)(v >> 32) == g.epoch) {
+                    out[k] = (int)((v >> sb[k]) & 0xffff);
+                    ok[k] = true;
+                }
+            }
+        }
+        bool all = true;
+#pragma unroll
+        for (int k = 0; k < K; k++) all = all && ok[k];
+        if (__builtin_amdgcn_ballot_w64(!all) == 0) break;
+        if (spins > (1u << MI_IR_GRAN_SPIN_LOG2)) {
+            atomicOr(g.err, 1);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 // Gather one block's edges from the picture (rav1d_prepare_intra_edges) and predict it, one
 // wave. Fused (the persistent reconstruction kernel): neighbour pixels were stored by other
 // CUs of this XCD during the launch, so every picture read is an L1-bypassing `sc1` load
 // (L2-served), and the prediction goes to the LDS tile lt.
 template <typename Px, bool Fused>
 __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlock &ib, int *eb, Px *ft, Px *edge,
-                                            Px *lt, int16_t *acl) {
+                                            Px *lt, int16_t *acl, const GranCtx *gran = nullptr) {
     const int lane = threadIdx.x;
     const int w = ib.w, h = ib.h, x = ib.x, y = ib.y;
     const bool have_left = ib.flags & MI_INTRA_HAVE_LEFT, have_top = ib.flags & MI_INTRA_HAVE_TOP;
@@ -505,26 +595,50 @@ __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlo
     // are filled as rav1d_prepare_intra_edges does (ipred_prepare.rs:118-204).
     const int i = lane;
     const int half = 1 << bd >> 1;
-    int vL = 0, vBL = 0, vT = 0, vTR = 0, vC = 0;
+    // the five edge samples of this lane (left, bottom-left, top, top-right, corner): a pixel
+    // position, or a constant where the edge is unavailable (ipred_prepare.rs:118-204)
+    int py[5], px[5], v[5] = { 0, 0, 0, 0, 0 };
+    bool rd[5] = { false, false, false, false, false };
+    auto at = [&](int k, int yy, int xx) { py[k] = yy; px[k] = xx; rd[k] = true; };
+#pragma unroll
+    for (int k = 0; k < 5; k++) py[k] = px[k] = 0;
     if (needs & 1) {
-        if (have_left) vL = P(y + min(i, min(h, (int)ib.tile_h - y) - 1), x - 1);
-        else vL = have_top ? P(y - 1, x) : half + 1;
+        if (have_left) at(0, y + min(i, min(h, (int)ib.tile_h - y) - 1), x - 1);
+        else if (have_top) at(0, y - 1, x);
+        else v[0] = half + 1;
         if (needs & 16) {
             const bool hbl = have_left && y + h < (int)ib.tile_h && (ib.flags & MI_INTRA_BOTTOM_LEFT);
-            if (hbl) vBL = P(y + h + min(i, min(h, (int)ib.tile_h - y - h) - 1), x - 1);
-            else vBL = have_left ? P(y + min(h, (int)ib.tile_h - y) - 1, x - 1) : (have_top ? P(y - 1, x) : half + 1);
+            if (hbl) at(1, y + h + min(i, min(h, (int)ib.tile_h - y - h) - 1), x - 1);
+            else if (have_left) at(1, y + min(h, (int)ib.tile_h - y) - 1, x - 1);
+            else if (have_top) at(1, y - 1, x);
+            else v[1] = half + 1;
         }
     }
     if (needs & 2) {
-        if (have_top) vT = P(y - 1, x + min(i, min(w, (int)ib.tile_w - x) - 1));
-        else vT = have_left ? P(y, x - 1) : half - 1;
+        if (have_top) at(2, y - 1, x + min(i, min(w, (int)ib.tile_w - x) - 1));
+        else if (have_left) at(2, y, x - 1);
+        else v[2] = half - 1;
         if (needs & 8) {
             const bool htr = have_top && x + w < (int)ib.tile_w && (ib.flags & MI_INTRA_TOP_RIGHT);
-            if (htr) vTR = P(y - 1, x + w + min(i, min(w, (int)ib.tile_w - x - w) - 1));
-            else vTR = have_top ? P(y - 1, x + min(w, (int)ib.tile_w - x) - 1) : (have_left ? P(y, x - 1) : half - 1);
+            if (htr) at(3, y - 1, x + w + min(i, min(w, (int)ib.tile_w - x - w) - 1));
+            else if (have_top) at(3, y - 1, x + min(w, (int)ib.tile_w - x) - 1);
+            else if (have_left) at(3, y, x - 1);
+            else v[3] = half - 1;
         }
     }
-    if (needs & 4) vC = have_top ? P(y - 1, x - (have_left ? 1 : 0)) : have_left ? P(y, x - 1) : half;
+    if (needs & 4) {
+        if (have_top) at(4, y - 1, x - (have_left ? 1 : 0));
+        else if (have_left) at(4, y, x - 1);
+        else v[4] = half;
+    }
+    if (Fused && gran) {
+        gran_fetch<5>(*gran, x, y, py, px, rd, v);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+            if (rd[k]) v[k] = P(py[k], px[k]);
+    }
+    const int vL = v[0], vBL = v[1], vT = v[2], vTR = v[3], vC = v[4];
     if ((needs & 1) && i < h) {
         tl[-1 - i] = (Px)vL;
         if (needs & 16) tl[-1 - h - i] = (Px)vBL;
@@ -768,7 +882,10 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
         }
         __syncthreads();
         DBG(i, 2);
-        intra_block<Px, true>(fr.ip, ib, eb, ft, edge, lt, acl);
+        GranCtx gc;
+        if (a.gran)
+            gc = gran_ctx(a.gran + fr.goff, fr.pw, fr.ph, fr.ss_hor, fr.ss_ver, fr.nplanes, ib.plane, a.epoch, a.err);
+        intra_block<Px, true>(fr.ip, ib, eb, ft, edge, lt, acl, a.gran ? &gc : nullptr);
         __syncthreads();
         DBG(i, 3);
         switch (tb.tx) {
@@ -781,6 +898,27 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
         DBG(i, 5);
         __syncthreads();
         DBG(i, 6);
+        if (a.gran) {
+            // the edges later blocks read, as granules: right column (lanes 0..h/2-1), bottom
+            // row (lanes 32..32+w/2-1), before the tile's own stores
+            const int w = ib.w, h = ib.h;
+            unsigned long long *gd = nullptr;
+            uint32_t p0 = 0, p1 = 0;
+            if (lane < (h >> 1)) {
+                const int r = 2 * lane;
+                p0 = lt[r * w + w - 1];
+                p1 = lt[(r + 1) * w + w - 1];
+                gd = gc.col + ((ib.x + w) >> 2) * gc.colp + ((ib.y + r) >> 1);
+            } else if (lane >= 32 && lane - 32 < (w >> 1)) {
+                const int c = 2 * (lane - 32);
+                p0 = lt[(h - 1) * w + c];
+                p1 = lt[(h - 1) * w + c + 1];
+                gd = gc.row + ((ib.y + h) >> 2) * gc.rowp + ((ib.x + c) >> 1);
+            }
+            if (gd)
+                __hip_atomic_store(gd, (unsigned long long)(p0 | (p1 << 16)) | ((unsigned long long)a.epoch << 32),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         // store the reconstructed tile: 4-pixel chunks, 4-B (8 bpc) / 8-B (hbd) `sc1` stores
         {
             const int w = ib.w, h = ib.h, cpr = w >> 2;
