@@ -525,8 +525,11 @@ def intra_1080p8(ctx, reps=5, nframes=24, ndesc=4):
         return ev[0].elapsed_time(ev[1]) / reps
 
     with torch.cuda.stream(s):
-        one_ms = timed(lambda: intra_recon(ctx, batch[:1], s, keep_coefs=False))
-        batch_ms = timed(lambda: intra_recon(ctx, batch, s, keep_coefs=False))
+        # edge granules (MI_IR_EDGE_GRANULES: the frames are intra-only) and done flags
+        one_ms = timed(lambda: intra_recon(ctx, batch[:1], s, keep_coefs=False, granules=True))
+        batch_ms = timed(lambda: intra_recon(ctx, batch, s, keep_coefs=False, granules=True))
+        one_flags_ms = timed(lambda: intra_recon(ctx, batch[:1], s, keep_coefs=False))
+        batch_flags_ms = timed(lambda: intra_recon(ctx, batch, s, keep_coefs=False))
         device_status(ctx, s)
         intra, pic = descs[0], batch[0][1]
         g = torch.cuda.CUDAGraph()
@@ -539,8 +542,9 @@ def intra_1080p8(ctx, reps=5, nframes=24, ndesc=4):
                 fps=round(nframes / (batch_ms / 1e3), 1), ms_per_frame=round(one_ms, 3),
                 frames_per_launch=nframes, batch_ms=round(batch_ms, 3),
                 single_frame_mpx_per_s=round(w * h / (one_ms / 1e3) / 1e6, 1),
+                ms_per_frame_flags=round(one_flags_ms, 3), batch_ms_flags=round(batch_flags_ms, 3),
                 level_launch_ms=round(level_ms, 3), levels=len(intra.levels), tx_blocks=int(len(fr["blocks"])),
-                kernel="intra_recon_kernel (persistent, one-wave workers, 3 frames per XCD)")
+                kernel="intra_recon_kernel (persistent, one-wave workers, 3 frames per XCD, edge granules)")
 
 
 def host_cpu():

@@ -327,8 +327,13 @@ int mi_intra_blocks(MiCtx *ctx, const MiPicture *pic, const MiIntraBlock *blocks
  * blocks[n] in an order where every block comes after the blocks it depends on; tx[i] is the
  * residual of blocks[i] (same plane, position and size); deps[dep_start[i] ..
  * dep_start[i + 1]) are the indices (< i) of the blocks owning any pixel blocks[i]'s edges
- * read. flags: MI_ITX_KEEP_COEFS as mi_itx_frame. A worker that waits ~0.5 s for a dependency
- * gives up (no hang); mi_ctx_device_status reports it. */
+ * read. flags: MI_ITX_KEEP_COEFS as mi_itx_frame; MI_IR_EDGE_GRANULES when every pixel any
+ * block's edges read is reconstructed by this call (intra-only frames: no inter-intra or
+ * MI_INTRA_RESID blocks, no inter pixels around the blocks): blocks then hand their right
+ * column and bottom row to later blocks as tagged 8-byte records instead of done flags plus
+ * picture reads, and only CfL and intra block copy blocks wait on their deps. A worker that
+ * waits ~0.5 s for a dependency gives up (no hang); mi_ctx_device_status reports it. */
+#define MI_IR_EDGE_GRANULES 2u
 typedef struct MiIntraFrame {
     MiPicture pic;
     const MiIntraBlock *blocks;

@@ -337,7 +337,7 @@ int mi_intra_blocks(MiCtx *ctx, const MiPicture *pic, const MiIntraBlock *blocks
 }
 
 int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned flags, void *stream) {
-    return mi_internal::intra_recon(ctx, frames, nframes, nullptr, 1, flags, stream);
+    return mi_internal::intra_recon(ctx, frames, nframes, nullptr, 1, flags, stream, (flags & MI_IR_EDGE_GRANULES) != 0);
 }
 
 int mi_ctx_device_status(MiCtx *ctx, void *stream) {
@@ -1630,6 +1630,17 @@ int intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, const int32
     a.dbg = ddbg;
     setenv("MI_IR_DBG_PTR", std::to_string((uintptr_t)dbg).c_str(), 1);
 #endif
+    static const bool tl_env = getenv("MI_IR_TIMELINE") != nullptr;
+    if (tl_env) {
+        if (ctx->ir_tl_n < ctx->ir_done_n) {
+            if (ctx->ir_tl) (void)hipFree(ctx->ir_tl);
+            ctx->ir_tl = nullptr;
+            ctx->ir_tl_n = 0;
+            if (hipMalloc((void **)&ctx->ir_tl, ctx->ir_done_n * 128) != hipSuccess) return fail(ctx, -ENOMEM);
+            ctx->ir_tl_n = ctx->ir_done_n;
+        }
+        a.tl = (uintptr_t)ctx->ir_tl - (uintptr_t)ctx->ir_done * 32;
+    }
     a.epoch = ctx->ir_epoch;
     a.nframes = nq;
     a.zero_coefs = (flags & MI_ITX_KEEP_COEFS) ? 0 : 1;

@@ -242,6 +242,9 @@ struct IntraReconArgs {
     // 4-px column boundary and its bottom row at its row boundary, as 8-B {two pixels, epoch}
     // records a consumer polls instead of a done flag plus pixel loads (ipred.hip)
     unsigned long long *gran;
+    // MI_IR_TIMELINE (diagnostics): 16 s_memrealtime stamps per unit, parallel to the done words:
+    // unit stamps at tl + 32 * (byte address of its done word), tl biased by the host
+    uintptr_t tl;
     uint32_t epoch;
     int nframes, zero_coefs;
 };

@@ -20,6 +20,8 @@ struct MiCtx {
     uint32_t ir_epoch = 0;        // never reset: done words and edge granules hold old epochs
     unsigned long long *ir_gran = nullptr;   // edge granules (ipred.hip GranCtx), zeroed when allocated
     size_t ir_gran_n = 0;
+    unsigned long long *ir_tl = nullptr;     // MI_IR_TIMELINE stamps (diagnostics)
+    size_t ir_tl_n = 0;
     // frame executor (frame_exec.cpp): device copy of one frame's descriptors, staged through
     // pinned host memory; `fx_ev` marks when the staging buffer may be rewritten
     uint8_t *fx_dev = nullptr, *fx_host = nullptr;
@@ -48,6 +50,7 @@ struct MiCtx {
         if (ir_done) (void)hipFree(ir_done);
         if (ir_words) (void)hipFree(ir_words);
         if (ir_gran) (void)hipFree(ir_gran);
+        if (ir_tl) (void)hipFree(ir_tl);
         if (fg_lut) (void)hipFree(fg_lut);
         if (fg_scaling) (void)hipFree(fg_scaling);
         if (fg_offsets) (void)hipFree(fg_offsets);

@@ -15,6 +15,7 @@
 // device fault), then copied into one pinned staging blob and uploaded with a single async
 // copy.
 #include <errno.h>
+#include <stdio.h>
 #include <string.h>
 #include <algorithm>
 #include <cstdlib>
@@ -290,9 +291,10 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
 // neighbour superblock or the superblock row above; an intra block copy source lies a
 // superblock row above or 256 px left of the current superblock, spec 7.11.2 / rav1d
 // decode.rs); if one did not, the frame stays on one XCD. Returns the number of strips (1: no
-// split); strip[i] per block, extra deps as CSR.
+// split); strip[i] per block, extra deps as CSR. With edge granules (frame_run) a block reads
+// the picture only for intra block copy and CfL's luma: edges need no extra deps.
 int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<int32_t> &xs,
-                 std::vector<int32_t> &xd) {
+                 std::vector<int32_t> &xd, bool granules) {
     static const int env = getenv("MI_IR_STRIPS") ? atoi(getenv("MI_IR_STRIPS")) : 8;
     const int n = f->n_intra;
     const int maxs = std::min(8, env);
@@ -349,6 +351,7 @@ int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<in
             const int j = f->deps[d];
             if (strip[j] == strip[i]) continue;
             const MiIntraBlock &o = f->intra[j];
+            if (granules && o.plane == p && b.mode != MI_INTRA_IBC) continue;   // an edge: granules
             if (o.plane != p) return 1;                       // (CfL luma: same strip by construction)
             const int x0 = std::max(bx0, (int)o.x), x1 = std::min(bx1, o.x + o.w);
             const int y0 = std::max(by0, (int)o.y), y1 = std::min(by1, o.y + o.h);
@@ -535,12 +538,15 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
     }();
     const bool inter = inter_present(f) || f->n_inter_tx;
     bool granules = gran_env && !inter && n > 0;
+    // MI_IR_TIMELINE=<file> (diagnostics): the launch's per-unit stamps, blocks and dependencies
+    static const char *tl_path = getenv("MI_IR_TIMELINE");
+    std::vector<int32_t> tl_ds, tl_deps, tl_strip;
     for (int i = 0; granules && i < n; i++)
         if ((f->intra[i].flags & MI_INTRA_II) || f->intra[i].mode == MI_INTRA_RESID) granules = false;
     if (n) {
         std::vector<int32_t> xs, xd;          // extra dependencies of the strip split (CSR)
         std::vector<int8_t> strip;
-        const int nstrips = intra_strips(f, strip, xs, xd);
+        const int nstrips = intra_strips(f, strip, xs, xd, granules);
         auto each_dep = [&](int i, auto &&fn) {
             for (int d = f->dep_start[i]; d < f->dep_start[i + 1]; d++) fn(f->deps[d]);
             if (nstrips > 1)
@@ -582,6 +588,16 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
             }
         }
         dep_start[n] = (int32_t)deps.size();
+        if (tl_path) {
+            // every dependency (with the strips' extra ones), in queue order
+            tl_ds.assign(n + 1, 0);
+            for (int k = 0; k < n; k++) {
+                tl_ds[k] = (int32_t)tl_deps.size();
+                each_dep(inv[k], [&](int d) { tl_deps.push_back(pos[d]); });
+            }
+            tl_ds[n] = (int32_t)tl_deps.size();
+            tl_strip.assign(strip_start.begin(), strip_start.end());
+        }
     }
     if (deps.empty()) deps.push_back(0);
     if (ctx->tm_on) ctx->tm_strips_ms += std::chrono::duration<double, std::milli>(clk::now() - t_lv).count();
@@ -702,6 +718,22 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         if ((r = mi_internal::intra_recon(ctx, &fr, 1, strip_start.empty() ? nullptr : strip_start.data(),
                                           (int)strip_start.size() - 1, 0, stream, granules)))
             return r;
+        if (tl_path && n > 1000) {
+            std::vector<unsigned long long> t((size_t)n * 16);
+            if (hipStreamSynchronize(s) == hipSuccess &&
+                hipMemcpy(t.data(), ctx->ir_tl, t.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+                if (FILE *fp = fopen(tl_path, "ab")) {
+                    const int32_t hdr[4] = { n, (int32_t)tl_deps.size(), (int32_t)tl_strip.size(), granules };
+                    fwrite(hdr, 4, 4, fp);
+                    fwrite(t.data(), 8, t.size(), fp);
+                    fwrite(blocks.data(), sizeof(MiIntraBlock), n, fp);
+                    fwrite(tl_ds.data(), 4, tl_ds.size(), fp);
+                    fwrite(tl_deps.data(), 4, tl_deps.size(), fp);
+                    fwrite(tl_strip.data(), 4, tl_strip.size(), fp);
+                    fclose(fp);
+                }
+            }
+        }
     }
     tev.mark(3, s);
     // the coded-width views of the pictures (stages before super-resolution)

@@ -29,8 +29,25 @@ __constant__ int8_t k_filter_intra_taps[5][64] = {
 };
 
 // TxfmType -> 1-D kinds (as itx.hip's k_row_kind / k_col_kind; levels.rs TxfmType is VERT_HORZ)
-__constant__ uint8_t k_col_kind_ip[16] = { KD, KA, KD, KA, KF, KD, KF, KA, KF, KI, KD, KI, KA, KI, KF, KI };
-__constant__ uint8_t k_row_kind_ip[16] = { KD, KD, KA, KA, KD, KF, KF, KF, KA, KI, KI, KD, KI, KA, KI, KF };
+// (2 bits per type, packed in an immediate: a table in memory is a scalar load per block)
+//   column: { KD, KA, KD, KA, KF, KD, KF, KA, KF, KI, KD, KI, KA, KI, KF, KI }
+//   row:    { KD, KD, KA, KA, KD, KF, KF, KF, KA, KI, KI, KD, KI, KA, KI, KF }
+__device__ __forceinline__ int col_kind_ip(int t) { return (int)((0xedce6244u >> (2 * t)) & 3); }
+__device__ __forceinline__ int row_kind_ip(int t) { return (int)((0xb73da850u >> (2 * t)) & 3); }
+
+// Sum over the wave by DPP row shifts and row broadcasts (VALU only, no LDS round trips), the
+// total read from lane 63
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+    int s = v;
+    s += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    s += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    s += __builtin_amdgcn_update_dpp(0, v, 0x113, 0xf, 0xf, false);   // row_shr:3
+    s += __builtin_amdgcn_update_dpp(0, s, 0x114, 0xf, 0xe, false);   // row_shr:4, banks 1-3
+    s += __builtin_amdgcn_update_dpp(0, s, 0x118, 0xf, 0xc, false);   // row_shr:8, banks 2-3
+    s += __builtin_amdgcn_update_dpp(0, s, 0x142, 0xa, 0xf, false);   // row_bcast:15, rows 1, 3
+    s += __builtin_amdgcn_update_dpp(0, s, 0x143, 0xc, 0xf, false);   // row_bcast:31, rows 2-3
+    return __builtin_amdgcn_readlane(s, 63);
+}
 
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
@@ -87,15 +104,46 @@ __device__ void upsample_edge_par(int *out, int hsz, const Px *in_, int from, in
     }
 }
 
+// plane base / stride by a (wave-uniform) plane index as selects: an indexed array of a
+// register-held argument struct would put the struct in scratch
+__device__ __forceinline__ uint8_t *plane_ptr(const IpredArgs &a, int p) {
+    return p == 0 ? a.dst[0] : p == 1 ? a.dst[1] : a.dst[2];
+}
+__device__ __forceinline__ int64_t plane_stride(const IpredArgs &a, int p) { return p ? a.stride[1] : a.stride[0]; }
+
+#ifdef MI_IR_EXP_DCSTAMP
+// (experiment: DC-path stamps k into the edge scratch eb[240 + 2k], read back by the kernel)
+#define DCSTAMP(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); \
+    if (threadIdx.x == 0) { eb[240 + 2 * (k)] = (int)t_; eb[241 + 2 * (k)] = (int)(t_ >> 32); } } while (0)
+#else
+#define DCSTAMP(k) do {} while (0)
+#endif
+// DC_PRED / LEFT_DC / TOP_DC (m 0 / 3 / 4) from the sum s of the edge samples they average
+// (ipred_tmpl.c:86-160: the 1/3 and 1/5 multipliers of rectangular blocks)
+__device__ __forceinline__ int dc_of_sum(int m, int s, int w, int h, int bpc) {
+    if (m == 4) return (s + (w >> 1)) >> (__ffs(w) - 1);
+    if (m == 3) return (s + (h >> 1)) >> (__ffs(h) - 1);
+    unsigned d = ((unsigned)s + ((w + h) >> 1)) >> (__ffs(w + h) - 1);
+    if (w != h) {
+        const bool q = w > h * 2 || h > w * 2;
+        if (bpc == 8) d = (d * (q ? 0x3334u : 0x5556u)) >> 16;
+        else d = (d * (q ? 0x6667u : 0xAAABu)) >> 17;
+    }
+    return (int)d;
+}
+
 // Predict one block from its gathered edge `tl` (global edge buffer or LDS). eb / ft: LDS
 // scratch for the directional edge and the filter-intra image.
 template <typename Px, bool ToLds = false>
 __device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredBlock &b, const Px *tl, int *eb, Px *ft,
-                                              Px *lt = nullptr, const int16_t *acl = nullptr) {
+                                              Px *lt = nullptr, const int16_t *acl = nullptr,
+                                              const int16_t *res = nullptr, int rdc = 0, int dcs = -1) {
     const int lane = threadIdx.x;
     const int w = b.w, h = b.h, n = w * h;
-    const int64_t st = a.stride[b.plane ? 1 : 0];
-    uint8_t *dst = a.dst[b.plane] + (int64_t)b.y * st + (int64_t)b.x * sizeof(Px);
+    // (w is a power of two: row / column of pixel i by shift and mask, not a division)
+    const int lw = 31 - __clz(w);
+    const int64_t st = plane_stride(a, b.plane);
+    uint8_t *dst = plane_ptr(a, b.plane) + (int64_t)b.y * st + (int64_t)b.x * sizeof(Px);
     const int bdmax = a.bdmax;
     // inter-intra (MI_IPRED_II): blend into the inter prediction with the block's mask
     // (mc.blend, mc_tmpl.c:621-630); the address is formed before the uniform branch
@@ -103,54 +151,58 @@ __device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredB
     const uint8_t *iim = a.idx + b.aux_off;
     // ToLds: the prediction goes to the w x h LDS tile lt (the fused intra reconstruction
     // adds the residual there); otherwise into the picture
+    // ToLds: plus the block's residual (res, or the DC-only block's constant rdc), clipped
     auto put = [&](int y, int x, int v) {
         Px *d = ToLds ? lt + y * w + x : reinterpret_cast<Px *>(dst + (int64_t)y * st) + x;
         if (ii) {
             const int m = iim[y * w + x];
             v = (*d * (64 - m) + v * m + 32) >> 6;
         }
+        if constexpr (ToLds) v = clampi(v + (res ? (int)res[y * w + x] : rdc), 0, bdmax);
         *d = (Px)v;
     };
     const int mode = b.mode & ~MI_IPRED_II;
 
     if (mode >= MI_IPRED_PAL) {                      // pal_pred: palette at edge_off, indices in idx
         const uint8_t *idx = a.idx + b.aux_off;
-        for (int i = lane; i < n; i += 64) put(i / w, i % w, tl[idx[i]]);
+        for (int i = lane; i < n; i += 64) put((i >> lw), (i & (w - 1)), tl[idx[i]]);
         return;
     }
     const bool cfl = mode >= MI_IPRED_CFL;
     const int m = cfl ? mode - MI_IPRED_CFL : mode;
     if (m == 0 || m == 3 || m == 4 || m == 5) {
         // DC family (ipred_tmpl.c:86-218) -> splat or CfL
+        DCSTAMP(0);
         int dc;
         if (m == 5) {
             dc = (bdmax + 1) >> 1;
         } else {
             int s = 0;
-            if (m != 3) for (int i = lane; i < w; i += 64) s += tl[1 + i];
-            if (m != 4) for (int i = lane; i < h; i += 64) s += tl[-(1 + i)];
-            s = wave_sum(s);
-            if (m == 4) dc = (s + (w >> 1)) >> __ffs(w) - 1;
-            else if (m == 3) dc = (s + (h >> 1)) >> __ffs(h) - 1;
-            else {
-                unsigned d = ((unsigned)s + ((w + h) >> 1)) >> (__ffs(w + h) - 1);
-                if (w != h) {
-                    const bool q = w > h * 2 || h > w * 2;
-                    if (a.bpc == 8) d = (d * (q ? 0x3334u : 0x5556u)) >> 16;
-                    else d = (d * (q ? 0x6667u : 0xAAABu)) >> 17;
-                }
-                dc = (int)d;
+            if (dcs >= 0) {
+                s = dcs;                             // (summed by the caller from its registers)
+            } else if (w + h <= 16) {
+                // a few samples: every lane sums them itself (broadcast LDS reads), no
+                // cross-lane reduction chain
+                if (m != 3) for (int i = 0; i < w; i++) s += tl[1 + i];
+                if (m != 4) for (int i = 0; i < h; i++) s += tl[-(1 + i)];
+            } else {
+                if (m != 3) for (int i = lane; i < w; i += 64) s += tl[1 + i];
+                if (m != 4) for (int i = lane; i < h; i += 64) s += tl[-(1 + i)];
+                s = wave_sum(s);
             }
+            dc = dc_of_sum(m, s, w, h, a.bpc);
         }
+        DCSTAMP(1);
         if (!cfl) {
-            for (int i = lane; i < n; i += 64) put(i / w, i % w, dc);
+            for (int i = lane; i < n; i += 64) put((i >> lw), (i & (w - 1)), dc);
+            DCSTAMP(2);
         } else {
             const int16_t *ac = acl ? acl : a.ac + b.aux_off;
             const int alpha = b.alpha;
             for (int i = lane; i < n; i += 64) {
                 const int diff = alpha * ac[i];
                 const int mag = (abs(diff) + 32) >> 6;
-                put(i / w, i % w, min(max(dc + (diff < 0 ? -mag : mag), 0), bdmax));
+                put((i >> lw), (i & (w - 1)), min(max(dc + (diff < 0 ? -mag : mag), 0), bdmax));
             }
         }
         return;
@@ -159,17 +211,17 @@ __device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredB
     // no per-pixel mode branch (a merged per-pixel three-way branch here was miscompiled by
     // hipcc 7.2: the store address was left undefined on one path)
     if (m == 1) {
-        for (int i = lane; i < n; i += 64) put(i / w, i % w, tl[1 + i % w]);
+        for (int i = lane; i < n; i += 64) put((i >> lw), (i & (w - 1)), tl[1 + (i & (w - 1))]);
         return;
     }
     if (m == 2) {
-        for (int i = lane; i < n; i += 64) put(i / w, i % w, tl[-(1 + i / w)]);
+        for (int i = lane; i < n; i += 64) put((i >> lw), (i & (w - 1)), tl[-(1 + (i >> lw))]);
         return;
     }
     if (m == 12) {
         const int c = tl[0];
         for (int i = lane; i < n; i += 64) {
-            const int y = i / w, x = i % w;
+            const int y = (i >> lw), x = (i & (w - 1));
             const int top = tl[1 + x], left = tl[-(1 + y)];
             const int base = left + top - c;
             const int ld = abs(left - base), td = abs(top - base), tld = abs(c - base);
@@ -180,7 +232,7 @@ __device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredB
     if (m == 9) {
         const int right = tl[w], bottom = tl[-h];
         for (int i = lane; i < n; i += 64) {
-            const int y = i / w, x = i % w;
+            const int y = (i >> lw), x = (i & (w - 1));
             const int wv = k_sm_weights[h + y], wh = k_sm_weights[w + x];
             put(y, x, (wv * tl[1 + x] + (256 - wv) * bottom + wh * tl[-(1 + y)] + (256 - wh) * right + 256) >> 9);
         }
@@ -189,7 +241,7 @@ __device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredB
     if (m == 10) {
         const int bottom = tl[-h];
         for (int i = lane; i < n; i += 64) {
-            const int y = i / w, x = i % w;
+            const int y = (i >> lw), x = (i & (w - 1));
             const int wv = k_sm_weights[h + y];
             put(y, x, (wv * tl[1 + x] + (256 - wv) * bottom + 128) >> 8);
         }
@@ -198,7 +250,7 @@ __device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredB
     if (m == 11) {
         const int right = tl[w];
         for (int i = lane; i < n; i += 64) {
-            const int y = i / w, x = i % w;
+            const int y = (i >> lw), x = (i & (w - 1));
             const int wh = k_sm_weights[w + x];
             put(y, x, (wh * tl[-(1 + y)] + (256 - wh) * right + 128) >> 8);
         }
@@ -225,7 +277,7 @@ __device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredB
         __syncthreads();
         const int base_inc = 1 + up;
         for (int i = lane; i < n; i += 64) {
-            const int y = i / w, x = i % w;
+            const int y = (i >> lw), x = (i & (w - 1));
             const int xpos = (y + 1) * dx, frac = xpos & 0x3E, base = (xpos >> 6) + x * base_inc;
             put(y, x, base < max_base_x ? (eb[base] * (64 - frac) + eb[base + 1] * frac + 32) >> 6 : eb[max_base_x]);
         }
@@ -261,7 +313,7 @@ __device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredB
         const int base_inc_x = 1 + up_above;
         const int lo = 64 - (1 + up_left);           // eb index of left[0]
         for (int i = lane; i < n; i += 64) {
-            const int y = i / w, x = i % w;
+            const int y = (i >> lw), x = (i & (w - 1));
             const int xpos = ((1 + up_above) << 6) - (y + 1) * dx;
             const int base_x = (xpos >> 6) + x * base_inc_x, frac_x = xpos & 0x3E;
             const int ti = min(max(64 + base_x, 0), 2 * 128);
@@ -298,7 +350,7 @@ __device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredB
         __syncthreads();
         const int base_inc = 1 + up;
         for (int i = lane; i < n; i += 64) {
-            const int y = i / w, x = i % w;
+            const int y = (i >> lw), x = (i & (w - 1));
             const int ypos = (x + 1) * dy, frac = ypos & 0x3E, base = (ypos >> 6) + y * base_inc;
             put(y, x, base < max_base_y ? (eb[lbase - base] * (64 - frac) + eb[lbase - base - 1] * frac + 32) >> 6
                                         : eb[lbase - max_base_y]);
@@ -332,7 +384,7 @@ __device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredB
             }
             __syncthreads();
         }
-        for (int i = lane; i < n; i += 64) put(i / w, i % w, ft[i]);
+        for (int i = lane; i < n; i += 64) put((i >> lw), (i & (w - 1)), ft[i]);
     }
 }
 
@@ -348,8 +400,13 @@ __global__ __launch_bounds__(64) void ipred_kernel(IpredArgs a) {
 
 // av1_intra_prediction_edges needs per implementation mode: LEFT 1, TOP 2, TOP_LEFT 4,
 // TOP_RIGHT 8, BOTTOM_LEFT 16 (ipred_prepare.rs:76-115)
-__constant__ uint8_t k_needs[14] = { 3, 2, 1, 1, 2, 0, 14, 7, 21, 3, 3, 3, 7, 7 };
-__constant__ uint8_t k_mode_angle[8] = { 90, 180, 45, 135, 113, 157, 203, 67 };
+// (5 bits per mode: { 3, 2, 1, 1, 2, 0, 14, 7, 21, 3, 3, 3, 7, 7 }; packed immediates, as the
+// transform kinds)
+__device__ __forceinline__ int needs_of(int m) {
+    return m < 12 ? (int)((0x718c753b80208443ull >> (5 * m)) & 31) : (int)(((0x718c753b80208443ull >> 60) | (0xeull << 4)) >> (5 * (m - 12)) & 31);
+}
+// base angles of the directional modes 1..8 { 90, 180, 45, 135, 113, 157, 203, 67 }
+__device__ __forceinline__ int mode_angle(int k) { return (int)((0x43cb9d71872db45aull >> (8 * k)) & 255); }
 
 // cfl_ac (ipred.rs:1326-1432; C ipred_tmpl.c:658-700) by one wave: each AC sample is the sum
 // of its 1/2/4 luma pixels scaled to <<3 in total, w_pad / h_pad 4-px groups replicate the last
@@ -359,11 +416,17 @@ __constant__ uint8_t k_mode_angle[8] = { 90, 180, 45, 135, 113, 157, 203, 67 };
 // A pixel read of the persistent kernel's hand-off: the aligned 4-byte word holding it, loaded
 // `sc1` (L1-bypassing, agent scope), and the pixel extracted. MI355X_MICROARCH.md's hand-off
 // table (row 1) covers 4-, 8- and 16-B `sc1` loads of bytes stored `sc1`, not 1-/2-B loads.
+// global (address space 1) `sc1` loads: a generic pointer would make them flat loads, which
+// also count in lgkmcnt and are not the `global_` form the hand-off rules name
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T *q) {
+    typedef __attribute__((address_space(1))) const T *gp;
+    return __hip_atomic_load((gp)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 template <typename Px>
 __device__ __forceinline__ int ld_px_sc1(const Px *q) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(q);
-    const uint32_t w = __hip_atomic_load(reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t w = ld_sc1(reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3));
     if constexpr (sizeof(Px) == 1) return (w >> (8 * (a & 3))) & 0xff;
     else return (w >> (8 * (a & 2))) & 0xffff;
 }
@@ -436,25 +499,23 @@ __device__ __forceinline__ GranCtx gran_ctx(unsigned long long *base, int pw, in
 }
 // The edge pixels (yy[k], xx[k]) (use[k]) of the block at (x, y) from the granules: a left-column
 // pixel from the column boundary x, a top-row pixel from the row boundary y, the top-left corner
-// from whichever of the two its block wrote. Every lane polls its records until each carries this
-// launch's epoch (one round of loads in the common case); bounded like the flag wait.
+// (only ever sample K-1) from whichever of the two its block wrote. Every lane polls its records
+// until each carries this launch's epoch, with two rounds of loads in flight (a record that
+// turns valid is seen about half a round trip sooner than by one load at a time); bounded like
+// the flag wait.
 template <int K>
 __device__ __forceinline__ void gran_fetch(const GranCtx &g, int x, int y, const int (&yy)[K], const int (&xx)[K],
                                            const bool (&use)[K], int (&out)[K]) {
-    const unsigned long long *pa[K], *pb[K];
-    int sa[K], sb[K];
+    const unsigned long long *pa[K], *pc;
+    int sa[K], sc = 0;
     bool ok[K];
 #pragma unroll
     for (int k = 0; k < K; k++) {
         ok[k] = !use[k];
-        pb[k] = nullptr;
-        sa[k] = sb[k] = 0;
-        if (xx[k] == x - 1 && yy[k] == y - 1) {
-            pa[k] = g.col + (x >> 2) * g.colp + ((y - 1) >> 1);
-            sa[k] = ((y - 1) & 1) * 16;
-            pb[k] = g.row + (y >> 2) * g.rowp + ((x - 1) >> 1);
-            sb[k] = ((x - 1) & 1) * 16;
-        } else if (xx[k] == x - 1) {
+        sa[k] = 0;
+        pa[k] = g.col;                                   // (unused samples: any valid record)
+        if (!use[k]) continue;
+        if (xx[k] == x - 1) {
             pa[k] = g.col + (x >> 2) * g.colp + (yy[k] >> 1);
             sa[k] = (yy[k] & 1) * 16;
         } else {
@@ -462,46 +523,80 @@ __device__ __forceinline__ void gran_fetch(const GranCtx &g, int x, int y, const
             sa[k] = (xx[k] & 1) * 16;
         }
     }
-    for (unsigned spins = 0;; spins++) {
+    // the corner's second record (row boundary y), if sample K-1 is the corner
+    const bool corner = use[K - 1] && xx[K - 1] == x - 1 && yy[K - 1] == y - 1;
+    pc = pa[K - 1];
+    if (corner) {
+        pc = g.row + (y >> 2) * g.rowp + ((x - 1) >> 1);
+        sc = ((x - 1) & 1) * 16;
+    }
+    auto ld = [](const unsigned long long *q) { return ld_sc1(q); };
+    auto take = [&](const unsigned long long (&v)[K], unsigned long long vc) {
 #pragma unroll
         for (int k = 0; k < K; k++) {
             if (ok[k]) continue;
-            unsigned long long v = __hip_atomic_load(pa[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((uint32_t)(v >> 32) == g.epoch) {
-                out[k] = (int)((v >> sa[k]) & 0xffff);
+            if ((uint32_t)(v[k] >> 32) == g.epoch) {
+                out[k] = (int)((v[k] >> sa[k]) & 0xffff);
                 ok[k] = true;
-            } else if (pb[k]) {
-                v = __hip_atomic_load(pb[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((uint32_t)(v >> 32) == g.epoch) {
-                    out[k] = (int)((v >> sb[k]) & 0xffff);
-                    ok[k] = true;
-                }
+            } else if (k == K - 1 && corner && (uint32_t)(vc >> 32) == g.epoch) {
+                out[k] = (int)((vc >> sc) & 0xffff);
+                ok[k] = true;
             }
         }
         bool all = true;
 #pragma unroll
         for (int k = 0; k < K; k++) all = all && ok[k];
-        if (__builtin_amdgcn_ballot_w64(!all) == 0) break;
+        return __builtin_amdgcn_ballot_w64(!all) == 0;
+    };
+    unsigned long long v0[K], v1[K], c0, c1;
+#pragma unroll
+    for (int k = 0; k < K; k++) v0[k] = ld(pa[k]);
+    c0 = ld(pc);
+    for (unsigned spins = 0;; spins++) {
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int k = 0; k < K; k++) v1[k] = ld(pa[k]);
+        c1 = ld(pc);
+        if (take(v0, c0)) break;
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int k = 0; k < K; k++) v0[k] = ld(pa[k]);
+        c0 = ld(pc);
+        if (take(v1, c1)) break;
         if (spins > (1u << MI_IR_GRAN_SPIN_LOG2)) {
             atomicOr(g.err, 1);
             break;
         }
-        __builtin_amdgcn_s_sleep(1);
     }
+#ifdef MI_IR_EXP_DRAIN
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 }
+
+// intra_block's result: MI_IR_TIMELINE stamps, and the value of a plain DC-family block that
+// was not written to the tile (-1: the tile holds the block)
+struct IntraOut {
+    unsigned long long tlx;
+    int dcv;
+};
 
 // Gather one block's edges from the picture (rav1d_prepare_intra_edges) and predict it, one
 // wave. Fused (the persistent reconstruction kernel): neighbour pixels were stored by other
 // CUs of this XCD during the launch, so every picture read is an L1-bypassing `sc1` load
 // (L2-served), and the prediction goes to the LDS tile lt.
 template <typename Px, bool Fused>
-__device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlock &ib, int *eb, Px *ft, Px *edge,
-                                            Px *lt, int16_t *acl, const GranCtx *gran = nullptr) {
+__device__ __forceinline__ IntraOut intra_block(const IpredArgs &a, const MiIntraBlock &ib, int *eb, Px *ft, Px *edge,
+                                            Px *lt, int16_t *acl, const int16_t *res = nullptr, int rdc = 0,
+                                            bool use_gran = false, GranCtx gran = {}, bool tlv = false) {
     const int lane = threadIdx.x;
+    // MI_IR_TIMELINE stamps 7..10 (lane k keeps stamp k), returned to the caller
+    unsigned long long tlx = 0;
+#define TLV(k) do { if (tlv) { const unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); if (lane == (k)) tlx = t_; } } while (0)
     const int w = ib.w, h = ib.h, x = ib.x, y = ib.y;
+    const int lw = 31 - __clz(w);                // (w a power of two)
     const bool have_left = ib.flags & MI_INTRA_HAVE_LEFT, have_top = ib.flags & MI_INTRA_HAVE_TOP;
-    const int64_t st = a.stride[ib.plane ? 1 : 0];
-    const Px *pic = reinterpret_cast<const Px *>(a.dst[ib.plane]);
+    const int64_t st = plane_stride(a, ib.plane);
+    const Px *pic = reinterpret_cast<const Px *>(plane_ptr(a, ib.plane));
     auto P = [&](int yy, int xx) -> int {
         const Px *q = reinterpret_cast<const Px *>(reinterpret_cast<const uint8_t *>(pic) + (int64_t)yy * st) + xx;
         if constexpr (Fused) return ld_px_sc1(q);
@@ -511,9 +606,13 @@ __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlo
         // inter-intra blends into the block's existing (inter) pixels, and the residual of an
         // inter-intra block (MI_INTRA_RESID) adds to them: start the tile from them
         if ((ib.flags & MI_INTRA_II) || ib.mode == MI_INTRA_RESID)
-            for (int i = lane; i < w * h; i += 64) lt[i] = (Px)P(y + i / w, x + i % w);
+            for (int i = lane; i < w * h; i += 64) lt[i] = (Px)P(y + (i >> lw), x + (i & (w - 1)));
     }
-    if (ib.mode == MI_INTRA_RESID) return;
+    if (ib.mode == MI_INTRA_RESID) {
+        if constexpr (Fused)
+            for (int i = lane; i < w * h; i += 64) lt[i] = (Px)clampi((int)lt[i] + (res ? (int)res[i] : rdc), 0, a.bdmax);
+        return { tlx, -1 };
+    }
     const int bd = a.bpc;
     if (ib.mode == MI_INTRA_IBC) {
         // intra block copy: bilinear put_bilin_c (mc_tmpl.c) from the already reconstructed
@@ -530,7 +629,7 @@ __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlo
         const int cw = ib.max_w - 1, chh = ib.max_h - 1;
         auto Q = [&](int yy, int xx) { return P(min(max(yy, 0), chh), min(max(xx, 0), cw)); };
         for (int i = lane; i < w * h; i += 64) {
-            const int yy = i / w, xx = i % w, py = sy + yy, px = sx + xx;
+            const int yy = (i >> lw), xx = (i & (w - 1)), py = sy + yy, px = sx + xx;
             const int s00 = Q(py, px);
             int v;
             if (mx && my) {
@@ -546,10 +645,10 @@ __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlo
                 v = s00;
             }
             v = min(max(v, 0), bdmax);
-            if constexpr (Fused) lt[i] = (Px)v;
-            else reinterpret_cast<Px *>(a.dst[ib.plane] + (int64_t)(y + yy) * st)[x + xx] = (Px)v;
+            if constexpr (Fused) lt[i] = (Px)clampi(v + (res ? (int)res[i] : rdc), 0, bdmax);
+            else reinterpret_cast<Px *>(plane_ptr(a, ib.plane) + (int64_t)(y + yy) * st)[x + xx] = (Px)v;
         }
-        return;
+        return { tlx, -1 };
     }
 
     MiIpredBlock b;
@@ -568,14 +667,14 @@ __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlo
     if (ib.mode == MI_IPRED_PAL) {
         b.mode = MI_IPRED_PAL;
         b.angle = 0;
-        predict_block<Px, Fused>(a, b, reinterpret_cast<const Px *>(a.pal) + ib.pal_off, eb, ft, lt);
-        return;
+        predict_block<Px, Fused>(a, b, reinterpret_cast<const Px *>(a.pal) + ib.pal_off, eb, ft, lt, nullptr, res, rdc);
+        return { tlx, -1 };
     }
     // mode remap (ipred_prepare.rs:148-172): all wave-uniform
     const bool cfl = ib.mode == MI_IPRED_CFL;
     int m = cfl ? 0 : ib.mode, angle = 0;
     if (m >= 1 && m <= 8) {
-        angle = k_mode_angle[m - 1] + 3 * ib.angle;
+        angle = mode_angle(m - 1) + 3 * ib.angle;
         if (angle <= 90) m = angle < 90 && have_top ? 6 : 1;
         else if (angle < 180) m = 7;
         else m = angle > 180 && have_left ? 8 : 2;
@@ -586,7 +685,7 @@ __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlo
     } else if (m == 13) {
         angle = ib.filt_idx;
     }
-    const int needs = k_needs[m];
+    const int needs = needs_of(m);
     Px *tl = edge + 128;
     const int tw4 = w >> 2, th4 = h >> 2;
     // Every edge sample in one round of loads (w, h <= 64: lane i owns sample i of each
@@ -631,14 +730,24 @@ __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlo
         else if (have_left) at(4, y, x - 1);
         else v[4] = half;
     }
-    if (Fused && gran) {
-        gran_fetch<5>(*gran, x, y, py, px, rd, v);
+    if (Fused && use_gran) {
+        gran_fetch<5>(gran, x, y, py, px, rd, v);
+        TLV(7);
     } else {
 #pragma unroll
         for (int k = 0; k < 5; k++)
             if (rd[k]) v[k] = P(py[k], px[k]);
     }
+    TLV(8);
     const int vL = v[0], vBL = v[1], vT = v[2], vTR = v[3], vC = v[4];
+    // DC family: the edge sum from the registers (lane i holds left[i] and top[i])
+    int dcs = -1;
+    if (Fused && (m == 0 || m == 3 || m == 4))
+        dcs = wave_sum_dpp((m != 3 && i < w ? vT : 0) + (m != 4 && i < h ? vL : 0));
+    // a plain DC-family block is one value: returned, no edge staging and no LDS tile (the
+    // caller stores dc + residual directly)
+    if (Fused && !cfl && !ii && (m == 0 || m == 3 || m == 4 || m == 5))
+        return { tlx, m == 5 ? (1 << bd) >> 1 : dc_of_sum(m, dcs, w, h, bd) };
     if ((needs & 1) && i < h) {
         tl[-1 - i] = (Px)vL;
         if (needs & 16) tl[-1 - h - i] = (Px)vBL;
@@ -655,6 +764,7 @@ __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlo
         tl[0] = (Px)c;
     }
     __syncthreads();
+    TLV(9);
     b.mode = (uint8_t)((cfl ? MI_IPRED_CFL + m : m) | ii);
     b.angle = (uint16_t)(angle | (ib.flags & MI_INTRA_SMOOTH_NB ? 512 : 0) | (ib.flags & MI_INTRA_EDGE_FILTER ? 1024 : 0));
     if (m == 13) b.angle = (uint16_t)ib.filt_idx;
@@ -663,10 +773,12 @@ __device__ __forceinline__ void intra_block(const IpredArgs &a, const MiIntraBlo
         const int ssh = (ib.reserved >> 16) & 1, ssv = (ib.reserved >> 17) & 1;
         const uint8_t *yb = a.dst[0] + (int64_t)(y << ssv) * a.stride[0] + (int64_t)(x << ssh) * sizeof(Px);
         cfl_ac_wave<Px, Fused>(acl, yb, a.stride[0], ib.reserved & 0xff, (ib.reserved >> 8) & 0xff, w, h, ssh, ssv);
-        predict_block<Px, Fused>(a, b, tl, eb, ft, lt, acl);
-        return;
+        predict_block<Px, Fused>(a, b, tl, eb, ft, lt, acl, res, rdc, dcs);
+        return { tlx, -1 };
     }
-    predict_block<Px, Fused>(a, b, tl, eb, ft, lt);
+    predict_block<Px, Fused>(a, b, tl, eb, ft, lt, nullptr, res, rdc, dcs);
+    TLV(10);
+    return { tlx, -1 };
 }
 
 template <typename Px>
@@ -708,11 +820,11 @@ __device__ __forceinline__ unsigned xcc_id() {
     return v & 0xf;
 }
 
-// Inverse transform of one block by one wave, in two halves: itx_rows (coefficients only, so
-// it runs while the block still waits for its neighbours) leaves the shifted/clipped rows in
-// tmp, or returns the DC-only block's value; itx_cols adds the columns' residual into the
-// w x h LDS tile lt. The per-block semantics of itx_size (itx.hip): lane j = row j, then
-// column j.
+// Inverse transform of one block by one wave, in two halves, both from the coefficients only,
+// so both run while the block still waits for its neighbours: itx_rows leaves the
+// shifted/clipped rows in tmp, or returns the DC-only block's value; itx_cols leaves the w x h
+// residual in res (int16), which the prediction's stores add (predict_block's put). The
+// per-block semantics of itx_size (itx.hip): lane j = row j, then column j.
 template <int TX, typename Px, typename Cf, typename Lt, bool Wide>
 __device__ __forceinline__ int itx_rows(const MiTxBlock &b, Cf *cf, bool zero, int bdmax, Lt *tmp) {
     constexpr TxDim D = tx_dim(TX);
@@ -757,7 +869,7 @@ __device__ __forceinline__ int itx_rows(const MiTxBlock &b, Cf *cf, bool zero, i
                 for (int x = 0; x < 4; x++) tmp[j * LS + x] = (Lt)r[x];
             }
         } else {
-            itx1d<Wide, Wd>(k_row_kind_ip[b.txtp], r, row_lo, row_hi);
+            itx1d<Wide, Wd>(row_kind_ip(b.txtp), r, row_lo, row_hi);
 #pragma unroll
             for (int x = 0; x < Wd; x++) tmp[j * LS + x] = (Lt)clampi((r[x] + Rnd) >> Shift, col_lo, col_hi);
         }
@@ -766,15 +878,11 @@ __device__ __forceinline__ int itx_rows(const MiTxBlock &b, Cf *cf, bool zero, i
 }
 
 template <int TX, typename Px, typename Lt, bool Wide>
-__device__ __forceinline__ void itx_cols(const MiTxBlock &b, int bdmax, int dc, Px *lt, const Lt *tmp) {
+__device__ __forceinline__ void itx_cols(const MiTxBlock &b, int bdmax, int16_t *res, const Lt *tmp) {
     constexpr TxDim D = tx_dim(TX);
     constexpr int Wd = D.w, Ht = D.h, SH = imin_c(Ht, 32);
     constexpr int LS = Wd + 1;
     const int j = threadIdx.x;
-    if (b.txtp == 0 && b.eob < 1) {
-        for (int i = j; i < Wd * Ht; i += 64) lt[i] = (Px)clampi((int)lt[i] + dc, 0, bdmax);
-        return;
-    }
     int col_lo;
     if constexpr (sizeof(Px) == 1) col_lo = -32768;
     else col_lo = (int)((unsigned)~bdmax << 5);
@@ -787,14 +895,62 @@ __device__ __forceinline__ void itx_cols(const MiTxBlock &b, int bdmax, int dc, 
             if constexpr (TX == 0) {
                 iwht4(c);
 #pragma unroll
-                for (int y = 0; y < 4; y++) lt[y * Wd + j] = (Px)clampi((int)lt[y * Wd + j] + c[y], 0, bdmax);
+                for (int y = 0; y < 4; y++) res[y * Wd + j] = (int16_t)c[y];
             }
         } else {
-            itx1d<Wide, Ht>(k_col_kind_ip[b.txtp], c, col_lo, col_hi);
+            itx1d<Wide, Ht>(col_kind_ip(b.txtp), c, col_lo, col_hi);
+            // (c clamped to col_lo..col_hi: (c + 8) >> 4 fits int16 at every bit depth)
 #pragma unroll
-            for (int y = 0; y < Ht; y++) lt[y * Wd + j] = (Px)clampi((int)lt[y * Wd + j] + ((c[y] + 8) >> 4), 0, bdmax);
+            for (int y = 0; y < Ht; y++) res[y * Wd + j] = (int16_t)((c[y] + 8) >> 4);
         }
     }
+}
+
+// An opaque copy into a scalar register: the value is then no longer a (rematerialisable)
+// kernel-argument load
+template <typename T>
+__device__ __forceinline__ T sreg(T v) {
+    asm volatile("" : "+s"(v));
+    return v;
+}
+// ... for a pointer, through a global-address-space copy, so that its uses stay `global_` /
+// `s_load` accesses (a laundered generic pointer would make every access a flat one)
+template <typename T>
+__device__ __forceinline__ T *sreg(T *v) {
+    typedef __attribute__((address_space(1))) T *G;
+    G g = (G)v;
+    asm volatile("" : "+s"(g));
+    return (T *)g;
+}
+__device__ __forceinline__ IntraReconFrame frame_regs(const IntraReconFrame &g) {
+    IntraReconFrame f;
+    for (int p = 0; p < 3; p++) f.ip.dst[p] = sreg(g.ip.dst[p]);
+    f.ip.stride[0] = sreg(g.ip.stride[0]);
+    f.ip.stride[1] = sreg(g.ip.stride[1]);
+    f.ip.blocks = nullptr;
+    f.ip.edges = nullptr;
+    f.ip.ac = sreg(g.ip.ac);
+    f.ip.idx = sreg(g.ip.idx);
+    f.ip.iblocks = sreg(g.ip.iblocks);
+    f.ip.pal = sreg(g.ip.pal);
+    f.ip.bpc = sreg(g.ip.bpc);
+    f.ip.bdmax = sreg(g.ip.bdmax);
+    f.tx = sreg(g.tx);
+    f.coef = sreg(g.coef);
+    f.dep_start = sreg(g.dep_start);
+    f.deps = sreg(g.deps);
+    f.done = sreg(g.done);
+    f.head = sreg(g.head);
+    f.n = sreg(g.n);
+    f.base = sreg(g.base);
+    f.pw = (uint16_t)sreg((int)g.pw);
+    f.ph = (uint16_t)sreg((int)g.ph);
+    f.ss_hor = (uint8_t)sreg((int)g.ss_hor);
+    f.ss_ver = (uint8_t)sreg((int)g.ss_ver);
+    f.nplanes = (uint8_t)sreg((int)g.nplanes);
+    f.pad_ = 0;
+    f.goff = sreg(g.goff);
+    return f;
 }
 
 template <typename Px, typename Cf, typename Lt, bool Wide>
@@ -805,6 +961,7 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
     __shared__ int16_t acl[32 * 32];           // MI_INTRA_CFL_AC
     __shared__ __attribute__((aligned(16))) Px lt[64 * 64];
     __shared__ Lt tmp[32 * 65];
+    __shared__ int16_t res[64 * 64];            // the block's residual (itx_cols)
     const unsigned xcc = xcc_id();
 #ifdef MI_IR_DEBUG
     if (threadIdx.x == 0) {
@@ -815,6 +972,9 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
 #else
 #define DBG(i, v) do {} while (0)
 #endif
+    // MI_IR_TIMELINE: stamp k of the current unit into lane k's tl_v (one store per unit)
+    unsigned long long tl_v = 0;
+#define TL(k) do { if (tl_base) { const unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); if (threadIdx.x == (k)) tl_v = t_; } } while (0)
     // queues xcc, xcc + 8, ... (frames, or the strips of one frame) belong to this XCD; its
     // workers are dealt over them round robin
     const int lane = threadIdx.x;
@@ -822,7 +982,15 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
     if (nper <= 0) return;
     const int rank = __builtin_amdgcn_readfirstlane(atomicAdd(a.xcd_rank + xcc, lane == 0 ? 1 : 0));
     const int fidx = xcc + 8 * (rank % nper);
-    const IntraReconFrame &fr = a.fr[fidx];
+    // the queue's descriptor and the launch constants in registers for the whole launch: read
+    // at each use they are scalar loads of the kernel arguments, which the descriptors streaming
+    // through the scalar cache evict (a miss on the critical path of every block)
+    const IntraReconFrame fr = frame_regs(a.fr[fidx]);
+    const uint32_t epoch = sreg(a.epoch);
+    unsigned long long *const gran = sreg(a.gran);
+    int *const err = sreg(a.err), *const desc_err = sreg(a.desc_err);
+    const uintptr_t tl_base = sreg(a.tl);
+    const int zero_coefs = sreg(a.zero_coefs);
     for (;;) {
         // The block index must be provably wave-uniform and the loop free of lane-divergent
         // branches: otherwise the structurizer may run lanes 1..63 into the next iteration
@@ -833,6 +1001,9 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
         // per 1080p frame, a worker blocked on its first block also holds the second)
         const int i = __builtin_amdgcn_readfirstlane(atomicAdd(fr.head, lane == 0 ? 1 : 0));
         if (i >= fr.n) return;
+        unsigned long long *tl =
+            tl_base ? reinterpret_cast<unsigned long long *>(tl_base + (uintptr_t)(fr.done + fr.base + i) * 32) : nullptr;
+        TL(0);
         DBG(i, 1);
         const MiIntraBlock ib = fr.ip.iblocks[i];
         const MiTxBlock tb = fr.tx[i];
@@ -848,8 +1019,8 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
             const bool ok = __builtin_amdgcn_readfirstlane((int)ok_) != 0;
             if (!ok) {
                 if (lane == 0) {
-                    atomicOr(a.desc_err, 2);
-                    __hip_atomic_store(fr.done + fr.base + i, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    atomicOr(desc_err, 2);
+                    __hip_atomic_store(fr.done + fr.base + i, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 continue;
             }
@@ -858,23 +1029,39 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
         Cf *cf = reinterpret_cast<Cf *>(fr.coef) + tb.coef_off;
         int dc = 0;
         switch (tb.tx) {
-#define CASE(n) case n: dc = itx_rows<n, Px, Cf, Lt, Wide>(tb, cf, a.zero_coefs, fr.ip.bdmax, tmp); break;
+#define CASE(n) case n: dc = itx_rows<n, Px, Cf, Lt, Wide>(tb, cf, zero_coefs, fr.ip.bdmax, tmp); break;
             CASE(0) CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9)
             CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16) CASE(17) CASE(18)
 #undef CASE
         default: break;
         }
-        // wait for the blocks this one's edges read; wave-uniform loop exits (a ballot)
-        const int d0 = fr.dep_start[i], d1 = fr.dep_start[i + 1];
+        // the column pass too (the residual), unless the block is DC-only (a constant dc)
+        const bool dconly = tb.txtp == 0 && tb.eob < 1;
+        if (!dconly) {
+            __syncthreads();
+            switch (tb.tx) {
+#define CASE(n) case n: itx_cols<n, Px, Lt, Wide>(tb, fr.ip.bdmax, res, tmp); break;
+                CASE(0) CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9)
+                CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16) CASE(17) CASE(18)
+#undef CASE
+            default: break;
+            }
+        }
+        TL(1);
+        // wait for the blocks this one's edges read; wave-uniform loop exits (a ballot). With
+        // edge granules only CfL (its luma) and intra block copy (its source) read pixels of
+        // other blocks outside the granules
+        const int d0 = fr.dep_start[i];
+        const int d1 = gran && ib.mode != MI_IPRED_CFL && ib.mode != MI_INTRA_IBC ? d0 : fr.dep_start[i + 1];
         for (int base = d0; base < d1; base += 64) {
             const int d = base + lane;
             const uint32_t *flag = fr.done + (d < d1 ? fr.deps[d] : 0);
             bool ok = d >= d1;
             for (unsigned spins = 0;; spins++) {
-                if (!ok) ok = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
+                if (!ok) ok = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
                 if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
                 if (spins > (1u << MI_IR_SPIN_LOG2)) {
-                    atomicOr(a.err, 1);
+                    atomicOr(err, 1);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -882,23 +1069,34 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
         }
         __syncthreads();
         DBG(i, 2);
-        GranCtx gc;
-        if (a.gran)
-            gc = gran_ctx(a.gran + fr.goff, fr.pw, fr.ph, fr.ss_hor, fr.ss_ver, fr.nplanes, ib.plane, a.epoch, a.err);
-        intra_block<Px, true>(fr.ip, ib, eb, ft, edge, lt, acl, a.gran ? &gc : nullptr);
-        __syncthreads();
-        DBG(i, 3);
-        switch (tb.tx) {
-#define CASE(n) case n: itx_cols<n, Px, Lt, Wide>(tb, fr.ip.bdmax, dc, lt, tmp); break;
-            CASE(0) CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9)
-            CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16) CASE(17) CASE(18)
-#undef CASE
-        default: break;
+        TL(2);
+        GranCtx gc = {};
+        if (gran)
+            gc = gran_ctx(gran + fr.goff, fr.pw, fr.ph, fr.ss_hor, fr.ss_ver, fr.nplanes, ib.plane, epoch, err);
+        int dcv;
+        {
+            const IntraOut o = intra_block<Px, true>(fr.ip, ib, eb, ft, edge, lt, acl, dconly ? nullptr : res, dc,
+                                                     gran != nullptr, gc, tl_base != 0);
+            dcv = o.dcv;
+            if (lane >= 7 && lane <= 10) tl_v = o.tlx;
+#ifdef MI_IR_EXP_DCSTAMP
+            if (lane >= 11 && lane <= 13)
+                tl_v = (unsigned)eb[240 + 2 * (lane - 11)] | ((unsigned long long)(unsigned)eb[241 + 2 * (lane - 11)] << 32);
+#endif
         }
-        DBG(i, 5);
-        __syncthreads();
-        DBG(i, 6);
-        if (a.gran) {
+        // pixel (yy, xx) of the reconstructed block: the LDS tile, or a DC-family block's value
+        // plus the residual (res was complete before the dependency wait's barrier)
+        const bool direct = dcv >= 0;
+        const int bdmax_ = fr.ip.bdmax;
+        auto pix = [&](int yy, int xx) -> uint32_t {
+            if (direct) return (uint32_t)clampi(dcv + (dconly ? dc : (int)res[yy * ib.w + xx]), 0, bdmax_);
+            return lt[yy * ib.w + xx];
+        };
+        if (!direct) __syncthreads();
+        DBG(i, 3);
+        TL(3);
+        TL(4);
+        if (gran) {
             // the edges later blocks read, as granules: right column (lanes 0..h/2-1), bottom
             // row (lanes 32..32+w/2-1), before the tile's own stores
             const int w = ib.w, h = ib.h;
@@ -906,40 +1104,39 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
             uint32_t p0 = 0, p1 = 0;
             if (lane < (h >> 1)) {
                 const int r = 2 * lane;
-                p0 = lt[r * w + w - 1];
-                p1 = lt[(r + 1) * w + w - 1];
+                p0 = pix(r, w - 1);
+                p1 = pix(r + 1, w - 1);
                 gd = gc.col + ((ib.x + w) >> 2) * gc.colp + ((ib.y + r) >> 1);
             } else if (lane >= 32 && lane - 32 < (w >> 1)) {
                 const int c = 2 * (lane - 32);
-                p0 = lt[(h - 1) * w + c];
-                p1 = lt[(h - 1) * w + c + 1];
+                p0 = pix(h - 1, c);
+                p1 = pix(h - 1, c + 1);
                 gd = gc.row + ((ib.y + h) >> 2) * gc.rowp + ((ib.x + c) >> 1);
             }
             if (gd)
-                __hip_atomic_store(gd, (unsigned long long)(p0 | (p1 << 16)) | ((unsigned long long)a.epoch << 32),
+                __hip_atomic_store(gd, (unsigned long long)(p0 | (p1 << 16)) | ((unsigned long long)epoch << 32),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         // store the reconstructed tile: 4-pixel chunks, 4-B (8 bpc) / 8-B (hbd) `sc1` stores
         {
-            const int w = ib.w, h = ib.h, cpr = w >> 2;
-            const int64_t st = fr.ip.stride[ib.plane ? 1 : 0];
-            uint8_t *base = fr.ip.dst[ib.plane] + (int64_t)ib.y * st + (int64_t)ib.x * sizeof(Px);
+            const int w = ib.w, h = ib.h, cpr = w >> 2, lcpr = 29 - __clz(w);
+            const int64_t st = plane_stride(fr.ip, ib.plane);
+            uint8_t *base = plane_ptr(fr.ip, ib.plane) + (int64_t)ib.y * st + (int64_t)ib.x * sizeof(Px);
             for (int c = lane; c < h * cpr; c += 64) {
-                const int yy = c / cpr, xx = (c % cpr) * 4;
-                const Px *src = lt + yy * w + xx;
+                const int yy = c >> lcpr, xx = (c & (cpr - 1)) * 4;
+                const uint32_t q0 = pix(yy, xx), q1 = pix(yy, xx + 1), q2 = pix(yy, xx + 2), q3 = pix(yy, xx + 3);
                 if constexpr (sizeof(Px) == 2)
                     __hip_atomic_store(reinterpret_cast<uint64_t *>(base + yy * st + xx * 2),
-                                       (uint64_t)(src[0] | ((uint32_t)src[1] << 16)) |
-                                           ((uint64_t)(src[2] | ((uint32_t)src[3] << 16)) << 32),
+                                       (uint64_t)(q0 | (q1 << 16)) | ((uint64_t)(q2 | (q3 << 16)) << 32),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 else
                     __hip_atomic_store(reinterpret_cast<uint32_t *>(base + yy * st + xx),
-                                       src[0] | ((uint32_t)src[1] << 8) | ((uint32_t)src[2] << 16) |
-                                           ((uint32_t)src[3] << 24),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                       q0 | (q1 << 8) | (q2 << 16) | (q3 << 24), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         DBG(i, 7);
+        TL(5);
         // hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1): every byte
         // stored `sc1`, the storing wave drains its stores, then ONE lane stores the flag `sc1`
         // (agent scope); consumers poll it with `sc1` loads and read the pixels with 4-B `sc1`
@@ -948,8 +1145,11 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
         DBG(i, 8);
         __syncthreads();
         DBG(i, 4);
-        if (lane == 0) __hip_atomic_store(fr.done + fr.base + i, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(fr.done + fr.base + i, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        TL(6);
+        if (tl && lane < 16) tl[lane] = tl_v;   // (stamps kept in lane k's register until here)
     }
+#undef TL
 }
 
 // After the persistent launch, in stream order: every frame's queue head must have passed its

@@ -112,17 +112,21 @@ class IntraFrame:
         d.n = len(self.fr["blocks"])
         return d
 
-    def recon(self, pic, stream=None, keep_coefs=True):
+    def recon(self, pic, stream=None, keep_coefs=True, granules=False):
         """Whole-frame reconstruction in one persistent launch (mi_intra_recon)."""
-        intra_recon(self.ctx, [(self, pic)], stream, keep_coefs)
+        intra_recon(self.ctx, [(self, pic)], stream, keep_coefs, granules)
 
 
-def intra_recon(ctx, frames, stream=None, keep_coefs=True):
+IR_EDGE_GRANULES = 2   # mi_av1dsp.h MI_IR_EDGE_GRANULES
+
+
+def intra_recon(ctx, frames, stream=None, keep_coefs=True, granules=False):
     """Reconstruct up to 24 independent intra frames in one launch: frames = [(IntraFrame,
-    MiPicture)], frame f on XCD f % 8."""
+    MiPicture)], frame f on XCD f % 8. granules: MI_IR_EDGE_GRANULES (every pixel an edge reads
+    is reconstructed by this call: intra-only frames)."""
     from . import MiIntraFrame
     descs = (MiIntraFrame * len(frames))(*[f.frame_desc(p) for f, p in frames])
-    flags = ITX_KEEP_COEFS if keep_coefs else 0
+    flags = (ITX_KEEP_COEFS if keep_coefs else 0) | (IR_EDGE_GRANULES if granules else 0)
     F.check(F.lib().mi_intra_recon(ctx.h, descs, len(frames), flags, F._stream_ptr(stream)), "mi_intra_recon")
 
 

@@ -104,10 +104,14 @@ def _oracle_recon(init, fr, bpc):
     return exp
 
 
-@pytest.mark.parametrize("bpc,layout,ii", [(8, 1, 0.0), (10, 1, 0.2), (12, 3, 0.0), (8, 0, 0.0), (10, 2, 0.1)])
-def test_intra_recon_fused(gpu, bpc, layout, ii):
+@pytest.mark.parametrize("bpc,layout,ii,granules", [(8, 1, 0.0, False), (10, 1, 0.2, False), (12, 3, 0.0, False),
+                                                   (8, 0, 0.0, False), (10, 2, 0.1, False), (8, 1, 0.0, True),
+                                                   (10, 1, 0.0, True), (12, 3, 0.0, True), (8, 0, 0.0, True),
+                                                   (10, 2, 0.0, True)])
+def test_intra_recon_fused(gpu, bpc, layout, ii, granules):
     """The persistent fused path (mi_intra_recon: one launch, per-block dependency waits,
-    prediction + residual per block) vs the oracle's interleaved decode-order recon."""
+    prediction + residual per block) vs the oracle's interleaved decode-order recon; granules:
+    MI_IR_EDGE_GRANULES (edges handed over as tagged records; intra-only frames)."""
     from rav1d_amd.intra import IntraFrame, device_status, make_intra_residuals
     w, h = 256, 192
     rng = np.random.default_rng(bpc * 37 + layout)
@@ -120,7 +124,7 @@ def test_intra_recon_fused(gpu, bpc, layout, ii):
     for rep in range(2):   # a second launch (new epoch) over the same buffers must give the same result
         for p in range(len(cur.planes)):
             cur.set_buffer_np(p, init[p])
-        intra.recon(cur.picture())
+        intra.recon(cur.picture(), granules=granules)
         device_status(gpu)
         exp = _oracle_recon(init, fr, bpc)
         for p in range(len(cur.planes)):
@@ -130,8 +134,8 @@ def test_intra_recon_fused(gpu, bpc, layout, ii):
                 raise AssertionError(f"rep {rep} plane {p}: {len(bad)} mismatches, first at {bad[0]}")
 
 
-@pytest.mark.parametrize("nframes", [8, 19])
-def test_intra_recon_fused_multi_frame(gpu, nframes):
+@pytest.mark.parametrize("nframes,granules", [(8, False), (19, False), (19, True)])
+def test_intra_recon_fused_multi_frame(gpu, nframes, granules):
     """Several different frames in one launch (frame f on XCD f % 8; 19 frames: XCDs serving
     two and three frames), large blocks and deep chains, coefficients zeroed after use (the
     itxfm_add contract)."""
@@ -147,7 +151,7 @@ def test_intra_recon_fused_multi_frame(gpu, nframes):
         frs.append(fr)
         frames.append(IntraFrame(gpu, fr))
         curs.append(cur)
-    intra_recon(gpu, [(frames[f], curs[f].picture()) for f in range(nframes)], keep_coefs=False)
+    intra_recon(gpu, [(frames[f], curs[f].picture()) for f in range(nframes)], keep_coefs=False, granules=granules)
     device_status(gpu)
     for f in range(nframes):
         exp = _oracle_recon(inits[f], frs[f], bpc)
@@ -156,7 +160,8 @@ def test_intra_recon_fused_multi_frame(gpu, nframes):
         assert int(torch.count_nonzero(frames[f].coef)) == 0, f"frame {f}: coefficients not zeroed"
 
 
-def test_intra_recon_bench_1080p8(gpu):
+@pytest.mark.parametrize("granules", [False, True])
+def test_intra_recon_bench_1080p8(gpu, granules):
     """The exact workload bench.py times for configs[1]: 1080p 8-bit 4:2:0 intra frames from the
     four bench descriptor seeds (0x1A7A0001 + k), cycled through a 24-frame batch in one
     persistent launch, coefficients zeroed as consumed (itxfm_add contract). Every frame is
@@ -170,7 +175,7 @@ def test_intra_recon_bench_1080p8(gpu):
     intras = [IntraFrame(gpu, frs[f % ndesc]) for f in range(nframes)]   # one coefficient arena per frame
     curs = [Frame(w, h, bpc, 1) for _ in range(nframes)]
     init = [curs[0].buffer_np(p) for p in range(3)]
-    intra_recon(gpu, [(intras[f], curs[f].picture()) for f in range(nframes)], keep_coefs=False)
+    intra_recon(gpu, [(intras[f], curs[f].picture()) for f in range(nframes)], keep_coefs=False, granules=granules)
     device_status(gpu)
     for k in range(ndesc):
         fr = frs[k]
@@ -207,10 +212,10 @@ def test_intra_recon_block_copy_heavy(gpu, bpc, layout):
     exp, _ = oracle_lib.intra_recon(init, bpc, b, fr["tx_blocks"][fr["tx_of_block"]], fr["ac"], fr["idx"], fr["pal"],
                                     fr["coef"])
     intra = IntraFrame(gpu, fr)
-    for fused in (False, True):
+    for fused in (False, True, "granules"):
         cur = Frame(w, h, bpc, layout)
         if fused:
-            intra.recon(cur.picture())
+            intra.recon(cur.picture(), granules=fused == "granules")
             device_status(gpu)
         else:
             intra.step(cur.picture())
