@@ -1644,11 +1644,15 @@ int intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, const int32
     a.epoch = ctx->ir_epoch;
     a.nframes = nq;
     a.zero_coefs = (flags & MI_ITX_KEEP_COEFS) ? 0 : 1;
-    // one-wave workers per XCD (occupancy allows 3 per SIMD = 384 per XCD): 128 per queue, plus
-    // 64 per extra queue the XCD serves
+    // one-wave workers per XCD (VGPRs allow 2 per SIMD = 256 per XCD, LDS 7 per CU): one per
+    // ~96 units of the busiest XCD's first queue, 128 to 192 (a worker that arrives after its
+    // block's producer finished adds to the chain: 4K intra frames gain 25 % from 128 to 192;
+    // 352x288 frames lose 15 % at 64), plus 64 per extra queue the XCD serves
     const int per_xcd = (nq + 7) / 8;
+    int n_xcd = 0;
+    for (int q = 0; q < nq && q < 8; q++) n_xcd = std::max(n_xcd, a.fr[q].n);
     static const int wenv = getenv("MI_IR_WORKERS") ? atoi(getenv("MI_IR_WORKERS")) : 0;
-    const int wpx = wenv ? wenv : std::min(384, 128 + 64 * (per_xcd - 1));
+    const int wpx = wenv ? wenv : std::min(256, std::max(128, std::min(192, n_xcd / 96)) + 64 * (per_xcd - 1));
     return mi::launch_intra_recon(a, bpc, wpx, s) ? fail(ctx, -EIO) : 0;
 }
 

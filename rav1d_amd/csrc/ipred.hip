@@ -959,8 +959,12 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
     __shared__ Px ft[32 * 32];
     __shared__ Px edge[2 * 128 + 1];
     __shared__ int16_t acl[32 * 32];           // MI_INTRA_CFL_AC
-    __shared__ __attribute__((aligned(16))) Px lt[64 * 64];
-    __shared__ Lt tmp[32 * 65];
+    // the row pass's tmp and the block's tile lt share their LDS: tmp lives from the row pass
+    // to the column pass (before the dependency wait), lt from the prediction to the stores
+    constexpr int kLtB = 64 * 64 * (int)sizeof(Px), kTmpB = 32 * 65 * (int)sizeof(Lt);
+    __shared__ __attribute__((aligned(16))) unsigned char lt_tmp[kLtB > kTmpB ? kLtB : kTmpB];
+    Px *const lt = reinterpret_cast<Px *>(lt_tmp);
+    Lt *const tmp = reinterpret_cast<Lt *>(lt_tmp);
     __shared__ int16_t res[64 * 64];            // the block's residual (itx_cols)
     const unsigned xcc = xcc_id();
 #ifdef MI_IR_DEBUG
