@@ -630,11 +630,11 @@ def single_stream(args, world, rank, local):
     from rav1d_amd.sstream import DeviceExecutor, PipelinedStream, make_stream_specs
     specs = make_stream_specs(W, H, BPC, LAYOUT, args.single_stream, 0x55400001, reuse=True)
     ctx = F.Context(local)
-    ex = DeviceExecutor(ctx)
+    ex = DeviceExecutor(ctx, bands=args.bands)
     for s in specs:
         if s.idx % world == rank:
             ex.prepare(s)
-    ps = PipelinedStream(ex, ex.alloc, rank, world, "cuda")
+    ps = PipelinedStream(ex, ex.alloc, rank, world, "cuda", bands=args.bands)
     for _ in range(max(1, args.warmup)):
         ps.run(specs)
     torch.cuda.synchronize()
@@ -648,7 +648,9 @@ def single_stream(args, world, rank, local):
             "fps": round(frames / elapsed, 2), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "u16", "data": "synthetic hierarchical GOP (rav1d_amd.sstream)",
             "config": {"workload": f"one 4K10 stream of {len(specs)} frames per step, frame k on rank k % N, "
-                                   f"references sent point to point", "parallelism": f"frame-pipelined x{world}"}}))
+                                   f"references sent point to point"
+                                   + (f" in {args.bands} bands, MC per band (row-level progress)" if args.bands > 1 else ""),
+                       "parallelism": f"frame-pipelined x{world}"}}))
     if world > 1:
         dist.destroy_process_group()
 
@@ -663,6 +665,8 @@ def main():
     ap.add_argument("--no-intra", action="store_true", help="skip the separate 1080p8 intra measurement")
     ap.add_argument("--no-verify", action="store_true", help="skip the per-rank oracle check of the output")
     ap.add_argument("--no-extra", action="store_true", help="skip the coherent-motion MC and output-side measurements")
+    ap.add_argument("--bands", type=int, default=1,
+                    help="--single-stream: references sent in this many row bands, MC launched per band")
     ap.add_argument("--single-stream", type=int, default=0, metavar="FRAMES",
                     help="instead of replicas: one 4K10 stream of FRAMES frames (hierarchical GOP of 8), frame k "
                          "reconstructed on rank k %% N, references exchanged point to point (rav1d_amd.sstream)")

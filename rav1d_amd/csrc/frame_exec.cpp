@@ -310,6 +310,20 @@ int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<in
     for (int q = 0; q <= ns; q++) sx[q] = (int)((int64_t)q * units / ns) * unit;
     // strip of every block (by its luma column) and the owner of every 4x4 unit of each plane
     strip.resize(n);
+    // with edge granules only intra block copy reads pixels across strips (CfL's luma lies in
+    // its own strip): without such blocks there are no extra deps and no owner map is needed
+    bool need_own = !granules;
+    for (int i = 0; !need_own && i < n; i++) need_own = f->intra[i].mode == MI_INTRA_IBC;
+    if (!need_own) {
+        for (int i = 0; i < n; i++) {
+            const MiIntraBlock &b = f->intra[i];
+            const int xl = b.plane ? b.x << ssh : b.x;
+            strip[i] = (int8_t)(std::upper_bound(sx.begin(), sx.end(), xl) - sx.begin() - 1);
+        }
+        xs.assign(n + 1, 0);
+        xd.clear();
+        return ns;
+    }
     const int aw = (f->w + 127) & ~127, ah = (f->h + 127) & ~127;
     int pw4[3], ph4[3];
     std::vector<int32_t> own[3];
@@ -547,6 +561,7 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         std::vector<int32_t> xs, xd;          // extra dependencies of the strip split (CSR)
         std::vector<int8_t> strip;
         const int nstrips = intra_strips(f, strip, xs, xd, granules);
+        const auto t_a = clk::now();
         auto each_dep = [&](int i, auto &&fn) {
             for (int d = f->dep_start[i]; d < f->dep_start[i + 1]; d++) fn(f->deps[d]);
             if (nstrips > 1)
@@ -560,6 +575,7 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
             level[i] = l;
             maxl = std::max(maxl, l);
         }
+        const auto t_b = clk::now();
         // counting sort by (strip, level), decode order within
         const int nkeys = nstrips * (maxl + 1);
         auto key = [&](int i) { return (nstrips > 1 ? strip[i] * (maxl + 1) : 0) + level[i]; };
@@ -573,21 +589,40 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         for (int i = 0; i < n; i++) pos[i] = cnt[key(i)]++;
         std::vector<int32_t> inv(n);
         for (int i = 0; i < n; i++) inv[pos[i]] = i;
-        deps.reserve(f->n_deps + xd.size() + 1);
-        for (int k = 0; k < n; k++) {
-            const int i = inv[k];
-            blocks[k] = f->intra[i];
-            tx[k] = f->intra_tx[i];
-            dep_start[k] = (int32_t)deps.size();
+        const auto t_c = clk::now();
+        // the queue-ordered copies, walking the units in decode order (their deps point to
+        // recent units: the reads stay in cache) and scattering the writes: count each unit's
+        // kernel deps, prefix sum in queue order, then fill
+        auto kdeps = [&](int i, auto &&fn) {
             const MiIntraBlock &b = f->intra[i];
             if (!granules || b.mode == MI_INTRA_IBC || b.mode == MI_IPRED_CFL) {
-                each_dep(i, [&](int d) { deps.push_back(pos[d]); });
+                each_dep(i, [&](int d) { fn(pos[d]); });
             } else {
                 for (int d = f->dep_start[i]; d < f->dep_start[i + 1]; d++)
-                    if (f->intra[f->deps[d]].plane != b.plane) deps.push_back(pos[f->deps[d]]);
+                    if (f->intra[f->deps[d]].plane != b.plane) fn(pos[f->deps[d]]);
             }
+        };
+        dep_start[0] = 0;
+        for (int i = 0; i < n; i++) {
+            const int k = pos[i];
+            blocks[k] = f->intra[i];
+            tx[k] = f->intra_tx[i];
+            int c = 0;
+            kdeps(i, [&](int) { c++; });
+            dep_start[k + 1] = c;
         }
-        dep_start[n] = (int32_t)deps.size();
+        for (int k = 0; k < n; k++) dep_start[k + 1] += dep_start[k];
+        deps.resize(dep_start[n]);
+        for (int i = 0; i < n; i++) {
+            int o = dep_start[pos[i]];
+            kdeps(i, [&](int d) { deps[o++] = d; });
+        }
+        static const bool prof = getenv("MI_FX_PROFILE") != nullptr;
+        if (prof) {
+            auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            fprintf(stderr, "frame_run n=%d strips %.3f levels %.3f sort %.3f permute %.3f ms\n", n, ms(t_lv, t_a),
+                    ms(t_a, t_b), ms(t_b, t_c), ms(t_c, clk::now()));
+        }
         if (tl_path) {
             // every dependency (with the strips' extra ones), in queue order
             tl_ds.assign(n + 1, 0);

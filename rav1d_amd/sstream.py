@@ -9,6 +9,15 @@ tensors, no host staging), host-staged under "gloo". Dependencies are whole fram
 starts once its references are complete), which is rav1d's frame-threading model without
 row-level progress.
 
+Row-level progress (bands > 1), after rav1d's per-sbrow reference waits
+(src/thread_task.rs:450-575, recon.rs's `wait_for_ref` before each superblock row's MC): a
+reference picture travels in `bands` horizontal bands, top first, and a consumer runs its MC
+in the same bands: the units of band group g (mc_band_groups: every reference row a unit's
+8-tap window reads lies in bands 0..g) are launched once bands 0..g of every remote reference
+have arrived, so the transfer of the lower bands overlaps the MC of the upper ones. The
+residual and the loop filters follow the last band, as in rav1d, where the filters of a row
+need the rows below it.
+
 Transfer protocol, deadlock-free by construction:
   * the producer of frame r posts a non-blocking send of r's output picture to every rank that
     owns a later frame referencing r, as soon as r is reconstructed (sends never block the
@@ -97,14 +106,56 @@ def gop_specs(n, gop=8):
     return [(d, [dec_of[r] for r in refs_disp[d]]) for d in order]
 
 
+def band_height(h, bands):
+    """Luma rows per band: h split into `bands` bands of a multiple of 8 rows (the last may be
+    shorter)."""
+    return max(8, ((h + bands - 1) // bands + 7) // 8 * 8)
+
+
+def band_rows(b, bh, h, ss_v):
+    """Rows [lo, hi) of band b in a plane subsampled by ss_v (luma band height bh)."""
+    lo, hi = (b * bh) >> ss_v, (min(h, (b + 1) * bh) + ss_v) >> ss_v
+    return lo, hi
+
+
+def mc_band_groups(units, h, layout, bands):
+    """Band group of every MC unit (MiMcBlock records): the smallest g such that every
+    reference row the unit's 8-tap window can read (rows up to y + h + mv_y / 8 + 4, in the
+    unit's plane, per reference) lies in luma bands 0..g. A unit reading beyond the frame's
+    last row (the border replicate of emu_edge) needs the last band. A chroma MASK unit reads
+    the mask the luma unit of its block writes (a SEG block's chroma), so it joins the luma
+    unit's group when that is later."""
+    bh = band_height(h, bands)
+    ss_h, ss_v = int(layout in (1, 2)), int(layout == 1)
+    sv = np.where(units["plane"] > 0, ss_v, 0).astype(np.int64)
+    end = np.zeros(len(units), np.int64)
+    for k in range(2):
+        used = (units["ref"][:, k] >= 0)
+        dy = units["mvy"][:, k].astype(np.int64) >> (3 + sv)
+        e = ((units["y"].astype(np.int64) + units["h"] + dy + 5) << sv) + sv   # luma row bound
+        end = np.where(used, np.maximum(end, e), end)
+    g = np.clip((np.minimum(end, h) + bh - 1) // bh - 1, 0, bands - 1)
+    g = np.where(end >= h, bands - 1, g)
+    later = (units["plane"] > 0) & (units["ref"][:, 1] >= 0) & (units["comp"] == 2)
+    if later.any():
+        luma = {(int(u["x"]), int(u["y"])): int(gi) for u, gi in zip(units[units["plane"] == 0], g[units["plane"] == 0])}
+        for i in np.nonzero(later)[0]:
+            key = (int(units["x"][i]) << ss_h, int(units["y"][i]) << ss_v)
+            g[i] = max(int(g[i]), luma.get(key, bands - 1))
+    return g
+
+
 class PipelinedStream:
     """Frame-pipelined decode of one stream over the ranks of the default process group."""
 
-    def __init__(self, executor, alloc, rank, world, device):
-        """executor(spec, [ref pictures]) -> picture (an object with .planes: uint8 tensors);
+    def __init__(self, executor, alloc, rank, world, device, bands=1):
+        """executor(spec, [ref pictures]) -> picture (an object with .planes: uint8 tensors), or
+        with bands > 1 executor(spec, [ref pictures], ready), where ready(g) returns once bands
+        0..g of every reference have arrived (None when every reference is local);
         alloc(spec) -> an empty picture of the frame's geometry (receive buffer)."""
         self.executor, self.alloc = executor, alloc
         self.rank, self.world, self.device = rank, world, device
+        self.bands = max(1, int(bands))
         self.gloo = dist.is_initialized() and dist.get_backend() == "gloo"
         # one communicator per direction (every rank creates both, in the same order)
         self.up = self.down = None
@@ -115,55 +166,91 @@ class PipelinedStream:
         """lower -> higher rank messages on `up`, higher -> lower on `down`"""
         return self.up if (peer > self.rank) == sending else self.down
 
-    def _send(self, pic, dst, pending):
-        g = self._group(dst, True)
-        for t in pic.planes:
-            src = t.cpu() if self.gloo and t.is_cuda else t
-            pending.append((dist.isend(src, dst, group=g), src))
+    def _geom(self, spec):
+        fr = spec.desc
+        return fr["h"], int(fr["layout"] == 1)
 
-    def _recv(self, spec_of, r, src):
-        pic = self.alloc(spec_of[r])
+    def _send(self, spec, pic, dst, pending):
+        """Every band of `pic`, top first, each band as one message per plane."""
+        g = self._group(dst, True)
+        h, ss_v = self._geom(spec) if self.bands > 1 else (0, 0)
+        bh = band_height(h, self.bands) if self.bands > 1 else 0
+        for b in range(self.bands):
+            for p, t in enumerate(pic.planes):
+                if self.bands > 1:
+                    lo, hi = band_rows(b, bh, h, ss_v if p else 0)
+                    t = t[lo:hi]
+                src = t.cpu() if self.gloo and t.is_cuda else t.contiguous()
+                pending.append((dist.isend(src, dst, group=g), src))
+
+    def _recv_band(self, spec, pic, b, src):
         g = self._group(src, False)
-        for t in pic.planes:
+        h, ss_v = self._geom(spec) if self.bands > 1 else (0, 0)
+        bh = band_height(h, self.bands) if self.bands > 1 else 0
+        for p, t in enumerate(pic.planes):
+            if self.bands > 1:
+                lo, hi = band_rows(b, bh, h, ss_v if p else 0)
+                t = t[lo:hi]
             if self.gloo and t.is_cuda:
-                h = torch.empty_like(t, device="cpu")
-                dist.recv(h, src, group=g)
-                t.copy_(h)
+                hbuf = torch.empty_like(t, device="cpu")
+                dist.recv(hbuf, src, group=g)
+                t.copy_(hbuf)
             else:
                 dist.recv(t, src, group=g)
-        return pic
 
     def run(self, specs):
         """Decode my frames; returns {decode index: output picture} for the frames this rank
         reconstructed (the caller hashes / outputs them)."""
         plan, lu = transfer_plan(specs, self.world), last_use(specs)
         spec_of = {s.idx: s for s in specs}
-        # per peer: the frames it will send me, in its send order (increasing r)
+        B = self.bands
+        # per peer: the (frame, band) messages it will send me, in its send order (increasing
+        # r, bands top first)
         incoming = {}
         for r, dsts in sorted(plan.items()):
             if self.rank in dsts:
-                incoming.setdefault(owner(r, self.world), []).append(r)
+                incoming.setdefault(owner(r, self.world), []).extend((r, b) for b in range(B))
         got = {}          # r -> picture (mine or received), freed after last use
+        have = {}         # r -> bands of r received so far (B: complete)
         mine = {}
         pending = []      # (work, tensor) of non-blocking sends
+
+        def pull(r, band):
+            """Receive, in the peer's order, until bands 0..band of r are here."""
+            src = owner(r, self.world)
+            q = incoming[src]
+            while have.get(r, 0) <= band:
+                n, b = q.pop(0)
+                if n not in got:
+                    got[n] = self.alloc(spec_of[n])
+                self._recv_band(spec_of[n], got[n], b, src)
+                have[n] = b + 1
+
         for s in specs:
             if owner(s.idx, self.world) != self.rank:
                 continue
-            for r in s.refs:
-                if r in got:
-                    continue
-                src = owner(r, self.world)
-                q = incoming[src]
-                while True:                    # in the peer's order, up to r
-                    n = q.pop(0)
-                    got[n] = self._recv(spec_of, n, src)
-                    if n == r:
-                        break
-            out = self.executor(s, [got[r] for r in s.refs])
+            remote = [r for r in s.refs if owner(r, self.world) != self.rank and have.get(r, 0) < B]
+            if B > 1 and remote:
+                for r in remote:               # allocate (first band may come later)
+                    pull(r, 0)
+
+                def ready(g, remote=remote):
+                    for r in remote:
+                        pull(r, min(g, B - 1))
+                out = self.executor(s, [got[r] for r in s.refs], ready)
+                for r in remote:
+                    pull(r, B - 1)
+            else:
+                for r in s.refs:
+                    if owner(r, self.world) != self.rank:
+                        pull(r, B - 1)
+                out = self.executor(s, [got[r] for r in s.refs], None) if B > 1 else \
+                    self.executor(s, [got[r] for r in s.refs])
             got[s.idx] = out
+            have[s.idx] = B
             mine[s.idx] = out
             for d in plan.get(s.idx, []):
-                self._send(out, d, pending)
+                self._send(s, out, d, pending)
             for r in list(got):
                 if lu.get(r, -1) <= s.idx and r not in mine:
                     del got[r]
@@ -185,8 +272,8 @@ class DeviceExecutor:
     prepare() uploads the frame's descriptors and allocates its pictures once, outside the
     decode loop, so a frame costs five C calls at decode time."""
 
-    def __init__(self, ctx, stream=None):
-        self.ctx, self.stream = ctx, stream
+    def __init__(self, ctx, stream=None, bands=1):
+        self.ctx, self.stream, self.bands = ctx, stream, bands
         self.prepared = {}
 
     def prepare(self, spec):
@@ -199,6 +286,22 @@ class DeviceExecutor:
                  mc=F.McMeta(*fr["mc"]) if fr.get("mc") is not None else None)
         d["coef"] = d["coef0"].clone()
         d["cdef"] = F.CdefMeta(fr["lf"]["masks"], fr["cdef"], masks_dev=d["lf"].masks)
+        if d["mc"] is not None and self.bands > 1:
+            # row-level progress: the units split by band group, one mi_mc_frame per group
+            # (one shared mask buffer)
+            from .synth import mc_sort_units
+            units = fr["mc"][0]
+            grp = mc_band_groups(units, fr["h"], fr["layout"], self.bands)
+            d["mc_bands"] = []
+            for g in range(self.bands):
+                ug = units[grp == g]
+                if len(ug) == 0:
+                    d["mc_bands"].append(None)
+                    continue
+                ug, cs = mc_sort_units(ug)
+                m = F.McMeta(ug, cs, np.zeros(1, np.uint8))
+                m.masks = d["mc"].masks
+                d["mc_bands"].append(m)
         d["frames"] = [self.alloc(spec) for _ in range(4)]            # A, D, B, O
         d["pics"] = [f.picture() for f in d["frames"]]
         d["ss"] = (ctypes.c_uint32 * 20)(*[int(v) for v in fr["size_start"]])
@@ -216,7 +319,9 @@ class DeviceExecutor:
         fr = spec.desc
         return F.Frame(fr["w"], fr["h"], fr["bpc"], fr["layout"])
 
-    def __call__(self, spec, refs):
+    def __call__(self, spec, refs, ready=None):
+        """ready (row-level progress, bands > 1): ready(g) returns once bands 0..g of every
+        reference have arrived; the MC of band group g is enqueued after it."""
         import ctypes
         from . import frame as F
         if spec.idx not in self.prepared:
@@ -227,8 +332,15 @@ class DeviceExecutor:
         d["coef"].copy_(d["coef0"])                 # itxfm_add zeroes the arena it consumes
         if d["mc"] is not None:
             rp = (F.MiPicture * len(refs))(*[r.picture() for r in refs])
-            F.check(L.mi_mc_frame(h, ctypes.byref(pa), rp, len(refs), ctypes.c_void_p(d["mc"].blocks.data_ptr()),
-                                  d["mc"].class_start, ctypes.c_void_p(d["mc"].masks.data_ptr()), None, sp), "mc")
+            if ready is not None and d.get("mc_bands"):
+                for g, m in enumerate(d["mc_bands"]):
+                    ready(g)
+                    if m is not None:
+                        F.check(L.mi_mc_frame(h, ctypes.byref(pa), rp, len(refs), ctypes.c_void_p(m.blocks.data_ptr()),
+                                              m.class_start, ctypes.c_void_p(m.masks.data_ptr()), None, sp), "mc")
+            else:
+                F.check(L.mi_mc_frame(h, ctypes.byref(pa), rp, len(refs), ctypes.c_void_p(d["mc"].blocks.data_ptr()),
+                                      d["mc"].class_start, ctypes.c_void_p(d["mc"].masks.data_ptr()), None, sp), "mc")
         else:
             for t, t0 in zip(d["frames"][0].planes, d["A0"]):
                 t.copy_(t0)

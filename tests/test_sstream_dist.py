@@ -47,7 +47,32 @@ def oracle_alloc(spec):
     ss_h, ss_v = int(LAYOUT in (1, 2)), int(LAYOUT == 1)
     dt = np.uint8 if BPC == 8 else np.uint16
     dims = [(H, W)] + [((H + ss_v) >> ss_v, (W + ss_h) >> ss_h)] * 2
-    return OraclePicture([np.zeros(d, dt) for d in dims])
+    # receive buffers start as a sentinel: a row still holding it was not received
+    return OraclePicture([np.full(d, SENTINEL, dt) for d in dims])
+
+
+SENTINEL = 0xA5
+BANDS = 3
+
+
+def band_oracle_executor(spec, refs, ready):
+    """Row-level progress check: for every band group g, after ready(g) every reference row
+    the group's MC units read (bands 0..g of every plane) must have arrived; then the frame
+    is reconstructed from the complete references as before."""
+    from rav1d_amd.sstream import band_height, band_rows, mc_band_groups
+    if ready is not None and spec.desc.get("mc") is not None:
+        units = spec.desc["mc"][0]
+        grp = mc_band_groups(units, H, LAYOUT, BANDS)
+        bh, ss_v = band_height(H, BANDS), int(LAYOUT == 1)
+        for g in range(BANDS):
+            ready(g)
+            if not (grp == g).any():
+                continue
+            for r in refs:
+                for p, a in enumerate(r.np):
+                    hi = band_rows(g, bh, H, ss_v if p else 0)[1]
+                    assert not (a[:hi] == SENTINEL).all(axis=1).any(), (spec.idx, g, p)
+    return oracle_executor(spec, refs)
 
 
 def sequential_digests(specs):
@@ -57,12 +82,13 @@ def sequential_digests(specs):
     return {i: picture_digest(p.np) for i, p in pics.items()}
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, bands=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from rav1d_amd.sstream import PipelinedStream
     specs = make_stream_specs(W, H, BPC, LAYOUT, N, SEED)
-    mine = PipelinedStream(oracle_executor, oracle_alloc, rank, world, "cpu").run(specs)
+    ex = band_oracle_executor if bands > 1 else oracle_executor
+    mine = PipelinedStream(ex, oracle_alloc, rank, world, "cpu", bands=bands).run(specs)
     local = {i: picture_digest([p.view(np.uint8 if BPC == 8 else np.uint16) for p in [t.numpy() for t in pic.planes]])
              for i, pic in mine.items()}
     out = [None] * world
@@ -88,14 +114,39 @@ def test_transfer_plan_only_cross_rank():
         assert all(any(s.idx % 2 == q and r in s.refs for s in specs) for q in dsts)
 
 
-@pytest.mark.parametrize("world", [2])
-def test_pipelined_stream_equals_sequential(world):
+def test_mc_band_groups_cover_reads():
+    """Every unit's group covers the reference rows its 8-tap window reads, and a chroma MASK
+    unit never runs before the luma unit whose mask it reads."""
+    from rav1d_amd.sstream import band_height, mc_band_groups
+    from rav1d_amd.synth import make_mc_units
+    w, h, bands = 256, 192, 5
+    rng = np.random.default_rng(7)
+    units, _, _ = make_mc_units(w, h, 1, rng, nrefs=2, compound_frac=0.6, mv_px=48)
+    g = mc_band_groups(units, h, 1, bands)
+    bh = band_height(h, bands)
+    for u, gi in zip(units, g):
+        sv = 1 if u["plane"] else 0
+        for k in range(2):
+            if u["ref"][k] < 0:
+                continue
+            last = ((int(u["y"]) + int(u["h"]) + (int(u["mvy"][k]) >> (3 + sv)) + 4) << sv) + sv
+            assert last >= h - 1 and gi == bands - 1 or last < (gi + 1) * bh, (u, gi)
+    lg = {(int(u["x"]), int(u["y"])): gi for u, gi in zip(units, g) if u["plane"] == 0}
+    for u, gi in zip(units, g):
+        if u["plane"] > 0 and u["ref"][1] >= 0 and u["comp"] == 2:
+            assert gi >= lg[(int(u["x"]) * 2, int(u["y"]) * 2)]
+    assert len(set(g.tolist())) > 1
+
+
+@pytest.mark.parametrize("world,bands", [(2, 1), (2, BANDS)])
+def test_pipelined_stream_equals_sequential(world, bands):
+    """bands > 1: references travel in bands and MC waits per band (row-level progress)."""
     specs = make_stream_specs(W, H, BPC, LAYOUT, N, SEED)
     want = sequential_digests(specs)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, bands)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]

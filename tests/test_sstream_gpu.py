@@ -15,7 +15,7 @@ from tests.test_sstream_dist import _free_port, sequential_digests, W, H, BPC, L
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, bands=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     torch.cuda.set_device(0)
@@ -24,11 +24,11 @@ def _worker(rank, world, port, q):
     from rav1d_amd.sstream import DeviceExecutor, PipelinedStream
     ctx = Context(0)
     specs = make_stream_specs(W, H, BPC, LAYOUT, N, SEED)
-    ex = DeviceExecutor(ctx)
+    ex = DeviceExecutor(ctx, bands=bands)
     for s in specs:
         if s.idx % world == rank:
             ex.prepare(s)
-    mine = PipelinedStream(ex, ex.alloc, rank, world, "cuda").run(specs)
+    mine = PipelinedStream(ex, ex.alloc, rank, world, "cuda", bands=bands).run(specs)
     torch.cuda.synchronize()
     local = {i: picture_digest([f.plane_np(p) for p in range(len(f.planes))]) for i, f in mine.items()}
     out = [None] * world
@@ -37,14 +37,16 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_device_pipelined_stream_equals_oracle_sequential():
+@pytest.mark.parametrize("bands", [1, 3])
+def test_device_pipelined_stream_equals_oracle_sequential(bands):
+    """bands 3: row-level progress (references in bands, MC launched per band group)."""
     specs = make_stream_specs(W, H, BPC, LAYOUT, N, SEED)
     want = sequential_digests(specs)
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, bands)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=100) for _ in range(world)]
