@@ -31,7 +31,8 @@ __device__ __forceinline__ int dir_off(int dir, int k, int ts) {
 #define MI_CDEF_T1 1     // 0: no shifted copy, odd taps read unaligned words
 #endif
 #ifndef MI_CDEF_DIAG
-#define MI_CDEF_DIAG 0   // experiment builds only: 1 no filtering, 2 no filtering or direction search, 3 no tile fetch
+#define MI_CDEF_DIAG 0   // experiment builds only: 1 no filtering, 2 no filtering or direction search, 3 no tile fetch,
+                         // 4 no chroma filter, 5 no luma filter
 #endif
 // Luma tile: 68 rows (2-row halo) x 88 int16 (frame columns x0-8 .. x0+79; interior at column 8).
 // 88 = 44 dwords per row: a 32-lane group's 8 rows x 4 dwords fall on 32 distinct banks, and
@@ -620,9 +621,10 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
     __syncthreads();
 
     // luma: 2048 pairs, one 8x8 block per 32-lane group at a time
-    filter_luma<Px, kTS>(ty, ytaps, bstate, y_sec, a.damping, bdm8, a.src[0], a.dst[0], a.stride[0],
-                         x0, y0, fwy, fhy);
-    if (L) {
+    if (MI_CDEF_DIAG != 5)
+        filter_luma<Px, kTS>(ty, ytaps, bstate, y_sec, a.damping, bdm8, a.src[0], a.dst[0], a.stride[0],
+                             x0, y0, fwy, fhy);
+    if (L && MI_CDEF_DIAG != 4) {
         // chroma: lanes 0..255 U, 256..511 V (damping - 1, cdef_apply.rs)
         const int p = 1 + (threadIdx.x >> 8);
         // (the chroma tile is only staged when uv_lvl != 0: unfiltered chroma copies from D)

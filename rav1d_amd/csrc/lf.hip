@@ -431,6 +431,257 @@ __device__ __forceinline__ void lf_rows_class(Px *t, const uint16_t *list, int n
     }
 }
 
+// ---- two pixel lines per lane in packed 16-bit arithmetic ----
+//
+// The two lines of a lane belong to one edge unit, so they share the filter width and level.
+// Every value of the filter fits 16 bits (12-bit pixels: differences within +-4095, the 8-tap
+// sums within 8 * 4095 + 4; the 16-weight sums of the 13-tap smoother within 65528, so they are
+// shifted as unsigned), and the branches of loopfilter.rs:396-721 become per-half masks
+// (0xffff where a condition holds, from the sign of a difference) merged with v_bfi_b32.
+// This halves the VALU issue of the filter, which bounds the tile kernel.
+typedef short lf_s2 __attribute__((ext_vector_type(2)));
+typedef unsigned short lf_u2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ lf_s2 pk_splat(int x) { return lf_s2{(short)x, (short)x}; }
+__device__ __forceinline__ lf_s2 pk_absd(lf_s2 a, lf_s2 b) {
+    const lf_s2 d = a - b;
+    return __builtin_elementwise_max(d, -d);
+}
+__device__ __forceinline__ lf_s2 pk_max(lf_s2 a, lf_s2 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ lf_s2 pk_min(lf_s2 a, lf_s2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ lf_s2 pk_clamp(lf_s2 a, lf_s2 lo, lf_s2 hi) { return pk_min(pk_max(a, lo), hi); }
+// per half: m ? a : b, for m in {0, 0xffff}
+__device__ __forceinline__ lf_s2 pk_sel(lf_s2 m, lf_s2 a, lf_s2 b) {
+    const uint32_t mu = __builtin_bit_cast(uint32_t, m);
+    return __builtin_bit_cast(lf_s2, (mu & __builtin_bit_cast(uint32_t, a)) | (~mu & __builtin_bit_cast(uint32_t, b)));
+}
+__device__ __forceinline__ uint32_t pk_bits(lf_s2 m) { return __builtin_bit_cast(uint32_t, m); }
+// sum >> 4 of a non-negative 16-bit sum (up to 65535)
+__device__ __forceinline__ lf_s2 pk_shr4u(lf_s2 s) { return __builtin_bit_cast(lf_s2, __builtin_bit_cast(lf_u2, s) >> (unsigned short)4); }
+
+// v[8] = q0, v[7] = p0 (as filter_regs), two lines per element. Lines whose filter mask is
+// clear are returned unchanged.
+template <int WD>
+__device__ __forceinline__ void filter_pk(lf_s2 (&v)[16], int E, int I, int H, int bdm8, int bdmax) {
+    const lf_s2 F = pk_splat(1 << bdm8), zero = pk_splat(0), bmax = pk_splat(bdmax);
+    const lf_s2 Es = pk_splat(E << bdm8), Is = pk_splat(I << bdm8), Hs = pk_splat(H << bdm8);
+    const lf_s2 p3 = v[4], p2 = v[5], p1 = v[6], p0 = v[7], q0 = v[8], q1 = v[9], q2 = v[10], q3 = v[11];
+    const lf_s2 a10 = pk_max(pk_absd(p1, p0), pk_absd(q1, q0));
+    // fm <=> every limit minus its distance is >= 0: sign of the minimum
+    lf_s2 t = pk_min(Is - a10, Es - (pk_absd(p0, q0) * (short)2 + (pk_absd(p1, q1) >> (short)1)));
+    if constexpr (WD > 4) t = pk_min(t, Is - pk_max(pk_absd(p2, p1), pk_absd(q2, q1)));
+    if constexpr (WD > 6) t = pk_min(t, Is - pk_max(pk_absd(p3, p2), pk_absd(q3, q2)));
+    const lf_s2 fm = ~(t >> (short)15);                  // 0xffff: the line is filtered
+    if (!pk_bits(fm)) return;
+    lf_s2 narrow = fm;                                   // lines taking the 4-tap filter
+    lf_s2 flat = zero;
+    if constexpr (WD >= 6) {
+        lf_s2 d = pk_max(pk_max(pk_absd(p2, p0), pk_absd(q2, q0)), a10);
+        if constexpr (WD >= 8) d = pk_max(d, pk_max(pk_absd(p3, p0), pk_absd(q3, q0)));
+        flat = fm & ~((F - d) >> (short)15);             // fm && flat_in
+        narrow = fm & ~flat;
+    }
+    if (pk_bits(narrow)) {
+        const lf_s2 dlo = pk_splat(-(128 << bdm8)), dhi = pk_splat((128 << bdm8) - 1);
+        const lf_s2 hev = (Hs - a10) >> (short)15;       // 0xffff: |p1-p0| or |q1-q0| > H
+        lf_s2 f = pk_clamp(p1 - q1, dlo, dhi) & hev;
+        f = pk_clamp((q0 - p0) * (short)3 + f, dlo, dhi);
+        const lf_s2 f1 = pk_min(f + (short)4, dhi) >> (short)3;
+        const lf_s2 f2 = pk_min(f + (short)3, dhi) >> (short)3;
+        const lf_s2 g = (f1 + (short)1) >> (short)1;
+        v[7] = pk_sel(narrow, pk_clamp(p0 + f2, zero, bmax), v[7]);
+        v[8] = pk_sel(narrow, pk_clamp(q0 - f1, zero, bmax), v[8]);
+        const lf_s2 nh = narrow & ~hev;
+        v[6] = pk_sel(nh, pk_clamp(p1 + g, zero, bmax), v[6]);
+        v[9] = pk_sel(nh, pk_clamp(q1 - g, zero, bmax), v[9]);
+    }
+    if constexpr (WD == 6) {
+        if (pk_bits(flat)) {
+            const lf_s2 c4 = pk_splat(4);
+            v[6] = pk_sel(flat, (p2 * (short)3 + p1 * (short)2 + p0 * (short)2 + q0 + c4) >> (short)3, v[6]);
+            v[7] = pk_sel(flat, (p2 + p1 * (short)2 + p0 * (short)2 + q0 * (short)2 + q1 + c4) >> (short)3, v[7]);
+            v[8] = pk_sel(flat, (p1 + p0 * (short)2 + q0 * (short)2 + q1 * (short)2 + q2 + c4) >> (short)3, v[8]);
+            v[9] = pk_sel(flat, (p0 + q0 * (short)2 + q1 * (short)2 + q2 * (short)3 + c4) >> (short)3, v[9]);
+        }
+    }
+    if constexpr (WD >= 8) {
+        lf_s2 flat8 = flat;
+        if constexpr (WD == 16) {
+            if (pk_bits(flat)) {
+                const lf_s2 d = pk_max(pk_max(pk_max(pk_absd(v[1], p0), pk_absd(v[2], p0)), pk_max(pk_absd(v[3], p0), pk_absd(v[12], q0))),
+                                       pk_max(pk_absd(v[13], q0), pk_absd(v[14], q0)));
+                const lf_s2 flat16 = flat & ~((F - d) >> (short)15);
+                flat8 = flat & ~flat16;
+                if (pk_bits(flat16)) {
+                    // the running 16-weight sum of filter_regs, as unsigned 16-bit
+                    lf_s2 o[12];
+                    lf_s2 s = pk_splat(8) + v[1] * (short)7 + v[2] * (short)2 + v[3] * (short)2 + v[4] + v[5] + v[6] + v[7] + v[8];
+#pragma unroll
+                    for (int k = 0; k < 12; k++) {
+                        const int j = k + 2;
+                        o[k] = pk_shr4u(s);
+                        if (k < 11) {
+                            const int hi = j + 7 > 14 ? 14 : j + 7, lo = j - 6 < 1 ? 1 : j - 6;
+                            s += v[hi] - v[lo] + v[j + 2] - v[j - 1];
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < 12; k++) v[2 + k] = pk_sel(flat16, o[k], v[2 + k]);
+                }
+            }
+        }
+        if (pk_bits(flat8)) {
+            const lf_s2 c4 = pk_splat(4);
+            const lf_s2 n5 = (p3 * (short)3 + p2 * (short)2 + p1 + p0 + q0 + c4) >> (short)3;
+            const lf_s2 n6 = (p3 * (short)2 + p2 + p1 * (short)2 + p0 + q0 + q1 + c4) >> (short)3;
+            const lf_s2 n7 = (p3 + p2 + p1 + p0 * (short)2 + q0 + q1 + q2 + c4) >> (short)3;
+            const lf_s2 n8 = (p2 + p1 + p0 + q0 * (short)2 + q1 + q2 + q3 + c4) >> (short)3;
+            const lf_s2 n9 = (p1 + p0 + q0 + q1 * (short)2 + q2 + q3 * (short)2 + c4) >> (short)3;
+            const lf_s2 n10 = (p0 + q0 + q1 + q2 * (short)2 + q3 * (short)3 + c4) >> (short)3;
+            v[5] = pk_sel(flat8, n5, v[5]);
+            v[6] = pk_sel(flat8, n6, v[6]);
+            v[7] = pk_sel(flat8, n7, v[7]);
+            v[8] = pk_sel(flat8, n8, v[8]);
+            v[9] = pk_sel(flat8, n9, v[9]);
+            v[10] = pk_sel(flat8, n10, v[10]);
+        }
+    }
+}
+
+// Pixel pairs <-> packed lanes. Column edges: a lane holds rows r and r + 1 of one edge unit
+// (low half = row r), gathered from the two rows' 4-pixel quads with v_perm_b32.
+template <typename Px>
+__device__ __forceinline__ void pk_load_quad(const Px *w0, const Px *w1, int q, lf_s2 *o) {
+    if constexpr (sizeof(Px) == 2) {
+        const uint2 d = reinterpret_cast<const uint2 *>(w0)[q], e = reinterpret_cast<const uint2 *>(w1)[q];
+        o[0] = __builtin_bit_cast(lf_s2, __builtin_amdgcn_perm(e.x, d.x, 0x05040100u));
+        o[1] = __builtin_bit_cast(lf_s2, __builtin_amdgcn_perm(e.x, d.x, 0x07060302u));
+        o[2] = __builtin_bit_cast(lf_s2, __builtin_amdgcn_perm(e.y, d.y, 0x05040100u));
+        o[3] = __builtin_bit_cast(lf_s2, __builtin_amdgcn_perm(e.y, d.y, 0x07060302u));
+    } else {
+        const uint32_t d = reinterpret_cast<const uint32_t *>(w0)[q], e = reinterpret_cast<const uint32_t *>(w1)[q];
+        o[0] = __builtin_bit_cast(lf_s2, __builtin_amdgcn_perm(e, d, 0x0c040c00u));
+        o[1] = __builtin_bit_cast(lf_s2, __builtin_amdgcn_perm(e, d, 0x0c050c01u));
+        o[2] = __builtin_bit_cast(lf_s2, __builtin_amdgcn_perm(e, d, 0x0c060c02u));
+        o[3] = __builtin_bit_cast(lf_s2, __builtin_amdgcn_perm(e, d, 0x0c070c03u));
+    }
+}
+// rows r / r + 1 of the pixel pair (v[k], v[k + 1]) as one dword (u16) or halfword (u8) each
+__device__ __forceinline__ uint32_t pk_row_lo(lf_s2 a, lf_s2 b) {
+    return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, a), 0x05040100u);
+}
+__device__ __forceinline__ uint32_t pk_row_hi(lf_s2 a, lf_s2 b) {
+    return __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, a), 0x07060302u);
+}
+__device__ __forceinline__ uint16_t pk_row_lo8(lf_s2 a, lf_s2 b) {
+    return (uint16_t)__builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, a), 0x0c0c0400u);
+}
+__device__ __forceinline__ uint16_t pk_row_hi8(lf_s2 a, lf_s2 b) {
+    return (uint16_t)__builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, a), 0x0c0c0602u);
+}
+
+template <int WD, typename Px, int P>
+__device__ __forceinline__ void lf_col_pair(Px *t, const uint16_t *list, int i, const uint8_t *le,
+                                            const uint8_t *li, int bdm8, int bdmax) {
+    {
+        const int e = list[i >> 1];
+        const int u = e >> 6, L = e & 63;
+        const int r = (u / kLfEdgesV) * 4 + 2 * (i & 1), k = u % kLfEdgesV;
+        Px *w0 = &t[r * P + 4 + 4 * k], *w1 = w0 + P;
+        constexpr int q0 = WD == 16 ? 0 : 1, q1 = WD == 16 ? 4 : 3;   // quads loaded
+        lf_s2 v[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) v[j] = pk_splat(0);
+#pragma unroll
+        for (int q = q0; q < q1; q++) pk_load_quad<Px>(w0, w1, q, &v[4 * q]);
+        filter_pk<WD>(v, le[L], li[L], L >> 4, bdm8, bdmax);
+        if constexpr (WD >= 8) {
+#pragma unroll
+            for (int q = q0; q < q1; q++) {
+                if constexpr (sizeof(Px) == 2) {
+                    reinterpret_cast<uint2 *>(w0)[q] = make_uint2(pk_row_lo(v[4 * q], v[4 * q + 1]), pk_row_lo(v[4 * q + 2], v[4 * q + 3]));
+                    reinterpret_cast<uint2 *>(w1)[q] = make_uint2(pk_row_hi(v[4 * q], v[4 * q + 1]), pk_row_hi(v[4 * q + 2], v[4 * q + 3]));
+                } else {
+                    reinterpret_cast<uint32_t *>(w0)[q] = pk_row_lo8(v[4 * q], v[4 * q + 1]) | ((uint32_t)pk_row_lo8(v[4 * q + 2], v[4 * q + 3]) << 16);
+                    reinterpret_cast<uint32_t *>(w1)[q] = pk_row_hi8(v[4 * q], v[4 * q + 1]) | ((uint32_t)pk_row_hi8(v[4 * q + 2], v[4 * q + 3]) << 16);
+                }
+            }
+        } else {
+            if constexpr (sizeof(Px) == 2) {
+                reinterpret_cast<uint32_t *>(w0)[3] = pk_row_lo(v[6], v[7]);
+                reinterpret_cast<uint32_t *>(w0)[4] = pk_row_lo(v[8], v[9]);
+                reinterpret_cast<uint32_t *>(w1)[3] = pk_row_hi(v[6], v[7]);
+                reinterpret_cast<uint32_t *>(w1)[4] = pk_row_hi(v[8], v[9]);
+            } else {
+                reinterpret_cast<uint16_t *>(w0)[3] = pk_row_lo8(v[6], v[7]);
+                reinterpret_cast<uint16_t *>(w0)[4] = pk_row_lo8(v[8], v[9]);
+                reinterpret_cast<uint16_t *>(w1)[3] = pk_row_hi8(v[6], v[7]);
+                reinterpret_cast<uint16_t *>(w1)[4] = pk_row_hi8(v[8], v[9]);
+            }
+        }
+    }
+}
+
+// Row edges: a lane holds two adjacent pixel columns (one LDS dword per row for u16).
+template <int WD, typename Px, int P>
+__device__ __forceinline__ void lf_row_pair(Px *t, const uint16_t *list, int i, const uint8_t *le,
+                                            const uint8_t *li, int bdm8, int bdmax) {
+    constexpr int nr = WD == 16 ? 7 : WD == 8 ? 4 : WD == 6 ? 3 : 2;   // rows read each side
+    constexpr int lo = WD == 16 ? 2 : WD == 8 ? 5 : 6;                 // rows [lo, 16 - lo) written
+    {
+        const int e = list[i >> 1];
+        const int u = e >> 6, L = e & 63;
+        const int k = u / (kLfTW / 4), col = (u % (kLfTW / 4)) * 4 + 2 * (i & 1);
+        Px *w = &t[(4 * k) * P + 16 + col];
+        lf_s2 v[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            v[j] = pk_splat(0);
+            if (j >= 8 - nr && j < 8 + nr) {
+                if constexpr (sizeof(Px) == 2)
+                    v[j] = __builtin_bit_cast(lf_s2, *reinterpret_cast<const uint32_t *>(w + j * P));
+                else
+                    v[j] = __builtin_bit_cast(lf_s2, __builtin_amdgcn_perm(0u, (uint32_t)*reinterpret_cast<const uint16_t *>(w + j * P), 0x0c010c00u));
+            }
+        }
+        filter_pk<WD>(v, le[L], li[L], L >> 4, bdm8, bdmax);
+#pragma unroll
+        for (int j = lo; j < 16 - lo; j++) {
+            if constexpr (sizeof(Px) == 2)
+                *reinterpret_cast<uint32_t *>(w + j * P) = __builtin_bit_cast(uint32_t, v[j]);
+            else
+                *reinterpret_cast<uint16_t *>(w + j * P) = (uint16_t)__builtin_amdgcn_perm(0u, __builtin_bit_cast(uint32_t, v[j]), 0x0c0c0200u);
+        }
+    }
+}
+
+// The four width classes of one direction as one sequence of 64-pair chunks, dealt to the
+// workgroup's waves in turn: every chunk runs one filter branch (wave-uniform class), and a
+// class leaves at most one partial wave instead of one partial 256-lane pass.
+template <bool COLS, typename Px, int P>
+__device__ __forceinline__ void lf_dir_pk(Px *t, const uint16_t (*lists)[COLS ? (kLfRows / 4) * kLfEdgesV : kLfEdgesH * (kLfTW / 4)],
+                                          const int *cnt, const uint8_t *le, const uint8_t *li, int bdm8, int bdmax) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // chunk prefix over the classes (wave-uniform: the counts are LDS broadcasts)
+    const int c0 = (cnt[0] * 2 + 63) >> 6, c1 = c0 + ((cnt[1] * 2 + 63) >> 6);
+    const int c2 = c1 + ((cnt[2] * 2 + 63) >> 6), c3 = c2 + ((cnt[3] * 2 + 63) >> 6);
+    for (int g = wave; g < c3; g += 4) {
+        const int cls = g < c0 ? 0 : g < c1 ? 1 : g < c2 ? 2 : 3;
+        const int base = cls == 0 ? 0 : cls == 1 ? c0 : cls == 2 ? c1 : c2;
+        const int i = (g - base) * 64 + lane;
+        if (i >= cnt[cls] * 2) continue;
+        switch (cls) {
+#define LF_CASE(k, wd)                                                                     \
+        case k:                                                                            \
+            if constexpr (COLS) lf_col_pair<wd, Px, P>(t, lists[k], i, le, li, bdm8, bdmax); \
+            else lf_row_pair<wd, Px, P>(t, lists[k], i, le, li, bdm8, bdmax);                \
+            break;
+        LF_CASE(0, 4) LF_CASE(1, 6) LF_CASE(2, 8) LF_CASE(3, 16)
+#undef LF_CASE
+        }
+    }
+}
+
 // wd -> work class (lines of one class run the same filter branch)
 __device__ __forceinline__ int lf_class(int wd) { return wd == 4 ? 0 : wd == 6 ? 1 : wd == 8 ? 2 : 3; }
 
@@ -513,6 +764,7 @@ __global__ __launch_bounds__(256) void lf_tile_kernel(LfTileArgs a) {
     }
     __syncthreads();
     // column edges, then row edges, one loop per width class
+#if defined(MI_LF_UNPACKED)
     lf_cols_class<4, Px, P>(t, listv[0], cnt[0], le, li, a.bdm8, a.bdmax);
     lf_cols_class<6, Px, P>(t, listv[1], cnt[1], le, li, a.bdm8, a.bdmax);
     lf_cols_class<8, Px, P>(t, listv[2], cnt[2], le, li, a.bdm8, a.bdmax);
@@ -522,6 +774,11 @@ __global__ __launch_bounds__(256) void lf_tile_kernel(LfTileArgs a) {
     lf_rows_class<6, Px, P>(t, listh[1], cnt[5], le, li, a.bdm8, a.bdmax);
     lf_rows_class<8, Px, P>(t, listh[2], cnt[6], le, li, a.bdm8, a.bdmax);
     lf_rows_class<16, Px, P>(t, listh[3], cnt[7], le, li, a.bdm8, a.bdmax);
+#elif !defined(MI_LF_NOFILTER)
+    lf_dir_pk<true, Px, P>(t, listv, cnt, le, li, a.bdm8, a.bdmax);
+    __syncthreads();
+    lf_dir_pk<false, Px, P>(t, listh, cnt + 4, le, li, a.bdm8, a.bdmax);
+#endif
     __syncthreads();
     uint8_t *dst = a.dst[p];
     constexpr int VPT = kLfTW / VPX;
