@@ -304,6 +304,17 @@ int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
                  const uint32_t size_start[MI_N_RECT_TX_SIZES + 1], void *coef,
                  unsigned flags, void *stream);
 
+/* mi_itx_frame with the blocks of each size further grouped into MI_ITX_BANDS horizontal
+ * picture bands: blocks of size s in band q are blocks[band_start[s][q] .. band_start[s][q+1]),
+ * with band_start[s][MI_ITX_BANDS] == band_start[s+1][0]. Any grouping gives the same pixels;
+ * grouping by position (band q = plane rows [q*h/8, (q+1)*h/8), as mi_itx_band_of) makes each
+ * band run on one XCD, so a pixel line is fetched into and written back from one L2 whichever
+ * transform sizes touch it. */
+#define MI_ITX_BANDS 8
+int mi_itx_frame_banded(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
+                        const uint32_t band_start[MI_N_RECT_TX_SIZES][MI_ITX_BANDS + 1], void *coef,
+                        unsigned flags, void *stream);
+
 /* Intra prediction of n independent blocks (one wavefront step of a frame, or any set of
  * blocks whose edges are final): writes each block into `pic` from its gathered edges
  * (rav1d_prepare_intra_edges output, src/ipred_prepare.rs:118-204). `blocks`, `edges`

@@ -137,6 +137,8 @@ def lib():
     _sig(L, "mi_ctx_last_error", ctypes.c_int, [_VP])
     _sig(L, "mi_itx_frame", ctypes.c_int,
          [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.POINTER(ctypes.c_uint32), _VP, ctypes.c_uint, _VP])
+    _sig(L, "mi_itx_frame_banded", ctypes.c_int,
+         [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.POINTER(ctypes.c_uint32), _VP, ctypes.c_uint, _VP])
     _sig(L, "mi_dsp_itxfm_add", ctypes.c_int,
          [ctypes.c_int, ctypes.c_int, _VP, ctypes.c_ssize_t, _VP, ctypes.c_int, ctypes.c_int])
     _sig(L, "mi_mc_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture), ctypes.c_int,
@@ -210,7 +212,7 @@ def lib():
 
 # Every symbol include/mi_av1dsp.h declares (checked by tests/test_abi.py).
 EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
-            "mi_itx_frame", "mi_mc_frame", "mi_mc_frame_ex", "mi_mc_scaled", "mi_mc_warp", "mi_mc_combine", "mi_superres_frame",
+            "mi_itx_frame", "mi_itx_frame_banded", "mi_mc_frame", "mi_mc_frame_ex", "mi_mc_scaled", "mi_mc_warp", "mi_mc_combine", "mi_superres_frame",
             "mi_ipred_blocks", "mi_intra_blocks", "mi_intra_recon", "mi_ctx_device_status", "mi_deblock_frame", "mi_deblock_frame_to", "mi_cdef_frame", "mi_lr_frame",
             "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply", "mi_frame_run", "mi_frame_end", "mi_frame_validate",
             "mi_ctx_set_timing", "mi_ctx_timing",

@@ -90,6 +90,12 @@ struct ItxArgs {
     int wg_start[20];   // first workgroup of the i-th size in grid order (kItxLaunchOrder)
     int wg_size[19];    // tx size of the i-th range
     int blk_start[20];  // block ranges per tx size (enum order, as the caller groups them)
+    // nbands 8: inside a size the blocks are further grouped by horizontal picture band (band q
+    // = blocks[band_start[s][q] .. band_start[s][q + 1])), and band q's workgroups get grid
+    // indices = q mod 8, i.e. run on XCD q (the dispatcher's round robin): every pixel line of
+    // the band is fetched into, and written back from, one XCD's L2 whichever sizes touch it
+    int band_start[19][9];
+    int nbands;         // 1 or 8
     int pw[3], ph[3];   // plane extents (128-aligned picture area; 0 = no such plane)
     int *err;           // device error word: set when a descriptor is rejected
 };
@@ -105,8 +111,10 @@ __host__ __device__ constexpr uint32_t itx_legal_types(int tx) {
 // order of the tx sizes in the itx grid: the 64-point sizes first (few workgroups, the longest),
 // then the 32-point sizes, then every size with both sides <= 16
 constexpr int kItxLaunchOrder[19] = { 4, 11, 12, 17, 18, 3, 9, 10, 15, 16, 0, 1, 2, 5, 6, 7, 8, 13, 14 };
-// fills wg_start / wg_size / blk_start; returns the grid size
-int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start);
+constexpr int kItxBands = 8;
+// fills wg_start / wg_size / blk_start (and the band table when band_start, [19][9], is given);
+// returns the grid size
+int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start, const uint32_t *band_start = nullptr);
 
 // launcher (itx.hip)
 int launch_itx_frame(const ItxArgs &a, int nwg, int bpc, hipStream_t s);

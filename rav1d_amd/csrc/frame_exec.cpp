@@ -651,14 +651,24 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         for (int i = 0; i < (k ? f->n_obmc_v : f->n_obmc_h); i++) (scaled[u[i].ref[0]] ? lap_s[k] : plain).push_back(u[i]);
         bucket_mc(plain.data(), (int)plain.size(), lap_b[k], lap_cs[k]);
     }
+    // residuals grouped by (tx size, picture band) for mi_itx_frame_banded: a counting sort
+    // keeping decode order inside a group
     std::vector<MiTxBlock> itx_b(f->n_inter_tx);
-    uint32_t itx_ss[MI_N_RECT_TX_SIZES + 1] = {};
+    uint32_t itx_bs[MI_N_RECT_TX_SIZES][MI_ITX_BANDS + 1] = {};
     {
-        for (int i = 0; i < f->n_inter_tx; i++) itx_ss[f->inter_tx[i].tx + 1]++;
-        for (int t = 0; t < MI_N_RECT_TX_SIZES; t++) itx_ss[t + 1] += itx_ss[t];
-        uint32_t pos[MI_N_RECT_TX_SIZES];
-        memcpy(pos, itx_ss, sizeof(pos));
-        for (int i = 0; i < f->n_inter_tx; i++) itx_b[pos[f->inter_tx[i].tx]++] = f->inter_tx[i];
+        constexpr int NK = MI_N_RECT_TX_SIZES * MI_ITX_BANDS;
+        const int ah = (f->h + 127) & ~127, ssv = f->layout == 1;
+        auto key = [&](const MiTxBlock &b) {
+            const int ph = b.plane ? ah >> ssv : ah;
+            const int q = (int)((int64_t)b.y * MI_ITX_BANDS / ph);
+            return (int)b.tx * MI_ITX_BANDS + (q < MI_ITX_BANDS - 1 ? q : MI_ITX_BANDS - 1);
+        };
+        uint32_t start[NK + 1] = {};
+        for (int i = 0; i < f->n_inter_tx; i++) start[key(f->inter_tx[i]) + 1]++;
+        for (int k = 0; k < NK; k++) start[k + 1] += start[k];
+        for (int t = 0; t < MI_N_RECT_TX_SIZES; t++)
+            for (int q = 0; q <= MI_ITX_BANDS; q++) itx_bs[t][q] = start[t * MI_ITX_BANDS + q];
+        for (int i = 0; i < f->n_inter_tx; i++) itx_b[start[key(f->inter_tx[i])]++] = f->inter_tx[i];
     }
     const int sb128h = (f->h + 127) >> 7;
     std::vector<Section> secs = {
@@ -731,7 +741,7 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
                 return r;
         }
         if (f->n_inter_tx &&
-            (r = mi_itx_frame(ctx, &cur, (const MiTxBlock *)D(20), itx_ss, D(4), 0, stream)))
+            (r = mi_itx_frame_banded(ctx, &cur, (const MiTxBlock *)D(20), itx_bs, D(4), 0, stream)))
             return r;
     }
 

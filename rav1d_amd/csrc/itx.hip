@@ -19,6 +19,7 @@
 // integer networks, not contractions).
 #include "common.h"
 #include "itx_1d.h"
+#include <algorithm>
 #include <type_traits>
 
 namespace mi {
@@ -86,6 +87,17 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
 
     const int t = threadIdx.x;
     const int lb = t / TPB, j = t % TPB;
+    // this workgroup's block range: the whole size, or (banded grid) band lwg % 8 of it
+    int bs = a.blk_start[TX], be = a.blk_start[TX + 1], k = lwg;
+    if (a.nbands > 1) {
+        const int q = lwg & 7;
+        k = lwg >> 3;
+        bs = a.band_start[TX][0];
+        be = a.band_start[TX][1];
+#pragma unroll
+        for (int i = 1; i < 8; i++)
+            if (q == i) { bs = a.band_start[TX][i]; be = a.band_start[TX][i + 1]; }
+    }
     // per-plane arguments as locals (selected by value, never by address into the kernarg)
     uint8_t *const plane3[3] = { a.plane[0], a.plane[1], a.plane[2] };
     const int64_t stride3[3] = { a.stride[0], a.stride[1], a.stride[2] };
@@ -106,8 +118,8 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     int ck[CR][CW];
 #pragma unroll
     for (int rd = 0; rd < ROUNDS; rd++) {
-        const int bi = a.blk_start[TX] + (lwg * ROUNDS + rd) * BPW + lb;
-        bool valid = bi < a.blk_start[TX + 1];
+        const int bi = bs + (k * ROUNDS + rd) * BPW + lb;
+        bool valid = bi < be;
         MiTxBlock b{};
         if (valid) {
             b = a.blocks[bi];
@@ -300,18 +312,33 @@ __global__ __launch_bounds__(kItxThreads, MI_ITX_MINW) void itx_frame_kernel(Itx
     }
 }
 
-int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start) {
+int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start, const uint32_t *band_start) {
     int wg = 0;
+    a.nbands = band_start ? kItxBands : 1;
     for (int i = 0; i < 19; i++) {
         const int sz = kItxLaunchOrder[i];
         a.wg_start[i] = wg;
         a.wg_size[i] = sz;
-        const int n = (int)(size_start[sz + 1] - size_start[sz]);
         const int per_wg = itx_blocks_per_wg(sz) * itx_rounds(sz);
-        wg += (n + per_wg - 1) / per_wg;
+        if (band_start) {
+            // 8 x the largest band's workgroup count: grid index 8m + q serves band q
+            const uint32_t *b = band_start + sz * (kItxBands + 1);
+            int m = 0;
+            for (int q = 0; q < kItxBands; q++) {
+                const int n = (int)(b[q + 1] - b[q]);
+                m = std::max(m, (n + per_wg - 1) / per_wg);
+            }
+            wg += kItxBands * m;
+        } else {
+            const int n = (int)(size_start[sz + 1] - size_start[sz]);
+            wg += (n + per_wg - 1) / per_wg;
+        }
     }
     a.wg_start[19] = wg;
     for (int k = 0; k <= 19; k++) a.blk_start[k] = (int)size_start[k];
+    if (band_start)
+        for (int s = 0; s < 19; s++)
+            for (int q = 0; q <= kItxBands; q++) a.band_start[s][q] = (int)band_start[s * (kItxBands + 1) + q];
     return wg;
 }
 

@@ -121,12 +121,20 @@ def _stream_ptr(stream):
     return ctypes.c_void_p(stream.cuda_stream)
 
 
-def itx_frame(ctx, frame, blocks_dev, size_start, coef_dev, flags=0, stream=None):
-    """mi_itx_frame: inverse transform + add for all blocks of a frame (device tensors)."""
+def itx_frame(ctx, frame, blocks_dev, size_start, coef_dev, flags=0, stream=None, band_start=None):
+    """mi_itx_frame: inverse transform + add for all blocks of a frame (device tensors).
+    band_start ([19][9], synth.itx_band_order): the blocks are also grouped by picture band
+    and run through mi_itx_frame_banded (one XCD per band)."""
     pic = frame.picture()
-    ss = (ctypes.c_uint32 * 20)(*[int(v) for v in size_start])
     if blocks_dev.dtype != torch.uint8 or not blocks_dev.is_cuda:
         raise MiError("blocks must be a device uint8 tensor holding MiTxBlock records")
+    if band_start is not None:
+        bs = (ctypes.c_uint32 * (19 * 9))(*[int(v) for v in np.asarray(band_start).reshape(-1)])
+        rc = lib().mi_itx_frame_banded(ctx.h, ctypes.byref(pic), ctypes.c_void_p(blocks_dev.data_ptr()), bs,
+                                       ctypes.c_void_p(coef_dev.data_ptr()), flags, _stream_ptr(stream))
+        check(rc, "mi_itx_frame_banded")
+        return
+    ss = (ctypes.c_uint32 * 20)(*[int(v) for v in size_start])
     rc = lib().mi_itx_frame(ctx.h, ctypes.byref(pic), ctypes.c_void_p(blocks_dev.data_ptr()), ss,
                             ctypes.c_void_p(coef_dev.data_ptr()), flags, _stream_ptr(stream))
     check(rc, "mi_itx_frame")

@@ -171,6 +171,28 @@ def itx_device_order(blocks):
     return blocks, np.searchsorted(blocks["tx"], np.arange(N_RECT_TX_SIZES + 1)).astype(np.uint32)
 
 
+ITX_BANDS = 8
+
+
+def itx_band_order(blocks, plane_heights):
+    """mi_itx_frame_banded order: grouped by tx size, inside a size by picture band (band q =
+    plane rows [q*h/8, (q+1)*h/8) of the block's plane, h = the 128-aligned plane height),
+    then as itx_device_order. Returns (blocks, size_start, band_start[19][9])."""
+    ph = np.asarray(plane_heights, np.int64)
+    band = np.minimum(blocks["y"].astype(np.int64) * ITX_BANDS // ph[blocks["plane"]], ITX_BANDS - 1)
+    dc = (blocks["txtp"] == 0) & (blocks["eob"] < 1)
+    order = np.lexsort((blocks["x"], blocks["y"], blocks["plane"], ~dc, band, blocks["tx"]))
+    blocks = blocks[order]
+    band = band[order]
+    key = blocks["tx"].astype(np.int64) * ITX_BANDS + band
+    band_start = np.searchsorted(key, np.arange(N_RECT_TX_SIZES * ITX_BANDS + 1)).astype(np.uint32)
+    bs = np.empty((N_RECT_TX_SIZES, ITX_BANDS + 1), np.uint32)
+    for t in range(N_RECT_TX_SIZES):
+        bs[t] = band_start[t * ITX_BANDS:(t + 1) * ITX_BANDS + 1]
+    size_start = np.searchsorted(blocks["tx"], np.arange(N_RECT_TX_SIZES + 1)).astype(np.uint32)
+    return blocks, size_start, bs
+
+
 def itx_algorithmic_bytes(blocks, bpc, zero_coefs=True):
     """sum over blocks of coefB*n_coef (+ the zeroing write) + 2*pixB*w*h,
     plus the 16-byte descriptor."""

@@ -10,20 +10,24 @@ import torch
 
 from rav1d_amd import ITX_KEEP_COEFS, lib
 from rav1d_amd.frame import Frame, itx_frame
-from rav1d_amd.synth import TX_DIMS, make_coefs, make_itx_frame, tx_types
+from rav1d_amd.synth import TX_DIMS, itx_band_order, make_coefs, make_itx_frame, tx_types
 from tests import oracle_lib
 from tests.oracle_lib import ptr
 
 pytestmark = pytest.mark.gpu
 
 
-def run_frame(gpu, fr, flags=0):
+def run_frame(gpu, fr, flags=0, banded=False):
     f = Frame(fr["w"], fr["h"], fr["bpc"], fr["layout"])
     for p, arr in enumerate(fr["planes"]):
         f.set_plane_np(p, arr)
-    blocks = torch.from_numpy(fr["blocks"].view(np.uint8).copy()).cuda()
+    blk, bands = fr["blocks"], None
+    if banded:
+        ah = (fr["h"] + 127) & ~127
+        blk, _, bands = itx_band_order(blk, [ah, ah >> 1, ah >> 1])
+    blocks = torch.from_numpy(blk.view(np.uint8).copy()).cuda()
     coef = torch.from_numpy(fr["coef"].copy()).cuda()
-    itx_frame(gpu, f, blocks, fr["size_start"], coef, flags)
+    itx_frame(gpu, f, blocks, fr["size_start"], coef, flags, band_start=bands)
     torch.cuda.synchronize()
     return [f.plane_np(p) for p in range(len(fr["planes"]))], coef.cpu().numpy()
 
@@ -48,12 +52,48 @@ def test_itx_keep_coefs_flag(gpu):
 
 
 @pytest.mark.parametrize("bpc", [8, 10])
-def test_itx_frame_1080p_matches_oracle(gpu, bpc):
+@pytest.mark.parametrize("banded", [False, True])
+def test_itx_frame_1080p_matches_oracle(gpu, bpc, banded):
     fr = make_itx_frame(1920, 1080, bpc=bpc, seed=0x1D1C0001)
-    got, _ = run_frame(gpu, fr)
+    got, coef_after = run_frame(gpu, fr, banded=banded)
     ref = oracle_lib.itx_frame([p.copy() for p in fr["planes"]], fr["blocks"], fr["coef"].copy(), bpc)
     for p in range(3):
         assert np.array_equal(got[p], ref[p])
+    assert not coef_after.any()
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+def test_itx_banded_small_frames_match_oracle(gpu, bpc):
+    # bands with no blocks of a size, bands holding a single workgroup's blocks, WHT blocks
+    for seed, (w, h) in enumerate([(64, 64), (256, 192), (640, 360)]):
+        fr = make_itx_frame(w, h, bpc=bpc, seed=seed + 11, with_wht=True)
+        got, coef_after = run_frame(gpu, fr, banded=True)
+        ref = oracle_lib.itx_frame([p.copy() for p in fr["planes"]], fr["blocks"], fr["coef"].copy(), bpc)
+        for p in range(3):
+            assert np.array_equal(got[p], ref[p]), (w, h, p)
+        assert not coef_after.any()
+
+
+def test_itx_banded_rejects_malformed_band_table(gpu):
+    import ctypes
+    from rav1d_amd.frame import _stream_ptr
+    fr = make_itx_frame(128, 128, bpc=10, seed=3)
+    ah = 128
+    blk, _, bands = itx_band_order(fr["blocks"], [ah, ah >> 1, ah >> 1])
+    f = Frame(128, 128, 10, 1)
+    blocks = torch.from_numpy(blk.view(np.uint8).copy()).cuda()
+    coef = torch.from_numpy(fr["coef"].copy()).cuda()
+    assert bands[0, 3] > 0
+    pic = f.picture()
+    dec = bands.copy()
+    dec[0, 4] = dec[0, 3] - 1                  # a band range that runs backwards
+    gap = bands.copy()
+    gap[1:, :] += 1                            # size 1 does not start where size 0 ends
+    for bad in (dec, gap):
+        arr = (ctypes.c_uint32 * 171)(*[int(v) for v in bad.reshape(-1)])
+        rc = lib().mi_itx_frame_banded(gpu.h, ctypes.byref(pic), ctypes.c_void_p(blocks.data_ptr()), arr,
+                                       ctypes.c_void_p(coef.data_ptr()), 0, _stream_ptr(None))
+        assert rc == -22
 
 
 @pytest.mark.parametrize("bpc", [8, 10, 12])
