@@ -164,6 +164,9 @@ __device__ __forceinline__ void predict(const McArgs &a, const int16_t *win, int
 #ifndef MI_MC_LPT
 #define MI_MC_LPT 0   // 1: classes dispatched largest first; measured slower at 4K10 (83 vs 75 us)
 #endif
+#ifndef MI_MC_XCD_CLASS
+#define MI_MC_XCD_CLASS 1   // each class's waves in 8 contiguous chunks, one per XCD
+#endif
 template <typename Px>
 // g: 0 / 1 = the waves of plane group 0 / 1; 2 = both groups in one grid (group 0's waves,
 // then group 1's; mi_mc_frame_ex with MI_MC_ONE_GRID: no chroma unit reads a mask written
@@ -191,9 +194,20 @@ __global__ __launch_bounds__(64, MC_MIN_WAVES) void mc_kernel(McArgs a, int g) {
     for (int k = 1; k < MI_MC_NCLASS; k++)
         if (fw[k] <= (uint32_t)wave) c = k;
 #endif
-    const int item = wave - (int)fw[c];
+    int item = wave - (int)fw[c];
     const ClassGeom G = class_geom(c);
     const uint32_t cls_begin = a.class_start[g * MI_MC_NCLASS + c], cls_end = a.class_start[g * MI_MC_NCLASS + c + 1];
+#if MI_MC_XCD_CLASS && !MI_MC_LPT
+    {
+        // the class's waves (padded to a multiple of 8, mc_plan) as 8 contiguous chunks, chunk x
+        // on XCD x (grid index mod 8): units are in picture order inside a class, so each XCD
+        // predicts one band of the picture and reads the reference rows around it into its L2
+        const int chunk = (int)(fw[c + 1] - fw[c]) >> 3;
+        item = (item & 7) * chunk + (item >> 3);
+        const uint32_t n = cls_end - cls_begin;
+        if ((uint32_t)item >= (G.T == 1 ? (n + G.U - 1) / G.U : n * G.T)) return;
+    }
+#endif
 
     // this lane's unit, tile origin, column and rows
     int uu, tx0 = 0, ty0 = 0, rg, col;
@@ -420,6 +434,7 @@ int mc_plan(McArgs &a, int g) {
             if ((TR + 7) * win_stride(TW) > kWinElems) return -1;
             waves += n * (uint32_t)((w / TW) * (h / TR));
         }
+        if (MI_MC_XCD_CLASS && !MI_MC_LPT) waves = (waves + 7) & ~7u;   // whole chunks per XCD (mc_kernel)
     }
     a.first_wave[g][MI_MC_NCLASS] = waves;
     return (int)waves;

@@ -606,9 +606,11 @@ def mc_sort_units(units):
     stably sorted units and class_start[2 * MC_NCLASS + 1]."""
     grp = (units["plane"] > 0).astype(np.int64)
     key = grp * MC_NCLASS + mc_class_of(units)
-    # within a class, units grouped by compound type / single-reference destination: waves stay uniform
+    # within a class, units in 64-row picture bands (mi_mc_frame deals a class's waves to the
+    # XCDs in 8 contiguous chunks: each XCD then predicts one region of the picture), inside a
+    # band grouped by compound type / single-reference destination: waves stay uniform
     sub = units["comp"].astype(np.int64) + 16 * (units["ref"][:, 1] < 0)
-    order = np.lexsort((sub, key))
+    order = np.lexsort((sub, units["y"].astype(np.int64) >> 6, key))
     cs = np.searchsorted(key[order], np.arange(2 * MC_NCLASS + 1)).astype(np.uint32)
     return units[order], cs
 
