@@ -58,12 +58,12 @@ __host__ __device__ constexpr int itx_lanes(int tx) {
 constexpr int kItxThreads = 256;
 __host__ __device__ constexpr int itx_blocks_per_wg(int tx) { return kItxThreads / itx_lanes(tx); }
 // Rounds of itx_blocks_per_wg blocks per workgroup: the small sizes' loads of all rounds are in
-// flight together (4-lane blocks: 4 rounds, 8-lane: 2).
+// flight together (4-lane blocks: 4 rounds; 8-lane blocks: 1).
 #ifndef MI_ITX_ROUNDS4
 #define MI_ITX_ROUNDS4 4
 #endif
 #ifndef MI_ITX_ROUNDS8
-#define MI_ITX_ROUNDS8 2
+#define MI_ITX_ROUNDS8 1   // 8-lane sizes: 1 round (banded grid, 4K10: 49.8 vs 50.7-51.3 us with 2; 4 rounds 56-58)
 #endif
 __host__ __device__ constexpr int itx_rounds(int tx) { return itx_lanes(tx) <= 4 ? MI_ITX_ROUNDS4 : itx_lanes(tx) <= 8 ? MI_ITX_ROUNDS8 : 1; }
 
@@ -135,7 +135,10 @@ struct LfArgs {
 #ifndef MI_LF_TW
 #define MI_LF_TW 64   // 64x64 measured fastest at 4K10: 29.6 us vs 34.9 (128x64), 32.5 (32x64)
 #endif
-constexpr int kLfTW = MI_LF_TW, kLfTH = 64;
+#ifndef MI_LF_TH
+#define MI_LF_TH 64
+#endif
+constexpr int kLfTW = MI_LF_TW, kLfTH = MI_LF_TH;
 struct LfTileArgs {
     const uint8_t *src[3];
     uint8_t *dst[3];

@@ -392,7 +392,10 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
     int16_t *hor = reinterpret_cast<int16_t *>(A);    // Wiener: [70][64] aliases A
 
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    const int blk = blockIdx.x;
+#ifndef MI_LR_XCD
+#define MI_LR_XCD 0   // tile -> XCD: 0 hardware round robin, 1 contiguous ranges (xcd_block), C > 1 runs of C
+#endif
+    const int blk = MI_LR_XCD == 1 ? xcd_block(blockIdx.x, gridDim.x) : MI_LR_XCD > 1 ? xcd_chunk(blockIdx.x, gridDim.x, MI_LR_XCD) : blockIdx.x;
     const int p = blk < a.blk_start[1] ? 0 : blk < a.blk_start[2] ? 1 : 2;
     const int lb = blk - a.blk_start[p];
     const int tiles = a.tiles_x[p];
