@@ -248,8 +248,8 @@ void oracle_fg_apply(void *const out[3], void *const in[3], const ptrdiff_t stri
     const FGData *data = data_;
     FPX px = { bpc > 8, (1 << bpc) - 1, bpc - 8 };
     const int bdmax = px.bdmax;
-    static int16_t lut[3][GH + 1][GW];
-    static uint8_t scaling[3][4096];
+    static _Thread_local int16_t lut[3][GH + 1][GW];
+    static _Thread_local uint8_t scaling[3][4096];
     const int ss_y = layout == 1, ss_x = layout == 1 || layout == 2;
 
     oracle_fg_generate_grain_y(&lut[0][0][0], data, bdmax);

@@ -574,7 +574,7 @@ void oracle_itxfm_add(int tx, int txtp, void *dst_, ptrdiff_t stride, void *coef
     else { row_lo = (int)((unsigned)~bdmax << 7); col_lo = (int)((unsigned)~bdmax << 5); }
     const int row_hi = ~row_lo, col_hi = ~col_lo;
 
-    static int32_t tmp[64 * 64];
+    static _Thread_local int32_t tmp[64 * 64];
     memset(tmp, 0, sizeof(tmp));
     const int rk = ty_row[txtp], ck = ty_col[txtp];
     for (int y = 0; y < sh; y++) {

@@ -35,10 +35,10 @@ static const uint16_t sgr_params[16][2] = {
 };
 /* x_by_x[z] = round(256 / (z + 1)) with the ends pinned to 255 and 0; checked against the
  * reference table by tests/test_oracle_lr.py when the reference is mounted. */
-static uint8_t sgr_x_by_x[256];
+static _Thread_local uint8_t sgr_x_by_x[256];
 static void init_tables(void)
 {
-    static int done;
+    static _Thread_local int done;
     if (done) return;
     for (int z = 0; z < 256; z++) sgr_x_by_x[z] = (uint8_t)((256 + (z + 1) / 2) / (z + 1));
     sgr_x_by_x[0] = 255;
@@ -124,7 +124,7 @@ typedef struct {
 static void wiener(const PX *px, void *p, ptrdiff_t ps, const int (*left)[4], const void *lpf,
                    int w, int h, const LrParams *prm, int edges)
 {
-    static int tmp[70 * RUS], hor[70 * RUS];
+    static _Thread_local int tmp[70 * RUS], hor[70 * RUS];
     padding(px, tmp, p, ps, left, lpf, w, h, edges);
     const int bd = px->bd;
     const int rbh = 3 + (bd == 12) * 2;
@@ -168,7 +168,7 @@ static void boxsum(int *sumsq, int *sum, const int *src, int w, int h, int r, in
 static void selfguided(const PX *px, int *dst, const int *src, int w, int h, int n, unsigned s)
 {
     init_tables();
-    static int sumsq[70 * RUS], sum[70 * RUS];
+    static _Thread_local int sumsq[70 * RUS], sum[70 * RUS];
     const unsigned one_by_x = n == 25 ? 164 : 455;
     const int step = (n == 25) + 1;
     boxsum(sumsq, sum, src, w, h, n == 25 ? 2 : 1, step);
@@ -225,7 +225,7 @@ static void selfguided(const PX *px, int *dst, const int *src, int w, int h, int
 static void sgr(const PX *px, int kind, void *p, ptrdiff_t ps, const int (*left)[4], const void *lpf,
                 int w, int h, const LrParams *prm, int edges)
 {
-    static int tmp[70 * RUS], d0[64 * 384], d1[64 * 384];
+    static _Thread_local int tmp[70 * RUS], d0[64 * 384], d1[64 * 384];
     padding(px, tmp, p, ps, left, lpf, w, h, edges);
     if (kind != 1) selfguided(px, d0, tmp, w, h, 25, (unsigned)prm->s0);
     if (kind != 0) selfguided(px, d1, tmp, w, h, 9, (unsigned)prm->s1);
@@ -323,7 +323,7 @@ static void lr_sbrow(const LrFrame *f, uint8_t *p, ptrdiff_t stride, int y, int 
     const int max_unit_size = unit_size + half_unit_size;
     const int row_y = y + ((8 >> ss_ver) * !!y);
     const int shift_hor = 7 - ss_hor;
-    static int pre_lr_border[2][128 + 8][4];
+    static _Thread_local int pre_lr_border[2][128 + 8][4];
     const ORestUnit *lr[2];
     int edges = (y > 0 ? LR_HAVE_TOP : 0) | LR_HAVE_RIGHT;
     int aligned_unit_pos = row_y & ~(unit_size - 1);

@@ -89,7 +89,7 @@ static void mc_8tap(void *dst, ptrdiff_t ds, int16_t *tmp, const void *src, ptrd
     const int8_t *fh = hfilter(mx, w, filter_type & 3), *fv = vfilter(my, h, filter_type >> 2);
     const int ib = b.ib;
     if (fh && fv) {
-        int16_t *mid = malloc(sizeof(int16_t) * 128 * 135);
+        static _Thread_local int16_t mid_a[128 * 135]; int16_t *mid = mid_a;
         for (int y = 0; y < h + 7; y++)
             for (int x = 0; x < w; x++)
                 mid[y * 128 + x] = (int16_t)rnd(tap8_px(src, ss, y - 3, x, 0, 1, fh, b.bpc), 6 - ib);
@@ -98,7 +98,7 @@ static void mc_8tap(void *dst, ptrdiff_t ds, int16_t *tmp, const void *src, ptrd
                 if (tmp) tmp[y * w + x] = (int16_t)(rnd(tap8_mid(mid, 128, y + 3, x, fv), 6) - b.bias);
                 else stp(dst, ds, y, x, clip(rnd(tap8_mid(mid, 128, y + 3, x, fv), 6 + ib), 0, b.bdmax), b.bpc);
             }
-        free(mid);
+        
     } else if (fh) {
         const int irnd = 32 + ((1 << (6 - ib)) >> 1);
         for (int y = 0; y < h; y++)
@@ -131,7 +131,7 @@ static void mc_bilin(void *dst, ptrdiff_t ds, int16_t *tmp, const void *src, ptr
     const int ib = b.ib;
 #define BIL_PX(y, x, m, dy, dx) (16 * ldp(src, ss, y, x, b.bpc) + (m) * (ldp(src, ss, (y) + (dy), (x) + (dx), b.bpc) - ldp(src, ss, y, x, b.bpc)))
     if (mx && my) {
-        int16_t *mid = malloc(sizeof(int16_t) * 128 * 129);
+        static _Thread_local int16_t mid_b[128 * 129]; int16_t *mid = mid_b;
         for (int y = 0; y < h + 1; y++)
             for (int x = 0; x < w; x++) mid[y * 128 + x] = (int16_t)rnd(BIL_PX(y, x, mx, 0, 1), 4 - ib);
         for (int y = 0; y < h; y++)
@@ -141,7 +141,7 @@ static void mc_bilin(void *dst, ptrdiff_t ds, int16_t *tmp, const void *src, ptr
                 if (tmp) tmp[y * w + x] = (int16_t)(rnd(s, 4) - b.bias);
                 else stp(dst, ds, y, x, clip(rnd(s, 4 + ib), 0, b.bdmax), b.bpc);
             }
-        free(mid);
+        
     } else if (mx) {
         const int irnd = (1 << ib) >> 1;
         for (int y = 0; y < h; y++)
@@ -191,7 +191,7 @@ void oracle_mc_scaled(int filter2d, int prep, void *dst, ptrdiff_t dst_stride, i
     const int ib = b.ib;
     if (filter2d == 9) {
         const int tmp_h = (((h - 1) * dy + my) >> 10) + 2;
-        int16_t *mid = malloc(sizeof(int16_t) * 128 * (256 + 1));
+        static _Thread_local int16_t mid_c[128 * (256 + 1)]; int16_t *mid = mid_c;
         for (int y = 0; y < tmp_h; y++) {
             int imx = mx, ioff = 0;
             for (int x = 0; x < w; x++) {
@@ -215,12 +215,12 @@ void oracle_mc_scaled(int filter2d, int prep, void *dst, ptrdiff_t dst_stride, i
             row += my >> 10;
             my &= 0x3ff;
         }
-        free(mid);
+        
         return;
     }
     const int ft = f2d_h[filter2d] | f2d_v[filter2d] << 2;
     const int tmp_h = (((h - 1) * dy + my) >> 10) + 8;
-    int16_t *mid = malloc(sizeof(int16_t) * 128 * (256 + 7));
+    static _Thread_local int16_t mid_d[128 * (256 + 7)]; int16_t *mid = mid_d;
     for (int y = 0; y < tmp_h; y++) {
         int imx = mx, ioff = 0;
         for (int x = 0; x < w; x++) {
@@ -248,7 +248,7 @@ void oracle_mc_scaled(int filter2d, int prep, void *dst, ptrdiff_t dst_stride, i
         row += my >> 10;
         my &= 0x3ff;
     }
-    free(mid);
+    
 }
 
 /* avg_c / w_avg_c / mask_c (mc_tmpl.c:561-620) */
@@ -419,7 +419,7 @@ static void mc_block(const McBlock *bk, int i, void *dst, ptrdiff_t ds, int16_t 
     ptrdiff_t ref_stride = rs;
     uint8_t *emu = NULL;
     if (dx < !!mx * 3 || dy < !!my * 3 || dx + bk->w + !!mx * 4 > w || dy + bk->h + !!my * 4 > h) {
-        emu = malloc((size_t)192 * 192 * pb);
+        { static _Thread_local uint16_t emu_a[192 * 192]; emu = (uint8_t *)emu_a; }
         oracle_mc_emu_edge(bk->w + !!mx * 7, bk->h + !!my * 7, w, h, dx - !!mx * 3, dy - !!my * 3,
                            emu, 192 * pb, refp, rs, bpc);
         ref = emu + (192 * !!my * 3 + !!mx * 3) * pb;
@@ -429,7 +429,7 @@ static void mc_block(const McBlock *bk, int i, void *dst, ptrdiff_t ds, int16_t 
     }
     if (tmp) oracle_mc_prep(bk->filter2d, tmp, ref, ref_stride, bk->w, bk->h, mx << !ss_hor, my << !ss_ver, bpc);
     else oracle_mc_put(bk->filter2d, dst, ds, ref, ref_stride, bk->w, bk->h, mx << !ss_hor, my << !ss_ver, bpc);
-    free(emu);
+    
 }
 
 void oracle_mc_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layout, int bpc,
@@ -438,7 +438,7 @@ void oracle_mc_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layo
     const McBlock *bl = blocks;
     const int pb = bpc == 8 ? 1 : 2;
     const int chr_ss_hor = layout == 1 || layout == 2, chr_ss_ver = layout == 1;
-    int16_t *t0 = malloc(sizeof(int16_t) * 128 * 128), *t1 = malloc(sizeof(int16_t) * 128 * 128);
+    static _Thread_local int16_t t0_s[128 * 128], t1_s[128 * 128]; int16_t *t0 = t0_s, *t1 = t1_s;
     for (int k = 0; k < n; k++) {
         const McBlock *bk = &bl[k];
         const int p = bk->plane;
@@ -461,11 +461,11 @@ void oracle_mc_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layo
             McBlock lb = *bk;
             const int v_mul = 4 >> ss_ver;
             if (bk->comp == 4) lb.h = (uint8_t)((((bk->param / v_mul) * 3 + 3) >> 2) * v_mul);
-            uint8_t *lap = malloc((size_t)128 * 128 * pb);
+            static _Thread_local uint16_t lap_a[128 * 128]; uint8_t *lap = (uint8_t *)lap_a;
             mc_block(&lb, 0, lap, lb.w * pb, NULL, rp, rs, ref_wh[r * 2], ref_wh[r * 2 + 1], ss_hor, ss_ver, bpc);
             if (bk->comp == 4) oracle_mc_blend_h(dst, ds, lap, bk->w, bk->param, bpc);
             else oracle_mc_blend_v(dst, ds, lap, bk->w, bk->h, bpc);
-            free(lap);
+            
             continue;
         }
         for (int i = 0; i < nref; i++) {
@@ -487,8 +487,8 @@ void oracle_mc_frame(void *const cur[3], const ptrdiff_t cur_stride[2], int layo
         }
         }
     }
-    free(t0);
-    free(t1);
+    
+    
 }
 
 /* ---- scaled references, warp, combine, super-resolution (frame drivers) ---- */
@@ -526,7 +526,7 @@ void oracle_mc_scaled_frame(void *const cur[3], const ptrdiff_t cur_stride[2], i
         const void *ref;
         uint8_t *emu = NULL;
         if (left < 3 || top < 3 || right + 4 > w || bottom + 4 > h) {
-            emu = malloc((size_t)320 * 320 * pb);
+            { static _Thread_local uint16_t emu_b[320 * 320]; emu = (uint8_t *)emu_b; }
             oracle_mc_emu_edge(right - left + 7, bottom - top + 7, w, h, left - 3, top - 3, emu, 320 * pb, rp, rs, bpc);
             ref = emu + (320 * 3 + 3) * pb;
             rs = 320 * pb;
@@ -537,17 +537,17 @@ void oracle_mc_scaled_frame(void *const cur[3], const ptrdiff_t cur_stride[2], i
         uint8_t *dst = (uint8_t *)cur[p] + bk->y * ds + bk->x * pb;
         const int prep = bk->comp == 6;
         if (bk->comp == 4 || bk->comp == 5) {
-            uint8_t *lap = malloc((size_t)128 * 128 * pb);
+            static _Thread_local uint16_t lap_b[128 * 128]; uint8_t *lap = (uint8_t *)lap_b;
             oracle_mc_scaled(bk->filter2d, 0, lap, bk->w * pb, NULL, ref, rs, bk->w, bh_, pos_x & 0x3ff, pos_y & 0x3ff,
                              stx, sty, bpc);
             if (bk->comp == 4) oracle_mc_blend_h(dst, ds, lap, bk->w, bk->param, bpc);
             else oracle_mc_blend_v(dst, ds, lap, bk->w, bk->h, bpc);
-            free(lap);
+            
         } else {
             oracle_mc_scaled(bk->filter2d, prep, dst, ds, prep ? tmp_arena + bk->mask_off : NULL, ref, rs, bk->w, bk->h,
                              pos_x & 0x3ff, pos_y & 0x3ff, stx, sty, bpc);
         }
-        free(emu);
+        
     }
 }
 
