@@ -451,6 +451,38 @@ __device__ __forceinline__ void filter_plane(const int16_t *T, int lane, const i
     }
 }
 
+// 4:2:0 chroma of one unit (32x32 per plane, 64 4x4 blocks): lanes 0..255 U, 256..511 V. A
+// 32-lane group takes four horizontally adjacent blocks at a time (lane: block l / 8, row
+// (l % 8) / 2, pair column l % 2), so a tap read of the group touches four directions instead of
+// the eight of a row-major mapping (half the bank conflicts), and the direction's tap deltas
+// are three broadcast-per-block LDS reads (table built once per unit) instead of a per-lane
+// decode of the direction nibbles.
+template <typename Px, int TS>
+__device__ __forceinline__ void filter_chroma420(const int16_t *T, const int4 (*taps)[3], const int8_t *bdir,
+                                                 const int8_t *bflag, int pri, int sec, int damping, int bdm8,
+                                                 const uint8_t *src, uint8_t *dst, int64_t stride, int gx0, int gy0) {
+    const int ln = threadIdx.x & 255, gq = ln >> 5, l = ln & 31;
+    const int j = l >> 3, rr = (l & 7) >> 1, e = l & 1;
+#pragma unroll
+    for (int it = 0; it < 2; it++) {
+        const int b = it * 32 + gq * 4 + j, by = b >> 3, bx = b & 7;
+        const int r = by * 4 + rr, x = bx * 4 + 2 * e;
+        Px *dp = reinterpret_cast<Px *>(dst + (int64_t)(gy0 + r) * stride) + gx0 + x;
+        if (bflag[b] & 2) {
+            const int dir = pri ? bdir[b] : 0;
+            PairTaps t;
+            const int4 q0 = taps[dir][0], q1 = taps[dir][1], q2 = taps[dir][2];
+            t.pri[0] = q0.x; t.pri[1] = q0.y; t.pri[2] = q0.z; t.pri[3] = q0.w;
+            t.sec[0] = q1.x; t.sec[1] = q1.y; t.sec[2] = q1.z; t.sec[3] = q1.w;
+            t.sec[4] = q2.x; t.sec[5] = q2.y; t.sec[6] = q2.z; t.sec[7] = q2.w;
+            const char *P = reinterpret_cast<const char *>(T + (r + 2) * TS + x + 8);
+            store_pair<Px>(dp, cdef_pair(P, t, pri, sec, damping, bdm8));
+        } else {
+            copy_pair<Px>(dp, reinterpret_cast<const Px *>(src + (int64_t)(gy0 + r) * stride) + gx0 + x);
+        }
+    }
+}
+
 // Luma of one 64x64 unit, one 8x8 block per 32-lane group at a time: lane l of group g takes
 // row g*8 + l/4 and pair column l%4 of the blocks (g, 0..7) in turn. Every lane of a group then
 // shares the block's direction, so a tap read touches 8 rows x 4 consecutive dwords: with the
@@ -504,10 +536,10 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
     __shared__ __align__(16) int16_t tuv[2][NT * CN];          // per chroma plane: T, T1
     __shared__ int8_t bdir[64];
     __shared__ int8_t bflag[64];          // bit0 luma filtered, bit1 chroma filtered
-    __shared__ int16_t bpri[64];
     __shared__ unsigned dcost[8][64];     // find_dir costs per direction and block
     __shared__ int bstate[64];            // luma: filtered | dir << 8 | adjusted pri << 16
     __shared__ int4 ytaps[8][3];          // luma tap byte deltas per direction (PairTaps order)
+    __shared__ int4 ctaps[8][3];          // 4:2:0 chroma tap byte deltas per direction
 
     const int bid = xcd_block(blockIdx.x, gridDim.x);
     const int tx = bid % a.tiles_x, tyy = bid / a.tiles_x;
@@ -548,6 +580,12 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
         ytaps[threadIdx.x][0] = make_int4(t.pri[0], t.pri[1], t.pri[2], t.pri[3]);
         ytaps[threadIdx.x][1] = make_int4(t.sec[0], t.sec[1], t.sec[2], t.sec[3]);
         ytaps[threadIdx.x][2] = make_int4(t.sec[4], t.sec[5], t.sec[6], t.sec[7]);
+    } else if (L == 1 && threadIdx.x < 16) {
+        PairTaps t;
+        make_taps<CTS, MI_CDEF_T1 ? CN * 2 : 2>(t, threadIdx.x - 8);
+        ctaps[threadIdx.x - 8][0] = make_int4(t.pri[0], t.pri[1], t.pri[2], t.pri[3]);
+        ctaps[threadIdx.x - 8][1] = make_int4(t.sec[0], t.sec[1], t.sec[2], t.sec[3]);
+        ctaps[threadIdx.x - 8][2] = make_int4(t.sec[4], t.sec[5], t.sec[6], t.sec[7]);
     }
     {
         VecTileLoad<Px, 68, 68, NTH> ly;
@@ -615,7 +653,6 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
         if (MI_CDEF_DIAG == 1 || MI_CDEF_DIAG == 2) flag = 0;
         bdir[b] = (int8_t)dir;
         bflag[b] = (int8_t)flag;
-        bpri[b] = (int16_t)pri;
         bstate[b] = (flag & 1) | (y_pri ? dir : 0) << 8 | (y_pri ? pri : 0) << 16;
     }
     __syncthreads();
@@ -628,9 +665,13 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
         // chroma: lanes 0..255 U, 256..511 V (damping - 1, cdef_apply.rs)
         const int p = 1 + (threadIdx.x >> 8);
         // (the chroma tile is only staged when uv_lvl != 0: unfiltered chroma copies from D)
-        filter_plane<Px, CW, CH, UVW, UVH, 256, CTS, MI_CDEF_T1 ? CN * 2 : 2, 2, false>(
-            tuv[p - 1], threadIdx.x & 255, bdir, bflag, bpri, false, uv_pri, uv_sec, a.damping - 1, bdm8,
-            L == 2, a.src[p], a.dst[p], a.stride[p], x0 >> SSH, y0 >> SSV, fwc, fhc);
+        if constexpr (L == 1)
+            filter_chroma420<Px, CTS>(tuv[p - 1], ctaps, bdir, bflag, uv_pri, uv_sec, a.damping - 1, bdm8,
+                                      a.src[p], a.dst[p], a.stride[p], x0 >> SSH, y0 >> SSV);
+        else
+            filter_plane<Px, CW, CH, UVW, UVH, 256, CTS, MI_CDEF_T1 ? CN * 2 : 2, 2, false>(
+                tuv[p - 1], threadIdx.x & 255, bdir, bflag, nullptr, false, uv_pri, uv_sec, a.damping - 1, bdm8,
+                L == 2, a.src[p], a.dst[p], a.stride[p], x0 >> SSH, y0 >> SSV, fwc, fhc);
     }
 }
 
