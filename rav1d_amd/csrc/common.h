@@ -136,9 +136,10 @@ struct LfArgs {
 #define MI_LF_TW 64   // 64x64 measured fastest at 4K10: 29.6 us vs 34.9 (128x64), 32.5 (32x64)
 #endif
 #ifndef MI_LF_TH
-#define MI_LF_TH 64
+#define MI_LF_TH 128   // 64x128 tiles, 512 lanes: 29.0-29.2 us at 4K10 against 31.5-32.3 for 64x64 (256 lanes)
 #endif
 constexpr int kLfTW = MI_LF_TW, kLfTH = MI_LF_TH;
+constexpr int kLfThreads = kLfTH * 4;   // lf_tile_kernel workgroup: 256 lanes per 64 tile rows
 struct LfTileArgs {
     const uint8_t *src[3];
     uint8_t *dst[3];

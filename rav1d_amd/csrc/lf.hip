@@ -365,7 +365,7 @@ __device__ __forceinline__ bool filter_regs(int (&v)[16], int E, int I, int H, i
 template <int WD, typename Px, int P>
 __device__ __forceinline__ void lf_cols_class(Px *t, const uint16_t *list, int n, const uint8_t *le,
                                               const uint8_t *li, int bdm8, int bdmax) {
-    for (int i = threadIdx.x; i < n * 4; i += 256) {
+    for (int i = threadIdx.x; i < n * 4; i += kLfThreads) {
         const int e = list[i >> 2];
         const int u = e >> 6, L = e & 63;
         const int r = (u / kLfEdgesV) * 4 + (i & 3), k = u % kLfEdgesV;
@@ -417,7 +417,7 @@ __device__ __forceinline__ void lf_rows_class(Px *t, const uint16_t *list, int n
                                               const uint8_t *li, int bdm8, int bdmax) {
     constexpr int nr = WD == 16 ? 7 : WD == 8 ? 4 : WD == 6 ? 3 : 2;   // rows read each side
     constexpr int lo = WD == 16 ? 2 : WD == 8 ? 5 : 6;                 // rows [lo, 16 - lo) written
-    for (int i = threadIdx.x; i < n * 4; i += 256) {
+    for (int i = threadIdx.x; i < n * 4; i += kLfThreads) {
         const int e = list[i >> 2];
         const int u = e >> 6, L = e & 63;
         const int k = u / (kLfTW / 4), col = (u % (kLfTW / 4)) * 4 + (i & 3);
@@ -665,7 +665,7 @@ __device__ __forceinline__ void lf_dir_pk(Px *t, const uint16_t (*lists)[COLS ? 
     // chunk prefix over the classes (wave-uniform: the counts are LDS broadcasts)
     const int c0 = (cnt[0] * 2 + 63) >> 6, c1 = c0 + ((cnt[1] * 2 + 63) >> 6);
     const int c2 = c1 + ((cnt[2] * 2 + 63) >> 6), c3 = c2 + ((cnt[3] * 2 + 63) >> 6);
-    for (int g = wave; g < c3; g += 4) {
+    for (int g = wave; g < c3; g += kLfThreads / 64) {
         const int cls = g < c0 ? 0 : g < c1 ? 1 : g < c2 ? 2 : 3;
         const int base = cls == 0 ? 0 : cls == 1 ? c0 : cls == 2 ? c1 : c2;
         const int i = (g - base) * 64 + lane;
@@ -686,7 +686,7 @@ __device__ __forceinline__ void lf_dir_pk(Px *t, const uint16_t (*lists)[COLS ? 
 __device__ __forceinline__ int lf_class(int wd) { return wd == 4 ? 0 : wd == 6 ? 1 : wd == 8 ? 2 : 3; }
 
 template <typename Px>
-__global__ __launch_bounds__(256) void lf_tile_kernel(LfTileArgs a) {
+__global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
     constexpr int VB = 16;                        // bytes per vector
     constexpr int VPX = VB / sizeof(Px);          // pixels per vector
     constexpr int P = kLfCols;                    // LDS pitch in pixels
@@ -713,12 +713,13 @@ __global__ __launch_bounds__(256) void lf_tile_kernel(LfTileArgs a) {
     // no edge reaches them), and fetch every edge unit's mask and level words. All of these
     // loads are independent and issued before any is used.
     constexpr int VPR = P / VPX;                  // vectors per staged row
-    constexpr int NS = (kLfRows * VPR + 255) / 256;
-    constexpr int NU = (NV + NH + 255) / 256;
+    constexpr int NS = (kLfRows * VPR + kLfThreads - 1) / kLfThreads;
+    constexpr int NU = (NV + NH + kLfThreads - 1) / kLfThreads;
+    static_assert((NV > NH ? NV : NH) << 6 <= 65536, "work-list entries (unit << 6 | level) must fit 16 bits");
     uint4 sv[NS];
 #pragma unroll
     for (int j = 0; j < NS; j++) {
-        const int i = tid + 256 * j;
+        const int i = tid + kLfThreads * j;
         const int r = i / VPR, c = (i % VPR) * VPX;
         const int y = y0 - 12 + r, x = x0 - 16 + c;
         sv[j] = make_uint4(0, 0, 0, 0);
@@ -731,7 +732,7 @@ __global__ __launch_bounds__(256) void lf_tile_kernel(LfTileArgs a) {
     LfEdgeRaw raw[NU];
 #pragma unroll
     for (int j = 0; j < NU; j++) {
-        const int i = tid + 256 * j;
+        const int i = tid + kLfThreads * j;
         const bool v = i < NV;
         const int u = v ? i : i - NV;
         raw[j].bit = 0;
@@ -745,12 +746,12 @@ __global__ __launch_bounds__(256) void lf_tile_kernel(LfTileArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < NS; j++) {
-        const int i = tid + 256 * j;
+        const int i = tid + kLfThreads * j;
         if (i < kLfRows * VPR) *reinterpret_cast<uint4 *>(&t[(i / VPR) * P + (i % VPR) * VPX]) = sv[j];
     }
 #pragma unroll
     for (int j = 0; j < NU; j++) {
-        const int i = tid + 256 * j;
+        const int i = tid + kLfThreads * j;
         const bool v = i < NV;
         const int u = v ? i : i - NV;
         const int k = v ? u % kLfEdgesV : u / (kLfTW / 4);
@@ -782,7 +783,7 @@ __global__ __launch_bounds__(256) void lf_tile_kernel(LfTileArgs a) {
     __syncthreads();
     uint8_t *dst = a.dst[p];
     constexpr int VPT = kLfTW / VPX;
-    for (int i = tid; i < kLfTH * VPT; i += 256) {
+    for (int i = tid; i < kLfTH * VPT; i += kLfThreads) {
         const int r = i / VPT, c = (i % VPT) * VPX;
         const int y = y0 + r, x = x0 + c;
         if (y < ph && x < pw)
@@ -794,8 +795,8 @@ __global__ __launch_bounds__(256) void lf_tile_kernel(LfTileArgs a) {
 int launch_deblock_tiles(const LfTileArgs &a, int bpc, hipStream_t s) {
     const int n = a.tile_start[3];
     if (!n) return 0;
-    if (bpc == 8) hipLaunchKernelGGL(lf_tile_kernel<uint8_t>, dim3(n), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(lf_tile_kernel<uint16_t>, dim3(n), dim3(256), 0, s, a);
+    if (bpc == 8) hipLaunchKernelGGL(lf_tile_kernel<uint8_t>, dim3(n), dim3(kLfThreads), 0, s, a);
+    else hipLaunchKernelGGL(lf_tile_kernel<uint16_t>, dim3(n), dim3(kLfThreads), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
