@@ -665,7 +665,10 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
         // chroma: lanes 0..255 U, 256..511 V (damping - 1, cdef_apply.rs)
         const int p = 1 + (threadIdx.x >> 8);
         // (the chroma tile is only staged when uv_lvl != 0: unfiltered chroma copies from D)
-        if constexpr (L == 1)
+#ifndef MI_CDEF_C420
+#define MI_CDEF_C420 1
+#endif
+        if constexpr (L == 1 && MI_CDEF_C420)
             filter_chroma420<Px, CTS>(tuv[p - 1], ctaps, bdir, bflag, uv_pri, uv_sec, a.damping - 1, bdm8,
                                       a.src[p], a.dst[p], a.stride[p], x0 >> SSH, y0 >> SSV);
         else

@@ -740,8 +740,15 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
                                                        (int)lap_s[k].size(), tmp, stream)))
                 return r;
         }
+#ifndef MI_FX_ITX_BANDED
+#define MI_FX_ITX_BANDED 1
+#endif
+        uint32_t itx_ss[MI_N_RECT_TX_SIZES + 1];
+        for (int t = 0; t < MI_N_RECT_TX_SIZES; t++) itx_ss[t] = itx_bs[t][0];
+        itx_ss[MI_N_RECT_TX_SIZES] = itx_bs[MI_N_RECT_TX_SIZES - 1][MI_ITX_BANDS];
         if (f->n_inter_tx &&
-            (r = mi_itx_frame_banded(ctx, &cur, (const MiTxBlock *)D(20), itx_bs, D(4), 0, stream)))
+            (r = MI_FX_ITX_BANDED ? mi_itx_frame_banded(ctx, &cur, (const MiTxBlock *)D(20), itx_bs, D(4), 0, stream)
+                                  : mi_itx_frame(ctx, &cur, (const MiTxBlock *)D(20), itx_ss, D(4), 0, stream)))
             return r;
     }
 
