@@ -833,6 +833,7 @@ __device__ __forceinline__ int itx_rows(const MiTxBlock &b, Cf *cf, bool zero, i
     constexpr bool Rect2 = (Wd == 2 * Ht) || (Ht == 2 * Wd);
     constexpr int Shift = D.shift, Rnd = (1 << Shift) >> 1;
     const int j = threadIdx.x;
+    if (b.eob < 0) return 0;  // no residual (skip / prediction only): the arena is not read
     if (b.txtp == 0 && b.eob < 1) {
         int dc = (int)cf[0];
         if (Rect2) dc = (dc * 181 + 128) >> 8;
@@ -895,13 +896,16 @@ __device__ __forceinline__ void itx_cols(const MiTxBlock &b, int bdmax, int16_t 
             if constexpr (TX == 0) {
                 iwht4(c);
 #pragma unroll
-                for (int y = 0; y < 4; y++) res[y * Wd + j] = (int16_t)c[y];
+                for (int y = 0; y < 4; y++) res[y * Wd + j] = (int16_t)clampi(c[y], -32768, 32767);
             }
         } else {
             itx1d<Wide, Ht>(col_kind_ip(b.txtp), c, col_lo, col_hi);
-            // (c clamped to col_lo..col_hi: (c + 8) >> 4 fits int16 at every bit depth)
+            // (c + 8) >> 4 does NOT always fit int16: the identity column transforms are not
+            // clipped (itx_1d.rs:1106-1121), so at 12 bpc identity32 reaches 4 * 131071 and the
+            // residual +32768. Saturating is exact: any |r| > 32767 exceeds
+            // bdmax, and the pixel clips to the same bound as with the unsaturated int
 #pragma unroll
-            for (int y = 0; y < Ht; y++) res[y * Wd + j] = (int16_t)((c[y] + 8) >> 4);
+            for (int y = 0; y < Ht; y++) res[y * Wd + j] = (int16_t)clampi((c[y] + 8) >> 4, -32768, 32767);
         }
     }
 }
@@ -1040,7 +1044,7 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
         default: break;
         }
         // the column pass too (the residual), unless the block is DC-only (a constant dc)
-        const bool dconly = tb.txtp == 0 && tb.eob < 1;
+        const bool dconly = tb.eob < 0 || (tb.txtp == 0 && tb.eob < 1);
         if (!dconly) {
             __syncthreads();
             switch (tb.tx) {

@@ -225,3 +225,45 @@ def test_intra_recon_block_copy_heavy(gpu, bpc, layout):
             if not np.array_equal(got, exp[p]):
                 bad = np.argwhere(got != exp[p])
                 raise AssertionError(f"fused={fused} plane {p}: {len(bad)} mismatches, first at {bad[0]}")
+
+
+@pytest.mark.parametrize("granules", [False, True])
+def test_intra_recon_12bit_identity32_saturates(gpu, granules):
+    """12 bpc identity transforms on 32-point columns with every coefficient at the row clip:
+    the column pass's identity32 (x4, unclipped, itx_1d.rs:1106-1121) drives (c + 8) >> 4 to
+    +32768, one past int16. The fused kernel keeps the residual in int16 LDS,
+    so it must saturate rather than wrap (a wrapped +32768 turns a pixel that clips to 4095
+    into 0: Argon 12-bit test15549_5522_4902). Negative blocks reach -32768 exactly."""
+    from rav1d_amd.intra import IntraFrame, device_status, make_intra_residuals
+    from rav1d_amd.synth import TX_DIMS
+    w, h, bpc, layout = 256, 192, 12, 3
+    rng = np.random.default_rng(0x12B1D)
+    fr = make_intra_residuals(make_intra_frame(w, h, bpc, layout, rng, sb=64, min_bs=8, tx_split=0.2), bpc, rng)
+    cf_max = (128 << bpc) - 1
+    tb, coef = fr["tx_blocks"], fr["coef"]
+    hit = set()
+    for k in range(len(tb)):
+        tw, th = TX_DIMS[int(tb[k]["tx"])]
+        if th != 32 or tw < 8:
+            continue
+        n = min(tw, 32) * 32
+        off = int(tb[k]["coef_off"])
+        sign = 1 if k % 3 else -1
+        coef[off:off + n] = sign * cf_max
+        tb[k]["txtp"] = 9          # IDTX
+        tb[k]["eob"] = n - 1
+        hit.add((tw, th))
+    assert {(32, 32), (8, 32), (16, 32)} <= hit, f"sizes covered: {sorted(hit)}"
+    cur = Frame(w, h, bpc, layout)
+    for p in range(len(cur.planes)):
+        cur.set_buffer_np(p, rng.integers(0, 1 << bpc, size=cur.buffer_np(p).shape))
+    init = [cur.buffer_np(p) for p in range(len(cur.planes))]
+    IntraFrame(gpu, fr).recon(cur.picture(), granules=granules)
+    device_status(gpu)
+    exp = _oracle_recon(init, fr, bpc)
+    for p in range(len(cur.planes)):
+        got = cur.buffer_np(p)
+        if not np.array_equal(got, exp[p]):
+            bad = np.argwhere(got != exp[p])
+            raise AssertionError(f"plane {p}: {len(bad)} mismatches, first at {bad[0]}: got {got[tuple(bad[0])]} "
+                                 f"exp {exp[p][tuple(bad[0])]}")

@@ -17,7 +17,9 @@ import pytest
 from tests.stream_lib import decode_stream
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "streams")
-VECTORS = json.load(open(os.path.join(GOLDEN, "vectors.json")))
+# the CPU suite decodes the "cpu" subset (every tool, layout and bit depth; a few minutes);
+# test_streams_gpu.py runs all of them on the device
+VECTORS = [v for v in json.load(open(os.path.join(GOLDEN, "vectors.json"))) if v.get("cpu")]
 
 
 def load(v):

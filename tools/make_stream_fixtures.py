@@ -55,6 +55,9 @@ PINNED = [
     ("issue_318", "10-bit/issues/318_tx_4x4.ivf"),                    # 1920x1080 10-bit, 35 frames
     ("00001141", "8-bit/data/00001141.ivf"),                          # 3840x2160 8-bit, 3 frames
     ("issue_295", "8-bit/issues/295_adst_precision.ivf"),             # 2780x2136 8-bit, 25 frames
+    # 12-bit identity32 residuals at the column clip (the fused intra kernel's int16 residual
+    # wrapped there in round 3)
+    ("test15549_5522_4902", "12-bit/argon/test15549_5522_4902.obu"),
 ]
 
 # the reference's --filmgrain 1 tests (explicit test() entries in the meson files: film grain
@@ -68,6 +71,28 @@ GRAIN = [
     ("test5606", "10-bit/argon/test5606.obu", "0888c66e9ad2f6ebc7f6d6fd8b464dd8"),
 ]
 
+
+
+def driver_suite(by_path):
+    """The rest of the driver-run GPU suite (round 4): every 10-bit, 12-bit and multi-bit vector
+    of the meson lists, and a representative 8-bit subset (all size / quantizer / features /
+    issues / cdfupdate / mfmv / mv / resize vectors, every 6th 8-bit/data vector under 100 KB,
+    the two smallest vq_suite streams). Returns [(name, rel, md5)], names unique."""
+    base = "/root/reference/tests/dav1d-test-data"
+    out = []
+    data8 = sorted(r for r in by_path if r.startswith("8-bit/data/") and os.path.getsize(os.path.join(base, r)) < 100_000)
+    vq = sorted((r for r in by_path if r.startswith("8-bit/vq_suite/")), key=lambda r: os.path.getsize(os.path.join(base, r)))
+    for rel in sorted(by_path):
+        top, sub = rel.split("/")[:2]
+        keep = top in ("10-bit", "12-bit", "multi-bit")
+        keep |= top == "8-bit" and sub in ("size", "quantizer", "features", "issues", "cdfupdate", "mfmv", "mv", "resize",
+                                           "intra")
+        keep |= rel in data8[::6] or rel in vq[:2]
+        if keep:
+            out.append((by_path[rel][0], rel, by_path[rel][1]))
+    return out
+
+
 if __name__ == "__main__":
     out = os.path.join(ROOT, "tests", "golden", "streams")
     os.makedirs(out, exist_ok=True)
@@ -79,11 +104,23 @@ if __name__ == "__main__":
         name = alias[0] if alias else name
         dst = rel.replace("/", "__")
         shutil.copyfile(os.path.join("/root/reference/tests/dav1d-test-data", rel), os.path.join(out, dst))
+        table.append({"name": name, "file": dst, "md5": md5, "cpu": 1, "source": f"tests/dav1d-test-data/{rel}"})
+    have = {t["source"] for t in table}
+    names = {t["name"] for t in table}
+    for name, rel, md5 in driver_suite(by_path):
+        if f"tests/dav1d-test-data/{rel}" in have:
+            continue
+        if name in names:
+            name = f"{name}_{rel.split('/')[0].replace('-', '')}"
+        assert name not in names, name
+        names.add(name)
+        dst = rel.replace("/", "__")
+        shutil.copyfile(os.path.join("/root/reference/tests/dav1d-test-data", rel), os.path.join(out, dst))
         table.append({"name": name, "file": dst, "md5": md5, "source": f"tests/dav1d-test-data/{rel}"})
     for name, rel, md5 in GRAIN:
         dst = rel.replace("/", "__")
         shutil.copyfile(os.path.join("/root/reference/tests/dav1d-test-data", rel), os.path.join(out, dst))
-        table.append({"name": name, "file": dst, "md5": md5, "filmgrain": 1,
+        table.append({"name": name, "file": dst, "md5": md5, "filmgrain": 1, "cpu": 1,
                       "source": f"tests/dav1d-test-data/{rel} --filmgrain 1"})
     json.dump(table, open(os.path.join(out, "vectors.json"), "w"), indent=1)
     print(len(table), "vectors")
