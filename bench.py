@@ -30,6 +30,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from rav1d_amd import ITX_KEEP_COEFS  # noqa: E402
 from rav1d_amd import frame as F  # noqa: E402
 from rav1d_amd.synth import frame_bytes, itx_algorithmic_bytes, itx_band_order, make_frame, mc_algorithmic_bytes  # noqa: E402
 
@@ -39,8 +40,9 @@ W, H, BPC, LAYOUT = 3840, 2160, 10, 1
 
 class Pipeline:
     """Device buffers + descriptors for one stream's frames. `ring` pre-filled copies of the
-    coefficient arena: itx zeroes the arena it consumes (itxfm_add's contract), so every step
-    takes the next fresh arena and the timed frames are the frame the oracle verifies."""
+    coefficient arena: every step reads the next arena, as a decoder uploads a new one per
+    frame (the device arena is a staged copy that itx reads once and leaves as it is, so the
+    ring is not there for zeroing but so that no step finds its coefficients in a cache)."""
 
     def __init__(self, ctx, fr, ring=1):
         self.ctx, self.fr = ctx, fr
@@ -85,7 +87,9 @@ class Pipeline:
         lvl_bytes = ((w + 3) >> 2) * ((h + 3) >> 2) * 4
         mask_bytes = fr["lf"]["masks"].nbytes
         self.algo = {
-            "itx": itx_algorithmic_bytes(fr["blocks"], bpc, zero_coefs=True),
+            # coefficients counted once: the device arena is the frame's staged
+            # copy, read once and not zeroed (MI_ITX_KEEP_COEFS, as the frame executor runs it)
+            "itx": itx_algorithmic_bytes(fr["blocks"], bpc, zero_coefs=False),
             "deblock": 2 * fb + lvl_bytes + mask_bytes,
             "cdef": 2 * fb + mask_bytes,
             "lr": 2 * fb + fb * 4 // 64 + fr["lr"]["lr_mask"].nbytes,
@@ -138,10 +142,10 @@ class Pipeline:
         self.k += 1
         if self.itx_bands is not None:
             timed("itx", lambda: F.check(lib.mi_itx_frame_banded(ctx, ctypes.byref(pa), ctypes.c_void_p(self.blocks.data_ptr()),
-                                                                 self.itx_bands, ctypes.c_void_p(coef.data_ptr()), 0, sp), "itx"))
+                                                                 self.itx_bands, ctypes.c_void_p(coef.data_ptr()), ITX_KEEP_COEFS, sp), "itx"))
         else:
             timed("itx", lambda: F.check(lib.mi_itx_frame(ctx, ctypes.byref(pa), ctypes.c_void_p(self.blocks.data_ptr()),
-                                                          ss, ctypes.c_void_p(coef.data_ptr()), 0, sp), "itx"))
+                                                          ss, ctypes.c_void_p(coef.data_ptr()), ITX_KEEP_COEFS, sp), "itx"))
         timed("deblock", lambda: F.check(lib.mi_deblock_frame_to(ctx, ctypes.byref(pa), ctypes.byref(pd),
                                                                  ctypes.byref(self.lf.s), sp), "lf"))
         timed("cdef", lambda: F.check(lib.mi_cdef_frame(ctx, ctypes.byref(pd), ctypes.byref(pb),

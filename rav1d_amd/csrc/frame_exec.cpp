@@ -702,6 +702,10 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
     uint8_t *dev = ctx->fx_dev;
     auto D = [&](int i) -> void * { return secs[i].bytes ? dev + secs[i].off : nullptr; };
 
+    // The coefficient arena D(4) is this frame's staged copy of the front-end's arena (which
+    // the front-end zeroes on the host, as itxfm_add's contract asks of the caller's buffer):
+    // no block reads it twice, so the device kernels leave it as it is (MI_ITX_KEEP_COEFS)
+    // instead of spending a write pass on zeroing a copy nobody reads again.
     // 0. inter prediction (recon_b_inter's mc / warp_affine / compound / obmc calls over the
     // whole frame: they read reference pictures only), then the inter residuals
     if (inter) {
@@ -747,8 +751,9 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         for (int t = 0; t < MI_N_RECT_TX_SIZES; t++) itx_ss[t] = itx_bs[t][0];
         itx_ss[MI_N_RECT_TX_SIZES] = itx_bs[MI_N_RECT_TX_SIZES - 1][MI_ITX_BANDS];
         if (f->n_inter_tx &&
-            (r = MI_FX_ITX_BANDED ? mi_itx_frame_banded(ctx, &cur, (const MiTxBlock *)D(20), itx_bs, D(4), 0, stream)
-                                  : mi_itx_frame(ctx, &cur, (const MiTxBlock *)D(20), itx_ss, D(4), 0, stream)))
+            (r = MI_FX_ITX_BANDED
+                     ? mi_itx_frame_banded(ctx, &cur, (const MiTxBlock *)D(20), itx_bs, D(4), MI_ITX_KEEP_COEFS, stream)
+                     : mi_itx_frame(ctx, &cur, (const MiTxBlock *)D(20), itx_ss, D(4), MI_ITX_KEEP_COEFS, stream)))
             return r;
     }
 
@@ -768,7 +773,7 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         fr.pal = D(6);
         fr.n = n;
         if ((r = mi_internal::intra_recon(ctx, &fr, 1, strip_start.empty() ? nullptr : strip_start.data(),
-                                          (int)strip_start.size() - 1, 0, stream, granules)))
+                                          (int)strip_start.size() - 1, MI_ITX_KEEP_COEFS, stream, granules)))
             return r;
         if (tl_path && n > 1000) {
             std::vector<unsigned long long> t((size_t)n * 16);

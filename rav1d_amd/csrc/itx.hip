@@ -306,7 +306,10 @@ __global__ __launch_bounds__(kItxThreads, MI_ITX_MINW) void itx_frame_kernel(Itx
     switch (s) {
 #define CASE(n) case n: itx_size<n, Px, Cf, Lt, Wide>(a, lwg, lds); break;
         CASE(0) CASE(1) CASE(2) CASE(5) CASE(6) CASE(7) CASE(8) CASE(13) CASE(14)
-        CASE(3) CASE(4) CASE(9) CASE(10) CASE(11) CASE(12) CASE(15) CASE(16) CASE(17) CASE(18)
+        CASE(3) CASE(9) CASE(10) CASE(15) CASE(16)
+#ifndef MI_ITX_EXP_NO64   // experiment builds only: the 64-point sizes compiled out
+        CASE(4) CASE(11) CASE(12) CASE(17) CASE(18)
+#endif
 #undef CASE
     default: break;
     }

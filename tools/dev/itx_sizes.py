@@ -1,37 +1,45 @@
-"""Per-size itx time on the bench's 4K10 frame: mi_itx_frame with only one size's range
-non-empty (diagnostic, not a test)."""
+"""Per-size itx time on the bench's 4K10 frame through mi_itx_frame_banded (the bench's call),
+coefficients kept (MI_ITX_KEEP_COEFS), with only one size's range non-empty (diagnostic)."""
 import os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import torch
 from rav1d_amd import frame as F
-from rav1d_amd.synth import make_frame, TX_DIMS
+from rav1d_amd.synth import make_frame, TX_DIMS, itx_band_order, itx_algorithmic_bytes
 fr = make_frame(3840, 2160, 10, 1, seed=0x4C100001, with_fg=False, with_mc=True)
 ctx = F.Context(0)
 A = F.Frame(3840, 2160, 10, 1)
-blocks = torch.from_numpy(fr["blocks"].view(np.uint8).copy()).cuda()
+for p, a in enumerate(fr["planes"]):
+    A.set_plane_np(p, a)
+ah = 2176
+blk, _, bs = itx_band_order(fr["blocks"], [ah, ah >> 1, ah >> 1])
+blocks = torch.from_numpy(blk.view(np.uint8).copy()).cuda()
 coef = torch.from_numpy(fr["coef"].copy()).cuda()
-ss = np.asarray(fr["size_start"], np.int64)
-b = fr["blocks"]
-def t(ssx, reps=50):
+bs = np.asarray(bs, np.int64).reshape(19, 9)
+def t(bsx, reps=50):
     for _ in range(3):
-        F.itx_frame(ctx, A, blocks, ssx, coef, 0)
+        F.itx_frame(ctx, A, blocks, None, coef, 1, band_start=bsx)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        F.itx_frame(ctx, A, blocks, ssx, coef, 0)
+        F.itx_frame(ctx, A, blocks, None, coef, 1, band_start=bsx)
     e1.record(); torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps * 1e3
-print("all", round(t(ss), 1), "us", len(b), "blocks")
+tot = t(bs)
+ab = itx_algorithmic_bytes(blk, 10, zero_coefs=False)
+print(f"all {tot:.1f} us, {len(blk)} blocks, {ab/1e6:.1f} MB, {ab/tot/1e3:.0f} GB/s")
 for s in range(19):
-    n = int(ss[s + 1] - ss[s])
-    if not n:
+    lo, hi = int(bs[s, 0]), int(bs[s, 8])
+    if hi == lo:
         continue
-    one = ss.copy()
-    one[:s + 1] = ss[s]
-    one[s + 1:] = ss[s + 1]
-    sub = b[ss[s]:ss[s + 1]]
+    one = bs.copy()
+    for k in range(19):
+        one[k, :] = lo if k <= s else hi
+    one[s] = bs[s]
+    sub = blk[lo:hi]
     dc = int(((sub["txtp"] == 0) & (sub["eob"] < 1)).sum())
-    print(f"tx {s:2d} {TX_DIMS[s][0]:2d}x{TX_DIMS[s][1]:<2d} n={n:6d} dconly={dc:6d} {t(one):7.1f} us")
+    us = t(one)
+    b = itx_algorithmic_bytes(sub, 10, zero_coefs=False)
+    print(f"tx {s:2d} {TX_DIMS[s][0]:2d}x{TX_DIMS[s][1]:<2d} n={hi-lo:6d} dconly={dc:6d} {us:7.1f} us {b/1e6:6.2f} MB {b/us/1e3:6.0f} GB/s")
