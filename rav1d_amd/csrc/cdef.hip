@@ -12,6 +12,8 @@
 // pixels straight out of LDS and streams C back with coalesced stores.
 #include "common.h"
 
+MI_KTL_DEFINE(cdef)
+
 namespace mi {
 
 
@@ -540,6 +542,7 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
     __shared__ int bstate[64];            // luma: filtered | dir << 8 | adjusted pri << 16
     __shared__ int4 ytaps[8][3];          // luma tap byte deltas per direction (PairTaps order)
     __shared__ int4 ctaps[8][3];          // 4:2:0 chroma tap byte deltas per direction
+    KTL(0);
 
     const int bid = xcd_block(blockIdx.x, gridDim.x);
     const int tx = bid % a.tiles_x, tyy = bid / a.tiles_x;
@@ -676,6 +679,7 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
                 tuv[p - 1], threadIdx.x & 255, bdir, bflag, nullptr, false, uv_pri, uv_sec, a.damping - 1, bdm8,
                 L == 2, a.src[p], a.dst[p], a.stride[p], x0 >> SSH, y0 >> SSV, fwc, fhc);
     }
+    KTL(5);
 }
 
 // ---- per-call cdef.fb[] / cdef.dir (cdef.rs:567-1031) ----

@@ -5,6 +5,38 @@
 #include <stdint.h>
 #include "../../include/mi_av1dsp.h"
 
+// Kernel timelines (diagnostic builds only, -DMI_KTL): lane 0 of every workgroup stores
+// s_memrealtime stamps (100 MHz) at phase boundaries into ktl_buf[blockIdx.x * 8 + k], slot 7 =
+// the XCC id. Each translation unit has its own buffer pointer, set from the host through
+// mi_ktl_set_<unit> (no relocatable device code).
+#ifdef MI_KTL
+#define MI_KTL_DEFINE(unit)                                                                        \
+    __device__ unsigned long long *ktl_buf;                                                        \
+    extern "C" int mi_ktl_set_##unit(void *p) {                                                    \
+        return hipMemcpyToSymbol(HIP_SYMBOL(ktl_buf), &p, sizeof(p)) == hipSuccess ? 0 : -5;     \
+    }
+#define KTL(k)                                                                                     \
+    do {                                                                                           \
+        if (ktl_buf && threadIdx.x == 0) {                                                         \
+            ktl_buf[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();              \
+            if ((k) == 0) {                                                                        \
+                unsigned x_;                                                                       \
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x_));                  \
+                ktl_buf[(size_t)blockIdx.x * 8 + 7] = x_ & 0xf;                                    \
+            }                                                                                      \
+        }                                                                                          \
+    } while (0)
+// slot k <- an arbitrary value (e.g. the work class of the workgroup)
+#define KTLV(k, v)                                                                                 \
+    do {                                                                                           \
+        if (ktl_buf && threadIdx.x == 0) ktl_buf[(size_t)blockIdx.x * 8 + (k)] = (unsigned long long)(v); \
+    } while (0)
+#else
+#define MI_KTL_DEFINE(unit)
+#define KTL(k) do {} while (0)
+#define KTLV(k, v) do {} while (0)
+#endif
+
 namespace mi {
 
 // The dispatcher hands workgroup b to XCD b % 8 (MI355X: 8 XCDs, each with its own 4 MB L2).

@@ -22,6 +22,8 @@
 #include <algorithm>
 #include <type_traits>
 
+MI_KTL_DEFINE(itx)
+
 namespace mi {
 
 // TxfmType -> 1-D kinds (levels.rs TxfmType is VERT_HORZ; itx_tmpl.c:196-233)
@@ -211,6 +213,7 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
         }
     }
     __syncthreads();
+    if (rd == 0) KTL(1);
 
     // ---- 3. column pass: residual back into LDS (rows >= SH are reused as needed) ----
     int colres[Ht];
@@ -296,6 +299,7 @@ template <typename Px, typename Cf, typename Lt, bool Wide>
 __global__ __launch_bounds__(kItxThreads, MI_ITX_MINW) void itx_frame_kernel(ItxArgs a) {
     __shared__ Lt lds[itx_lds_max(true) > itx_lds_max(false) ? itx_lds_max(true) : itx_lds_max(false)];
     const int wg = blockIdx.x;
+    KTL(0);
     // the size range holding this workgroup, with compile-time indices only (a runtime index
     // into the kernel-argument struct makes the compiler copy it to scratch)
     int s = a.wg_size[0], base = a.wg_start[0];
@@ -313,6 +317,8 @@ __global__ __launch_bounds__(kItxThreads, MI_ITX_MINW) void itx_frame_kernel(Itx
 #undef CASE
     default: break;
     }
+    KTL(5);
+    KTLV(6, s);
 }
 
 int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start, const uint32_t *band_start) {

@@ -14,6 +14,8 @@
 // Row-edge lanes: 64 consecutive pixel columns per wave (every access a coalesced row read).
 #include "common.h"
 
+MI_KTL_DEFINE(lf)
+
 namespace mi {
 
 
@@ -706,6 +708,7 @@ __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
     const int pw = a.pw[p], ph = a.ph[p];
     const int64_t st = a.stride[p];
     const uint8_t *src = a.src[p];
+    KTL(0);
     if (tid < 64) { le[tid] = a.lim_e[tid]; li[tid] = a.lim_i[tid]; }
     if (tid < 8) cnt[tid] = 0;
     __syncthreads();
@@ -749,6 +752,7 @@ __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
         const int i = tid + kLfThreads * j;
         if (i < kLfRows * VPR) *reinterpret_cast<uint4 *>(&t[(i / VPR) * P + (i % VPR) * VPX]) = sv[j];
     }
+    KTL(1);
 #pragma unroll
     for (int j = 0; j < NU; j++) {
         const int i = tid + kLfThreads * j;
@@ -764,6 +768,7 @@ __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
         (v ? listv[c] : listh[c])[slot] = (uint16_t)((u << 6) | (code & 63));
     }
     __syncthreads();
+    KTL(2);
     // column edges, then row edges, one loop per width class
 #if defined(MI_LF_UNPACKED)
     lf_cols_class<4, Px, P>(t, listv[0], cnt[0], le, li, a.bdm8, a.bdmax);
@@ -778,9 +783,11 @@ __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
 #elif !defined(MI_LF_NOFILTER)
     lf_dir_pk<true, Px, P>(t, listv, cnt, le, li, a.bdm8, a.bdmax);
     __syncthreads();
+    KTL(3);
     lf_dir_pk<false, Px, P>(t, listh, cnt + 4, le, li, a.bdm8, a.bdmax);
 #endif
     __syncthreads();
+    KTL(4);
     uint8_t *dst = a.dst[p];
     constexpr int VPT = kLfTW / VPX;
     for (int i = tid; i < kLfTH * VPT; i += kLfThreads) {
@@ -790,6 +797,7 @@ __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
             *reinterpret_cast<uint4 *>(dst + (int64_t)y * st + (int64_t)x * sizeof(Px)) =
                 *reinterpret_cast<const uint4 *>(&t[(12 + r) * P + 16 + c]);
     }
+    KTL(5);
 }
 
 int launch_deblock_tiles(const LfTileArgs &a, int bpc, hipStream_t s) {

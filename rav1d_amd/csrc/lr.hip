@@ -13,6 +13,8 @@
 // output streamed to a separate picture O.
 #include "common.h"
 
+MI_KTL_DEFINE(lr)
+
 namespace mi {
 
 constexpr int kLrWin = 80;             // LDS window row stride (int16): columns x0-8 .. x0+71
@@ -391,6 +393,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
     __shared__ __attribute__((aligned(16))) int16_t B[66 * kLrAB];
     int16_t *hor = reinterpret_cast<int16_t *>(A);    // Wiener: [70][64] aliases A
 
+    KTL(0);
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
 #ifndef MI_LR_XCD
 #define MI_LR_XCD 0   // tile -> XCD: 0 hardware round robin, 1 contiguous ranges (xcd_block), C > 1 runs of C
@@ -497,6 +500,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
         wiener_ver(hor, B, wr, sh, tw, fv, bd, rbv, bdmax);
         __syncthreads();
         store_tile<Px>(B, O, st, S, sh, x0, tw);
+        KTL(5);
         return;
     }
 
@@ -512,6 +516,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
     sgr_pairs(A, B, win, sh, tw, bdm8, s0, s1, w0, w1, xbyx, bdmax);
     __syncthreads();
     store_tile<Px>(B, O, st, S, sh, x0, tw);
+    KTL(5);
 }
 
 // ---- per-call lr.wiener / lr.sgr (looprestoration.rs:91-107, 139-912) ----

@@ -18,6 +18,8 @@
 #include "common.h"
 #include <type_traits>
 
+MI_KTL_DEFINE(mc)
+
 namespace mi {
 
 __constant__ __attribute__((aligned(8))) int8_t k_subpel[6][15][8] = {
@@ -174,6 +176,7 @@ template <typename Px>
 __global__ __launch_bounds__(64, MC_MIN_WAVES) void mc_kernel(McArgs a, int g) {
     __shared__ __attribute__((aligned(16))) int16_t win[kWinElems];
     const int lane = threadIdx.x;
+    KTL(0);
 #ifndef MI_MC_XCD_CHUNK
 #define MI_MC_XCD_CHUNK 1
 #endif

@@ -18,14 +18,8 @@ for p, a in enumerate(fr["planes"]):
 blk, _, bs = itx_band_order(b, [2176, 1088, 1088])
 blocks = torch.from_numpy(blk.view(np.uint8).copy()).cuda()
 coef = torch.from_numpy(fr["coef"].copy()).cuda()
-for _ in range(5):
-    F.itx_frame(ctx, A, blocks, None, coef, 1, band_start=bs)
-torch.cuda.synchronize()
-e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-e0.record()
-for _ in range(50):
-    F.itx_frame(ctx, A, blocks, None, coef, 1, band_start=bs)
-e1.record(); torch.cuda.synchronize()
-us = e0.elapsed_time(e1) / 50 * 1e3
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from gtime import gtime
+us = gtime(lambda s: F.itx_frame(ctx, A, blocks, None, coef, 1, band_start=bs, stream=s))
 ab = itx_algorithmic_bytes(blk, 10, zero_coefs=False)
 print(f"{os.path.basename(os.environ.get('MI_LIB', 'base'))}: {len(blk)} blocks {us:.1f} us {ab/us/1e3:.0f} GB/s")

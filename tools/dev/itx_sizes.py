@@ -17,16 +17,10 @@ blk, _, bs = itx_band_order(fr["blocks"], [ah, ah >> 1, ah >> 1])
 blocks = torch.from_numpy(blk.view(np.uint8).copy()).cuda()
 coef = torch.from_numpy(fr["coef"].copy()).cuda()
 bs = np.asarray(bs, np.int64).reshape(19, 9)
-def t(bsx, reps=50):
-    for _ in range(3):
-        F.itx_frame(ctx, A, blocks, None, coef, 1, band_start=bsx)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        F.itx_frame(ctx, A, blocks, None, coef, 1, band_start=bsx)
-    e1.record(); torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps * 1e3
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from gtime import gtime
+def t(bsx):
+    return gtime(lambda s: F.itx_frame(ctx, A, blocks, None, coef, 1, band_start=bsx, stream=s))
 tot = t(bs)
 ab = itx_algorithmic_bytes(blk, 10, zero_coefs=False)
 print(f"all {tot:.1f} us, {len(blk)} blocks, {ab/1e6:.1f} MB, {ab/tot/1e3:.0f} GB/s")
