@@ -127,6 +127,9 @@ int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, i
 /* The host-side checks mi_frame_run applies before enqueuing anything, without a device: 0, or
  * -EINVAL with *why (if non-NULL) naming the failed check. */
 int mi_frame_validate(const MiDecFrame *f, const MiFramePictures *pics, const char **why);
+/* Diagnostic: mean host time (ms) of mi_frame_run's planning pass over `f` (intra queue order,
+ * dependency lists, inter unit buckets, residual bands), reps times; no device work. */
+double mi_frame_plan_ms(const MiDecFrame *f, int reps);
 
 /* Wait for the work enqueued on `stream` and report device-side failures of the frame(s):
  * 0; -EINVAL when a kernel rejected (skipped) a descriptor no valid stream produces; -EIO

@@ -20,12 +20,37 @@
 #include <algorithm>
 #include <cstdlib>
 #include <chrono>
+#include <thread>
 #include <vector>
 
 #include "ctx.h"
 #include "../../include/mi_av1dec.h"
 
 namespace {
+
+// fn(lo, hi) over [0, n) in up to `threads` contiguous ranges on std::threads (the caller runs
+// the first range). Host planning of large frames only: below `min_n` items it runs inline.
+template <typename Fn>
+int parallel_ranges(int n, int min_n, Fn &&fn) {
+    static const int hw = [] {
+        const char *e = getenv("MI_FX_THREADS");
+        const int t = e ? atoi(e) : (int)std::thread::hardware_concurrency();
+        return std::max(1, std::min(t, 8));
+    }();
+    const int nt = n < min_n ? 1 : hw;
+    if (nt <= 1) {
+        fn(0, n, 0);
+        return 1;
+    }
+    std::vector<std::thread> th;
+    th.reserve(nt - 1);
+    for (int t = 1; t < nt; t++)
+        th.emplace_back([&, t] { fn((int)((int64_t)n * t / nt), (int)((int64_t)n * (t + 1) / nt), t); });
+    fn(0, (int)((int64_t)n / nt), 0);
+    for (std::thread &x : th) x.join();
+    return nt;
+}
+
 
 // Legal TxfmType values per RectTxfmSize (itx.rs:400-457): the 4/8/16-class rectangles and
 // 8x8 and below carry all 16 (4x4 also WHT_WHT = 16), 16x16 the first 12, the 32 class
@@ -332,19 +357,22 @@ int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<in
         ph4[p] = (p ? ah >> ssv : ah) >> 2;
         own[p].assign((size_t)pw4[p] * ph4[p], -1);
     }
-    for (int i = 0; i < n; i++) {
-        const MiIntraBlock &b = f->intra[i];
-        const int xl = b.plane ? b.x << ssh : b.x;
-        strip[i] = (int8_t)(std::upper_bound(sx.begin(), sx.end(), xl) - sx.begin() - 1);
-        for (int y = b.y >> 2; y < (b.y + b.h) >> 2; y++)
-            for (int x = b.x >> 2; x < (b.x + b.w) >> 2; x++) own[b.plane][(size_t)y * pw4[b.plane] + x] = i;
-    }
+    // (blocks of one plane never overlap: the owner map fills in any order, on several threads)
+    parallel_ranges(n, 32768, [&](int lo, int hi, int) {
+        for (int i = lo; i < hi; i++) {
+            const MiIntraBlock &b = f->intra[i];
+            const int xl = b.plane ? b.x << ssh : b.x;
+            strip[i] = (int8_t)(std::upper_bound(sx.begin(), sx.end(), xl) - sx.begin() - 1);
+            for (int y = b.y >> 2; y < (b.y + b.h) >> 2; y++)
+                for (int x = b.x >> 2; x < (b.x + b.w) >> 2; x++) own[b.plane][(size_t)y * pw4[b.plane] + x] = i;
+        }
+    });
     xs.assign(n + 1, 0);
     xd.clear();
     const int lpx = 128 / pxb;                                // plane px per line
-    std::vector<int32_t> add;
-    for (int i = 0; i < n; i++) {
-        xs[i] = (int32_t)xd.size();
+    // the blocks writing a line that block i reads across a strip boundary (false: a later
+    // writer, so the frame stays on one XCD)
+    auto scan_block = [&](int i, std::vector<int32_t> &add) -> bool {
         const MiIntraBlock &b = f->intra[i];
         const int p = b.plane;
         add.clear();
@@ -366,7 +394,7 @@ int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<in
             if (strip[j] == strip[i]) continue;
             const MiIntraBlock &o = f->intra[j];
             if (granules && o.plane == p && b.mode != MI_INTRA_IBC) continue;   // an edge: granules
-            if (o.plane != p) return 1;                       // (CfL luma: same strip by construction)
+            if (o.plane != p) return false;                   // (CfL luma: same strip by construction)
             const int x0 = std::max(bx0, (int)o.x), x1 = std::min(bx1, o.x + o.w);
             const int y0 = std::max(by0, (int)o.y), y1 = std::min(by1, o.y + o.h);
             if (x0 >= x1 || y0 >= y1) continue;
@@ -375,13 +403,37 @@ int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<in
                 for (int u = (l0 * lpx) >> 2; u < std::min(pw4[p], ((l1 + 1) * lpx) >> 2); u++) {
                     const int w = own[p][(size_t)y * pw4[p] + u];
                     if (w < 0 || w == j) continue;
-                    if (w >= i) return 1;                     // a later writer: no split
+                    if (w >= i) return false;                 // a later writer: no split
                     add.push_back(w);
                 }
         }
         std::sort(add.begin(), add.end());
         add.erase(std::unique(add.begin(), add.end()), add.end());
-        xd.insert(xd.end(), add.begin(), add.end());
+        return true;
+    };
+    // the extra dependencies per block range (each range its own CSR part), then concatenated
+    std::vector<int32_t> part_xd[8];
+    int part_lo[9] = {};
+    int split_ok = 1;
+    const int nparts = parallel_ranges(n, 32768, [&](int lo, int hi, int t) {
+        part_lo[t] = lo;
+        std::vector<int32_t> &pxd = part_xd[t];
+        std::vector<int32_t> add;
+        for (int i = lo; i < hi; i++) {
+            xs[i] = (int32_t)pxd.size();
+            if (!__atomic_load_n(&split_ok, __ATOMIC_RELAXED) || !scan_block(i, add)) {
+                __atomic_store_n(&split_ok, 0, __ATOMIC_RELAXED);
+                return;
+            }
+            pxd.insert(pxd.end(), add.begin(), add.end());
+        }
+    });
+    if (!split_ok) return 1;
+    for (int t = 0; t < nparts; t++) {
+        const int lo = part_lo[t], hi = t + 1 < nparts ? part_lo[t + 1] : n;
+        const int32_t base = (int32_t)xd.size();
+        for (int i = lo; i < hi; i++) xs[i] += base;
+        xd.insert(xd.end(), part_xd[t].begin(), part_xd[t].end());
     }
     xs[n] = (int32_t)xd.size();
     return ns;
@@ -419,11 +471,18 @@ int stage_upload(MiCtx *ctx, std::vector<Section> &secs, hipStream_t s, hipEvent
         ctx->fx_dev_bytes = n;
     }
     size_t upload = 0;
+    // the sections' bytes in 1-MB pieces, copied on several threads (tens of MB for a 4K frame)
+    struct Piece { size_t dst, len; const uint8_t *src; };
+    std::vector<Piece> pieces;
     for (const Section &x : secs)
         if (x.bytes && x.src) {
-            memcpy(ctx->fx_host + x.off, x.src, x.bytes);
+            for (size_t o = 0; o < x.bytes; o += (1u << 20))
+                pieces.push_back({ x.off + o, std::min<size_t>(1u << 20, x.bytes - o), (const uint8_t *)x.src + o });
             upload = std::max(upload, x.off + x.bytes);
         }
+    parallel_ranges((int)pieces.size(), 4, [&](int lo, int hi, int) {
+        for (int i = lo; i < hi; i++) memcpy(ctx->fx_host + pieces[i].dst, pieces[i].src, pieces[i].len);
+    });
     if (!ctx->fx_ev && hipEventCreateWithFlags(&ctx->fx_ev, hipEventDisableTiming) != hipSuccess) return -EIO;
     if (before && hipEventRecord(before, s) != hipSuccess) return -EIO;
     if (bytes) *bytes = (int64_t)upload;
@@ -525,21 +584,38 @@ int mi_ctx_timing(MiCtx *ctx, MiFrameTiming *out) {
 
 namespace {
 
-int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int *final, void *stream,
-              StageEvents &tev, int64_t *bytes) {
-    int r = validate(f, pics);
-    if (r) return ctx->last_error = r;
-    hipStream_t s = (hipStream_t)stream;
-    const size_t cb = f->bpc == 8 ? 2 : 4, pb = f->bpc == 8 ? 1 : 2;
+// The host side of one frame's execution (no device calls): the intra blocks in the
+// persistent queue's order (dependency levels within XCD strips) with their dependency lists
+// in queue positions, the inter units bucketed by shape class, the inter residuals grouped by
+// (tx size, picture band). scaled[k]: reference k is scaled (OBMC laps then take mi_mc_scaled).
+struct FramePlan {
+    std::vector<MiIntraBlock> blocks;
+    std::vector<MiTxBlock> tx;
+    std::vector<int32_t> dep_start, deps, strip_start;
+    bool inter = false, granules = false;
+    std::vector<int32_t> tl_ds, tl_deps, tl_strip;     // MI_IR_TIMELINE
+    std::vector<MiMcBlock> mc_b, lap_b[2], lap_s[2];
+    uint32_t mc_cs[2 * MI_MC_NCLASS + 1], lap_cs[2][2 * MI_MC_NCLASS + 1];
+    std::vector<MiTxBlock> itx_b;
+    uint32_t itx_bs[MI_N_RECT_TX_SIZES][MI_ITX_BANDS + 1];
+    double strips_ms = 0;
+};
+
+void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
     const int n = f->n_intra;
+    std::vector<MiIntraBlock> &blocks = pl.blocks;
+    std::vector<MiTxBlock> &tx = pl.tx;
+    std::vector<int32_t> &dep_start = pl.dep_start, &deps = pl.deps, &strip_start = pl.strip_start;
+    std::vector<int32_t> &tl_ds = pl.tl_ds, &tl_deps = pl.tl_deps, &tl_strip = pl.tl_strip;
+    blocks.resize(n);
+    tx.resize(n);
+    dep_start.assign(n + 1, 0);
+    deps.clear();
+    strip_start.clear();
 
     // dependency levels (deps always point backwards): level order lets the persistent
     // kernel's workers run every block of a level side by side. A single frame is split into
     // vertical strips, one per XCD (intra_strips), each strip's blocks in level order.
-    std::vector<MiIntraBlock> blocks(n);
-    std::vector<MiTxBlock> tx(n);
-    std::vector<int32_t> dep_start(n + 1), deps;
-    std::vector<int32_t> strip_start;
     using clk = std::chrono::steady_clock;
     const auto t_lv = clk::now();
     // edge granules (ipred.hip gran_fetch) when every pixel an intra edge reads is written in the
@@ -550,11 +626,11 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         const char *e = getenv("MI_IR_GRANULES");
         return !(e && e[0] == '0');
     }();
-    const bool inter = inter_present(f) || f->n_inter_tx;
-    bool granules = gran_env && !inter && n > 0;
+    const bool inter = pl.inter = inter_present(f) || f->n_inter_tx;
+    bool &granules = pl.granules;
+    granules = gran_env && !inter && n > 0;
     // MI_IR_TIMELINE=<file> (diagnostics): the launch's per-unit stamps, blocks and dependencies
     static const char *tl_path = getenv("MI_IR_TIMELINE");
-    std::vector<int32_t> tl_ds, tl_deps, tl_strip;
     for (int i = 0; granules && i < n; i++)
         if ((f->intra[i].flags & MI_INTRA_II) || f->intra[i].mode == MI_INTRA_RESID) granules = false;
     if (n) {
@@ -602,21 +678,26 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
                     if (f->intra[f->deps[d]].plane != b.plane) fn(pos[f->deps[d]]);
             }
         };
+        // (gathered in queue order over ranges of queue positions, on several threads)
         dep_start[0] = 0;
-        for (int i = 0; i < n; i++) {
-            const int k = pos[i];
-            blocks[k] = f->intra[i];
-            tx[k] = f->intra_tx[i];
-            int c = 0;
-            kdeps(i, [&](int) { c++; });
-            dep_start[k + 1] = c;
-        }
+        parallel_ranges(n, 32768, [&](int lo, int hi, int) {
+            for (int k = lo; k < hi; k++) {
+                const int i = inv[k];
+                blocks[k] = f->intra[i];
+                tx[k] = f->intra_tx[i];
+                int c = 0;
+                kdeps(i, [&](int) { c++; });
+                dep_start[k + 1] = c;
+            }
+        });
         for (int k = 0; k < n; k++) dep_start[k + 1] += dep_start[k];
         deps.resize(dep_start[n]);
-        for (int i = 0; i < n; i++) {
-            int o = dep_start[pos[i]];
-            kdeps(i, [&](int d) { deps[o++] = d; });
-        }
+        parallel_ranges(n, 32768, [&](int lo, int hi, int) {
+            for (int k = lo; k < hi; k++) {
+                int o = dep_start[k];
+                kdeps(inv[k], [&](int d) { deps[o++] = d; });
+            }
+        });
         static const bool prof = getenv("MI_FX_PROFILE") != nullptr;
         if (prof) {
             auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -635,15 +716,10 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         }
     }
     if (deps.empty()) deps.push_back(0);
-    if (ctx->tm_on) ctx->tm_strips_ms += std::chrono::duration<double, std::milli>(clk::now() - t_lv).count();
-    // inter frames: the references, units bucketed for mi_mc_frame (OBMC laps split by whether
-    // their reference is scaled), residuals grouped by transform size for mi_itx_frame
-    bool scaled[7] = {};
-    if (inter) {
-        if ((r = validate_refs(f, pics, scaled)) || (r = validate_inter(f, pics, scaled))) return ctx->last_error = r;
-    }
-    std::vector<MiMcBlock> mc_b, lap_b[2], lap_s[2];
-    uint32_t mc_cs[2 * MI_MC_NCLASS + 1], lap_cs[2][2 * MI_MC_NCLASS + 1];
+    pl.strips_ms = std::chrono::duration<double, std::milli>(clk::now() - t_lv).count();
+    std::vector<MiMcBlock> &mc_b = pl.mc_b, (&lap_b)[2] = pl.lap_b, (&lap_s)[2] = pl.lap_s;
+    uint32_t *mc_cs = pl.mc_cs;
+    uint32_t (&lap_cs)[2][2 * MI_MC_NCLASS + 1] = pl.lap_cs;
     bucket_mc(f->mc, f->n_mc, mc_b, mc_cs);
     for (int k = 0; k < 2; k++) {
         const MiMcBlock *u = k ? f->obmc_v : f->obmc_h;
@@ -653,8 +729,10 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
     }
     // residuals grouped by (tx size, picture band) for mi_itx_frame_banded: a counting sort
     // keeping decode order inside a group
-    std::vector<MiTxBlock> itx_b(f->n_inter_tx);
-    uint32_t itx_bs[MI_N_RECT_TX_SIZES][MI_ITX_BANDS + 1] = {};
+    std::vector<MiTxBlock> &itx_b = pl.itx_b;
+    itx_b.resize(f->n_inter_tx);
+    uint32_t (&itx_bs)[MI_N_RECT_TX_SIZES][MI_ITX_BANDS + 1] = pl.itx_bs;
+    memset(itx_bs, 0, sizeof(itx_bs));
     {
         constexpr int NK = MI_N_RECT_TX_SIZES * MI_ITX_BANDS;
         const int ah = (f->h + 127) & ~127, ssv = f->layout == 1;
@@ -670,6 +748,35 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
             for (int q = 0; q <= MI_ITX_BANDS; q++) itx_bs[t][q] = start[t * MI_ITX_BANDS + q];
         for (int i = 0; i < f->n_inter_tx; i++) itx_b[start[key(f->inter_tx[i])]++] = f->inter_tx[i];
     }
+}
+
+int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int *final, void *stream,
+              StageEvents &tev, int64_t *bytes) {
+    int r = validate(f, pics);
+    if (r) return ctx->last_error = r;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t cb = f->bpc == 8 ? 2 : 4, pb = f->bpc == 8 ? 1 : 2;
+    const int n = f->n_intra;
+    using clk = std::chrono::steady_clock;
+    // inter frames: the references (OBMC laps are split by whether their reference is scaled)
+    bool scaled[7] = {};
+    if (inter_present(f) || f->n_inter_tx) {
+        if ((r = validate_refs(f, pics, scaled)) || (r = validate_inter(f, pics, scaled))) return ctx->last_error = r;
+    }
+    FramePlan pl;
+    plan_frame(f, scaled, pl);
+    if (ctx->tm_on) ctx->tm_strips_ms += pl.strips_ms;
+    const bool inter = pl.inter, granules = pl.granules;
+    std::vector<MiIntraBlock> &blocks = pl.blocks;
+    std::vector<MiTxBlock> &tx = pl.tx;
+    std::vector<int32_t> &dep_start = pl.dep_start, &deps = pl.deps, &strip_start = pl.strip_start;
+    std::vector<int32_t> &tl_ds = pl.tl_ds, &tl_deps = pl.tl_deps, &tl_strip = pl.tl_strip;
+    std::vector<MiMcBlock> &mc_b = pl.mc_b, (&lap_b)[2] = pl.lap_b, (&lap_s)[2] = pl.lap_s;
+    uint32_t *mc_cs = pl.mc_cs;
+    uint32_t (&lap_cs)[2][2 * MI_MC_NCLASS + 1] = pl.lap_cs;
+    std::vector<MiTxBlock> &itx_b = pl.itx_b;
+    uint32_t (&itx_bs)[MI_N_RECT_TX_SIZES][MI_ITX_BANDS + 1] = pl.itx_bs;
+    static const char *tl_path = getenv("MI_IR_TIMELINE");
     const int sb128h = (f->h + 127) >> 7;
     std::vector<Section> secs = {
         { blocks.data(), blocks.size() * sizeof(MiIntraBlock), 0 },
@@ -889,6 +996,18 @@ int mi_frame_validate(const MiDecFrame *f, const MiFramePictures *pics, const ch
     }
     if (why) *why = r ? (g_why ? g_why : "?") : nullptr;
     return r;
+}
+
+double mi_frame_plan_ms(const MiDecFrame *f, int reps) {
+    if (!f || reps < 1) return -1.0;
+    bool scaled[7] = {};
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    for (int i = 0; i < reps; i++) {
+        FramePlan pl;
+        plan_frame(f, scaled, pl);
+    }
+    return std::chrono::duration<double, std::milli>(clk::now() - t0).count() / reps;
 }
 
 int mi_frame_end(MiCtx *ctx, void *stream) {

@@ -1,0 +1,9 @@
+# streaming deblock (lf_seg_kernel) parity + A/B against the tile kernel (diagnostic)
+set -o pipefail
+mkdir -p gpurun_out
+MI_LF_SEGH=128 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_lf_gpu.py tests/test_pipeline_gpu.py tests/test_inloop_filters.py -p no:cacheprovider > gpurun_out/r4_lfseg_t.log 2>&1; rc=$?; tail -3 gpurun_out/r4_lfseg_t.log; [ $rc -eq 0 ] || exit $rc
+MI_LF_SEGH=256 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_lf_gpu.py tests/test_pipeline_gpu.py -p no:cacheprovider > gpurun_out/r4_lfseg_t2.log 2>&1; rc=$?; tail -2 gpurun_out/r4_lfseg_t2.log; [ $rc -eq 0 ] || exit $rc
+for h in 0 128 192 256 0; do
+  MI_LF_SEGH=$h timeout -k 10 200 python bench.py --steps 30 --no-cpu-baseline --no-fg --no-intra --no-extra --no-verify > gpurun_out/r4_lfseg_$h.json 2>/dev/null || { echo "bench $h failed"; exit 1; }
+  python -c "import json,sys;d=json.load(open(sys.argv[1]));print('segh',sys.argv[2],d['value'],d['stage_ms'])" gpurun_out/r4_lfseg_$h.json $h
+done
