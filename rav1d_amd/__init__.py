@@ -197,6 +197,7 @@ def lib():
                                   ctypes.POINTER(MiFilmGrainData), ctypes.c_int, _VP])
     _sig(L, "mi_film_grain_prep", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiFilmGrainData), _VP])
     _sig(L, "mi_frame_run", ctypes.c_int, [_VP, _VP, ctypes.POINTER(MiFramePictures), ctypes.POINTER(ctypes.c_int), _VP])
+    _sig(L, "mi_frame_plan_ms", ctypes.c_double, [_VP, ctypes.c_int])
     _sig(L, "mi_frame_end", ctypes.c_int, [_VP, _VP])
     _sig(L, "mi_frame_validate", ctypes.c_int, [_VP, ctypes.POINTER(MiFramePictures), ctypes.POINTER(ctypes.c_char_p)])
     _sig(L, "mi_ctx_set_timing", ctypes.c_int, [_VP, ctypes.c_int])
@@ -214,7 +215,7 @@ def lib():
 EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
             "mi_itx_frame", "mi_itx_frame_banded", "mi_mc_frame", "mi_mc_frame_ex", "mi_mc_scaled", "mi_mc_warp", "mi_mc_combine", "mi_superres_frame",
             "mi_ipred_blocks", "mi_intra_blocks", "mi_intra_recon", "mi_ctx_device_status", "mi_deblock_frame", "mi_deblock_frame_to", "mi_cdef_frame", "mi_lr_frame",
-            "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply", "mi_frame_run", "mi_frame_end", "mi_frame_validate",
+            "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply", "mi_frame_run", "mi_frame_end", "mi_frame_validate", "mi_frame_plan_ms",
             "mi_ctx_set_timing", "mi_ctx_timing",
             "mi_dsp_itxfm_add", "mi_dsp_intra_pred", "mi_dsp_cfl_pred", "mi_dsp_pal_pred", "mi_dsp_cfl_ac",
             "mi_dsp_loop_filter_sb", "mi_dsp_cdef_filter", "mi_dsp_cdef_dir", "mi_dsp_mc_put", "mi_dsp_mc_prep",
