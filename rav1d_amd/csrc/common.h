@@ -85,9 +85,20 @@ __host__ __device__ constexpr int imax_c(int a, int b) { return a > b ? a : b; }
 // Lanes per transform block in the itx kernel: one lane per row in the row pass, one lane
 // per column in the column pass.
 __host__ __device__ constexpr int itx_lanes(int tx) {
+#ifndef MI_ITX_PAIR64
+#define MI_ITX_PAIR64 0
+#endif
+    // 64-point sizes (itx.hip itx_size64): a 64-point transform runs on a lane pair, so the
+    // row pass takes 2 lanes per 64-wide row and the column pass 2 per 64-tall column
+    if (MI_ITX_PAIR64 && (tx_dim(tx).w == 64 || tx_dim(tx).h == 64))
+        return imax_c(imin_c(tx_dim(tx).h, 32) * (tx_dim(tx).w == 64 ? 2 : 1),
+                      tx_dim(tx).w * (tx_dim(tx).h == 64 ? 2 : 1));
     return imax_c(imin_c(tx_dim(tx).h, 32), tx_dim(tx).w);
 }
-constexpr int kItxThreads = 256;
+#ifndef MI_ITX_THREADS
+#define MI_ITX_THREADS 256
+#endif
+constexpr int kItxThreads = MI_ITX_THREADS;
 __host__ __device__ constexpr int itx_blocks_per_wg(int tx) { return kItxThreads / itx_lanes(tx); }
 // Rounds of itx_blocks_per_wg blocks per workgroup: the small sizes' loads of all rounds are in
 // flight together (4-lane blocks: 4 rounds; 8-lane blocks: 1).

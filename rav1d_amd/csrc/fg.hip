@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kPrepThreads) void fg_prep_kernel(FgArgs a) {
     if (threadIdx.x == 0) *prog = ly ? -1 : 1 << 30;   // luma progress (caller's luma: final)
     __syncthreads();
 #ifndef MI_FG_AR_WAVE
-#define MI_FG_AR_WAVE 1
+#define MI_FG_AR_WAVE 0
 #endif
     switch (d.ar_coeff_lag) {
     case 0: grain_ar_all<0>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;

@@ -360,6 +360,161 @@ __device__ __forceinline__ void idct64(int *c, int lo, int hi) {
     dct_merge<64, S>(c, o, lo, hi);
 }
 
+// The 64-point DCT over a lane pair (the even and the odd lane of an aligned pair), so that no
+// lane holds more than 32 values: idct64 is its even half (a 32-point DCT of inputs 0, 2, ..,
+// 30) merged with its odd half (the t32..t63 network of inputs 1, 3, .., 31). In: y[k] = input
+// 2k (even lane) or 2k + 1 (odd lane), k < 16 (inputs >= 32 are zero, as in idct64). Out: the
+// even lane's y[i] = output i, the odd lane's y[i] = output 63 - i. The merge trades each
+// lane's half with its partner by DPP (quad_perm [1,0,3,2]); both lanes run both halves'
+// code paths masked, so a wave stays converged.
+__device__ __forceinline__ int pair_swap(int v) {
+    return __builtin_amdgcn_mov_dpp(v, 0xb1, 0xf, 0xf, false);
+}
+#define OD(i) y[((i) - 1) >> 1]
+template <bool W>
+__device__ __forceinline__ void idct64_odd(int *y, int lo, int hi) {
+    using A = Ar<W>;
+    int t[64];
+    t[32] = A::s12(OD(1), 101);   t[33] = A::s12(OD(31), -2824);
+    t[34] = A::s12(OD(17), 1660); t[35] = A::s12(OD(15), -1474);
+    t[36] = A::s12(OD(9), 897);   t[37] = A::s12(OD(23), -2191);
+    t[38] = A::s12(OD(25), 2359); t[39] = A::s12(OD(7), -700);
+    t[40] = A::s12(OD(5), 501);   t[41] = A::s12(OD(27), -2520);
+    t[42] = A::s12(OD(21), 2019); t[43] = A::s12(OD(11), -1092);
+    t[44] = A::s12(OD(13), 1285); t[45] = A::s12(OD(19), -1842);
+    t[46] = A::s12(OD(29), 2675); t[47] = A::s12(OD(3), -301);
+    t[48] = A::s12(OD(3), 4085);  t[49] = A::s12(OD(29), 3102);
+    t[50] = A::s12(OD(19), 3659); t[51] = A::s12(OD(13), 3889);
+    t[52] = A::s12(OD(11), 3948); t[53] = A::s12(OD(21), 3564);
+    t[54] = A::s12(OD(27), 3229); t[55] = A::s12(OD(5), 4065);
+    t[56] = A::s12(OD(7), 4036);  t[57] = A::s12(OD(25), 3349);
+    t[58] = A::s12(OD(23), 3461); t[59] = A::s12(OD(9), 3996);
+    t[60] = A::s12(OD(15), 3822); t[61] = A::s12(OD(17), 3745);
+    t[62] = A::s12(OD(31), 2967); t[63] = A::s12(OD(1), 4095);
+    int u[64];
+#pragma unroll
+    for (int g = 32; g < 64; g += 4) {
+        u[g] = clampi(t[g] + t[g + 1], lo, hi);
+        u[g + 1] = clampi(t[g] - t[g + 1], lo, hi);
+        u[g + 2] = clampi(t[g + 3] - t[g + 2], lo, hi);
+        u[g + 3] = clampi(t[g + 3] + t[g + 2], lo, hi);
+    }
+    {
+        const int a33 = A::r12(u[33], -4076, u[62], 401);
+        const int a62 = A::r12(u[33], 401, u[62], 4076);
+        const int a34 = A::r12(u[34], -401, u[61], -4076);
+        const int a61 = A::r12(u[34], -4076, u[61], 401);
+        const int a37 = A::r12(u[37], -2598, u[58], 3166);
+        const int a58 = A::r12(u[37], 3166, u[58], 2598);
+        const int a38 = A::r12(u[38], -3166, u[57], -2598);
+        const int a57 = A::r12(u[38], -2598, u[57], 3166);
+        const int a41 = A::r12(u[41], -3612, u[54], 1931);
+        const int a54 = A::r12(u[41], 1931, u[54], 3612);
+        const int a42 = A::r12(u[42], -1931, u[53], -3612);
+        const int a53 = A::r12(u[42], -3612, u[53], 1931);
+        const int a45 = A::r12(u[45], -1189, u[50], 3920);
+        const int a50 = A::r12(u[45], 3920, u[50], 1189);
+        const int a46 = A::r12(u[46], -3920, u[49], -1189);
+        const int a49 = A::r12(u[46], -1189, u[49], 3920);
+        u[33] = a33; u[62] = a62; u[34] = a34; u[61] = a61;
+        u[37] = a37; u[58] = a58; u[38] = a38; u[57] = a57;
+        u[41] = a41; u[54] = a54; u[42] = a42; u[53] = a53;
+        u[45] = a45; u[50] = a50; u[46] = a46; u[49] = a49;
+    }
+    int v[64];
+#pragma unroll
+    for (int g = 32; g < 64; g += 8) {
+        v[g] = clampi(u[g] + u[g + 3], lo, hi);
+        v[g + 1] = clampi(u[g + 1] + u[g + 2], lo, hi);
+        v[g + 2] = clampi(u[g + 1] - u[g + 2], lo, hi);
+        v[g + 3] = clampi(u[g] - u[g + 3], lo, hi);
+        v[g + 4] = clampi(u[g + 7] - u[g + 4], lo, hi);
+        v[g + 5] = clampi(u[g + 6] - u[g + 5], lo, hi);
+        v[g + 6] = clampi(u[g + 6] + u[g + 5], lo, hi);
+        v[g + 7] = clampi(u[g + 7] + u[g + 4], lo, hi);
+    }
+    {
+        const int b34 = A::r12(v[34], -4017, v[61], 799);
+        const int b61 = A::r12(v[34], 799, v[61], 4017);
+        const int b35 = A::r12(v[35], -4017, v[60], 799);
+        const int b60 = A::r12(v[35], 799, v[60], 4017);
+        const int b36 = A::r12(v[36], -799, v[59], -4017);
+        const int b59 = A::r12(v[36], -4017, v[59], 799);
+        const int b37 = A::r12(v[37], -799, v[58], -4017);
+        const int b58 = A::r12(v[37], -4017, v[58], 799);
+        const int b42 = A::r12(v[42], -2276, v[53], 3406);
+        const int b53 = A::r12(v[42], 3406, v[53], 2276);
+        const int b43 = A::r12(v[43], -2276, v[52], 3406);
+        const int b52 = A::r12(v[43], 3406, v[52], 2276);
+        const int b44 = A::r12(v[44], -3406, v[51], -2276);
+        const int b51 = A::r12(v[44], -2276, v[51], 3406);
+        const int b45 = A::r12(v[45], -3406, v[50], -2276);
+        const int b50 = A::r12(v[45], -2276, v[50], 3406);
+        v[34] = b34; v[61] = b61; v[35] = b35; v[60] = b60;
+        v[36] = b36; v[59] = b59; v[37] = b37; v[58] = b58;
+        v[42] = b42; v[53] = b53; v[43] = b43; v[52] = b52;
+        v[44] = b44; v[51] = b51; v[45] = b45; v[50] = b50;
+    }
+    int w[64];
+#pragma unroll
+    for (int g = 32; g < 64; g += 16) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            w[g + k] = clampi(v[g + k] + v[g + 7 - k], lo, hi);
+            w[g + 7 - k] = clampi(v[g + k] - v[g + 7 - k], lo, hi);
+            w[g + 8 + k] = clampi(v[g + 15 - k] - v[g + 8 + k], lo, hi);
+            w[g + 15 - k] = clampi(v[g + 15 - k] + v[g + 8 + k], lo, hi);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int p = 36 + k, q = 59 - k;
+        const int wp = w[p], wq = w[q];
+        w[p] = A::r12(wp, -3784, wq, 1567);
+        w[q] = A::r12(wp, 1567, wq, 3784);
+        const int r = 40 + k, s = 55 - k;
+        const int wr = w[r], ws = w[s];
+        w[r] = A::r12(wr, -1567, ws, -3784);
+        w[s] = A::r12(wr, -3784, ws, 1567);
+    }
+    int x[64];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        x[32 + k] = clampi(w[32 + k] + w[47 - k], lo, hi);
+        x[47 - k] = clampi(w[32 + k] - w[47 - k], lo, hi);
+        x[48 + k] = clampi(w[63 - k] - w[48 + k], lo, hi);
+        x[63 - k] = clampi(w[63 - k] + w[48 + k], lo, hi);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int l = 40 + k, h = 55 - k;
+        const int xl = x[l], xh = x[h];
+        x[l] = A::h181(xh - xl);
+        x[h] = A::h181(xh + xl);
+    }
+#pragma unroll
+    for (int i = 0; i < 32; i++) y[i] = x[32 + i];
+}
+#undef OD
+
+template <bool W>
+__device__ __forceinline__ void idct64_pair(int *y, bool odd, int lo, int hi) {
+    if (!odd) {
+#pragma unroll
+        for (int i = 16; i < 32; i++) y[i] = 0;
+        idct32<W, 1>(y, lo, hi, true);
+    } else {
+        idct64_odd<W>(y, lo, hi);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const int a = y[i], b = y[31 - i];
+        const int sa = pair_swap(a), sb = pair_swap(b);
+        y[i] = odd ? clampi(sa - b, lo, hi) : clampi(a + sb, lo, hi);
+        y[31 - i] = odd ? clampi(sb - a, lo, hi) : clampi(b + sa, lo, hi);
+    }
+}
+
 // ---- ADST: outputs written in natural order into `out` (flip handled by the caller) ----
 
 template <bool W>
