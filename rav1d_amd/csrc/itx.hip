@@ -26,6 +26,10 @@ MI_KTL_DEFINE(itx)
 
 namespace mi {
 
+#ifndef MI_ITX_PERSIST
+#define MI_ITX_PERSIST 0   // > 0: a persistent grid of 256 x MI_ITX_PERSIST workgroups walks the schedule
+#endif
+
 // TxfmType -> 1-D kinds (levels.rs TxfmType is VERT_HORZ; itx_tmpl.c:196-233)
 __constant__ uint8_t k_col_kind[16] = { KD, KA, KD, KA, KF, KD, KF, KA, KF, KI, KD, KI, KA, KI, KF, KI };
 __constant__ uint8_t k_row_kind[16] = { KD, KD, KA, KA, KD, KF, KF, KF, KA, KI, KI, KD, KI, KA, KI, KF };
@@ -87,7 +91,10 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     constexpr int NCH = (Ht * CPR + TPB - 1) / TPB;   // chunks per lane
     using V = typename Vec4<Px>::T;
 
-    const int t = threadIdx.x;
+    int t = threadIdx.x;
+#if MI_ITX_PERSIST
+    asm volatile("" : "+v"(t));   // (persistent grid: nothing derived from the lane is hoisted out of the item loop)
+#endif
     const int lb = t / TPB, j = t % TPB;
     // this workgroup's block range: the whole size, or (banded grid) band lwg % 8 of it
     int bs = a.blk_start[TX], be = a.blk_start[TX + 1], k = lwg;
@@ -308,7 +315,10 @@ __device__ __forceinline__ void itx_size64(const ItxArgs &a, int lwg, Lt *lds) {
     constexpr int NCH = (Ht * CPR + TPB - 1) / TPB;      // chunks per lane
     using V = typename Vec4<Px>::T;
 
-    const int t = threadIdx.x;
+    int t = threadIdx.x;
+#if MI_ITX_PERSIST
+    asm volatile("" : "+v"(t));   // (persistent grid: nothing derived from the lane is hoisted out of the item loop)
+#endif
     const int lb = t / TPB, j = t % TPB;
     int bs = a.blk_start[TX], be = a.blk_start[TX + 1], k = lwg;
     if (a.nbands > 1) {
@@ -473,8 +483,14 @@ template <typename Px, typename Cf, typename Lt, bool Wide>
 #endif
 __global__ __launch_bounds__(kItxThreads, MI_ITX_MINW) void itx_frame_kernel(ItxArgs a) {
     __shared__ Lt lds[itx_lds_max(true) > itx_lds_max(false) ? itx_lds_max(true) : itx_lds_max(false)];
-    const int wg = blockIdx.x;
     KTL(0);
+#if MI_ITX_PERSIST
+    for (int wg = blockIdx.x; wg < a.wg_start[19]; wg += gridDim.x) {
+    if (wg != (int)blockIdx.x) __syncthreads();   // the previous item's LDS reads are done
+#else
+    {
+    const int wg = blockIdx.x;
+#endif
     // the size range holding this workgroup, with compile-time indices only (a runtime index
     // into the kernel-argument struct makes the compiler copy it to scratch)
     int s = a.wg_size[0], base = a.wg_start[0];
@@ -498,8 +514,9 @@ __global__ __launch_bounds__(kItxThreads, MI_ITX_MINW) void itx_frame_kernel(Itx
 #endif
     default: break;
     }
-    KTL(5);
     KTLV(6, s);
+    }
+    KTL(5);
 }
 
 int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start, const uint32_t *band_start) {
@@ -534,6 +551,7 @@ int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start, const uint32_t *ba
 
 int launch_itx_frame(const ItxArgs &a, int nwg, int bpc, hipStream_t s) {
     if (nwg <= 0) return 0;
+    if (MI_ITX_PERSIST) nwg = std::min(nwg, 256 * MI_ITX_PERSIST);   // a multiple of 8: the band -> XCD rule holds
     if (bpc == 8) hipLaunchKernelGGL((itx_frame_kernel<uint8_t, int16_t, int16_t, false>), dim3(nwg), dim3(kItxThreads), 0, s, a);
     else if (bpc == 10) hipLaunchKernelGGL((itx_frame_kernel<uint16_t, int32_t, int16_t, false>), dim3(nwg), dim3(kItxThreads), 0, s, a);
     else hipLaunchKernelGGL((itx_frame_kernel<uint16_t, int32_t, int32_t, true>), dim3(nwg), dim3(kItxThreads), 0, s, a);
