@@ -20,6 +20,9 @@
 #include <algorithm>
 #include <cstdlib>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -28,29 +31,81 @@
 
 namespace {
 
-// fn(lo, hi) over [0, n) in up to `threads` contiguous ranges on std::threads (the caller runs
-// the first range). Host planning of large frames only: below `min_n` items it runs inline.
-template <typename Fn>
-int parallel_ranges(int n, int min_n, Fn &&fn) {
-    static const int hw = [] {
+// A small pool of host threads for the planning pass of large frames (created on first use,
+// never torn down). One job at a time: a caller that finds the pool busy (another context's
+// frame_run on another host thread) runs its ranges inline.
+class PlanPool {
+  public:
+    explicit PlanPool(int n) : n_(n) {
+        for (int t = 1; t < n_; t++) std::thread([this, t] { worker(t); }).detach();
+    }
+    int size() const { return n_; }
+    // fn(t) for t in [0, n_) (t = 0 on the calling thread); false: the pool is busy
+    bool run(const std::function<void(int)> &fn) {
+        std::unique_lock<std::mutex> use(use_, std::try_to_lock);
+        if (!use.owns_lock()) return false;
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &fn;
+            left_ = n_ - 1;
+            gen_++;
+        }
+        cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [this] { return left_ == 0; });
+        job_ = nullptr;
+        return true;
+    }
+
+  private:
+    void worker(int t) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)> *job;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return gen_ != seen; });
+                seen = gen_;
+                job = job_;
+            }
+            (*job)(t);
+            std::lock_guard<std::mutex> g(m_);
+            if (--left_ == 0) done_.notify_one();
+        }
+    }
+    const int n_;
+    std::mutex use_, m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)> *job_ = nullptr;
+    uint64_t gen_ = 0;
+    int left_ = 0;
+};
+
+PlanPool *plan_pool() {
+    static PlanPool *pool = [] {
         const char *e = getenv("MI_FX_THREADS");
         const int t = e ? atoi(e) : (int)std::thread::hardware_concurrency();
-        return std::max(1, std::min(t, 8));
+        return new PlanPool(std::max(1, std::min(t, 8)));
     }();
-    const int nt = n < min_n ? 1 : hw;
-    if (nt <= 1) {
-        fn(0, n, 0);
-        return 1;
-    }
-    std::vector<std::thread> th;
-    th.reserve(nt - 1);
-    for (int t = 1; t < nt; t++)
-        th.emplace_back([&, t] { fn((int)((int64_t)n * t / nt), (int)((int64_t)n * (t + 1) / nt), t); });
-    fn(0, (int)((int64_t)n / nt), 0);
-    for (std::thread &x : th) x.join();
-    return nt;
+    return pool;
 }
 
+// fn(lo, hi, t) over [0, n) in contiguous ranges, one per pool thread; below `min_n` items (or
+// with the pool busy) on the calling thread alone. Returns the number of ranges.
+template <typename Fn>
+int parallel_ranges(int n, int min_n, Fn &&fn) {
+    PlanPool *pool = plan_pool();
+    const int nt = n < min_n ? 1 : pool->size();
+    if (nt > 1) {
+        const std::function<void(int)> job = [&](int t) {
+            fn((int)((int64_t)n * t / nt), (int)((int64_t)n * (t + 1) / nt), t);
+        };
+        if (pool->run(job)) return nt;
+    }
+    fn(0, n, 0);
+    return 1;
+}
 
 // Legal TxfmType values per RectTxfmSize (itx.rs:400-457): the 4/8/16-class rectangles and
 // 8x8 and below carry all 16 (4x4 also WHT_WHT = 16), 16x16 the first 12, the 32 class
@@ -678,11 +733,11 @@ void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
                     if (f->intra[f->deps[d]].plane != b.plane) fn(pos[f->deps[d]]);
             }
         };
-        // (gathered in queue order over ranges of queue positions, on several threads)
+        // (ranges of decode order on several threads: every unit has its own queue slot)
         dep_start[0] = 0;
         parallel_ranges(n, 32768, [&](int lo, int hi, int) {
-            for (int k = lo; k < hi; k++) {
-                const int i = inv[k];
+            for (int i = lo; i < hi; i++) {
+                const int k = pos[i];
                 blocks[k] = f->intra[i];
                 tx[k] = f->intra_tx[i];
                 int c = 0;
@@ -693,9 +748,9 @@ void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
         for (int k = 0; k < n; k++) dep_start[k + 1] += dep_start[k];
         deps.resize(dep_start[n]);
         parallel_ranges(n, 32768, [&](int lo, int hi, int) {
-            for (int k = lo; k < hi; k++) {
-                int o = dep_start[k];
-                kdeps(inv[k], [&](int d) { deps[o++] = d; });
+            for (int i = lo; i < hi; i++) {
+                int o = dep_start[pos[i]];
+                kdeps(i, [&](int d) { deps[o++] = d; });
             }
         });
         static const bool prof = getenv("MI_FX_PROFILE") != nullptr;
