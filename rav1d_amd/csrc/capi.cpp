@@ -439,6 +439,15 @@ int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, v
     return r ? fail(ctx, -EIO) : 0;
 }
 
+// Loop restoration over picture bands, one XCD per band (LrArgs.banded); MI_LR_BANDS=0 turns it off
+static int lr_banded() {
+    static const int v = [] {
+        const char *e = getenv("MI_LR_BANDS");
+        return e ? atoi(e) != 0 : 0;
+    }();
+    return v;
+}
+
 // Rows per streaming deblock segment (lf_seg_kernel), 0 = the tile kernel. MI_LF_SEGH
 // overrides (a multiple of 32).
 static int lf_seg_rows() {
@@ -591,8 +600,18 @@ int mi_lr_frame(MiCtx *ctx, const MiPicture *cdef, const MiPicture *deblocked, c
         // stripes: 64 luma rows, the first 56 (lr_apply.rs:54)
         int stripes = 0;
         while ((stripes ? (64 * stripes - 8) >> sv : 0) < a.ph[p]) stripes++;
-        nb += stripes * a.tiles_x[p];
+        a.stripes[p] = stripes;
+        if (lr_banded()) {
+            // band q = stripes [q * stripes / 8, (q + 1) * stripes / 8)
+            int m = 0;
+            for (int q = 0; q < 8; q++) m = std::max(m, ((q + 1) * stripes / 8 - q * stripes / 8) * a.tiles_x[p]);
+            a.band_m[p] = m;
+            nb += 8 * m;
+        } else {
+            nb += stripes * a.tiles_x[p];
+        }
     }
+    a.banded = lr_banded();
     a.blk_start[3] = nb;
     const int r = mi::launch_lr(a, cdef->bpc, (hipStream_t)stream);
     return r ? fail(ctx, -EIO) : 0;

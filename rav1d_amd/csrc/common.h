@@ -324,6 +324,11 @@ struct LrArgs {
     int unit_log2[2];
     int pw[3], ph[3], tw[3], tiles_x[3];
     int blk_start[4];
+    // banded grid (MI_LR_BANDS): plane p's stripes in 8 bands of consecutive stripes, band q's
+    // tiles at grid indices = q mod 8 (XCD q under the dispatcher's round robin), so the column
+    // halo lines neighbouring tiles share are fetched into one L2; stripes[p] = stripe count,
+    // band_m[p] = workgroups per band (the largest band's tile count)
+    int stripes[3], band_m[3], banded;
 };
 // launchers (lr.hip)
 int launch_lr(const LrArgs &a, int bpc, hipStream_t s);

@@ -174,7 +174,11 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     for (int c4 = 0; c4 < NCH; c4++) pix[c4] = pk[rd][c4];
     Cf *cf = reinterpret_cast<Cf *>(a.coef) + b.coef_off;
     const bool wht = (TX == 0) && b.txtp == 16;
+#ifdef MI_ITX_SKEL   // experiment builds only: every block as DC-only (the memory skeleton)
+    const bool dconly = true;
+#else
     const bool dconly = b.txtp == 0 && b.eob < 1;
+#endif
     uint8_t *pbase = sel3(plane3, b.plane) + (int64_t)b.y * sel3(stride3, b.plane) + (int64_t)b.x * sizeof(Px);
     const int64_t st = sel3(stride3, b.plane);
 

@@ -400,8 +400,15 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
 #endif
     const int blk = MI_LR_XCD == 1 ? xcd_block(blockIdx.x, gridDim.x) : MI_LR_XCD > 1 ? xcd_chunk(blockIdx.x, gridDim.x, MI_LR_XCD) : blockIdx.x;
     const int p = blk < a.blk_start[1] ? 0 : blk < a.blk_start[2] ? 1 : 2;
-    const int lb = blk - a.blk_start[p];
+    int lb = blk - a.blk_start[p];
     const int tiles = a.tiles_x[p];
+    if (a.banded) {
+        // grid index 8m + q: the m-th tile of band q (plane starts are multiples of 8)
+        const int q = lb & 7, m = lb >> 3, ns = a.stripes[p];
+        const int s0 = q * ns / 8, s1 = (q + 1) * ns / 8;
+        if (m >= (s1 - s0) * tiles) return;           // padding of a smaller band
+        lb = s0 * tiles + m;
+    }
     const int k = lb / tiles, ti = lb - k * tiles;
     const int ssv = p ? a.ss_ver : 0, ssh = p ? a.ss_hor : 0;
     const int pw = a.pw[p], ph = a.ph[p];

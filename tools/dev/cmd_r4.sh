@@ -10,11 +10,11 @@ MI_LIB=$PWD/rav1d_amd/librav1d_amd_ktl.so timeout -k 10 300 python -u tools/dev/
 MI_LF_SEGH=128 MI_LIB=$PWD/rav1d_amd/librav1d_amd_ktl.so KTL_UNITS=lf timeout -k 10 300 python -u tools/dev/ktl.py > gpurun_out/r4_ktl_seg.log 2>&1; echo "ktl seg rc=$?"; cat gpurun_out/r4_ktl_seg.log
 timeout -k 10 60 ./tools/dev/anyorder_test
 # 4. itx variants (64-class excluded, then all)
-for v in base no64 no64w6 t64 t64no64 t128 new p4 p8 t64p16 p4n; do
+for v in base no64 no64w6 t64 t64no64 t128 new p4 p8 t64p16 p4n skel; do
   if [ $v = base ]; then L=$PWD/rav1d_amd/librav1d_amd.so; else L=$PWD/rav1d_amd/librav1d_amd_$v.so; fi
   MI_LIB=$L timeout -k 10 120 python -u tools/dev/exp_itx_sub.py || exit 1
 done
-for v in base t64 t128 new p4 p8 t64p16 p4n; do
+for v in base t64 t128 new p4 p8 t64p16 p4n skel; do
   if [ $v = base ]; then L=$PWD/rav1d_amd/librav1d_amd.so; else L=$PWD/rav1d_amd/librav1d_amd_$v.so; fi
   NO64=0 MI_LIB=$L timeout -k 10 120 python -u tools/dev/exp_itx_sub.py || exit 1
 done
