@@ -448,17 +448,6 @@ static int lr_banded() {
     return v;
 }
 
-// Rows per streaming deblock segment (lf_seg_kernel), 0 = the tile kernel. MI_LF_SEGH
-// overrides (a multiple of 32).
-static int lf_seg_rows() {
-    static const int v = [] {
-        const char *e = getenv("MI_LF_SEGH");
-        const int r = e ? atoi(e) : 0;
-        return r > 0 && r % 32 == 0 ? r : 0;
-    }();
-    return v;
-}
-
 int mi_deblock_frame_to(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const MiLoopFilter *lf,
                         void *stream) {
     if (!ctx || !src || !dst || !lf) return fail(ctx, -EINVAL);
@@ -516,16 +505,9 @@ int mi_deblock_frame_to(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, 
         a.rows_px[p] = p && !filter_uv ? 0 : a.pw[p];
         a.rows_uy[p] = p && !filter_uv ? 0 : p ? sb128h * (32 >> v) : a.h4;
         a.tiles_x[p] = (a.pw[p] + mi::kLfTW - 1) / mi::kLfTW;
-        if (lf_seg_rows()) {
-            a.seg_h[p] = lf_seg_rows();
-            a.segs[p] = (a.ph[p] + a.seg_h[p] - 1) / a.seg_h[p];
-            n += a.tiles_x[p] * a.segs[p];
-        } else {
-            n += a.tiles_x[p] * ((a.ph[p] + mi::kLfTH - 1) / mi::kLfTH);
-        }
+        n += a.tiles_x[p] * ((a.ph[p] + mi::kLfTH - 1) / mi::kLfTH);
     }
     a.tile_start[3] = n;
-    if (lf_seg_rows()) return mi::launch_deblock_segs(a, src->bpc, (hipStream_t)stream) ? fail(ctx, -EIO) : 0;
     return mi::launch_deblock_tiles(a, src->bpc, (hipStream_t)stream) ? fail(ctx, -EIO) : 0;
 }
 

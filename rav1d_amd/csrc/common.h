@@ -196,13 +196,8 @@ struct LfTileArgs {
     int pw[3], ph[3], tiles_x[3];   // staged plane area (128-aligned picture), tiles per row
     int tile_start[4];
     uint8_t lim_e[64], lim_i[64];
-    // streaming segments (lf_seg_kernel): plane p is cut into tiles_x[p] columns of kLfTW px and
-    // segs[p] segments of seg_h[p] rows (a multiple of 32); tile_start then counts segments
-    int seg_h[3], segs[3];
 };
 int launch_deblock_tiles(const LfTileArgs &a, int bpc, hipStream_t s);
-int launch_deblock_segs(const LfTileArgs &a, int bpc, hipStream_t s);
-constexpr int kLfSegThreads = 256;
 // launchers (lf.hip)
 int launch_deblock(const LfArgs &cols, const LfArgs &rows, int bpc, hipStream_t s);
 

@@ -360,79 +360,6 @@ __device__ __forceinline__ bool filter_regs(int (&v)[16], int E, int I, int H, i
     return true;
 }
 
-// Column edges of one width class: 4 lines per listed unit. The 16-px window [e-8, e+8) of
-// a line is 4 aligned 4-px quads of LDS. Write-back granules are chosen inside the span
-// no other edge of the direction touches (a wd-16 edge owns its whole window, a wd-8 edge
-// [e-4, e+4), a wd-4/6 edge [e-2, e+2)), so whole quads / pairs are stored.
-template <int WD, typename Px, int P>
-__device__ __forceinline__ void lf_cols_class(Px *t, const uint16_t *list, int n, const uint8_t *le,
-                                              const uint8_t *li, int bdm8, int bdmax) {
-    for (int i = threadIdx.x; i < n * 4; i += kLfThreads) {
-        const int e = list[i >> 2];
-        const int u = e >> 6, L = e & 63;
-        const int r = (u / kLfEdgesV) * 4 + (i & 3), k = u % kLfEdgesV;
-        Px *w = &t[r * P + 4 + 4 * k];
-        constexpr int q0 = WD == 16 ? 0 : 1, q1 = WD == 16 ? 4 : 3;   // quads loaded
-        int v[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) v[j] = 0;
-#pragma unroll
-        for (int q = q0; q < q1; q++) {
-            if constexpr (sizeof(Px) == 2) {
-                const uint2 d = reinterpret_cast<const uint2 *>(w)[q];
-                v[4 * q] = d.x & 0xffff; v[4 * q + 1] = d.x >> 16;
-                v[4 * q + 2] = d.y & 0xffff; v[4 * q + 3] = d.y >> 16;
-            } else {
-                const uint32_t d = reinterpret_cast<const uint32_t *>(w)[q];
-#pragma unroll
-                for (int j = 0; j < 4; j++) v[4 * q + j] = (d >> (8 * j)) & 0xff;
-            }
-        }
-        if (!filter_regs<WD>(v, le[L], li[L], L >> 4, bdm8, bdmax)) continue;
-        if constexpr (WD >= 8) {
-#pragma unroll
-            for (int q = q0; q < q1; q++) {
-                if constexpr (sizeof(Px) == 2)
-                    reinterpret_cast<uint2 *>(w)[q] = make_uint2(v[4 * q] | (v[4 * q + 1] << 16),
-                                                                 v[4 * q + 2] | (v[4 * q + 3] << 16));
-                else
-                    reinterpret_cast<uint32_t *>(w)[q] = v[4 * q] | (v[4 * q + 1] << 8) |
-                                                         (v[4 * q + 2] << 16) | (v[4 * q + 3] << 24);
-            }
-        } else {
-            if constexpr (sizeof(Px) == 2) {
-                reinterpret_cast<uint32_t *>(w)[3] = v[6] | (v[7] << 16);
-                reinterpret_cast<uint32_t *>(w)[4] = v[8] | (v[9] << 16);
-            } else {
-                reinterpret_cast<uint16_t *>(w)[3] = v[6] | (v[7] << 8);
-                reinterpret_cast<uint16_t *>(w)[4] = v[8] | (v[9] << 8);
-            }
-        }
-    }
-}
-
-// Row edges of one width class: 4 pixel columns per listed unit. Edge row e = y0 - 4 + 4k
-// sits at staged row 8 + 4k; v[8] is that row. (Two columns per lane with 2-pixel LDS
-// accesses measured slower: 28.8 -> 31.1 us at 4K10.)
-template <int WD, typename Px, int P>
-__device__ __forceinline__ void lf_rows_class(Px *t, const uint16_t *list, int n, const uint8_t *le,
-                                              const uint8_t *li, int bdm8, int bdmax) {
-    constexpr int nr = WD == 16 ? 7 : WD == 8 ? 4 : WD == 6 ? 3 : 2;   // rows read each side
-    constexpr int lo = WD == 16 ? 2 : WD == 8 ? 5 : 6;                 // rows [lo, 16 - lo) written
-    for (int i = threadIdx.x; i < n * 4; i += kLfThreads) {
-        const int e = list[i >> 2];
-        const int u = e >> 6, L = e & 63;
-        const int k = u / (kLfTW / 4), col = (u % (kLfTW / 4)) * 4 + (i & 3);
-        Px *w = &t[(4 * k) * P + 16 + col];
-        int v[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) v[j] = (j >= 8 - nr && j < 8 + nr) ? (int)w[j * P] : 0;
-        if (!filter_regs<WD>(v, le[L], li[L], L >> 4, bdm8, bdmax)) continue;
-#pragma unroll
-        for (int j = lo; j < 16 - lo; j++) w[j * P] = (Px)v[j];
-    }
-}
-
 // ---- two pixel lines per lane in packed 16-bit arithmetic ----
 //
 // The two lines of a lane belong to one edge unit, so they share the filter width and level.
@@ -770,17 +697,7 @@ __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
     __syncthreads();
     KTL(2);
     // column edges, then row edges, one loop per width class
-#if defined(MI_LF_UNPACKED)
-    lf_cols_class<4, Px, P>(t, listv[0], cnt[0], le, li, a.bdm8, a.bdmax);
-    lf_cols_class<6, Px, P>(t, listv[1], cnt[1], le, li, a.bdm8, a.bdmax);
-    lf_cols_class<8, Px, P>(t, listv[2], cnt[2], le, li, a.bdm8, a.bdmax);
-    lf_cols_class<16, Px, P>(t, listv[3], cnt[3], le, li, a.bdm8, a.bdmax);
-    __syncthreads();
-    lf_rows_class<4, Px, P>(t, listh[0], cnt[4], le, li, a.bdm8, a.bdmax);
-    lf_rows_class<6, Px, P>(t, listh[1], cnt[5], le, li, a.bdm8, a.bdmax);
-    lf_rows_class<8, Px, P>(t, listh[2], cnt[6], le, li, a.bdm8, a.bdmax);
-    lf_rows_class<16, Px, P>(t, listh[3], cnt[7], le, li, a.bdm8, a.bdmax);
-#elif !defined(MI_LF_NOFILTER)
+#if !defined(MI_LF_NOFILTER)
     lf_dir_pk<true, Px, P>(t, listv, cnt, le, li, a.bdm8, a.bdmax);
     __syncthreads();
     KTL(3);
@@ -798,249 +715,6 @@ __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
                 *reinterpret_cast<const uint4 *>(&t[(12 + r) * P + 16 + c]);
     }
     KTL(5);
-}
-
-// ---- streaming deblock: one workgroup walks down a 64-px column segment ----
-//
-// The tile kernel above stages every tile's 24-row vertical halo and runs one tile per
-// workgroup: at 4K10 its 1,560 tiles of 64x128 take 1.5 rounds of the 1,024 workgroups the
-// LDS admits, and each workgroup's staging latency is exposed. Here a 256-lane workgroup owns
-// the 64-px column [x0, x0+64) of rows [ys, ye) of one plane and walks down it in steps of 32
-// rows through a 64-row LDS ring (pitch kLfCols: columns x0-16 .. x0+79):
-//   step k (E = ys + 32k) - the chunk of rows [E+16, E+48) (fetched into registers during step
-//   k-1) goes into the ring and gets its column edges; then the row edges e in [E, E+32) (they
-//   read rows e-7 .. e+6, all column-filtered by now), and rows [E-16, E+16) are final and
-//   stored. Step -1 loads rows [ys-16, ys+16) and filters the one edge above the segment
-//   (ys-4) whose writes reach row ys.
-// The next step's pixels and edge units are loaded while the current step filters, so a
-// workgroup streams; the only halo is 28 rows per segment. Equal to the tile kernel (all
-// column edges, then all row edges): within one direction the edges'
-// read and write footprints are disjoint, so the order of edges does not matter.
-constexpr int kSegRing = 64;                    // ring rows (a power of two)
-constexpr int kSegNV = 8 * kLfEdgesV;           // column-edge units of one 32-row chunk
-constexpr int kSegNH = 8 * (kLfTW / 4);         // row-edge units of one step (8 edge rows)
-constexpr int kSegNU = kSegNV + kSegNH;
-
-template <int WD, typename Px>
-__device__ __forceinline__ void seg_col_pair(Px *ring, const uint16_t *list, int i, int c0, const uint8_t *le,
-                                             const uint8_t *li, int bdm8, int bdmax) {
-    constexpr int P = kLfCols;
-    const int e = list[i >> 1];
-    const int u = e >> 6, L = e & 63;
-    const int y = c0 + (u / kLfEdgesV) * 4 + 2 * (i & 1), k = u % kLfEdgesV;
-    Px *w0 = &ring[(y & (kSegRing - 1)) * P + 4 + 4 * k], *w1 = w0 + P;   // y even: y + 1 does not wrap
-    constexpr int q0 = WD == 16 ? 0 : 1, q1 = WD == 16 ? 4 : 3;
-    lf_s2 v[16];
-#pragma unroll
-    for (int j = 0; j < 16; j++) v[j] = pk_splat(0);
-#pragma unroll
-    for (int q = q0; q < q1; q++) pk_load_quad<Px>(w0, w1, q, &v[4 * q]);
-    filter_pk<WD>(v, le[L], li[L], L >> 4, bdm8, bdmax);
-    if constexpr (WD >= 8) {
-#pragma unroll
-        for (int q = q0; q < q1; q++) {
-            if constexpr (sizeof(Px) == 2) {
-                reinterpret_cast<uint2 *>(w0)[q] = make_uint2(pk_row_lo(v[4 * q], v[4 * q + 1]), pk_row_lo(v[4 * q + 2], v[4 * q + 3]));
-                reinterpret_cast<uint2 *>(w1)[q] = make_uint2(pk_row_hi(v[4 * q], v[4 * q + 1]), pk_row_hi(v[4 * q + 2], v[4 * q + 3]));
-            } else {
-                reinterpret_cast<uint32_t *>(w0)[q] = pk_row_lo8(v[4 * q], v[4 * q + 1]) | ((uint32_t)pk_row_lo8(v[4 * q + 2], v[4 * q + 3]) << 16);
-                reinterpret_cast<uint32_t *>(w1)[q] = pk_row_hi8(v[4 * q], v[4 * q + 1]) | ((uint32_t)pk_row_hi8(v[4 * q + 2], v[4 * q + 3]) << 16);
-            }
-        }
-    } else {
-        if constexpr (sizeof(Px) == 2) {
-            reinterpret_cast<uint32_t *>(w0)[3] = pk_row_lo(v[6], v[7]);
-            reinterpret_cast<uint32_t *>(w0)[4] = pk_row_lo(v[8], v[9]);
-            reinterpret_cast<uint32_t *>(w1)[3] = pk_row_hi(v[6], v[7]);
-            reinterpret_cast<uint32_t *>(w1)[4] = pk_row_hi(v[8], v[9]);
-        } else {
-            reinterpret_cast<uint16_t *>(w0)[3] = pk_row_lo8(v[6], v[7]);
-            reinterpret_cast<uint16_t *>(w0)[4] = pk_row_lo8(v[8], v[9]);
-            reinterpret_cast<uint16_t *>(w1)[3] = pk_row_hi8(v[6], v[7]);
-            reinterpret_cast<uint16_t *>(w1)[4] = pk_row_hi8(v[8], v[9]);
-        }
-    }
-}
-
-template <int WD, typename Px>
-__device__ __forceinline__ void seg_row_pair(Px *ring, const uint16_t *list, int i, int eb, const uint8_t *le,
-                                             const uint8_t *li, int bdm8, int bdmax) {
-    constexpr int P = kLfCols;
-    constexpr int nr = WD == 16 ? 7 : WD == 8 ? 4 : WD == 6 ? 3 : 2;   // rows read each side
-    constexpr int lo = WD == 16 ? 2 : WD == 8 ? 5 : 6;                 // rows [lo, 16 - lo) written
-    const int e = list[i >> 1];
-    const int u = e >> 6, L = e & 63;
-    const int ey = eb + 4 * (u / (kLfTW / 4)), col = 16 + (u % (kLfTW / 4)) * 4 + 2 * (i & 1);
-    lf_s2 v[16];
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        v[j] = pk_splat(0);
-        if (j >= 8 - nr && j < 8 + nr) {
-            const Px *w = &ring[((ey - 8 + j) & (kSegRing - 1)) * P + col];
-            if constexpr (sizeof(Px) == 2)
-                v[j] = __builtin_bit_cast(lf_s2, *reinterpret_cast<const uint32_t *>(w));
-            else
-                v[j] = __builtin_bit_cast(lf_s2, __builtin_amdgcn_perm(0u, (uint32_t)*reinterpret_cast<const uint16_t *>(w), 0x0c010c00u));
-        }
-    }
-    filter_pk<WD>(v, le[L], li[L], L >> 4, bdm8, bdmax);
-#pragma unroll
-    for (int j = lo; j < 16 - lo; j++) {
-        Px *w = &ring[((ey - 8 + j) & (kSegRing - 1)) * P + col];
-        if constexpr (sizeof(Px) == 2)
-            *reinterpret_cast<uint32_t *>(w) = __builtin_bit_cast(uint32_t, v[j]);
-        else
-            *reinterpret_cast<uint16_t *>(w) = (uint16_t)__builtin_amdgcn_perm(0u, __builtin_bit_cast(uint32_t, v[j]), 0x0c0c0200u);
-    }
-}
-
-// the four width classes of one direction as 64-pair chunks dealt to the waves (lf_dir_pk)
-template <bool COLS, typename Px>
-__device__ __forceinline__ void seg_dir(Px *ring, const uint16_t (*lists)[COLS ? kSegNV : kSegNH], const int *cnt,
-                                        int base_row, const uint8_t *le, const uint8_t *li, int bdm8, int bdmax,
-                                        int tid) {
-    const int wave = tid >> 6, lane = tid & 63;
-    const int c0 = (cnt[0] * 2 + 63) >> 6, c1 = c0 + ((cnt[1] * 2 + 63) >> 6);
-    const int c2 = c1 + ((cnt[2] * 2 + 63) >> 6), c3 = c2 + ((cnt[3] * 2 + 63) >> 6);
-    for (int g = wave; g < c3; g += kLfSegThreads / 64) {
-        const int cls = g < c0 ? 0 : g < c1 ? 1 : g < c2 ? 2 : 3;
-        const int base = cls == 0 ? 0 : cls == 1 ? c0 : cls == 2 ? c1 : c2;
-        const int i = (g - base) * 64 + lane;
-        if (i >= cnt[cls] * 2) continue;
-        switch (cls) {
-#define SEG_CASE(k, wd)                                                                          \
-        case k:                                                                                  \
-            if constexpr (COLS) seg_col_pair<wd, Px>(ring, lists[k], i, base_row, le, li, bdm8, bdmax); \
-            else seg_row_pair<wd, Px>(ring, lists[k], i, base_row, le, li, bdm8, bdmax);          \
-            break;
-        SEG_CASE(0, 4) SEG_CASE(1, 6) SEG_CASE(2, 8) SEG_CASE(3, 16)
-#undef SEG_CASE
-        }
-    }
-}
-
-// The pixels of chunk rows [E + 16, E + 48) (columns x0-16 .. x0+79, 0 outside the plane or
-// at rows >= lim) and the edge units of step E: the column edges of those rows and the row
-// edges e in [E, E + 32) that the segment [ys, ye) needs. Independent loads only.
-template <typename Px, int NS, int NU>
-__device__ __forceinline__ void seg_fetch(const LfTileArgs &a, int p, const uint8_t *src, int64_t st, int x0, int pw,
-                                          int lim, int ys, int ye, int E, uint4 (&sv)[NS], LfEdgeRaw (&raw)[NU],
-                                          int tid) {
-    constexpr int VPX = 16 / sizeof(Px), VPR = kLfCols / VPX;
-    const int c0 = E + 16, ux0 = (x0 >> 2) - 1;
-#pragma unroll
-    for (int j = 0; j < NS; j++) {
-        const int i = tid + kLfSegThreads * j;
-        const int r = i / VPR, c = (i % VPR) * VPX;
-        const int y = c0 + r, x = x0 - 16 + c;
-        sv[j] = make_uint4(0, 0, 0, 0);
-        if (i < 32 * VPR && y >= 0 && y < lim && x >= 0 && x < pw)
-            sv[j] = *reinterpret_cast<const uint4 *>(src + (int64_t)y * st + (int64_t)x * sizeof(Px));
-    }
-#pragma unroll
-    for (int j = 0; j < NU; j++) {
-        const int i = tid + kLfSegThreads * j;
-        raw[j].bit = 0;
-        if (i < kSegNV) {
-            raw[j] = lf_edge_fetch(a, p, 0, ux0 + i % kLfEdgesV, (c0 >> 2) + i / kLfEdgesV);
-        } else if (i < kSegNU) {
-            const int u = i - kSegNV, e = E + 4 * (u / (kLfTW / 4));
-            if (e >= ys - 4 && e <= ye + 4) raw[j] = lf_edge_fetch(a, p, 1, (x0 >> 2) + u % (kLfTW / 4), e >> 2);
-        }
-    }
-}
-
-#ifndef MI_LF_SEG_MINW
-#define MI_LF_SEG_MINW 5
-#endif
-template <typename Px>
-__global__ __launch_bounds__(kLfSegThreads, MI_LF_SEG_MINW) void lf_seg_kernel(LfTileArgs a) {
-    constexpr int P = kLfCols;
-    constexpr int VPX = 16 / sizeof(Px), VPR = P / VPX;          // 16-B vectors per ring row
-    constexpr int NS = (32 * VPR + kLfSegThreads - 1) / kLfSegThreads;
-    constexpr int NU = (kSegNU + kLfSegThreads - 1) / kLfSegThreads;
-    constexpr int VPT = kLfTW / VPX;                              // output vectors per row
-    static_assert(kSegNV << 6 <= 65536 && kSegNH << 6 <= 65536, "work-list entries must fit 16 bits");
-    __shared__ __attribute__((aligned(16))) Px ring[kSegRing * P];
-    __shared__ uint16_t listv[4][kSegNV], listh[4][kSegNH];
-    __shared__ int cnt[8];
-    __shared__ uint8_t le[64], li[64];
-    KTL(0);
-    const int b = xcd_block(blockIdx.x, gridDim.x);
-    const int p = b < a.tile_start[1] ? 0 : b < a.tile_start[2] ? 1 : 2;
-    const int lb = b - a.tile_start[p];
-    const int x0 = (lb % a.tiles_x[p]) * kLfTW;
-    const int pw = a.pw[p], ph = a.ph[p];
-    const int ys = (lb / a.tiles_x[p]) * a.seg_h[p], ye = min(ys + a.seg_h[p], ph);
-    const int lim = min(ph, ye + 12);        // rows at or past lim are never read
-    const int64_t st = a.stride[p];
-    const uint8_t *src = a.src[p];
-    uint8_t *dst = a.dst[p];
-    if (threadIdx.x < 64) { le[threadIdx.x] = a.lim_e[threadIdx.x]; li[threadIdx.x] = a.lim_i[threadIdx.x]; }
-    const int ux0 = (x0 >> 2) - 1;
-    // registers: the pixels of chunk rows [c0, c0 + 32) and the step's edge units
-    uint4 sv[NS];
-    LfEdgeRaw raw[NU];
-    const int K = (ye - ys + 47) >> 5;       // steps -1 .. K-1: outputs [E - 16, E + 16) cover [ys, ye)
-    seg_fetch<Px, NS, NU>(a, p, src, st, x0, pw, lim, ys, ye, ys - 32, sv, raw, threadIdx.x);
-    for (int k = -1; k < K; k++) {
-        const int E = ys + 32 * k, c0 = E + 16;
-        // the lane index as a value of this iteration: nothing derived from it is hoisted out
-        // of the loop (LICM kept ~60 per-lane addresses live across the filters otherwise)
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        __syncthreads();                     // the previous step's stores have read the ring
-        // (a) chunk -> ring, counters reset
-#pragma unroll
-        for (int j = 0; j < NS; j++) {
-            const int i = tid + kLfSegThreads * j;
-            if (i < 32 * VPR)
-                *reinterpret_cast<uint4 *>(&ring[((c0 + i / VPR) & (kSegRing - 1)) * P + (i % VPR) * VPX]) = sv[j];
-        }
-        if (tid < 8) cnt[tid] = 0;
-        __syncthreads();
-        // (b) the step's edge units into the work lists
-#pragma unroll
-        for (int j = 0; j < NU; j++) {
-            const int i = tid + kLfSegThreads * j;
-            if (i >= kSegNU) continue;
-            const bool v = i < kSegNV;
-            const int u = v ? i : i - kSegNV;
-            const int kk = v ? u % kLfEdgesV : 0;
-            const int code = v ? lf_edge_decode(raw[j], 0, ux0 + kk, 0)
-                               : lf_edge_decode(raw[j], 1, 0, (E >> 2) + u / (kLfTW / 4));
-            const int wd = code >> 8;
-            if (!wd || (v && (kk == 0 || kk == kLfEdgesV - 1) && wd != 16)) continue;
-            const int c = lf_class(wd);
-            const int slot = atomicAdd(&cnt[(v ? 0 : 4) + c], 1);
-            (v ? listv[c] : listh[c])[slot] = (uint16_t)((u << 6) | (code & 63));
-        }
-        // (c) the next step's chunk and units, in flight while this step filters
-        if (k + 1 < K) seg_fetch<Px, NS, NU>(a, p, src, st, x0, pw, lim, ys, ye, E + 32, sv, raw, tid);
-        __syncthreads();
-        if (k == -1) KTL(1);
-        // (d) column edges of the chunk, (e) the step's row edges
-        seg_dir<true, Px>(ring, listv, cnt, c0, le, li, a.bdm8, a.bdmax, tid);
-        __syncthreads();
-        seg_dir<false, Px>(ring, listh, cnt + 4, E, le, li, a.bdm8, a.bdmax, tid);
-        __syncthreads();
-        // (f) rows [E - 16, E + 16) are final
-        for (int i = tid; i < 32 * VPT; i += kLfSegThreads) {
-            const int y = E - 16 + i / VPT, c = (i % VPT) * VPX;
-            if (y >= ys && y < ye && x0 + c < pw)
-                *reinterpret_cast<uint4 *>(dst + (int64_t)y * st + (int64_t)(x0 + c) * sizeof(Px)) =
-                    *reinterpret_cast<const uint4 *>(&ring[(y & (kSegRing - 1)) * P + 16 + c]);
-        }
-    }
-    KTL(5);
-}
-
-int launch_deblock_segs(const LfTileArgs &a, int bpc, hipStream_t s) {
-    const int n = a.tile_start[3];
-    if (!n) return 0;
-    if (bpc == 8) hipLaunchKernelGGL(lf_seg_kernel<uint8_t>, dim3(n), dim3(kLfSegThreads), 0, s, a);
-    else hipLaunchKernelGGL(lf_seg_kernel<uint16_t>, dim3(n), dim3(kLfSegThreads), 0, s, a);
-    return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 int launch_deblock_tiles(const LfTileArgs &a, int bpc, hipStream_t s) {
