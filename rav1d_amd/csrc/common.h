@@ -96,7 +96,7 @@ __host__ __device__ constexpr int itx_lanes(int tx) {
     return imax_c(imin_c(tx_dim(tx).h, 32), tx_dim(tx).w);
 }
 #ifndef MI_ITX_THREADS
-#define MI_ITX_THREADS 256
+#define MI_ITX_THREADS 64   // one-wave workgroups: 4K10 itx 34.1 -> 30.2 us (no cross-wave barriers; r04)
 #endif
 constexpr int kItxThreads = MI_ITX_THREADS;
 __host__ __device__ constexpr int itx_blocks_per_wg(int tx) { return kItxThreads / itx_lanes(tx); }
@@ -139,6 +139,16 @@ struct ItxArgs {
     // the band is fetched into, and written back from, one XCD's L2 whichever sizes touch it
     int band_start[19][9];
     int nbands;         // 1 or 8
+    // rounds (banded grid): the grid runs in nrounds rounds; round r holds, for every size in
+    // launch order, the band workgroups k in [r*m/R, (r+1)*m/R) (m = m_size[size], the size's
+    // workgroups per band). With each (size, band) list ordered by sub-band (one of R per band)
+    // first, round r covers about sub-band r of every band with all sizes, so the blocks of
+    // different sizes sharing a pixel line run close in time and the line is read and written
+    // back once instead of once per size (partially written lines evicted between sizes cost
+    // 1.75x the algorithmic writes at 4K10)
+    int nrounds;
+    int m_size[19];
+    int round_start[17];
     int pw[3], ph[3];   // plane extents (128-aligned picture area; 0 = no such plane)
     int *err;           // device error word: set when a descriptor is rejected
 };
@@ -155,6 +165,12 @@ __host__ __device__ constexpr uint32_t itx_legal_types(int tx) {
 // then the 32-point sizes, then every size with both sides <= 16
 constexpr int kItxLaunchOrder[19] = { 4, 11, 12, 17, 18, 3, 9, 10, 15, 16, 0, 1, 2, 5, 6, 7, 8, 13, 14 };
 constexpr int kItxBands = 8;
+#ifndef MI_ITX_NROUNDS
+#define MI_ITX_NROUNDS 1   // rounds of the banded grid (1: sizes one after the other; 4 or 8 cut HBM
+                           // traffic 96 -> 82 MB at 4K10 but ran 20 % slower: sizes interleaved)
+#endif
+constexpr int kItxRounds = MI_ITX_NROUNDS;
+static_assert(kItxRounds >= 1 && kItxRounds <= 16, "rounds");
 // fills wg_start / wg_size / blk_start (and the band table when band_start, [19][9], is given);
 // returns the grid size
 int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start, const uint32_t *band_start = nullptr);

@@ -789,18 +789,20 @@ void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
     uint32_t (&itx_bs)[MI_N_RECT_TX_SIZES][MI_ITX_BANDS + 1] = pl.itx_bs;
     memset(itx_bs, 0, sizeof(itx_bs));
     {
-        constexpr int NK = MI_N_RECT_TX_SIZES * MI_ITX_BANDS;
+        // (tx size, band, sub-band): sub-band r of a band goes with round r of the grid
+        constexpr int NF = MI_ITX_BANDS * mi::kItxRounds;         // fine bands per plane
+        constexpr int NK = MI_N_RECT_TX_SIZES * NF;
         const int ah = (f->h + 127) & ~127, ssv = f->layout == 1;
         auto key = [&](const MiTxBlock &b) {
             const int ph = b.plane ? ah >> ssv : ah;
-            const int q = (int)((int64_t)b.y * MI_ITX_BANDS / ph);
-            return (int)b.tx * MI_ITX_BANDS + (q < MI_ITX_BANDS - 1 ? q : MI_ITX_BANDS - 1);
+            const int q = (int)((int64_t)b.y * NF / ph);
+            return (int)b.tx * NF + (q < NF - 1 ? q : NF - 1);
         };
-        uint32_t start[NK + 1] = {};
+        std::vector<uint32_t> start(NK + 1, 0);
         for (int i = 0; i < f->n_inter_tx; i++) start[key(f->inter_tx[i]) + 1]++;
         for (int k = 0; k < NK; k++) start[k + 1] += start[k];
         for (int t = 0; t < MI_N_RECT_TX_SIZES; t++)
-            for (int q = 0; q <= MI_ITX_BANDS; q++) itx_bs[t][q] = start[t * MI_ITX_BANDS + q];
+            for (int q = 0; q <= MI_ITX_BANDS; q++) itx_bs[t][q] = start[t * NF + q * mi::kItxRounds];
         for (int i = 0; i < f->n_inter_tx; i++) itx_b[start[key(f->inter_tx[i])]++] = f->inter_tx[i];
     }
 }

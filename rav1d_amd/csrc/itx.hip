@@ -75,6 +75,17 @@ __device__ __forceinline__ typename Vec4<Px>::T pack4(const int *o) {
     }
 }
 
+// An int of the kernel-argument struct at a run-time byte offset: a scalar load from the
+// kernarg segment. Indexing the by-value ItxArgs with a run-time index would copy it to
+// scratch, and the compile-time-index selects used before kept every table entry live in SGPRs
+// (hundreds of SGPR spills); this reads only the entries a workgroup needs.
+__device__ __forceinline__ int karg_i32(size_t off) {
+    typedef const int __attribute__((address_space(4))) *CI;
+    typedef const char __attribute__((address_space(4))) *CC;
+    return *(CI)((CC)__builtin_amdgcn_kernarg_segment_ptr() + off);
+}
+#define KARG(field, idx) karg_i32(offsetof(ItxArgs, field) + 4 * (size_t)(idx))
+
 // a[i] for i in 0..2 as selects (a dynamic index into the kernel-argument struct would make
 // the compiler copy the whole struct to scratch)
 template <typename T> __device__ __forceinline__ T sel3(const T (&v)[3], int i) { return i == 0 ? v[0] : i == 1 ? v[1] : v[2]; }
@@ -101,11 +112,8 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     if (a.nbands > 1) {
         const int q = lwg & 7;
         k = lwg >> 3;
-        bs = a.band_start[TX][0];
-        be = a.band_start[TX][1];
-#pragma unroll
-        for (int i = 1; i < 8; i++)
-            if (q == i) { bs = a.band_start[TX][i]; be = a.band_start[TX][i + 1]; }
+        bs = KARG(band_start, TX * 9 + q);
+        be = KARG(band_start, TX * 9 + q + 1);
     }
     // per-plane arguments as locals (selected by value, never by address into the kernarg)
     uint8_t *const plane3[3] = { a.plane[0], a.plane[1], a.plane[2] };
@@ -328,11 +336,8 @@ __device__ __forceinline__ void itx_size64(const ItxArgs &a, int lwg, Lt *lds) {
     if (a.nbands > 1) {
         const int q = lwg & 7;
         k = lwg >> 3;
-        bs = a.band_start[TX][0];
-        be = a.band_start[TX][1];
-#pragma unroll
-        for (int i = 1; i < 8; i++)
-            if (q == i) { bs = a.band_start[TX][i]; be = a.band_start[TX][i + 1]; }
+        bs = KARG(band_start, TX * 9 + q);
+        be = KARG(band_start, TX * 9 + q + 1);
     }
     uint8_t *const plane3[3] = { a.plane[0], a.plane[1], a.plane[2] };
     const int64_t stride3[3] = { a.stride[0], a.stride[1], a.stride[2] };
@@ -497,11 +502,29 @@ __global__ __launch_bounds__(kItxThreads, MI_ITX_MINW) void itx_frame_kernel(Itx
 #endif
     // the size range holding this workgroup, with compile-time indices only (a runtime index
     // into the kernel-argument struct makes the compiler copy it to scratch)
-    int s = a.wg_size[0], base = a.wg_start[0];
-#pragma unroll
-    for (int k = 1; k < 19; k++)
-        if (wg >= a.wg_start[k]) { s = a.wg_size[k]; base = a.wg_start[k]; }
-    const int lwg = wg - base;
+    int s, lwg;
+    if (a.nrounds > 1) {
+        // round r, then the size within the round; lwg = 8 k + band (itx_size's convention)
+        int r = 0;
+        for (int i = 1; i < kItxRounds; i++)
+            if (wg >= KARG(round_start, i)) r = i;
+        int w = wg - KARG(round_start, r);
+        constexpr int R = kItxRounds;
+        int i = 0, k0 = 0;
+        for (;; i++) {
+            const int m = KARG(m_size, i), lo = r * m / R, n = 8 * ((r + 1) * m / R - lo);
+            if (w < n || i == 18) { k0 = lo; break; }
+            w -= n;
+        }
+        s = KARG(wg_size, i);
+        lwg = 8 * k0 + w;
+    } else {
+        int i = 0;
+        for (int k = 1; k < 19; k++)
+            if (wg >= KARG(wg_start, k)) i = k;
+        s = KARG(wg_size, i);
+        lwg = wg - KARG(wg_start, i);
+    }
     switch (s) {
 #define CASE(n) case n: itx_size<n, Px, Cf, Lt, Wide>(a, lwg, lds); break;
         CASE(0) CASE(1) CASE(2) CASE(5) CASE(6) CASE(7) CASE(8) CASE(13) CASE(14)
@@ -540,12 +563,23 @@ int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start, const uint32_t *ba
                 m = std::max(m, (n + per_wg - 1) / per_wg);
             }
             wg += kItxBands * m;
+            a.m_size[i] = m;
         } else {
             const int n = (int)(size_start[sz + 1] - size_start[sz]);
             wg += (n + per_wg - 1) / per_wg;
         }
     }
     a.wg_start[19] = wg;
+    a.nrounds = band_start && !MI_ITX_PERSIST ? kItxRounds : 1;
+    if (a.nrounds > 1) {
+        int acc = 0;
+        for (int r = 0; r < a.nrounds; r++) {
+            a.round_start[r] = acc;
+            for (int i = 0; i < 19; i++)
+                acc += kItxBands * ((r + 1) * a.m_size[i] / a.nrounds - r * a.m_size[i] / a.nrounds);
+        }
+        a.round_start[a.nrounds] = acc;   // == wg
+    }
     for (int k = 0; k <= 19; k++) a.blk_start[k] = (int)size_start[k];
     if (band_start)
         for (int s = 0; s < 19; s++)
