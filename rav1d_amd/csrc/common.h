@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <type_traits>
 #include "../../include/mi_av1dsp.h"
 
 // Kernel timelines (diagnostic builds only, -DMI_KTL): lane 0 of every workgroup stores
@@ -38,6 +39,21 @@
 #endif
 
 namespace mi {
+
+// A field of the kernel-argument struct (the kernel's only argument) at a run-time byte
+// offset: a scalar load from the kernarg segment. Indexing a by-value argument struct with a
+// run-time index makes the compiler copy it to scratch, and compile-time selects keep every
+// candidate live in SGPRs; this loads only the entry the workgroup needs.
+template <typename T>
+__device__ __forceinline__ T karg_at(size_t off) {
+    typedef const T __attribute__((address_space(4))) *CT;
+    typedef const char __attribute__((address_space(4))) *CC;
+    return *(CT)((CC)__builtin_amdgcn_kernarg_segment_ptr() + off);
+}
+// field[idx] of the argument struct S
+#define KARG_OF(S, field, idx) \
+    ::mi::karg_at<typename std::remove_cv<typename std::remove_reference<decltype(((S *)0)->field[0])>::type>::type>( \
+        offsetof(S, field) + sizeof(((S *)0)->field[0]) * (size_t)(idx))
 
 // The dispatcher hands workgroup b to XCD b % 8 (MI355X: 8 XCDs, each with its own 4 MB L2).
 // xcd_block renumbers the grid so that XCD k walks one contiguous chunk of the work list:

@@ -127,14 +127,18 @@ __device__ void grain_ar_all(int16_t (*lut)[kGH][kGW], const MiFilmGrainData &d,
                     }
                 }
             }
-            int sum = 0, ci = 0;
+            // four partial sums: the step's critical path is the multiply-add chain, so it is
+            // cut from NT dependent adds to NT / 4 + 2
+            int part[4] = { 0, 0, 0, 0 }, ci = 0;
 #pragma unroll
             for (int dy = -LAG; dy <= 0; dy++)
 #pragma unroll
                 for (int dx = -LAG; dx <= LAG; dx++) {
                     if (dy == 0 && dx == 0) break;
-                    sum += coef[ci++] * (dy < 0 ? wv[dy + LAG][dx + LAG] : cv[dx + LAG]);
+                    part[ci & 3] += coef[ci] * (dy < 0 ? wv[dy + LAG][dx + LAG] : cv[dx + LAG]);
+                    ci++;
                 }
+            int sum = (part[0] + part[1]) + (part[2] + part[3]);
             if (lterm) {
                 const int lx = ((x - 3) << subx) + 3, ly = ((y - 3) << suby) + 3;
                 const int16_t *q = &lut[0][ly][lx];
@@ -152,95 +156,6 @@ __device__ void grain_ar_all(int16_t (*lut)[kGH][kGW], const MiFilmGrainData &d,
             }
         }
         __syncthreads();
-    }
-}
-
-// The same auto-regression with one wave per plane and two template rows per lane (luma: 70
-// filtered rows in 35 lanes), so a step needs no workgroup barrier: lane k's rows read rows
-// written by lane k-1 (or by itself) in earlier steps, and a wave's LDS accesses complete in
-// program order. Each lane's two rows run the skewed wavefront of grain_ar_all (row y lags row
-// y-1 by LAG+1 columns). The chroma waves follow the luma wave through an LDS progress word:
-// chroma step tc reads luma samples finished by luma step (tc << subx) + subx + (suby ? LAG+1 : 0).
-// Per step: the new column x+LAG of each row above (LDS), 2 x NT multiply-adds, two LDS stores.
-template <int LAG>
-__device__ void grain_ar_wave(int16_t (*lut)[kGH][kGW], const MiFilmGrainData &d, bool ly, bool uv0, bool uv1,
-                              int cw, int chh, int subx, int suby, int gmin, int gmax, int *prog) {
-    constexpr int NT = 2 * LAG * LAG + 2 * LAG, S = LAG + 1;
-    constexpr int WA = LAG, WC = 2 * LAG + 1;
-    const int role = threadIdx.x >> 6, lane = threadIdx.x & 63;   // role: wave-uniform
-    if (role > 2) return;
-    const bool on = role == 0 ? ly : role == 1 ? uv0 : uv1;
-    if (!on) return;
-    const int8_t *cg = role == 0 ? d.ar_coeffs_y : d.ar_coeffs_uv[role - 1];
-    int coef[NT + 1];
-#pragma unroll
-    for (int i = 0; i <= NT; i++) coef[i] = cg[i];
-    const int gw = role ? cw : kGW, gh = role ? chh : kGH;
-    const bool lterm = role && d.num_y_points;
-    const int shift = (int)d.ar_coeff_shift;
-    const int steps = (gw - 6) + S * (gh - 4);
-    const int lsteps = (kGW - 6) + S * (kGH - 4);
-    int16_t *buf = &lut[role][0][0];
-    const int ya = 3 + 2 * lane;
-    int wv[2][WA][WC], cv[2][WA];
-    bool primed[2] = { false, false };
-    for (int t = 0; t < steps; t++) {
-        if (role) {
-            // wait until the luma samples this step reads are final (one lane polls)
-            int need = (t << subx) + subx + (suby ? S : 0);
-            need = need < lsteps - 1 ? need : lsteps - 1;
-            if (lane == 0)
-                while (__hip_atomic_load(prog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
-                    __builtin_amdgcn_s_sleep(1);
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int y = ya + h;
-            const int x = 3 + t - S * (y - 3);
-            if (y < gh && x >= 3 && x < gw - 3) {
-                const int16_t *p = buf + y * kGW + x;
-                if (!primed[h]) {
-#pragma unroll
-                    for (int r = 0; r < LAG; r++)
-#pragma unroll
-                        for (int c = 0; c < WC; c++) wv[h][r][c] = p[(r - LAG) * kGW + c - LAG];
-#pragma unroll
-                    for (int c = 0; c < LAG; c++) cv[h][c] = p[c - LAG];
-                    primed[h] = true;
-                } else {
-#pragma unroll
-                    for (int r = 0; r < LAG; r++) {
-#pragma unroll
-                        for (int c = 0; c < WC - 1; c++) wv[h][r][c] = wv[h][r][c + 1];
-                        wv[h][r][WC - 1] = p[(r - LAG) * kGW + LAG];
-                    }
-                }
-                int sum = 0, ci = 0;
-#pragma unroll
-                for (int dy = -LAG; dy <= 0; dy++)
-#pragma unroll
-                    for (int dx = -LAG; dx <= LAG; dx++) {
-                        if (dy == 0 && dx == 0) break;
-                        sum += coef[ci++] * (dy < 0 ? wv[h][dy + LAG][dx + LAG] : cv[h][dx + LAG]);
-                    }
-                if (lterm) {
-                    const int lx = ((x - 3) << subx) + 3, lyy = ((y - 3) << suby) + 3;
-                    const int16_t *q = &lut[0][lyy][lx];
-                    int l = q[0];
-                    if (subx) l += q[1];
-                    if (suby) { l += q[kGW]; if (subx) l += q[kGW + 1]; }
-                    sum += round2i(l, subx + suby) * coef[NT];
-                }
-                const int g = min(max(p[0] + round2i(sum, shift), gmin), gmax);
-                buf[y * kGW + x] = (int16_t)g;
-#pragma unroll
-                for (int c = 0; c < LAG - 1; c++) cv[h][c] = cv[h][c + 1];
-                cv[h][LAG - 1] = g;
-            }
-        }
-        if (role == 0 && lane == 0) __hip_atomic_store(prog, t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
@@ -267,7 +182,6 @@ __device__ int scaling_entry(const uint8_t (*pts)[2], int num, int e, int shx) {
 
 __global__ __launch_bounds__(kPrepThreads) void fg_prep_kernel(FgArgs a) {
     __shared__ int16_t lut[3][kGH][kGW];
-    __shared__ int prog[1];
     const MiFilmGrainData &d = a.data;
     const int bdm8 = a.bpc - 8;
     const int shift = 4 - bdm8 + d.grain_scale_shift;
@@ -281,24 +195,13 @@ __global__ __launch_bounds__(kPrepThreads) void fg_prep_kernel(FgArgs a) {
     grain_fill_all(lut, d.seed, shift, ly, uv0, uv1, cw, chh);
     if (!ly)
         for (int i = threadIdx.x; i < kGH * kGW; i += kPrepThreads) (&lut[0][0][0])[i] = a.lut_y[i];
-    if (threadIdx.x == 0) *prog = ly ? -1 : 1 << 30;   // luma progress (caller's luma: final)
     __syncthreads();
-#ifndef MI_FG_AR_WAVE
-#define MI_FG_AR_WAVE 0
-#endif
     switch (d.ar_coeff_lag) {
     case 0: grain_ar_all<0>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
-#if MI_FG_AR_WAVE
-    case 1: grain_ar_wave<1>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1, prog); break;
-    case 2: grain_ar_wave<2>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1, prog); break;
-    default: grain_ar_wave<3>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1, prog); break;
-#else
     case 1: grain_ar_all<1>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
     case 2: grain_ar_all<2>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
     default: grain_ar_all<3>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
-#endif
     }
-    __syncthreads();
     // export templates
     for (int i = threadIdx.x; i < 3 * kGH * kGP; i += kPrepThreads) {
         const int r = i / kGP, c = i - r * kGP;

@@ -236,7 +236,7 @@ __device__ __forceinline__ LfEdgeRaw lf_edge_fetch(const LfTileArgs &a, int p, i
     int half = 0;
     unsigned bit = 0;
     if (dir == 0) {
-        if (ux >= a.cols_ux[p] || uy * 4 >= a.cols_rows[p]) return r;
+        if (ux >= KARG_OF(LfTileArgs, cols_ux, p) || uy * 4 >= KARG_OF(LfTileArgs, cols_rows, p)) return r;
         if (p == 0) {
             const int X = ux >> 5, x = ux & 31, Y = uy >> 5, yy = uy & 31;
             half = yy >> 4;
@@ -254,7 +254,7 @@ __device__ __forceinline__ LfEdgeRaw lf_edge_fetch(const LfTileArgs &a, int p, i
             m = &a.masks[Y * a.sb128w + X].filter_uv[0][x][0][0];
         }
     } else {
-        if (ux * 4 >= a.rows_px[p] || uy >= a.rows_uy[p]) return r;
+        if (ux * 4 >= KARG_OF(LfTileArgs, rows_px, p) || uy >= KARG_OF(LfTileArgs, rows_uy, p)) return r;
         if (p == 0) {
             const int X = ux >> 5, xx = ux & 31, Y = uy >> 5, y = uy & 31;
             half = xx >> 4;
@@ -618,7 +618,12 @@ template <typename Px>
 __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
     constexpr int VB = 16;                        // bytes per vector
     constexpr int VPX = VB / sizeof(Px);          // pixels per vector
-    constexpr int P = kLfCols;                    // LDS pitch in pixels
+#ifndef MI_LF_PITCH
+#define MI_LF_PITCH kLfCols   // (+8 px of padding cut the LDS bank conflicts 3.15 -> 2.2 M cycles but ran 31 vs 29 us)
+#endif
+    // LDS pitch in pixels (the staged kLfCols)
+    constexpr int P = MI_LF_PITCH;
+    static_assert(P % 8 == 0 && P >= kLfCols, "16-B aligned rows");
     constexpr int NV = (kLfRows / 4) * kLfEdgesV; // column-edge units (4 lines each)
     constexpr int NH = kLfEdgesH * (kLfTW / 4);   // row-edge units
     __shared__ __attribute__((aligned(16))) Px t[kLfRows * P];
@@ -630,11 +635,14 @@ __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
     const int tid = threadIdx.x;
     const int b = xcd_block(blockIdx.x, gridDim.x);
     const int p = b < a.tile_start[1] ? 0 : b < a.tile_start[2] ? 1 : 2;
-    const int lb = b - a.tile_start[p];
-    const int x0 = (lb % a.tiles_x[p]) * kLfTW, y0 = (lb / a.tiles_x[p]) * kLfTH;
-    const int pw = a.pw[p], ph = a.ph[p];
-    const int64_t st = a.stride[p];
-    const uint8_t *src = a.src[p];
+    // the plane's fields by kernarg offset (KARG_OF): selecting among the three copies kept
+    // every per-plane field in SGPRs (78 SGPRs: 7 instead of 8 waves' worth per CU)
+    const int lb = b - KARG_OF(LfTileArgs, tile_start, p);
+    const int tx = KARG_OF(LfTileArgs, tiles_x, p);
+    const int x0 = (lb % tx) * kLfTW, y0 = (lb / tx) * kLfTH;
+    const int pw = KARG_OF(LfTileArgs, pw, p), ph = KARG_OF(LfTileArgs, ph, p);
+    const int64_t st = KARG_OF(LfTileArgs, stride, p);
+    const uint8_t *src = KARG_OF(LfTileArgs, src, p);
     KTL(0);
     if (tid < 64) { le[tid] = a.lim_e[tid]; li[tid] = a.lim_i[tid]; }
     if (tid < 8) cnt[tid] = 0;
@@ -642,7 +650,7 @@ __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
     // Stage rows y0-12 .. y0+75, columns x0-16 .. x0+79 (pixels outside the plane read as 0:
     // no edge reaches them), and fetch every edge unit's mask and level words. All of these
     // loads are independent and issued before any is used.
-    constexpr int VPR = P / VPX;                  // vectors per staged row
+    constexpr int VPR = kLfCols / VPX;            // vectors per staged row
     constexpr int NS = (kLfRows * VPR + kLfThreads - 1) / kLfThreads;
     constexpr int NU = (NV + NH + kLfThreads - 1) / kLfThreads;
     static_assert((NV > NH ? NV : NH) << 6 <= 65536, "work-list entries (unit << 6 | level) must fit 16 bits");
@@ -705,7 +713,7 @@ __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
 #endif
     __syncthreads();
     KTL(4);
-    uint8_t *dst = a.dst[p];
+    uint8_t *dst = KARG_OF(LfTileArgs, dst, p);
     constexpr int VPT = kLfTW / VPX;
     for (int i = tid; i < kLfTH * VPT; i += kLfThreads) {
         const int r = i / VPT, c = (i % VPT) * VPX;

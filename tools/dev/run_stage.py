@@ -1,0 +1,29 @@
+"""One bench stage (STAGE=deblock|cdef|lr|mc|itx) of the 4K10 bench frame, REPS times, for PMC
+passes (diagnostic). The pipeline runs once first so every input is the real one."""
+import os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import ctypes
+import torch
+import bench
+from rav1d_amd import frame as F
+from rav1d_amd.synth import make_frame
+fr = make_frame(3840, 2160, 10, 1, seed=0x4C100001, with_fg=False, with_mc=True)
+ctx = F.Context(0)
+pipe = bench.Pipeline(ctx, fr, ring=2)
+s = torch.cuda.current_stream()
+pipe.step(s)
+torch.cuda.synchronize()
+L = F.lib()
+st = os.environ.get("STAGE", "deblock")
+sp = F._stream_ptr(s)
+pa, pb, po, pd = pipe.A.picture(), pipe.B.picture(), pipe.O.picture(), pipe.D.picture()
+for _ in range(int(os.environ.get("REPS", "10"))):
+    if st == "deblock":
+        F.check(L.mi_deblock_frame_to(ctx.h, ctypes.byref(pa), ctypes.byref(pd), ctypes.byref(pipe.lf.s), sp), "lf")
+    elif st == "cdef":
+        F.check(L.mi_cdef_frame(ctx.h, ctypes.byref(pd), ctypes.byref(pb), ctypes.byref(pipe.cdef.s), sp), "cdef")
+    elif st == "lr":
+        F.check(L.mi_lr_frame(ctx.h, ctypes.byref(pb), ctypes.byref(pd), ctypes.byref(po), ctypes.byref(pipe.lr.s), sp), "lr")
+torch.cuda.synchronize()
+print("done")
