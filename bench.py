@@ -244,6 +244,10 @@ def film_grain_8k(ctx, stream, reps=20):
     torch.cuda.synchronize()
     prep_t, apply_t = 0.0, 0.0
     for _ in range(reps):
+        # a short spin kernel first keeps the stream busy while the host enqueues, so the event
+        # pairs time the kernels and not the host's launch latency
+        with torch.cuda.stream(stream):
+            torch.cuda._sleep(200000)
         ev[0].record(stream)
         F.check(lib.mi_film_grain_prep(ctx.h, ctypes.byref(ps), ctypes.byref(d), sp), "fg prep")
         ev[1].record(stream)

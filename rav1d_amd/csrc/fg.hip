@@ -15,6 +15,8 @@
 // offsets are read through L1/L2 (cache resident), the scaling LUT from LDS.
 #include "common.h"
 
+MI_KTL_DEFINE(fg)
+
 namespace mi {
 
 __constant__ int16_t k_gauss[2048] = {
@@ -24,7 +26,7 @@ __constant__ uint16_t k_lfsr_jump[256][16];   // M^(24*i) as 16 column vectors
 
 constexpr int kGW = 82, kGH = 73, kDrawsPerLane = 24;
 constexpr int kGP = 88;             // pitch of the exported templates (16-byte rows for vector loads)
-constexpr int kPrepThreads = 384;   // prep: 3 x 128 lanes (luma, U, V template rows)
+constexpr int kPrepThreads = 448;   // prep: 7 waves (AR: luma, U, V; scaling LUTs: 4)
 
 __device__ __forceinline__ unsigned lfsr_step(unsigned s) {
     const unsigned bit = (s ^ (s >> 1) ^ (s >> 3) ^ (s >> 12)) & 1;
@@ -71,96 +73,8 @@ __device__ void grain_fill_all(int16_t (*lut)[kGH][kGW], unsigned seed, int shif
     }
 }
 
-// Luma and both chroma templates in one skewed wavefront: threads 0-127 own luma rows,
-// 128-255 U rows, 256-383 V rows. Chroma sample (r, c) needs the luma samples under it final;
-// luma (Y, X) is final after step (X - 3) + skew (Y - 3), so the chroma wavefront can start
-// t0 = 1 + max over (r, c) of [last luma step it reads - its own step] steps after the luma
-// one, instead of after the whole luma template (8K10 4:2:0, lag 3: 353 steps, not 526).
-template <int LAG>
-__device__ void grain_ar_all(int16_t (*lut)[kGH][kGW], const MiFilmGrainData &d, bool ly, bool uv0, bool uv1,
-                             int cw, int chh, int subx, int suby, int gmin, int gmax) {
-    constexpr int NT = 2 * LAG * LAG + 2 * LAG, skew = LAG + 1;
-    const int role = threadIdx.x >> 7, lane = threadIdx.x & 127;   // role: wave-uniform
-    const int8_t *cg = role == 0 ? d.ar_coeffs_y : d.ar_coeffs_uv[role - 1];
-    int coef[NT + 1];
-#pragma unroll
-    for (int i = 0; i <= NT; i++) coef[i] = cg[i];
-    const int gw = role ? cw : kGW, gh = role ? chh : kGH;
-    const bool on = role == 0 ? ly : role == 1 ? uv0 : uv1;
-    const bool own = on && lane < gh - 3;
-    const bool lterm = role && d.num_y_points;
-    const int shift = (int)d.ar_coeff_shift;
-    const int cmax = cw - 7, rmax = chh - 4;
-    const int t0 = 1 + cmax * ((1 << subx) - 1) + subx + skew * (rmax * ((1 << suby) - 1) + suby);
-    const int lsteps = (kGW - 6) + skew * (kGH - 4);
-    const int csteps = (cw - 6) + skew * (chh - 4);
-    const int steps = max(lsteps, uv0 || uv1 ? t0 + csteps : 0);
-    const int tstart = role ? t0 : 0;
-    int16_t *buf = &lut[role][0][0];
-    const int y = 3 + lane;
-    // The lane's neighbourhood slides one column per step: rows y-LAG .. y-1 over columns
-    // x-LAG .. x+LAG and its own row's last LAG outputs live in registers, so a step reads
-    // only the new column x+LAG of the rows above (final: those rows run skew = LAG+1 columns
-    // ahead) instead of all NT neighbours.
-    constexpr int WA = LAG ? LAG : 1, WC = 2 * LAG + 1;
-    int wv[WA][WC], cv[WA];
-    bool primed = false;
-    for (int t = 0; t < steps; t++) {
-        const int x = 3 + (t - tstart) - skew * lane;
-        if (own && x >= 3 && x < gw - 3) {
-            const int16_t *p = buf + y * kGW + x;
-            if constexpr (LAG > 0) {
-                if (!primed) {
-#pragma unroll
-                    for (int r = 0; r < LAG; r++)
-#pragma unroll
-                        for (int c = 0; c < WC; c++) wv[r][c] = p[(r - LAG) * kGW + c - LAG];
-#pragma unroll
-                    for (int c = 0; c < LAG; c++) cv[c] = p[c - LAG];
-                    primed = true;
-                } else {
-#pragma unroll
-                    for (int r = 0; r < LAG; r++) {
-#pragma unroll
-                        for (int c = 0; c < WC - 1; c++) wv[r][c] = wv[r][c + 1];
-                        wv[r][WC - 1] = p[(r - LAG) * kGW + LAG];
-                    }
-                }
-            }
-            // four partial sums: the step's critical path is the multiply-add chain, so it is
-            // cut from NT dependent adds to NT / 4 + 2
-            int part[4] = { 0, 0, 0, 0 }, ci = 0;
-#pragma unroll
-            for (int dy = -LAG; dy <= 0; dy++)
-#pragma unroll
-                for (int dx = -LAG; dx <= LAG; dx++) {
-                    if (dy == 0 && dx == 0) break;
-                    part[ci & 3] += coef[ci] * (dy < 0 ? wv[dy + LAG][dx + LAG] : cv[dx + LAG]);
-                    ci++;
-                }
-            int sum = (part[0] + part[1]) + (part[2] + part[3]);
-            if (lterm) {
-                const int lx = ((x - 3) << subx) + 3, ly = ((y - 3) << suby) + 3;
-                const int16_t *q = &lut[0][ly][lx];
-                int l = q[0];
-                if (subx) l += q[1];
-                if (suby) { l += q[kGW]; if (subx) l += q[kGW + 1]; }
-                sum += round2i(l, subx + suby) * coef[NT];
-            }
-            const int g = min(max(p[0] + round2i(sum, shift), gmin), gmax);
-            buf[y * kGW + x] = (int16_t)g;
-            if constexpr (LAG > 0) {
-#pragma unroll
-                for (int c = 0; c < LAG - 1; c++) cv[c] = cv[c + 1];
-                cv[LAG - 1] = g;
-            }
-        }
-        __syncthreads();
-    }
-}
-
 // Closed form of generate_scaling (fg_apply.rs:14-72) for entry e.
-__device__ int scaling_coarse(const uint8_t (*pts)[2], int num, int k /* coarse index */) {
+__device__ __forceinline__ int scaling_coarse(const uint8_t (*pts)[2], int num, int k /* coarse index */) {
     if (k < pts[0][0]) return pts[0][1];
     if (k >= pts[num - 1][0]) return pts[num - 1][1];
     int i = 0;
@@ -169,7 +83,7 @@ __device__ int scaling_coarse(const uint8_t (*pts)[2], int num, int k /* coarse 
     const int delta = dy * ((0x10000 + (dx >> 1)) / dx);
     return by + ((0x8000 + (k - bx) * delta) >> 16);
 }
-__device__ int scaling_entry(const uint8_t (*pts)[2], int num, int e, int shx) {
+__device__ __forceinline__ int scaling_entry(const uint8_t (*pts)[2], int num, int e, int shx) {
     if (num == 0) return 0;
     const int k = e >> shx, n = e & ((1 << shx) - 1);
     const int base = scaling_coarse(pts, num, k);
@@ -178,6 +92,214 @@ __device__ int scaling_entry(const uint8_t (*pts)[2], int num, int e, int shx) {
     const int range = (next & 0xff) - (base & 0xff);
     const int r = ((1 << shx) >> 1) + n * range;
     return ((base & 0xff) + (r >> shx)) & 0xff;
+}
+
+// Luma and both chroma templates as three in-register wavefronts, one wave each (wave 0 luma,
+// 1 U, 2 V). Lane l owns template rows l and l + 64 (all rows, the three border rows included)
+// and runs column X of row y at step t = X + skew y (skew = lag + 1), every column of the row
+// from -lag on: border samples pass through (out = fill value), interior ones are filtered.
+// Then the samples a step needs from the rows above (column X + lag) were produced one step
+// earlier by lane l - 1, which holds them as int16 pairs: its last two outputs and, for the
+// rows further up, the pair its own window received lag steps before. One wave_ror:1 DPP per
+// window row moves a ready pair, the taps are v_dot2_i32_i16 over the pair rings (a register
+// ring per window row, indexed by the step: the step loop is unrolled to the ring period so
+// every index is a constant), and no barrier, LDS read or branch sits on the per-step path;
+// the step's own fill value (and the chroma's luma average) is read one step ahead. Chroma
+// sample (r, c) needs the luma samples under it final: the chroma waves run t0 = 1 + max over
+// (r, c) of [last luma step it reads - its own step] steps plus one barrier block behind the
+// luma one; the waves meet at one barrier per block of steps. The other waves fill the
+// scaling LUTs meanwhile, one entry per lane per block.
+__device__ __forceinline__ int dpp_from_prev_lane(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x13C /* wave_ror:1: lane l reads lane l - 1 */, 0xf, 0xf, false);
+}
+typedef short ar_s2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int dot2(int pair, int cpair, int acc) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(ar_s2, pair), __builtin_bit_cast(ar_s2, cpair), acc, false);
+}
+__device__ __forceinline__ int pk16(int lo, int hi) { return (int)__builtin_amdgcn_perm((unsigned)hi, (unsigned)lo, 0x05040100u); }
+constexpr int ar_unroll(int lag) { return lag == 3 ? 12 : 4; }   // lcm(window ring 2 lag, output ring 4)
+constexpr int ar_block(int lag) { return lag == 3 ? 24 : 16; }   // steps per barrier, a multiple of the unroll
+
+// AR coefficient i of plane pl (0 luma, 1 U, 2 V), read from the kernel-argument segment (a
+// role-indexed access into the by-value FgArgs makes the compiler copy it to scratch)
+__device__ __forceinline__ int ar_coef(int pl, int i) {
+    constexpr size_t y = offsetof(FgArgs, data) + offsetof(MiFilmGrainData, ar_coeffs_y);
+    constexpr size_t uv = offsetof(FgArgs, data) + offsetof(MiFilmGrainData, ar_coeffs_uv);
+    if (pl == 0) return i < 24 ? karg_at<int8_t>(y + i) : 0;
+    return karg_at<int8_t>(uv + (pl == 2 ? 28 : 0) + i);
+}
+
+// scaling LUT entry i of the three planes (closed form of generate_scaling)
+__device__ __forceinline__ void scaling_at(const FgArgs &a, const uint8_t (*pts)[2], int i) {
+    // pts: the y points (14) then the two uv point sets (10 each), staged in LDS
+    const MiFilmGrainData &d = a.data;
+    const int bdm8 = a.bpc - 8, size = 1 << a.bpc;
+    if (i >= 3 * size) return;
+    const int pl = i >> a.bpc, e = i & (size - 1);
+    int v = 0;
+    if (pl == 0) { if (d.num_y_points || d.chroma_scaling_from_luma) v = scaling_entry(pts, d.num_y_points, e, bdm8); }
+    else {
+        const int n = pl == 1 ? d.num_uv_points[0] : d.num_uv_points[1];
+        if (n) v = scaling_entry(pts + 14 + 10 * (pl - 1), n, e, bdm8);
+    }
+    a.scaling[pl * 4096 + e] = (uint8_t)v;
+}
+
+// average of the luma samples under chroma sample (y, x) (filmgrain.rs generate_grain_uv)
+__device__ __forceinline__ int luma_avg(const int16_t *q, int subx, int suby) {
+    // four reads whatever the subsampling: (a + a + b + b + 2) >> 2 == (a + b + 1) >> 1
+    const int sy = suby * kGW;
+    return (q[0] + q[subx] + q[sy] + q[sy + subx] + 2) >> 2;
+}
+
+template <int LAG, bool LT>
+__device__ __forceinline__ int ar_waves(int16_t (*lut)[kGH][kGW], int16_t *dummy, const uint8_t (*pts)[2], const FgArgs &a, bool ly, bool uv0, bool uv1,
+                        int cw, int chh, int gmin, int gmax) {
+    const MiFilmGrainData &d = a.data;
+    const int subx = a.ss_x, suby = a.ss_y;
+    constexpr int NT = 2 * LAG * LAG + 2 * LAG, S = LAG + 1, WC = 2 * LAG + 1;
+    const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int shift = (int)d.ar_coeff_shift, rnd = (1 << shift) >> 1;
+    {
+        constexpr int U = ar_unroll(LAG), B = ar_block(LAG), R = 2 * LAG;
+        const int gw = role ? cw : kGW, gh = role ? chh : kGH;
+        const bool on = role == 0 ? ly : role == 1 ? uv0 : role == 2 ? uv1 : false;
+        const int t0 = 1 + (cw - 7) * ((1 << subx) - 1) + subx + S * ((chh - 4) * ((1 << suby) - 1) + suby);
+        const int lend = S * (kGH - 1) + kGW;            // last luma step + 1
+        const int cend = S * (chh - 1) + cw;
+        const int lagc = ly ? t0 + B : 0;
+        // every wave starts U steps early (a row is entered lag steps before its column 0)
+        const int total = max(ly ? lend + U : 0, uv0 || uv1 ? lagc + cend + U : 0);
+        const int tlag = (role == 1 || role == 2 ? lagc : 0) + U;
+        int cg[NT + 1];
+#pragma unroll
+        for (int i = 0; i <= NT; i++) cg[i] = ar_coef(role, i);
+        // packed coefficient pairs: window row r, pair k (columns X - LAG + 2k, + 1) and the
+        // newest column X + LAG (high half); own row
+        int cpr[LAG][LAG + 1], cown[2];
+#pragma unroll
+        for (int r = 0; r < LAG; r++) {
+#pragma unroll
+            for (int k = 0; k < LAG; k++) cpr[r][k] = pk16(cg[r * WC + 2 * k], cg[r * WC + 2 * k + 1]);
+            cpr[r][LAG] = pk16(0, cg[r * WC + 2 * LAG]);
+        }
+        const int *co = cg + LAG * WC;   // own row: columns X - LAG .. X - 1
+        if (LAG == 3) { cown[0] = pk16(co[1], co[2]); cown[1] = pk16(0, co[0]); }
+        else if (LAG == 2) { cown[0] = pk16(co[0], co[1]); cown[1] = 0; }
+        else { cown[0] = pk16(0, co[0]); cown[1] = 0; }
+        const int lc = cg[NT];
+        int16_t *buf = &lut[role < 3 ? role : 0][0][0];
+        const int16_t *luma = &lut[0][0][0];
+        // per row of the lane (k = 0: row lane, 1: row lane + 64): the step its second row is
+        // entered, the column at step t (t - S y), the LDS offset of (y, X) (t + ro), whether
+        // (y, X) is inside the template, and the luma offset of the chroma term
+        const int y0 = lane, y1 = lane + 64;
+        const int thr = S * y1 - LAG;
+        const int ro0 = y0 * kGW - S * y0, ro1 = y1 * kGW - S * y1;
+        const int lo0 = (((min(max(y0 - 3, 0), gh - 4)) << suby) + 3) * kGW + 3 - ((S * y0 + 3) << subx);
+        const int lo1 = (((min(max(y1 - 3, 0), gh - 4)) << suby) + 3) * kGW + 3 - ((S * y1 + 3) << subx);
+        // interior iff (unsigned)(t - xs) < gw - 6 (rows outside 3 .. gh - 1 never)
+        const int xs0 = y0 >= 3 && y0 < gh ? S * y0 + 3 : -(1 << 28), xs1 = y1 < gh ? S * y1 + 3 : -(1 << 28);
+        const int maxoff = kGH * kGW - 1, lmaxoff = maxoff - subx - suby * kGW;   // (the luma average's reach)
+        int win[LAG][R], outp[4], outv = 0;
+#pragma unroll
+        for (int r = 0; r < LAG; r++)
+#pragma unroll
+            for (int c = 0; c < R; c++) win[r][c] = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) outp[c] = 0;
+        // the LDS reads of step t, issued one step ahead: fill value of (y, X), the four luma
+        // samples of the chroma term (summed at the step)
+        const int sy = suby * kGW;
+        auto fetch = [&](int t, int &p0, int &l0, int &l1, int &l2, int &l3) {
+            const bool second = t >= thr;
+            p0 = buf[min(max(t + (second ? ro1 : ro0), 0), maxoff)];
+            if (LT) {
+                const int16_t *q = luma + min(max((t << subx) + (second ? lo1 : lo0), 0), lmaxoff);
+                l0 = q[0]; l1 = q[subx]; l2 = q[sy]; l3 = q[sy + subx];
+            }
+        };
+        int p0, l0 = 0, l1 = 0, l2 = 0, l3 = 0;
+        fetch(-tlag, p0, l0, l1, l2, l3);
+        int nb = 0;
+        for (int b0 = 0; b0 < total; b0 += B, nb++) {
+            if (on) {
+                for (int tb = b0 - tlag; tb < b0 - tlag + B; tb += U) {
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        const int t = tb + u;
+                        // new window pairs (X + LAG - 1, X + LAG): row y - 1 from lane l - 1's last two
+                        // outputs, rows further up from the pair its window row r + 1 got LAG steps ago
+                        win[LAG - 1][u % R] = dpp_from_prev_lane(outp[(u + 3) % 4]);
+#pragma unroll
+                        for (int r = 0; r < LAG - 1; r++) win[r][u % R] = dpp_from_prev_lane(win[r + 1][(u + 3 * R - 1 - LAG) % R]);
+                        // taps: pair k of row r is ring slot (u - (2 LAG - 1) + 2k), the newest column
+                        // the high half of slot u; own columns X - 2, X - 1 = outp(t - 1), X - 3 the
+                        // high half of outp(t - 3)
+                        // four reads whatever the subsampling: (a + a + b + b + 2) >> 2 == (a + b + 1) >> 1
+                        const int lt = LT ? __mul24((l0 + l1 + l2 + l3 + 2) >> 2, lc) : 0;
+                        int acc[4] = { rnd + lt, 0, 0, 0 };
+#pragma unroll
+                        for (int r = 0; r < LAG; r++) {
+#pragma unroll
+                            for (int k = 0; k < LAG; k++)
+                                acc[(r + k) & 3] = dot2(win[r][(u + 3 * R - (2 * LAG - 1) + 2 * k) % R], cpr[r][k], acc[(r + k) & 3]);
+                            acc[(r + LAG) & 3] = dot2(win[r][u % R], cpr[r][LAG], acc[(r + LAG) & 3]);
+                        }
+                        acc[1] = dot2(outp[(u + 3) % 4], cown[0], acc[1]);
+                        if (LAG == 3) acc[2] = dot2(outp[(u + 1) % 4], cown[1], acc[2]);
+                        const int sum = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+                        const bool second = t >= thr;
+                        const bool interior = (unsigned)(t - (second ? xs1 : xs0)) < (unsigned)(gw - 6);
+                        const int g = interior ? min(max(p0 + (sum >> shift), gmin), gmax) : p0;
+                        outp[u % 4] = pk16(outv, g);
+                        outv = g;
+                        int16_t *dst = interior ? buf + t + (second ? ro1 : ro0) : dummy + lane;
+                        *dst = (int16_t)g;
+                        fetch(t + 1, p0, l0, l1, l2, l3);
+                    }
+                }
+            } else if (role >= 3) {
+                scaling_at(a, pts, (int)threadIdx.x - 192 + 256 * nb);
+            }
+            __syncthreads();
+        }
+        return nb;
+    }
+}
+
+template <int LAG>
+__device__ int grain_ar_all(int16_t (*lut)[kGH][kGW], int16_t *dummy, const uint8_t (*pts)[2], const FgArgs &a, bool ly, bool uv0, bool uv1,
+                            int cw, int chh, int gmin, int gmax) {
+    const MiFilmGrainData &d = a.data;
+    const int subx = a.ss_x, suby = a.ss_y;
+    constexpr int NT = 2 * LAG * LAG + 2 * LAG, S = LAG + 1, WC = 2 * LAG + 1;
+    const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int shift = (int)d.ar_coeff_shift, rnd = (1 << shift) >> 1;
+    if constexpr (LAG == 0) {
+        // no neighbours: samples are independent (luma first: chroma reads it)
+        for (int ph = 0; ph < 2; ph++) {
+            const bool on = ph == 0 ? role == 0 && ly : (role == 1 && uv0) || (role == 2 && uv1);
+            if (on) {
+                const int gw = role ? cw : kGW, gh = role ? chh : kGH;
+                const int lc = ar_coef(role, 0);
+                const bool lterm = role && d.num_y_points;
+                int16_t *buf = &lut[role][0][0];
+                for (int e = lane; e < (gh - 3) * (gw - 6); e += 64) {
+                    const int i = e / (gw - 6), x = e - i * (gw - 6);
+                    int16_t *q = buf + (3 + i) * kGW + 3 + x;
+                    const int lt = lterm ? __mul24(luma_avg(&lut[0][(i << suby) + 3][(x << subx) + 3], subx, suby), lc) : 0;
+                    *q = (int16_t)min(max(*q + ((lt + rnd) >> shift), gmin), gmax);
+                }
+            }
+            __syncthreads();
+        }
+        return 0;
+    } else {
+        const bool lterm = (role == 1 || role == 2) && d.num_y_points;
+        return lterm ? ar_waves<LAG, true>(lut, dummy, pts, a, ly, uv0, uv1, cw, chh, gmin, gmax)
+                     : ar_waves<LAG, false>(lut, dummy, pts, a, ly, uv0, uv1, cw, chh, gmin, gmax);
+    }
 }
 
 __global__ __launch_bounds__(kPrepThreads) void fg_prep_kernel(FgArgs a) {
@@ -192,31 +314,39 @@ __global__ __launch_bounds__(kPrepThreads) void fg_prep_kernel(FgArgs a) {
     const bool uv1 = ly ? a.layout && (d.num_uv_points[1] || d.chroma_scaling_from_luma) : a.uv_only == 2;
     const int cw = a.ss_x ? 44 : kGW, chh = a.ss_y ? 38 : kGH;
 
+    KTL(0);
+    // scaling points staged in LDS (y 14, u 10, v 10 pairs), read before the first barrier
+    __shared__ uint8_t pts[34][2];
+    {
+        constexpr size_t yo = offsetof(FgArgs, data) + offsetof(MiFilmGrainData, y_points);
+        constexpr size_t uvo = offsetof(FgArgs, data) + offsetof(MiFilmGrainData, uv_points);
+        const int i = threadIdx.x;
+        if (i < 28) (&pts[0][0])[i] = karg_at<uint8_t>(yo + i);
+        else if (i < 68) (&pts[0][0])[i] = karg_at<uint8_t>(uvo + i - 28);
+    }
     grain_fill_all(lut, d.seed, shift, ly, uv0, uv1, cw, chh);
     if (!ly)
         for (int i = threadIdx.x; i < kGH * kGW; i += kPrepThreads) (&lut[0][0][0])[i] = a.lut_y[i];
     __syncthreads();
+    KTL(1);
+    __shared__ int16_t dummy[64];
+    int nb;
     switch (d.ar_coeff_lag) {
-    case 0: grain_ar_all<0>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
-    case 1: grain_ar_all<1>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
-    case 2: grain_ar_all<2>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
-    default: grain_ar_all<3>(lut, d, ly, uv0, uv1, cw, chh, a.ss_x, a.ss_y, -gctr, gctr - 1); break;
+    case 0: nb = grain_ar_all<0>(lut, dummy, pts, a, ly, uv0, uv1, cw, chh, -gctr, gctr - 1); break;
+    case 1: nb = grain_ar_all<1>(lut, dummy, pts, a, ly, uv0, uv1, cw, chh, -gctr, gctr - 1); break;
+    case 2: nb = grain_ar_all<2>(lut, dummy, pts, a, ly, uv0, uv1, cw, chh, -gctr, gctr - 1); break;
+    default: nb = grain_ar_all<3>(lut, dummy, pts, a, ly, uv0, uv1, cw, chh, -gctr, gctr - 1); break;
     }
+    KTL(2);
     // export templates
     for (int i = threadIdx.x; i < 3 * kGH * kGP; i += kPrepThreads) {
         const int r = i / kGP, c = i - r * kGP;
         a.lut[i] = c < kGW ? (&lut[0][0][0])[r * kGW + c] : 0;
     }
-
-    // scaling LUTs
-    const int size = 1 << a.bpc;
-    for (int i = threadIdx.x; i < 3 * size; i += kPrepThreads) {
-        const int pl = i / size, e = i % size;
-        int v = 0;
-        if (pl == 0) { if (d.num_y_points || d.chroma_scaling_from_luma) v = scaling_entry(d.y_points, d.num_y_points, e, bdm8); }
-        else if (d.num_uv_points[pl - 1]) v = scaling_entry(d.uv_points[pl - 1], d.num_uv_points[pl - 1], e, bdm8);
-        a.scaling[pl * 4096 + e] = (uint8_t)v;
-    }
+    KTL(3);
+    // scaling LUT entries the AR blocks left (waves 3-6 fill 256 per block)
+    for (int i = 256 * nb + threadIdx.x; i < 3 << a.bpc; i += kPrepThreads) scaling_at(a, pts, i);
+    KTL(4);
 }
 
 // Per-block offsets (filmgrain.rs row_seed + one 8-bit draw per 32-wide block along the row):
@@ -246,7 +376,7 @@ __device__ __forceinline__ int lut_at(const int16_t *lut, int rv, int subx, int 
 }
 
 __device__ __forceinline__ int blend(int a, int b, int wa, int wb, int gmin, int gmax) {
-    return min(max(round2i(a * wa + b * wb, 5), gmin), gmax);
+    return min(max(round2i(__mul24(a, wa) + __mul24(b, wb), 5), gmin), gmax);
 }
 
 // Position of one 8-pixel chunk inside its grain block and the block offsets it needs.
@@ -487,11 +617,11 @@ __global__ __launch_bounds__(256) void fg_apply_kernel(FgArgs a) {
             if (p) {
                 val = lum[j];
                 if (!d.chroma_scaling_from_luma) {
-                    const int comb = lum[j] * d.uv_luma_mult[p - 1] + sv[j] * d.uv_mult[p - 1];
+                    const int comb = __mul24(lum[j], (int)d.uv_luma_mult[p - 1]) + __mul24(sv[j], (int)d.uv_mult[p - 1]);
                     val = min(max((comb >> 6) + d.uv_offset[p - 1] * (1 << bdm8), 0), bdmax);
                 }
             }
-            const int noise = round2i(scl[val] * g[j], d.scaling_shift);
+            const int noise = round2i(__mul24((int)scl[val], g[j]), d.scaling_shift);
             ov[j] = min(max(sv[j] + noise, minv), maxv);
         }
         store8(dst, ov, n);
