@@ -443,7 +443,7 @@ int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, v
 static int lr_banded() {
     static const int v = [] {
         const char *e = getenv("MI_LR_BANDS");
-        return e ? atoi(e) != 0 : 0;
+        return e ? atoi(e) : 0;   // 1 bands, 2 contiguous eighths of the tile order per XCD
     }();
     return v;
 }
@@ -583,7 +583,7 @@ int mi_lr_frame(MiCtx *ctx, const MiPicture *cdef, const MiPicture *deblocked, c
         int stripes = 0;
         while ((stripes ? (64 * stripes - 8) >> sv : 0) < a.ph[p]) stripes++;
         a.stripes[p] = stripes;
-        if (lr_banded()) {
+        if (lr_banded() == 1) {
             // band q = stripes [q * stripes / 8, (q + 1) * stripes / 8)
             int m = 0;
             for (int q = 0; q < 8; q++) m = std::max(m, ((q + 1) * stripes / 8 - q * stripes / 8) * a.tiles_x[p]);

@@ -57,7 +57,9 @@ __device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, u
     const int x = 2 * cp - 2;                          // positions x, x + 1 (valid: -1 .. tw)
     if (g >= G || x > tw) return;
     const int nrows = sh + 2;
-    const int per = (nrows + G - 1) / G;
+    // R = 2 keeps A/B on odd rows only: an even row count per group starts every group on an
+    // odd row, so the row parity test below is the same for all lanes (no divergent halves)
+    const int per = R == 2 ? (((nrows + G - 1) / G) + 1) & ~1 : (nrows + G - 1) / G;
     const int y0 = -1 + g * per, y1 = min(-1 + (g + 1) * per, sh + 1);
     if (y0 >= y1) return;
     const uint32_t *col = reinterpret_cast<const uint32_t *>(win + x - 2 + kWX);
@@ -211,6 +213,7 @@ __device__ __forceinline__ void sgr_pairs(int *A, int16_t *B, const int16_t *win
     if (s0) {
         sgr_ab<2>(win, A, B, sh, tw, (unsigned)s0, bdm8, xbyx);
         __syncthreads();
+        KTL(2);
         if (act) {
             // A/B on odd rows: even j uses rows j-1 and j+1, odd j row j (r0 is even)
             int cau[2], sau[2], cbu[2], sbu[2], cad[2], sad[2], cbd[2], sbd[2];
@@ -242,10 +245,12 @@ __device__ __forceinline__ void sgr_pairs(int *A, int16_t *B, const int16_t *win
             }
         }
         __syncthreads();
+        KTL(3);
     }
     if (s1) {
         sgr_ab<1>(win, A, B, sh, tw, (unsigned)s1, bdm8, xbyx);
         __syncthreads();
+        KTL(4);
         if (act) {
             int c0[2], t0[2], d0[2], u0[2], c1[2], t1[2], d1[2], u1[2], c2[2], t2[2], d2[2], u2[2];
             ld(r0 - 1, c0, t0, d0, u0);
@@ -398,11 +403,16 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
 #ifndef MI_LR_XCD
 #define MI_LR_XCD 0   // tile -> XCD: 0 hardware round robin, 1 contiguous ranges (xcd_block), C > 1 runs of C
 #endif
-    const int blk = MI_LR_XCD == 1 ? xcd_block(blockIdx.x, gridDim.x) : MI_LR_XCD > 1 ? xcd_chunk(blockIdx.x, gridDim.x, MI_LR_XCD) : blockIdx.x;
+    // a.banded == 2: XCD k walks the k-th eighth of the (plane, stripe, tile) order, so
+    // horizontally adjacent tiles share their halo lines in one L2
+    // a.banded = C >= 3: runs of C consecutive tiles dealt to the XCDs in turn
+    const int blk = a.banded == 2 || MI_LR_XCD == 1 ? xcd_block(blockIdx.x, gridDim.x)
+                  : a.banded >= 3 ? xcd_chunk(blockIdx.x, gridDim.x, a.banded)
+                  : MI_LR_XCD > 1 ? xcd_chunk(blockIdx.x, gridDim.x, MI_LR_XCD) : blockIdx.x;
     const int p = blk < a.blk_start[1] ? 0 : blk < a.blk_start[2] ? 1 : 2;
     int lb = blk - a.blk_start[p];
     const int tiles = a.tiles_x[p];
-    if (a.banded) {
+    if (a.banded == 1) {
         // grid index 8m + q: the m-th tile of band q (plane starts are multiples of 8)
         const int q = lb & 7, m = lb >> 3, ns = a.stripes[p];
         const int s0 = q * ns / 8, s1 = (q + 1) * ns / 8;
@@ -449,8 +459,11 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
             if (x + 8 <= x0 + tw) store8<Px>(dp, load8<Px>(sp));   // O = C
             else for (int j = 0; j < x0 + tw - x; j++) dp[j] = sp[j];
         }
+        KTLV(6, 0);
+        KTL(5);
         return;
     }
+    KTLV(6, type);
 
     // ---- stage the (sh+6)-row window, columns x0-8 .. x0+71 (C inside the stripe, D across
     // its edges) as 8-pixel vectors; columns outside the plane replicate the edge pixel ----
@@ -487,6 +500,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
         if (rr < wr) *reinterpret_cast<uint4 *>(&win[rr * kLrWin + 8 * (i % kNV)]) = sv[q];
     }
     __syncthreads();
+    KTL(1);
 
     // (the tile filter is written out here rather than through lr_wiener_tile / lr_sgr_tile:
     //  that form measured 70.5 vs 63 us at 4K10 with the same registers and LDS size, most
@@ -504,8 +518,10 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
         const int clip_h = (1 << (bd + 1 + 7 - rbh)) - 1;
         wiener_hor(win, hor, wr, tw, fh, bd, rbh, clip_h);
         __syncthreads();
+        KTL(2);
         wiener_ver(hor, B, wr, sh, tw, fv, bd, rbv, bdmax);
         __syncthreads();
+        KTL(3);
         store_tile<Px>(B, O, st, S, sh, x0, tw);
         KTL(5);
         return;

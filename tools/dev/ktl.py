@@ -73,3 +73,16 @@ for u in UNITS:
         for c in np.unique(cls):
             m = cls == c
             print(f"   size {int(c):2d}: {m.sum():5d} wg, life mean {life[m].mean():6.1f} max {life[m].max():6.1f}, start {st[m].min():5.1f}-{st[m].max():5.1f}")
+    if u == "lr":
+        cls = a[:, 6]
+        for c in np.unique(cls):
+            m = cls == c
+            line = f"   type {int(c)}: {m.sum():5d} wg, life mean {life[m].mean():5.1f}"
+            prev = a[m, 0]
+            for k in range(1, 6):
+                col = a[m, k]
+                ok = (col != 0) & (col >= prev)
+                if ok.mean() > 0.5:
+                    line += f" | {k - 1}->{k} {((col[ok] - prev[ok]) / 100.0).mean():.2f}"
+                    prev = np.where(ok, col, prev)
+            print(line)

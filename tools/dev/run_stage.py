@@ -27,3 +27,16 @@ for _ in range(int(os.environ.get("REPS", "10"))):
         F.check(L.mi_lr_frame(ctx.h, ctypes.byref(pb), ctypes.byref(pd), ctypes.byref(po), ctypes.byref(pipe.lr.s), sp), "lr")
 torch.cuda.synchronize()
 print("done")
+if os.environ.get("TIME"):
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from gtime import gtime
+
+    def one(stream):
+        p = F._stream_ptr(stream)
+        if st == "deblock":
+            F.check(L.mi_deblock_frame_to(ctx.h, ctypes.byref(pa), ctypes.byref(pd), ctypes.byref(pipe.lf.s), p), "lf")
+        elif st == "cdef":
+            F.check(L.mi_cdef_frame(ctx.h, ctypes.byref(pd), ctypes.byref(pb), ctypes.byref(pipe.cdef.s), p), "cdef")
+        elif st == "lr":
+            F.check(L.mi_lr_frame(ctx.h, ctypes.byref(pb), ctypes.byref(pd), ctypes.byref(po), ctypes.byref(pipe.lr.s), p), "lr")
+    print(f"{st} {gtime(one):.2f} us", flush=True)
