@@ -576,6 +576,9 @@ int mi_lr_frame(MiCtx *ctx, const MiPicture *cdef, const MiPicture *deblocked, c
         const int sh = p ? ss_hor : 0, sv = p ? ss_ver : 0;
         a.pw[p] = (cdef->w + sh) >> sh;
         a.ph[p] = (cdef->h + sv) >> sv;
+        // lr.hip forms row offsets with one 24-bit multiply
+        if (a.stride[p] <= 0 || a.stride[p] >= (1 << 24) || (int64_t)a.ph[p] * a.stride[p] >= (1LL << 32))
+            return fail(ctx, -EINVAL);
         const int us = 1 << lr->unit_size_log2[p ? 1 : 0];
         a.tw[p] = ((a.restore >> p) & 1) && us < 64 ? 32 : 64;
         a.tiles_x[p] = (a.pw[p] + a.tw[p] - 1) / a.tw[p];

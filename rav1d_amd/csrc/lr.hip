@@ -90,13 +90,16 @@ __device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, u
             const bool on[2] = { c0, c1 };
 #pragma unroll
             for (int e = 0; e < 2; e++) {
+                // a, b < 2^21 (25 squares of 8-bit-scaled samples) and xv * one_by_x < 2^17, sums
+                // < 2^17: 24-bit multiplies (full rate) except p * s, which wraps in u32 as the
+                // reference's does
                 const int a = (sqs[e] + ((1 << (2 * bdm8)) >> 1)) >> (2 * bdm8);
                 const int b = (sums[e] + ((1 << bdm8) >> 1)) >> bdm8;
-                const unsigned p = (unsigned)max(a * n - b * b, 0);
+                const unsigned p = (unsigned)max((int)__umul24((unsigned)a, (unsigned)n) - (int)__umul24((unsigned)b, (unsigned)b), 0);
                 const unsigned z = (p * s + (1u << 19)) >> 20;
                 const unsigned xv = xbyx[min(z, 255u)];
                 if (on[e]) {
-                    A[(y + 1) * kLrAB + x + e + 1] = (int)((xv * (unsigned)sums[e] * one_by_x + (1u << 11)) >> 12);
+                    A[(y + 1) * kLrAB + x + e + 1] = (int)((__umul24(__umul24(xv, one_by_x), (unsigned)sums[e]) + (1u << 11)) >> 12);
                     B[(y + 1) * kLrAB + x + e + 1] = (int16_t)xv;
                 }
             }
@@ -228,7 +231,7 @@ __device__ __forceinline__ void sgr_pairs(int *A, int16_t *B, const int16_t *win
                     for (int e = 0; e < 2; e++) {
                         const int a = (cbu[e] + cbd[e]) * 6 + (sbu[e] + sbd[e]) * 5;
                         const int b = (cau[e] + cad[e]) * 6 + (sau[e] + sad[e]) * 5;
-                        acc[e][q] += w0 * ((b - a * v[e] + (1 << 8)) >> 9);
+                        acc[e][q] += __mul24(w0, (b - __mul24(a, v[e]) + (1 << 8)) >> 9);
                     }
                 }
                 if (r0 + q + 1 < r1) {
@@ -237,7 +240,7 @@ __device__ __forceinline__ void sgr_pairs(int *A, int16_t *B, const int16_t *win
                     for (int e = 0; e < 2; e++) {
                         const int a = cbd[e] * 6 + sbd[e] * 5;
                         const int b = cad[e] * 6 + sad[e] * 5;
-                        acc[e][q + 1] += w0 * ((b - a * v[e] + (1 << 7)) >> 8);
+                        acc[e][q + 1] += __mul24(w0, (b - __mul24(a, v[e]) + (1 << 7)) >> 8);
                     }
                 }
 #pragma unroll
@@ -265,7 +268,7 @@ __device__ __forceinline__ void sgr_pairs(int *A, int16_t *B, const int16_t *win
                     for (int e = 0; e < 2; e++) {
                         const int a = (d1[e] + u1[e] + d0[e] + d2[e]) * 4 + (u0[e] + u2[e]) * 3;
                         const int b = (c1[e] + t1[e] + c0[e] + c2[e]) * 4 + (t0[e] + t2[e]) * 3;
-                        acc[e][q] += w1 * ((b - a * v[e] + (1 << 8)) >> 9);
+                        acc[e][q] += __mul24(w1, (b - __mul24(a, v[e]) + (1 << 8)) >> 9);
                     }
                 }
 #pragma unroll
@@ -343,13 +346,16 @@ __device__ __forceinline__ void store8(Px *p, const uint4 &u) {
         *reinterpret_cast<uint2 *>(p) = d;
     }
 }
+// byte offset of plane row y: rows < 2^24 and strides < 2^24 with a product below 4 GB (an 8K
+// 16-bit plane is 70 MB), so one 24-bit multiply instead of a 64-bit one
+__device__ __forceinline__ size_t row_off(int y, int64_t st) { return (size_t)__umul24((unsigned)y, (unsigned)st); }
 // the finished sh x tw output tile (int16, row stride 64, in LDS) -> O with 8-pixel stores
 template <typename Px>
 __device__ __forceinline__ void store_tile(const int16_t *t, uint8_t *O, int64_t st, int S, int sh, int x0, int tw) {
     for (int i = threadIdx.x; i < sh * 8; i += kNT) {
         const int r = i >> 3, c = 8 * (i & 7);
         if (c >= tw) continue;
-        Px *dp = reinterpret_cast<Px *>(O + (int64_t)(S + r) * st) + x0 + c;
+        Px *dp = reinterpret_cast<Px *>(O + row_off(S + r, st)) + x0 + c;
         if (c + 8 <= tw) store8<Px>(dp, *reinterpret_cast<const uint4 *>(t + r * 64 + c));
         else for (int j = 0; j < tw - c; j++) dp[j] = (Px)t[r * 64 + c + j];
     }
@@ -454,8 +460,8 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
         for (int i = threadIdx.x; i < sh * 8; i += kNT) {
             const int r = i >> 3, x = x0 + 8 * (i & 7);
             if (x >= x0 + tw) continue;
-            const Px *sp = reinterpret_cast<const Px *>(C + (int64_t)(S + r) * st) + x;
-            Px *dp = reinterpret_cast<Px *>(O + (int64_t)(S + r) * st) + x;
+            const Px *sp = reinterpret_cast<const Px *>(C + row_off(S + r, st)) + x;
+            Px *dp = reinterpret_cast<Px *>(O + row_off(S + r, st)) + x;
             if (x + 8 <= x0 + tw) store8<Px>(dp, load8<Px>(sp));   // O = C
             else for (int j = 0; j < x0 + tw - x; j++) dp[j] = sp[j];
         }
@@ -483,7 +489,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
             if (r >= 0 && r < sh) { src = C; yy = S + r; }
             else if (r < 0) { src = have_top ? D : C; yy = have_top ? S - 2 + (r == -1) : S; }
             else { src = have_bottom ? D : C; yy = have_bottom ? min(E + (r > sh), ph - 1) : E - 1; }
-            const Px *row = reinterpret_cast<const Px *>(src + (int64_t)yy * st);
+            const Px *row = reinterpret_cast<const Px *>(src + row_off(yy, st));
             if (x >= 0 && x + 8 <= pw) sv[q] = load8<Px>(row + x);
             else {
                 int e[8];
