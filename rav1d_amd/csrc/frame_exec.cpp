@@ -19,6 +19,7 @@
 #include <string.h>
 #include <algorithm>
 #include <cstdlib>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <functional>
@@ -298,7 +299,9 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
     if ((f->n_intra || f->n_inter_tx) && f->ncoef < 16) return BAD();
     if (f->dep_start && (f->dep_start[0] != 0 || f->dep_start[f->n_intra] != f->n_deps)) return BAD();
     const bool inter = inter_present(f);
-    for (int i = 0; i < f->n_intra; i++) {
+    // per-block checks on the planning pool (ranges of blocks; a failing range is re-checked
+    // on the calling thread, whose g_why the caller reads)
+    auto check = [&](int i) -> int {
         const MiIntraBlock &b = f->intra[i];
         const MiTxBlock &t = f->intra_tx[i];
         if (b.plane >= nplanes || t.plane != b.plane || t.x != b.x || t.y != b.y) return BAD();
@@ -348,7 +351,16 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
         for (int d = f->dep_start[i]; d < f->dep_start[i + 1]; d++)
             if (d < 0 || d >= f->n_deps || f->deps[d] < 0 || f->deps[d] >= i) return BAD();
         if (f->dep_start[i + 1] < f->dep_start[i]) return BAD();
-    }
+        return 0;
+    };
+    std::atomic<int> bad{0};
+    parallel_ranges(f->n_intra, 32768, [&](int lo, int hi, int) {
+        for (int i = lo; i < hi && !bad.load(std::memory_order_relaxed); i++)
+            if (check(i)) bad.store(1, std::memory_order_relaxed);
+    });
+    if (bad.load())
+        for (int i = 0; i < f->n_intra; i++)
+            if (int e = check(i)) return e;
     const int sb128w = (f->w + 127) >> 7, sb128h = (f->h + 127) >> 7;
     if (f->filter_y && (!f->lf_level || !f->lf_masks || f->sb128w != sb128w || f->sb128h != sb128h ||
                         f->b4_stride < sb128w * 32))
@@ -406,7 +418,10 @@ int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<in
     }
     const int aw = (f->w + 127) & ~127, ah = (f->h + 127) & ~127;
     int pw4[3], ph4[3];
-    std::vector<int32_t> own[3];
+    // (per-thread scratch kept across frames: a fresh multi-MB map per frame costs its page
+    // faults; bound by reference here, since the pool threads below must see this thread's)
+    static thread_local std::vector<int32_t> own_tl[3];
+    std::vector<int32_t> (&own)[3] = own_tl;
     for (int p = 0; p < nplanes; p++) {
         pw4[p] = (p ? aw >> ssh : aw) >> 2;
         ph4[p] = (p ? ah >> ssv : ah) >> 2;
@@ -667,6 +682,12 @@ void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
     dep_start.assign(n + 1, 0);
     deps.clear();
     strip_start.clear();
+    // (a plan is reused frame after frame: every list that is appended to starts empty)
+    tl_ds.clear();
+    tl_deps.clear();
+    tl_strip.clear();
+    pl.lap_s[0].clear();
+    pl.lap_s[1].clear();
 
     // dependency levels (deps always point backwards): level order lets the persistent
     // kernel's workers run every block of a level side by side. A single frame is split into
@@ -689,8 +710,12 @@ void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
     for (int i = 0; granules && i < n; i++)
         if ((f->intra[i].flags & MI_INTRA_II) || f->intra[i].mode == MI_INTRA_RESID) granules = false;
     if (n) {
-        std::vector<int32_t> xs, xd;          // extra dependencies of the strip split (CSR)
-        std::vector<int8_t> strip;
+        // per-thread scratch kept across frames (no per-frame page faults)
+        // (the scratch is bound by reference: the pool threads must see this thread's vectors)
+        static thread_local std::vector<int32_t> xs_tl, xd_tl;   // extra dependencies of the strip split (CSR)
+        static thread_local std::vector<int8_t> strip_tl;
+        std::vector<int32_t> &xs = xs_tl, &xd = xd_tl;
+        std::vector<int8_t> &strip = strip_tl;
         const int nstrips = intra_strips(f, strip, xs, xd, granules);
         const auto t_a = clk::now();
         auto each_dep = [&](int i, auto &&fn) {
@@ -698,9 +723,14 @@ void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
             if (nstrips > 1)
                 for (int d = xs[i]; d < xs[i + 1]; d++) fn(xd[d]);
         };
-        std::vector<int32_t> level(n), pos(n);
+        static thread_local std::vector<int32_t> level_tl, pos_tl;
+        std::vector<int32_t> &level = level_tl, &pos = pos_tl;
+        level.assign(n, 0);
+        pos.resize(n);
         int maxl = 0;
-        for (int i = 0; i < n; i++) {
+        // MI_IR_NOLEVELS=1 (experiment): decode order within a strip, no level pass
+        static const bool nolevels = [] { const char *e = getenv("MI_IR_NOLEVELS"); return e && e[0] == '1'; }();
+        for (int i = 0; i < n && !nolevels; i++) {
             int l = 0;
             each_dep(i, [&](int d) { l = std::max(l, level[d] + 1); });
             level[i] = l;
@@ -718,7 +748,9 @@ void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
             for (int q = 0; q <= nstrips; q++) strip_start[q] = cnt[q * (maxl + 1)];
         }
         for (int i = 0; i < n; i++) pos[i] = cnt[key(i)]++;
-        std::vector<int32_t> inv(n);
+        static thread_local std::vector<int32_t> inv_tl;
+        std::vector<int32_t> &inv = inv_tl;
+        inv.resize(n);
         for (int i = 0; i < n; i++) inv[pos[i]] = i;
         const auto t_c = clk::now();
         // the queue-ordered copies, walking the units in decode order (their deps point to
@@ -809,8 +841,13 @@ void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
 
 int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int *final, void *stream,
               StageEvents &tev, int64_t *bytes) {
+    static const bool fx_prof = getenv("MI_FX_PROFILE") != nullptr;
+    const auto t_val = std::chrono::steady_clock::now();
     int r = validate(f, pics);
     if (r) return ctx->last_error = r;
+    if (fx_prof)
+        fprintf(stderr, "frame_run validate %.3f ms\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_val).count());
     hipStream_t s = (hipStream_t)stream;
     const size_t cb = f->bpc == 8 ? 2 : 4, pb = f->bpc == 8 ? 1 : 2;
     const int n = f->n_intra;
@@ -820,7 +857,8 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
     if (inter_present(f) || f->n_inter_tx) {
         if ((r = validate_refs(f, pics, scaled)) || (r = validate_inter(f, pics, scaled))) return ctx->last_error = r;
     }
-    FramePlan pl;
+    static thread_local FramePlan pl_tl;   // vectors keep their capacity across frames
+    FramePlan &pl = pl_tl;
     plan_frame(f, scaled, pl);
     if (ctx->tm_on) ctx->tm_strips_ms += pl.strips_ms;
     const bool inter = pl.inter, granules = pl.granules;
@@ -862,6 +900,7 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
     const auto t_st = clk::now();
     if ((r = stage_upload(ctx, secs, s, tev.ev[0], bytes))) return ctx->last_error = r;
     if (ctx->tm_on) ctx->tm_stage_ms += std::chrono::duration<double, std::milli>(clk::now() - t_st).count();
+    if (fx_prof) fprintf(stderr, "frame_run stage %.3f ms\n", std::chrono::duration<double, std::milli>(clk::now() - t_st).count());
     tev.mark(1, s);
     uint8_t *dev = ctx->fx_dev;
     auto D = [&](int i) -> void * { return secs[i].bytes ? dev + secs[i].off : nullptr; };
@@ -1060,10 +1099,9 @@ double mi_frame_plan_ms(const MiDecFrame *f, int reps) {
     bool scaled[7] = {};
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
-    for (int i = 0; i < reps; i++) {
-        FramePlan pl;
-        plan_frame(f, scaled, pl);
-    }
+    static thread_local FramePlan pl_tl;   // as mi_frame_run keeps it: reused frame after frame
+    FramePlan &pl = pl_tl;
+    for (int i = 0; i < reps; i++) plan_frame(f, scaled, pl);
     return std::chrono::duration<double, std::milli>(clk::now() - t0).count() / reps;
 }
 

@@ -510,10 +510,9 @@ __device__ __forceinline__ uint16_t pk_row_hi8(lf_s2 a, lf_s2 b) {
 }
 
 template <int WD, typename Px, int P>
-__device__ __forceinline__ void lf_col_pair(Px *t, const uint16_t *list, int i, const uint8_t *le,
+__device__ __forceinline__ void lf_col_pair(Px *t, int e, int i, const uint8_t *le,
                                             const uint8_t *li, int bdm8, int bdmax) {
     {
-        const int e = list[i >> 1];
         const int u = e >> 6, L = e & 63;
         const int r = (u / kLfEdgesV) * 4 + 2 * (i & 1), k = u % kLfEdgesV;
         Px *w0 = &t[r * P + 4 + 4 * k], *w1 = w0 + P;
@@ -553,12 +552,11 @@ __device__ __forceinline__ void lf_col_pair(Px *t, const uint16_t *list, int i, 
 
 // Row edges: a lane holds two adjacent pixel columns (one LDS dword per row for u16).
 template <int WD, typename Px, int P>
-__device__ __forceinline__ void lf_row_pair(Px *t, const uint16_t *list, int i, const uint8_t *le,
+__device__ __forceinline__ void lf_row_pair(Px *t, int e, int i, const uint8_t *le,
                                             const uint8_t *li, int bdm8, int bdmax) {
     constexpr int nr = WD == 16 ? 7 : WD == 8 ? 4 : WD == 6 ? 3 : 2;   // rows read each side
     constexpr int lo = WD == 16 ? 2 : WD == 8 ? 5 : 6;                 // rows [lo, 16 - lo) written
     {
-        const int e = list[i >> 1];
         const int u = e >> 6, L = e & 63;
         const int k = u / (kLfTW / 4), col = (u % (kLfTW / 4)) * 4 + 2 * (i & 1);
         Px *w = &t[(4 * k) * P + 16 + col];
@@ -586,10 +584,14 @@ __device__ __forceinline__ void lf_row_pair(Px *t, const uint16_t *list, int i, 
 
 // The four width classes of one direction as one sequence of 64-pair chunks, dealt to the
 // workgroup's waves in turn: every chunk runs one filter branch (wave-uniform class), and a
-// class leaves at most one partial wave instead of one partial 256-lane pass.
+// class leaves at most one partial wave instead of one partial 256-lane pass. Work lists: two
+// arrays of N entries per direction, classes 0 / 2 filled upwards from the front and 1 / 3
+// downwards from the back (a class pair never holds more than N units), half the LDS of four
+// N-entry lists: 4 workgroups per CU instead of 3.
 template <bool COLS, typename Px, int P>
 __device__ __forceinline__ void lf_dir_pk(Px *t, const uint16_t (*lists)[COLS ? (kLfRows / 4) * kLfEdgesV : kLfEdgesH * (kLfTW / 4)],
                                           const int *cnt, const uint8_t *le, const uint8_t *li, int bdm8, int bdmax) {
+    constexpr int N = COLS ? (kLfRows / 4) * kLfEdgesV : kLfEdgesH * (kLfTW / 4);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // chunk prefix over the classes (wave-uniform: the counts are LDS broadcasts)
     const int c0 = (cnt[0] * 2 + 63) >> 6, c1 = c0 + ((cnt[1] * 2 + 63) >> 6);
@@ -599,11 +601,12 @@ __device__ __forceinline__ void lf_dir_pk(Px *t, const uint16_t (*lists)[COLS ? 
         const int base = cls == 0 ? 0 : cls == 1 ? c0 : cls == 2 ? c1 : c2;
         const int i = (g - base) * 64 + lane;
         if (i >= cnt[cls] * 2) continue;
+        const int e = lists[cls >> 1][cls & 1 ? N - 1 - (i >> 1) : i >> 1];
         switch (cls) {
 #define LF_CASE(k, wd)                                                                     \
         case k:                                                                            \
-            if constexpr (COLS) lf_col_pair<wd, Px, P>(t, lists[k], i, le, li, bdm8, bdmax); \
-            else lf_row_pair<wd, Px, P>(t, lists[k], i, le, li, bdm8, bdmax);                \
+            if constexpr (COLS) lf_col_pair<wd, Px, P>(t, e, i, le, li, bdm8, bdmax);     \
+            else lf_row_pair<wd, Px, P>(t, e, i, le, li, bdm8, bdmax);                    \
             break;
         LF_CASE(0, 4) LF_CASE(1, 6) LF_CASE(2, 8) LF_CASE(3, 16)
 #undef LF_CASE
@@ -629,7 +632,7 @@ __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
     __shared__ __attribute__((aligned(16))) Px t[kLfRows * P];
     // work lists: active edge units bucketed by width class, so that the lanes of a wave run
     // one filter branch; entry = (unit index << 6) | L
-    __shared__ uint16_t listv[4][NV], listh[4][NH];
+    __shared__ uint16_t listv[2][NV], listh[2][NH];
     __shared__ int cnt[8];
     __shared__ uint8_t le[64], li[64];
     const int tid = threadIdx.x;
@@ -700,7 +703,8 @@ __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
         if (!wd || ((k == 0 || k == (v ? kLfEdgesV : kLfEdgesH) - 1) && wd != 16)) continue;
         const int c = lf_class(wd);
         const int slot = atomicAdd(&cnt[(v ? 0 : 4) + c], 1);
-        (v ? listv[c] : listh[c])[slot] = (uint16_t)((u << 6) | (code & 63));
+        const int N = v ? NV : NH;
+        (v ? listv[c >> 1] : listh[c >> 1])[c & 1 ? N - 1 - slot : slot] = (uint16_t)((u << 6) | (code & 63));
     }
     __syncthreads();
     KTL(2);
