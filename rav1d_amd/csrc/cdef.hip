@@ -568,6 +568,7 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
                 *reinterpret_cast<uint2 *>(a.dst[p] + off) = *reinterpret_cast<const uint2 *>(a.src[p] + off);
             }
         }
+        KTL(5);
         return;
     }
 
@@ -609,6 +610,7 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
         }
     }
     __syncthreads();
+    KTL(1);
 
     if (MI_CDEF_DIAG != 2 && (y_pri || uv_pri)) {
         const int b = threadIdx.x & 63, w = threadIdx.x >> 6;   // wave-uniform direction
@@ -627,6 +629,7 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
         dcost[w][b] = c;
         __syncthreads();
     }
+    KTL(2);
 
     if (threadIdx.x < 64) {
         const int b = threadIdx.x, bxl = b & 7, byl = b >> 3;
@@ -659,11 +662,13 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
         bstate[b] = (flag & 1) | (y_pri ? dir : 0) << 8 | (y_pri ? pri : 0) << 16;
     }
     __syncthreads();
+    KTL(3);
 
     // luma: 2048 pairs, one 8x8 block per 32-lane group at a time
     if (MI_CDEF_DIAG != 5)
         filter_luma<Px, kTS>(ty, ytaps, bstate, y_sec, a.damping, bdm8, a.src[0], a.dst[0], a.stride[0],
                              x0, y0, fwy, fhy);
+    KTL(4);
     if (L && MI_CDEF_DIAG != 4) {
         // chroma: lanes 0..255 U, 256..511 V (damping - 1, cdef_apply.rs)
         const int p = 1 + (threadIdx.x >> 8);
