@@ -456,23 +456,10 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
         u = &a.lr_mask[sbi].lr[p][ui];
         type = u->type;
     }
-    if (type == 0) {   // RESTORATION_NONE: O = C, 8-pixel vectors
-        for (int i = threadIdx.x; i < sh * 8; i += kNT) {
-            const int r = i >> 3, x = x0 + 8 * (i & 7);
-            if (x >= x0 + tw) continue;
-            const Px *sp = reinterpret_cast<const Px *>(C + row_off(S + r, st)) + x;
-            Px *dp = reinterpret_cast<Px *>(O + row_off(S + r, st)) + x;
-            if (x + 8 <= x0 + tw) store8<Px>(dp, load8<Px>(sp));   // O = C
-            else for (int j = 0; j < x0 + tw - x; j++) dp[j] = sp[j];
-        }
-        KTLV(6, 0);
-        KTL(5);
-        return;
-    }
-    KTLV(6, type);
-
     // ---- stage the (sh+6)-row window, columns x0-8 .. x0+71 (C inside the stripe, D across
-    // its edges) as 8-pixel vectors; columns outside the plane replicate the edge pixel ----
+    // its edges) as 8-pixel vectors; columns outside the plane replicate the edge pixel. The
+    // tile's restoration type is only tested after the window is staged, so the loads do not
+    // wait for the type's load; a RESTORATION_NONE tile copies its rows out of the window ----
     const bool have_top = k > 0, have_bottom = E < ph;
     const int wr = sh + 6;
     constexpr int kNV = kLrWin / 8;                   // vectors per window row
@@ -499,6 +486,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
             }
         }
     }
+
 #pragma unroll
     for (int q = 0; q < kSV; q++) {
         const int i = threadIdx.x + q * kNT;
@@ -507,6 +495,20 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
     }
     __syncthreads();
     KTL(1);
+    if (type == 0) {   // RESTORATION_NONE: O = C, the window's in-stripe rows as 8-pixel vectors
+        for (int i = threadIdx.x; i < sh * 8; i += kNT) {
+            const int r = i >> 3, c = 8 * (i & 7);
+            if (c >= tw) continue;
+            const uint4 v = *reinterpret_cast<const uint4 *>(&win[(r + 3) * kLrWin + kWX + c]);
+            Px *dp = reinterpret_cast<Px *>(O + row_off(S + r, st)) + x0 + c;
+            if (c + 8 <= tw) store8<Px>(dp, v);
+            else for (int e = 0; e < tw - c; e++) dp[e] = (Px)win[(r + 3) * kLrWin + kWX + c + e];
+        }
+        KTLV(6, 0);
+        KTL(5);
+        return;
+    }
+    KTLV(6, type);
 
     // (the tile filter is written out here rather than through lr_wiener_tile / lr_sgr_tile:
     //  that form measured 70.5 vs 63 us at 4K10 with the same registers and LDS size, most

@@ -306,6 +306,7 @@ __global__ __launch_bounds__(64, MC_MIN_WAVES) void mc_kernel(McArgs a, int g) {
     const bool any2 = __any(active && nref == 2);
     stage(rs[0], win);
     __syncthreads();
+    KTL(1);
 
     // everything after staging runs with the rows per lane R as a compile-time constant
     // (min(h, 8) is wave-uniform): no per-row exec masking in the filters and epilogues
@@ -414,6 +415,8 @@ __global__ __launch_bounds__(64, MC_MIN_WAVES) void mc_kernel(McArgs a, int g) {
     if (G.R == 8) finish(std::integral_constant<int, 8>{});
     else if (G.R == 4) finish(std::integral_constant<int, 4>{});
     else finish(std::integral_constant<int, 2>{});
+    KTLV(6, c + (any2 ? 64 : 0));
+    KTL(5);
 }
 
 // Waves per class for one plane group: packed small units or one wave per 64-lane tile.
