@@ -547,19 +547,12 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
     const int bid = xcd_block(blockIdx.x, gridDim.x);
     const int tx = bid % a.tiles_x, tyy = bid / a.tiles_x;
     const int x0 = tx * 64, y0 = tyy * 64;
-    const int fwy = a.bw4 * 4, fhy = a.bh4 * 4;
-    const int fwc = fwy >> SSH, fhc = fhy >> SSV;
-    // the luma tile's loads issue before the unit's strengths are read (their loads would
-    // otherwise delay the tile by a full memory latency; a copy-only unit then re-reads its
-    // pixels from L2)
-    VecTileLoad<Px, 68, 68, NTH> ly;
-#if MI_CDEF_DIAG != 3
-    ly.fetch(a.src[0], a.stride[0], x0, y0, fwy, fhy);
-#endif
     const MiAv1Filter *lf = &a.masks[(tyy >> 1) * a.sb128w + (tx >> 1)];
     const int cdef_idx = lf->cdef_idx[(tyy & 1) * 2 + (tx & 1)];
     const int y_lvl = cdef_idx >= 0 ? a.y_strength[cdef_idx] : 0;
     const int uv_lvl = cdef_idx >= 0 && L ? a.uv_strength[cdef_idx] : 0;
+    const int fwy = a.bw4 * 4, fhy = a.bh4 * 4;
+    const int fwc = fwy >> SSH, fhc = fhy >> SSV;
 
     if (!y_lvl && !uv_lvl) {
         // untouched 64x64 unit: C = D, 8 bytes per lane
@@ -599,8 +592,10 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
         ctaps[threadIdx.x - 8][2] = make_int4(t.sec[4], t.sec[5], t.sec[6], t.sec[7]);
     }
     {
+        VecTileLoad<Px, 68, 68, NTH> ly;
         VecTileLoad<Px, CH + 4, CW + 4, NTH> lu, lv;
 #if MI_CDEF_DIAG != 3
+        ly.fetch(a.src[0], a.stride[0], x0, y0, fwy, fhy);
         if (L && uv_lvl) {
 #else
         if (false) {

@@ -20,10 +20,6 @@ namespace mi {
 constexpr int kLrWin = 80;             // LDS window row stride (int16): columns x0-8 .. x0+71
 constexpr int kWX = 8;                 // window column of x0 (8-px aligned halo: vector staging)
 constexpr int kLrAB = 68;              // A/B row stride
-#ifndef MI_LR_UNIFORM
-#define MI_LR_UNIFORM 0   // 1: A/B row loops with a uniform trip count, out-of-range rows stored to a spare row
-#endif
-constexpr int kAbRows = 66 + MI_LR_UNIFORM;   // A/B rows (+ the spare row of MI_LR_UNIFORM)
 constexpr int kNY = 8;                 // waves (row groups) per workgroup
 constexpr int kNR = 64 / kNY;          // output rows per lane
 constexpr int kNT = 64 * kNY;          // lanes per workgroup
@@ -84,16 +80,7 @@ __device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, u
 #pragma unroll
     for (int k = 0; k < 2 * R; k++) hsum(y0 - R + k, rs0[k], rq0[k], rs1[k], rq1[k]);
     const bool c0 = x >= -1, c1 = x + 1 <= tw;
-#if MI_LR_UNIFORM
-    // every active lane runs `per` rows (no per-row exec masking): a row past the group's end,
-    // or a column past the tile, is stored to the spare row 66
-    for (int kk = 0; kk < per; kk++) {
-        const int y = y0 + kk;
-        const bool vy = y < y1;
-#else
     for (int y = y0; y < y1; y++) {
-        const bool vy = true;
-#endif
         hsum(y + R, rs0[2 * R], rq0[2 * R], rs1[2 * R], rq1[2 * R]);
         if (R == 1 || !((y + 1) & 1)) {
             int sum0 = 0, sq0 = 0, sum1 = 0, sq1 = 0;
@@ -111,18 +98,10 @@ __device__ void sgr_ab(const int16_t *win, int *A, int16_t *B, int sh, int tw, u
                 const unsigned p = (unsigned)max((int)__umul24((unsigned)a, (unsigned)n) - (int)__umul24((unsigned)b, (unsigned)b), 0);
                 const unsigned z = (p * s + (1u << 19)) >> 20;
                 const unsigned xv = xbyx[min(z, 255u)];
-#if MI_LR_UNIFORM
-                {
-                    const int row = vy && on[e] ? y + 1 : 66;
-                    A[row * kLrAB + x + e + 1] = (int)((__umul24(__umul24(xv, one_by_x), (unsigned)sums[e]) + (1u << 11)) >> 12);
-                    B[row * kLrAB + x + e + 1] = (int16_t)xv;
-                }
-#else
                 if (on[e]) {
                     A[(y + 1) * kLrAB + x + e + 1] = (int)((__umul24(__umul24(xv, one_by_x), (unsigned)sums[e]) + (1u << 11)) >> 12);
                     B[(y + 1) * kLrAB + x + e + 1] = (int16_t)xv;
                 }
-#endif
             }
         }
 #pragma unroll
@@ -421,8 +400,8 @@ __device__ __forceinline__ void lr_sgr_tile(int s0, int s1, int w0, int w1, int1
 template <typename Px>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES))) void lr_kernel(LrArgs a) {
     __shared__ __attribute__((aligned(16))) int16_t win[70 * kLrWin];
-    __shared__ __attribute__((aligned(16))) int A[kAbRows * kLrAB];
-    __shared__ __attribute__((aligned(16))) int16_t B[kAbRows * kLrAB];
+    __shared__ __attribute__((aligned(16))) int A[66 * kLrAB];
+    __shared__ __attribute__((aligned(16))) int16_t B[66 * kLrAB];
     int16_t *hor = reinterpret_cast<int16_t *>(A);    // Wiener: [70][64] aliases A
 
     KTL(0);
@@ -477,10 +456,23 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
         u = &a.lr_mask[sbi].lr[p][ui];
         type = u->type;
     }
+    if (type == 0) {   // RESTORATION_NONE: O = C, 8-pixel vectors
+        for (int i = threadIdx.x; i < sh * 8; i += kNT) {
+            const int r = i >> 3, x = x0 + 8 * (i & 7);
+            if (x >= x0 + tw) continue;
+            const Px *sp = reinterpret_cast<const Px *>(C + row_off(S + r, st)) + x;
+            Px *dp = reinterpret_cast<Px *>(O + row_off(S + r, st)) + x;
+            if (x + 8 <= x0 + tw) store8<Px>(dp, load8<Px>(sp));   // O = C
+            else for (int j = 0; j < x0 + tw - x; j++) dp[j] = sp[j];
+        }
+        KTLV(6, 0);
+        KTL(5);
+        return;
+    }
+    KTLV(6, type);
+
     // ---- stage the (sh+6)-row window, columns x0-8 .. x0+71 (C inside the stripe, D across
-    // its edges) as 8-pixel vectors; columns outside the plane replicate the edge pixel. The
-    // tile's restoration type is only tested after the window is staged, so the loads do not
-    // wait for the type's load; a RESTORATION_NONE tile copies its rows out of the window ----
+    // its edges) as 8-pixel vectors; columns outside the plane replicate the edge pixel ----
     const bool have_top = k > 0, have_bottom = E < ph;
     const int wr = sh + 6;
     constexpr int kNV = kLrWin / 8;                   // vectors per window row
@@ -507,7 +499,6 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
             }
         }
     }
-
 #pragma unroll
     for (int q = 0; q < kSV; q++) {
         const int i = threadIdx.x + q * kNT;
@@ -516,20 +507,6 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
     }
     __syncthreads();
     KTL(1);
-    if (type == 0) {   // RESTORATION_NONE: O = C, the window's in-stripe rows as 8-pixel vectors
-        for (int i = threadIdx.x; i < sh * 8; i += kNT) {
-            const int r = i >> 3, c = 8 * (i & 7);
-            if (c >= tw) continue;
-            const uint4 v = *reinterpret_cast<const uint4 *>(&win[(r + 3) * kLrWin + kWX + c]);
-            Px *dp = reinterpret_cast<Px *>(O + row_off(S + r, st)) + x0 + c;
-            if (c + 8 <= tw) store8<Px>(dp, v);
-            else for (int e = 0; e < tw - c; e++) dp[e] = (Px)win[(r + 3) * kLrWin + kWX + c + e];
-        }
-        KTLV(6, 0);
-        KTL(5);
-        return;
-    }
-    KTLV(6, type);
 
     // (the tile filter is written out here rather than through lr_wiener_tile / lr_sgr_tile:
     //  that form measured 70.5 vs 63 us at 4K10 with the same registers and LDS size, most
@@ -579,8 +556,8 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
 template <typename Px>
 __global__ __launch_bounds__(kNT) void lr_call_kernel(LrCallArgs a) {
     __shared__ __attribute__((aligned(16))) int16_t win[70 * kLrWin];
-    __shared__ __attribute__((aligned(16))) int A[kAbRows * kLrAB];
-    __shared__ __attribute__((aligned(16))) int16_t B[kAbRows * kLrAB];
+    __shared__ __attribute__((aligned(16))) int A[66 * kLrAB];
+    __shared__ __attribute__((aligned(16))) int16_t B[66 * kLrAB];
     int16_t *hor = reinterpret_cast<int16_t *>(A);
     const int x0 = blockIdx.x * 64, tw = min(64, a.w - x0), h = a.h;
     const bool hl = a.edges & 1, hr = a.edges & 2, ht = a.edges & 4, hb = a.edges & 8;
