@@ -591,12 +591,9 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
         ctaps[threadIdx.x - 8][1] = make_int4(t.sec[0], t.sec[1], t.sec[2], t.sec[3]);
         ctaps[threadIdx.x - 8][2] = make_int4(t.sec[4], t.sec[5], t.sec[6], t.sec[7]);
     }
-#ifndef MI_CDEF_LATE_UV
-#define MI_CDEF_LATE_UV 0   // 1: the chroma tiles' loads stay in flight through the direction search
-#endif
-    VecTileLoad<Px, CH + 4, CW + 4, NTH> lu, lv;
     {
         VecTileLoad<Px, 68, 68, NTH> ly;
+        VecTileLoad<Px, CH + 4, CW + 4, NTH> lu, lv;
 #if MI_CDEF_DIAG != 3
         ly.fetch(a.src[0], a.stride[0], x0, y0, fwy, fhy);
         if (L && uv_lvl) {
@@ -607,7 +604,7 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
             lv.fetch(a.src[2], a.stride[2], x0 >> SSH, y0 >> SSV, fwc, fhc);
         }
         ly.store(ty, ty + YN, kTS);
-        if (!MI_CDEF_LATE_UV && L && uv_lvl) {
+        if (L && uv_lvl) {
             lu.store(tuv[0], tuv[0] + CN, CTS);
             lv.store(tuv[1], tuv[1] + CN, CTS);
         }
@@ -663,11 +660,6 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
         bdir[b] = (int8_t)dir;
         bflag[b] = (int8_t)flag;
         bstate[b] = (flag & 1) | (y_pri ? dir : 0) << 8 | (y_pri ? pri : 0) << 16;
-    }
-    if (MI_CDEF_LATE_UV && L && uv_lvl) {
-        // (tuv is read only by the chroma filter, after the barrier below)
-        lu.store(tuv[0], tuv[0] + CN, CTS);
-        lv.store(tuv[1], tuv[1] + CN, CTS);
     }
     __syncthreads();
     KTL(3);
