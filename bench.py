@@ -675,9 +675,84 @@ def single_stream(args, world, rank, local):
         dist.destroy_process_group()
 
 
-def main():
+class CudaHw:
+    """The device side of the replica path: one HIP device per rank, RCCL ("nccl") for the
+    control collectives. tests/test_bench_dist.py swaps in a CPU stand-in with the same
+    methods to run main()'s replica path end to end over gloo."""
+    device, backend = "cuda", "nccl"
+
+    def setup(self, local):
+        torch.cuda.set_device(local)
+
+    def pg_kwargs(self, local):
+        return {"device_id": torch.device("cuda", local)}
+
+    def context(self, local):
+        return F.Context(local)
+
+    def pipeline(self, ctx, fr, ring):
+        return Pipeline(ctx, fr, ring=ring)
+
+    def sync(self):
+        torch.cuda.synchronize()
+
+    def stream(self, new=False):
+        return torch.cuda.Stream() if new else torch.cuda.current_stream()
+
+    def oracle_digest(self, fr):
+        return oracle_digest(fr)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`--gpus N` (N > 1) without a launcher: start N ranks as fresh child processes, one per
+    GPU, with the environment torch.distributed.run would give them (rendezvous on 127.0.0.1).
+    This process never touches the GPU (only children initialise HIP), and it exits with the
+    first non-zero exit code of its ranks. Rank 0 prints the JSON line."""
+    import signal
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    codes = [None] * n
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None:
+                codes[i] = p.poll()
+        if any(c not in (None, 0) for c in codes):
+            # one rank failed: the others would wait for it in a collective
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    p.send_signal(signal.SIGTERM)
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    try:
+                        codes[i] = p.wait(30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        codes[i] = p.wait()
+            break
+        time.sleep(0.05)
+    bad = [c for c in codes if c]
+    return bad[0] if bad else 0
+
+
+def parse_args(argv):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (ranks) of this node. Under torch.distributed.run it must equal WORLD_SIZE; "
+                         "without a launcher, N > 1 starts N rank processes itself")
+    ap.add_argument("--frame", default=f"{W}x{H}", help=argparse.SUPPRESS)   # tests: a small frame
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -699,41 +774,63 @@ def main():
     ap.add_argument("--stagger", type=int, default=0, help="with --inflight > 1: frame k's MC waits for frame k-1's")
     ap.add_argument("--mv", choices=["uniform", "coherent"], default="uniform",
                     help="motion field of the timed frame (uniform: SURVEY.md 8(d) config 3)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+
+def main(argv=None, hw=None):
+    """Returns the process exit code. hw: the device side (CudaHw unless a test injects one)."""
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args.gpus, argv)
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    hw = hw or CudaHw()
+    hw.setup(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    stream = torch.cuda.current_stream()
+        dist.init_process_group(hw.backend, **hw.pg_kwargs(local))
 
     if args.single_stream:
-        return single_stream(args, world, rank, local)
+        single_stream(args, world, rank, local)
+        return 0
+    replicas(args, world, rank, local, hw)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
 
-    cfg = broadcast_config({"w": W, "h": H, "bpc": BPC, "layout": LAYOUT,
+
+def replicas(args, world, rank, local, hw):
+    """The headline: every rank decodes its own independent stream (seed + rank) on its own
+    GPU; no data-path collective."""
+    fw, fh = (int(v) for v in args.frame.split("x"))
+    stream = hw.stream()
+    cfg = broadcast_config({"w": fw, "h": fh, "bpc": BPC, "layout": LAYOUT,
                             "seeds": [0x4C100001 + r for r in range(world)]}, world)
     fr = make_frame(cfg["w"], cfg["h"], cfg["bpc"], cfg["layout"], seed=cfg["seeds"][rank], with_fg=False,
                     with_mc=True, mv_mode=args.mv)
-    ctx = F.Context(local)
-    # one pre-filled coefficient arena per timed step (itx consumes and zeroes its arena)
+    ctx = hw.context(local)
+    # one pre-filled coefficient arena per timed step (each step reads a fresh one)
     ring = min(max(args.steps, 1), 512)
-    pipe = Pipeline(ctx, fr, ring=ring)
-    torch.cuda.synchronize()
+    pipe = hw.pipeline(ctx, fr, ring)
+    hw.sync()
 
     for _ in range(args.warmup):
         pipe.step(stream)
-    torch.cuda.synchronize()
+    hw.sync()
     pipe.refill()
 
     # per-kernel timing pass (HIP events on the launch stream), then the clean timed pass
     ev = {}
     for _ in range(max(5, args.steps // 5)):
         pipe.step(stream, ev)
-    torch.cuda.synchronize()
+    hw.sync()
     pipe.refill()
-    torch.cuda.synchronize()
+    hw.sync()
     stage_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
 
     # frames in flight: independent frames on their own streams (and contexts: a context's
@@ -745,15 +842,15 @@ def main():
     n_pipes = max(args.inflight, 2 if args.two_in_flight else 1)
     pipes = [(pipe, stream)]
     for _ in range(n_pipes - 1):
-        pk = Pipeline(F.Context(local), fr, ring=ring)
-        pipes.append((pk, torch.cuda.Stream()))
+        pk = hw.pipeline(hw.context(local), fr, ring)
+        pipes.append((pk, hw.stream(new=True)))
     for pk, sk in pipes[1:]:
         for _ in range(args.warmup):
             pk.step(sk)
-        torch.cuda.synchronize()
+        hw.sync()
         pk.refill()
-    torch.cuda.synchronize()
-    marks = [torch.cuda.Event() for _ in pipes]
+    hw.sync()
+    marks = [torch.cuda.Event() for _ in pipes] if args.stagger else [None] * len(pipes)
 
     def step_k(k):
         def run():
@@ -772,22 +869,22 @@ def main():
         with torch.cuda.graph(graph, stream=cap):
             for pk, _ in pipes[:args.inflight]:
                 pk.step(cap)
-        torch.cuda.synchronize()
+        hw.sync()
         step_fn = graph.replay
         for _ in range(args.warmup):
             step_fn()
-        torch.cuda.synchronize()
-    elapsed = timed_region(step_fn, args.steps, torch.cuda.synchronize, world, "cuda")
+        hw.sync()
+    elapsed = timed_region(step_fn, args.steps, hw.sync, world, hw.device)
     # the picture the last timed step left (every timed step consumed a fresh arena, so it is
     # the frame the oracle computes); checked below with the rank's oracle digest
     timed_digest = pipe.output_digest()
-    want = oracle_digest(fr) if not args.no_verify else None
+    want = hw.oracle_digest(fr) if not args.no_verify else None
     elapsed2, concurrent_ok = None, None
     if args.inflight == 1 and n_pipes >= 2:
         for pk, _ in pipes[:2]:
             pk.refill()
-        torch.cuda.synchronize()
-        elapsed2 = timed_region(step_k(2), args.steps, torch.cuda.synchronize, world, "cuda")
+        hw.sync()
+        elapsed2 = timed_region(step_k(2), args.steps, hw.sync, world, hw.device)
         conc = [pk.output_digest() for pk, _ in pipes[:2]]
         concurrent_ok = conc[0] == conc[1] == (want or timed_digest)
 
@@ -795,14 +892,14 @@ def main():
     # against the oracle on this rank's host cores (outside the timed region)
     pipe.restore()
     pipe.step(stream)
-    torch.cuda.synchronize()
+    hw.sync()
     digest = pipe.output_digest()
     verified = (digest == want and (args.graph or timed_digest == want)) if want is not None else None
     # the other in-flight frames (own buffers, streams and contexts) produce the same picture
     for pk, sk in pipes[1:]:
         pk.restore()
         pk.step(sk)
-        torch.cuda.synchronize()
+        hw.sync()
         if verified is not None:
             verified = verified and pk.output_digest() == digest
     ranks = gather_results({"rank": rank, "frames": args.steps * args.inflight, "ns": int(elapsed * 1e9),
@@ -811,7 +908,7 @@ def main():
     dom = max(stage_ms, key=stage_ms.get)
     achieved = pipe.algo[dom] / (stage_ms[dom] / 1e3) / 1e9
     frames = args.steps * world * args.inflight
-    value = frames * W * H / elapsed / 1e6
+    value = frames * fw * fh / elapsed / 1e6
     if rank == 0:
         out = {
             "metric": "decoded Mpixels/s (4K 10-bit 4:2:0, post-entropy reconstruction DSP)",
@@ -824,7 +921,7 @@ def main():
             "fps": round(frames / elapsed, 2),
             "frames_in_flight": args.inflight,
             "two_frames_in_flight": None if elapsed2 is None else {
-                "value": round(2 * args.steps * world * W * H / elapsed2 / 1e6, 2),
+                "value": round(2 * args.steps * world * fw * fh / elapsed2 / 1e6, 2),
                 "ms_per_step": round(elapsed2 / args.steps * 1e3, 4),
                 "outputs_match_sequential": concurrent_ok,
                 "note": "two independent frames per step on two HIP streams / contexts (frame threading); "
@@ -836,10 +933,11 @@ def main():
             "data": "synthetic (seeded inter-frame descriptors per SURVEY.md §8d config 3: uniformly random MVs, the "
                     "worst case for reference reuse); the reference's real 4K / 1080p inter and intra streams are "
                     "under real_streams",
+            "frame": f"{fw}x{fh}",
             "headline": "kernel-only: every input resident in HBM, one fresh coefficient arena per step; the "
                         "PCIe-inclusive figure (upload + kernels + output copy) is end_to_end_4k10",
             "arena_ring": ring,
-            "config": {"workload": f"4K10 4:2:0 {W}x{H} inter frame: mc (2 refs, 30% compound) + itx residual "
+            "config": {"workload": f"4K10 4:2:0 {fw}x{fh} inter frame: mc (2 refs, 30% compound) + itx residual "
                                    f"+ deblock + cdef + lr",
                        "parallelism": f"replicas{world} (one independent stream per GPU)"},
             "verified": all(r["verified"] for r in ranks) if not args.no_verify else None,
@@ -875,10 +973,8 @@ def main():
             out["real_streams"] = real_streams(ctx)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(fr)
-        print(json.dumps(out))
-    if world > 1:
-        dist.destroy_process_group()
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -128,7 +128,8 @@ int mi_frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, i
  * -EINVAL with *why (if non-NULL) naming the failed check. */
 int mi_frame_validate(const MiDecFrame *f, const MiFramePictures *pics, const char **why);
 /* Diagnostic: mean host time (ms) of mi_frame_run's planning pass over `f` (intra queue order,
- * dependency lists, inter unit buckets, residual bands), reps times; no device work. */
+ * dependency lists, inter unit buckets, residual bands), reps times; no device work. -1.0 when
+ * the work list fails mi_frame_validate's checks (the pictures are not checked). */
 double mi_frame_plan_ms(const MiDecFrame *f, int reps);
 
 /* Wait for the work enqueued on `stream` and report device-side failures of the frame(s):

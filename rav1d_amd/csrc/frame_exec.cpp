@@ -17,6 +17,7 @@
 #include <errno.h>
 #include <stdio.h>
 #include <string.h>
+#include <unistd.h>
 #include <algorithm>
 #include <cstdlib>
 #include <atomic>
@@ -34,28 +35,39 @@ namespace {
 
 // A small pool of host threads for the planning pass of large frames (created on first use,
 // never torn down). One job at a time: a caller that finds the pool busy (another context's
-// frame_run on another host thread) runs its ranges inline.
+// frame_run on another host thread) runs its ranges inline. In a forked child the workers do
+// not exist, so a process other than the pool's creator always runs inline; a range whose
+// worker threw (bad_alloc) is re-run on the calling thread, where the exception reaches the
+// caller as it would in a serial pass.
 class PlanPool {
   public:
-    explicit PlanPool(int n) : n_(n) {
+    explicit PlanPool(int n) : n_(n), pid_(getpid()) {
         for (int t = 1; t < n_; t++) std::thread([this, t] { worker(t); }).detach();
     }
-    int size() const { return n_; }
+    int size() const { return getpid() == pid_ ? n_ : 1; }
     // fn(t) for t in [0, n_) (t = 0 on the calling thread); false: the pool is busy
     bool run(const std::function<void(int)> &fn) {
+        if (getpid() != pid_) return false;
         std::unique_lock<std::mutex> use(use_, std::try_to_lock);
         if (!use.owns_lock()) return false;
         {
             std::lock_guard<std::mutex> g(m_);
             job_ = &fn;
             left_ = n_ - 1;
+            failed_.assign(n_, 0);
             gen_++;
         }
         cv_.notify_all();
         fn(0);
-        std::unique_lock<std::mutex> g(m_);
-        done_.wait(g, [this] { return left_ == 0; });
-        job_ = nullptr;
+        std::vector<char> failed;
+        {
+            std::unique_lock<std::mutex> g(m_);
+            done_.wait(g, [this] { return left_ == 0; });
+            job_ = nullptr;
+            failed.swap(failed_);
+        }
+        for (int t = 1; t < n_; t++)
+            if (failed[t]) fn(t);
         return true;
     }
 
@@ -70,12 +82,20 @@ class PlanPool {
                 seen = gen_;
                 job = job_;
             }
-            (*job)(t);
+            bool ok = true;
+            try {
+                (*job)(t);
+            } catch (...) {
+                ok = false;
+            }
             std::lock_guard<std::mutex> g(m_);
+            if (!ok) failed_[t] = 1;
             if (--left_ == 0) done_.notify_one();
         }
     }
     const int n_;
+    const pid_t pid_;
+    std::vector<char> failed_;
     std::mutex use_, m_;
     std::condition_variable cv_, done_;
     const std::function<void(int)> *job_ = nullptr;
@@ -84,11 +104,7 @@ class PlanPool {
 };
 
 PlanPool *plan_pool() {
-    static PlanPool *pool = [] {
-        const char *e = getenv("MI_FX_THREADS");
-        const int t = e ? atoi(e) : (int)std::thread::hardware_concurrency();
-        return new PlanPool(std::max(1, std::min(t, 8)));
-    }();
+    static PlanPool *pool = new PlanPool(std::max(1, std::min((int)std::thread::hardware_concurrency(), 8)));
     return pool;
 }
 
@@ -279,18 +295,28 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
     if (f->layout < 0 || f->layout > 3 || f->w <= 0 || f->h <= 0) return BAD();
     // super-resolution (up_w > w): every picture has the upscaled geometry
     if (f->up_w < f->w || f->up_w > 2 * f->w + 16) return BAD();
-    const MiPicture *pics[4] = { &p->recon, &p->deblocked, &p->cdef, &p->restored };
-    for (const MiPicture *q : pics)
-        if (q->bpc != f->bpc || q->layout != f->layout || q->w != f->up_w || q->h != f->h || !q->data[0] ||
-            (f->layout && (!q->data[1] || !q->data[2])) || q->stride[0] != p->recon.stride[0] ||
-            q->stride[1] != p->recon.stride[1])
-            return BAD();
     const int ss_hor = f->layout == 1 || f->layout == 2, ss_ver = f->layout == 1;
     const int nplanes = f->layout ? 3 : 1;
     const int aw = (f->w + 127) & ~127, ah = (f->h + 127) & ~127, aw_up = (f->up_w + 127) & ~127;
     const size_t pb = f->bpc == 8 ? 1 : 2;
-    for (int pl = 0; pl < nplanes; pl++)
-        if ((size_t)std::abs(p->recon.stride[pl ? 1 : 0]) < (size_t)(aw_up >> (pl ? ss_hor : 0)) * pb) return BAD();
+    if (p) {   // (nullptr: the work list alone, as mi_frame_plan_ms checks it)
+        const MiPicture *pics[4] = { &p->recon, &p->deblocked, &p->cdef, &p->restored };
+        for (const MiPicture *q : pics)
+            if (q->bpc != f->bpc || q->layout != f->layout || q->w != f->up_w || q->h != f->h || !q->data[0] ||
+                (f->layout && (!q->data[1] || !q->data[2])) || q->stride[0] != p->recon.stride[0] ||
+                q->stride[1] != p->recon.stride[1])
+                return BAD();
+        for (int pl = 0; pl < nplanes; pl++)
+            if ((size_t)std::abs(p->recon.stride[pl ? 1 : 0]) < (size_t)(aw_up >> (pl ? ss_hor : 0)) * pb) return BAD();
+        // loop restoration takes positive strides below 2^24 and planes below 4 GB (mi_lr_frame
+        // makes the same check; made here too so that nothing is enqueued before it fails)
+        if (f->restore_planes)
+            for (int pl = 0; pl < nplanes; pl++) {
+                const int64_t st = p->recon.stride[pl ? 1 : 0];
+                const int64_t ph = pl ? (f->h + ss_ver) >> ss_ver : f->h;
+                if (st <= 0 || st >= (1 << 24) || ph * st >= (1LL << 32)) return BAD();
+            }
+    }
     // every array a count refers to is present (they are copied from during the call)
     if (f->n_intra < 0 || (f->n_intra && (!f->intra || !f->intra_tx || !f->dep_start))) return BAD();
     if (f->n_deps < 0 || (f->n_deps && !f->deps) || (f->ncoef && !f->coef) || (f->nidx && !f->idx) ||
@@ -427,14 +453,23 @@ int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<in
         ph4[p] = (p ? ah >> ssv : ah) >> 2;
         own[p].assign((size_t)pw4[p] * ph4[p], -1);
     }
-    // (blocks of one plane never overlap: the owner map fills in any order, on several threads)
+    // The owner of a cell is its LAST writer in decode order: an inter-intra item and the
+    // residual items over the same rectangle (MI_INTRA_II then MI_INTRA_RESID) overlap, and the
+    // residual must win. Several threads fill the map, so each cell keeps the maximum index
+    // (a relaxed CAS loop; the pool's join orders it before the reads below).
     parallel_ranges(n, 32768, [&](int lo, int hi, int) {
         for (int i = lo; i < hi; i++) {
             const MiIntraBlock &b = f->intra[i];
             const int xl = b.plane ? b.x << ssh : b.x;
             strip[i] = (int8_t)(std::upper_bound(sx.begin(), sx.end(), xl) - sx.begin() - 1);
             for (int y = b.y >> 2; y < (b.y + b.h) >> 2; y++)
-                for (int x = b.x >> 2; x < (b.x + b.w) >> 2; x++) own[b.plane][(size_t)y * pw4[b.plane] + x] = i;
+                for (int x = b.x >> 2; x < (b.x + b.w) >> 2; x++) {
+                    int32_t *cell = &own[b.plane][(size_t)y * pw4[b.plane] + x];
+                    int32_t cur = __atomic_load_n(cell, __ATOMIC_RELAXED);
+                    while (cur < i && !__atomic_compare_exchange_n(cell, &cur, i, true, __ATOMIC_RELAXED,
+                                                                   __ATOMIC_RELAXED)) {
+                    }
+                }
         }
     });
     xs.assign(n + 1, 0);
@@ -1096,6 +1131,9 @@ int mi_frame_validate(const MiDecFrame *f, const MiFramePictures *pics, const ch
 
 double mi_frame_plan_ms(const MiDecFrame *f, int reps) {
     if (!f || reps < 1) return -1.0;
+    // the work list's own checks (mi_frame_run's, without the pictures): plan_frame indexes the
+    // owner map, levels and CSR arrays by the list's coordinates and dependency indices
+    if (validate(f, nullptr)) return -1.0;
     bool scaled[7] = {};
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
