@@ -64,14 +64,12 @@ class Pipeline:
             self.mc = F.McMeta(*fr["mc"])
             self.ref_pics = (F.MiPicture * len(self.refs))(*[r.picture() for r in self.refs])
         self.blocks = torch.from_numpy(fr["blocks"].view(np.uint8).copy()).cuda()
-        # itx over picture bands, one XCD per band (mi_itx_frame_banded); MI_ITX_BANDED=0: by size only
-        self.itx_bands = None
-        if os.environ.get("MI_ITX_BANDED", "1") != "0":
-            ah = (h + 127) & ~127
-            ssv = 1 if lay == 1 else 0
-            blk, _, bs = itx_band_order(fr["blocks"], [ah, ah >> ssv, ah >> ssv])
-            self.blocks = torch.from_numpy(blk.view(np.uint8).copy()).cuda()
-            self.itx_bands = (ctypes.c_uint32 * bs.size)(*[int(v) for v in bs.reshape(-1)])
+        # itx over picture bands, one XCD per band (mi_itx_frame_banded, as the frame executor runs it)
+        ah = (h + 127) & ~127
+        ssv = 1 if lay == 1 else 0
+        blk, _, bs = itx_band_order(fr["blocks"], [ah, ah >> ssv, ah >> ssv])
+        self.blocks = torch.from_numpy(blk.view(np.uint8).copy()).cuda()
+        self.itx_bands = (ctypes.c_uint32 * bs.size)(*[int(v) for v in bs.reshape(-1)])
         self.coef = torch.from_numpy(fr["coef"].copy()).cuda()
         self.coef0 = self.coef.clone()               # itx zeroes the arena it consumes
         self.coefs = [self.coef] + [self.coef0.clone() for _ in range(max(1, ring) - 1)]
@@ -137,15 +135,10 @@ class Pipeline:
                                                         ctypes.c_void_p(self.mc.masks.data_ptr()), None, sp), "mc"))
         if mark is not None:
             mark.record(stream)
-        ss = (ctypes.c_uint32 * 20)(*[int(v) for v in self.fr["size_start"]])
         coef = self.coefs[self.k % len(self.coefs)]
         self.k += 1
-        if self.itx_bands is not None:
-            timed("itx", lambda: F.check(lib.mi_itx_frame_banded(ctx, ctypes.byref(pa), ctypes.c_void_p(self.blocks.data_ptr()),
-                                                                 self.itx_bands, ctypes.c_void_p(coef.data_ptr()), ITX_KEEP_COEFS, sp), "itx"))
-        else:
-            timed("itx", lambda: F.check(lib.mi_itx_frame(ctx, ctypes.byref(pa), ctypes.c_void_p(self.blocks.data_ptr()),
-                                                          ss, ctypes.c_void_p(coef.data_ptr()), ITX_KEEP_COEFS, sp), "itx"))
+        timed("itx", lambda: F.check(lib.mi_itx_frame_banded(ctx, ctypes.byref(pa), ctypes.c_void_p(self.blocks.data_ptr()),
+                                                             self.itx_bands, ctypes.c_void_p(coef.data_ptr()), ITX_KEEP_COEFS, sp), "itx"))
         timed("deblock", lambda: F.check(lib.mi_deblock_frame_to(ctx, ctypes.byref(pa), ctypes.byref(pd),
                                                                  ctypes.byref(self.lf.s), sp), "lf"))
         timed("cdef", lambda: F.check(lib.mi_cdef_frame(ctx, ctypes.byref(pd), ctypes.byref(pb),

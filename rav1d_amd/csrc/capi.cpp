@@ -439,15 +439,6 @@ int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, v
     return r ? fail(ctx, -EIO) : 0;
 }
 
-// Loop restoration over picture bands, one XCD per band (LrArgs.banded); MI_LR_BANDS=0 turns it off
-static int lr_banded() {
-    static const int v = [] {
-        const char *e = getenv("MI_LR_BANDS");
-        return e ? atoi(e) : 0;   // 1 bands, 2 contiguous eighths of the tile order per XCD
-    }();
-    return v;
-}
-
 int mi_deblock_frame_to(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const MiLoopFilter *lf,
                         void *stream) {
     if (!ctx || !src || !dst || !lf) return fail(ctx, -EINVAL);
@@ -585,18 +576,8 @@ int mi_lr_frame(MiCtx *ctx, const MiPicture *cdef, const MiPicture *deblocked, c
         // stripes: 64 luma rows, the first 56 (lr_apply.rs:54)
         int stripes = 0;
         while ((stripes ? (64 * stripes - 8) >> sv : 0) < a.ph[p]) stripes++;
-        a.stripes[p] = stripes;
-        if (lr_banded() == 1) {
-            // band q = stripes [q * stripes / 8, (q + 1) * stripes / 8)
-            int m = 0;
-            for (int q = 0; q < 8; q++) m = std::max(m, ((q + 1) * stripes / 8 - q * stripes / 8) * a.tiles_x[p]);
-            a.band_m[p] = m;
-            nb += 8 * m;
-        } else {
-            nb += stripes * a.tiles_x[p];
-        }
+        nb += stripes * a.tiles_x[p];
     }
-    a.banded = lr_banded();
     a.blk_start[3] = nb;
     const int r = mi::launch_lr(a, cdef->bpc, (hipStream_t)stream);
     return r ? fail(ctx, -EIO) : 0;
@@ -1699,8 +1680,7 @@ int intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, const int32
     const int per_xcd = (nq + 7) / 8;
     int n_xcd = 0;
     for (int q = 0; q < nq && q < 8; q++) n_xcd = std::max(n_xcd, a.fr[q].n);
-    static const int wenv = getenv("MI_IR_WORKERS") ? atoi(getenv("MI_IR_WORKERS")) : 0;
-    const int wpx = wenv ? wenv : std::min(256, std::max(128, std::min(192, n_xcd / 96)) + 64 * (per_xcd - 1));
+    const int wpx = std::min(256, std::max(128, std::min(192, n_xcd / 96)) + 64 * (per_xcd - 1));
     return mi::launch_intra_recon(a, bpc, wpx, s) ? fail(ctx, -EIO) : 0;
 }
 

@@ -29,13 +29,6 @@ __device__ __forceinline__ int dir_off(int dir, int k, int ts) {
     return k == 0 ? nib(DY0, dir) * ts + nib(DX0, dir) : nib(DY1, dir) * ts + nib(DX1, dir);
 }
 
-#ifndef MI_CDEF_T1
-#define MI_CDEF_T1 1     // 0: no shifted copy, odd taps read unaligned words
-#endif
-#ifndef MI_CDEF_DIAG
-#define MI_CDEF_DIAG 0   // experiment builds only: 1 no filtering, 2 no filtering or direction search, 3 no tile fetch,
-                         // 4 no chroma filter, 5 no luma filter
-#endif
 // Luma tile: 68 rows (2-row halo) x 88 int16 (frame columns x0-8 .. x0+79; interior at column 8).
 // 88 = 44 dwords per row: a 32-lane group's 8 rows x 4 dwords fall on 32 distinct banks, and
 // every 8-px block row is 16-B aligned for ds_read_b128.
@@ -298,7 +291,6 @@ struct VecTileLoad {
             const int r = i / NV, j = i - r * NV;
             int16_t *tr = t + r * ts + 8 * j, *t1r = t1 + r * ts + 8 * j;
             *reinterpret_cast<uint4 *>(tr) = make_uint4(w[k][0], w[k][1], w[k][2], w[k][3]);
-            if (!MI_CDEF_T1) continue;
             *reinterpret_cast<uint3 *>(t1r) = make_uint3((w[k][0] >> 16) | (w[k][1] << 16),
                                                          (w[k][1] >> 16) | (w[k][2] << 16),
                                                          (w[k][2] >> 16) | (w[k][3] << 16));
@@ -524,16 +516,13 @@ __device__ __forceinline__ void filter_luma(const int16_t *T, const int4 (*taps)
 // direction in the search, 34 KB of LDS for four workgroups = 32 waves per CU). L = layout (0 I400,
 // 1 I420, 2 I422, 3 I444), compile-time so every tile index is a shift or a constant divide.
 template <typename Px, int L>
-#ifndef MI_CDEF_MINW
-#define MI_CDEF_MINW 8
-#endif
-__global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
+__global__ __launch_bounds__(512, 8) void cdef_kernel(CdefArgs a) {
     constexpr int NTH = 512;
     constexpr int SSH = L == 1 || L == 2, SSV = L == 1;
     constexpr int CW = 64 >> SSH, CH = 64 >> SSV, CTS = CW == 64 ? 88 : 48;   // 24-dword rows: two rows 2 apart are 16 banks apart
     constexpr int UVW = 8 >> SSH, UVH = 8 >> SSV;
     constexpr int YN = kTY * kTS, CN = L ? (CH + 4) * CTS : 2;
-    constexpr int NT = MI_CDEF_T1 ? 2 : 1;
+    constexpr int NT = 2;
     __shared__ __align__(16) int16_t ty[NT * YN];              // T, T1
     __shared__ __align__(16) int16_t tuv[2][NT * CN];          // per chroma plane: T, T1
     __shared__ int8_t bdir[64];
@@ -580,13 +569,13 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
 
     if (threadIdx.x < 8) {
         PairTaps t;
-        make_taps<kTS, MI_CDEF_T1 ? YN * 2 : 2>(t, threadIdx.x);
+        make_taps<kTS, YN * 2>(t, threadIdx.x);
         ytaps[threadIdx.x][0] = make_int4(t.pri[0], t.pri[1], t.pri[2], t.pri[3]);
         ytaps[threadIdx.x][1] = make_int4(t.sec[0], t.sec[1], t.sec[2], t.sec[3]);
         ytaps[threadIdx.x][2] = make_int4(t.sec[4], t.sec[5], t.sec[6], t.sec[7]);
     } else if (L == 1 && threadIdx.x < 16) {
         PairTaps t;
-        make_taps<CTS, MI_CDEF_T1 ? CN * 2 : 2>(t, threadIdx.x - 8);
+        make_taps<CTS, CN * 2>(t, threadIdx.x - 8);
         ctaps[threadIdx.x - 8][0] = make_int4(t.pri[0], t.pri[1], t.pri[2], t.pri[3]);
         ctaps[threadIdx.x - 8][1] = make_int4(t.sec[0], t.sec[1], t.sec[2], t.sec[3]);
         ctaps[threadIdx.x - 8][2] = make_int4(t.sec[4], t.sec[5], t.sec[6], t.sec[7]);
@@ -594,12 +583,8 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
     {
         VecTileLoad<Px, 68, 68, NTH> ly;
         VecTileLoad<Px, CH + 4, CW + 4, NTH> lu, lv;
-#if MI_CDEF_DIAG != 3
         ly.fetch(a.src[0], a.stride[0], x0, y0, fwy, fhy);
         if (L && uv_lvl) {
-#else
-        if (false) {
-#endif
             lu.fetch(a.src[1], a.stride[1], x0 >> SSH, y0 >> SSV, fwc, fhc);
             lv.fetch(a.src[2], a.stride[2], x0 >> SSH, y0 >> SSV, fwc, fhc);
         }
@@ -612,7 +597,7 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
     __syncthreads();
     KTL(1);
 
-    if (MI_CDEF_DIAG != 2 && (y_pri || uv_pri)) {
+    if (y_pri || uv_pri) {
         const int b = threadIdx.x & 63, w = threadIdx.x >> 6;   // wave-uniform direction
         const int16_t *tb = ty + ((b >> 3) * 8 + 2) * kTS + (b & 7) * 8 + 8;
         unsigned c;
@@ -656,7 +641,6 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
                 if (uv_lvl) flag |= 2;
             }
         }
-        if (MI_CDEF_DIAG == 1 || MI_CDEF_DIAG == 2) flag = 0;
         bdir[b] = (int8_t)dir;
         bflag[b] = (int8_t)flag;
         bstate[b] = (flag & 1) | (y_pri ? dir : 0) << 8 | (y_pri ? pri : 0) << 16;
@@ -665,22 +649,18 @@ __global__ __launch_bounds__(512, MI_CDEF_MINW) void cdef_kernel(CdefArgs a) {
     KTL(3);
 
     // luma: 2048 pairs, one 8x8 block per 32-lane group at a time
-    if (MI_CDEF_DIAG != 5)
-        filter_luma<Px, kTS>(ty, ytaps, bstate, y_sec, a.damping, bdm8, a.src[0], a.dst[0], a.stride[0],
+    filter_luma<Px, kTS>(ty, ytaps, bstate, y_sec, a.damping, bdm8, a.src[0], a.dst[0], a.stride[0],
                              x0, y0, fwy, fhy);
     KTL(4);
-    if (L && MI_CDEF_DIAG != 4) {
+    if (L) {
         // chroma: lanes 0..255 U, 256..511 V (damping - 1, cdef_apply.rs)
         const int p = 1 + (threadIdx.x >> 8);
         // (the chroma tile is only staged when uv_lvl != 0: unfiltered chroma copies from D)
-#ifndef MI_CDEF_C420
-#define MI_CDEF_C420 1
-#endif
-        if constexpr (L == 1 && MI_CDEF_C420)
+        if constexpr (L == 1)
             filter_chroma420<Px, CTS>(tuv[p - 1], ctaps, bdir, bflag, uv_pri, uv_sec, a.damping - 1, bdm8,
                                       a.src[p], a.dst[p], a.stride[p], x0 >> SSH, y0 >> SSV);
         else
-            filter_plane<Px, CW, CH, UVW, UVH, 256, CTS, MI_CDEF_T1 ? CN * 2 : 2, 2, false>(
+            filter_plane<Px, CW, CH, UVW, UVH, 256, CTS, CN * 2, 2, false>(
                 tuv[p - 1], threadIdx.x & 255, bdir, bflag, nullptr, false, uv_pri, uv_sec, a.damping - 1, bdm8,
                 L == 2, a.src[p], a.dst[p], a.stride[p], x0 >> SSH, y0 >> SSV, fwc, fhc);
     }

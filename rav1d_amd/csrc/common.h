@@ -63,24 +63,8 @@ __device__ __forceinline__ T karg_at(size_t off) {
 // with it (their cost per workgroup varies along the list, so equal-count chunks per XCD end
 // unevenly), so they keep the hardware order.
 __device__ inline int xcd_block(int b, int n) {
-#ifdef MI_NO_XCD_REMAP
-    (void)n;
-    return b;
-#else
     const int x = b & 7, q = n >> 3, r = n & 7;
     return x * q + (x < r ? x : r) + (b >> 3);
-#endif
-}
-
-// Chunked XCD interleave: XCD b % 8 processes runs of C consecutive work items, the runs dealt
-// round robin over the XCDs. Neighbouring items (spatially sorted units) share one L2 while
-// every XCD still samples the whole list (balanced where the cost per item drifts along
-// it). Bijective on [0, n): whole rounds of 8 * C items are permuted, the tail is identity.
-__device__ inline int xcd_chunk(int b, int n, int C) {
-    const int full = n / (8 * C) * (8 * C);
-    if (b >= full || C <= 1) return b;
-    const int x = b & 7, r = b >> 3;
-    return ((r / C) * 8 + x) * C + (r % C);
 }
 
 // RectTxfmSize -> dimensions (src/levels.rs:46-82) and the inverse-transform row shift
@@ -101,30 +85,15 @@ __host__ __device__ constexpr int imax_c(int a, int b) { return a > b ? a : b; }
 // Lanes per transform block in the itx kernel: one lane per row in the row pass, one lane
 // per column in the column pass.
 __host__ __device__ constexpr int itx_lanes(int tx) {
-#ifndef MI_ITX_PAIR64
-#define MI_ITX_PAIR64 0
-#endif
-    // 64-point sizes (itx.hip itx_size64): a 64-point transform runs on a lane pair, so the
-    // row pass takes 2 lanes per 64-wide row and the column pass 2 per 64-tall column
-    if (MI_ITX_PAIR64 && (tx_dim(tx).w == 64 || tx_dim(tx).h == 64))
-        return imax_c(imin_c(tx_dim(tx).h, 32) * (tx_dim(tx).w == 64 ? 2 : 1),
-                      tx_dim(tx).w * (tx_dim(tx).h == 64 ? 2 : 1));
     return imax_c(imin_c(tx_dim(tx).h, 32), tx_dim(tx).w);
 }
-#ifndef MI_ITX_THREADS
-#define MI_ITX_THREADS 64   // one-wave workgroups: 4K10 itx 34.1 -> 30.2 us (no cross-wave barriers; r04)
-#endif
-constexpr int kItxThreads = MI_ITX_THREADS;
+// one-wave workgroups: 4K10 itx 34.1 -> 30.2 us (no cross-wave barriers; r04)
+constexpr int kItxThreads = 64;
 __host__ __device__ constexpr int itx_blocks_per_wg(int tx) { return kItxThreads / itx_lanes(tx); }
 // Rounds of itx_blocks_per_wg blocks per workgroup: the small sizes' loads of all rounds are in
-// flight together (4-lane blocks: 4 rounds; 8-lane blocks: 1).
-#ifndef MI_ITX_ROUNDS4
-#define MI_ITX_ROUNDS4 4
-#endif
-#ifndef MI_ITX_ROUNDS8
-#define MI_ITX_ROUNDS8 1   // 8-lane sizes: 1 round (banded grid, 4K10: 49.8 vs 50.7-51.3 us with 2; 4 rounds 56-58)
-#endif
-__host__ __device__ constexpr int itx_rounds(int tx) { return itx_lanes(tx) <= 4 ? MI_ITX_ROUNDS4 : itx_lanes(tx) <= 8 ? MI_ITX_ROUNDS8 : 1; }
+// flight together (4-lane blocks: 4 rounds; 8-lane blocks: 1 (banded grid, 4K10: 49.8 vs
+// 50.7-51.3 us with 2; 4 rounds 56-58)).
+__host__ __device__ constexpr int itx_rounds(int tx) { return itx_lanes(tx) <= 4 ? 4 : 1; }
 
 // Which transform types are legal for a size (src/itx.rs:400-457): 16 types for sizes up to
 // 16 on both sides except 16x16 (12 types), DCT_DCT + IDTX when a side is 32, DCT_DCT only
@@ -155,16 +124,6 @@ struct ItxArgs {
     // the band is fetched into, and written back from, one XCD's L2 whichever sizes touch it
     int band_start[19][9];
     int nbands;         // 1 or 8
-    // rounds (banded grid): the grid runs in nrounds rounds; round r holds, for every size in
-    // launch order, the band workgroups k in [r*m/R, (r+1)*m/R) (m = m_size[size], the size's
-    // workgroups per band). With each (size, band) list ordered by sub-band (one of R per band)
-    // first, round r covers about sub-band r of every band with all sizes, so the blocks of
-    // different sizes sharing a pixel line run close in time and the line is read and written
-    // back once instead of once per size (partially written lines evicted between sizes cost
-    // 1.75x the algorithmic writes at 4K10)
-    int nrounds;
-    int m_size[19];
-    int round_start[17];
     int pw[3], ph[3];   // plane extents (128-aligned picture area; 0 = no such plane)
     int *err;           // device error word: set when a descriptor is rejected
 };
@@ -181,12 +140,6 @@ __host__ __device__ constexpr uint32_t itx_legal_types(int tx) {
 // then the 32-point sizes, then every size with both sides <= 16
 constexpr int kItxLaunchOrder[19] = { 4, 11, 12, 17, 18, 3, 9, 10, 15, 16, 0, 1, 2, 5, 6, 7, 8, 13, 14 };
 constexpr int kItxBands = 8;
-#ifndef MI_ITX_NROUNDS
-#define MI_ITX_NROUNDS 1   // rounds of the banded grid (1: sizes one after the other; 4 or 8 cut HBM
-                           // traffic 96 -> 82 MB at 4K10 but ran 20 % slower: sizes interleaved)
-#endif
-constexpr int kItxRounds = MI_ITX_NROUNDS;
-static_assert(kItxRounds >= 1 && kItxRounds <= 16, "rounds");
 // fills wg_start / wg_size / blk_start (and the band table when band_start, [19][9], is given);
 // returns the grid size
 int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start, const uint32_t *band_start = nullptr);
@@ -351,11 +304,6 @@ struct LrArgs {
     int unit_log2[2];
     int pw[3], ph[3], tw[3], tiles_x[3];
     int blk_start[4];
-    // banded grid (MI_LR_BANDS): plane p's stripes in 8 bands of consecutive stripes, band q's
-    // tiles at grid indices = q mod 8 (XCD q under the dispatcher's round robin), so the column
-    // halo lines neighbouring tiles share are fetched into one L2; stripes[p] = stripe count,
-    // band_m[p] = workgroups per band (the largest band's tile count)
-    int stripes[3], band_m[3], banded;
 };
 // launchers (lr.hip)
 int launch_lr(const LrArgs &a, int bpc, hipStream_t s);
@@ -375,10 +323,7 @@ struct LrCallArgs {
 };
 int launch_lr_call(const LrCallArgs &a, int bpc, hipStream_t s);
 
-#ifndef MI_FG_ITEMS
-#define MI_FG_ITEMS 1
-#endif
-constexpr int kFgItems = MI_FG_ITEMS;   // wave-items (512-px row segments) per wave in fg_apply_kernel (8K10 apply: 1 -> 72.5 us, 4 -> 75.7, 8 -> 78.4)
+constexpr int kFgItems = 1;   // wave-items (512-px row segments) per wave in fg_apply_kernel (8K10 apply: 1 -> 72.5 us, 4 -> 75.7, 8 -> 78.4)
 
 struct FgArgs {
     MiFilmGrainData data;

@@ -413,10 +413,9 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
 // the picture only for intra block copy and CfL's luma: edges need no extra deps.
 int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<int32_t> &xs,
                  std::vector<int32_t> &xd, bool granules) {
-    static const int env = getenv("MI_IR_STRIPS") ? atoi(getenv("MI_IR_STRIPS")) : 8;
     const int n = f->n_intra;
-    const int maxs = std::min(8, env);
-    if (maxs < 2 || n < 64) return 1;
+    const int maxs = 8;
+    if (n < 64) return 1;
     const int pxb = f->bpc == 8 ? 1 : 2;
     const int ssh = f->layout == 1 || f->layout == 2, ssv = f->layout == 1;
     const int nplanes = f->layout ? 3 : 1;
@@ -732,14 +731,10 @@ void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
     // edge granules (ipred.hip gran_fetch) when every pixel an intra edge reads is written in the
     // same launch: no inter units, no inter-intra blends or inter residuals. A block then waits
     // on flags only for the pixels it reads beyond its edges (CfL's luma, intra block copy's
-    // source); the levels still follow every dependency. MI_IR_GRANULES=0 turns them off.
-    static const bool gran_env = [] {
-        const char *e = getenv("MI_IR_GRANULES");
-        return !(e && e[0] == '0');
-    }();
+    // source); the levels still follow every dependency.
     const bool inter = pl.inter = inter_present(f) || f->n_inter_tx;
     bool &granules = pl.granules;
-    granules = gran_env && !inter && n > 0;
+    granules = !inter && n > 0;
     // MI_IR_TIMELINE=<file> (diagnostics): the launch's per-unit stamps, blocks and dependencies
     static const char *tl_path = getenv("MI_IR_TIMELINE");
     for (int i = 0; granules && i < n; i++)
@@ -764,8 +759,7 @@ void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
         pos.resize(n);
         int maxl = 0;
         // MI_IR_NOLEVELS=1 (experiment): decode order within a strip, no level pass
-        static const bool nolevels = [] { const char *e = getenv("MI_IR_NOLEVELS"); return e && e[0] == '1'; }();
-        for (int i = 0; i < n && !nolevels; i++) {
+        for (int i = 0; i < n; i++) {
             int l = 0;
             each_dep(i, [&](int d) { l = std::max(l, level[d] + 1); });
             level[i] = l;
@@ -856,8 +850,7 @@ void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
     uint32_t (&itx_bs)[MI_N_RECT_TX_SIZES][MI_ITX_BANDS + 1] = pl.itx_bs;
     memset(itx_bs, 0, sizeof(itx_bs));
     {
-        // (tx size, band, sub-band): sub-band r of a band goes with round r of the grid
-        constexpr int NF = MI_ITX_BANDS * mi::kItxRounds;         // fine bands per plane
+        constexpr int NF = MI_ITX_BANDS;                           // bands per plane
         constexpr int NK = MI_N_RECT_TX_SIZES * NF;
         const int ah = (f->h + 127) & ~127, ssv = f->layout == 1;
         auto key = [&](const MiTxBlock &b) {
@@ -869,7 +862,7 @@ void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
         for (int i = 0; i < f->n_inter_tx; i++) start[key(f->inter_tx[i]) + 1]++;
         for (int k = 0; k < NK; k++) start[k + 1] += start[k];
         for (int t = 0; t < MI_N_RECT_TX_SIZES; t++)
-            for (int q = 0; q <= MI_ITX_BANDS; q++) itx_bs[t][q] = start[t * NF + q * mi::kItxRounds];
+            for (int q = 0; q <= MI_ITX_BANDS; q++) itx_bs[t][q] = start[t * NF + q];
         for (int i = 0; i < f->n_inter_tx; i++) itx_b[start[key(f->inter_tx[i])]++] = f->inter_tx[i];
     }
 }
@@ -982,16 +975,8 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
                                                        (int)lap_s[k].size(), tmp, stream)))
                 return r;
         }
-#ifndef MI_FX_ITX_BANDED
-#define MI_FX_ITX_BANDED 1
-#endif
-        uint32_t itx_ss[MI_N_RECT_TX_SIZES + 1];
-        for (int t = 0; t < MI_N_RECT_TX_SIZES; t++) itx_ss[t] = itx_bs[t][0];
-        itx_ss[MI_N_RECT_TX_SIZES] = itx_bs[MI_N_RECT_TX_SIZES - 1][MI_ITX_BANDS];
         if (f->n_inter_tx &&
-            (r = MI_FX_ITX_BANDED
-                     ? mi_itx_frame_banded(ctx, &cur, (const MiTxBlock *)D(20), itx_bs, D(4), MI_ITX_KEEP_COEFS, stream)
-                     : mi_itx_frame(ctx, &cur, (const MiTxBlock *)D(20), itx_ss, D(4), MI_ITX_KEEP_COEFS, stream)))
+            (r = mi_itx_frame_banded(ctx, &cur, (const MiTxBlock *)D(20), itx_bs, D(4), MI_ITX_KEEP_COEFS, stream)))
             return r;
     }
 

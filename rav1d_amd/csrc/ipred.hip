@@ -111,13 +111,6 @@ __device__ __forceinline__ uint8_t *plane_ptr(const IpredArgs &a, int p) {
 }
 __device__ __forceinline__ int64_t plane_stride(const IpredArgs &a, int p) { return p ? a.stride[1] : a.stride[0]; }
 
-#ifdef MI_IR_EXP_DCSTAMP
-// (experiment: DC-path stamps k into the edge scratch eb[240 + 2k], read back by the kernel)
-#define DCSTAMP(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); \
-    if (threadIdx.x == 0) { eb[240 + 2 * (k)] = (int)t_; eb[241 + 2 * (k)] = (int)(t_ >> 32); } } while (0)
-#else
-#define DCSTAMP(k) do {} while (0)
-#endif
 // DC_PRED / LEFT_DC / TOP_DC (m 0 / 3 / 4) from the sum s of the edge samples they average
 // (ipred_tmpl.c:86-160: the 1/3 and 1/5 multipliers of rectangular blocks)
 __device__ __forceinline__ int dc_of_sum(int m, int s, int w, int h, int bpc) {
@@ -172,7 +165,6 @@ __device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredB
     const int m = cfl ? mode - MI_IPRED_CFL : mode;
     if (m == 0 || m == 3 || m == 4 || m == 5) {
         // DC family (ipred_tmpl.c:86-218) -> splat or CfL
-        DCSTAMP(0);
         int dc;
         if (m == 5) {
             dc = (bdmax + 1) >> 1;
@@ -192,10 +184,8 @@ __device__ __forceinline__ void predict_block(const IpredArgs &a, const MiIpredB
             }
             dc = dc_of_sum(m, s, w, h, a.bpc);
         }
-        DCSTAMP(1);
         if (!cfl) {
             for (int i = lane; i < n; i += 64) put((i >> lw), (i & (w - 1)), dc);
-            DCSTAMP(2);
         } else {
             const int16_t *ac = acl ? acl : a.ac + b.aux_off;
             const int alpha = b.alpha;
@@ -568,9 +558,6 @@ __device__ __forceinline__ void gran_fetch(const GranCtx &g, int x, int y, const
             break;
         }
     }
-#ifdef MI_IR_EXP_DRAIN
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
 }
 
 // intra_block's result: MI_IR_TIMELINE stamps, and the value of a plain DC-family block that
@@ -1087,10 +1074,6 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
                                                      gran != nullptr, gc, tl_base != 0);
             dcv = o.dcv;
             if (lane >= 7 && lane <= 10) tl_v = o.tlx;
-#ifdef MI_IR_EXP_DCSTAMP
-            if (lane >= 11 && lane <= 13)
-                tl_v = (unsigned)eb[240 + 2 * (lane - 11)] | ((unsigned long long)(unsigned)eb[241 + 2 * (lane - 11)] << 32);
-#endif
         }
         // pixel (yy, xx) of the reconstructed block: the LDS tile, or a DC-family block's value
         // plus the residual (res was complete before the dependency wait's barrier)

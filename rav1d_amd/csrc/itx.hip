@@ -26,10 +26,6 @@ MI_KTL_DEFINE(itx)
 
 namespace mi {
 
-#ifndef MI_ITX_PERSIST
-#define MI_ITX_PERSIST 0   // > 0: a persistent grid of 256 x MI_ITX_PERSIST workgroups walks the schedule
-#endif
-
 // TxfmType -> 1-D kinds (levels.rs TxfmType is VERT_HORZ; itx_tmpl.c:196-233)
 __constant__ uint8_t k_col_kind[16] = { KD, KA, KD, KA, KF, KD, KF, KA, KF, KI, KD, KI, KA, KI, KF, KI };
 __constant__ uint8_t k_row_kind[16] = { KD, KD, KA, KA, KD, KF, KF, KF, KA, KI, KI, KD, KI, KA, KI, KF };
@@ -102,10 +98,7 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     constexpr int NCH = (Ht * CPR + TPB - 1) / TPB;   // chunks per lane
     using V = typename Vec4<Px>::T;
 
-    int t = threadIdx.x;
-#if MI_ITX_PERSIST
-    asm volatile("" : "+v"(t));   // (persistent grid: nothing derived from the lane is hoisted out of the item loop)
-#endif
+    const int t = threadIdx.x;
     const int lb = t / TPB, j = t % TPB;
     // this workgroup's block range: the whole size, or (banded grid) band lwg % 8 of it
     int bs = a.blk_start[TX], be = a.blk_start[TX + 1], k = lwg;
@@ -182,11 +175,7 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     for (int c4 = 0; c4 < NCH; c4++) pix[c4] = pk[rd][c4];
     Cf *cf = reinterpret_cast<Cf *>(a.coef) + b.coef_off;
     const bool wht = (TX == 0) && b.txtp == 16;
-#ifdef MI_ITX_SKEL   // experiment builds only: every block as DC-only (the memory skeleton)
-    const bool dconly = true;
-#else
     const bool dconly = b.txtp == 0 && b.eob < 1;
-#endif
     uint8_t *pbase = sel3(plane3, b.plane) + (int64_t)b.y * sel3(stride3, b.plane) + (int64_t)b.x * sizeof(Px);
     const int64_t st = sel3(stride3, b.plane);
 
@@ -305,244 +294,35 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     }
 }
 
-// The 64-point sizes (64x64, 64x32, 32x64, 64x16, 16x64: DCT_DCT only, itx.rs:1072-1110).
-// Every 64-point 1-D transform runs on a lane pair (idct64_pair: the even lane the 32-point
-// even half, the odd lane the odd half, merged by DPP), so no lane holds more than 32 values
-// and these sizes no longer set the kernel's register budget (128 VGPRs with a 64-point
-// transform per lane). Row pass: 64-wide rows on lane pairs (the even lane writes columns
-// 0..31, the odd lane 63..32); column pass: 64-tall columns on lane pairs (rows 0..31 on the
-// even lane, 63..32 on the odd one), the residual added in two 32-row halves through the LDS
-// slab. Pair conditions (row, column, block) are equal on both lanes of a pair, so the DPP
-// exchange always sees its partner active.
-template <int TX, typename Px, typename Cf, typename Lt, bool Wide>
-__device__ __forceinline__ void itx_size64(const ItxArgs &a, int lwg, Lt *lds) {
-    constexpr TxDim D = tx_dim(TX);
-    constexpr int Wd = D.w, Ht = D.h, SH = imin_c(Ht, 32);
-    constexpr bool RS = Wd == 64, CS = Ht == 64;        // row / column transforms on lane pairs
-    constexpr int TPB = itx_lanes(TX), BPW = kItxThreads / TPB;
-    constexpr int LS = Wd + 1;
-    constexpr bool Rect2 = (Wd == 2 * Ht) || (Ht == 2 * Wd);
-    constexpr int Shift = D.shift, Rnd = (1 << Shift) >> 1;
-    constexpr int CPR = Wd / 4;                          // 4-px chunks per row
-    constexpr int NCH = (Ht * CPR + TPB - 1) / TPB;      // chunks per lane
-    using V = typename Vec4<Px>::T;
-
-    int t = threadIdx.x;
-#if MI_ITX_PERSIST
-    asm volatile("" : "+v"(t));   // (persistent grid: nothing derived from the lane is hoisted out of the item loop)
-#endif
-    const int lb = t / TPB, j = t % TPB;
-    int bs = a.blk_start[TX], be = a.blk_start[TX + 1], k = lwg;
-    if (a.nbands > 1) {
-        const int q = lwg & 7;
-        k = lwg >> 3;
-        bs = KARG(band_start, TX * 9 + q);
-        be = KARG(band_start, TX * 9 + q + 1);
-    }
-    uint8_t *const plane3[3] = { a.plane[0], a.plane[1], a.plane[2] };
-    const int64_t stride3[3] = { a.stride[0], a.stride[1], a.stride[2] };
-    const int pw3[3] = { a.pw[0], a.pw[1], a.pw[2] }, ph3[3] = { a.ph[0], a.ph[1], a.ph[2] };
-    const int bdmax = a.bdmax;
-    Lt *tmp = lds + lb * SH * LS;
-
-    const int bi = bs + k * BPW + lb;
-    bool valid = bi < be;
-    MiTxBlock b{};
-    if (valid) {
-        b = a.blocks[bi];
-        const bool ok = b.tx == TX && b.txtp < 17 && ((itx_legal_types(TX) >> b.txtp) & 1) && b.plane < 3 &&
-                        b.x + Wd <= sel3(pw3, b.plane) && b.y + Ht <= sel3(ph3, b.plane);
-        if (!ok) {
-            valid = false;
-            if (j == 0) atomicOr(a.err, 2);
-        }
-    }
-    uint8_t *pbase = sel3(plane3, b.plane) + (int64_t)b.y * sel3(stride3, b.plane) + (int64_t)b.x * sizeof(Px);
-    const int64_t st = sel3(stride3, b.plane);
-    Cf *cf = reinterpret_cast<Cf *>(a.coef) + b.coef_off;
-    const bool dconly = b.txtp == 0 && b.eob < 1;
-    int dc = 0;
-    if (valid && dconly) {
-        dc = (int)cf[0];
-        if (Rect2) dc = (dc * 181 + 128) >> 8;
-        dc = (dc * 181 + 128) >> 8;
-        dc = (dc + Rnd) >> Shift;
-        dc = (dc * 181 + 128 + 2048) >> 12;
-        if (j == 0 && a.zero_coefs) cf[0] = 0;
-    }
-    int row_lo, col_lo;
-    if constexpr (sizeof(Px) == 1) { row_lo = -32768; col_lo = -32768; }
-    else { row_lo = (int)((unsigned)~bdmax << 7); col_lo = (int)((unsigned)~bdmax << 5); }
-    const int row_hi = ~row_lo, col_hi = ~col_lo;
-    const bool full = valid && !dconly;
-
-    // ---- row pass ----
-    if constexpr (RS) {
-        const int row = j >> 1, h = j & 1;
-        if (full && row < SH) {
-            int y[32];
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const int v = (int)cf[row + (2 * i + h) * SH];
-                y[i] = Rect2 ? (v * 181 + 128) >> 8 : v;
-            }
-            if (a.zero_coefs) {
-#pragma unroll
-                for (int i = 0; i < 16; i++) cf[row + (2 * i + h) * SH] = 0;
-            }
-            idct64_pair<Wide>(y, h != 0, row_lo, row_hi);
-#pragma unroll
-            for (int i = 0; i < 32; i++)
-                tmp[row * LS + (h ? 63 - i : i)] = (Lt)clampi((y[i] + Rnd) >> Shift, col_lo, col_hi);
-        }
-    } else {
-        if (full && j < SH) {
-            int r[Wd];
-#pragma unroll
-            for (int x = 0; x < Wd; x++) {
-                const int v = (int)cf[j + x * SH];
-                r[x] = Rect2 ? (v * 181 + 128) >> 8 : v;
-            }
-            if (a.zero_coefs) {
-#pragma unroll
-                for (int x = 0; x < Wd; x++) cf[j + x * SH] = 0;
-            }
-            itx1d<Wide, Wd>(KD, r, row_lo, row_hi);
-#pragma unroll
-            for (int x = 0; x < Wd; x++) tmp[j * LS + x] = (Lt)clampi((r[x] + Rnd) >> Shift, col_lo, col_hi);
-        }
-    }
-    __syncthreads();
-
-    // ---- column pass: the residual of 32 rows (pairs) or Ht <= 32 rows per lane ----
-    constexpr int NR = CS ? 32 : Ht;
-    int res[NR];
-    if constexpr (CS) {
-        const int col = j >> 1, h = j & 1;
-        if (full && col < Wd) {
-#pragma unroll
-            for (int i = 0; i < 16; i++) res[i] = (int)tmp[(2 * i + h) * LS + col];
-            idct64_pair<Wide>(res, h != 0, col_lo, col_hi);
-#pragma unroll
-            for (int i = 0; i < 32; i++) res[i] = (res[i] + 8) >> 4;
-        }
-    } else {
-        if (full && j < Wd) {
-#pragma unroll
-            for (int y = 0; y < Ht; y++) res[y] = (int)tmp[y * LS + j];
-            itx1d<Wide, Ht>(KD, res, col_lo, col_hi);
-#pragma unroll
-            for (int y = 0; y < Ht; y++) res[y] = (res[y] + 8) >> 4;
-        }
-    }
-
-    // ---- add + vector stores, in 32-row halves through the slab ----
-    // (the destination pixels are loaded only now: prefetched before the transforms they would
-    // hold 16 VGPRs through both passes, and these sizes would again set the kernel's budget)
-    V pix[NCH];
-#pragma unroll
-    for (int c4 = 0; c4 < NCH; c4++) {
-        const int c = j + c4 * TPB;
-        if (valid && c < Ht * CPR)
-            pix[c4] = *reinterpret_cast<const V *>(pbase + (int64_t)(c / CPR) * st + (c % CPR) * 4 * sizeof(Px));
-    }
-#pragma unroll
-    for (int half = 0; half < (CS ? 2 : 1); half++) {
-        __syncthreads();                                   // the slab's previous contents are read
-        if constexpr (CS) {
-            const int col = j >> 1, h = j & 1;
-            if (full && col < Wd && h == half) {
-                // even lane: rows 0..31 (res[i] = row i); odd lane: rows 63..32 (res[i] = row 63 - i)
-#pragma unroll
-                for (int i = 0; i < 32; i++) tmp[(h ? 31 - i : i) * LS + col] = (Lt)res[i];
-            }
-        } else {
-            if (full && j < Wd) {
-#pragma unroll
-                for (int y = 0; y < Ht; y++) tmp[y * LS + j] = (Lt)res[y];
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int c4 = 0; c4 < NCH; c4++) {
-            const int c = j + c4 * TPB;
-            const int y = c / CPR;
-            if (valid && c < Ht * CPR && (y >> 5) == half) {
-                int px[4];
-                unpack4<Px>(pix[c4], px);
-                const int x0 = (c % CPR) * 4;
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    px[q] = clampi(px[q] + (dconly ? dc : (int)tmp[(y & 31) * LS + x0 + q]), 0, bdmax);
-                *reinterpret_cast<V *>(pbase + (int64_t)y * st + x0 * sizeof(Px)) = pack4<Px>(px);
-            }
-        }
-    }
-}
-
 // One launch for every size. The workgroups of the 64- and 32-point sizes come first in the
 // grid: they are few but the longest (a 64-point transform per lane, ~15 us at 4K10), so they
 // start first and the small sizes fill the machine around them. Measured against two launches
 // (sides <= 16, then the rest, each with its own register budget: 66 / 127 VGPRs): 56.3 ->
 // 46.4 us at 4K10; the small sizes lose little from the larger register budget, the large
 // ones stop being a serial tail.
+// (64-point transforms on lane pairs, a persistent grid, and a schedule interleaving every size
+// in 4 or 8 rounds were measured slower and removed: DESIGN.md §5)
 template <typename Px, typename Cf, typename Lt, bool Wide>
-#ifndef MI_ITX_MINW
-#define MI_ITX_MINW 4
-#endif
-__global__ __launch_bounds__(kItxThreads, MI_ITX_MINW) void itx_frame_kernel(ItxArgs a) {
+__global__ __launch_bounds__(kItxThreads, 4) void itx_frame_kernel(ItxArgs a) {
     __shared__ Lt lds[itx_lds_max(true) > itx_lds_max(false) ? itx_lds_max(true) : itx_lds_max(false)];
     KTL(0);
-#if MI_ITX_PERSIST
-    for (int wg = blockIdx.x; wg < a.wg_start[19]; wg += gridDim.x) {
-    if (wg != (int)blockIdx.x) __syncthreads();   // the previous item's LDS reads are done
-#else
-    {
     const int wg = blockIdx.x;
-#endif
     // the size range holding this workgroup, with compile-time indices only (a runtime index
     // into the kernel-argument struct makes the compiler copy it to scratch)
-    int s, lwg;
-    if (a.nrounds > 1) {
-        // round r, then the size within the round; lwg = 8 k + band (itx_size's convention)
-        int r = 0;
-        for (int i = 1; i < kItxRounds; i++)
-            if (wg >= KARG(round_start, i)) r = i;
-        int w = wg - KARG(round_start, r);
-        constexpr int R = kItxRounds;
-        int i = 0, k0 = 0;
-        for (;; i++) {
-            const int m = KARG(m_size, i), lo = r * m / R, n = 8 * ((r + 1) * m / R - lo);
-            if (w < n || i == 18) { k0 = lo; break; }
-            w -= n;
-        }
-        s = KARG(wg_size, i);
-        lwg = 8 * k0 + w;
-    } else {
-        int i = 0;
-        for (int k = 1; k < 19; k++)
-            if (wg >= KARG(wg_start, k)) i = k;
-        s = KARG(wg_size, i);
-        lwg = wg - KARG(wg_start, i);
-    }
+    int i = 0;
+    for (int k = 1; k < 19; k++)
+        if (wg >= KARG(wg_start, k)) i = k;
+    const int s = KARG(wg_size, i);
+    const int lwg = wg - KARG(wg_start, i);
     switch (s) {
 #define CASE(n) case n: itx_size<n, Px, Cf, Lt, Wide>(a, lwg, lds); break;
         CASE(0) CASE(1) CASE(2) CASE(5) CASE(6) CASE(7) CASE(8) CASE(13) CASE(14)
         CASE(3) CASE(9) CASE(10) CASE(15) CASE(16)
-#undef CASE
-#ifndef MI_ITX_EXP_NO64   // experiment builds only: the 64-point sizes compiled out
-#if MI_ITX_PAIR64
-#define CASE(n) case n: itx_size64<n, Px, Cf, Lt, Wide>(a, lwg, lds); break;
-#else
-#define CASE(n) case n: itx_size<n, Px, Cf, Lt, Wide>(a, lwg, lds); break;
-#endif
         CASE(4) CASE(11) CASE(12) CASE(17) CASE(18)
 #undef CASE
-#endif
     default: break;
     }
     KTLV(6, s);
-    }
     KTL(5);
 }
 
@@ -563,23 +343,12 @@ int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start, const uint32_t *ba
                 m = std::max(m, (n + per_wg - 1) / per_wg);
             }
             wg += kItxBands * m;
-            a.m_size[i] = m;
         } else {
             const int n = (int)(size_start[sz + 1] - size_start[sz]);
             wg += (n + per_wg - 1) / per_wg;
         }
     }
     a.wg_start[19] = wg;
-    a.nrounds = band_start && !MI_ITX_PERSIST ? kItxRounds : 1;
-    if (a.nrounds > 1) {
-        int acc = 0;
-        for (int r = 0; r < a.nrounds; r++) {
-            a.round_start[r] = acc;
-            for (int i = 0; i < 19; i++)
-                acc += kItxBands * ((r + 1) * a.m_size[i] / a.nrounds - r * a.m_size[i] / a.nrounds);
-        }
-        a.round_start[a.nrounds] = acc;   // == wg
-    }
     for (int k = 0; k <= 19; k++) a.blk_start[k] = (int)size_start[k];
     if (band_start)
         for (int s = 0; s < 19; s++)
@@ -589,7 +358,6 @@ int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start, const uint32_t *ba
 
 int launch_itx_frame(const ItxArgs &a, int nwg, int bpc, hipStream_t s) {
     if (nwg <= 0) return 0;
-    if (MI_ITX_PERSIST) nwg = std::min(nwg, 256 * MI_ITX_PERSIST);   // a multiple of 8: the band -> XCD rule holds
     if (bpc == 8) hipLaunchKernelGGL((itx_frame_kernel<uint8_t, int16_t, int16_t, false>), dim3(nwg), dim3(kItxThreads), 0, s, a);
     else if (bpc == 10) hipLaunchKernelGGL((itx_frame_kernel<uint16_t, int32_t, int16_t, false>), dim3(nwg), dim3(kItxThreads), 0, s, a);
     else hipLaunchKernelGGL((itx_frame_kernel<uint16_t, int32_t, int32_t, true>), dim3(nwg), dim3(kItxThreads), 0, s, a);

@@ -394,11 +394,9 @@ __device__ __forceinline__ void lr_sgr_tile(int s0, int s1, int w0, int w1, int1
     __syncthreads();
 }
 
-#ifndef MI_LR_WAVES
-#define MI_LR_WAVES 8   // 64 VGPRs: four 512-lane workgroups per CU (the LDS allows four)
-#endif
+// amdgpu_waves_per_eu(8): 64 VGPRs, four 512-lane workgroups per CU (the LDS allows four)
 template <typename Px>
-__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES))) void lr_kernel(LrArgs a) {
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(8))) void lr_kernel(LrArgs a) {
     __shared__ __attribute__((aligned(16))) int16_t win[70 * kLrWin];
     __shared__ __attribute__((aligned(16))) int A[66 * kLrAB];
     __shared__ __attribute__((aligned(16))) int16_t B[66 * kLrAB];
@@ -406,25 +404,12 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MI_LR_WAVES
 
     KTL(0);
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-#ifndef MI_LR_XCD
-#define MI_LR_XCD 0   // tile -> XCD: 0 hardware round robin, 1 contiguous ranges (xcd_block), C > 1 runs of C
-#endif
-    // a.banded == 2: XCD k walks the k-th eighth of the (plane, stripe, tile) order, so
-    // horizontally adjacent tiles share their halo lines in one L2
-    // a.banded = C >= 3: runs of C consecutive tiles dealt to the XCDs in turn
-    const int blk = a.banded == 2 || MI_LR_XCD == 1 ? xcd_block(blockIdx.x, gridDim.x)
-                  : a.banded >= 3 ? xcd_chunk(blockIdx.x, gridDim.x, a.banded)
-                  : MI_LR_XCD > 1 ? xcd_chunk(blockIdx.x, gridDim.x, MI_LR_XCD) : blockIdx.x;
+    // (hardware round robin: XCD-local orders of the tiles cut LR's HBM reads from 70 to 28 MB
+    // but ran 1.3-5.9 us slower)
+    const int blk = blockIdx.x;
     const int p = blk < a.blk_start[1] ? 0 : blk < a.blk_start[2] ? 1 : 2;
-    int lb = blk - a.blk_start[p];
+    const int lb = blk - a.blk_start[p];
     const int tiles = a.tiles_x[p];
-    if (a.banded == 1) {
-        // grid index 8m + q: the m-th tile of band q (plane starts are multiples of 8)
-        const int q = lb & 7, m = lb >> 3, ns = a.stripes[p];
-        const int s0 = q * ns / 8, s1 = (q + 1) * ns / 8;
-        if (m >= (s1 - s0) * tiles) return;           // padding of a smaller band
-        lb = s0 * tiles + m;
-    }
     const int k = lb / tiles, ti = lb - k * tiles;
     const int ssv = p ? a.ss_ver : 0, ssh = p ? a.ss_hor : 0;
     const int pw = a.pw[p], ph = a.ph[p];

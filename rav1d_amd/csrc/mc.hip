@@ -160,47 +160,28 @@ __device__ __forceinline__ void predict(const McArgs &a, const int16_t *win, int
     }
 }
 
-#ifndef MC_MIN_WAVES
-#define MC_MIN_WAVES 1
-#endif
-#ifndef MI_MC_LPT
-#define MI_MC_LPT 0   // 1: classes dispatched largest first; measured slower at 4K10 (83 vs 75 us)
-#endif
-#ifndef MI_MC_XCD_CLASS
-#define MI_MC_XCD_CLASS 1   // each class's waves in 8 contiguous chunks, one per XCD
-#endif
+// (dispatching the classes largest first was measured slower at 4K10: 83 vs 75 us)
 template <typename Px>
 // g: 0 / 1 = the waves of plane group 0 / 1; 2 = both groups in one grid (group 0's waves,
 // then group 1's; mi_mc_frame_ex with MI_MC_ONE_GRID: no chroma unit reads a mask written
 // in the same grid), so the small chroma units fill the luma tail.
-__global__ __launch_bounds__(64, MC_MIN_WAVES) void mc_kernel(McArgs a, int g) {
+__global__ __launch_bounds__(64, 1) void mc_kernel(McArgs a, int g) {
     __shared__ __attribute__((aligned(16))) int16_t win[kWinElems];
     const int lane = threadIdx.x;
     KTL(0);
-#ifndef MI_MC_XCD_CHUNK
-#define MI_MC_XCD_CHUNK 1
-#endif
-    int wave = xcd_chunk(blockIdx.x, gridDim.x, MI_MC_XCD_CHUNK);
+    int wave = blockIdx.x;
     if (g == 2) {
         g = wave >= (int)a.first_wave[0][MI_MC_NCLASS];
         if (g) wave -= (int)a.first_wave[0][MI_MC_NCLASS];
     }
     const uint32_t *fw = a.first_wave[g];
     // class of this wave: last class whose first wave <= wave (wave-uniform scan)
-#if MI_MC_LPT
-    // classes dispatched largest first: the class is the smallest one whose first wave <= wave
-    int c = MI_MC_NCLASS - 1;
-    for (int k = MI_MC_NCLASS - 2; k >= 0; k--)
-        if (fw[k] <= (uint32_t)wave) c = k;
-#else
     int c = 0;
     for (int k = 1; k < MI_MC_NCLASS; k++)
         if (fw[k] <= (uint32_t)wave) c = k;
-#endif
     int item = wave - (int)fw[c];
     const ClassGeom G = class_geom(c);
     const uint32_t cls_begin = a.class_start[g * MI_MC_NCLASS + c], cls_end = a.class_start[g * MI_MC_NCLASS + c + 1];
-#if MI_MC_XCD_CLASS && !MI_MC_LPT
     {
         // the class's waves (padded to a multiple of 8, mc_plan) as 8 contiguous chunks, chunk x
         // on XCD x (grid index mod 8): units are in picture order inside a class, so each XCD
@@ -210,7 +191,6 @@ __global__ __launch_bounds__(64, MC_MIN_WAVES) void mc_kernel(McArgs a, int g) {
         const uint32_t n = cls_end - cls_begin;
         if ((uint32_t)item >= (G.T == 1 ? (n + G.U - 1) / G.U : n * G.T)) return;
     }
-#endif
 
     // this lane's unit, tile origin, column and rows
     int uu, tx0 = 0, ty0 = 0, rg, col;
@@ -423,7 +403,7 @@ __global__ __launch_bounds__(64, MC_MIN_WAVES) void mc_kernel(McArgs a, int g) {
 int mc_plan(McArgs &a, int g) {
     uint32_t waves = 0;
     for (int i = 0; i < MI_MC_NCLASS; i++) {
-        const int c = MI_MC_LPT ? MI_MC_NCLASS - 1 - i : i;
+        const int c = i;
         a.first_wave[g][c] = waves;
         const uint32_t n = a.class_start[g * MI_MC_NCLASS + c + 1] - a.class_start[g * MI_MC_NCLASS + c];
         if (!n) continue;
@@ -440,7 +420,7 @@ int mc_plan(McArgs &a, int g) {
             if ((TR + 7) * win_stride(TW) > kWinElems) return -1;
             waves += n * (uint32_t)((w / TW) * (h / TR));
         }
-        if (MI_MC_XCD_CLASS && !MI_MC_LPT) waves = (waves + 7) & ~7u;   // whole chunks per XCD (mc_kernel)
+        waves = (waves + 7) & ~7u;   // whole chunks per XCD (mc_kernel)
     }
     a.first_wave[g][MI_MC_NCLASS] = waves;
     return (int)waves;

@@ -7,7 +7,6 @@ DC-only 60 % / partial 30 % / full 10 %, coefficient magnitudes inside the dequa
 range (|c| <= (128 << bpc) - 1, rav1d src/recon.rs decode_coefs clamp). Everything is a pure
 function of (geometry, seed), so the same inputs regenerate bit-identically anywhere.
 """
-import os
 
 import numpy as np
 
@@ -176,20 +175,14 @@ def itx_device_order(blocks):
 ITX_BANDS = 8
 
 
-ITX_ROUNDS = int(os.environ.get("MI_SYNTH_ITX_ROUNDS", "1"))   # common.h kItxRounds: sub-bands per band, one per round of the banded grid
-
-
 def itx_band_order(blocks, plane_heights):
     """mi_itx_frame_banded order: grouped by tx size, inside a size by picture band (band q =
     plane rows [q*h/8, (q+1)*h/8) of the block's plane, h = the 128-aligned plane height),
-    inside a band by sub-band (ITX_ROUNDS per band: round r of the grid takes about sub-band r
-    of every size), then as itx_device_order. Returns (blocks, size_start, band_start[19][9])."""
+    then as itx_device_order. Returns (blocks, size_start, band_start[19][9])."""
     ph = np.asarray(plane_heights, np.int64)
-    fine = np.minimum(blocks["y"].astype(np.int64) * (ITX_BANDS * ITX_ROUNDS) // ph[blocks["plane"]],
-                      ITX_BANDS * ITX_ROUNDS - 1)
-    band = fine // ITX_ROUNDS
+    band = np.minimum(blocks["y"].astype(np.int64) * ITX_BANDS // ph[blocks["plane"]], ITX_BANDS - 1)
     dc = (blocks["txtp"] == 0) & (blocks["eob"] < 1)
-    order = np.lexsort((blocks["x"], blocks["y"], blocks["plane"], ~dc, fine, blocks["tx"]))
+    order = np.lexsort((blocks["x"], blocks["y"], blocks["plane"], ~dc, band, blocks["tx"]))
     blocks = blocks[order]
     band = band[order]
     key = blocks["tx"].astype(np.int64) * ITX_BANDS + band
