@@ -12,6 +12,11 @@
 #include <cerrno>
 #include <cstdio>
 #include <string>
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <new>
+#include <thread>
 
 #include "framedec.h"
 
@@ -140,9 +145,9 @@ void FrameDec::setup_tile(TileState &t, const uint8_t *data, size_t sz, int row,
             const int u_idx = unit_idx + ((px_x & 64) >> 6);
             const int sb128x = px_x >> 7;
             if (sb128x >= fw.sr_sb128w) continue;
-            u = &fw.lr_mask[sb_idx + sb128x].lr[p][u_idx];
+            u = &mw.lr_mask[sb_idx + sb128x].lr[p][u_idx];
         } else {
-            u = &fw.lr_mask[sb_idx].lr[p][unit_idx];
+            u = &mw.lr_mask[sb_idx].lr[p][unit_idx];
         }
         u->filter_v[0] = 3;
         u->filter_v[1] = -7;
@@ -693,7 +698,7 @@ void FrameDec::create_lf_mask_intra(const Block &b, int has_chroma) {
     if (bw4 > 0 && bh4 > 0) {
         for (int y = 0; y < bh4; y++)
             for (int x = 0; x < bw4; x++) {
-                uint8_t *lv = &fw.lf_level[(((size_t)(by + y) * b4_stride) + bx + x) * 4];
+                uint8_t *lv = &mw.lf_level[(((size_t)(by + y) * b4_stride) + bx + x) * 4];
                 lv[0] = fl[0][0][0];
                 lv[1] = fl[1][0][0];
             }
@@ -706,7 +711,7 @@ void FrameDec::create_lf_mask_intra(const Block &b, int has_chroma) {
     if (cbw4 <= 0 || cbh4 <= 0) return;
     for (int y = 0; y < cbh4; y++)
         for (int x = 0; x < cbw4; x++) {
-            uint8_t *lv = &fw.lf_level[(((size_t)((by >> ss_ver) + y) * b4_stride) + (bx >> ss_hor) + x) * 4];
+            uint8_t *lv = &mw.lf_level[(((size_t)((by >> ss_ver) + y) * b4_stride) + (bx >> ss_hor) + x) * 4];
             lv[2] = fl[2][0][0];
             lv[3] = fl[3][0][0];
         }
@@ -721,7 +726,7 @@ void FrameDec::create_lf_mask_intra(const Block &b, int has_chroma) {
 
 void FrameDec::add_deps(int plane, int x0, int y0, int x1, int y1, std::vector<int32_t> &out) {
     // pixel rectangle [x0, x1) x [y0, y1) of `plane`, 4x4 granular
-    const std::vector<int32_t> &o = owner[plane];
+    const Span<int32_t> &o = owner[plane];
     for (int y = y0 >> 2; y < (y1 + 3) >> 2; y++)
         for (int x = x0 >> 2; x < (x1 + 3) >> 2; x++) {
             if (x < 0 || y < 0 || x >= owner_stride) continue;
@@ -799,7 +804,7 @@ void FrameDec::emit_intra(const Block &b, int edge_flags, const uint8_t *pal_idx
         }
         fw.intra_tx.push_back(tb);
         // ownership of the written pixels
-        std::vector<int32_t> &o = owner[plane];
+        Span<int32_t> &o = owner[plane];
         for (int yy = y >> 2; yy < (y + hh) >> 2; yy++)
             for (int xx = x >> 2; xx < (x + w) >> 2; xx++) o[(size_t)yy * owner_stride + xx] = k;
     };
@@ -1192,7 +1197,7 @@ void FrameDec::push_ibc(const Block &b, Mv mv, int plane, int tx, int tbx, int t
         if (eob >= 0) tb.coef_off = store_coefs(cf, tx, *txtp, eob);
     }
     fw.intra_tx.push_back(tb);
-    std::vector<int32_t> &o = owner[plane];
+    Span<int32_t> &o = owner[plane];
     for (int yy = py >> 2; yy < (py + ib.h) >> 2; yy++)
         for (int xx = px >> 2; xx < (px + ib.w) >> 2; xx++) {
             const size_t q = (size_t)yy * owner_stride + xx;
@@ -1858,7 +1863,7 @@ int FrameDec::decode_tile_sbrow(int tile_row, int tile_col) {
     const int sb128y = by >> 5;
     const int root = s.sb128 ? BL_128 : BL_64;
     for (bx = ts->col_start; bx < ts->col_end; bx += sb_step) {
-        lf_mask = &fw.lf_masks[(size_t)sb128y * sb128w + (bx >> 5)];
+        lf_mask = &mw.lf_masks[(size_t)sb128y * sb128w + (bx >> 5)];
         if (root == BL_128) {
             cur_cdef_idx = lf_mask->cdef_idx;
             for (int i = 0; i < 4; i++) cur_cdef_idx[i] = -1;
@@ -1889,7 +1894,7 @@ int FrameDec::decode_tile_sbrow(int tile_row, int tile_col) {
                     const int px_x = x << (usl + sh);
                     const int sb_idx = (by >> 5) * fw.sr_sb128w + (px_x >> 7);
                     const int unit_idx = ((by & 16) >> 3) + ((px_x & 64) >> 6);
-                    read_lr(&fw.lr_mask[sb_idx].lr[p][unit_idx], p, ftype);
+                    read_lr(&mw.lr_mask[sb_idx].lr[p][unit_idx], p, ftype);
                 }
             } else {
                 const int x = 4 * bx >> sh;
@@ -1898,7 +1903,7 @@ int FrameDec::decode_tile_sbrow(int tile_row, int tile_col) {
                 if (x && x + half > w) continue;
                 const int sb_idx = (by >> 5) * fw.sr_sb128w + (bx >> 5);
                 const int unit_idx = ((by & 16) >> 3) + ((bx & 16) >> 4);
-                read_lr(&fw.lr_mask[sb_idx].lr[p][unit_idx], p, ftype);
+                read_lr(&mw.lr_mask[sb_idx].lr[p][unit_idx], p, ftype);
             }
         }
         const int r = decode_sb(root, true, false);
@@ -1929,7 +1934,7 @@ void FrameDec::tile_fixups() {
         const int starty4 = (sby & is_sb64) << 4;
         const unsigned endy4 = starty4 + imin(h4 - sby * sbsz, sbsz);
         const unsigned uv_endy4 = (endy4 + ss_ver) >> ss_ver;
-        MiAv1Filter *lflvl = &fw.lf_masks[(size_t)(sby >> is_sb64) * sb128w];
+        MiAv1Filter *lflvl = &mw.lf_masks[(size_t)(sby >> is_sb64) * sb128w];
         const uint8_t *lpf_y = &tx_lpf_right[0][sby << sbl2];
         const uint8_t *lpf_uv = &tx_lpf_right[1][sby << (sbl2 - ss_ver)];
         for (int tc = 1;; tc++) {
@@ -1966,7 +1971,7 @@ void FrameDec::tile_fixups() {
         for (int tr = 1; tr < h.tiling.rows; tr++)
             if (h.tiling.row_start_sb[tr] == sby) tile_row = tr;
         if (tile_row > 0) {
-            const std::vector<uint8_t> &ay = a_tx_lpf_end[0][tile_row - 1], &auv = a_tx_lpf_end[1][tile_row - 1];
+            const std::vector<uint8_t> &ay = S->a_tx_lpf_end[0][tile_row - 1], &auv = S->a_tx_lpf_end[1][tile_row - 1];
             for (int x = 0; x < sb128w; x++) {
                 uint16_t (*yv)[2] = lflvl[x].filter_y[1][starty4];
                 const unsigned w = imin(32, w4 - (x << 5));
@@ -1996,8 +2001,7 @@ void FrameDec::tile_fixups() {
     }
 }
 
-int FrameDec::run(FrameResult &res, std::string &err) {
-    err_ = &err;
+int FrameDec::init_frame() {
     inter_frame = !is_intra_frame(h);
     layout = s.layout;
     ss_hor = layout == 1 || layout == 2;
@@ -2031,8 +2035,6 @@ int FrameDec::run(FrameResult &res, std::string &err) {
     fw.b4_stride = b4_stride;
     fw.sb128w = sb128w;
     fw.sb128h = sb128h;
-    fw.lf_level.assign((size_t)b4_stride * sb128h * 32 * 4, 0);
-    fw.lf_masks.assign((size_t)sb128w * sb128h, MiAv1Filter{});
     fw.filter_y = h.lf.level_y[0] || h.lf.level_y[1];
     fw.filter_uv = h.lf.level_u || h.lf.level_v;
     // E / I limits (lf_mask.rs calc_eih)
@@ -2054,7 +2056,6 @@ int FrameDec::run(FrameResult &res, std::string &err) {
         fw.cdef_uv[i] = (uint8_t)h.cdef.uv_strength[i];
     }
     fw.sr_sb128w = (h.width[1] + 127) >> 7;
-    fw.lr_mask.assign((size_t)fw.sr_sb128w * sb128h, MiAv1Restoration{});
     fw.restore_planes = (h.lr.type[0] != RESTORE_NONE) | ((h.lr.type[1] != RESTORE_NONE) << 1) |
                         ((h.lr.type[2] != RESTORE_NONE) << 2);
     fw.lr_unit_size[0] = h.lr.unit_size[0];
@@ -2065,23 +2066,34 @@ int FrameDec::run(FrameResult &res, std::string &err) {
     init_quant(h.quant.yac, dq_frame);
     static const int8_t zero4[4] = {0, 0, 0, 0};
     calc_lf_values(lflvl_frame, zero4);
-    segmap.assign((size_t)b4_stride * sb128h * 32, 0);
     const int align_h = (bh + 31) & ~31;
-    tx_lpf_right[0].assign((size_t)align_h * h.tiling.cols, 0);
-    tx_lpf_right[1].assign((size_t)(align_h >> ss_ver) * h.tiling.cols, 0);
-    a_tx_lpf_end[0].resize(h.tiling.rows);
-    a_tx_lpf_end[1].resize(h.tiling.rows);
     owner_stride = (b4_stride + 32);
-    for (int p = 0; p < 3; p++) owner[p].assign((size_t)owner_stride * (sb128h * 32 + 32), -1);
-    if (h.allow_intrabc || inter_frame) {
-        RefMvBlock none{};
-        none.mv[0] = kInvalidMv;
-        none.ref[0] = -1;
-        none.ref[1] = -1;
-        rmv_stride = b4_stride + 16;
-        rmv.assign((size_t)rmv_stride * (sb128h * 32 + 16), none);
-        f2d_map.assign(rmv.size(), 0);
+    if (h.allow_intrabc || inter_frame) rmv_stride = b4_stride + 16;
+    if (master_) {
+        // the frame's maps: allocated once, shared with the tile decoders
+        fw.lf_level.assign((size_t)b4_stride * sb128h * 32 * 4, 0);
+        fw.lf_masks.assign((size_t)sb128w * sb128h, MiAv1Filter{});
+        fw.lr_mask.assign((size_t)fw.sr_sb128w * sb128h, MiAv1Restoration{});
+        S->segmap.assign((size_t)b4_stride * sb128h * 32, 0);
+        S->tx_lpf_right[0].assign((size_t)align_h * h.tiling.cols, 0);
+        S->tx_lpf_right[1].assign((size_t)(align_h >> ss_ver) * h.tiling.cols, 0);
+        S->a_tx_lpf_end[0].assign(h.tiling.rows, std::vector<uint8_t>());
+        S->a_tx_lpf_end[1].assign(h.tiling.rows, std::vector<uint8_t>());
+        for (int p = 0; p < 3; p++) S->owner[p].assign((size_t)owner_stride * (sb128h * 32 + 32), -1);
+        if (h.allow_intrabc || inter_frame) {
+            RefMvBlock none{};
+            none.mv[0] = kInvalidMv;
+            none.ref[0] = -1;
+            none.ref[1] = -1;
+            S->rmv.assign((size_t)rmv_stride * (sb128h * 32 + 16), none);
+            S->f2d_map.assign(S->rmv.size(), 0);
+        }
     }
+    segmap.bind(S->segmap);
+    for (int k = 0; k < 2; k++) tx_lpf_right[k].bind(S->tx_lpf_right[k]);
+    for (int p = 0; p < 3; p++) owner[p].bind(S->owner[p]);
+    rmv.bind(S->rmv);
+    f2d_map.bind(S->f2d_map);
     if (inter_frame) {
         refmvs_init_frame();
         inter_frame_init();
@@ -2090,7 +2102,103 @@ int FrameDec::run(FrameResult &res, std::string &err) {
     l.alloc(64);
     memset(al_pal, 0, sizeof(al_pal));
     memset(pal_sz_uv, 0, sizeof(pal_sz_uv));
+    return 0;
+}
 
+// All superblock rows of tile k (decode.rs decode_tile_sbrow over the tile). tile_tmvs: the
+// temporal MVs projected (load_tmvs) and saved (save_tmvs) over the tile's columns per sbrow,
+// as rav1d's tile threads do (thread_task.rs); the result equals the frame-wide passes of the
+// single-threaded decode (decode.rs decode_frame_main), which run() uses without threads.
+int FrameDec::decode_tile(int k, bool tile_tmvs) {
+    const int tr = k / h.tiling.cols, tc = k % h.tiling.cols;
+    ts = &ts_[k];
+    a.reset(is_intra_frame(h));
+    const int sb_end = imin(h.tiling.row_start_sb[tr + 1], sbh);
+    const int c8s = ts->col_start >> 1, c8e = ts->col_end >> 1;
+    for (int sby = h.tiling.row_start_sb[tr]; sby < sb_end; sby++) {
+        by = sby << sb_shift;
+        if (tile_tmvs && inter_frame && h.use_ref_frame_mvs) load_tmvs(by >> 1, (by + sb_step) >> 1, c8s, c8e);
+        if (ts->msac.cnt < -15) return fail("symbol decoder overread");
+        const int r = decode_tile_sbrow(tr, tc);
+        if (r) return r;
+        if (tile_tmvs && inter_frame) save_tmvs(by >> 1, (by + sb_step) >> 1, c8s, c8e);
+    }
+    // the above context at the tile row's end (loop-filter fixups at the next tile row), the
+    // tile's columns
+    if (tr + 1 < h.tiling.rows) {
+        for (int pl = 0; pl < 2; pl++) {
+            const std::vector<uint8_t> &src = pl ? a.tx_lpf_uv : a.tx_lpf_y;
+            std::vector<uint8_t> &dst = S->a_tx_lpf_end[pl][tr];
+            const int sh = pl ? ss_hor : 0;
+            const int x0 = ts->col_start >> sh, x1 = imin((ts->col_end + sh) >> sh, (int)src.size());
+            for (int x = x0; x < x1; x++) dst[x] = src[x];
+        }
+    }
+    return 0;
+}
+
+// Append tile decoder t's work lists, rebasing every index into the lists and arenas it
+// points at (intra blocks of dependencies, coefficient / idx / palette / mask / tmp arenas)
+void FrameDec::merge_tile(const FrameWork &t) {
+    const uint32_t intra_base = (uint32_t)fw.intra.size(), deps_base = (uint32_t)fw.deps.size();
+    const uint32_t coef_base = (uint32_t)fw.ncoef, idx_base = (uint32_t)fw.idx.size();
+    const uint32_t pal_base = (uint32_t)(fw.pal.size() / (s.bpc == 8 ? 1 : 2));
+    const uint32_t masks_base = (uint32_t)fw.masks.size(), tmp_base = (uint32_t)fw.ntmp;
+    for (MiIntraBlock b : t.intra) {
+        if (b.mode == MI_IPRED_PAL) {
+            b.aux_off += idx_base;
+            b.pal_off += pal_base;
+        } else if (b.flags & MI_INTRA_II) {
+            b.aux_off += idx_base;
+        }
+        fw.intra.push_back(b);
+    }
+    for (MiTxBlock b : t.intra_tx) {
+        b.coef_off += coef_base;
+        fw.intra_tx.push_back(b);
+    }
+    for (int32_t d : t.dep_start) fw.dep_start.push_back(d + (int32_t)deps_base);
+    for (int32_t d : t.deps) fw.deps.push_back(d + (int32_t)intra_base);
+    for (MiTxBlock b : t.inter_tx) {
+        b.coef_off += coef_base;
+        fw.inter_tx.push_back(b);
+    }
+    auto mc_list = [&](const std::vector<MiMcBlock> &src, std::vector<MiMcBlock> &dst) {
+        for (MiMcBlock u : src) {
+            if (u.comp == MI_MC_MASK || u.comp == MI_MC_SEG) u.mask_off += masks_base;
+            else if (u.comp == MI_MC_PREP) u.mask_off += tmp_base;
+            dst.push_back(u);
+        }
+    };
+    mc_list(t.mc, fw.mc);
+    mc_list(t.obmc_h, fw.obmc_h);
+    mc_list(t.obmc_v, fw.obmc_v);
+    mc_list(t.scaled, fw.scaled);
+    for (MiWarpBlock w : t.warp) {
+        if (w.prep) w.tmp_off += tmp_base;
+        fw.warp.push_back(w);
+    }
+    auto combine_list = [&](const std::vector<MiMcCombine> &src, std::vector<MiMcCombine> &dst) {
+        for (MiMcCombine c : src) {
+            c.tmp_off[0] += tmp_base;
+            c.tmp_off[1] += tmp_base;
+            if (c.comp == MI_MC_MASK || c.comp == MI_MC_SEG) c.mask_off += masks_base;
+            dst.push_back(c);
+        }
+    };
+    combine_list(t.combine_y, fw.combine_y);
+    combine_list(t.combine_uv, fw.combine_uv);
+    fw.masks.insert(fw.masks.end(), t.masks.begin(), t.masks.end());
+    fw.ntmp += t.ntmp;
+    fw.coef.insert(fw.coef.end(), t.coef.begin(), t.coef.end());
+    fw.ncoef += t.ncoef;
+    fw.idx.insert(fw.idx.end(), t.idx.begin(), t.idx.end());
+    fw.pal.insert(fw.pal.end(), t.pal.begin(), t.pal.end());
+}
+
+int FrameDec::run(FrameResult &res, std::string &err, int threads) {
+    err_ = &err;
+    if (int r = init_frame()) return r;
     const int n_tiles = h.tiling.cols * h.tiling.rows;
     if ((int)in_.tiles.size() != n_tiles) return fail("tile count mismatch");
     ts_.resize(n_tiles);
@@ -2099,24 +2207,73 @@ int FrameDec::run(FrameResult &res, std::string &err) {
             const int k = tr * h.tiling.cols + tc;
             setup_tile(ts_[k], in_.tiles[k].data, in_.tiles[k].size, tr, tc);
         }
-    for (int tr = 0; tr < h.tiling.rows; tr++) {
-        a.reset(is_intra_frame(h));
-        const int sb_end = imin(h.tiling.row_start_sb[tr + 1], sbh);
-        for (int sby = h.tiling.row_start_sb[tr]; sby < sb_end; sby++) {
-            by = sby << sb_shift;
-            // decode.rs decode_frame_main (C decode.c:3225-3244): temporal MVs projected per
-            // sbrow before its tiles, this frame's MVs saved after them
-            if (inter_frame && h.use_ref_frame_mvs) load_tmvs(by >> 1, (by + sb_step) >> 1);
-            for (int tc = 0; tc < h.tiling.cols; tc++) {
-                ts = &ts_[tr * h.tiling.cols + tc];
-                if (ts->msac.cnt < -15) return fail("symbol decoder overread");
-                const int r = decode_tile_sbrow(tr, tc);
-                if (r) return r;
+    for (int tr = 0; tr + 1 < h.tiling.rows; tr++)
+        for (int pl = 0; pl < 2; pl++) S->a_tx_lpf_end[pl][tr].assign(a.tx_lpf_y.size(), 0);
+    const int nt = imin(threads, n_tiles);
+    if (nt <= 1) {
+        // decode.rs decode_frame_main (C decode.c:3225-3244): per sbrow, temporal MVs projected
+        // over the frame before its tiles and this frame's MVs saved after them
+        for (int tr = 0; tr < h.tiling.rows; tr++) {
+            a.reset(is_intra_frame(h));
+            const int sb_end = imin(h.tiling.row_start_sb[tr + 1], sbh);
+            for (int sby = h.tiling.row_start_sb[tr]; sby < sb_end; sby++) {
+                by = sby << sb_shift;
+                if (inter_frame && h.use_ref_frame_mvs) load_tmvs(by >> 1, (by + sb_step) >> 1, 0, iw8);
+                for (int tc = 0; tc < h.tiling.cols; tc++) {
+                    ts = &ts_[tr * h.tiling.cols + tc];
+                    if (ts->msac.cnt < -15) return fail("symbol decoder overread");
+                    const int r = decode_tile_sbrow(tr, tc);
+                    if (r) return r;
+                }
+                if (inter_frame) save_tmvs(by >> 1, (by + sb_step) >> 1, 0, iw8);
             }
-            if (inter_frame) save_tmvs(by >> 1, (by + sb_step) >> 1);
+            if (tr + 1 < h.tiling.rows) {
+                S->a_tx_lpf_end[0][tr] = a.tx_lpf_y;
+                S->a_tx_lpf_end[1][tr] = a.tx_lpf_uv;
+            }
         }
-        a_tx_lpf_end[0][tr] = a.tx_lpf_y;
-        a_tx_lpf_end[1][tr] = a.tx_lpf_uv;
+    } else {
+        // rav1d's tile threads: tiles are independent in entropy, contexts and prediction; each
+        // runs on its own decoder (own above / left contexts and work lists), tiles dealt to
+        // nt threads in turn, then the lists are appended in tile order
+        std::vector<FrameWork> tw(n_tiles);
+        std::vector<std::string> terr(n_tiles);
+        std::vector<int> trc(n_tiles, 0);
+        std::atomic<int> next{0};
+        std::vector<double> tdur(n_tiles, 0.0);
+        auto worker = [&] {
+            for (int k; (k = next.fetch_add(1)) < n_tiles;) {
+                FrameDec td(*this, tw[k]);
+                td.err_ = &terr[k];
+                try {
+                    const auto a0 = std::chrono::steady_clock::now();
+                    trc[k] = td.init_frame();
+                    if (!trc[k]) trc[k] = td.decode_tile(k, true);
+                    tdur[k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a0).count();
+                } catch (const std::bad_alloc &) {
+                    trc[k] = -ENOMEM;
+                    terr[k] = "out of memory";
+                }
+            }
+        };
+        static const bool trace = getenv("MI_DEC_TRACE") != nullptr;   // (diagnostics)
+        const auto t0 = std::chrono::steady_clock::now();
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; t++) th.emplace_back(worker);
+        worker();
+        for (std::thread &t : th) t.join();
+        const auto t1 = std::chrono::steady_clock::now();
+        if (trace) {
+            fprintf(stderr, "  tiles %.2f ms:", std::chrono::duration<double, std::milli>(t1 - t0).count());
+            for (double d : tdur) fprintf(stderr, " %.2f", d);
+            fprintf(stderr, "\n");
+        }
+        for (int k = 0; k < n_tiles; k++)
+            if (trc[k]) {
+                err = terr[k];
+                return trc[k];
+            }
+        for (int k = 0; k < n_tiles; k++) merge_tile(tw[k]);
     }
     if (h.tiling.cols > 1 || h.tiling.rows > 1) tile_fixups();
     fw.dep_start.push_back((int32_t)fw.deps.size());
@@ -2129,7 +2286,7 @@ int FrameDec::run(FrameResult &res, std::string &err) {
     }
     if (inter_frame) res.mvs = rp;
     if (h.seg.enabled) {
-        if (h.seg.update_map) res.segmap = std::make_shared<std::vector<uint8_t>>(std::move(segmap));
+        if (h.seg.update_map) res.segmap = std::make_shared<std::vector<uint8_t>>(std::move(S->segmap));
         else if (in_.prev_segmap) res.segmap = std::make_shared<std::vector<uint8_t>>(*in_.prev_segmap);
         else res.segmap = std::make_shared<std::vector<uint8_t>>((size_t)b4_stride * sb128h * 32, 0);
     }
@@ -2138,9 +2295,9 @@ int FrameDec::run(FrameResult &res, std::string &err) {
 
 }  // namespace fd
 
-int decode_frame(const FrameInputs &in, FrameWork &work, FrameResult &res, std::string &err) {
+int decode_frame(const FrameInputs &in, FrameWork &work, FrameResult &res, std::string &err, int threads) {
     fd::FrameDec d(in, work);
-    return d.run(res, err);
+    return d.run(res, err, threads);
 }
 
 }  // namespace av1

@@ -1,7 +1,9 @@
 // decoder.h — the front-end decoder: sequence / frame state, reference slots, and the
 // per-frame block decoder that turns a frame's tile data into a FrameWork.
 #pragma once
+#include <condition_variable>
 #include <deque>
+#include <mutex>
 #include <thread>
 #include <memory>
 #include <string>
@@ -53,8 +55,9 @@ public:
     // 1 and ev filled, 0 when no event is queued, or -errno (a frame decoded on a worker
     // thread failed; error explains). Waits for the oldest frame's worker.
     int pop(DecEvent &ev);
-    // Frame threads (rav1d's n_fc): intra frames are decoded on up to n worker threads while
-    // send() parses on; events still come out in decode order. 1 (default): synchronous.
+    // Frame threads (rav1d's n_fc): frames are decoded on up to n worker threads while send()
+    // parses on (an inter frame's job waits for the jobs of its references), each frame's
+    // tiles on up to n threads; events still come out in decode order. 1 (default): synchronous.
     void set_threads(int n) { threads_ = n < 1 ? 1 : n > 64 ? 64 : n; }
     ~Decoder();
     std::string error;
@@ -101,25 +104,44 @@ struct FrameInputs {
     struct Tile { const uint8_t *data; size_t size; };
     std::vector<Tile> tiles;                                // in tile order
 };
-int decode_frame(const FrameInputs &in, FrameWork &work, FrameResult &res, std::string &err);
+// threads > 1: the frame's tiles on up to that many threads
+int decode_frame(const FrameInputs &in, FrameWork &work, FrameResult &res, std::string &err, int threads = 1);
 
 // One frame decoded on a worker thread: copies of everything the decoder may replace while
-// it runs (sequence header, frame header, input CDFs, the temporal unit bytes).
+// it runs (sequence header, frame header, the temporal unit bytes, the reference slots it
+// reads). An inter frame's job first waits for the jobs of the frames its references come from
+// (their entropy state, segment map and saved motion vectors), as rav1d's frame threads wait
+// on their references' progress (thread_task.rs), then decodes its tiles.
 struct FrameJob {
     SeqHdr seq;
     std::shared_ptr<const FrameHdr> hdr;
     std::shared_ptr<const Cdf> in_cdf;
     std::vector<std::shared_ptr<std::vector<uint8_t>>> bufs;
     FrameInputs in;
+    RefSlot refs[7];          // inter: refs_[refidx[i]] as they were at submission
+    int primary = -1;         // index into refs of primary_ref_frame (-1: none)
+    bool seg_from_primary = false;
     std::shared_ptr<FrameWork> work;
     FrameResult res;
     std::string err;
     int rc = 0;
     std::thread th;
+    // completion: set once by the job's thread; wait() may be called from any thread
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false;
+    void finish() {
+        std::lock_guard<std::mutex> g(m);
+        done = true;
+        cv.notify_all();
+    }
     void wait() {
+        std::unique_lock<std::mutex> g(m);
+        cv.wait(g, [this] { return done; });
+    }
+    ~FrameJob() {
         if (th.joinable()) th.join();
     }
-    ~FrameJob() { wait(); }
 };
 
 }  // namespace av1

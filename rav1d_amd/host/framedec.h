@@ -30,6 +30,35 @@ struct Block {
 
 enum { II_NONE, II_BLEND, II_WEDGE };
 
+// A view of a frame-wide array owned by FrameShared: the tile decoders of one frame write
+// disjoint parts of it (their tiles' 4x4 units, superblocks' mask words, 8x8 MV rows)
+template <typename T>
+struct Span {
+    T *p = nullptr;
+    size_t n = 0;
+    T &operator[](size_t i) const { return p[i]; }
+    T *data() const { return p; }
+    size_t size() const { return n; }
+    void bind(std::vector<T> &v) {
+        p = v.data();
+        n = v.size();
+    }
+};
+
+// The per-4x4 / per-8x8 maps of a frame that every tile decoder of it reads and writes (within
+// its own tile): segment ids, the loop filter's tile-edge contexts, intra owners, refmvs blocks,
+// projected and saved temporal MVs
+struct FrameShared {
+    std::vector<uint8_t> segmap;
+    std::vector<uint8_t> tx_lpf_right[2];
+    std::vector<std::vector<uint8_t>> a_tx_lpf_end[2];
+    std::vector<int32_t> owner[3];
+    std::vector<RefMvBlock> rmv;
+    std::vector<uint8_t> f2d_map;
+    std::vector<TmvBlock> rp_proj;
+    std::shared_ptr<std::vector<TmvBlock>> rp;
+};
+
 struct TileState {
     Cdf cdf;
     Msac msac;
@@ -49,19 +78,34 @@ struct MvCand {
 
 class FrameDec {
 public:
-    FrameDec(const FrameInputs &in, FrameWork &fw) : in_(in), s(*in.seq), h(*in.hdr), fw(fw) {}
-    int run(FrameResult &res, std::string &err);
+    // the frame's decoder: its work lists and maps in fw
+    FrameDec(const FrameInputs &in, FrameWork &fw)
+        : in_(in), s(*in.seq), h(*in.hdr), fw(fw), mw(fw), own_sh_(new FrameShared), S(own_sh_.get()), master_(true) {}
+    // a tile decoder of `m`'s frame: its blocks' work lists in `own` (merged by the frame's
+    // decoder afterwards), the frame's maps in m's FrameWork and FrameShared
+    FrameDec(const FrameDec &m, FrameWork &own)
+        : in_(m.in_), s(m.s), h(m.h), fw(own), mw(m.fw), S(m.S), master_(false), ts_(m.ts_) {}
+    // threads > 1: the frame's tiles decoded on up to that many threads (rav1d's tile threads)
+    int run(FrameResult &res, std::string &err, int threads = 1);
 
 private:
     const FrameInputs &in_;
     const SeqHdr &s;
     const FrameHdr &h;
-    FrameWork &fw;
+    FrameWork &fw;        // work lists of the blocks this decoder decodes
+    FrameWork &mw;        // the frame's loop-filter / CDEF / LR maps (== fw for the frame's decoder)
+    std::unique_ptr<FrameShared> own_sh_;
+    FrameShared *S;
+    const bool master_;
+    int init_frame();
+    int decode_tile(int k, bool tile_tmvs);
+    void merge_tile(const FrameWork &t);
 
     int bw, bh, w4, h4, sb128w, sb128h, sb_shift, sb_step, sbh, b4_stride, layout, ss_hor, ss_ver, hbd_idx;
     uint16_t dq_frame[8][3][2];
     LfLvl lflvl_frame;
-    std::vector<TileState> ts_;
+    std::vector<TileState> ts_stor_;
+    std::vector<TileState> &ts_ = ts_stor_;   // (a tile decoder's refers to the frame decoder's)
     TileState *ts = nullptr;
     BlockCtx a, l;
     int bx = 0, by = 0;
@@ -69,10 +113,9 @@ private:
     MiAv1Filter *lf_mask = nullptr;
     uint16_t al_pal[2][32][3][8];            // [above / left][pos][plane][entry]
     uint8_t pal_sz_uv[2][32];
-    std::vector<uint8_t> segmap;
-    std::vector<uint8_t> tx_lpf_right[2];    // per tile column: left context at the tile's right edge
-    std::vector<std::vector<uint8_t>> a_tx_lpf_end[2];   // above context at the end of each tile row
-    std::vector<int32_t> owner[3];           // per plane, per 4x4: index of the intra block there
+    Span<uint8_t> segmap;
+    Span<uint8_t> tx_lpf_right[2];           // per tile column: left context at the tile's right edge
+    Span<int32_t> owner[3];                  // per plane, per 4x4: index (in its tile's list) of the intra block there
     int owner_stride;
     std::string *err_ = nullptr;
     bool inter_frame = false;
@@ -108,8 +151,8 @@ private:
 
     // motion-vector state: the frame's refmvs blocks (per 4x4, padded by 8 units on each side)
     // and the per-4x4 Filter2d of inter blocks (frame_thread.b[].filter2d)
-    std::vector<RefMvBlock> rmv;
-    std::vector<uint8_t> f2d_map;
+    Span<RefMvBlock> rmv;
+    Span<uint8_t> f2d_map;
     int rmv_stride = 0;
     std::vector<int32_t> dep_tmp;     // one block's dependency list (reused)
     RefMvBlock &rmv_at(int y4, int x4) { return rmv[(size_t)(y4 + 8) * rmv_stride + (x4 + 8)]; }
@@ -133,12 +176,12 @@ private:
     int8_t pocdiff[7] = {};
     int n_mfmvs = 0, mfmv_ref[3] = {}, mfmv_ref2cur[3] = {}, mfmv_ref2ref[3][7] = {};
     int rp_stride = 0;
-    std::vector<TmvBlock> rp_proj;    // projected temporal MVs of the current sbrow's 8x8 rows
+    Span<TmvBlock> rp_proj;           // projected temporal MVs (8x8 rows of the frame)
     std::shared_ptr<std::vector<TmvBlock>> rp;   // this frame's saved MVs (save_tmvs)
     const TmvBlock *rp_ref[7] = {};
     void refmvs_init_frame();
-    void load_tmvs(int row_start8, int row_end8);
-    void save_tmvs(int row_start8, int row_end8);
+    void load_tmvs(int row_start8, int row_end8, int col_start8, int col_end8);
+    void save_tmvs(int row_start8, int row_end8, int col_start8, int col_end8);
     void refmvs_find(MvCand stack[8], int *cnt, int *ctx, int ref0, int ref1, int bs, int edge_flags);
     Mv gmv_2d(int ref, int bw4, int bh4) const;
     void fix_mv(Mv &mv) const;

@@ -682,7 +682,7 @@ void FrameDec::create_lf_mask_inter(const Block &b, int has_chroma) {
     if (bw4 > 0 && bh4 > 0) {
         for (int y = 0; y < bh4; y++)
             for (int x = 0; x < bw4; x++) {
-                uint8_t *lv = &fw.lf_level[(((size_t)(by + y) * b4_stride) + bx + x) * 4];
+                uint8_t *lv = &mw.lf_level[(((size_t)(by + y) * b4_stride) + bx + x) * 4];
                 lv[0] = fl[0][ri][mi];
                 lv[1] = fl[1][ri][mi];
             }
@@ -695,7 +695,7 @@ void FrameDec::create_lf_mask_inter(const Block &b, int has_chroma) {
     if (cbw4 <= 0 || cbh4 <= 0) return;
     for (int y = 0; y < cbh4; y++)
         for (int x = 0; x < cbw4; x++) {
-            uint8_t *lv = &fw.lf_level[(((size_t)((by >> ss_ver) + y) * b4_stride) + (bx >> ss_hor) + x) * 4];
+            uint8_t *lv = &mw.lf_level[(((size_t)((by >> ss_ver) + y) * b4_stride) + (bx >> ss_hor) + x) * 4];
             lv[2] = fl[2][ri][mi];
             lv[3] = fl[3][ri][mi];
         }

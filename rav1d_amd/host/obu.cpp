@@ -4,6 +4,8 @@
 // decode.rs submit_frame (C src/decode.c:3363-3753).
 #include <cerrno>
 #include <climits>
+#include <chrono>
+#include <new>
 #include <cstdio>
 
 #include "decoder.h"
@@ -867,6 +869,20 @@ void Decoder::release_unused(DecEvent &ev, const int *old_ids) {
     }
 }
 
+// A copy of a reference slot whose frame is still being decoded on a worker: wait for that job
+// and take its results (the job's own thread, for the slots it read at submission).
+static int resolve_copy(RefSlot &r) {
+    if (!r.job) return 0;
+    r.job->wait();
+    if (r.job->rc < 0) return r.job->rc;
+    if (r.cdf_from_job) r.cdf = r.job->res.out_cdf;
+    r.segmap = r.job->res.segmap;
+    r.mvs = r.mvs_from_job ? r.job->res.mvs : nullptr;
+    r.job.reset();
+    r.cdf_from_job = r.mvs_from_job = false;
+    return 0;
+}
+
 int Decoder::submit_frame() {
     const SeqHdr &s = *seq_;
     FrameHdr &h = *frame_hdr_;
@@ -875,9 +891,18 @@ int Decoder::submit_frame() {
     in.hdr = &h;
     in.in_cdf = nullptr;
     for (int i = 0; i < 7; i++) in.refs[i] = nullptr;
-    if (!is_intra_frame(h)) resolve_all();
-    if (h.primary_ref_frame != 7) resolve(refs_[h.refidx[h.primary_ref_frame]]);
-    if (!is_intra_frame(h)) {
+    // threads > 1: every frame on a worker (an inter frame's job resolves its references
+    // itself); the slot CDF of a frame that does not refresh its context is its primary
+    // reference's, resolved here (rare: refresh_context is 1 in every stream we decode)
+    const bool async = threads_ > 1;
+    const bool intra = is_intra_frame(h);
+    if (!async) {
+        if (!intra) resolve_all();
+        if (h.primary_ref_frame != 7) resolve(refs_[h.refidx[h.primary_ref_frame]]);
+    } else if (h.primary_ref_frame != 7 && !h.refresh_context) {
+        resolve(refs_[h.refidx[h.primary_ref_frame]]);
+    }
+    if (!intra) {
         for (int i = 0; i < 7; i++) {
             const RefSlot &r = refs_[h.refidx[i]];
             if (!r.hdr || r.pic_id < 0) {
@@ -887,14 +912,18 @@ int Decoder::submit_frame() {
             in.refs[i] = &r;
         }
     }
+    bool seg_from_primary = false;
     if (h.primary_ref_frame != 7) {
         const RefSlot &r = refs_[h.refidx[h.primary_ref_frame]];
-        if (!r.cdf) return -EINVAL;
+        if (!r.hdr || (!r.cdf && !(r.job && r.cdf_from_job))) return -EINVAL;
         in.in_cdf = r.cdf.get();
         if (h.seg.enabled && (h.seg.temporal || !h.seg.update_map)) {
             const int rw = ((r.hdr->width[0] + 7) >> 3) << 1, rh = ((r.hdr->height + 7) >> 3) << 1;
             const int bw = ((h.width[0] + 7) >> 3) << 1, bh = ((h.height + 7) >> 3) << 1;
-            if (rw == bw && rh == bh) in.prev_segmap = r.segmap;
+            if (rw == bw && rh == bh) {
+                in.prev_segmap = r.segmap;
+                seg_from_primary = true;
+            }
         }
     }
     // split the tile groups into tiles (tile_size_bytes prefixes, decode.rs decode_frame_init_cdf)
@@ -918,10 +947,15 @@ int Decoder::submit_frame() {
             sz -= tsz;
         }
     }
+    static const bool trace = getenv("MI_DEC_TRACE") != nullptr;   // (diagnostics)
+    if (trace)
+        fprintf(stderr, "frame %d: %dx%d type %d show %d tiles %dx%d refresh_ctx %d primary %d refresh_flags %02x\n",
+                next_pic_, h.width[0], h.height, h.frame_type, h.show_frame, h.tiling.cols, h.tiling.rows,
+                h.refresh_context, h.primary_ref_frame, h.refresh_frame_flags);
     auto work = std::make_shared<FrameWork>();
     FrameResult res;
     std::shared_ptr<FrameJob> job;
-    if (threads_ > 1 && is_intra_frame(h)) {
+    if (async) {
         // frame thread: the job owns copies of what the decoder may replace meanwhile
         while ((int)running_.size() >= threads_) {
             running_.front()->wait();
@@ -930,18 +964,58 @@ int Decoder::submit_frame() {
         job = std::make_shared<FrameJob>();
         job->seq = s;
         job->hdr = frame_hdr_;
-        if (in.in_cdf) job->in_cdf = refs_[h.refidx[h.primary_ref_frame]].cdf;
         job->bufs = tile_bufs_;
         job->in = in;
         job->in.seq = &job->seq;
         job->in.hdr = job->hdr.get();
-        job->in.in_cdf = job->in_cdf.get();
+        job->in.in_cdf = nullptr;
+        job->in.prev_segmap = nullptr;
+        for (int i = 0; i < 7; i++) {
+            job->in.refs[i] = nullptr;
+            if (!intra || (h.primary_ref_frame != 7 && i == h.primary_ref_frame)) {
+                job->refs[i] = refs_[h.refidx[i]];
+                if (!intra) job->in.refs[i] = &job->refs[i];
+            }
+        }
+        job->primary = h.primary_ref_frame != 7 ? h.primary_ref_frame : -1;
+        job->seg_from_primary = seg_from_primary;
         job->work = work;
         FrameJob *j = job.get();
-        job->th = std::thread([j] { j->rc = decode_frame(j->in, *j->work, j->res, j->err); });
+        const int nth = threads_;
+        job->th = std::thread([j, nth, intra] {
+            try {
+                // the references' entropy state, segment map and motion vectors
+                for (int i = 0; i < 7 && !j->rc; i++)
+                    if (!intra || i == j->primary) j->rc = resolve_copy(j->refs[i]);
+                if (j->rc) {
+                    j->err = "reference frame failed";
+                } else {
+                    if (j->primary >= 0) {
+                        const RefSlot &p = j->refs[j->primary];
+                        j->in_cdf = p.cdf;
+                        j->in.in_cdf = p.cdf.get();
+                        if (j->seg_from_primary) j->in.prev_segmap = p.segmap;
+                    }
+                    if (j->primary >= 0 && !j->in.in_cdf) {
+                        j->rc = -EINVAL;
+                        j->err = "missing reference entropy state";
+                    } else {
+                        j->rc = decode_frame(j->in, *j->work, j->res, j->err, nth);
+                    }
+                }
+            } catch (const std::bad_alloc &) {
+                j->rc = -ENOMEM;
+                j->err = "out of memory";
+            }
+            j->finish();
+        });
         running_.push_back(job);
     } else {
-        const int r = decode_frame(in, *work, res, error);
+        const auto t0 = std::chrono::steady_clock::now();
+        const int r = decode_frame(in, *work, res, error, 1);
+        if (trace)
+            fprintf(stderr, "  frame %.2f ms\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         if (r < 0) return r;
     }
 
@@ -949,7 +1023,7 @@ int Decoder::submit_frame() {
     ev.work = work;
     ev.job = job;
     ev.pic_id = next_pic_++;
-    if (!is_intra_frame(h))
+    if (!intra)
         for (int i = 0; i < 7; i++) ev.ref_pic[i] = in.refs[i]->pic_id;
     if (h.show_frame) {
         ev.show_pic = ev.pic_id;
@@ -969,7 +1043,7 @@ int Decoder::submit_frame() {
         slot_cdf = c;
     }
     int refpoc[7] = {0};
-    if (!is_intra_frame(h))
+    if (!intra)
         for (int i = 0; i < 7; i++) refpoc[i] = in.refs[i]->hdr->frame_offset;
     int old_ids[8];
     for (int i = 0; i < 8; i++) old_ids[i] = refs_[i].pic_id;

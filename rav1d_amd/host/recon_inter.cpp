@@ -297,7 +297,7 @@ void FrameDec::emit_interintra(const Block &b, int has_chroma) {
             if (k_txdim[t].w * 4 == w && k_txdim[t].h * 4 == hh) tb.tx = (uint8_t)t;
         tb.eob = -1;
         fw.intra_tx.push_back(tb);
-        std::vector<int32_t> &o = owner[pl];
+        Span<int32_t> &o = owner[pl];
         for (int yy = y >> 2; yy < (y + hh) >> 2; yy++)
             for (int xx = x >> 2; xx < (x + w) >> 2; xx++) {
                 const size_t q = (size_t)yy * owner_stride + xx;
@@ -361,7 +361,7 @@ void FrameDec::emit_inter_residual(const Block &b, int has_chroma) {
         fw.dep_start.push_back((int32_t)fw.deps.size());
         for (int32_t d : deps) fw.deps.push_back(d);
         fw.intra_tx.push_back(tb);
-        std::vector<int32_t> &o = owner[plane];
+        Span<int32_t> &o = owner[plane];
         for (int yy = py >> 2; yy < (py + ib.h) >> 2; yy++)
             for (int xx = px >> 2; xx < (px + ib.w) >> 2; xx++) {
                 const size_t q = (size_t)yy * owner_stride + xx;

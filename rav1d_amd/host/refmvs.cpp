@@ -106,8 +106,12 @@ void FrameDec::refmvs_init_frame() {
     }
     TmvBlock inv{};
     inv.mv = kInvalid;
-    rp_proj.assign((size_t)rp_stride * (sb128h * 16 + 16), inv);
-    rp = std::make_shared<std::vector<TmvBlock>>((size_t)rp_stride * sb128h * 16, TmvBlock{});
+    if (master_) {
+        S->rp_proj.assign((size_t)rp_stride * (sb128h * 16 + 16), inv);
+        S->rp = std::make_shared<std::vector<TmvBlock>>((size_t)rp_stride * sb128h * 16, TmvBlock{});
+    }
+    rp_proj.bind(S->rp_proj);
+    rp = S->rp;
 }
 
 // mv_projection (refmvs.rs; C refmvs.c:175-191)
@@ -124,9 +128,11 @@ static Mv mv_projection(Mv mv, int num, int den) {
     return r;
 }
 
-void FrameDec::load_tmvs(int row_start8, int row_end8) {
+// over the 8x8 columns [col_start8, col_end8): the frame (decode_frame_main) or one tile (rav1d's
+// tile threads pass the tile's columns, thread_task.rs)
+void FrameDec::load_tmvs(int row_start8, int row_end8, int col_start8, int col_end8) {
     row_end8 = imin(row_end8, ih8);
-    const int col_start8 = 0, col_end8 = iw8;
+    col_end8 = imin(col_end8, iw8);
     const int col_start8i = imax(col_start8 - 8, 0), col_end8i = imin(col_end8 + 8, iw8);
     const ptrdiff_t stride = rp_stride;
     for (int y = row_start8; y < row_end8; y++)
@@ -176,12 +182,12 @@ void FrameDec::load_tmvs(int row_start8, int row_end8) {
     }
 }
 
-void FrameDec::save_tmvs(int row_start8, int row_end8) {
+void FrameDec::save_tmvs(int row_start8, int row_end8, int col_start8, int col_end8) {
     row_end8 = imin(row_end8, ih8);
-    const int col_end8 = iw8;
+    col_end8 = imin(col_end8, iw8);
     for (int y = row_start8; y < row_end8; y++) {
         TmvBlock *out = rp->data() + (size_t)y * rp_stride;
-        for (int x = 0; x < col_end8;) {
+        for (int x = col_start8; x < col_end8;) {
             const RefMvBlock &c = rmv_at(2 * y + 1, 2 * x + 1);
             const int bw8 = (k_bdim[c.bs].w4 + 1) >> 1;
             TmvBlock t{};

@@ -26,9 +26,12 @@ def load(v):
     return open(os.path.join(GOLDEN, v["file"]), "rb").read()
 
 
+@pytest.mark.parametrize("threads", [1, 4], ids=["t1", "t4"])
 @pytest.mark.parametrize("v", VECTORS, ids=[v["name"] for v in VECTORS])
-def test_oracle_matches_reference_md5(v):
-    md5, n = decode_stream(load(v), apply_grain=bool(v.get("filmgrain")))
+def test_oracle_matches_reference_md5(v, threads):
+    """threads 4: the front-end's frame threads (intra frames) and tile threads (every frame's
+    tiles on their own decoders, work lists merged in tile order)."""
+    md5, n = decode_stream(load(v), apply_grain=bool(v.get("filmgrain")), threads=threads)
     assert n > 0
     assert md5 == v["md5"], f"{v['name']}: {n} frames, md5 {md5} != {v['md5']}"
 
