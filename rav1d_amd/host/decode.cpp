@@ -725,7 +725,13 @@ void FrameDec::create_lf_mask_intra(const Block &b, int has_chroma) {
 // of the pixels its prediction reads
 
 void FrameDec::add_deps(int plane, int x0, int y0, int x1, int y1, std::vector<int32_t> &out) {
-    // pixel rectangle [x0, x1) x [y0, y1) of `plane`, 4x4 granular
+    // pixel rectangle [x0, x1) x [y0, y1) of `plane`, 4x4 granular, inside the current tile:
+    // prediction never reads across a tile edge (the edge flags stop at it; the top-left sample
+    // is read only with both a left and a top neighbour), and the owners of other tiles' pixels
+    // are indices into those tiles' lists
+    const int sh = plane ? ss_hor : 0, sv = plane ? ss_ver : 0;
+    x0 = imax(x0, (ts->col_start * 4) >> sh);
+    y0 = imax(y0, (ts->row_start * 4) >> sv);
     const Span<int32_t> &o = owner[plane];
     for (int y = y0 >> 2; y < (y1 + 3) >> 2; y++)
         for (int x = x0 >> 2; x < (x1 + 3) >> 2; x++) {

@@ -55,11 +55,12 @@ def _refs(pics, ev, key=lambda p: p):
     return out
 
 
-def decode_ivf(ctx, data, stream=None, sync_each=True, inloop_filters=14):
+def decode_ivf(ctx, data, stream=None, sync_each=True, inloop_filters=14, threads=1):
     """Decode a stream (IVF, Annex B or section 5) on the device; yields the shown pictures (Frame, device planes) in
     output order. With sync_each, every frame is checked with mi_frame_end before it is shown.
-    inloop_filters: Dav1dSettings.inloop_filters (rav1d_amd.av1dec.INLOOPFILTER_*)."""
-    dec = Av1Decoder(inloop_filters=inloop_filters)
+    inloop_filters: Dav1dSettings.inloop_filters (rav1d_amd.av1dec.INLOOPFILTER_*). threads > 1: the
+    front-end's frame and tile threads (mi_dec_set_threads)."""
+    dec = Av1Decoder(threads, inloop_filters=inloop_filters)
     pics = {}
     for tu in stream_units(data):
         dec.send(tu)

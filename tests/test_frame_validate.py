@@ -28,10 +28,11 @@ def fake_picture(w, h, bpc, layout, base):
     return p
 
 
-def frames_with_pictures(data):
-    """(MiDecFrame copy, MiFramePictures) of every frame of a stream, refs filled."""
+def frames_with_pictures(data, threads=1):
+    """(MiDecFrame copy, MiFramePictures) of every frame of a stream, refs filled. threads > 1:
+    the front-end's frame and tile threads (work lists merged from the tiles' decoders)."""
     geo = {}
-    for ev in stream_events(data):
+    for ev in stream_events(data, threads):
         if not ev.frame:
             continue
         fr = MiDecFrame.from_buffer_copy(ev.frame.contents)
@@ -52,11 +53,12 @@ def validate(fr, ps):
     return rc, (why.value or b"").decode()
 
 
+@pytest.mark.parametrize("threads", [1, 8], ids=["t1", "t8"])
 @pytest.mark.parametrize("v", VECTORS, ids=[v["name"] for v in VECTORS])
-def test_front_end_frames_validate(v):
+def test_front_end_frames_validate(v, threads):
     data = open(os.path.join(GOLDEN, v["file"]), "rb").read()
     n = 0
-    for fr, ps, _ in frames_with_pictures(data):
+    for fr, ps, _ in frames_with_pictures(data, threads):
         rc, why = validate(fr, ps)
         assert rc == 0, f"{v['name']} frame {n}: rejected by {why}"
         n += 1

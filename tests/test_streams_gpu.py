@@ -17,11 +17,11 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "str
 VECTORS = json.load(open(os.path.join(GOLDEN, "vectors.json")))
 
 
-def gpu_md5(ctx, data):
+def gpu_md5(ctx, data, threads=1):
     from rav1d_amd.stream import decode_ivf
     md5 = hashlib.md5()
     n = 0
-    for pic in decode_ivf(ctx, data):
+    for pic in decode_ivf(ctx, data, threads=threads):
         planes = [pic.buffer_np(p) for p in range(len(pic.planes))]
         md5_update_picture(md5, planes, pic.w, pic.h, pic.layout)
         n += 1
@@ -29,9 +29,14 @@ def gpu_md5(ctx, data):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("threads", [1, 8], ids=["t1", "t8"])
 @pytest.mark.parametrize("v", VECTORS, ids=[v["name"] for v in VECTORS])
-def test_gpu_decode_matches_reference_md5(gpu, v):
+def test_gpu_decode_matches_reference_md5(gpu, v, threads):
+    """threads 8: the work lists of the front-end's tile decoders (merged in tile order, intra
+    dependencies inside each tile) and frame threads, through the device."""
     data = open(os.path.join(GOLDEN, v["file"]), "rb").read()
+    if v.get("filmgrain") and threads > 1:
+        pytest.skip("grain vectors: covered at threads 1 (the grain path does not depend on the work lists)")
     if v.get("filmgrain"):
         # --filmgrain 1: the grain is applied on the device as the picture is output
         from rav1d_amd.output import Muxer
@@ -41,7 +46,7 @@ def test_gpu_decode_matches_reference_md5(gpu, v):
         md5 = m.digest()
         m.close()
     else:
-        md5, n = gpu_md5(gpu, data)
+        md5, n = gpu_md5(gpu, data, threads)
     assert n > 0
     assert md5 == v["md5"], f"{v['name']}: {n} frames, md5 {md5} != {v['md5']}"
 
