@@ -86,6 +86,20 @@ typedef struct MiDecFrame {
     const uint8_t *masks;             /* wedge masks (MASK inputs) and room for SEG outputs */
     size_t nmasks;
     size_t ntmp;                      /* int16 elements of the arena the prep sides write */
+    /* Optional: the intra queue mi_frame_run would plan (intra_plan.h), made off its critical
+     * path (the front-end's frame jobs fill it): the n_intra blocks / transforms in queue order
+     * (vertical strips, one per XCD, each by dependency level), dependencies as queue positions
+     * (CSR, q_dep_start has n_intra + 1 entries), q_nstrips > 1: strip k = queue entries
+     * [q_strip_start[k], q_strip_start[k + 1]); q_granules: edges handed over as granules (an
+     * intra-only frame without inter-intra items). NULL q_intra: mi_frame_run plans. */
+    const MiIntraBlock *q_intra;
+    const MiTxBlock *q_intra_tx;
+    const int32_t *q_dep_start;
+    const int32_t *q_deps;
+    int32_t q_n_deps;
+    const int32_t *q_strip_start;
+    int32_t q_nstrips;
+    int32_t q_granules;
 } MiDecFrame;
 
 /* One decoder event: a frame to reconstruct into picture `pic_id` (frame != NULL; its inter

@@ -40,7 +40,10 @@ class MiDecFrame(ctypes.Structure):
                 ("combine_y", ctypes.c_void_p), ("n_combine_y", ctypes.c_int32),
                 ("combine_uv", ctypes.c_void_p), ("n_combine_uv", ctypes.c_int32),
                 ("masks", ctypes.c_void_p), ("nmasks", ctypes.c_size_t),
-                ("ntmp", ctypes.c_size_t)]
+                ("ntmp", ctypes.c_size_t),
+                ("q_intra", ctypes.c_void_p), ("q_intra_tx", ctypes.c_void_p), ("q_dep_start", ctypes.c_void_p),
+                ("q_deps", ctypes.c_void_p), ("q_n_deps", ctypes.c_int32), ("q_strip_start", ctypes.c_void_p),
+                ("q_nstrips", ctypes.c_int32), ("q_granules", ctypes.c_int32)]
 
 
 class MiDecEvent(ctypes.Structure):
@@ -230,6 +233,7 @@ def stream_events(data, threads=1, lookahead=None, inloop_filters=INLOOPFILTER_A
     valid until the next one is requested."""
     dec = Av1Decoder(threads, inloop_filters)
     la = 0 if threads <= 1 else (lookahead if lookahead is not None else 2 * threads)
+    # (threads > 1 with lookahead 0: one temporal unit at a time, its frame's tiles in parallel)
     sent = 0
     for tu in stream_units(data):
         dec.send(tu)

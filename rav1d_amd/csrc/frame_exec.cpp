@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "ctx.h"
+#include "intra_plan.h"
 #include "../../include/mi_av1dec.h"
 
 namespace {
@@ -181,9 +182,7 @@ size_t coef_span(const mi::TxDim &d, int txtp, int eob) {
 
 bool pow2_in(int v, int lo, int hi) { return v >= lo && v <= hi && !(v & (v - 1)); }
 
-bool inter_present(const MiDecFrame *f) {
-    return f->n_mc || f->n_obmc_h || f->n_obmc_v || f->n_warp || f->n_scaled || f->n_combine_y || f->n_combine_uv;
-}
+bool inter_present(const MiDecFrame *f) { return mi_plan::inter_present(f); }
 
 // The reference pictures an inter frame's units read (same bit depth and layout, planes present)
 // and which of them differ in size from the frame (the scaled-reference path).
@@ -327,9 +326,8 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
     const bool inter = inter_present(f);
     // per-block checks on the planning pool (ranges of blocks; a failing range is re-checked
     // on the calling thread, whose g_why the caller reads)
-    auto check = [&](int i) -> int {
-        const MiIntraBlock &b = f->intra[i];
-        const MiTxBlock &t = f->intra_tx[i];
+    // one block with its transform (decode order, or the front-end's queue order)
+    auto check_block = [&](const MiIntraBlock &b, const MiTxBlock &t) -> int {
         if (b.plane >= nplanes || t.plane != b.plane || t.x != b.x || t.y != b.y) return BAD();
         const int tx = tx_of(b.w, b.h);
         if (tx < 0 || t.tx != tx) return BAD();
@@ -374,6 +372,10 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
             // inter-intra: slots 0-12 with the blend mask in idx, in an inter frame
             if (mode > 12 || (size_t)b.aux_off + (size_t)b.w * b.h > f->nidx || !inter) return BAD();
         }
+        return 0;
+    };
+    auto check = [&](int i) -> int {
+        if (int e = check_block(f->intra[i], f->intra_tx[i])) return e;
         for (int d = f->dep_start[i]; d < f->dep_start[i + 1]; d++)
             if (d < 0 || d >= f->n_deps || f->deps[d] < 0 || f->deps[d] >= i) return BAD();
         if (f->dep_start[i + 1] < f->dep_start[i]) return BAD();
@@ -387,6 +389,26 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
     if (bad.load())
         for (int i = 0; i < f->n_intra; i++)
             if (int e = check(i)) return e;
+    // the front-end's intra queue (MiDecFrame.q_*): every block as above, dependencies inside
+    // the queue (they may point forward across strips: the kernel waits on them), strips
+    // partitioning it
+    if (f->q_intra) {
+        const int n = f->n_intra;
+        if (!f->q_intra_tx || !f->q_dep_start || f->q_n_deps < 0 || (f->q_n_deps && !f->q_deps)) return BAD();
+        if (f->q_dep_start[0] != 0 || f->q_dep_start[n] != f->q_n_deps) return BAD();
+        for (int i = 0; i < n; i++) {
+            if (int e = check_block(f->q_intra[i], f->q_intra_tx[i])) return e;
+            if (f->q_dep_start[i + 1] < f->q_dep_start[i]) return BAD();
+            for (int d = f->q_dep_start[i]; d < f->q_dep_start[i + 1]; d++)
+                if (f->q_deps[d] < 0 || f->q_deps[d] >= n || f->q_deps[d] == i) return BAD();
+        }
+        if (f->q_nstrips > 1) {
+            if (!f->q_strip_start || f->q_nstrips > 8 || f->q_strip_start[0] != 0 || f->q_strip_start[f->q_nstrips] != n)
+                return BAD();
+            for (int k = 0; k < f->q_nstrips; k++)
+                if (f->q_strip_start[k + 1] < f->q_strip_start[k]) return BAD();
+        }
+    }
     const int sb128w = (f->w + 127) >> 7, sb128h = (f->h + 127) >> 7;
     if (f->filter_y && (!f->lf_level || !f->lf_masks || f->sb128w != sb128w || f->sb128h != sb128h ||
                         f->b4_stride < sb128w * 32))
@@ -394,153 +416,6 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
     if (f->cdef_on && (!f->lf_masks || f->sb128w != sb128w || f->sb128h != sb128h)) return BAD();
     if (f->restore_planes && (!f->lr_mask || f->lr_sb128w != ((f->up_w + 127) >> 7))) return BAD();
     return 0;
-}
-
-// ---- one frame's intra blocks over every XCD (mi_internal::intra_recon strips) ----
-//
-// The persistent reconstruction hands pixels from block to block through the reading XCD's L2
-// (ipred.hip), so a line must never be read on an XCD while another XCD may still write it.
-// The frame is cut into up to 8 vertical strips, strip q reconstructed on XCD q, with every
-// boundary a 128-B line boundary in every plane (and a multiple of 64 luma px). A block that
-// reads pixels of another strip (its left column, top-left and top-right edges at a strip
-// boundary) gets, besides the owners of those pixels, every block writing the lines they lie
-// in: when it first reads such a line on its XCD, the line is final. All those writers precede
-// the block in decode order (the lines lie in superblocks decoded before it: the left
-// neighbour superblock or the superblock row above; an intra block copy source lies a
-// superblock row above or 256 px left of the current superblock, spec 7.11.2 / rav1d
-// decode.rs); if one did not, the frame stays on one XCD. Returns the number of strips (1: no
-// split); strip[i] per block, extra deps as CSR. With edge granules (frame_run) a block reads
-// the picture only for intra block copy and CfL's luma: edges need no extra deps.
-int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<int32_t> &xs,
-                 std::vector<int32_t> &xd, bool granules) {
-    const int n = f->n_intra;
-    const int maxs = 8;
-    if (n < 64) return 1;
-    const int pxb = f->bpc == 8 ? 1 : 2;
-    const int ssh = f->layout == 1 || f->layout == 2, ssv = f->layout == 1;
-    const int nplanes = f->layout ? 3 : 1;
-    const int unit = (128 / pxb) << (f->layout ? ssh : 0);   // luma px per line of the widest plane
-    const int units = (f->w + unit - 1) / unit;
-    const int ns = std::min(maxs, units);
-    if (ns < 2) return 1;
-    std::vector<int> sx(ns + 1);
-    for (int q = 0; q <= ns; q++) sx[q] = (int)((int64_t)q * units / ns) * unit;
-    // strip of every block (by its luma column) and the owner of every 4x4 unit of each plane
-    strip.resize(n);
-    // with edge granules only intra block copy reads pixels across strips (CfL's luma lies in
-    // its own strip): without such blocks there are no extra deps and no owner map is needed
-    bool need_own = !granules;
-    for (int i = 0; !need_own && i < n; i++) need_own = f->intra[i].mode == MI_INTRA_IBC;
-    if (!need_own) {
-        for (int i = 0; i < n; i++) {
-            const MiIntraBlock &b = f->intra[i];
-            const int xl = b.plane ? b.x << ssh : b.x;
-            strip[i] = (int8_t)(std::upper_bound(sx.begin(), sx.end(), xl) - sx.begin() - 1);
-        }
-        xs.assign(n + 1, 0);
-        xd.clear();
-        return ns;
-    }
-    const int aw = (f->w + 127) & ~127, ah = (f->h + 127) & ~127;
-    int pw4[3], ph4[3];
-    // (per-thread scratch kept across frames: a fresh multi-MB map per frame costs its page
-    // faults; bound by reference here, since the pool threads below must see this thread's)
-    static thread_local std::vector<int32_t> own_tl[3];
-    std::vector<int32_t> (&own)[3] = own_tl;
-    for (int p = 0; p < nplanes; p++) {
-        pw4[p] = (p ? aw >> ssh : aw) >> 2;
-        ph4[p] = (p ? ah >> ssv : ah) >> 2;
-        own[p].assign((size_t)pw4[p] * ph4[p], -1);
-    }
-    // The owner of a cell is its LAST writer in decode order: an inter-intra item and the
-    // residual items over the same rectangle (MI_INTRA_II then MI_INTRA_RESID) overlap, and the
-    // residual must win. Several threads fill the map, so each cell keeps the maximum index
-    // (a relaxed CAS loop; the pool's join orders it before the reads below).
-    parallel_ranges(n, 32768, [&](int lo, int hi, int) {
-        for (int i = lo; i < hi; i++) {
-            const MiIntraBlock &b = f->intra[i];
-            const int xl = b.plane ? b.x << ssh : b.x;
-            strip[i] = (int8_t)(std::upper_bound(sx.begin(), sx.end(), xl) - sx.begin() - 1);
-            for (int y = b.y >> 2; y < (b.y + b.h) >> 2; y++)
-                for (int x = b.x >> 2; x < (b.x + b.w) >> 2; x++) {
-                    int32_t *cell = &own[b.plane][(size_t)y * pw4[b.plane] + x];
-                    int32_t cur = __atomic_load_n(cell, __ATOMIC_RELAXED);
-                    while (cur < i && !__atomic_compare_exchange_n(cell, &cur, i, true, __ATOMIC_RELAXED,
-                                                                   __ATOMIC_RELAXED)) {
-                    }
-                }
-        }
-    });
-    xs.assign(n + 1, 0);
-    xd.clear();
-    const int lpx = 128 / pxb;                                // plane px per line
-    // the blocks writing a line that block i reads across a strip boundary (false: a later
-    // writer, so the frame stays on one XCD)
-    auto scan_block = [&](int i, std::vector<int32_t> &add) -> bool {
-        const MiIntraBlock &b = f->intra[i];
-        const int p = b.plane;
-        add.clear();
-        // the pixels this block may read: its edges (rows y-1 .. y+2h-1, columns x-1 .. x+2w-1),
-        // or for intra block copy the source rectangle (+1 for the bilinear phase, +-1 margin)
-        int bx0 = std::max(0, (int)b.x - 1), by0 = std::max(0, (int)b.y - 1);
-        int bx1 = b.x + 2 * b.w, by1 = b.y + 2 * b.h;
-        if (b.mode == MI_INTRA_IBC) {
-            const int mvx = (int16_t)(b.reserved & 0xffff), mvy = (int16_t)(b.reserved >> 16);
-            const int sh = b.filt_idx & 1, sv = (b.filt_idx >> 1) & 1;
-            const int sx = b.x + (mvx >> (3 + sh)), sy = b.y + (mvy >> (3 + sv));
-            bx0 = std::max(0, sx - 1);
-            by0 = std::max(0, sy - 1);
-            bx1 = sx + b.w + 2;
-            by1 = sy + b.h + 2;
-        }
-        for (int d = f->dep_start[i]; d < f->dep_start[i + 1]; d++) {
-            const int j = f->deps[d];
-            if (strip[j] == strip[i]) continue;
-            const MiIntraBlock &o = f->intra[j];
-            if (granules && o.plane == p && b.mode != MI_INTRA_IBC) continue;   // an edge: granules
-            if (o.plane != p) return false;                   // (CfL luma: same strip by construction)
-            const int x0 = std::max(bx0, (int)o.x), x1 = std::min(bx1, o.x + o.w);
-            const int y0 = std::max(by0, (int)o.y), y1 = std::min(by1, o.y + o.h);
-            if (x0 >= x1 || y0 >= y1) continue;
-            const int l0 = x0 / lpx, l1 = (x1 - 1) / lpx;     // lines of those rows
-            for (int y = y0 >> 2; y <= (y1 - 1) >> 2; y++)
-                for (int u = (l0 * lpx) >> 2; u < std::min(pw4[p], ((l1 + 1) * lpx) >> 2); u++) {
-                    const int w = own[p][(size_t)y * pw4[p] + u];
-                    if (w < 0 || w == j) continue;
-                    if (w >= i) return false;                 // a later writer: no split
-                    add.push_back(w);
-                }
-        }
-        std::sort(add.begin(), add.end());
-        add.erase(std::unique(add.begin(), add.end()), add.end());
-        return true;
-    };
-    // the extra dependencies per block range (each range its own CSR part), then concatenated
-    std::vector<int32_t> part_xd[8];
-    int part_lo[9] = {};
-    int split_ok = 1;
-    const int nparts = parallel_ranges(n, 32768, [&](int lo, int hi, int t) {
-        part_lo[t] = lo;
-        std::vector<int32_t> &pxd = part_xd[t];
-        std::vector<int32_t> add;
-        for (int i = lo; i < hi; i++) {
-            xs[i] = (int32_t)pxd.size();
-            if (!__atomic_load_n(&split_ok, __ATOMIC_RELAXED) || !scan_block(i, add)) {
-                __atomic_store_n(&split_ok, 0, __ATOMIC_RELAXED);
-                return;
-            }
-            pxd.insert(pxd.end(), add.begin(), add.end());
-        }
-    });
-    if (!split_ok) return 1;
-    for (int t = 0; t < nparts; t++) {
-        const int lo = part_lo[t], hi = t + 1 < nparts ? part_lo[t + 1] : n;
-        const int32_t base = (int32_t)xd.size();
-        for (int i = lo; i < hi; i++) xs[i] += base;
-        xd.insert(xd.end(), part_xd[t].begin(), part_xd[t].end());
-    }
-    xs[n] = (int32_t)xd.size();
-    return ns;
 }
 
 int stage_upload(MiCtx *ctx, std::vector<Section> &secs, hipStream_t s, hipEvent_t before = nullptr,
@@ -693,11 +568,7 @@ namespace {
 // in queue positions, the inter units bucketed by shape class, the inter residuals grouped by
 // (tx size, picture band). scaled[k]: reference k is scaled (OBMC laps then take mi_mc_scaled).
 struct FramePlan {
-    std::vector<MiIntraBlock> blocks;
-    std::vector<MiTxBlock> tx;
-    std::vector<int32_t> dep_start, deps, strip_start;
-    bool inter = false, granules = false;
-    std::vector<int32_t> tl_ds, tl_deps, tl_strip;     // MI_IR_TIMELINE
+    mi_plan::IntraQueue iq;          // the intra queue, when the front-end did not provide one
     std::vector<MiMcBlock> mc_b, lap_b[2], lap_s[2];
     uint32_t mc_cs[2 * MI_MC_NCLASS + 1], lap_cs[2][2 * MI_MC_NCLASS + 1];
     std::vector<MiTxBlock> itx_b;
@@ -706,133 +577,17 @@ struct FramePlan {
 };
 
 void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
-    const int n = f->n_intra;
-    std::vector<MiIntraBlock> &blocks = pl.blocks;
-    std::vector<MiTxBlock> &tx = pl.tx;
-    std::vector<int32_t> &dep_start = pl.dep_start, &deps = pl.deps, &strip_start = pl.strip_start;
-    std::vector<int32_t> &tl_ds = pl.tl_ds, &tl_deps = pl.tl_deps, &tl_strip = pl.tl_strip;
-    blocks.resize(n);
-    tx.resize(n);
-    dep_start.assign(n + 1, 0);
-    deps.clear();
-    strip_start.clear();
     // (a plan is reused frame after frame: every list that is appended to starts empty)
-    tl_ds.clear();
-    tl_deps.clear();
-    tl_strip.clear();
     pl.lap_s[0].clear();
     pl.lap_s[1].clear();
-
-    // dependency levels (deps always point backwards): level order lets the persistent
-    // kernel's workers run every block of a level side by side. A single frame is split into
-    // vertical strips, one per XCD (intra_strips), each strip's blocks in level order.
-    using clk = std::chrono::steady_clock;
-    const auto t_lv = clk::now();
-    // edge granules (ipred.hip gran_fetch) when every pixel an intra edge reads is written in the
-    // same launch: no inter units, no inter-intra blends or inter residuals. A block then waits
-    // on flags only for the pixels it reads beyond its edges (CfL's luma, intra block copy's
-    // source); the levels still follow every dependency.
-    const bool inter = pl.inter = inter_present(f) || f->n_inter_tx;
-    bool &granules = pl.granules;
-    granules = !inter && n > 0;
-    // MI_IR_TIMELINE=<file> (diagnostics): the launch's per-unit stamps, blocks and dependencies
-    static const char *tl_path = getenv("MI_IR_TIMELINE");
-    for (int i = 0; granules && i < n; i++)
-        if ((f->intra[i].flags & MI_INTRA_II) || f->intra[i].mode == MI_INTRA_RESID) granules = false;
-    if (n) {
-        // per-thread scratch kept across frames (no per-frame page faults)
-        // (the scratch is bound by reference: the pool threads must see this thread's vectors)
-        static thread_local std::vector<int32_t> xs_tl, xd_tl;   // extra dependencies of the strip split (CSR)
-        static thread_local std::vector<int8_t> strip_tl;
-        std::vector<int32_t> &xs = xs_tl, &xd = xd_tl;
-        std::vector<int8_t> &strip = strip_tl;
-        const int nstrips = intra_strips(f, strip, xs, xd, granules);
-        const auto t_a = clk::now();
-        auto each_dep = [&](int i, auto &&fn) {
-            for (int d = f->dep_start[i]; d < f->dep_start[i + 1]; d++) fn(f->deps[d]);
-            if (nstrips > 1)
-                for (int d = xs[i]; d < xs[i + 1]; d++) fn(xd[d]);
-        };
-        static thread_local std::vector<int32_t> level_tl, pos_tl;
-        std::vector<int32_t> &level = level_tl, &pos = pos_tl;
-        level.assign(n, 0);
-        pos.resize(n);
-        int maxl = 0;
-        // MI_IR_NOLEVELS=1 (experiment): decode order within a strip, no level pass
-        for (int i = 0; i < n; i++) {
-            int l = 0;
-            each_dep(i, [&](int d) { l = std::max(l, level[d] + 1); });
-            level[i] = l;
-            maxl = std::max(maxl, l);
-        }
-        const auto t_b = clk::now();
-        // counting sort by (strip, level), decode order within
-        const int nkeys = nstrips * (maxl + 1);
-        auto key = [&](int i) { return (nstrips > 1 ? strip[i] * (maxl + 1) : 0) + level[i]; };
-        std::vector<int32_t> cnt(nkeys + 1, 0);
-        for (int i = 0; i < n; i++) cnt[key(i) + 1]++;
-        for (int k = 0; k < nkeys; k++) cnt[k + 1] += cnt[k];
-        if (nstrips > 1) {
-            strip_start.resize(nstrips + 1);
-            for (int q = 0; q <= nstrips; q++) strip_start[q] = cnt[q * (maxl + 1)];
-        }
-        for (int i = 0; i < n; i++) pos[i] = cnt[key(i)]++;
-        static thread_local std::vector<int32_t> inv_tl;
-        std::vector<int32_t> &inv = inv_tl;
-        inv.resize(n);
-        for (int i = 0; i < n; i++) inv[pos[i]] = i;
-        const auto t_c = clk::now();
-        // the queue-ordered copies, walking the units in decode order (their deps point to
-        // recent units: the reads stay in cache) and scattering the writes: count each unit's
-        // kernel deps, prefix sum in queue order, then fill
-        auto kdeps = [&](int i, auto &&fn) {
-            const MiIntraBlock &b = f->intra[i];
-            if (!granules || b.mode == MI_INTRA_IBC || b.mode == MI_IPRED_CFL) {
-                each_dep(i, [&](int d) { fn(pos[d]); });
-            } else {
-                for (int d = f->dep_start[i]; d < f->dep_start[i + 1]; d++)
-                    if (f->intra[f->deps[d]].plane != b.plane) fn(pos[f->deps[d]]);
-            }
-        };
-        // (ranges of decode order on several threads: every unit has its own queue slot)
-        dep_start[0] = 0;
-        parallel_ranges(n, 32768, [&](int lo, int hi, int) {
-            for (int i = lo; i < hi; i++) {
-                const int k = pos[i];
-                blocks[k] = f->intra[i];
-                tx[k] = f->intra_tx[i];
-                int c = 0;
-                kdeps(i, [&](int) { c++; });
-                dep_start[k + 1] = c;
-            }
-        });
-        for (int k = 0; k < n; k++) dep_start[k + 1] += dep_start[k];
-        deps.resize(dep_start[n]);
-        parallel_ranges(n, 32768, [&](int lo, int hi, int) {
-            for (int i = lo; i < hi; i++) {
-                int o = dep_start[pos[i]];
-                kdeps(i, [&](int d) { deps[o++] = d; });
-            }
-        });
-        static const bool prof = getenv("MI_FX_PROFILE") != nullptr;
-        if (prof) {
-            auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-            fprintf(stderr, "frame_run n=%d strips %.3f levels %.3f sort %.3f permute %.3f ms\n", n, ms(t_lv, t_a),
-                    ms(t_a, t_b), ms(t_b, t_c), ms(t_c, clk::now()));
-        }
-        if (tl_path) {
-            // every dependency (with the strips' extra ones), in queue order
-            tl_ds.assign(n + 1, 0);
-            for (int k = 0; k < n; k++) {
-                tl_ds[k] = (int32_t)tl_deps.size();
-                each_dep(inv[k], [&](int d) { tl_deps.push_back(pos[d]); });
-            }
-            tl_ds[n] = (int32_t)tl_deps.size();
-            tl_strip.assign(strip_start.begin(), strip_start.end());
-        }
+    pl.strips_ms = 0;
+    if (!f->q_intra) {
+        // MI_IR_TIMELINE=<file> (diagnostics): the launch's per-unit stamps, blocks and dependencies
+        static const char *tl_path = getenv("MI_IR_TIMELINE");
+        pl.iq.timeline = tl_path != nullptr;
+        mi_plan::plan_intra(f, pl.iq, [](int n, int min_n, auto &&fn) { return parallel_ranges(n, min_n, fn); });
+        pl.strips_ms = pl.iq.ms;
     }
-    if (deps.empty()) deps.push_back(0);
-    pl.strips_ms = std::chrono::duration<double, std::milli>(clk::now() - t_lv).count();
     std::vector<MiMcBlock> &mc_b = pl.mc_b, (&lap_b)[2] = pl.lap_b, (&lap_s)[2] = pl.lap_s;
     uint32_t *mc_cs = pl.mc_cs;
     uint32_t (&lap_cs)[2][2 * MI_MC_NCLASS + 1] = pl.lap_cs;
@@ -889,11 +644,18 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
     FramePlan &pl = pl_tl;
     plan_frame(f, scaled, pl);
     if (ctx->tm_on) ctx->tm_strips_ms += pl.strips_ms;
-    const bool inter = pl.inter, granules = pl.granules;
-    std::vector<MiIntraBlock> &blocks = pl.blocks;
-    std::vector<MiTxBlock> &tx = pl.tx;
-    std::vector<int32_t> &dep_start = pl.dep_start, &deps = pl.deps, &strip_start = pl.strip_start;
-    std::vector<int32_t> &tl_ds = pl.tl_ds, &tl_deps = pl.tl_deps, &tl_strip = pl.tl_strip;
+    // the intra queue: the front-end's (MiDecFrame.q_*, planned in its frame job) or this plan's
+    const bool inter = mi_plan::inter_present(f) || f->n_inter_tx;
+    const bool have_q = f->q_intra != nullptr;
+    const bool granules = have_q ? f->q_granules != 0 : pl.iq.granules;
+    const MiIntraBlock *q_blocks = have_q ? f->q_intra : pl.iq.blocks.data();
+    const MiTxBlock *q_tx = have_q ? f->q_intra_tx : pl.iq.tx.data();
+    const int32_t *q_ds = have_q ? f->q_dep_start : pl.iq.dep_start.data();
+    const int32_t *q_deps = have_q ? f->q_deps : pl.iq.deps.data();
+    const size_t n_qdeps = have_q ? (size_t)std::max(1, f->q_n_deps) : pl.iq.deps.size();
+    const int32_t *q_ss = have_q ? f->q_strip_start : pl.iq.strip_start.data();
+    const int n_qss = have_q ? (f->q_nstrips > 1 ? f->q_nstrips + 1 : 0) : (int)pl.iq.strip_start.size();
+    std::vector<int32_t> &tl_ds = pl.iq.tl_ds, &tl_deps = pl.iq.tl_deps, &tl_strip = pl.iq.tl_strip;
     std::vector<MiMcBlock> &mc_b = pl.mc_b, (&lap_b)[2] = pl.lap_b, (&lap_s)[2] = pl.lap_s;
     uint32_t *mc_cs = pl.mc_cs;
     uint32_t (&lap_cs)[2][2 * MI_MC_NCLASS + 1] = pl.lap_cs;
@@ -902,10 +664,10 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
     static const char *tl_path = getenv("MI_IR_TIMELINE");
     const int sb128h = (f->h + 127) >> 7;
     std::vector<Section> secs = {
-        { blocks.data(), blocks.size() * sizeof(MiIntraBlock), 0 },
-        { tx.data(), tx.size() * sizeof(MiTxBlock), 0 },
-        { dep_start.data(), dep_start.size() * 4, 0 },
-        { deps.data(), deps.size() * 4, 0 },
+        { q_blocks, (size_t)n * sizeof(MiIntraBlock), 0 },
+        { q_tx, (size_t)n * sizeof(MiTxBlock), 0 },
+        { q_ds, (size_t)(n + 1) * 4, 0 },
+        { q_deps, n_qdeps * 4, 0 },
         { f->coef, f->ncoef * cb, 0 },
         { f->idx, f->nidx, 0 },
         { f->pal, f->npal * pb, 0 },
@@ -995,10 +757,10 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         fr.idx = (const uint8_t *)D(5);
         fr.pal = D(6);
         fr.n = n;
-        if ((r = mi_internal::intra_recon(ctx, &fr, 1, strip_start.empty() ? nullptr : strip_start.data(),
-                                          (int)strip_start.size() - 1, MI_ITX_KEEP_COEFS, stream, granules)))
+        if ((r = mi_internal::intra_recon(ctx, &fr, 1, n_qss ? q_ss : nullptr, n_qss ? n_qss - 1 : 0,
+                                          MI_ITX_KEEP_COEFS, stream, granules)))
             return r;
-        if (tl_path && n > 1000) {
+        if (tl_path && !have_q && n > 1000) {
             std::vector<unsigned long long> t((size_t)n * 16);
             if (hipStreamSynchronize(s) == hipSuccess &&
                 hipMemcpy(t.data(), ctx->ir_tl, t.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
@@ -1006,7 +768,7 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
                     const int32_t hdr[4] = { n, (int32_t)tl_deps.size(), (int32_t)tl_strip.size(), granules };
                     fwrite(hdr, 4, 4, fp);
                     fwrite(t.data(), 8, t.size(), fp);
-                    fwrite(blocks.data(), sizeof(MiIntraBlock), n, fp);
+                    fwrite(q_blocks, sizeof(MiIntraBlock), n, fp);
                     fwrite(tl_ds.data(), 4, tl_ds.size(), fp);
                     fwrite(tl_deps.data(), 4, tl_deps.size(), fp);
                     fwrite(tl_strip.data(), 4, tl_strip.size(), fp);

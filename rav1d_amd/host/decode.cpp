@@ -10,6 +10,7 @@
 // availability of recon_b_intra (C src/recon_tmpl.c:1200-1603), which becomes the flags of
 // each MiIntraBlock.
 #include <cerrno>
+#include <climits>
 #include <cstdio>
 #include <string>
 #include <atomic>
@@ -2080,7 +2081,7 @@ int FrameDec::init_frame() {
         fw.lf_level.assign((size_t)b4_stride * sb128h * 32 * 4, 0);
         fw.lf_masks.assign((size_t)sb128w * sb128h, MiAv1Filter{});
         fw.lr_mask.assign((size_t)fw.sr_sb128w * sb128h, MiAv1Restoration{});
-        S->segmap.assign((size_t)b4_stride * sb128h * 32, 0);
+        S->segmap = std::make_shared<std::vector<uint8_t>>((size_t)b4_stride * sb128h * 32, 0);
         S->tx_lpf_right[0].assign((size_t)align_h * h.tiling.cols, 0);
         S->tx_lpf_right[1].assign((size_t)(align_h >> ss_ver) * h.tiling.cols, 0);
         S->a_tx_lpf_end[0].assign(h.tiling.rows, std::vector<uint8_t>());
@@ -2095,7 +2096,7 @@ int FrameDec::init_frame() {
             S->f2d_map.assign(S->rmv.size(), 0);
         }
     }
-    segmap.bind(S->segmap);
+    segmap.bind(*S->segmap);
     for (int k = 0; k < 2; k++) tx_lpf_right[k].bind(S->tx_lpf_right[k]);
     for (int p = 0; p < 3; p++) owner[p].bind(S->owner[p]);
     rmv.bind(S->rmv);
@@ -2123,12 +2124,15 @@ int FrameDec::decode_tile(int k, bool tile_tmvs) {
     const int c8s = ts->col_start >> 1, c8e = ts->col_end >> 1;
     for (int sby = h.tiling.row_start_sb[tr]; sby < sb_end; sby++) {
         by = sby << sb_shift;
+        if (int r = wait_refs(by)) return r;
         if (tile_tmvs && inter_frame && h.use_ref_frame_mvs) load_tmvs(by >> 1, (by + sb_step) >> 1, c8s, c8e);
         if (ts->msac.cnt < -15) return fail("symbol decoder overread");
         const int r = decode_tile_sbrow(tr, tc);
         if (r) return r;
         if (tile_tmvs && inter_frame) save_tmvs(by >> 1, (by + sb_step) >> 1, c8s, c8e);
+        if (in_.progress) in_.progress->tile_row_done(sby);
     }
+    if (k == h.tiling.update && h.refresh_context && in_.progress) in_.progress->publish_cdf(out_cdf());
     // the above context at the tile row's end (loop-filter fixups at the next tile row), the
     // tile's columns
     if (tr + 1 < h.tiling.rows) {
@@ -2202,9 +2206,33 @@ void FrameDec::merge_tile(const FrameWork &t) {
     fw.pal.insert(fw.pal.end(), t.pal.begin(), t.pal.end());
 }
 
-int FrameDec::run(FrameResult &res, std::string &err, int threads) {
+int FrameDec::wait_refs(int by) {
+    const int rows = by + sb_step;
+    for (int i = 0; i < 7; i++)
+        if (in_.ref_prog[i] && inter_frame && rp_ref[i] && !in_.ref_prog[i]->wait_rows(rows))
+            return fail("reference frame failed");
+    if (in_.prev_segmap_prog && h.seg.enabled && !in_.prev_segmap_prog->wait_rows(rows))
+        return fail("reference frame failed");
+    return 0;
+}
+
+// the entropy state later frames start from (refresh_context): the frame's initial CDFs with
+// the context-update tile's adapted ones (cdf.rs update)
+std::shared_ptr<const Cdf> FrameDec::out_cdf() {
+    auto c = std::make_shared<Cdf>();
+    if (in_.in_cdf) *c = *in_.in_cdf;
+    else cdf_init_default(*c, h.quant.yac);
+    cdf_update_frame(*c, ts_[h.tiling.update].cdf, is_intra_frame(h));
+    return c;
+}
+
+int FrameDec::run(FrameResult &res, std::string &err) {
     err_ = &err;
+    static const bool rtrace = getenv("MI_DEC_TRACE") != nullptr;   // (diagnostics)
+    const auto r0 = std::chrono::steady_clock::now();
+    auto rms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count(); };
     if (int r = init_frame()) return r;
+    if (rtrace) fprintf(stderr, "  init %.2f ms\n", rms());
     const int n_tiles = h.tiling.cols * h.tiling.rows;
     if ((int)in_.tiles.size() != n_tiles) return fail("tile count mismatch");
     ts_.resize(n_tiles);
@@ -2215,8 +2243,20 @@ int FrameDec::run(FrameResult &res, std::string &err, int threads) {
         }
     for (int tr = 0; tr + 1 < h.tiling.rows; tr++)
         for (int pl = 0; pl < 2; pl++) S->a_tx_lpf_end[pl][tr].assign(a.tx_lpf_y.size(), 0);
-    const int nt = imin(threads, n_tiles);
-    if (nt <= 1) {
+    // the frame's segment map as later frames see it: its own (update_map), its primary
+    // reference's, or zeros
+    std::shared_ptr<const std::vector<uint8_t>> seg_out;
+    if (h.seg.enabled) {
+        if (h.seg.update_map) seg_out = S->segmap;
+        else if (in_.prev_segmap) seg_out = in_.prev_segmap;
+        else seg_out = std::make_shared<std::vector<uint8_t>>((size_t)b4_stride * sb128h * 32, 0);
+    }
+    if (in_.progress) {
+        in_.progress->set_tiling(h.tiling.cols, sb_shift, sbh);
+        in_.progress->publish(inter_frame ? rp : nullptr, seg_out);
+    }
+    std::shared_ptr<const Cdf> cdf_done;
+    if (!in_.pool || n_tiles <= 1) {
         // decode.rs decode_frame_main (C decode.c:3225-3244): per sbrow, temporal MVs projected
         // over the frame before its tiles and this frame's MVs saved after them
         for (int tr = 0; tr < h.tiling.rows; tr++) {
@@ -2224,6 +2264,7 @@ int FrameDec::run(FrameResult &res, std::string &err, int threads) {
             const int sb_end = imin(h.tiling.row_start_sb[tr + 1], sbh);
             for (int sby = h.tiling.row_start_sb[tr]; sby < sb_end; sby++) {
                 by = sby << sb_shift;
+                if (int r = wait_refs(by)) return r;
                 if (inter_frame && h.use_ref_frame_mvs) load_tmvs(by >> 1, (by + sb_step) >> 1, 0, iw8);
                 for (int tc = 0; tc < h.tiling.cols; tc++) {
                     ts = &ts_[tr * h.tiling.cols + tc];
@@ -2232,10 +2273,15 @@ int FrameDec::run(FrameResult &res, std::string &err, int threads) {
                     if (r) return r;
                 }
                 if (inter_frame) save_tmvs(by >> 1, (by + sb_step) >> 1, 0, iw8);
+                if (in_.progress) in_.progress->rows_done((sby + 1) << sb_shift);
             }
             if (tr + 1 < h.tiling.rows) {
                 S->a_tx_lpf_end[0][tr] = a.tx_lpf_y;
                 S->a_tx_lpf_end[1][tr] = a.tx_lpf_uv;
+            }
+            if (h.refresh_context && tr == h.tiling.update / h.tiling.cols) {
+                cdf_done = out_cdf();
+                if (in_.progress) in_.progress->publish_cdf(cdf_done);
             }
         }
     } else {
@@ -2245,65 +2291,61 @@ int FrameDec::run(FrameResult &res, std::string &err, int threads) {
         std::vector<FrameWork> tw(n_tiles);
         std::vector<std::string> terr(n_tiles);
         std::vector<int> trc(n_tiles, 0);
-        std::atomic<int> next{0};
-        std::vector<double> tdur(n_tiles, 0.0);
-        auto worker = [&] {
-            for (int k; (k = next.fetch_add(1)) < n_tiles;) {
-                FrameDec td(*this, tw[k]);
-                td.err_ = &terr[k];
-                try {
-                    const auto a0 = std::chrono::steady_clock::now();
-                    trc[k] = td.init_frame();
-                    if (!trc[k]) trc[k] = td.decode_tile(k, true);
-                    tdur[k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a0).count();
-                } catch (const std::bad_alloc &) {
-                    trc[k] = -ENOMEM;
-                    terr[k] = "out of memory";
-                }
-            }
-        };
+        std::vector<double> tdur(n_tiles, 0.0), tstart(n_tiles, 0.0);   // (MI_DEC_TRACE)
         static const bool trace = getenv("MI_DEC_TRACE") != nullptr;   // (diagnostics)
         const auto t0 = std::chrono::steady_clock::now();
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; t++) th.emplace_back(worker);
-        worker();
-        for (std::thread &t : th) t.join();
+        in_.pool->run(n_tiles, [&](int k) {
+            FrameDec td(*this, tw[k]);
+            td.err_ = &terr[k];
+            try {
+                const auto a0 = std::chrono::steady_clock::now();
+                trc[k] = td.init_frame();
+                tstart[k] = std::chrono::duration<double, std::milli>(a0 - t0).count();
+                if (!trc[k]) trc[k] = td.decode_tile(k, true);
+                tdur[k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a0).count();
+            } catch (const std::bad_alloc &) {
+                trc[k] = -ENOMEM;
+                terr[k] = "out of memory";
+            }
+        });
         const auto t1 = std::chrono::steady_clock::now();
         if (trace) {
-            fprintf(stderr, "  tiles %.2f ms:", std::chrono::duration<double, std::milli>(t1 - t0).count());
-            for (double d : tdur) fprintf(stderr, " %.2f", d);
+            fprintf(stderr, "  tiles %.2f ms, each ms (started at):", std::chrono::duration<double, std::milli>(t1 - t0).count());
+            for (int k = 0; k < n_tiles; k++) fprintf(stderr, " %.2f(%.2f)", tdur[k], tstart[k]);
             fprintf(stderr, "\n");
         }
+        const auto t2 = std::chrono::steady_clock::now();
         for (int k = 0; k < n_tiles; k++)
             if (trc[k]) {
                 err = terr[k];
                 return trc[k];
             }
         for (int k = 0; k < n_tiles; k++) merge_tile(tw[k]);
+        if (trace)
+            fprintf(stderr, "  merge %.2f ms\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count());
     }
+    if (rtrace) fprintf(stderr, "  tiles done %.2f ms\n", rms());
     if (h.tiling.cols > 1 || h.tiling.rows > 1) tile_fixups();
     fw.dep_start.push_back((int32_t)fw.deps.size());
+    if (rtrace) fprintf(stderr, "  fixups done %.2f ms\n", rms());
 
-    if (h.refresh_context) {
-        res.out_cdf = std::make_shared<Cdf>();
-        if (in_.in_cdf) *res.out_cdf = *in_.in_cdf;
-        else cdf_init_default(*res.out_cdf, h.quant.yac);
-        cdf_update_frame(*res.out_cdf, ts_[h.tiling.update].cdf, is_intra_frame(h));
-    }
+    if (h.refresh_context) res.out_cdf = cdf_done ? cdf_done : out_cdf();
     if (inter_frame) res.mvs = rp;
-    if (h.seg.enabled) {
-        if (h.seg.update_map) res.segmap = std::make_shared<std::vector<uint8_t>>(std::move(S->segmap));
-        else if (in_.prev_segmap) res.segmap = std::make_shared<std::vector<uint8_t>>(*in_.prev_segmap);
-        else res.segmap = std::make_shared<std::vector<uint8_t>>((size_t)b4_stride * sb128h * 32, 0);
+    res.segmap = seg_out;
+    if (in_.progress) {
+        in_.progress->rows_done(INT_MAX);
+        if (h.refresh_context && !cdf_done) in_.progress->publish_cdf(res.out_cdf);
     }
+    if (rtrace) fprintf(stderr, "  result %.2f ms\n", rms());
     return 0;
 }
 
 }  // namespace fd
 
-int decode_frame(const FrameInputs &in, FrameWork &work, FrameResult &res, std::string &err, int threads) {
+int decode_frame(const FrameInputs &in, FrameWork &work, FrameResult &res, std::string &err) {
     fd::FrameDec d(in, work);
-    return d.run(res, err, threads);
+    return d.run(res, err);
 }
 
 }  // namespace av1

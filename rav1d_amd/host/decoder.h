@@ -11,6 +11,7 @@
 
 #include "av1.h"
 #include "frame.h"
+#include "pool.h"
 
 namespace av1 {
 
@@ -58,7 +59,7 @@ public:
     // Frame threads (rav1d's n_fc): frames are decoded on up to n worker threads while send()
     // parses on (an inter frame's job waits for the jobs of its references), each frame's
     // tiles on up to n threads; events still come out in decode order. 1 (default): synchronous.
-    void set_threads(int n) { threads_ = n < 1 ? 1 : n > 64 ? 64 : n; }
+    void set_threads(int n);
     ~Decoder();
     std::string error;
 
@@ -82,18 +83,50 @@ private:
     std::vector<TileData> tiles_;
     std::vector<std::shared_ptr<std::vector<uint8_t>>> tile_bufs_;
     int threads_ = 1;
+    std::unique_ptr<WorkerPool> pool_;   // threads_ - 1 workers (threads_ > 1)
     std::deque<std::shared_ptr<FrameJob>> running_;
     int n_tiles_ = 0;
     int next_pic_ = 0;
     std::deque<DecEvent> out_;
 };
 
+// What a frame decoding on a worker makes available to the frames that reference it before it
+// ends (rav1d's frame-thread progress, thread_task.rs / picture.rs progress): its saved-MV and
+// segment-id buffers once allocated (published), its entropy state once the context-update tile
+// is decoded, and the 4x4 rows of those buffers that are final. A failed frame wakes every
+// waiter with failure.
+struct FrameProgress {
+    std::shared_ptr<const std::vector<TmvBlock>> mvs;      // (set before published)
+    std::shared_ptr<const std::vector<uint8_t>> segmap;
+    std::shared_ptr<const Cdf> cdf;                         // (set before cdf_ready)
+
+    void publish(std::shared_ptr<const std::vector<TmvBlock>> m, std::shared_ptr<const std::vector<uint8_t>> sm);
+    void publish_cdf(std::shared_ptr<const Cdf> c);
+    // rows [0, n) final (n only grows); tiled decode: superblock row sby of one tile column
+    void rows_done(int n);
+    void set_tiling(int cols, int sb_shift, int sbh);
+    void tile_row_done(int sby);
+    void fail();
+    // false: the frame failed
+    bool wait_published();
+    bool wait_cdf();
+    bool wait_rows(int n);
+
+private:
+    std::mutex m_;
+    std::condition_variable cv_;
+    bool published_ = false, cdf_ready_ = false, failed_ = false;
+    int rows_ = 0;
+    int cols_ = 1, sb_shift_ = 0, front_ = 0;
+    std::vector<int> row_cols_;
+};
+
 // Decode one frame's tiles (decode.rs decode_frame_init + decode_tile_sbrow over every tile)
 // into `work`. Returns 0 or -errno. Fills the state later frames need.
 struct FrameResult {
-    std::shared_ptr<Cdf> out_cdf;                           // refresh_context
-    std::shared_ptr<std::vector<uint8_t>> segmap;
-    std::shared_ptr<std::vector<TmvBlock>> mvs;
+    std::shared_ptr<const Cdf> out_cdf;                     // refresh_context
+    std::shared_ptr<const std::vector<uint8_t>> segmap;
+    std::shared_ptr<const std::vector<TmvBlock>> mvs;
 };
 struct FrameInputs {
     const SeqHdr *seq;
@@ -103,15 +136,22 @@ struct FrameInputs {
     std::shared_ptr<const std::vector<uint8_t>> prev_segmap;
     struct Tile { const uint8_t *data; size_t size; };
     std::vector<Tile> tiles;                                // in tile order
+    WorkerPool *pool = nullptr;                             // tile threads (nullptr: this thread)
+    // frame threads: this frame's progress (signalled as it decodes) and the progress of the
+    // references still decoding whose saved MVs (ref_prog[i]) or segment ids (prev_segmap_prog)
+    // it reads (nullptr: complete)
+    FrameProgress *progress = nullptr;
+    FrameProgress *ref_prog[7] = {};
+    FrameProgress *prev_segmap_prog = nullptr;
 };
-// threads > 1: the frame's tiles on up to that many threads
-int decode_frame(const FrameInputs &in, FrameWork &work, FrameResult &res, std::string &err, int threads = 1);
+int decode_frame(const FrameInputs &in, FrameWork &work, FrameResult &res, std::string &err);
 
 // One frame decoded on a worker thread: copies of everything the decoder may replace while
 // it runs (sequence header, frame header, the temporal unit bytes, the reference slots it
-// reads). An inter frame's job first waits for the jobs of the frames its references come from
-// (their entropy state, segment map and saved motion vectors), as rav1d's frame threads wait
-// on their references' progress (thread_task.rs), then decodes its tiles.
+// reads). A frame's job waits for the entropy state of its primary reference's job, then
+// decodes its tiles, each superblock row once the references still decoding have finished
+// the saved MVs and segment ids of that row, as rav1d's frame threads wait on their
+// references' progress (thread_task.rs).
 struct FrameJob {
     SeqHdr seq;
     std::shared_ptr<const FrameHdr> hdr;
@@ -123,17 +163,29 @@ struct FrameJob {
     bool seg_from_primary = false;
     std::shared_ptr<FrameWork> work;
     FrameResult res;
+    FrameProgress prog;
     std::string err;
     int rc = 0;
     std::thread th;
-    // completion: set once by the job's thread; wait() may be called from any thread
+    // completion, set by the job's thread: the result later frames read (rc, err, res:
+    // finish_result), then the whole job (work with its intra queue: finish); the waits may be
+    // called from any thread
     std::mutex m;
     std::condition_variable cv;
-    bool done = false;
+    bool res_done = false, done = false;
+    void finish_result() {
+        std::lock_guard<std::mutex> g(m);
+        res_done = true;
+        cv.notify_all();
+    }
     void finish() {
         std::lock_guard<std::mutex> g(m);
-        done = true;
+        res_done = done = true;
         cv.notify_all();
+    }
+    void wait_result() {
+        std::unique_lock<std::mutex> g(m);
+        cv.wait(g, [this] { return res_done; });
     }
     void wait() {
         std::unique_lock<std::mutex> g(m);

@@ -5,6 +5,9 @@
 #include <vector>
 
 #include "av1.h"
+#include "mi_av1dec.h"
+
+namespace mi_plan { struct IntraQueue; }
 
 namespace av1 {
 
@@ -76,6 +79,15 @@ struct FrameWork {
     // film grain (applied to the output only)
     int fg_present;
     MiFilmGrainData fg;
+    // the intra queue of the frame executor (csrc/intra_plan.h), planned by plan_intra_queue
+    std::shared_ptr<const mi_plan::IntraQueue> q;
 };
+
+// The MiDecFrame of a FrameWork, every in-loop filter as the frame signals it, with the intra
+// queue when planned (plan.cpp)
+void frame_view(const FrameWork &w, MiDecFrame &f);
+// Plan the frame's intra queue into w.q (ranges of blocks on the pool's workers when given)
+class WorkerPool;
+void plan_intra_queue(FrameWork &w, WorkerPool *pool);
 
 }  // namespace av1

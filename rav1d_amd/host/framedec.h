@@ -49,7 +49,7 @@ struct Span {
 // its own tile): segment ids, the loop filter's tile-edge contexts, intra owners, refmvs blocks,
 // projected and saved temporal MVs
 struct FrameShared {
-    std::vector<uint8_t> segmap;
+    std::shared_ptr<std::vector<uint8_t>> segmap;   // (published to later frames as it fills)
     std::vector<uint8_t> tx_lpf_right[2];
     std::vector<std::vector<uint8_t>> a_tx_lpf_end[2];
     std::vector<int32_t> owner[3];
@@ -85,8 +85,8 @@ public:
     // decoder afterwards), the frame's maps in m's FrameWork and FrameShared
     FrameDec(const FrameDec &m, FrameWork &own)
         : in_(m.in_), s(m.s), h(m.h), fw(own), mw(m.fw), S(m.S), master_(false), ts_(m.ts_) {}
-    // threads > 1: the frame's tiles decoded on up to that many threads (rav1d's tile threads)
-    int run(FrameResult &res, std::string &err, int threads = 1);
+    // with in.pool: the frame's tiles decoded on its workers (rav1d's tile threads)
+    int run(FrameResult &res, std::string &err);
 
 private:
     const FrameInputs &in_;
@@ -99,6 +99,10 @@ private:
     const bool master_;
     int init_frame();
     int decode_tile(int k, bool tile_tmvs);
+    // before superblock row `by`: the references still decoding have finished the saved MVs and
+    // segment ids this row reads (frame threads; -EINVAL when one failed)
+    int wait_refs(int by);
+    std::shared_ptr<const Cdf> out_cdf();
     void merge_tile(const FrameWork &t);
 
     int bw, bh, w4, h4, sb128w, sb128h, sb_shift, sb_step, sbh, b4_stride, layout, ss_hor, ss_ver, hbd_idx;

@@ -21,6 +21,15 @@ static int poc_diff(int bits, int a, int b) {
 
 Decoder::Decoder() {}
 
+void Decoder::set_threads(int n) {
+    n = n < 1 ? 1 : n > 64 ? 64 : n;
+    if (n == threads_) return;
+    for (auto &j : running_) j->wait();
+    running_.clear();
+    threads_ = n;
+    pool_.reset(n > 1 ? new WorkerPool(n - 1) : nullptr);
+}
+
 int Decoder::parse_seq_hdr(Bits &gb, SeqHdr &s) {
     memset(&s, 0, sizeof(s));
     s.profile = gb.bits(3);
@@ -869,17 +878,88 @@ void Decoder::release_unused(DecEvent &ev, const int *old_ids) {
     }
 }
 
-// A copy of a reference slot whose frame is still being decoded on a worker: wait for that job
-// and take its results (the job's own thread, for the slots it read at submission).
-static int resolve_copy(RefSlot &r) {
+void FrameProgress::publish(std::shared_ptr<const std::vector<TmvBlock>> m,
+                            std::shared_ptr<const std::vector<uint8_t>> sm) {
+    std::lock_guard<std::mutex> g(m_);
+    mvs = std::move(m);
+    segmap = std::move(sm);
+    published_ = true;
+    cv_.notify_all();
+}
+
+void FrameProgress::publish_cdf(std::shared_ptr<const Cdf> c) {
+    std::lock_guard<std::mutex> g(m_);
+    cdf = std::move(c);
+    cdf_ready_ = true;
+    cv_.notify_all();
+}
+
+void FrameProgress::rows_done(int n) {
+    std::lock_guard<std::mutex> g(m_);
+    if (n > rows_) {
+        rows_ = n;
+        cv_.notify_all();
+    }
+}
+
+void FrameProgress::set_tiling(int cols, int sb_shift, int sbh) {
+    std::lock_guard<std::mutex> g(m_);
+    cols_ = cols;
+    sb_shift_ = sb_shift;
+    front_ = 0;
+    row_cols_.assign(sbh, 0);
+}
+
+void FrameProgress::tile_row_done(int sby) {
+    std::lock_guard<std::mutex> g(m_);
+    if (sby < 0 || sby >= (int)row_cols_.size()) return;
+    row_cols_[sby]++;
+    const int f0 = front_;
+    while (front_ < (int)row_cols_.size() && row_cols_[front_] == cols_) front_++;
+    if (front_ != f0 && (front_ << sb_shift_) > rows_) {
+        rows_ = front_ << sb_shift_;
+        cv_.notify_all();
+    }
+}
+
+void FrameProgress::fail() {
+    std::lock_guard<std::mutex> g(m_);
+    failed_ = true;
+    cv_.notify_all();
+}
+
+bool FrameProgress::wait_published() {
+    std::unique_lock<std::mutex> g(m_);
+    cv_.wait(g, [this] { return published_ || failed_; });
+    return !failed_;
+}
+
+bool FrameProgress::wait_cdf() {
+    std::unique_lock<std::mutex> g(m_);
+    cv_.wait(g, [this] { return cdf_ready_ || failed_; });
+    return !failed_;
+}
+
+bool FrameProgress::wait_rows(int n) {
+    std::unique_lock<std::mutex> g(m_);
+    cv_.wait(g, [&] { return rows_ >= n || failed_; });
+    return !failed_;
+}
+
+// A copy of a reference slot whose frame is still being decoded on a worker (the job's own
+// thread, for the slots it read at submission): the buffers that frame publishes as it starts
+// (saved MVs, segment ids: their rows are waited for as they are read) and, when `need_cdf`,
+// its entropy state. The slot keeps the job for those waits.
+static int resolve_copy(RefSlot &r, bool need_cdf) {
     if (!r.job) return 0;
-    r.job->wait();
-    if (r.job->rc < 0) return r.job->rc;
-    if (r.cdf_from_job) r.cdf = r.job->res.out_cdf;
-    r.segmap = r.job->res.segmap;
-    r.mvs = r.mvs_from_job ? r.job->res.mvs : nullptr;
-    r.job.reset();
-    r.cdf_from_job = r.mvs_from_job = false;
+    FrameProgress &p = r.job->prog;
+    if (!p.wait_published() || (need_cdf && r.cdf_from_job && !p.wait_cdf())) return -EINVAL;
+    if (need_cdf && r.cdf_from_job) {
+        r.cdf = p.cdf;
+        r.cdf_from_job = false;
+    }
+    r.segmap = p.segmap;
+    r.mvs = r.mvs_from_job ? p.mvs : nullptr;
     return 0;
 }
 
@@ -893,14 +973,18 @@ int Decoder::submit_frame() {
     for (int i = 0; i < 7; i++) in.refs[i] = nullptr;
     // threads > 1: every frame on a worker (an inter frame's job resolves its references
     // itself); the slot CDF of a frame that does not refresh its context is its primary
-    // reference's, resolved here (rare: refresh_context is 1 in every stream we decode)
+    // reference's, whose own job may still be adapting it: waited for here
     const bool async = threads_ > 1;
     const bool intra = is_intra_frame(h);
     if (!async) {
         if (!intra) resolve_all();
         if (h.primary_ref_frame != 7) resolve(refs_[h.refidx[h.primary_ref_frame]]);
     } else if (h.primary_ref_frame != 7 && !h.refresh_context) {
-        resolve(refs_[h.refidx[h.primary_ref_frame]]);
+        RefSlot &r = refs_[h.refidx[h.primary_ref_frame]];
+        if (r.job && r.cdf_from_job) {
+            r.cdf = r.job->prog.wait_cdf() ? r.job->prog.cdf : nullptr;   // (null: that frame failed)
+            r.cdf_from_job = false;
+        }
     }
     if (!intra) {
         for (int i = 0; i < 7; i++) {
@@ -949,9 +1033,9 @@ int Decoder::submit_frame() {
     }
     static const bool trace = getenv("MI_DEC_TRACE") != nullptr;   // (diagnostics)
     if (trace)
-        fprintf(stderr, "frame %d: %dx%d type %d show %d tiles %dx%d refresh_ctx %d primary %d refresh_flags %02x\n",
-                next_pic_, h.width[0], h.height, h.frame_type, h.show_frame, h.tiling.cols, h.tiling.rows,
-                h.refresh_context, h.primary_ref_frame, h.refresh_frame_flags);
+        fprintf(stderr, "frame %d: %dx%d type %d show %d tiles %dx%d upd %d refresh_ctx %d primary %d refresh_flags %02x ref_mvs %d seg %d/%d\n",
+                next_pic_, h.width[0], h.height, h.frame_type, h.show_frame, h.tiling.cols, h.tiling.rows, h.tiling.update,
+                h.refresh_context, h.primary_ref_frame, h.refresh_frame_flags, h.use_ref_frame_mvs, h.seg.enabled, h.seg.update_map);
     auto work = std::make_shared<FrameWork>();
     FrameResult res;
     std::shared_ptr<FrameJob> job;
@@ -980,13 +1064,20 @@ int Decoder::submit_frame() {
         job->primary = h.primary_ref_frame != 7 ? h.primary_ref_frame : -1;
         job->seg_from_primary = seg_from_primary;
         job->work = work;
+        job->in.pool = pool_.get();
         FrameJob *j = job.get();
-        const int nth = threads_;
-        job->th = std::thread([j, nth, intra] {
+        const int pic = next_pic_;
+        job->th = std::thread([j, intra, pic] {
+            using clk = std::chrono::steady_clock;
+            const auto t0 = clk::now();
+            auto t1 = t0, t2 = t0;
             try {
-                // the references' entropy state, segment map and motion vectors
+                // the references' entropy state (the primary's), segment map and motion vectors
                 for (int i = 0; i < 7 && !j->rc; i++)
-                    if (!intra || i == j->primary) j->rc = resolve_copy(j->refs[i]);
+                    if (!intra || i == j->primary) {
+                        j->rc = resolve_copy(j->refs[i], i == j->primary);
+                        if (j->refs[i].job) j->in.ref_prog[i] = &j->refs[i].job->prog;
+                    }
                 if (j->rc) {
                     j->err = "reference frame failed";
                 } else {
@@ -994,25 +1085,48 @@ int Decoder::submit_frame() {
                         const RefSlot &p = j->refs[j->primary];
                         j->in_cdf = p.cdf;
                         j->in.in_cdf = p.cdf.get();
-                        if (j->seg_from_primary) j->in.prev_segmap = p.segmap;
+                        if (j->seg_from_primary) {
+                            j->in.prev_segmap = p.segmap;
+                            j->in.prev_segmap_prog = j->in.ref_prog[j->primary];
+                        }
                     }
                     if (j->primary >= 0 && !j->in.in_cdf) {
                         j->rc = -EINVAL;
                         j->err = "missing reference entropy state";
                     } else {
-                        j->rc = decode_frame(j->in, *j->work, j->res, j->err, nth);
+                        t1 = clk::now();
+                        j->in.progress = &j->prog;
+                        j->rc = decode_frame(j->in, *j->work, j->res, j->err);
                     }
                 }
+                if (j->rc) j->prog.fail();
+                // (the references' jobs are no longer waited for: drop them, or every job would
+                // keep its references' jobs, and theirs, alive)
+                for (RefSlot &r : j->refs) r.job.reset();
+                for (FrameProgress *&p : j->in.ref_prog) p = nullptr;
+                j->in.prev_segmap_prog = nullptr;
+                // later frames need only the result; the event also needs the intra queue
+                j->finish_result();
+                t2 = clk::now();
+                if (!j->rc) plan_intra_queue(*j->work, j->in.pool);
             } catch (const std::bad_alloc &) {
                 j->rc = -ENOMEM;
                 j->err = "out of memory";
+                j->prog.fail();
             }
             j->finish();
+            static const bool jtrace = getenv("MI_DEC_TRACE") != nullptr;   // (diagnostics)
+            if (jtrace) {
+                auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+                fprintf(stderr, "  job %d: refs %.2f decode %.2f plan %.2f ms (start %.3f)\n", pic, ms(t0, t1), ms(t1, t2),
+                        ms(t2, clk::now()), std::chrono::duration<double>(t0.time_since_epoch()).count());
+            }
         });
         running_.push_back(job);
     } else {
         const auto t0 = std::chrono::steady_clock::now();
-        const int r = decode_frame(in, *work, res, error, 1);
+        const int r = decode_frame(in, *work, res, error);
+        if (!r) plan_intra_queue(*work, nullptr);
         if (trace)
             fprintf(stderr, "  frame %.2f ms\n",
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
@@ -1112,7 +1226,7 @@ int Decoder::pop(DecEvent &ev) {
 
 void Decoder::resolve(RefSlot &r) {
     if (!r.job) return;
-    r.job->wait();
+    r.job->wait_result();
     if (r.cdf_from_job) r.cdf = r.job->res.out_cdf;
     r.segmap = r.job->res.segmap;
     r.mvs = r.mvs_from_job ? r.job->res.mvs : nullptr;

@@ -100,8 +100,8 @@ def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=T
     apply_grain is set (Dav1dSettings.apply_grain, src/lib.rs). Returns the pictures written.
 
     pipelined: rav1d's frame threading on this path (src/thread_task.rs):
-      * the host front-end decodes intra frames on `threads` worker threads, a few temporal
-        units ahead of the device (mi_dec_set_threads);
+      * the host front-end decodes frames on `threads` worker threads (each frame's tiles on
+        their own threads too), a few temporal units ahead of the device (mi_dec_set_threads);
       * frames are reconstructed `in_flight` at a time, frame k on (context, stream) k % in_flight;
         a frame whose prediction reads other pictures waits for their events first (allintra:
         80 -> 49 ms with 2 lanes; inter streams whose front-end is the bound: unchanged);
@@ -109,7 +109,7 @@ def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=T
         stream sync), one picture behind; host pictures rotate.
     Device failures of any frame are reported by the mi_frame_end calls at the end of the
     stream. Without pipelined: one frame at a time, each checked by mi_frame_end before it is
-    shown, the front-end synchronous.
+    shown, the front-end one temporal unit at a time (its tiles still on `threads` threads).
 
     stats: a dict to receive the per-stage breakdown: host time waiting for the
     front-end's events (front_end_ms), host time inside mi_frame_run (run_host_ms), the device
@@ -123,7 +123,7 @@ def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=T
     from .output import HostPicture, output_picture
     import torch
     if not pipelined:
-        threads, in_flight = 1, 1
+        in_flight = 1
     lanes = _lanes(ctx, stream, max(1, in_flight))
     streams = [st if st is not None else torch.cuda.current_stream() for _, st in lanes]
     if len(lanes) > 1:
@@ -151,7 +151,9 @@ def decode_to_muxer(ctx, data, muxer, stream=None, apply_grain=True, pipelined=T
             n += 1
 
     slot = 0
-    events = iter(stream_events(data, threads if pipelined else 1, inloop_filters=inloop_filters))
+    # (without pipelined the front-end still decodes each frame's tiles on `threads` threads,
+    # but no temporal unit ahead of the one the device is given)
+    events = iter(stream_events(data, threads, lookahead=None if pipelined else 0, inloop_filters=inloop_filters))
     while True:
         t = clock()
         ev = next(events, None)

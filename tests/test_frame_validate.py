@@ -65,6 +65,44 @@ def test_front_end_frames_validate(v, threads):
     assert n > 0
 
 
+@pytest.mark.parametrize("name", ["av1-1-b8-02-allintra", "00001138"])
+def test_front_end_intra_queue(name):
+    """The front-end's intra queue (MiDecFrame.q_*) is a permutation of the decode-order blocks,
+    its dependencies lie inside it, its strips partition it; without it the frame still
+    validates (mi_frame_run plans), and a queue dependency out of range is rejected."""
+    v = next(x for x in VECTORS if x["name"] == name)
+    data = open(os.path.join(GOLDEN, v["file"]), "rb").read()
+    checked = 0
+    for fr, ps, _ in frames_with_pictures(data, 4):
+        n = fr.n_intra
+        if n == 0:
+            continue
+        assert fr.q_intra and fr.q_dep_start
+        blk = np.ctypeslib.as_array((ctypes.c_uint8 * (32 * n)).from_address(fr.intra)).reshape(n, 32)
+        qb = np.ctypeslib.as_array((ctypes.c_uint8 * (32 * n)).from_address(fr.q_intra)).reshape(n, 32)
+        key = lambda a: sorted(map(bytes, a))
+        assert key(blk) == key(qb)
+        ds = np.ctypeslib.as_array((ctypes.c_int32 * (n + 1)).from_address(fr.q_dep_start))
+        assert ds[0] == 0 and ds[-1] == fr.q_n_deps and (np.diff(ds) >= 0).all()
+        if fr.q_nstrips > 1:
+            ss = np.ctypeslib.as_array((ctypes.c_int32 * (fr.q_nstrips + 1)).from_address(fr.q_strip_start))
+            assert ss[0] == 0 and ss[-1] == n and (np.diff(ss) >= 0).all()
+        assert validate(fr, ps)[0] == 0
+        c = MiDecFrame.from_buffer_copy(fr)
+        c.q_intra = None
+        assert validate(c, ps)[0] == 0
+        if fr.q_n_deps:
+            deps = (ctypes.c_int32 * fr.q_n_deps)()
+            ctypes.memmove(deps, fr.q_deps, 4 * fr.q_n_deps)
+            deps[0] = n
+            c = MiDecFrame.from_buffer_copy(fr)
+            c.q_deps = ctypes.addressof(deps)
+            rc, why = validate(c, ps)
+            assert rc != 0 and why
+        checked += 1
+    assert checked > 0
+
+
 def test_malformed_inter_units_are_rejected():
     v = next(x for x in VECTORS if x["name"] == "00000706")
     data = open(os.path.join(GOLDEN, v["file"]), "rb").read()

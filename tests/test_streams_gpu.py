@@ -17,11 +17,23 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "str
 VECTORS = json.load(open(os.path.join(GOLDEN, "vectors.json")))
 
 
-def gpu_md5(ctx, data, threads=1):
-    from rav1d_amd.stream import decode_ivf
+def _without_queue(fr):
+    """A copy of a MiDecFrame without the front-end's intra queue: mi_frame_run plans it."""
+    from rav1d_amd.av1dec import MiDecFrame
+    c = MiDecFrame.from_buffer_copy(fr)
+    c.q_intra = c.q_intra_tx = c.q_dep_start = c.q_deps = c.q_strip_start = None
+    c.q_n_deps = c.q_nstrips = c.q_granules = 0
+    return c
+
+
+def gpu_md5(ctx, data, threads=1, plan="front-end", monkeypatch=None):
+    from rav1d_amd import stream as S
+    if plan == "executor":
+        run = S.run_frame
+        monkeypatch.setattr(S, "run_frame", lambda c, fr, *a, **k: run(c, _without_queue(fr), *a, **k))
     md5 = hashlib.md5()
     n = 0
-    for pic in decode_ivf(ctx, data, threads=threads):
+    for pic in S.decode_ivf(ctx, data, threads=threads):
         planes = [pic.buffer_np(p) for p in range(len(pic.planes))]
         md5_update_picture(md5, planes, pic.w, pic.h, pic.layout)
         n += 1
@@ -29,13 +41,16 @@ def gpu_md5(ctx, data, threads=1):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("threads", [1, 8], ids=["t1", "t8"])
+@pytest.mark.parametrize("threads,plan", [(1, "front-end"), (1, "executor"), (8, "front-end")],
+                         ids=["t1", "t1-own-plan", "t8"])
 @pytest.mark.parametrize("v", VECTORS, ids=[v["name"] for v in VECTORS])
-def test_gpu_decode_matches_reference_md5(gpu, v, threads):
+def test_gpu_decode_matches_reference_md5(gpu, v, threads, plan, monkeypatch):
     """threads 8: the work lists of the front-end's tile decoders (merged in tile order, intra
-    dependencies inside each tile) and frame threads, through the device."""
+    dependencies inside each tile) and frame threads, through the device. The intra queue is
+    the front-end's (MiDecFrame.q_*, planned on its frame threads) or, own-plan, the one
+    mi_frame_run plans itself from the decode-order lists."""
     data = open(os.path.join(GOLDEN, v["file"]), "rb").read()
-    if v.get("filmgrain") and threads > 1:
+    if v.get("filmgrain") and (threads > 1 or plan != "front-end"):
         pytest.skip("grain vectors: covered at threads 1 (the grain path does not depend on the work lists)")
     if v.get("filmgrain"):
         # --filmgrain 1: the grain is applied on the device as the picture is output
@@ -46,7 +61,7 @@ def test_gpu_decode_matches_reference_md5(gpu, v, threads):
         md5 = m.digest()
         m.close()
     else:
-        md5, n = gpu_md5(gpu, data, threads)
+        md5, n = gpu_md5(gpu, data, threads, plan, monkeypatch)
     assert n > 0
     assert md5 == v["md5"], f"{v['name']}: {n} frames, md5 {md5} != {v['md5']}"
 
