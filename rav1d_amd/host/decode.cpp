@@ -113,7 +113,7 @@ void FrameDec::calc_lf_values(LfLvl &out, const int8_t d[4]) {
 void FrameDec::setup_tile(TileState &t, const uint8_t *data, size_t sz, int row, int col) {
     const int col_sb_start = h.tiling.col_start_sb[col], col_sb_end = h.tiling.col_start_sb[col + 1];
     const int row_sb_start = h.tiling.row_start_sb[row], row_sb_end = h.tiling.row_start_sb[row + 1];
-    if (in_.in_cdf) t.cdf = *in_.in_cdf;
+    if (in_cdf_) t.cdf = *in_cdf_;
     else cdf_init_default(t.cdf, h.quant.yac);
     t.last_qidx = h.quant.yac;
     memset(t.last_delta_lf, 0, 4);
@@ -2081,7 +2081,8 @@ int FrameDec::init_frame() {
         fw.lf_level.assign((size_t)b4_stride * sb128h * 32 * 4, 0);
         fw.lf_masks.assign((size_t)sb128w * sb128h, MiAv1Filter{});
         fw.lr_mask.assign((size_t)fw.sr_sb128w * sb128h, MiAv1Restoration{});
-        S->segmap = std::make_shared<std::vector<uint8_t>>((size_t)b4_stride * sb128h * 32, 0);
+        if (in_.segmap_buf && in_.segmap_buf->size() == (size_t)b4_stride * sb128h * 32) S->segmap = in_.segmap_buf;
+        else S->segmap = std::make_shared<std::vector<uint8_t>>((size_t)b4_stride * sb128h * 32, 0);
         S->tx_lpf_right[0].assign((size_t)align_h * h.tiling.cols, 0);
         S->tx_lpf_right[1].assign((size_t)(align_h >> ss_ver) * h.tiling.cols, 0);
         S->a_tx_lpf_end[0].assign(h.tiling.rows, std::vector<uint8_t>());
@@ -2206,6 +2207,20 @@ void FrameDec::merge_tile(const FrameWork &t) {
     fw.pal.insert(fw.pal.end(), t.pal.begin(), t.pal.end());
 }
 
+}  // namespace fd
+
+void frame_buffers(const FrameHdr &h, std::shared_ptr<std::vector<TmvBlock>> &rp,
+                   std::shared_ptr<std::vector<uint8_t>> &segmap) {
+    // (init_frame's and refmvs_init_frame's geometry)
+    const int bw = ((h.width[0] + 7) >> 3) << 1, bh = ((h.height + 7) >> 3) << 1;
+    const int b4_stride = (bw + 31) & ~31, sb128h = (bh + 31) >> 5;
+    segmap = std::make_shared<std::vector<uint8_t>>((size_t)b4_stride * sb128h * 32, 0);
+    rp.reset();
+    if (!is_intra_frame(h)) rp = std::make_shared<std::vector<TmvBlock>>((size_t)(b4_stride >> 1) * sb128h * 16, TmvBlock{});
+}
+
+namespace fd {
+
 int FrameDec::wait_refs(int by) {
     const int rows = by + sb_step;
     for (int i = 0; i < 7; i++)
@@ -2220,7 +2235,7 @@ int FrameDec::wait_refs(int by) {
 // the context-update tile's adapted ones (cdf.rs update)
 std::shared_ptr<const Cdf> FrameDec::out_cdf() {
     auto c = std::make_shared<Cdf>();
-    if (in_.in_cdf) *c = *in_.in_cdf;
+    if (in_cdf_) *c = *in_cdf_;
     else cdf_init_default(*c, h.quant.yac);
     cdf_update_frame(*c, ts_[h.tiling.update].cdf, is_intra_frame(h));
     return c;
@@ -2235,6 +2250,21 @@ int FrameDec::run(FrameResult &res, std::string &err) {
     if (rtrace) fprintf(stderr, "  init %.2f ms\n", rms());
     const int n_tiles = h.tiling.cols * h.tiling.rows;
     if ((int)in_.tiles.size() != n_tiles) return fail("tile count mismatch");
+    // the frame's maps are published before its entropy state is waited for: frames whose
+    // primary reference is still adapting it are set up meanwhile
+    // (its own segment map also when it is all zeros: no update and no primary reference's)
+    std::shared_ptr<const std::vector<uint8_t>> seg_out;
+    if (h.seg.enabled) seg_out = h.seg.update_map || !in_.prev_segmap ? S->segmap : in_.prev_segmap;
+    if (in_.progress) {
+        in_.progress->set_tiling(h.tiling.cols, sb_shift, sbh);
+        in_.progress->publish(inter_frame ? rp : nullptr, seg_out);
+    }
+    in_cdf_ = in_.in_cdf;
+    if (in_.in_cdf_prog) {
+        if (!in_.in_cdf_prog->wait_cdf()) return fail("reference frame failed");
+        in_cdf_hold_ = in_.in_cdf_prog->cdf;
+        in_cdf_ = in_cdf_hold_.get();
+    }
     ts_.resize(n_tiles);
     for (int tr = 0; tr < h.tiling.rows; tr++)
         for (int tc = 0; tc < h.tiling.cols; tc++) {
@@ -2243,18 +2273,6 @@ int FrameDec::run(FrameResult &res, std::string &err) {
         }
     for (int tr = 0; tr + 1 < h.tiling.rows; tr++)
         for (int pl = 0; pl < 2; pl++) S->a_tx_lpf_end[pl][tr].assign(a.tx_lpf_y.size(), 0);
-    // the frame's segment map as later frames see it: its own (update_map), its primary
-    // reference's, or zeros
-    std::shared_ptr<const std::vector<uint8_t>> seg_out;
-    if (h.seg.enabled) {
-        if (h.seg.update_map) seg_out = S->segmap;
-        else if (in_.prev_segmap) seg_out = in_.prev_segmap;
-        else seg_out = std::make_shared<std::vector<uint8_t>>((size_t)b4_stride * sb128h * 32, 0);
-    }
-    if (in_.progress) {
-        in_.progress->set_tiling(h.tiling.cols, sb_shift, sbh);
-        in_.progress->publish(inter_frame ? rp : nullptr, seg_out);
-    }
     std::shared_ptr<const Cdf> cdf_done;
     if (!in_.pool || n_tiles <= 1) {
         // decode.rs decode_frame_main (C decode.c:3225-3244): per sbrow, temporal MVs projected
@@ -2294,7 +2312,9 @@ int FrameDec::run(FrameResult &res, std::string &err) {
         std::vector<double> tdur(n_tiles, 0.0), tstart(n_tiles, 0.0);   // (MI_DEC_TRACE)
         static const bool trace = getenv("MI_DEC_TRACE") != nullptr;   // (diagnostics)
         const auto t0 = std::chrono::steady_clock::now();
-        in_.pool->run(n_tiles, [&](int k) {
+        // (the context-update tile first: later frames start from its entropy state)
+        in_.pool->run(n_tiles, [&](int i) {
+            const int k = (i + h.tiling.update) % n_tiles;
             FrameDec td(*this, tw[k]);
             td.err_ = &terr[k];
             try {

@@ -100,6 +100,7 @@ struct FrameProgress {
     std::shared_ptr<const std::vector<uint8_t>> segmap;
     std::shared_ptr<const Cdf> cdf;                         // (set before cdf_ready)
 
+    // (once: later calls are ignored)
     void publish(std::shared_ptr<const std::vector<TmvBlock>> m, std::shared_ptr<const std::vector<uint8_t>> sm);
     void publish_cdf(std::shared_ptr<const Cdf> c);
     // rows [0, n) final (n only grows); tiled decode: superblock row sby of one tile column
@@ -141,9 +142,18 @@ struct FrameInputs {
     // references still decoding whose saved MVs (ref_prog[i]) or segment ids (prev_segmap_prog)
     // it reads (nullptr: complete)
     FrameProgress *progress = nullptr;
+    FrameProgress *in_cdf_prog = nullptr;                   // in_cdf: this frame's cdf once ready
     FrameProgress *ref_prog[7] = {};
     FrameProgress *prev_segmap_prog = nullptr;
+    // the saved-MV and segment-id buffers, allocated by the caller before the references are
+    // resolved so that later frames can be given them early (frame_buffers; nullptr: allocated
+    // by decode_frame)
+    std::shared_ptr<std::vector<TmvBlock>> rp_buf;
+    std::shared_ptr<std::vector<uint8_t>> segmap_buf;
 };
+// The saved-MV (inter frames) and segment-id buffers of a frame, zeroed
+void frame_buffers(const FrameHdr &h, std::shared_ptr<std::vector<TmvBlock>> &rp,
+                   std::shared_ptr<std::vector<uint8_t>> &segmap);
 int decode_frame(const FrameInputs &in, FrameWork &work, FrameResult &res, std::string &err);
 
 // One frame decoded on a worker thread: copies of everything the decoder may replace while

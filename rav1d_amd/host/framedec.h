@@ -84,7 +84,7 @@ public:
     // a tile decoder of `m`'s frame: its blocks' work lists in `own` (merged by the frame's
     // decoder afterwards), the frame's maps in m's FrameWork and FrameShared
     FrameDec(const FrameDec &m, FrameWork &own)
-        : in_(m.in_), s(m.s), h(m.h), fw(own), mw(m.fw), S(m.S), master_(false), ts_(m.ts_) {}
+        : in_(m.in_), s(m.s), h(m.h), fw(own), mw(m.fw), S(m.S), master_(false), in_cdf_(m.in_cdf_), ts_(m.ts_) {}
     // with in.pool: the frame's tiles decoded on its workers (rav1d's tile threads)
     int run(FrameResult &res, std::string &err);
 
@@ -97,6 +97,8 @@ private:
     std::unique_ptr<FrameShared> own_sh_;
     FrameShared *S;
     const bool master_;
+    const Cdf *in_cdf_ = nullptr;   // in.in_cdf, or once ready the cdf of in.in_cdf_prog
+    std::shared_ptr<const Cdf> in_cdf_hold_;
     int init_frame();
     int decode_tile(int k, bool tile_tmvs);
     // before superblock row `by`: the references still decoding have finished the saved MVs and

@@ -881,6 +881,7 @@ void Decoder::release_unused(DecEvent &ev, const int *old_ids) {
 void FrameProgress::publish(std::shared_ptr<const std::vector<TmvBlock>> m,
                             std::shared_ptr<const std::vector<uint8_t>> sm) {
     std::lock_guard<std::mutex> g(m_);
+    if (published_) return;
     mvs = std::move(m);
     segmap = std::move(sm);
     published_ = true;
@@ -1072,10 +1073,18 @@ int Decoder::submit_frame() {
             const auto t0 = clk::now();
             auto t1 = t0, t2 = t0;
             try {
-                // the references' entropy state (the primary's), segment map and motion vectors
+                // this frame's maps, published before the references are waited for unless the
+                // segment map is the primary reference's
+                frame_buffers(*j->in.hdr, j->in.rp_buf, j->in.segmap_buf);
+                const FrameHdr &fh = *j->in.hdr;
+                if (!fh.seg.enabled || fh.seg.update_map || !j->seg_from_primary)
+                    j->prog.publish(intra ? nullptr : j->in.rp_buf, fh.seg.enabled ? j->in.segmap_buf : nullptr);
+                // the references' segment maps and motion vectors (their rows are waited for as
+                // they are read) and the primary's entropy state (waited for by decode_frame
+                // once the frame is set up, when its job is still adapting it)
                 for (int i = 0; i < 7 && !j->rc; i++)
                     if (!intra || i == j->primary) {
-                        j->rc = resolve_copy(j->refs[i], i == j->primary);
+                        j->rc = resolve_copy(j->refs[i], false);
                         if (j->refs[i].job) j->in.ref_prog[i] = &j->refs[i].job->prog;
                     }
                 if (j->rc) {
@@ -1083,14 +1092,18 @@ int Decoder::submit_frame() {
                 } else {
                     if (j->primary >= 0) {
                         const RefSlot &p = j->refs[j->primary];
-                        j->in_cdf = p.cdf;
-                        j->in.in_cdf = p.cdf.get();
+                        if (p.job && p.cdf_from_job) {
+                            j->in.in_cdf_prog = &p.job->prog;
+                        } else {
+                            j->in_cdf = p.cdf;
+                            j->in.in_cdf = p.cdf.get();
+                        }
                         if (j->seg_from_primary) {
                             j->in.prev_segmap = p.segmap;
                             j->in.prev_segmap_prog = j->in.ref_prog[j->primary];
                         }
                     }
-                    if (j->primary >= 0 && !j->in.in_cdf) {
+                    if (j->primary >= 0 && !j->in.in_cdf && !j->in.in_cdf_prog) {
                         j->rc = -EINVAL;
                         j->err = "missing reference entropy state";
                     } else {
@@ -1104,7 +1117,7 @@ int Decoder::submit_frame() {
                 // keep its references' jobs, and theirs, alive)
                 for (RefSlot &r : j->refs) r.job.reset();
                 for (FrameProgress *&p : j->in.ref_prog) p = nullptr;
-                j->in.prev_segmap_prog = nullptr;
+                j->in.prev_segmap_prog = j->in.in_cdf_prog = nullptr;
                 // later frames need only the result; the event also needs the intra queue
                 j->finish_result();
                 t2 = clk::now();

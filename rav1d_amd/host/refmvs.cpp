@@ -108,7 +108,9 @@ void FrameDec::refmvs_init_frame() {
     inv.mv = kInvalid;
     if (master_) {
         S->rp_proj.assign((size_t)rp_stride * (sb128h * 16 + 16), inv);
-        S->rp = std::make_shared<std::vector<TmvBlock>>((size_t)rp_stride * sb128h * 16, TmvBlock{});
+        const size_t n = (size_t)rp_stride * sb128h * 16;
+        if (in_.rp_buf && in_.rp_buf->size() == n) S->rp = in_.rp_buf;
+        else S->rp = std::make_shared<std::vector<TmvBlock>>(n, TmvBlock{});
     }
     rp_proj.bind(S->rp_proj);
     rp = S->rp;
