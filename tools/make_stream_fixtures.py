@@ -74,23 +74,10 @@ GRAIN = [
 
 
 def driver_suite(by_path):
-    """The rest of the driver-run GPU suite (round 4): every 10-bit, 12-bit and multi-bit vector
-    of the meson lists, and a representative 8-bit subset (all size / quantizer / features /
-    issues / cdfupdate / mfmv / mv / resize vectors, every 6th 8-bit/data vector under 100 KB,
-    the two smallest vq_suite streams). Returns [(name, rel, md5)], names unique."""
-    base = "/root/reference/tests/dav1d-test-data"
-    out = []
-    data8 = sorted(r for r in by_path if r.startswith("8-bit/data/") and os.path.getsize(os.path.join(base, r)) < 100_000)
-    vq = sorted((r for r in by_path if r.startswith("8-bit/vq_suite/")), key=lambda r: os.path.getsize(os.path.join(base, r)))
-    for rel in sorted(by_path):
-        top, sub = rel.split("/")[:2]
-        keep = top in ("10-bit", "12-bit", "multi-bit")
-        keep |= top == "8-bit" and sub in ("size", "quantizer", "features", "issues", "cdfupdate", "mfmv", "mv", "resize",
-                                           "intra")
-        keep |= rel in data8[::6] or rel in vq[:2]
-        if keep:
-            out.append((by_path[rel][0], rel, by_path[rel][1]))
-    return out
+    """The rest of the driver-run GPU suite: every vector of the meson lists (round 4 held every
+    10-bit, 12-bit and multi-bit vector and an 8-bit subset; round 5 adds the remaining 8-bit
+    data and vq_suite streams). Returns [(name, rel, md5)], names unique."""
+    return [(by_path[rel][0], rel, by_path[rel][1]) for rel in sorted(by_path)]
 
 
 if __name__ == "__main__":
