@@ -216,7 +216,6 @@ __device__ __forceinline__ void sgr_pairs(int *A, int16_t *B, const int16_t *win
     if (s0) {
         sgr_ab<2>(win, A, B, sh, tw, (unsigned)s0, bdm8, xbyx);
         __syncthreads();
-        KTL(2);
         if (act) {
             // A/B on odd rows: even j uses rows j-1 and j+1, odd j row j (r0 is even)
             int cau[2], sau[2], cbu[2], sbu[2], cad[2], sad[2], cbd[2], sbd[2];
@@ -248,12 +247,10 @@ __device__ __forceinline__ void sgr_pairs(int *A, int16_t *B, const int16_t *win
             }
         }
         __syncthreads();
-        KTL(3);
     }
     if (s1) {
         sgr_ab<1>(win, A, B, sh, tw, (unsigned)s1, bdm8, xbyx);
         __syncthreads();
-        KTL(4);
         if (act) {
             int c0[2], t0[2], d0[2], u0[2], c1[2], t1[2], d1[2], u1[2], c2[2], t2[2], d2[2], u2[2];
             ld(r0 - 1, c0, t0, d0, u0);
@@ -870,7 +867,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(6))) void c
     lr_window_edges(cw, T, kFyS, 8, S, E, sh, a.ph[0], a.pw[0], x0, k > 0);
     lr_from_window<Px>(a, lr_unit(a, 0, k, x0, 0, 0), cw, A, B, xbyx, a.dst[0], a.stride[0], S, sh, x0,
                        min(64, a.pw[0] - x0));
-    KTL(5);
+    KTL(6);
 
     // ---- chroma planes: D tile (region 1), CDEF into the window, loop restoration ----
     if constexpr (L != 0) {
@@ -900,7 +897,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(6))) void c
         plane(std::integral_constant<int, 1>());
         plane(std::integral_constant<int, 2>());
     }
-    KTL(6);
+    KTL(5);
 }
 
 int launch_cdef_lr(const CdefLrArgs &a, int layout, int bpc, hipStream_t s) {
