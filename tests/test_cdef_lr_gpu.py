@@ -28,7 +28,9 @@ def run_case(gpu, w, h, bpc, layout, seed, unit_log2=None, restore_planes=None, 
     if cdef_off:
         cd["y_strength"][:] = 0
         cd["uv_strength"][:] = 0
-    lr = make_lr_meta(w, h, layout, rng, sb128=1, unit_log2=unit_log2)
+    # (a 64-px luma unit exists only with 64x64 superblocks: lr_unit_shift, obu.rs)
+    sb128 = 0 if unit_log2 is not None and unit_log2[0] == 6 else 1
+    lr = make_lr_meta(w, h, layout, rng, sb128=sb128, unit_log2=unit_log2)
     if restore_planes is not None:
         lr["restore_planes"] = restore_planes
     cm, lm = CdefMeta(lf["masks"], cd), LrMeta(lr)
@@ -43,11 +45,16 @@ def run_case(gpu, w, h, bpc, layout, seed, unit_log2=None, restore_planes=None, 
     cc = [ref_c[p][:a.shape[0], :a.shape[1]] for p, a in enumerate(planes)]
     ref = oracle_lib.lr_frame(pad_planes(cc, w, h, bpc, layout), pad_planes(planes, w, h, bpc, layout),
                               bpc, layout, w, h, lr)
+    def where(x, y):
+        bad = np.argwhere(x != y)
+        return f"{len(bad)} px differ, first (row, col) {bad[:6].tolist()}"
+
     for p, a in enumerate(planes):
         ph, pw = a.shape
         got = fused.plane_np(p)
-        assert np.array_equal(got, ref[p][:ph, :pw]), f"plane {p}: fused vs oracle"
-        assert np.array_equal(got, two.plane_np(p)), f"plane {p}: fused vs two-kernel path"
+        r = ref[p][:ph, :pw]
+        assert np.array_equal(two.plane_np(p), r), f"plane {p}: two-kernel path vs oracle: {where(two.plane_np(p), r)}"
+        assert np.array_equal(got, r), f"plane {p}: fused vs oracle: {where(got, r)}"
         assert np.array_equal(d.plane_np(p), a), "the deblocked picture must stay untouched"
 
 
