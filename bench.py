@@ -49,6 +49,7 @@ class Pipeline:
         w, h, bpc, lay = fr["w"], fr["h"], fr["bpc"], fr["layout"]
         self.A = F.Frame(w, h, bpc, lay)      # prediction -> reconstruction
         self.D = F.Frame(w, h, bpc, lay)      # deblocked (out of place: one fused tile launch)
+        self.B = F.Frame(w, h, bpc, lay)      # CDEF output
         self.O = F.Frame(w, h, bpc, lay)      # LR output (the reference frame)
         self.G = F.Frame(w, h, bpc, lay) if fr["fg"] else None   # displayed picture with film grain
         for p, a in enumerate(fr["planes"]):
@@ -88,17 +89,16 @@ class Pipeline:
             # copy, read once and not zeroed (MI_ITX_KEEP_COEFS, as the frame executor runs it)
             "itx": itx_algorithmic_bytes(fr["blocks"], bpc, zero_coefs=False),
             "deblock": 2 * fb + lvl_bytes + mask_bytes,
-            # CDEF + loop restoration in one pass (mi_cdef_lr_frame, as the frame executor runs
-            # them): D read once (its rows across stripe edges included), O written once
-            "cdef_lr": 2 * fb + mask_bytes + fr["lr"]["lr_mask"].nbytes,
+            "cdef": 2 * fb + mask_bytes,
+            "lr": 2 * fb + fb * 4 // 64 + fr["lr"]["lr_mask"].nbytes,
             "fg": 2 * fb,
         }
         if self.mc is not None:
             self.algo["mc"] = mc_algorithmic_bytes(fr["mc"][0], bpc) + fr["mc"][2].nbytes
         # kernel launches per stage per frame: mc = luma + chroma group
-        self.launches = {"mc": 2, "itx": 1, "deblock": 1, "cdef_lr": 1, "fg": 1}
+        self.launches = {"mc": 2, "itx": 1, "deblock": 1, "cdef": 1, "lr": 1, "fg": 1}
         self.kernels = {"mc": "mc_kernel", "itx": "itx_frame_kernel", "deblock": "lf_tile_kernel",
-                        "cdef_lr": "cdef_lr_kernel", "fg": "fg_apply_kernel"}
+                        "cdef": "cdef_kernel", "lr": "lr_kernel", "fg": "fg_apply_kernel"}
 
     def step(self, stream, ev=None, mark=None):
         """Enqueue one frame. ev: optional dict stage -> list of (start, end) events; mark:
@@ -106,7 +106,7 @@ class Pipeline:
         lib = F.lib()
         ctx = self.ctx.h
         sp = F._stream_ptr(stream)
-        pa, po, pd = self.A.picture(), self.O.picture(), self.D.picture()
+        pa, pb, po, pd = self.A.picture(), self.B.picture(), self.O.picture(), self.D.picture()
 
         prep_done = None
         if self.fgd is not None:
@@ -141,9 +141,10 @@ class Pipeline:
                                                              self.itx_bands, ctypes.c_void_p(coef.data_ptr()), ITX_KEEP_COEFS, sp), "itx"))
         timed("deblock", lambda: F.check(lib.mi_deblock_frame_to(ctx, ctypes.byref(pa), ctypes.byref(pd),
                                                                  ctypes.byref(self.lf.s), sp), "lf"))
-        timed("cdef_lr", lambda: F.check(lib.mi_cdef_lr_frame(ctx, ctypes.byref(pd), ctypes.byref(po),
-                                                              ctypes.byref(self.cdef.s), ctypes.byref(self.lr.s), sp),
-                                         "cdef_lr"))
+        timed("cdef", lambda: F.check(lib.mi_cdef_frame(ctx, ctypes.byref(pd), ctypes.byref(pb),
+                                                        ctypes.byref(self.cdef.s), sp), "cdef"))
+        timed("lr", lambda: F.check(lib.mi_lr_frame(ctx, ctypes.byref(pb), ctypes.byref(pd), ctypes.byref(po),
+                                                    ctypes.byref(self.lr.s), sp), "lr"))
         if self.fgd is not None:
             pg = self.G.picture()
             stream.wait_event(prep_done)

@@ -443,14 +443,6 @@ int mi_cdef_frame(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const 
 int mi_lr_frame(MiCtx *ctx, const MiPicture *cdef, const MiPicture *deblocked,
                 const MiPicture *dst, const MiLr *lr, void *stream);
 
-/* CDEF then loop restoration in one pass (the reference's back-to-back rav1d_cdef_brow and
- * rav1d_lr_sbrow per superblock row, src/recon.rs:4172-4283): reads the deblocked picture,
- * writes the restored one; the CDEF output is never stored. Same result as mi_cdef_frame into
- * a picture C, then mi_lr_frame(C, deblocked, dst). No super-resolution (CDEF and loop
- * restoration then see different widths): use the two calls. */
-int mi_cdef_lr_frame(MiCtx *ctx, const MiPicture *deblocked, const MiPicture *dst, const MiCdef *cdef,
-                     const MiLr *lr, void *stream);
-
 /* Film grain (output only; reference frames stay grain-free): out = in + grain. Replaces
  * rav1d_apply_grain (src/fg_apply.rs:272-284 = prep_grain + apply_grain_row per 32 rows).
  * mtrx_identity: seq_hdr.mtrx == DAV1D_MC_IDENTITY (restricted-range chroma clip).

@@ -192,8 +192,6 @@ def lib():
                                             ctypes.POINTER(MiCdef), _VP])
     _sig(L, "mi_lr_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
                                           ctypes.POINTER(MiPicture), ctypes.POINTER(MiLr), _VP])
-    _sig(L, "mi_cdef_lr_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
-                                               ctypes.POINTER(MiCdef), ctypes.POINTER(MiLr), _VP])
     for n in ("mi_film_grain_frame", "mi_film_grain_apply"):
         _sig(L, n, ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
                                   ctypes.POINTER(MiFilmGrainData), ctypes.c_int, _VP])
@@ -216,7 +214,7 @@ def lib():
 # Every symbol include/mi_av1dsp.h declares (checked by tests/test_abi.py).
 EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
             "mi_itx_frame", "mi_itx_frame_banded", "mi_mc_frame", "mi_mc_frame_ex", "mi_mc_scaled", "mi_mc_warp", "mi_mc_combine", "mi_superres_frame",
-            "mi_ipred_blocks", "mi_intra_blocks", "mi_intra_recon", "mi_ctx_device_status", "mi_deblock_frame", "mi_deblock_frame_to", "mi_cdef_frame", "mi_lr_frame", "mi_cdef_lr_frame",
+            "mi_ipred_blocks", "mi_intra_blocks", "mi_intra_recon", "mi_ctx_device_status", "mi_deblock_frame", "mi_deblock_frame_to", "mi_cdef_frame", "mi_lr_frame",
             "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply", "mi_frame_run", "mi_frame_end", "mi_frame_validate", "mi_frame_plan_ms",
             "mi_ctx_set_timing", "mi_ctx_timing",
             "mi_dsp_itxfm_add", "mi_dsp_intra_pred", "mi_dsp_cfl_pred", "mi_dsp_pal_pred", "mi_dsp_cfl_ac",

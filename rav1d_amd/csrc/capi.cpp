@@ -583,58 +583,6 @@ int mi_lr_frame(MiCtx *ctx, const MiPicture *cdef, const MiPicture *deblocked, c
     return r ? fail(ctx, -EIO) : 0;
 }
 
-int mi_cdef_lr_frame(MiCtx *ctx, const MiPicture *deblocked, const MiPicture *dst, const MiCdef *cd,
-                     const MiLr *lr, void *stream) {
-    if (!ctx || !deblocked || !dst || !cd || !cd->masks || !lr) return fail(ctx, -EINVAL);
-    if (!same_geometry(deblocked, dst)) return fail(ctx, -EINVAL);
-    const MiPicture *d = deblocked;
-    if (d->bpc != 8 && d->bpc != 10 && d->bpc != 12) return fail(ctx, -EINVAL);
-    if (cd->sb128w != (d->w + 127) >> 7) return fail(ctx, -EINVAL);
-    if (lr->restore_planes && (!lr->lr_mask || lr->sb128w != (d->w + 127) >> 7)) return fail(ctx, -EINVAL);
-    for (int c = 0; c < 2; c++) {
-        const int l2 = lr->unit_size_log2[c];
-        if ((lr->restore_planes & (c ? 6 : 1)) && (l2 < 5 || l2 > 8)) return fail(ctx, -EINVAL);
-    }
-    // (the luma unit is at least 64 px, a chroma unit at least the chroma tile's width: a tile
-    // never straddles two units)
-    if ((lr->restore_planes & 1) && lr->unit_size_log2[0] < 6) return fail(ctx, -EINVAL);
-    if ((lr->restore_planes & 6) && lr->unit_size_log2[1] < (d->layout == 1 || d->layout == 2 ? 5 : 6))
-        return fail(ctx, -EINVAL);
-    mi::CdefLrArgs a;
-    memset(&a, 0, sizeof(a));
-    const int ss_hor = d->layout == 1 || d->layout == 2, ss_ver = d->layout == 1;
-    const int nplanes = d->layout ? 3 : 1;
-    for (int p = 0; p < nplanes; p++) {
-        a.src[p] = (const uint8_t *)d->data[p];
-        a.dst[p] = (uint8_t *)dst->data[p];
-        a.stride[p] = d->stride[p ? 1 : 0];
-        const int sh = p ? ss_hor : 0, sv = p ? ss_ver : 0;
-        a.pw[p] = (d->w + sh) >> sh;
-        a.ph[p] = (d->h + sv) >> sv;
-        // lr.hip forms row offsets with one 24-bit multiply
-        if (a.stride[p] <= 0 || a.stride[p] >= (1 << 24) || (int64_t)a.ph[p] * a.stride[p] >= (1LL << 32))
-            return fail(ctx, -EINVAL);
-    }
-    a.masks = cd->masks;
-    a.lr_mask = lr->lr_mask;
-    a.sb128w = cd->sb128w;
-    a.lr_sb128w = lr->sb128w;
-    a.bw4 = ((d->w + 7) >> 3) << 1;
-    a.bh4 = ((d->h + 7) >> 3) << 1;
-    a.bdm8 = d->bpc - 8;
-    a.damping = cd->damping + a.bdm8;
-    a.restore = lr->restore_planes;
-    a.unit_log2[0] = lr->unit_size_log2[0];
-    a.unit_log2[1] = lr->unit_size_log2[1];
-    memcpy(a.y_strength, cd->y_strength, 8);
-    memcpy(a.uv_strength, cd->uv_strength, 8);
-    a.tiles_x = (a.pw[0] + 63) / 64;
-    // stripes: 64 luma rows, the first 56 (lr_apply.rs:54)
-    while ((a.stripes ? 64 * a.stripes - 8 : 0) < a.ph[0]) a.stripes++;
-    const int r = mi::launch_cdef_lr(a, d->layout, d->bpc, (hipStream_t)stream);
-    return r ? fail(ctx, -EIO) : 0;
-}
-
 static int fg_tables() {
     static std::once_flag once;
     static int tables_rc = 0;

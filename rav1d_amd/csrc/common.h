@@ -308,24 +308,6 @@ struct LrArgs {
 // launchers (lr.hip)
 int launch_lr(const LrArgs &a, int bpc, hipStream_t s);
 
-// fused CDEF + loop restoration (lr.hip): deblocked D -> restored O, one workgroup per
-// (stripe, 64 luma columns), every plane
-struct CdefLrArgs {
-    const uint8_t *src[3];        // deblocked D
-    uint8_t *dst[3];              // restored O
-    int64_t stride[3];
-    const MiAv1Filter *masks;     // cdef_idx, noskip_mask
-    const MiAv1Restoration *lr_mask;
-    int sb128w, lr_sb128w;
-    int bw4, bh4;                 // CDEF frame size in 4-px units, 8-px aligned
-    int pw[3], ph[3];             // plane sizes (loop restoration)
-    int bdm8, damping;            // damping includes bitdepth_min_8
-    int restore, unit_log2[2];
-    int tiles_x, stripes;         // 64-px luma columns, luma stripes
-    uint8_t y_strength[8], uv_strength[8];
-};
-int launch_cdef_lr(const CdefLrArgs &a, int layout, int bpc, hipStream_t s);
-
 // Wiener taps (centre +128 folded for every bit depth) or self-guided strengths / weights
 struct LrTileParams {
     bool wiener;

@@ -801,31 +801,6 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
     }
     const MiPicture *deblocked = cur;
     int dbl_idx = idx;
-    // 3+4. CDEF and loop restoration in one pass (recon.rs:4172-4283 runs them back to back on
-    // each superblock row), deblocked -> restored: without super-resolution, whose upscale sits
-    // between the two
-    const bool lr_units_ok = (!(f->restore_planes & 1) || f->lr_unit_size[0] >= 6) &&
-                             (!(f->restore_planes & 6) || f->lr_unit_size[1] >= (f->layout == 1 || f->layout == 2 ? 5 : 6));
-    if (f->cdef_on && f->restore_planes && f->up_w == f->w && lr_units_ok) {
-        MiCdef cd;
-        memset(&cd, 0, sizeof(cd));
-        cd.masks = (const MiAv1Filter *)D(8);
-        cd.sb128w = f->sb128w;
-        cd.damping = f->cdef_damping;
-        memcpy(cd.y_strength, f->cdef_y, 8);
-        memcpy(cd.uv_strength, f->cdef_uv, 8);
-        MiLr lr;
-        memset(&lr, 0, sizeof(lr));
-        lr.lr_mask = (const MiAv1Restoration *)D(9);
-        lr.sb128w = f->lr_sb128w;
-        lr.restore_planes = f->restore_planes;
-        lr.unit_size_log2[0] = f->lr_unit_size[0];
-        lr.unit_size_log2[1] = f->lr_unit_size[1];
-        if ((r = mi_cdef_lr_frame(ctx, cur, &cp[3], &cd, &lr, stream))) return r;
-        tev.mark(4, s);
-        *final = 3;
-        return 0;
-    }
     // 3. CDEF (cdef_apply.rs:159-507), deblocked -> cdef
     if (f->cdef_on) {
         MiCdef cd;

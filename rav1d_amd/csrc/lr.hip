@@ -11,7 +11,7 @@
 // window staged once in LDS, both filter passes
 // (or the box sums and the A/B maps of the self-guided filter) computed from LDS, and the
 // output streamed to a separate picture O.
-#include "cdef_dev.h"
+#include "common.h"
 
 MI_KTL_DEFINE(lr)
 
@@ -216,6 +216,7 @@ __device__ __forceinline__ void sgr_pairs(int *A, int16_t *B, const int16_t *win
     if (s0) {
         sgr_ab<2>(win, A, B, sh, tw, (unsigned)s0, bdm8, xbyx);
         __syncthreads();
+        KTL(2);
         if (act) {
             // A/B on odd rows: even j uses rows j-1 and j+1, odd j row j (r0 is even)
             int cau[2], sau[2], cbu[2], sbu[2], cad[2], sad[2], cbd[2], sbd[2];
@@ -247,10 +248,12 @@ __device__ __forceinline__ void sgr_pairs(int *A, int16_t *B, const int16_t *win
             }
         }
         __syncthreads();
+        KTL(3);
     }
     if (s1) {
         sgr_ab<1>(win, A, B, sh, tw, (unsigned)s1, bdm8, xbyx);
         __syncthreads();
+        KTL(4);
         if (act) {
             int c0[2], t0[2], d0[2], u0[2], c1[2], t1[2], d1[2], u1[2], c2[2], t2[2], d2[2], u2[2];
             ld(r0 - 1, c0, t0, d0, u0);
@@ -528,394 +531,6 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(8))) void l
     __syncthreads();
     store_tile<Px>(B, O, st, S, sh, x0, tw);
     KTL(5);
-}
-
-// ---- fused CDEF + loop restoration (cdef_apply.rs:159-507, then lr_apply.rs:28-329 on the same lines) ----
-//
-// The reference runs CDEF and loop restoration back to back on each superblock row
-// (recon.rs:4172-4283). Here one workgroup owns one loop-restoration stripe (64 luma rows, offset
-// 8 up) x 64 luma columns, every plane: it stages the deblocked picture D over the stripe with
-// CDEF's 2-px halo, runs CDEF into LDS (the 64 columns and the 8x8 blocks either side that
-// hold LR's 3-px halo: 10 block columns), takes LR's rows beyond the stripe edges from the same
-// staged D, and runs LR from LDS: the CDEF output C never leaves the CU. The direction of a
-// chroma block is its luma block's, found by the same workgroup.
-constexpr int kFyS = 96;                   // luma D tile row stride: frame columns x0-16 .. x0+79
-constexpr int kFyR = 68;                   // rows S-2 .. S+65
-constexpr int kFR1 = 66 * kLrAB * 6;       // region 1: D tile (T, T1), then A (int) + B (int16)
-static_assert(2 * kFyR * kFyS * 2 <= kFR1, "D tile fits region 1");
-
-// per 8x8 luma block: luma filter flag, direction, adjusted primary and secondary strength;
-// chroma flag, direction, primary and secondary strength (a plane's direction is the searched
-// one when that plane's unadjusted primary strength is nonzero, else 0)
-struct CdefBlk { uint8_t yflag, ydir, ypri, ysec, cflag, cdir, cpri, csec; };
-
-template <typename Px>
-__device__ __forceinline__ void store_cw(const int16_t *cw, uint8_t *O, int64_t st, int S, int sh, int x0, int tw) {
-    // C interior (window rows 3 .., columns kWX ..) -> O, 8-pixel vectors
-    for (int i = threadIdx.x; i < sh * 8; i += kNT) {
-        const int r = i >> 3, c = 8 * (i & 7);
-        if (c >= tw) continue;
-        Px *dp = reinterpret_cast<Px *>(O + row_off(S + r, st)) + x0 + c;
-        const int16_t *sp = cw + (r + 3) * kLrWin + kWX + c;
-        if (c + 8 <= tw) store8<Px>(dp, *reinterpret_cast<const uint4 *>(sp));
-        else for (int j = 0; j < tw - c; j++) dp[j] = (Px)sp[j];
-    }
-}
-
-// LR's window around the CDEF output of one plane (lr_kernel's staging, from LDS): the rows
-// beyond the stripe (D when that side has a neighbouring stripe, else C's edge row), then the
-// columns outside the plane (the edge pixel). T: the staged D, T row 0 = plane row S - 2,
-// T column = window column + tdx.
-__device__ __forceinline__ void lr_window_edges(int16_t *cw, const int16_t *T, int ts, int tdx, int S, int E, int sh,
-                                                int ph, int pw, int x0, bool have_top) {
-    const bool have_bottom = E < ph;
-    for (int i = threadIdx.x; i < 6 * (kLrWin / 2); i += kNT) {
-        const int j = i / (kLrWin / 2), c = 2 * (i - j * (kLrWin / 2));
-        const int rr = j < 3 ? j : sh + j, r = rr - 3;
-        uint32_t v;
-        if (r < 0) {
-            v = have_top ? *reinterpret_cast<const uint32_t *>(T + (r == -1 ? 1 : 0) * ts + c + tdx)
-                         : *reinterpret_cast<const uint32_t *>(cw + 3 * kLrWin + c);
-        } else {
-            v = have_bottom ? *reinterpret_cast<const uint32_t *>(T + (min(E + (r > sh), ph - 1) - (S - 2)) * ts + c + tdx)
-                            : *reinterpret_cast<const uint32_t *>(cw + (sh + 2) * kLrWin + c);
-        }
-        *reinterpret_cast<uint32_t *>(cw + rr * kLrWin + c) = v;
-    }
-    __syncthreads();
-    // window column c is plane column x0 - kWX + c
-    if (x0 - kWX < 0 || x0 - kWX + kLrWin > pw) {
-        for (int i = threadIdx.x; i < (sh + 6) * kLrWin; i += kNT) {
-            const int rr = i / kLrWin, c = i - rr * kLrWin, x = x0 - kWX + c;
-            if (x < 0 || x >= pw) cw[i] = cw[rr * kLrWin + min(max(x, 0), pw - 1) - (x0 - kWX)];
-        }
-    }
-    __syncthreads();
-}
-
-// The restoration unit of (plane p, stripe k, tile column x0) (lr_apply.rs:151-259 indexing)
-__device__ __forceinline__ const MiAv1RestorationUnit *lr_unit(const CdefLrArgs &a, int p, int k, int x0, int ssh,
-                                                               int ssv) {
-    if (!(a.restore & (1 << p))) return nullptr;
-    const int pw = a.pw[p], ph = a.ph[p];
-    const int us = 1 << a.unit_log2[p ? 1 : 0];
-    const int nu = max(1, (pw + (us >> 1)) / us);
-    const int uc = min(x0 / us, nu - 1);
-    const int xu = uc * us;
-    int ay = ((64 * k) >> ssv) & ~(us - 1);
-    if (ay && ay + (us >> 1) > ph) ay -= us;
-    ay <<= ssv;
-    const int sbi = (ay >> 7) * a.lr_sb128w + (xu >> (7 - ssh));
-    const int ui = (((ay >> 6) & 1) << 1) + ((xu >> (6 - ssh)) & 1);
-    const MiAv1RestorationUnit *u = &a.lr_mask[sbi].lr[p][ui];
-    return u->type ? u : nullptr;
-}
-
-// Loop restoration of one plane's tile from the finished window cw into O (lr_kernel's filter
-// part); without a unit O = C.
-template <typename Px>
-__device__ __forceinline__ void lr_from_window(const CdefLrArgs &a, const MiAv1RestorationUnit *u, int16_t *cw,
-                                               int *A, int16_t *B, const uint8_t *xbyx, uint8_t *O, int64_t st,
-                                               int S, int sh, int x0, int tw) {
-    const int bd = a.bdm8 + 8, bdmax = (1 << bd) - 1;
-    if (!u) {
-        store_cw<Px>(cw, O, st, S, sh, x0, tw);
-        return;
-    }
-    if (u->type == 2) {
-        int fh[7], fv[7];
-        fh[0] = fh[6] = u->filter_h[0]; fh[1] = fh[5] = u->filter_h[1]; fh[2] = fh[4] = u->filter_h[2];
-        fh[3] = 128 - 2 * (fh[0] + fh[1] + fh[2]);
-        fv[0] = fv[6] = u->filter_v[0]; fv[1] = fv[5] = u->filter_v[1]; fv[2] = fv[4] = u->filter_v[2];
-        fv[3] = 128 - 2 * (fv[0] + fv[1] + fv[2]);
-        const int rbh = bd == 12 ? 5 : 3, rbv = bd == 12 ? 9 : 11;
-        const int clip_h = (1 << (bd + 1 + 7 - rbh)) - 1;
-        int16_t *hor = reinterpret_cast<int16_t *>(A);
-        wiener_hor(cw, hor, sh + 6, tw, fh, bd, rbh, clip_h);
-        __syncthreads();
-        wiener_ver(hor, B, sh + 6, sh, tw, fv, bd, rbv, bdmax);
-    } else {
-        const int sidx = u->type - 3;
-        const int s0 = k_sgr_params[sidx][0], s1 = k_sgr_params[sidx][1];
-        const int w0 = u->sgr_weights[0];
-        const int w1 = 128 - (u->sgr_weights[0] + u->sgr_weights[1]);
-        sgr_pairs(A, B, cw, sh, tw, a.bdm8, s0, s1, w0, w1, xbyx, bdmax);
-    }
-    __syncthreads();
-    store_tile<Px>(B, O, st, S, sh, x0, tw);
-}
-
-__device__ __forceinline__ unsigned dir_cost_w(int w, const int16_t *t, int ts, int bdm8) {
-    switch (w) {
-    case 0: return dir_cost1<0>(t, ts, bdm8);
-    case 1: return dir_cost1<1>(t, ts, bdm8);
-    case 2: return dir_cost1<2>(t, ts, bdm8);
-    case 3: return dir_cost1<3>(t, ts, bdm8);
-    case 4: return dir_cost1<4>(t, ts, bdm8);
-    case 5: return dir_cost1<5>(t, ts, bdm8);
-    case 6: return dir_cost1<6>(t, ts, bdm8);
-    default: return dir_cost1<7>(t, ts, bdm8);
-    }
-}
-
-// CDEF of one chroma plane's 10 x 8 blocks into the window (pairs of the rows < shc)
-template <int BW, int BH, int CTS, int T1OFF, int TX0, int CWX>
-__device__ __forceinline__ void cdef_chroma_window(const int16_t *T, const CdefBlk *bst, const int4 (*taps)[3],
-                                                   int16_t *cw, int shc, int damping, int bdm8, bool remap422) {
-    constexpr int PPB = BW / 2, PW = 10 * PPB;    // pairs per block row, per window row
-    for (int i = threadIdx.x; i < shc * PW; i += kNT) {
-        const int r = i / PW, pc = i - r * PW;
-        const int bc = pc / PPB, px = 2 * (pc - bc * PPB);
-        const CdefBlk st = bst[(r / BH) * 10 + bc];
-        const char *P = reinterpret_cast<const char *>(T + (r + 2) * CTS + TX0 + BW * bc + px);
-        s16x2 v;
-        if (st.cflag) {
-            int dir = st.cdir;
-            if (remap422 && st.cpri) dir = nib(0x66654207u, dir) + 2;   // {7,0,2,4,5,6,6,6}
-            PairTaps t;
-            const int4 q0 = taps[dir][0], q1 = taps[dir][1], q2 = taps[dir][2];
-            t.pri[0] = q0.x; t.pri[1] = q0.y; t.pri[2] = q0.z; t.pri[3] = q0.w;
-            t.sec[0] = q1.x; t.sec[1] = q1.y; t.sec[2] = q1.z; t.sec[3] = q1.w;
-            t.sec[4] = q2.x; t.sec[5] = q2.y; t.sec[6] = q2.z; t.sec[7] = q2.w;
-            v = cdef_pair(P, t, st.cpri, st.csec, damping, bdm8);
-        } else {
-            v = ld2(P);
-        }
-        *reinterpret_cast<s16x2 *>(cw + (r + 3) * kLrWin + CWX + BW * bc + px) = v;
-    }
-}
-
-template <typename Px, int L>
-__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(6))) void cdef_lr_kernel(CdefLrArgs a) {
-    constexpr int SSH = L == 1 || L == 2, SSV = L == 1;
-    // chroma geometry: blocks BW x BH, D tile rows CR (S-2 ..) and stride CTS (columns from
-    // cx0 - 8 at 4:2:x, cx0 - 16 at 4:4:4), block column bc at tile column CTX0 + BW bc and
-    // window column CWX + BW bc
-    constexpr int BW = 8 >> SSH, BH = 8 >> SSV, CR = (64 >> SSV) + 4, CTS = SSH ? 48 : kFyS;
-    constexpr int CTX0 = SSH ? 4 : 8, CWX = SSH ? 4 : 0, CTDX = SSH ? 0 : 8;
-    __shared__ __align__(16) char r1[kFR1];
-    __shared__ __align__(16) int16_t cw[70 * kLrWin];
-    __shared__ unsigned dcost[8][80];
-    __shared__ CdefBlk bst[80];
-    __shared__ int4 ytaps[8][3], ctaps[8][3];
-    __shared__ uint8_t xbyx[256];
-    int16_t *T = reinterpret_cast<int16_t *>(r1);
-    int *A = reinterpret_cast<int *>(r1);
-    int16_t *B = reinterpret_cast<int16_t *>(r1 + 66 * kLrAB * 4);
-    KTL(0);
-
-    const int bid = xcd_block(blockIdx.x, gridDim.x);
-    const int k = bid / a.tiles_x, ti = bid - k * a.tiles_x;
-    const int x0 = ti * 64;
-    const int S = stripe_start(k, 0), E = min(stripe_start(k + 1, 0), a.ph[0]), sh = E - S;
-    const int fw = a.bw4 * 4, fh = a.bh4 * 4;
-    const int bdm8 = a.bdm8;
-    // any primary strength among the (up to) 3 x 2 64x64 units under the 10 x 8 blocks: the
-    // direction search is needed
-    bool any_pri = false;
-    for (int uy = S >> 6; uy <= (E - 1) >> 6; uy++)
-        for (int ux = max(x0 - 8, 0) >> 6; ux <= min(x0 + 71, fw - 1) >> 6; ux++) {
-            const int idx = a.masks[(uy >> 1) * a.sb128w + (ux >> 1)].cdef_idx[(uy & 1) * 2 + (ux & 1)];
-            if (idx >= 0 && ((a.y_strength[idx] >> 2) || (L && (a.uv_strength[idx] >> 2)))) any_pri = true;
-        }
-
-    // ---- stage luma D (and at 4:2:0 both chroma tiles, kept in registers until their phase) ----
-    {
-        VecTileLoad<Px, kFyR, 84, kNT> ly;
-        ly.fetch(a.src[0], a.stride[0], x0 - 8, S, fw, fh);
-        ly.store(T, T + kFyR * kFyS, kFyS);
-    }
-    VecTileLoad<Px, CR, 40, 256> lc;
-    if constexpr (L == 1) {
-        const int p = 1 + (threadIdx.x >> 8);
-        lc.fetch_lane(threadIdx.x & 255, a.src[p], a.stride[p], (x0 >> 1), stripe_start(k, 1), fw >> 1, fh >> 1);
-    }
-    if (threadIdx.x < 8) {
-        PairTaps t;
-        make_taps<kFyS, kFyR * kFyS * 2>(t, threadIdx.x);
-        ytaps[threadIdx.x][0] = make_int4(t.pri[0], t.pri[1], t.pri[2], t.pri[3]);
-        ytaps[threadIdx.x][1] = make_int4(t.sec[0], t.sec[1], t.sec[2], t.sec[3]);
-        ytaps[threadIdx.x][2] = make_int4(t.sec[4], t.sec[5], t.sec[6], t.sec[7]);
-    } else if (L && threadIdx.x < 16) {
-        PairTaps t;
-        make_taps<CTS, CR * CTS * 2>(t, threadIdx.x - 8);
-        ctaps[threadIdx.x - 8][0] = make_int4(t.pri[0], t.pri[1], t.pri[2], t.pri[3]);
-        ctaps[threadIdx.x - 8][1] = make_int4(t.sec[0], t.sec[1], t.sec[2], t.sec[3]);
-        ctaps[threadIdx.x - 8][2] = make_int4(t.sec[4], t.sec[5], t.sec[6], t.sec[7]);
-    } else if (threadIdx.x >= 256) {
-        xbyx[threadIdx.x - 256] = (uint8_t)sgr_x_by_x(threadIdx.x - 256);
-    }
-    __syncthreads();
-    KTL(1);
-
-    // ---- direction search (cdef.rs:921-1031): wave w = direction w; lane = one of the 64
-    // interior blocks, then 16 lanes for the blocks either side ----
-    if (any_pri) {
-        const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-        {
-            const int br = l >> 3, bc = 1 + (l & 7);
-            dcost[w][br * 10 + bc] = dir_cost_w(w, T + (8 * br + 2) * kFyS + 8 + 8 * bc, kFyS, bdm8);
-        }
-        if (l < 16) {
-            const int br = l >> 1, bc = (l & 1) ? 9 : 0;
-            dcost[w][br * 10 + bc] = dir_cost_w(w, T + (8 * br + 2) * kFyS + 8 + 8 * bc, kFyS, bdm8);
-        }
-    }
-    __syncthreads();
-    KTL(2);
-
-    // ---- per-block strengths, skip flags and direction (cdef_apply.rs:159-507) ----
-    if (threadIdx.x < 80) {
-        const int b = threadIdx.x, br = b / 10, bc = b - br * 10;
-        const int gx = x0 - 8 + 8 * bc, gy = S + 8 * br;
-        CdefBlk st = {};
-        if (gx >= 0 && gx < fw && gy < fh && gy < E) {
-            const int ux = gx >> 6, uy = gy >> 6;
-            const MiAv1Filter *lf = &a.masks[(uy >> 1) * a.sb128w + (ux >> 1)];
-            const int idx = lf->cdef_idx[(uy & 1) * 2 + (ux & 1)];
-            const int ylvl = idx >= 0 ? a.y_strength[idx] : 0, uvlvl = idx >= 0 && L ? a.uv_strength[idx] : 0;
-            const int bx = gx >> 2, by = gy >> 2, by_idx = (by & 30) >> 1;
-            const unsigned noskip = (unsigned)lf->noskip_mask[by_idx][1] << 16 | lf->noskip_mask[by_idx][0];
-            if ((ylvl || uvlvl) && (noskip & (3u << (bx & 30)))) {
-                const int y_pri = (ylvl >> 2) << bdm8, uv_pri = (uvlvl >> 2) << bdm8;
-                int y_sec = ylvl & 3; y_sec += y_sec == 3; y_sec <<= bdm8;
-                int uv_sec = uvlvl & 3; uv_sec += uv_sec == 3; uv_sec <<= bdm8;
-                int dir = 0;
-                unsigned var = 0;
-                if (y_pri || uv_pri) {
-                    unsigned bc_ = dcost[0][b];
-#pragma unroll
-                    for (int n = 1; n < 8; n++)
-                        if (dcost[n][b] > bc_) { bc_ = dcost[n][b]; dir = n; }
-                    var = (bc_ - dcost[dir ^ 4][b]) >> 10;
-                }
-                int pri = 0;
-                if (y_pri) {
-                    pri = adjust_strength(y_pri, var);
-                    st.yflag = pri || y_sec;
-                } else {
-                    st.yflag = y_sec != 0;
-                }
-                st.ydir = (uint8_t)(y_pri ? dir : 0);
-                st.ypri = (uint8_t)pri;
-                st.ysec = (uint8_t)y_sec;
-                st.cflag = uvlvl != 0;
-                st.cdir = (uint8_t)(uv_pri ? dir : 0);
-                st.cpri = (uint8_t)uv_pri;
-                st.csec = (uint8_t)uv_sec;
-            }
-        }
-        bst[b] = st;
-    }
-    __syncthreads();
-    KTL(3);
-
-    // ---- luma CDEF into the window: 32-lane groups over the 64 interior blocks (filter_luma's
-    // mapping), then 256 lanes for the 2 pairs of each halo block next to the tile ----
-    {
-        const int g = threadIdx.x >> 5, l = threadIdx.x & 31;
-        const int br = g >> 1, r = br * 8 + (l >> 2), c0 = 1 + (g & 1) * 4;
-        const char *prow = reinterpret_cast<const char *>(T + (r + 2) * kFyS + 8 + 2 * (l & 3));
-        int16_t *crow = cw + (r + 3) * kLrWin + 2 * (l & 3);
-        if (r < sh) {
-#pragma unroll
-            for (int i = c0; i < c0 + 4; i++) {
-                const CdefBlk st = bst[br * 10 + i];
-                const char *P = prow + 16 * i;
-                s16x2 v;
-                if (st.yflag) {
-                    const int dir = st.ydir;
-                    PairTaps t;
-                    const int4 q0 = ytaps[dir][0], q1 = ytaps[dir][1], q2 = ytaps[dir][2];
-                    t.pri[0] = q0.x; t.pri[1] = q0.y; t.pri[2] = q0.z; t.pri[3] = q0.w;
-                    t.sec[0] = q1.x; t.sec[1] = q1.y; t.sec[2] = q1.z; t.sec[3] = q1.w;
-                    t.sec[4] = q2.x; t.sec[5] = q2.y; t.sec[6] = q2.z; t.sec[7] = q2.w;
-                    v = cdef_pair(P, t, st.ypri, st.ysec, a.damping, bdm8);
-                } else {
-                    v = ld2(P);
-                }
-                *reinterpret_cast<s16x2 *>(crow + 8 * i) = v;
-            }
-        }
-        if (threadIdx.x < 256) {
-            const int hb = threadIdx.x >> 4, side = hb & 1, hbr = hb >> 1;
-            const int rr = hbr * 8 + ((threadIdx.x >> 1) & 7), bc = side ? 9 : 0;
-            const int px = 2 * (side ? (threadIdx.x & 1) : 2 + (threadIdx.x & 1));
-            if (rr < sh) {
-                const CdefBlk st = bst[hbr * 10 + bc];
-                const char *P = reinterpret_cast<const char *>(T + (rr + 2) * kFyS + 8 + 8 * bc + px);
-                s16x2 v;
-                if (st.yflag) {
-                    const int dir = st.ydir;
-                    PairTaps t;
-                    const int4 q0 = ytaps[dir][0], q1 = ytaps[dir][1], q2 = ytaps[dir][2];
-                    t.pri[0] = q0.x; t.pri[1] = q0.y; t.pri[2] = q0.z; t.pri[3] = q0.w;
-                    t.sec[0] = q1.x; t.sec[1] = q1.y; t.sec[2] = q1.z; t.sec[3] = q1.w;
-                    t.sec[4] = q2.x; t.sec[5] = q2.y; t.sec[6] = q2.z; t.sec[7] = q2.w;
-                    v = cdef_pair(P, t, st.ypri, st.ysec, a.damping, bdm8);
-                } else {
-                    v = ld2(P);
-                }
-                *reinterpret_cast<s16x2 *>(cw + (rr + 3) * kLrWin + 8 * bc + px) = v;
-            }
-        }
-    }
-    __syncthreads();
-    KTL(4);
-
-    // ---- luma loop restoration from the window ----
-    lr_window_edges(cw, T, kFyS, 8, S, E, sh, a.ph[0], a.pw[0], x0, k > 0);
-    lr_from_window<Px>(a, lr_unit(a, 0, k, x0, 0, 0), cw, A, B, xbyx, a.dst[0], a.stride[0], S, sh, x0,
-                       min(64, a.pw[0] - x0));
-    KTL(6);
-
-    // ---- chroma planes: D tile (region 1), CDEF into the window, loop restoration ----
-    if constexpr (L != 0) {
-        const int cx0 = x0 >> SSH, Sc = stripe_start(k, SSV);
-        // (the plane index a compile-time constant: indexing the argument arrays by a runtime
-        // plane copies the whole argument block to scratch)
-        auto plane = [&](auto pc) {
-            constexpr int p = decltype(pc)::value;
-            const int Ec = min(stripe_start(k + 1, SSV), a.ph[p]), shc = Ec - Sc;
-            if (shc <= 0 || cx0 >= a.pw[p]) return;
-            __syncthreads();   // region 1 and the window are free (previous plane's LR stored)
-            if constexpr (L == 1) {
-                lc.store_lane((threadIdx.x >> 8) + 1 == p ? (int)(threadIdx.x & 255) : -1, T, T + CR * CTS, CTS);
-            } else {
-                VecTileLoad<Px, CR, SSH ? 40 : 84, kNT> l2;
-                l2.fetch(a.src[p], a.stride[p], SSH ? cx0 : cx0 - 8, Sc, fw >> SSH, fh >> SSV);
-                l2.store(T, T + CR * CTS, CTS);
-            }
-            __syncthreads();
-            cdef_chroma_window<BW, BH, CTS, CR * CTS * 2, CTX0, CWX>(T, bst, ctaps, cw, shc, a.damping - 1, bdm8,
-                                                                    L == 2);
-            __syncthreads();
-            lr_window_edges(cw, T, CTS, CTDX, Sc, Ec, shc, a.ph[p], a.pw[p], cx0, k > 0);
-            lr_from_window<Px>(a, lr_unit(a, p, k, cx0, SSH, SSV), cw, A, B, xbyx, a.dst[p], a.stride[p], Sc, shc,
-                               cx0, min(64 >> SSH, a.pw[p] - cx0));
-        };
-        plane(std::integral_constant<int, 1>());
-        plane(std::integral_constant<int, 2>());
-    }
-    KTL(5);
-}
-
-int launch_cdef_lr(const CdefLrArgs &a, int layout, int bpc, hipStream_t s) {
-    const int n = a.tiles_x * a.stripes;
-    if (n <= 0) return 0;
-#define MI_CDEF_LR_LAUNCH(L)                                                                         \
-    do {                                                                                             \
-        if (bpc == 8) cdef_lr_kernel<uint8_t, L><<<n, kNT, 0, s>>>(a);                                \
-        else cdef_lr_kernel<uint16_t, L><<<n, kNT, 0, s>>>(a);                                        \
-    } while (0)
-    switch (layout) {
-    case 0: MI_CDEF_LR_LAUNCH(0); break;
-    case 1: MI_CDEF_LR_LAUNCH(1); break;
-    case 2: MI_CDEF_LR_LAUNCH(2); break;
-    default: MI_CDEF_LR_LAUNCH(3); break;
-    }
-#undef MI_CDEF_LR_LAUNCH
-    return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 // ---- per-call lr.wiener / lr.sgr (looprestoration.rs:91-107, 139-912) ----

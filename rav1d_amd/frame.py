@@ -303,13 +303,6 @@ def lr_frame(ctx, cdef, deblocked, dst, meta, stream=None):
                             ctypes.byref(meta.s), _stream_ptr(stream)), "mi_lr_frame")
 
 
-def cdef_lr_frame(ctx, deblocked, dst, cdef_meta, lr_meta, stream=None):
-    """CDEF then loop restoration in one pass (mi_cdef_lr_frame): deblocked -> dst."""
-    pd, po = deblocked.picture(), dst.picture()
-    check(lib().mi_cdef_lr_frame(ctx.h, ctypes.byref(pd), ctypes.byref(po), ctypes.byref(cdef_meta.s),
-                                 ctypes.byref(lr_meta.s), _stream_ptr(stream)), "mi_cdef_lr_frame")
-
-
 def film_grain_data(fg):
     """dict (rav1d_amd.synth.make_fg_params) -> MiFilmGrainData (a MiFilmGrainData is returned as is)"""
     if isinstance(fg, MiFilmGrainData):

@@ -107,7 +107,7 @@ class _OraclePipeline:
         import bench
         self.fr, self.digest = fr, None
         fb = 2 * fr["w"] * fr["h"] * 3 // 2
-        self.algo = {k: 2 * fb for k in ("mc", "itx", "deblock", "cdef_lr")}
+        self.algo = {k: 2 * fb for k in ("mc", "itx", "deblock", "cdef", "lr")}
         self.launches = {k: 1 for k in self.algo}
         self.kernels = {k: k for k in self.algo}
         self._bench = bench
@@ -116,7 +116,7 @@ class _OraclePipeline:
         a = _Ev()
         self.digest = self._bench.oracle_digest(self.fr)
         if ev is not None:
-            ev.setdefault("cdef_lr", []).append((a, _Ev()))
+            ev.setdefault("lr", []).append((a, _Ev()))
 
     def refill(self):
         pass

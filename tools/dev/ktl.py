@@ -73,12 +73,7 @@ for u in UNITS:
         for c in np.unique(cls):
             m = cls == c
             print(f"   size {int(c):2d}: {m.sum():5d} wg, life mean {life[m].mean():6.1f} max {life[m].max():6.1f}, start {st[m].min():5.1f}-{st[m].max():5.1f}")
-    if u == "lr" and (a[:, 6] >= a[:, 0]).all():
-        # the fused CDEF + LR kernel: slot 4 = luma CDEF done, 6 = luma LR done, 5 = end
-        for x, y, name in ((4, 6, "luma LR"), (6, 5, "chroma CDEF + LR")):
-            d = (a[:, y] - a[:, x]) / 100.0
-            print(f"   {name}: mean {d.mean():.2f} p50 {np.median(d):.2f} p90 {np.percentile(d, 90):.2f} us")
-    elif u == "lr":
+    if u == "lr":
         cls = a[:, 6]
         for c in np.unique(cls):
             m = cls == c

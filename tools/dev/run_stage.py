@@ -1,4 +1,4 @@
-"""One bench stage (STAGE=deblock|cdef|lr|cdef_lr) of the 4K10 bench frame, REPS times, for PMC
+"""One bench stage (STAGE=deblock|cdef|lr|mc|itx) of the 4K10 bench frame, REPS times, for PMC
 passes (diagnostic). The pipeline runs once first so every input is the real one."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -17,8 +17,7 @@ torch.cuda.synchronize()
 L = F.lib()
 st = os.environ.get("STAGE", "deblock")
 sp = F._stream_ptr(s)
-B = F.Frame(3840, 2160, 10, 1)   # CDEF output of the two-kernel path
-pa, pb, po, pd = pipe.A.picture(), B.picture(), pipe.O.picture(), pipe.D.picture()
+pa, pb, po, pd = pipe.A.picture(), pipe.B.picture(), pipe.O.picture(), pipe.D.picture()
 for _ in range(int(os.environ.get("REPS", "10"))):
     if st == "deblock":
         F.check(L.mi_deblock_frame_to(ctx.h, ctypes.byref(pa), ctypes.byref(pd), ctypes.byref(pipe.lf.s), sp), "lf")
@@ -26,8 +25,6 @@ for _ in range(int(os.environ.get("REPS", "10"))):
         F.check(L.mi_cdef_frame(ctx.h, ctypes.byref(pd), ctypes.byref(pb), ctypes.byref(pipe.cdef.s), sp), "cdef")
     elif st == "lr":
         F.check(L.mi_lr_frame(ctx.h, ctypes.byref(pb), ctypes.byref(pd), ctypes.byref(po), ctypes.byref(pipe.lr.s), sp), "lr")
-    elif st == "cdef_lr":
-        F.check(L.mi_cdef_lr_frame(ctx.h, ctypes.byref(pd), ctypes.byref(po), ctypes.byref(pipe.cdef.s), ctypes.byref(pipe.lr.s), sp), "cdef_lr")
 torch.cuda.synchronize()
 print("done")
 if os.environ.get("TIME"):
@@ -42,6 +39,4 @@ if os.environ.get("TIME"):
             F.check(L.mi_cdef_frame(ctx.h, ctypes.byref(pd), ctypes.byref(pb), ctypes.byref(pipe.cdef.s), p), "cdef")
         elif st == "lr":
             F.check(L.mi_lr_frame(ctx.h, ctypes.byref(pb), ctypes.byref(pd), ctypes.byref(po), ctypes.byref(pipe.lr.s), p), "lr")
-        elif st == "cdef_lr":
-            F.check(L.mi_cdef_lr_frame(ctx.h, ctypes.byref(pd), ctypes.byref(po), ctypes.byref(pipe.cdef.s), ctypes.byref(pipe.lr.s), p), "cdef_lr")
     print(f"{st} {gtime(one):.2f} us", flush=True)

@@ -22,9 +22,10 @@ STAGES = {
     "mc": (["mc_kernel"], 8, 2),                      # 4-sample (8-B) window quads, per-pixel stores
     "itx": (["itx_frame_kernel"], 8, 8),              # 4-pixel chunks in and out
     "deblock": (["lf_tile_kernel"], 16, 16),           # uint4 tile staging and stores
-    "cdef_lr": (["cdef_lr_kernel"], 16, 16),          # 8-sample vectors in, 8-pixel vectors out
+    "cdef": (["cdef_kernel"], 16, 4),                 # 8-sample vectors in, pixel pairs out
+    "lr": (["lr_kernel"], 16, 16),                    # 8-pixel vectors in and out
 }
-FRAME_KERNEL = "cdef_lr_kernel"                       # one dispatch per frame: counts the frames
+FRAME_KERNEL = "cdef_kernel"                          # one dispatch per frame: counts the frames
 
 
 def calib(root):
