@@ -381,27 +381,16 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
         if (f->dep_start[i + 1] < f->dep_start[i]) return BAD();
         return 0;
     };
-    std::atomic<int> bad{0};
-    parallel_ranges(f->n_intra, 32768, [&](int lo, int hi, int) {
-        for (int i = lo; i < hi && !bad.load(std::memory_order_relaxed); i++)
-            if (check(i)) bad.store(1, std::memory_order_relaxed);
-    });
-    if (bad.load())
-        for (int i = 0; i < f->n_intra; i++)
-            if (int e = check(i)) return e;
-    // the front-end's intra queue (MiDecFrame.q_*): every block as above, dependencies inside
-    // the queue (they may point forward across strips: the kernel waits on them), strips
-    // partitioning it
-    if (f->q_intra) {
-        const int n = f->n_intra;
+    // the front-end's intra queue (MiDecFrame.q_*), when given, is what the kernels read: its
+    // blocks get the per-block checks, and its dependencies must lie inside it and, within a
+    // strip, point to earlier queue entries (the strip's workers take entries in order; a
+    // dependency on another strip is waited for with a bounded wait). The decode-order lists
+    // then keep only their structural checks.
+    const bool q = f->q_intra != nullptr;
+    const int n = f->n_intra;
+    if (q) {
         if (!f->q_intra_tx || !f->q_dep_start || f->q_n_deps < 0 || (f->q_n_deps && !f->q_deps)) return BAD();
         if (f->q_dep_start[0] != 0 || f->q_dep_start[n] != f->q_n_deps) return BAD();
-        for (int i = 0; i < n; i++) {
-            if (int e = check_block(f->q_intra[i], f->q_intra_tx[i])) return e;
-            if (f->q_dep_start[i + 1] < f->q_dep_start[i]) return BAD();
-            for (int d = f->q_dep_start[i]; d < f->q_dep_start[i + 1]; d++)
-                if (f->q_deps[d] < 0 || f->q_deps[d] >= n || f->q_deps[d] == i) return BAD();
-        }
         if (f->q_nstrips > 1) {
             if (!f->q_strip_start || f->q_nstrips > 8 || f->q_strip_start[0] != 0 || f->q_strip_start[f->q_nstrips] != n)
                 return BAD();
@@ -409,6 +398,31 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
                 if (f->q_strip_start[k + 1] < f->q_strip_start[k]) return BAD();
         }
     }
+    const int nss = q && f->q_nstrips > 1 ? f->q_nstrips : 1;
+    auto check_q = [&](int i) -> int {
+        if (int e = check_block(f->q_intra[i], f->q_intra_tx[i])) return e;
+        if (f->q_dep_start[i + 1] < f->q_dep_start[i]) return BAD();
+        int lo = 0, hi = n;   // entry i's strip
+        for (int k = 0; nss > 1 && k < nss; k++)
+            if (i < f->q_strip_start[k + 1]) {
+                lo = f->q_strip_start[k];
+                hi = f->q_strip_start[k + 1];
+                break;
+            }
+        for (int d = f->q_dep_start[i]; d < f->q_dep_start[i + 1]; d++) {
+            const int j = f->q_deps[d];
+            if (j < 0 || j >= n || j == i || (j > i && j >= lo && j < hi)) return BAD();
+        }
+        return 0;
+    };
+    std::atomic<int> bad{0};
+    parallel_ranges(n, 32768, [&](int lo, int hi, int) {
+        for (int i = lo; i < hi && !bad.load(std::memory_order_relaxed); i++)
+            if (q ? check_q(i) : check(i)) bad.store(1, std::memory_order_relaxed);
+    });
+    if (bad.load())
+        for (int i = 0; i < n; i++)
+            if (int e = q ? check_q(i) : check(i)) return e;
     const int sb128w = (f->w + 127) >> 7, sb128h = (f->h + 127) >> 7;
     if (f->filter_y && (!f->lf_level || !f->lf_masks || f->sb128w != sb128w || f->sb128h != sb128h ||
                         f->b4_stride < sb128w * 32))
