@@ -416,6 +416,7 @@ def real_streams(ctx, reps=3, oracle_reps=5, oracle_budget_s=25.0):
                          frame's tiles on 8 threads, no temporal unit ahead),
                          mi_frame_run host time, upload / inter / intra / filter device time
                          (mi_ctx_timing), output copy (events), muxer (host)
+      stages_pipelined_ms the same for one pipelined pass (front-end frame threads running ahead)
       front_end_only_ms  the front-end alone (single thread); front_end_8_threads_ms: 8 threads
       cpu_oracle_ms      front-end + the CPU restatement (oracle/, single thread, no hashing), best
                          of up to `oracle_reps` within `oracle_budget_s` (kind "port": rav1d's own
@@ -450,6 +451,13 @@ def real_streams(ctx, reps=3, oracle_reps=5, oracle_budget_s=25.0):
         st = {}
         mm = Muxer("null")
         decode_to_muxer(ctx, data, mm, apply_grain=grain, pipelined=False, stats=st)
+        mm.close()
+        # the same breakdown of one pipelined pass: the front-end's frame and tile threads run
+        # ahead of the device (frame k+1's entropy decoding while frame k is reconstructed), so
+        # front_end_ms is what the host still waits for events
+        stp = {}
+        mm = Muxer("null")
+        decode_to_muxer(ctx, data, mm, apply_grain=grain, stats=stp)
         mm.close()
         # the front-end alone (one thread, and 8 threads: frame jobs + tile decoders, temporal
         # units ahead as the pipelined decode runs it); shown-picture pixels for the Mpixels/s figures
@@ -487,6 +495,8 @@ def real_streams(ctx, reps=3, oracle_reps=5, oracle_budget_s=25.0):
             stages_ms={k: round(st[k], 3) for k in ("front_end_ms", "run_host_ms", "run_levels_ms", "run_stage_ms",
                                                      "upload_ms", "inter_ms", "intra_ms", "filter_ms", "d2h_ms",
                                                      "mux_ms")},
+            stages_pipelined_ms={k: round(stp[k], 3) for k in ("front_end_ms", "run_host_ms", "upload_ms", "inter_ms",
+                                                                "intra_ms", "filter_ms", "d2h_ms", "mux_ms")},
             upload_mb=round(st["upload_bytes"] / 1e6, 2),
             front_end_only_ms=round(fe * 1e3, 3), front_end_8_threads_ms=round(fe_mt * 1e3, 3),
             cpu_oracle_ms=round(cpu * 1e3, 1), cpu_oracle_reps=creps, cpu_oracle_mpx_per_s=round(px / cpu / 1e6, 2))

@@ -9,7 +9,7 @@ OUT=$R/gpurun_out
 TAG=${1:-r}
 mkdir -p $OUT
 stop() { case $1 in 124|137|134|139|132|135|136) echo "stopping after rc=$1 ($2)"; exit $1;; esac; }
-timeout -k 10 420 python -u -m pytest $R/tests -m gpu -x -q --timeout 150 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1
+timeout -k 10 600 python -u -m pytest $R/tests -m gpu -x -q --timeout 150 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1
 rc=$?; tail -2 $OUT/pytest_gpu_$TAG.log; stop $rc pytest
 timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1
 rc=$?; tail -1 $OUT/smoke_$TAG.log; stop $rc smoke
