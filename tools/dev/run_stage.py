@@ -1,4 +1,4 @@
-"""One bench stage (STAGE=deblock|cdef|lr|mc|itx) of the 4K10 bench frame, REPS times, for PMC
+"""One bench stage (STAGE=deblock|cdef|lr|itx) of the 4K10 bench frame, REPS times, for PMC
 passes (diagnostic). The pipeline runs once first so every input is the real one."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -18,8 +18,15 @@ L = F.lib()
 st = os.environ.get("STAGE", "deblock")
 sp = F._stream_ptr(s)
 pa, pb, po, pd = pipe.A.picture(), pipe.B.picture(), pipe.O.picture(), pipe.D.picture()
+def itx(p):
+    F.check(L.mi_itx_frame_banded(ctx.h, ctypes.byref(pa), ctypes.c_void_p(pipe.blocks.data_ptr()), pipe.itx_bands,
+                                  ctypes.c_void_p(pipe.coefs[0].data_ptr()), bench.ITX_KEEP_COEFS, p), "itx")
+
+
 for _ in range(int(os.environ.get("REPS", "10"))):
-    if st == "deblock":
+    if st == "itx":
+        itx(sp)
+    elif st == "deblock":
         F.check(L.mi_deblock_frame_to(ctx.h, ctypes.byref(pa), ctypes.byref(pd), ctypes.byref(pipe.lf.s), sp), "lf")
     elif st == "cdef":
         F.check(L.mi_cdef_frame(ctx.h, ctypes.byref(pd), ctypes.byref(pb), ctypes.byref(pipe.cdef.s), sp), "cdef")
@@ -33,7 +40,9 @@ if os.environ.get("TIME"):
 
     def one(stream):
         p = F._stream_ptr(stream)
-        if st == "deblock":
+        if st == "itx":
+            itx(p)
+        elif st == "deblock":
             F.check(L.mi_deblock_frame_to(ctx.h, ctypes.byref(pa), ctypes.byref(pd), ctypes.byref(pipe.lf.s), p), "lf")
         elif st == "cdef":
             F.check(L.mi_cdef_frame(ctx.h, ctypes.byref(pd), ctypes.byref(pb), ctypes.byref(pipe.cdef.s), p), "cdef")
