@@ -86,16 +86,6 @@ __device__ __forceinline__ int karg_i32(size_t off) {
 // the compiler copy the whole struct to scratch)
 template <typename T> __device__ __forceinline__ T sel3(const T (&v)[3], int i) { return i == 0 ? v[0] : i == 1 ? v[1] : v[2]; }
 
-// a coefficient: read once per frame, so (MI_ITX_NT builds) as a streaming load that does not
-// displace the picture lines the blocks read and write in L2
-template <typename Cf> __device__ __forceinline__ Cf ldcf(const Cf *p) {
-#ifdef MI_ITX_NT
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
-
 template <int TX, typename Px, typename Cf, typename Lt, bool Wide>
 __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     constexpr TxDim D = tx_dim(TX);
@@ -142,13 +132,7 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
         bool valid = bi < be;
         MiTxBlock b{};
         if (valid) {
-#ifdef MI_ITX_NT
-            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 raw = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.blocks) + bi);
-            b = __builtin_bit_cast(MiTxBlock, raw);
-#else
             b = a.blocks[bi];
-#endif
             // a descriptor the reference could never issue (wrong size group, a type the
             // size's table slot lacks, a rectangle outside its plane) is skipped and reported
             const bool ok = b.tx == TX && b.txtp < 17 && ((itx_legal_types(TX) >> b.txtp) & 1) &&
@@ -166,12 +150,12 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
             if (valid && c < Ht * CPR)
                 pk[rd][c4] = *reinterpret_cast<const V *>(pbase + (int64_t)(c / CPR) * st + (c % CPR) * 4 * sizeof(Px));
         }
-        dk[rd] = valid && b.txtp == 0 && b.eob < 1 ? (int)ldcf(reinterpret_cast<const Cf *>(a.coef) + b.coef_off) : 0;
+        dk[rd] = valid && b.txtp == 0 && b.eob < 1 ? (int)(reinterpret_cast<const Cf *>(a.coef) + b.coef_off)[0] : 0;
         if constexpr (ROUNDS > 1) {
             const Cf *cq = reinterpret_cast<const Cf *>(a.coef) + b.coef_off;
             const bool need = valid && !(b.txtp == 0 && b.eob < 1) && j < SH;
 #pragma unroll
-            for (int x = 0; x < CW; x++) ck[rd][x] = need ? (int)ldcf(cq + j + x * SH) : 0;
+            for (int x = 0; x < CW; x++) ck[rd][x] = need ? (int)cq[j + x * SH] : 0;
         }
         bk[rd] = b;
         vk[rd] = valid;
@@ -212,7 +196,7 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
         for (int x = 0; x < SW; x++) {
             int v;
             if constexpr (ROUNDS > 1) v = ck[rd][x];
-            else v = (int)ldcf(cf + j + x * SH);
+            else v = (int)cf[j + x * SH];
             if constexpr (Rect2) r[x] = (v * 181 + 128) >> 8;
             else r[x] = v;
         }

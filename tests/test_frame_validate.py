@@ -84,6 +84,7 @@ def test_front_end_intra_queue(name):
         assert key(blk) == key(qb)
         ds = np.ctypeslib.as_array((ctypes.c_int32 * (n + 1)).from_address(fr.q_dep_start))
         assert ds[0] == 0 and ds[-1] == fr.q_n_deps and (np.diff(ds) >= 0).all()
+        ss = None
         if fr.q_nstrips > 1:
             ss = np.ctypeslib.as_array((ctypes.c_int32 * (fr.q_nstrips + 1)).from_address(fr.q_strip_start))
             assert ss[0] == 0 and ss[-1] == n and (np.diff(ss) >= 0).all()
@@ -99,6 +100,16 @@ def test_front_end_intra_queue(name):
             c.q_deps = ctypes.addressof(deps)
             rc, why = validate(c, ps)
             assert rc != 0 and why
+            # a dependency on a later entry of the same strip (its workers take entries in order)
+            i = next(i for i in range(n) if ds[i + 1] > ds[i])
+            end = n
+            if fr.q_nstrips > 1:
+                end = next(int(x) for x in ss[1:] if x > i)
+            if i + 1 < end:
+                ctypes.memmove(deps, fr.q_deps, 4 * fr.q_n_deps)
+                deps[ds[i]] = i + 1
+                rc, why = validate(c, ps)
+                assert rc != 0 and why
         checked += 1
     assert checked > 0
 

@@ -109,12 +109,29 @@ def test_frame_run_rejects_malformed_work_lists(gpu):
     k = next(i for i in range(n) if int.from_bytes(bytes(txs[16 * i + 12:16 * i + 16]), "little", signed=True) >= 0)
     t[16 * k:16 * k + 4] = (fr.ncoef + 10).to_bytes(4, "little")
     cases.append(("coef_off", bytes(blocks), t))
-    for what, bb, tt in cases:
+    # the same corruptions in the front-end's queue (the arrays the kernels read when it is given)
+    qb = (ctypes.c_uint8 * (32 * n)).from_address(fr.q_intra)
+    qt = (ctypes.c_uint8 * (16 * n)).from_address(fr.q_intra_tx)
+    b = bytearray(qb)
+    b[0:2] = (4000).to_bytes(2, "little")
+    cases.append(("queue x", b, bytes(qt), "q"))
+    t = bytearray(qt)
+    k = next(i for i in range(n) if int.from_bytes(bytes(qt[16 * i + 12:16 * i + 16]), "little", signed=True) >= 0)
+    t[16 * k:16 * k + 4] = (fr.ncoef + 10).to_bytes(4, "little")
+    cases.append(("queue coef_off", bytes(qb), t, "q"))
+    for what, bb, tt, *kind in cases:
         bad = MiDecFrame.from_buffer_copy(fr)
         bbuf = (ctypes.c_uint8 * len(bb)).from_buffer_copy(bytes(bb))
         tbuf = (ctypes.c_uint8 * len(tt)).from_buffer_copy(bytes(tt))
-        bad.intra = ctypes.addressof(bbuf)
-        bad.intra_tx = ctypes.addressof(tbuf)
+        if kind:
+            bad.q_intra = ctypes.addressof(bbuf)
+            bad.q_intra_tx = ctypes.addressof(tbuf)
+        else:
+            # decode-order lists: without a queue, mi_frame_run plans (and checks) them itself
+            bad.intra = ctypes.addressof(bbuf)
+            bad.intra_tx = ctypes.addressof(tbuf)
+            bad.q_intra = bad.q_intra_tx = bad.q_dep_start = bad.q_deps = bad.q_strip_start = None
+            bad.q_n_deps = bad.q_nstrips = bad.q_granules = 0
         assert isinstance(bad, MiDecFrame)
         assert L.mi_frame_run(gpu.h, ctypes.byref(bad), ctypes.byref(ps.pics), ctypes.byref(final), None) == -22, what
     assert L.mi_frame_end(gpu.h, None) == 0
