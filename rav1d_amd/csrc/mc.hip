@@ -165,6 +165,8 @@ template <typename Px>
 // g: 0 / 1 = the waves of plane group 0 / 1; 2 = both groups in one grid (group 0's waves,
 // then group 1's; mi_mc_frame_ex with MI_MC_ONE_GRID: no chroma unit reads a mask written
 // in the same grid), so the small chroma units fill the luma tail.
+// (forcing 6 or 8 waves per SIMD, with or without 4 window loads in flight per lane instead
+// of 8, spills and measured 73-147 us against 70 us for the two launches: DESIGN.md §5)
 __global__ __launch_bounds__(64, 1) void mc_kernel(McArgs a, int g) {
     __shared__ __attribute__((aligned(16))) int16_t win[kWinElems];
     const int lane = threadIdx.x;
