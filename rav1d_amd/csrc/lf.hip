@@ -596,16 +596,13 @@ __device__ __forceinline__ void lf_dir_pk(Px *t, const uint16_t (*lists)[COLS ? 
     // chunk prefix over the classes (wave-uniform: the counts are LDS broadcasts)
     const int c0 = (cnt[0] * 2 + 63) >> 6, c1 = c0 + ((cnt[1] * 2 + 63) >> 6);
     const int c2 = c1 + ((cnt[2] * 2 + 63) >> 6), c3 = c2 + ((cnt[3] * 2 + 63) >> 6);
-#ifndef MI_LF_SPLIT
-#define MI_LF_SPLIT 0
-#endif
+    // (lanes 2u / 2u + 1 take unit u; mapping lanes 0-31 and 32-63 to the two row pairs of the
+    // same 32 units measured the same: 29.0-29.3 vs 29.0-30.1 us, round 5)
     for (int g = wave; g < c3; g += kLfThreads / 64) {
         const int cls = g < c0 ? 0 : g < c1 ? 1 : g < c2 ? 2 : 3;
         const int base = cls == 0 ? 0 : cls == 1 ? c0 : cls == 2 ? c1 : c2;
-        // MI_LF_SPLIT (column edges): lanes 0-31 take rows 0-1 and lanes 32-63 rows 2-3 of the
-        // same 32 units (one b64 row read per 32-lane group) instead of lanes 2u / 2u + 1
-        const int ui = COLS && MI_LF_SPLIT ? (g - base) * 32 + (lane & 31) : ((g - base) * 64 + lane) >> 1;
-        const int i = COLS && MI_LF_SPLIT ? lane >> 5 : lane;   // (the callees read i & 1)
+        const int ui = ((g - base) * 64 + lane) >> 1;
+        const int i = lane;   // (the callees read i & 1)
         if (ui >= cnt[cls]) continue;
         const int e = lists[cls >> 1][cls & 1 ? N - 1 - ui : ui];
         switch (cls) {
@@ -627,11 +624,9 @@ template <typename Px>
 __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
     constexpr int VB = 16;                        // bytes per vector
     constexpr int VPX = VB / sizeof(Px);          // pixels per vector
-#ifndef MI_LF_PITCH
-#define MI_LF_PITCH kLfCols   // (+8 px of padding cut the LDS bank conflicts 3.15 -> 2.2 M cycles but ran 31 vs 29 us)
-#endif
-    // LDS pitch in pixels (the staged kLfCols)
-    constexpr int P = MI_LF_PITCH;
+    // LDS pitch in pixels: the staged kLfCols (+8 px of padding cut the LDS bank conflicts
+    // 3.15 -> 2.2 M cycles but ran 31 vs 29 us)
+    constexpr int P = kLfCols;
     static_assert(P % 8 == 0 && P >= kLfCols, "16-B aligned rows");
     constexpr int NV = (kLfRows / 4) * kLfEdgesV; // column-edge units (4 lines each)
     constexpr int NH = kLfEdgesH * (kLfTW / 4);   // row-edge units
