@@ -76,8 +76,8 @@ class Pipeline:
         self.k = 0
         self.A0 = [t.clone() for t in self.A.planes]
         self.lf = F.LoopFilterMeta(fr["lf"])
-        self.cdef = F.CdefMeta(fr["lf"]["masks"], fr["cdef"], masks_dev=self.lf.masks)
-        self.lr = F.LrMeta(fr["lr"])
+        self.cdef = F.CdefMeta(fr["lf"]["masks"], fr["cdef"], masks_dev=self.lf.masks, geometry=(w, h, lay))
+        self.lr = F.LrMeta(fr["lr"], geometry=(w, h, lay))
         self.fgd = F.film_grain_data(fr["fg"]) if fr["fg"] else None
         self.side = torch.cuda.Stream()
         fb = frame_bytes(w, h, bpc, lay)

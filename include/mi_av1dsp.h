@@ -97,7 +97,18 @@ typedef struct MiCdef {
     int32_t damping;             /* frame_hdr.cdef.damping (3..6) */
     uint8_t y_strength[8];       /* pri << 2 | sec, as coded */
     uint8_t uv_strength[8];
+    /* Optional (NULL: grid order): the order the 64x64-unit workgroups run in, a device array
+     * of mi_cdef_tile_order's length and contents. */
+    const int32_t *order;
 } MiCdef;
+
+/* The order mi_cdef_frame's workgroups run best in: the 64x64 units by descending cost (a
+ * primary strength: direction search and filter; a secondary strength only; nothing to filter:
+ * a copy), longest first. A host call on a host copy of the Av1Filter array for a w x h
+ * picture: writes the unit indices into `order` (capacity n) and returns their count, or
+ * -EINVAL. */
+int mi_cdef_tile_order(const MiAv1Filter *masks_host, int w, int h, int layout, const MiCdef *cdef, int32_t *order,
+                       int n);
 
 /* Loop-restoration unit parameters, byte-identical to Av1RestorationUnit / Av1Restoration
  * (src/lf_mask.rs:31-38, 55-58; C src/lf_mask.h:42-62). type: Dav1dRestorationType
@@ -117,7 +128,18 @@ typedef struct MiLr {
     int32_t sb128w;
     int32_t restore_planes;          /* bit0 Y, bit1 U, bit2 V (f->lf.restore_planes) */
     int32_t unit_size_log2[2];       /* frame_hdr.restoration.unit_size[luma, chroma] */
+    /* Optional (NULL: grid order): the order the (plane, stripe, tile) workgroups run in, a
+     * device array of mi_lr_tile_order's length and contents. */
+    const int32_t *order;
 } MiLr;
+
+/* The order mi_lr_frame's workgroups run best in: the restoration tiles by descending cost
+ * (self-guided with both radii, with one, Wiener, copy), so that the longest start first and the
+ * grid does not end on a tail of them (longest-processing-time-first). A host call on a host
+ * copy of the lr_mask for a w x h picture of `layout`: writes the tile indices into `order`
+ * (capacity n) and returns their count, or -EINVAL. */
+int mi_lr_tile_order(const MiAv1Restoration *lr_mask_host, int w, int h, int layout, const MiLr *lr,
+                     int32_t *order, int n);
 
 /* Film-grain parameters, byte-identical to Dav1dFilmGrainData (include/dav1d/headers.h:
  * 315-333; Rust Rav1dFilmGrainData include/dav1d/headers.rs:1585-1610). */

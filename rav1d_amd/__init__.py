@@ -56,12 +56,12 @@ class MiLoopFilter(ctypes.Structure):
 
 class MiCdef(ctypes.Structure):
     _fields_ = [("masks", ctypes.c_void_p), ("sb128w", ctypes.c_int32), ("damping", ctypes.c_int32),
-                ("y_strength", ctypes.c_uint8 * 8), ("uv_strength", ctypes.c_uint8 * 8)]
+                ("y_strength", ctypes.c_uint8 * 8), ("uv_strength", ctypes.c_uint8 * 8), ("order", ctypes.c_void_p)]
 
 
 class MiLr(ctypes.Structure):
     _fields_ = [("lr_mask", ctypes.c_void_p), ("sb128w", ctypes.c_int32), ("restore_planes", ctypes.c_int32),
-                ("unit_size_log2", ctypes.c_int32 * 2)]
+                ("unit_size_log2", ctypes.c_int32 * 2), ("order", ctypes.c_void_p)]
 
 
 class MiFilmGrainData(ctypes.Structure):
@@ -192,6 +192,10 @@ def lib():
                                             ctypes.POINTER(MiCdef), _VP])
     _sig(L, "mi_lr_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
                                           ctypes.POINTER(MiPicture), ctypes.POINTER(MiLr), _VP])
+    _sig(L, "mi_cdef_tile_order", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(MiCdef),
+                                                 ctypes.POINTER(ctypes.c_int32), ctypes.c_int])
+    _sig(L, "mi_lr_tile_order", ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(MiLr),
+                                               ctypes.POINTER(ctypes.c_int32), ctypes.c_int])
     for n in ("mi_film_grain_frame", "mi_film_grain_apply"):
         _sig(L, n, ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
                                   ctypes.POINTER(MiFilmGrainData), ctypes.c_int, _VP])
@@ -214,7 +218,7 @@ def lib():
 # Every symbol include/mi_av1dsp.h declares (checked by tests/test_abi.py).
 EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
             "mi_itx_frame", "mi_itx_frame_banded", "mi_mc_frame", "mi_mc_frame_ex", "mi_mc_scaled", "mi_mc_warp", "mi_mc_combine", "mi_superres_frame",
-            "mi_ipred_blocks", "mi_intra_blocks", "mi_intra_recon", "mi_ctx_device_status", "mi_deblock_frame", "mi_deblock_frame_to", "mi_cdef_frame", "mi_lr_frame",
+            "mi_ipred_blocks", "mi_intra_blocks", "mi_intra_recon", "mi_ctx_device_status", "mi_deblock_frame", "mi_deblock_frame_to", "mi_cdef_frame", "mi_lr_frame", "mi_lr_tile_order", "mi_cdef_tile_order",
             "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply", "mi_frame_run", "mi_frame_end", "mi_frame_validate", "mi_frame_plan_ms",
             "mi_ctx_set_timing", "mi_ctx_timing",
             "mi_dsp_itxfm_add", "mi_dsp_intra_pred", "mi_dsp_cfl_pred", "mi_dsp_pal_pred", "mi_dsp_cfl_ac",

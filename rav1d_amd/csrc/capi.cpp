@@ -529,47 +529,66 @@ int mi_cdef_frame(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const 
     memcpy(a.y_strength, cd->y_strength, 8);
     memcpy(a.uv_strength, cd->uv_strength, 8);
     a.tiles_x = (a.bw4 * 4 + 63) / 64;
+    a.order = cd->order;
     const int tiles_y = (a.bh4 * 4 + 63) / 64;
     const int r = mi::launch_cdef(a, a.tiles_x * tiles_y, src->bpc, (hipStream_t)stream);
     return r ? fail(ctx, -EIO) : 0;
 }
 
-int mi_lr_frame(MiCtx *ctx, const MiPicture *cdef, const MiPicture *deblocked, const MiPicture *dst,
-                const MiLr *lr, void *stream) {
-    if (!ctx || !cdef || !deblocked || !dst || !lr) return fail(ctx, -EINVAL);
-    if (!same_geometry(cdef, deblocked) || !same_geometry(cdef, dst)) return fail(ctx, -EINVAL);
-    if (cdef->bpc != 8 && cdef->bpc != 10 && cdef->bpc != 12) return fail(ctx, -EINVAL);
-    if (lr->restore_planes && (!lr->lr_mask || lr->sb128w != (cdef->w + 127) >> 7)) return fail(ctx, -EINVAL);
-    const int ss_hor = cdef->layout == 1 || cdef->layout == 2, ss_ver = cdef->layout == 1;
+int mi_cdef_tile_order(const MiAv1Filter *masks, int w, int h, int layout, const MiCdef *cd, int32_t *order, int n) {
+    if (!masks || !cd || !order || w <= 0 || h <= 0 || layout < 0 || layout > 3) return -EINVAL;
+    if (cd->sb128w != (w + 127) >> 7) return -EINVAL;
+    const int bw4 = ((w + 7) >> 3) << 1, bh4 = ((h + 7) >> 3) << 1;
+    const int tx = (bw4 * 4 + 63) / 64, ty = (bh4 * 4 + 63) / 64, nt = tx * ty;
+    if (nt > n) return -EINVAL;
+    // cost class per unit (cdef_kernel's own tests): 2 a primary strength (direction search and
+    // filter), 1 a secondary one only, 0 nothing to filter (no strength, or every 8x8 skipped);
+    // then a stable counting sort, costliest first
+    std::vector<uint8_t> cls(nt, 0);
+    for (int t = 0; t < nt; t++) {
+        const int x = t % tx, y = t / tx;
+        const MiAv1Filter &lf = masks[(y >> 1) * cd->sb128w + (x >> 1)];
+        const int idx = lf.cdef_idx[(y & 1) * 2 + (x & 1)];
+        if (idx < 0) continue;
+        const int yl = cd->y_strength[idx], uvl = layout ? cd->uv_strength[idx] : 0;
+        if (!yl && !uvl) continue;
+        // the unit's 8x8 rows (16 per 128-px superblock row, half of them per 64-px unit) and
+        // its half of each row's 32-bit noskip word
+        unsigned any = 0;
+        for (int r = 8 * (y & 1); r < 8 * (y & 1) + 8; r++)
+            any |= ((unsigned)lf.noskip_mask[r][1] << 16 | lf.noskip_mask[r][0]) >> (16 * (x & 1)) & 0xffffu;
+        if (!any) continue;
+        cls[t] = (yl >> 2) || (uvl >> 2) ? 2 : 1;
+    }
+    int start[4] = {};
+    for (uint8_t c : cls) start[2 - c + 1]++;
+    for (int c = 0; c < 3; c++) start[c + 1] += start[c];
+    for (int t = 0; t < nt; t++) order[start[2 - cls[t]]++] = t;
+    return nt;
+}
+
+// The (plane, stripe, tile) grid of mi_lr_frame for a w x h picture (pw, ph, tw, tiles_x,
+// blk_start of `a`); -EINVAL for unit sizes outside the bitstream's
+static int lr_layout(int w, int h, int layout, const MiLr *lr, mi::LrArgs &a) {
+    const int ss_hor = layout == 1 || layout == 2, ss_ver = layout == 1;
     for (int c = 0; c < 2; c++) {
         const int l2 = lr->unit_size_log2[c];
-        if ((lr->restore_planes & (c ? 6 : 1)) && (l2 < 5 || l2 > 8)) return fail(ctx, -EINVAL);
+        if ((lr->restore_planes & (c ? 6 : 1)) && (l2 < 5 || l2 > 8)) return -EINVAL;
     }
-    mi::LrArgs a;
-    memset(&a, 0, sizeof(a));
-    a.lr_mask = lr->lr_mask;
-    a.sb128w = lr->sb128w;
     a.restore = lr->restore_planes;
-    a.bd = cdef->bpc;
     a.ss_hor = ss_hor;
     a.ss_ver = ss_ver;
     a.unit_log2[0] = lr->unit_size_log2[0];
     a.unit_log2[1] = lr->unit_size_log2[1];
-    const int nplanes = cdef->layout ? 3 : 1;
+    a.sb128w = lr->sb128w;
+    const int nplanes = layout ? 3 : 1;
     int nb = 0;
     for (int p = 0; p < 3; p++) {
         a.blk_start[p] = nb;
         if (p >= nplanes) continue;
-        a.src[p] = (const uint8_t *)cdef->data[p];
-        a.lpf[p] = (const uint8_t *)deblocked->data[p];
-        a.dst[p] = (uint8_t *)dst->data[p];
-        a.stride[p] = cdef->stride[p ? 1 : 0];
         const int sh = p ? ss_hor : 0, sv = p ? ss_ver : 0;
-        a.pw[p] = (cdef->w + sh) >> sh;
-        a.ph[p] = (cdef->h + sv) >> sv;
-        // lr.hip forms row offsets with one 24-bit multiply
-        if (a.stride[p] <= 0 || a.stride[p] >= (1 << 24) || (int64_t)a.ph[p] * a.stride[p] >= (1LL << 32))
-            return fail(ctx, -EINVAL);
+        a.pw[p] = (w + sh) >> sh;
+        a.ph[p] = (h + sv) >> sv;
         const int us = 1 << lr->unit_size_log2[p ? 1 : 0];
         a.tw[p] = ((a.restore >> p) & 1) && us < 64 ? 32 : 64;
         a.tiles_x[p] = (a.pw[p] + a.tw[p] - 1) / a.tw[p];
@@ -579,8 +598,63 @@ int mi_lr_frame(MiCtx *ctx, const MiPicture *cdef, const MiPicture *deblocked, c
         nb += stripes * a.tiles_x[p];
     }
     a.blk_start[3] = nb;
+    return 0;
+}
+
+int mi_lr_frame(MiCtx *ctx, const MiPicture *cdef, const MiPicture *deblocked, const MiPicture *dst,
+                const MiLr *lr, void *stream) {
+    if (!ctx || !cdef || !deblocked || !dst || !lr) return fail(ctx, -EINVAL);
+    if (!same_geometry(cdef, deblocked) || !same_geometry(cdef, dst)) return fail(ctx, -EINVAL);
+    if (cdef->bpc != 8 && cdef->bpc != 10 && cdef->bpc != 12) return fail(ctx, -EINVAL);
+    if (lr->restore_planes && (!lr->lr_mask || lr->sb128w != (cdef->w + 127) >> 7)) return fail(ctx, -EINVAL);
+    mi::LrArgs a;
+    memset(&a, 0, sizeof(a));
+    if (lr_layout(cdef->w, cdef->h, cdef->layout, lr, a)) return fail(ctx, -EINVAL);
+    a.lr_mask = lr->lr_mask;
+    a.bd = cdef->bpc;
+    a.order = lr->order;
+    for (int p = 0; p < (cdef->layout ? 3 : 1); p++) {
+        a.src[p] = (const uint8_t *)cdef->data[p];
+        a.lpf[p] = (const uint8_t *)deblocked->data[p];
+        a.dst[p] = (uint8_t *)dst->data[p];
+        a.stride[p] = cdef->stride[p ? 1 : 0];
+        // lr.hip forms row offsets with one 24-bit multiply
+        if (a.stride[p] <= 0 || a.stride[p] >= (1 << 24) || (int64_t)a.ph[p] * a.stride[p] >= (1LL << 32))
+            return fail(ctx, -EINVAL);
+    }
     const int r = mi::launch_lr(a, cdef->bpc, (hipStream_t)stream);
     return r ? fail(ctx, -EIO) : 0;
+}
+
+int mi_lr_tile_order(const MiAv1Restoration *mask, int w, int h, int layout, const MiLr *lr, int32_t *order,
+                     int n) {
+    if (!lr || !order || w <= 0 || h <= 0 || layout < 0 || layout > 3) return -EINVAL;
+    if (lr->restore_planes && !mask) return -EINVAL;
+    mi::LrArgs a;
+    memset(&a, 0, sizeof(a));
+    if (lr_layout(w, h, layout, lr, a) || a.blk_start[3] > n) return -EINVAL;
+    // cost class per tile (lr_kernel's unit lookup): 3 self-guided with both radii, 2 with one
+    // (sgr_params 10-15), 1 Wiener, 0 copy; then a stable counting sort, costliest first
+    std::vector<uint8_t> cls(a.blk_start[3], 0);
+    for (int p = 0; p < 3; p++) {
+        if (!((a.restore >> p) & 1)) continue;
+        const int ssh = p ? a.ss_hor : 0, ssv = p ? a.ss_ver : 0, pw = a.pw[p], ph = a.ph[p];
+        const int us = 1 << a.unit_log2[p ? 1 : 0], nu = std::max(1, (pw + (us >> 1)) / us);
+        for (int b = a.blk_start[p]; b < a.blk_start[p + 1]; b++) {
+            const int lb = b - a.blk_start[p], k = lb / a.tiles_x[p], ti = lb - k * a.tiles_x[p];
+            const int xu = std::min(ti * a.tw[p] / us, nu - 1) * us;
+            int ay = ((64 * k) >> ssv) & ~(us - 1);
+            if (ay && ay + (us >> 1) > ph) ay -= us;
+            ay <<= ssv;
+            const int t = mask[(ay >> 7) * a.sb128w + (xu >> (7 - ssh))].lr[p][(((ay >> 6) & 1) << 1) + ((xu >> (6 - ssh)) & 1)].type;
+            cls[b] = t == 0 ? 0 : t == 2 ? 1 : t >= 3 && t - 3 < 10 ? 3 : t >= 3 ? 2 : 0;
+        }
+    }
+    int start[5] = {};
+    for (uint8_t c : cls) start[3 - c + 1]++;
+    for (int c = 0; c < 4; c++) start[c + 1] += start[c];
+    for (int b = 0; b < a.blk_start[3]; b++) order[start[3 - cls[b]]++] = b;
+    return a.blk_start[3];
 }
 
 static int fg_tables() {

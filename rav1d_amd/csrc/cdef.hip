@@ -533,7 +533,12 @@ __global__ __launch_bounds__(512, 8) void cdef_kernel(CdefArgs a) {
     __shared__ int4 ctaps[8][3];          // 4:2:0 chroma tap byte deltas per direction
     KTL(0);
 
-    const int bid = xcd_block(blockIdx.x, gridDim.x);
+    int bid = xcd_block(blockIdx.x, gridDim.x);
+    if (a.order) {
+        // the caller's order (mi_cdef_tile_order): the costliest units first
+        bid = a.order[blockIdx.x];
+        if ((unsigned)bid >= gridDim.x) return;
+    }
     const int tx = bid % a.tiles_x, tyy = bid / a.tiles_x;
     const int x0 = tx * 64, y0 = tyy * 64;
     const MiAv1Filter *lf = &a.masks[(tyy >> 1) * a.sb128w + (tx >> 1)];

@@ -196,6 +196,7 @@ struct CdefArgs {
     int ss_hor, ss_ver, layout;
     int bdm8, damping;            // damping already includes bitdepth_min_8
     uint8_t y_strength[8], uv_strength[8];
+    const int32_t *order;         // workgroup -> 64x64 unit (null: xcd_block's grid order)
 };
 // launchers (cdef.hip)
 int launch_cdef(const CdefArgs &a, int tiles, int bpc, hipStream_t s);
@@ -304,6 +305,7 @@ struct LrArgs {
     int unit_log2[2];
     int pw[3], ph[3], tw[3], tiles_x[3];
     int blk_start[4];
+    const int32_t *order;         // workgroup -> tile (null: grid order)
 };
 // launchers (lr.hip)
 int launch_lr(const LrArgs &a, int bpc, hipStream_t s);

@@ -587,6 +587,9 @@ struct FramePlan {
     uint32_t mc_cs[2 * MI_MC_NCLASS + 1], lap_cs[2][2 * MI_MC_NCLASS + 1];
     std::vector<MiTxBlock> itx_b;
     uint32_t itx_bs[MI_N_RECT_TX_SIZES][MI_ITX_BANDS + 1];
+    // CDEF and loop-restoration workgroup orders, costliest first (mi_cdef_tile_order /
+    // mi_lr_tile_order)
+    std::vector<int32_t> cdef_order, lr_order;
     double strips_ms = 0;
 };
 
@@ -611,6 +614,33 @@ void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
         std::vector<MiMcBlock> plain;
         for (int i = 0; i < (k ? f->n_obmc_v : f->n_obmc_h); i++) (scaled[u[i].ref[0]] ? lap_s[k] : plain).push_back(u[i]);
         bucket_mc(plain.data(), (int)plain.size(), lap_b[k], lap_cs[k]);
+    }
+    // the post-filters' workgroups, longest first, so that a launch does not end on a tail of
+    // long ones (LR 35.8 -> 31.1 us on the 4K10 bench frame)
+    pl.cdef_order.clear();
+    pl.lr_order.clear();
+    if (f->cdef_on) {
+        MiCdef cd;
+        memset(&cd, 0, sizeof(cd));
+        cd.sb128w = f->sb128w;
+        memcpy(cd.y_strength, f->cdef_y, 8);
+        memcpy(cd.uv_strength, f->cdef_uv, 8);
+        pl.cdef_order.resize((size_t)((f->w + 63) / 64 + 1) * ((f->h + 63) / 64 + 1));
+        const int n = mi_cdef_tile_order(f->lf_masks, f->w, f->h, f->layout, &cd, pl.cdef_order.data(),
+                                         (int)pl.cdef_order.size());
+        pl.cdef_order.resize(n > 0 ? n : 0);
+    }
+    if (f->restore_planes) {
+        MiLr lr;
+        memset(&lr, 0, sizeof(lr));
+        lr.sb128w = f->lr_sb128w;
+        lr.restore_planes = f->restore_planes;
+        lr.unit_size_log2[0] = f->lr_unit_size[0];
+        lr.unit_size_log2[1] = f->lr_unit_size[1];
+        pl.lr_order.resize((size_t)3 * ((f->h + 63) / 64 + 1) * ((f->up_w + 31) / 32 + 1));
+        const int n = mi_lr_tile_order(f->lr_mask, f->up_w, f->h, f->layout, &lr, pl.lr_order.data(),
+                                       (int)pl.lr_order.size());
+        pl.lr_order.resize(n > 0 ? n : 0);
     }
     // residuals grouped by (tx size, picture band) for mi_itx_frame_banded: a counting sort
     // keeping decode order inside a group
@@ -700,6 +730,8 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         { f->masks, f->nmasks, 0 },                                                 // 19
         { itx_b.data(), itx_b.size() * sizeof(MiTxBlock), 0 },                     // 20
         { nullptr, f->ntmp * 2, 0 },                                                // 21: tmp arena
+        { pl.cdef_order.data(), pl.cdef_order.size() * 4, 0 },                     // 22
+        { pl.lr_order.data(), pl.lr_order.size() * 4, 0 },                         // 23
     };
     const auto t_st = clk::now();
     if ((r = stage_upload(ctx, secs, s, tev.ev[0], bytes))) return ctx->last_error = r;
@@ -824,6 +856,7 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         cd.damping = f->cdef_damping;
         memcpy(cd.y_strength, f->cdef_y, 8);
         memcpy(cd.uv_strength, f->cdef_uv, 8);
+        cd.order = (const int32_t *)D(22);
         if ((r = mi_cdef_frame(ctx, cur, &cp[2], &cd, stream))) return r;
         cur = &cp[2];
         idx = 2;
@@ -861,6 +894,7 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         lr.restore_planes = f->restore_planes;
         lr.unit_size_log2[0] = f->lr_unit_size[0];
         lr.unit_size_log2[1] = f->lr_unit_size[1];
+        lr.order = (const int32_t *)D(23);
         int out = 3;
         if (f->up_w != f->w)
             for (int k = 0; k < 4; k++)

@@ -406,7 +406,12 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(8))) void l
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     // (hardware round robin: XCD-local orders of the tiles cut LR's HBM reads from 70 to 28 MB
     // but ran 1.3-5.9 us slower)
-    const int blk = blockIdx.x;
+    int blk = blockIdx.x;
+    if (a.order) {
+        // the caller's order (mi_lr_tile_order): longest tiles first
+        blk = a.order[blk];
+        if ((unsigned)blk >= (unsigned)a.blk_start[3]) return;
+    }
     const int p = blk < a.blk_start[1] ? 0 : blk < a.blk_start[2] ? 1 : 2;
     const int lb = blk - a.blk_start[p];
     const int tiles = a.tiles_x[p];

@@ -263,9 +263,11 @@ def deblock_frame(ctx, frame, meta, stream=None, dst=None):
 
 
 class CdefMeta:
-    """Device copy of the Av1Filter array + frame CDEF params (MiCdef)."""
+    """Device copy of the Av1Filter array + frame CDEF params (MiCdef). With the picture's
+    (w, h, layout), also the workgroup order mi_cdef_tile_order computes on the host (costliest
+    units first), as the frame executor passes it."""
 
-    def __init__(self, masks, cdef, masks_dev=None):
+    def __init__(self, masks, cdef, masks_dev=None, geometry=None):
         self.masks = masks_dev if masks_dev is not None else \
             torch.from_numpy(np.ascontiguousarray(masks).view(np.uint8).reshape(-1)).cuda()
         s = MiCdef()
@@ -275,6 +277,16 @@ class CdefMeta:
         s.y_strength[:] = [int(v) for v in cdef["y_strength"]]
         s.uv_strength[:] = [int(v) for v in cdef["uv_strength"]]
         self.s = s
+        self.order = None
+        if geometry is not None:
+            w, h, layout = geometry
+            m = np.ascontiguousarray(masks)
+            cap = ((w + 63) // 64 + 1) * ((h + 63) // 64 + 1)
+            buf = (ctypes.c_int32 * cap)()
+            n = lib().mi_cdef_tile_order(m.ctypes.data_as(ctypes.c_void_p), w, h, layout, ctypes.byref(s), buf, cap)
+            check(n if n < 0 else 0, "mi_cdef_tile_order")
+            self.order = torch.tensor(list(buf[:n]), dtype=torch.int32).cuda()
+            s.order = self.order.data_ptr()
 
 
 def cdef_frame(ctx, src, dst, meta, stream=None):
@@ -284,9 +296,11 @@ def cdef_frame(ctx, src, dst, meta, stream=None):
 
 
 class LrMeta:
-    """Device copy of the Av1Restoration array + frame LR params (MiLr)."""
+    """Device copy of the Av1Restoration array + frame LR params (MiLr). With the picture's
+    (w, h, layout), also the workgroup order mi_lr_tile_order computes on the host (longest
+    tiles first), as the frame executor passes it."""
 
-    def __init__(self, lr):
+    def __init__(self, lr, geometry=None):
         m = np.ascontiguousarray(lr["lr_mask"])
         self.mask = torch.from_numpy(m.view(np.uint8).reshape(-1)).cuda()
         s = MiLr()
@@ -295,6 +309,15 @@ class LrMeta:
         s.restore_planes = int(lr["restore_planes"])
         s.unit_size_log2[0], s.unit_size_log2[1] = [int(v) for v in lr["unit_size_log2"]]
         self.s = s
+        self.order = None
+        if geometry is not None:
+            w, h, layout = geometry
+            cap = 3 * ((h + 63) // 64 + 1) * ((w + 31) // 32 + 1)
+            buf = (ctypes.c_int32 * cap)()
+            n = lib().mi_lr_tile_order(m.ctypes.data_as(ctypes.c_void_p), w, h, layout, ctypes.byref(s), buf, cap)
+            check(n if n < 0 else 0, "mi_lr_tile_order")
+            self.order = torch.tensor(list(buf[:n]), dtype=torch.int32).cuda()
+            s.order = self.order.data_ptr()
 
 
 def lr_frame(ctx, cdef, deblocked, dst, meta, stream=None):

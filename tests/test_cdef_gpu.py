@@ -11,7 +11,7 @@ from tests.test_oracle_lf import frame, pad_planes
 pytestmark = pytest.mark.gpu
 
 
-def run_case(gpu, w, h, bpc, layout, seed):
+def run_case(gpu, w, h, bpc, layout, seed, ordered=False):
     planes, lf = frame(w, h, bpc, layout, seed)
     planes = planes[:1] if layout == 0 else planes
     rng = np.random.default_rng(seed + 99)
@@ -20,7 +20,7 @@ def run_case(gpu, w, h, bpc, layout, seed):
     for p, a in enumerate(planes):
         src.set_plane_np(p, a)
     dst = Frame(w, h, bpc, layout)
-    cdef_frame(gpu, src, dst, CdefMeta(lf["masks"], cd))
+    cdef_frame(gpu, src, dst, CdefMeta(lf["masks"], cd, geometry=(w, h, layout) if ordered else None))
     torch.cuda.synchronize()
     ref = oracle_lib.cdef_frame(pad_planes(planes, w, h, bpc, layout), bpc, layout, w, h, lf["masks"], cd)
     for p in range(len(planes)):
@@ -40,3 +40,11 @@ def test_cdef_matches_oracle(gpu, bpc, layout, size):
 @pytest.mark.parametrize("bpc", [8, 10])
 def test_cdef_1080p_matches_oracle(gpu, bpc):
     run_case(gpu, 1920, 1080, bpc, 1, seed=0xCDEF)
+
+
+@pytest.mark.parametrize("layout", [0, 1, 2, 3])
+def test_cdef_unit_order_matches_oracle(gpu, layout):
+    """The workgroups in mi_cdef_tile_order's order (costliest units first): the same pixels."""
+    run_case(gpu, 330, 200, 10, layout, seed=0xC0 + layout, ordered=True)
+    if layout == 1:
+        run_case(gpu, 1920, 1080, 10, layout, seed=0xC5, ordered=True)

@@ -16,6 +16,10 @@ pipe.step(s)
 torch.cuda.synchronize()
 L = F.lib()
 st = os.environ.get("STAGE", "deblock")
+lr_grid = F.MiLr.from_buffer_copy(pipe.lr.s)   # the same LR call in grid order
+lr_grid.order = None
+cdef_grid = F.MiCdef.from_buffer_copy(pipe.cdef.s)
+cdef_grid.order = None
 sp = F._stream_ptr(s)
 pa, pb, po, pd = pipe.A.picture(), pipe.B.picture(), pipe.O.picture(), pipe.D.picture()
 def itx(p):
@@ -32,6 +36,10 @@ for _ in range(int(os.environ.get("REPS", "10"))):
         F.check(L.mi_cdef_frame(ctx.h, ctypes.byref(pd), ctypes.byref(pb), ctypes.byref(pipe.cdef.s), sp), "cdef")
     elif st == "lr":
         F.check(L.mi_lr_frame(ctx.h, ctypes.byref(pb), ctypes.byref(pd), ctypes.byref(po), ctypes.byref(pipe.lr.s), sp), "lr")
+    elif st == "lr_grid":
+        F.check(L.mi_lr_frame(ctx.h, ctypes.byref(pb), ctypes.byref(pd), ctypes.byref(po), ctypes.byref(lr_grid), sp), "lr")
+    elif st == "cdef_grid":
+        F.check(L.mi_cdef_frame(ctx.h, ctypes.byref(pd), ctypes.byref(pb), ctypes.byref(cdef_grid), sp), "cdef")
 torch.cuda.synchronize()
 print("done")
 if os.environ.get("TIME"):
@@ -48,4 +56,8 @@ if os.environ.get("TIME"):
             F.check(L.mi_cdef_frame(ctx.h, ctypes.byref(pd), ctypes.byref(pb), ctypes.byref(pipe.cdef.s), p), "cdef")
         elif st == "lr":
             F.check(L.mi_lr_frame(ctx.h, ctypes.byref(pb), ctypes.byref(pd), ctypes.byref(po), ctypes.byref(pipe.lr.s), p), "lr")
+        elif st == "lr_grid":
+            F.check(L.mi_lr_frame(ctx.h, ctypes.byref(pb), ctypes.byref(pd), ctypes.byref(po), ctypes.byref(lr_grid), p), "lr")
+        elif st == "cdef_grid":
+            F.check(L.mi_cdef_frame(ctx.h, ctypes.byref(pd), ctypes.byref(pb), ctypes.byref(cdef_grid), p), "cdef")
     print(f"{st} {gtime(one):.2f} us", flush=True)
