@@ -535,6 +535,30 @@ int mi_cdef_frame(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const 
     return r ? fail(ctx, -EIO) : 0;
 }
 
+// Costliest class first (cls[t] in 0 .. nclass-1, higher = costlier); within a class the items
+// are dealt to the XCDs in contiguous picture runs: workgroup b runs on XCD b % 8, so XCD x takes
+// one run of each class and neighbouring tiles share an L2 (the locality xcd_block gives the
+// grid order: CDEF 39.2 us this way, 40.1 in xcd_block's grid order, 42.2 for a plain
+// costliest-first order)
+static void deal_classes(const std::vector<uint8_t> &cls, int nclass, int32_t *order) {
+    const int nt = (int)cls.size();
+    int b = 0;
+    for (int c = nclass - 1; c >= 0; c--) {
+        std::vector<int32_t> items;
+        for (int t = 0; t < nt; t++)
+            if (cls[t] == c) items.push_back(t);
+        const int L = (int)items.size();
+        int cnt[8] = {}, pos[8];
+        for (int r = 0; r < L; r++) cnt[(b + r) & 7]++;
+        for (int x = 0, acc = 0; x < 8; x++) {
+            pos[x] = acc;
+            acc += cnt[x];
+        }
+        for (int r = 0; r < L; r++) order[b + r] = items[pos[(b + r) & 7]++];
+        b += L;
+    }
+}
+
 int mi_cdef_tile_order(const MiAv1Filter *masks, int w, int h, int layout, const MiCdef *cd, int32_t *order, int n) {
     if (!masks || !cd || !order || w <= 0 || h <= 0 || layout < 0 || layout > 3) return -EINVAL;
     if (cd->sb128w != (w + 127) >> 7) return -EINVAL;
@@ -560,10 +584,7 @@ int mi_cdef_tile_order(const MiAv1Filter *masks, int w, int h, int layout, const
         if (!any) continue;
         cls[t] = (yl >> 2) || (uvl >> 2) ? 2 : 1;
     }
-    int start[4] = {};
-    for (uint8_t c : cls) start[2 - c + 1]++;
-    for (int c = 0; c < 3; c++) start[c + 1] += start[c];
-    for (int t = 0; t < nt; t++) order[start[2 - cls[t]]++] = t;
+    deal_classes(cls, 3, order);
     return nt;
 }
 
