@@ -592,7 +592,8 @@ template <bool COLS, typename Px, int P>
 __device__ __forceinline__ void lf_dir_pk(Px *t, const uint16_t (*lists)[COLS ? (kLfRows / 4) * kLfEdgesV : kLfEdgesH * (kLfTW / 4)],
                                           const int *cnt, const uint8_t *le, const uint8_t *li, int bdm8, int bdmax) {
     constexpr int N = COLS ? (kLfRows / 4) * kLfEdgesV : kLfEdgesH * (kLfTW / 4);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tid = (int)threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
     // chunk prefix over the classes (wave-uniform: the counts are LDS broadcasts)
     const int c0 = (cnt[0] * 2 + 63) >> 6, c1 = c0 + ((cnt[1] * 2 + 63) >> 6);
     const int c2 = c1 + ((cnt[2] * 2 + 63) >> 6), c3 = c2 + ((cnt[3] * 2 + 63) >> 6);
@@ -617,124 +618,181 @@ __device__ __forceinline__ void lf_dir_pk(Px *t, const uint16_t (*lists)[COLS ? 
     }
 }
 
+
 // wd -> work class (lines of one class run the same filter branch)
 __device__ __forceinline__ int lf_class(int wd) { return wd == 4 ? 0 : wd == 6 ? 1 : wd == 8 ? 2 : 3; }
 
+// Staging shapes of one tile
 template <typename Px>
-__global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
-    constexpr int VB = 16;                        // bytes per vector
-    constexpr int VPX = VB / sizeof(Px);          // pixels per vector
+struct LfShape {
+    static constexpr int VPX = 16 / sizeof(Px);                 // pixels per 16-B vector
     // LDS pitch in pixels: the staged kLfCols (+8 px of padding cut the LDS bank conflicts
     // 3.15 -> 2.2 M cycles but ran 31 vs 29 us)
-    constexpr int P = kLfCols;
+    static constexpr int P = kLfCols;
+    static constexpr int NV = (kLfRows / 4) * kLfEdgesV;        // column-edge units (4 lines each)
+    static constexpr int NH = kLfEdgesH * (kLfTW / 4);          // row-edge units
+    static constexpr int VPR = kLfCols / VPX;                   // vectors per staged row
+    static constexpr int NS = (kLfRows * VPR + kLfThreads - 1) / kLfThreads;
+    static constexpr int NU = (NV + NH + kLfThreads - 1) / kLfThreads;
+    static constexpr int VPT = kLfTW / VPX;                     // vectors per tile row
     static_assert(P % 8 == 0 && P >= kLfCols, "16-B aligned rows");
-    constexpr int NV = (kLfRows / 4) * kLfEdgesV; // column-edge units (4 lines each)
-    constexpr int NH = kLfEdgesH * (kLfTW / 4);   // row-edge units
-    __shared__ __attribute__((aligned(16))) Px t[kLfRows * P];
-    // work lists: active edge units bucketed by width class, so that the lanes of a wave run
-    // one filter branch; entry = (unit index << 6) | L
-    __shared__ uint16_t listv[2][NV], listh[2][NH];
-    __shared__ int cnt[8];
-    __shared__ uint8_t le[64], li[64];
-    const int tid = threadIdx.x;
-    const int b = xcd_block(blockIdx.x, gridDim.x);
-    const int p = b < a.tile_start[1] ? 0 : b < a.tile_start[2] ? 1 : 2;
-    // the plane's fields by kernarg offset (KARG_OF): selecting among the three copies kept
-    // every per-plane field in SGPRs (78 SGPRs: 7 instead of 8 waves' worth per CU)
-    const int lb = b - KARG_OF(LfTileArgs, tile_start, p);
-    const int tx = KARG_OF(LfTileArgs, tiles_x, p);
-    const int x0 = (lb % tx) * kLfTW, y0 = (lb / tx) * kLfTH;
-    const int pw = KARG_OF(LfTileArgs, pw, p), ph = KARG_OF(LfTileArgs, ph, p);
-    const int64_t st = KARG_OF(LfTileArgs, stride, p);
-    const uint8_t *src = KARG_OF(LfTileArgs, src, p);
-    KTL(0);
-    if (tid < 64) { le[tid] = a.lim_e[tid]; li[tid] = a.lim_i[tid]; }
-    if (tid < 8) cnt[tid] = 0;
-    __syncthreads();
-    // Stage rows y0-12 .. y0+75, columns x0-16 .. x0+79 (pixels outside the plane read as 0:
-    // no edge reaches them), and fetch every edge unit's mask and level words. All of these
-    // loads are independent and issued before any is used.
-    constexpr int VPR = kLfCols / VPX;            // vectors per staged row
-    constexpr int NS = (kLfRows * VPR + kLfThreads - 1) / kLfThreads;
-    constexpr int NU = (NV + NH + kLfThreads - 1) / kLfThreads;
     static_assert((NV > NH ? NV : NH) << 6 <= 65536, "work-list entries (unit << 6 | level) must fit 16 bits");
-    uint4 sv[NS];
+};
+
+// Tile b of the launch: its plane and origin. The plane's fields are read by kernarg offset
+// (KARG_OF): selecting among the three copies kept every per-plane field in SGPRs.
+struct LfTile {
+    int p, x0, y0, pw, ph;
+    int64_t st;
+};
+__device__ __forceinline__ LfTile lf_tile_at(const LfTileArgs &a, int b) {
+    LfTile g;
+    g.p = b < a.tile_start[1] ? 0 : b < a.tile_start[2] ? 1 : 2;
+    const int lb = b - KARG_OF(LfTileArgs, tile_start, g.p);
+    const int tx = KARG_OF(LfTileArgs, tiles_x, g.p);
+    g.x0 = (lb % tx) * kLfTW; g.y0 = (lb / tx) * kLfTH;
+    g.pw = KARG_OF(LfTileArgs, pw, g.p); g.ph = KARG_OF(LfTileArgs, ph, g.p);
+    g.st = KARG_OF(LfTileArgs, stride, g.p);
+    return g;
+}
+
+// Issue every load of tile g: rows y0-12 .. y0+TH+11, columns x0-16 .. x0+TW+15 (pixels
+// outside the plane read as 0: no edge reaches them), and every edge unit's mask and level
+// words. All of them are independent; none is waited for here.
+template <typename Px>
+__device__ __forceinline__ void lf_fetch_pixels(const LfTileArgs &a, const LfTile &g, uint4 (&sv)[LfShape<Px>::NS]) {
+    using S = LfShape<Px>;
+    const int tid = (int)threadIdx.x;
+    const uint8_t *src = KARG_OF(LfTileArgs, src, g.p);
 #pragma unroll
-    for (int j = 0; j < NS; j++) {
+    for (int j = 0; j < S::NS; j++) {
         const int i = tid + kLfThreads * j;
-        const int r = i / VPR, c = (i % VPR) * VPX;
-        const int y = y0 - 12 + r, x = x0 - 16 + c;
+        const int r = i / S::VPR, c = (i % S::VPR) * S::VPX;
+        const int y = g.y0 - 12 + r, x = g.x0 - 16 + c;
         sv[j] = make_uint4(0, 0, 0, 0);
-        if (i < kLfRows * VPR && y >= 0 && y < ph && x >= 0 && x < pw)
-            sv[j] = *reinterpret_cast<const uint4 *>(src + (int64_t)y * st + (int64_t)x * sizeof(Px));
+        if (i < kLfRows * S::VPR && y >= 0 && y < g.ph && x >= 0 && x < g.pw)
+            sv[j] = *reinterpret_cast<const uint4 *>(src + (int64_t)y * g.st + (int64_t)x * sizeof(Px));
     }
+}
+template <typename Px>
+__device__ __forceinline__ void lf_fetch_edges(const LfTileArgs &a, const LfTile &g, LfEdgeRaw (&raw)[LfShape<Px>::NU]) {
+    using S = LfShape<Px>;
+    const int tid = (int)threadIdx.x;
     // Edge units. The outermost edge of each direction (k = 0, 18) reaches the tile only
     // with the 16-wide filter (it writes e-6 .. e+5); narrower ones are skipped there.
-    const int ux0 = (x0 >> 2) - 1, uy0 = (y0 >> 2) - 3;   // unit of the first edge / staged row
-    LfEdgeRaw raw[NU];
+    const int ux0 = (g.x0 >> 2) - 1, uy0 = (g.y0 >> 2) - 3;   // unit of the first edge / staged row
 #pragma unroll
-    for (int j = 0; j < NU; j++) {
+    for (int j = 0; j < S::NU; j++) {
         const int i = tid + kLfThreads * j;
-        const bool v = i < NV;
-        const int u = v ? i : i - NV;
+        const bool v = i < S::NV;
+        const int u = v ? i : i - S::NV;
         raw[j].bit = 0;
-#ifdef MI_LF_NOFETCH
-        if (0)
-#else
-        if (i < NV + NH)
-#endif
-            raw[j] = v ? lf_edge_fetch(a, p, 0, ux0 + u % kLfEdgesV, uy0 + u / kLfEdgesV)
-                       : lf_edge_fetch(a, p, 1, (x0 >> 2) + u % (kLfTW / 4), (y0 >> 2) - 1 + u / (kLfTW / 4));
+        if (i < S::NV + S::NH)
+            raw[j] = v ? lf_edge_fetch(a, g.p, 0, ux0 + u % kLfEdgesV, uy0 + u / kLfEdgesV)
+                       : lf_edge_fetch(a, g.p, 1, (g.x0 >> 2) + u % (kLfTW / 4), (g.y0 >> 2) - 1 + u / (kLfTW / 4));
     }
+}
+
+
+template <typename Px>
+__device__ __forceinline__ void lf_fetch(const LfTileArgs &a, const LfTile &g, uint4 (&sv)[LfShape<Px>::NS],
+                                         LfEdgeRaw (&raw)[LfShape<Px>::NU]) {
+    lf_fetch_pixels<Px>(a, g, sv);
+    lf_fetch_edges<Px>(a, g, raw);
+}
+
+template <typename Px>
+__device__ __forceinline__ void lf_commit_pixels(Px *t, const uint4 (&sv)[LfShape<Px>::NS]) {
+    using S = LfShape<Px>;
+    const int tid = (int)threadIdx.x;
 #pragma unroll
-    for (int j = 0; j < NS; j++) {
+    for (int j = 0; j < S::NS; j++) {
         const int i = tid + kLfThreads * j;
-        if (i < kLfRows * VPR) *reinterpret_cast<uint4 *>(&t[(i / VPR) * P + (i % VPR) * VPX]) = sv[j];
+        if (i < kLfRows * S::VPR) *reinterpret_cast<uint4 *>(&t[(i / S::VPR) * S::P + (i % S::VPR) * S::VPX]) = sv[j];
     }
-    KTL(1);
+}
+
+// Decode the edge units and bucket the filtered ones by width class (cnt[] zeroed and visible)
+template <typename Px>
+__device__ __forceinline__ void lf_build_lists(const LfTile &g, const LfEdgeRaw (&raw)[LfShape<Px>::NU],
+                                               uint16_t (*listv)[LfShape<Px>::NV], uint16_t (*listh)[LfShape<Px>::NH], int *cnt) {
+    using S = LfShape<Px>;
+    const int tid = (int)threadIdx.x;
+    const int ux0 = (g.x0 >> 2) - 1;
 #pragma unroll
-    for (int j = 0; j < NU; j++) {
+    for (int j = 0; j < S::NU; j++) {
         const int i = tid + kLfThreads * j;
-        const bool v = i < NV;
-        const int u = v ? i : i - NV;
+        const bool v = i < S::NV;
+        const int u = v ? i : i - S::NV;
         const int k = v ? u % kLfEdgesV : u / (kLfTW / 4);
         const int code = v ? lf_edge_decode(raw[j], 0, ux0 + k, 0)
-                           : lf_edge_decode(raw[j], 1, 0, (y0 >> 2) - 1 + k);
+                           : lf_edge_decode(raw[j], 1, 0, (g.y0 >> 2) - 1 + k);
         const int wd = code >> 8;
         if (!wd || ((k == 0 || k == (v ? kLfEdgesV : kLfEdgesH) - 1) && wd != 16)) continue;
         const int c = lf_class(wd);
         const int slot = atomicAdd(&cnt[(v ? 0 : 4) + c], 1);
-        const int N = v ? NV : NH;
+        const int N = v ? S::NV : S::NH;
         (v ? listv[c >> 1] : listh[c >> 1])[c & 1 ? N - 1 - slot : slot] = (uint16_t)((u << 6) | (code & 63));
     }
+}
+
+template <typename Px>
+__device__ __forceinline__ void lf_store_tile(const LfTile &g, const Px *t) {
+    using S = LfShape<Px>;
+    const int tid = (int)threadIdx.x;
+    uint8_t *dst = KARG_OF(LfTileArgs, dst, g.p);
+    static_assert((kLfTH * S::VPT) % kLfThreads == 0, "whole store rounds");
+#pragma unroll
+    for (int j = 0; j < kLfTH * S::VPT / kLfThreads; j++) {
+        const int i = tid + kLfThreads * j;
+        const int r = i / S::VPT, c = (i % S::VPT) * S::VPX;
+        const int y = g.y0 + r, x = g.x0 + c;
+        if (y < g.ph && x < g.pw)
+            *reinterpret_cast<uint4 *>(dst + (int64_t)y * g.st + (int64_t)x * sizeof(Px)) =
+                *reinterpret_cast<const uint4 *>(&t[(12 + r) * S::P + 16 + c]);
+    }
+}
+
+template <typename Px>
+__global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
+    using S = LfShape<Px>;
+    __shared__ __attribute__((aligned(16))) Px t[kLfRows * S::P];
+    // work lists: active edge units bucketed by width class, so that the lanes of a wave run
+    // one filter branch; entry = (unit index << 6) | L
+    __shared__ uint16_t listv[2][S::NV], listh[2][S::NH];
+    __shared__ int cnt[8];
+    __shared__ uint8_t le[64], li[64];
+    const int tid = threadIdx.x;
+    KTL(0);
+    if (tid < 64) { le[tid] = a.lim_e[tid]; li[tid] = a.lim_i[tid]; }
+    if (tid < 8) cnt[tid] = 0;
+    const LfTile g = lf_tile_at(a, xcd_block(blockIdx.x, gridDim.x));
+    __syncthreads();
+    uint4 sv[S::NS];
+    LfEdgeRaw raw[S::NU];
+    lf_fetch<Px>(a, g, sv, raw);
+    lf_commit_pixels<Px>(t, sv);
+    KTL(1);
+    lf_build_lists<Px>(g, raw, listv, listh, cnt);
     __syncthreads();
     KTL(2);
     // column edges, then row edges, one loop per width class
-#if !defined(MI_LF_NOFILTER)
-    lf_dir_pk<true, Px, P>(t, listv, cnt, le, li, a.bdm8, a.bdmax);
+    lf_dir_pk<true, Px, S::P>(t, listv, cnt, le, li, a.bdm8, a.bdmax);
     __syncthreads();
     KTL(3);
-    lf_dir_pk<false, Px, P>(t, listh, cnt + 4, le, li, a.bdm8, a.bdmax);
-#endif
+    lf_dir_pk<false, Px, S::P>(t, listh, cnt + 4, le, li, a.bdm8, a.bdmax);
     __syncthreads();
     KTL(4);
-    uint8_t *dst = KARG_OF(LfTileArgs, dst, p);
-    constexpr int VPT = kLfTW / VPX;
-    for (int i = tid; i < kLfTH * VPT; i += kLfThreads) {
-        const int r = i / VPT, c = (i % VPT) * VPX;
-        const int y = y0 + r, x = x0 + c;
-        if (y < ph && x < pw)
-            *reinterpret_cast<uint4 *>(dst + (int64_t)y * st + (int64_t)x * sizeof(Px)) =
-                *reinterpret_cast<const uint4 *>(&t[(12 + r) * P + 16 + c]);
-    }
+    lf_store_tile<Px>(g, t);
     KTL(5);
 }
 
 int launch_deblock_tiles(const LfTileArgs &a, int bpc, hipStream_t s) {
     const int n = a.tile_start[3];
     if (!n) return 0;
-    if (bpc == 8) hipLaunchKernelGGL(lf_tile_kernel<uint8_t>, dim3(n), dim3(kLfThreads), 0, s, a);
-    else hipLaunchKernelGGL(lf_tile_kernel<uint16_t>, dim3(n), dim3(kLfThreads), 0, s, a);
+    const int grid = n;
+    if (bpc == 8) hipLaunchKernelGGL(lf_tile_kernel<uint8_t>, dim3(grid), dim3(kLfThreads), 0, s, a);
+    else hipLaunchKernelGGL(lf_tile_kernel<uint16_t>, dim3(grid), dim3(kLfThreads), 0, s, a);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
