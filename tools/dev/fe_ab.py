@@ -1,5 +1,6 @@
 """A/B of two front-end libraries (MI_DEC_LIB) on stream decode time, interleaved runs in fresh
-processes: python tools/dev/fe_ab.py LIB_A LIB_B NAME[,NAME..] [REPS] [THREADS]"""
+processes: python tools/dev/fe_ab.py LIB_A LIB_B NAME[,NAME..] [REPS] [THREADS]
+(LOOKAHEAD=0 in the environment: one temporal unit at a time, as bench.py's unpipelined pass)"""
 import json
 import os
 import statistics
@@ -17,9 +18,10 @@ G = "tests/golden/streams"; V = {v["name"]: v for v in json.load(open(G + "/vect
 out = {}
 for name in sys.argv[1].split(","):
     data = open(os.path.join(G, V[name]["file"]), "rb").read()
-    sum(1 for e in stream_events(data, int(sys.argv[2])))
+    la = None if os.environ.get("LOOKAHEAD") is None else int(os.environ["LOOKAHEAD"])
+    sum(1 for e in stream_events(data, int(sys.argv[2]), lookahead=la))
     t = time.perf_counter()
-    sum(1 for e in stream_events(data, int(sys.argv[2])))
+    sum(1 for e in stream_events(data, int(sys.argv[2]), lookahead=la))
     out[name] = (time.perf_counter() - t) * 1e3
 print(json.dumps(out))
 '''
