@@ -18,7 +18,7 @@ G = "tests/golden/streams"; V = {v["name"]: v for v in json.load(open(G + "/vect
 out = {}
 for name in sys.argv[1].split(","):
     data = open(os.path.join(G, V[name]["file"]), "rb").read()
-    la = None if os.environ.get("LOOKAHEAD") is None else int(os.environ["LOOKAHEAD"])
+    la = int(os.environ["LOOKAHEAD"]) if os.environ.get("LOOKAHEAD") else None
     sum(1 for e in stream_events(data, int(sys.argv[2]), lookahead=la))
     t = time.perf_counter()
     sum(1 for e in stream_events(data, int(sys.argv[2]), lookahead=la))
