@@ -104,7 +104,8 @@ typedef struct MiCdef {
 
 /* The order mi_cdef_frame's workgroups run best in: the 64x64 units by descending cost (a
  * primary strength: direction search and filter; a secondary strength only; nothing to filter:
- * a copy), longest first. A host call on a host copy of the Av1Filter array for a w x h
+ * a copy), longest first, each class dealt to the 8 XCDs in contiguous picture runs (workgroup
+ * b runs on XCD b % 8) so that neighbouring units share an L2. A host call on a host copy of the Av1Filter array for a w x h
  * picture: writes the unit indices into `order` (capacity n) and returns their count, or
  * -EINVAL. */
 int mi_cdef_tile_order(const MiAv1Filter *masks_host, int w, int h, int layout, const MiCdef *cdef, int32_t *order,
