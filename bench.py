@@ -874,15 +874,24 @@ def replicas(args, world, rank, local, hw):
         return run
     step_fn = step_k(args.inflight)
     if args.graph:
-        # the step's launches captured once into a HIP graph (the C-ABI calls only enqueue
-        # kernels on the stream they are given), replayed per step
-        graph, cap = torch.cuda.CUDAGraph(), torch.cuda.Stream()
+        # the step's launches captured into HIP graphs (the C-ABI calls only enqueue kernels on
+        # the stream they are given), one graph per arena of the coefficient ring, replayed in
+        # ring order: every step still reads a fresh arena
+        cap = torch.cuda.Stream()
         cap.wait_stream(stream)
-        with torch.cuda.graph(graph, stream=cap):
-            for pk, _ in pipes[:args.inflight]:
-                pk.step(cap)
+        graphs = []
+        for _ in range(len(pipe.coefs)):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=cap):
+                for pk, _ in pipes[:args.inflight]:
+                    pk.step(cap)
+            graphs.append(g)
         hw.sync()
-        step_fn = graph.replay
+        gi = [0]
+
+        def step_fn():
+            graphs[gi[0] % len(graphs)].replay()
+            gi[0] += 1
         for _ in range(args.warmup):
             step_fn()
         hw.sync()
