@@ -2089,12 +2089,12 @@ int FrameDec::init_frame() {
         S->a_tx_lpf_end[1].assign(h.tiling.rows, std::vector<uint8_t>());
         for (int p = 0; p < 3; p++) S->owner[p].assign((size_t)owner_stride * (sb128h * 32 + 32), -1);
         if (h.allow_intrabc || inter_frame) {
-            RefMvBlock none{};
-            none.mv[0] = kInvalidMv;
-            none.ref[0] = -1;
-            none.ref[1] = -1;
-            S->rmv.assign((size_t)rmv_stride * (sb128h * 32 + 16), none);
-            S->f2d_map.assign(S->rmv.size(), 0);
+            // the refmvs blocks and their filter map are read only where this frame wrote them
+            // (above / left neighbours inside the tile, as refmvs.rs reads its rows), so they are
+            // not reset: decoding every reference vector with both filled with garbage instead
+            // is MD5-exact
+            S->rmv.reset((size_t)rmv_stride * (sb128h * 32 + 16));
+            S->f2d_map.reset(S->rmv.size());
         }
     }
     segmap.bind(*S->segmap);

@@ -43,6 +43,29 @@ struct Span {
         p = v.data();
         n = v.size();
     }
+    template <typename B>
+    void bind(B &v) {
+        p = v.data();
+        n = v.size();
+    }
+};
+
+// An array of a plain type left uninitialised: for maps whose entries are only read where the
+// frame has written them
+template <typename T>
+class RawBuf {
+public:
+    void reset(size_t n) {
+        if (n != n_) p_.reset(n ? new T[n] : nullptr);
+        n_ = n;
+    }
+    void clear() { reset(0); }
+    T *data() { return p_.get(); }
+    size_t size() const { return n_; }
+
+private:
+    std::unique_ptr<T[]> p_;
+    size_t n_ = 0;
 };
 
 // The per-4x4 / per-8x8 maps of a frame that every tile decoder of it reads and writes (within
@@ -53,8 +76,8 @@ struct FrameShared {
     std::vector<uint8_t> tx_lpf_right[2];
     std::vector<std::vector<uint8_t>> a_tx_lpf_end[2];
     std::vector<int32_t> owner[3];
-    std::vector<RefMvBlock> rmv;
-    std::vector<uint8_t> f2d_map;
+    RawBuf<RefMvBlock> rmv;       // (read only where written: no reset value)
+    RawBuf<uint8_t> f2d_map;
     std::vector<TmvBlock> rp_proj;
     std::shared_ptr<std::vector<TmvBlock>> rp;
 };
