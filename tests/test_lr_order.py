@@ -90,3 +90,38 @@ def test_cdef_order_is_a_permutation_costliest_first(layout):
     last_prim = max((i for i, t in enumerate(o) if prim(t)), default=-1)
     first_none = min((i for i, t in enumerate(o) if none(t)), default=len(o))
     assert last_prim < first_none
+
+
+def test_cdef_order_deals_each_class_to_xcds_in_runs():
+    """Within a cost class, the units workgroup b % 8 == x takes (XCD x) are one increasing,
+    contiguous run of that class's units in picture order, and the runs follow XCD order."""
+    w, h = 1920, 1080
+    _, lf = frame(w, h, 8, 1, 11)
+    cd = add_cdef_meta(lf, np.random.default_rng(12))
+    o = cdef_order_of(w, h, 1, lf, cd)
+    assert isinstance(o, np.ndarray) and np.array_equal(np.sort(o), np.arange(len(o)))
+    m = lf["masks"]
+    tx = (w + 63) // 64
+
+    def cls(t):   # (mi_cdef_tile_order's classes: 2 a primary strength, 1 secondary only, 0 none)
+        x, y = t % tx, t // tx
+        sb = m[y >> 1, x >> 1]
+        idx = int(sb["cdef_idx"][(y & 1) * 2 + (x & 1)])
+        if idx < 0:
+            return 0
+        yl, uvl = int(cd["y_strength"][idx]), int(cd["uv_strength"][idx])
+        if not yl and not uvl:
+            return 0
+        rows = sb["noskip_mask"][8 * (y & 1):8 * (y & 1) + 8]
+        if not any(((int(r[1]) << 16 | int(r[0])) >> (16 * (x & 1))) & 0xffff for r in rows):
+            return 0
+        return 2 if (yl >> 2 or uvl >> 2) else 1
+
+    c = np.array([cls(int(t)) for t in o])
+    assert np.all(np.diff(c) <= 0), "classes costliest first"
+    for k in np.unique(c):
+        pos = np.nonzero(c == k)[0]
+        items = sorted(int(t) for t in o[pos])   # the class's units in picture order
+        runs = [[int(o[p]) for p in pos if p % 8 == x] for x in range(8)]
+        flat = [t for r in runs for t in r]
+        assert flat == items, "XCD x holds the x-th contiguous run of the class"
