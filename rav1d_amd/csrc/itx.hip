@@ -160,6 +160,14 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
         bk[rd] = b;
         vk[rd] = valid;
     }
+#ifdef MI_KTL
+    {
+        // (timeline builds) the first descriptor's arrival: every load above is already issued
+        const unsigned d0 = bk[0].coef_off;
+        asm volatile("" ::"v"(d0));
+        KTL(1);
+    }
+#endif
 
     int row_lo, col_lo;
     if constexpr (sizeof(Px) == 1) { row_lo = -32768; col_lo = -32768; }
@@ -221,7 +229,7 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
         }
     }
     __syncthreads();
-    if (rd == 0) KTL(1);
+    if (rd == 0) KTL(2);
 
     // ---- 3. column pass: residual back into LDS (rows >= SH are reused as needed) ----
     int colres[Ht];
