@@ -108,6 +108,13 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
         bs = KARG(band_start, TX * 9 + q);
         be = KARG(band_start, TX * 9 + q + 1);
     }
+#ifdef MI_KTL
+    {
+        // (timeline builds) the block range known: the kernel-argument reads are done
+        asm volatile("" ::"s"(bs), "s"(be));
+        KTL(3);
+    }
+#endif
     // per-plane arguments as locals (selected by value, never by address into the kernarg)
     uint8_t *const plane3[3] = { a.plane[0], a.plane[1], a.plane[2] };
     const int64_t stride3[3] = { a.stride[0], a.stride[1], a.stride[2] };
