@@ -781,8 +781,9 @@ def parse_args(argv):
                     help="frames reconstructed concurrently per GPU, each on its own HIP stream and context "
                          "(rav1d's frame threads, n_fc): a step is then that many frames")
     ap.add_argument("--graph", type=int, default=0, help="1: replay the step as one captured HIP graph")
-    ap.add_argument("--two-in-flight", action="store_true",
-                    help="also time two independent frames per step on two streams (two_frames_in_flight)")
+    ap.add_argument("--two-in-flight", action=argparse.BooleanOptionalAction, default=True,
+                    help="also time two independent frames per step on two streams (two_frames_in_flight; "
+                         "reported beside the headline, never as `value`)")
     ap.add_argument("--stagger", type=int, default=0, help="with --inflight > 1: frame k's MC waits for frame k-1's")
     ap.add_argument("--mv", choices=["uniform", "coherent"], default="uniform",
                     help="motion field of the timed frame (uniform: SURVEY.md 8(d) config 3)")
