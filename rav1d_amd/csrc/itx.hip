@@ -329,6 +329,13 @@ __global__ __launch_bounds__(kItxThreads, 4) void itx_frame_kernel(ItxArgs a) {
         if (wg >= KARG(wg_start, k)) i = k;
     const int s = KARG(wg_size, i);
     const int lwg = wg - KARG(wg_start, i);
+#ifdef MI_KTL
+    {
+        // (timeline builds) the size known, before the jump into its path
+        asm volatile("" ::"s"(s), "s"(lwg));
+        KTL(4);
+    }
+#endif
     switch (s) {
 #define CASE(n) case n: itx_size<n, Px, Cf, Lt, Wide>(a, lwg, lds); break;
         CASE(0) CASE(1) CASE(2) CASE(5) CASE(6) CASE(7) CASE(8) CASE(13) CASE(14)
