@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 
 from rav1d_amd import ITX_KEEP_COEFS  # noqa: E402
 from rav1d_amd import frame as F  # noqa: E402
-from rav1d_amd.synth import frame_bytes, itx_algorithmic_bytes, itx_band_order, make_frame, mc_algorithmic_bytes  # noqa: E402
+from rav1d_amd.synth import frame_bytes, itx_algorithmic_bytes, itx_band_order, make_frame, mc_algorithmic_bytes, mc_sync_ok  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 W, H, BPC, LAYOUT = 3840, 2160, 10, 1
@@ -63,6 +63,9 @@ class Pipeline:
                 self.refs.append(r)
             self.mc = F.McMeta(*fr["mc"])
             self.ref_pics = (F.MiPicture * len(self.refs))(*[r.picture() for r in self.refs])
+            # one grid, the chroma units of SEG blocks waiting in-launch for their luma mask
+            # (mi_mc_frame_sync, as the frame executor runs it when the offsets allow)
+            self.mc_sync = mc_sync_ok(fr["mc"][0])
         self.blocks = torch.from_numpy(fr["blocks"].view(np.uint8).copy()).cuda()
         # itx over picture bands, one XCD per band (mi_itx_frame_banded, as the frame executor runs it)
         ah = (h + 127) & ~127
@@ -95,8 +98,9 @@ class Pipeline:
         }
         if self.mc is not None:
             self.algo["mc"] = mc_algorithmic_bytes(fr["mc"][0], bpc) + fr["mc"][2].nbytes
-        # kernel launches per stage per frame: mc = luma + chroma group
-        self.launches = {"mc": 2, "itx": 1, "deblock": 1, "cdef": 1, "lr": 1, "fg": 1}
+        # kernel launches per stage per frame: mc = one grid (mi_mc_frame_sync), or luma + chroma group
+        self.launches = {"mc": 1 if self.mc is not None and self.mc_sync else 2, "itx": 1, "deblock": 1, "cdef": 1,
+                         "lr": 1, "fg": 1}
         self.kernels = {"mc": "mc_kernel", "itx": "itx_frame_kernel", "deblock": "lf_tile_kernel",
                         "cdef": "cdef_kernel", "lr": "lr_kernel", "fg": "fg_apply_kernel"}
 
@@ -129,7 +133,12 @@ class Pipeline:
             else:
                 fn()
 
-        if self.mc is not None:
+        if self.mc is not None and self.mc_sync:
+            timed("mc", lambda: F.check(lib.mi_mc_frame_sync(ctx, ctypes.byref(pa), self.ref_pics, len(self.refs),
+                                                             ctypes.c_void_p(self.mc.blocks.data_ptr()), self.mc.class_start,
+                                                             ctypes.c_void_p(self.mc.masks.data_ptr()), self.mc.masks.numel(),
+                                                             None, sp), "mc"))
+        elif self.mc is not None:
             timed("mc", lambda: F.check(lib.mi_mc_frame(ctx, ctypes.byref(pa), self.ref_pics, len(self.refs),
                                                         ctypes.c_void_p(self.mc.blocks.data_ptr()), self.mc.class_start,
                                                         ctypes.c_void_p(self.mc.masks.data_ptr()), None, sp), "mc"))

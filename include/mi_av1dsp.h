@@ -426,6 +426,20 @@ int mi_mc_frame(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nre
 int mi_mc_frame_ex(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
                    const MiMcBlock *blocks, const uint32_t class_start[2 * MI_MC_NCLASS + 1],
                    uint8_t *masks, int16_t *tmp, unsigned flags, void *stream);
+/* mi_mc_frame as one grid whatever the units: a chroma MASK unit whose mask a SEG unit of the
+ * same call writes carries MI_MC_AFTER_SEG in `param` (bit 6) and waits inside the launch for
+ * that SEG unit's tiles (they publish the mask with agent-scope word stores and a flag per
+ * tile; the luma waves precede the chroma ones in the grid, so a waiting wave only waits for
+ * waves already started). SEG and MASK mask offsets must be multiples of 16 and mask_bytes
+ * the size of the mask buffer. A wait that does not end reports -EIO from
+ * mi_mc_sync_status. */
+#define MI_MC_AFTER_SEG 0x40u
+int mi_mc_frame_sync(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
+                     const MiMcBlock *blocks, const uint32_t class_start[2 * MI_MC_NCLASS + 1],
+                     uint8_t *masks, size_t mask_bytes, int16_t *tmp, void *stream);
+/* 0, or -EIO when a hand-off wait of an earlier mi_mc_frame_sync on the context timed out
+ * (synchronises the context's stream; clears the status) */
+int mi_mc_sync_status(MiCtx *ctx, void *stream);
 /* OBMC: the caller runs mi_mc_frame a second time with the above-neighbour laps
  * (MI_MC_OBMC_H units) and a third time with the left-neighbour laps (MI_MC_OBMC_V), as
  * obmc() blends above before left. `tmp` (device, int16) receives MI_MC_PREP units; may be

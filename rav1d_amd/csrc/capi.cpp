@@ -249,6 +249,58 @@ int mi_mc_frame_ex(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int 
     return r ? fail(ctx, -EIO) : 0;
 }
 
+int mi_mc_frame_sync(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
+                     const MiMcBlock *blocks, const uint32_t class_start[2 * MI_MC_NCLASS + 1], uint8_t *masks,
+                     size_t mask_bytes, int16_t *tmp, void *stream) {
+    if (!ctx || !cur || !class_start) return fail(ctx, -EINVAL);
+    for (int k = 0; k < 2 * MI_MC_NCLASS; k++)
+        if (class_start[k] > class_start[k + 1]) return fail(ctx, -EINVAL);
+    mi::McArgs a;
+    if (int e = fill_mc_args(a, cur, refs, nrefs, true)) return fail(ctx, e);
+    if (class_start[2 * MI_MC_NCLASS] == class_start[0]) return 0;
+    if (!blocks || !nrefs || (mask_bytes && !masks)) return fail(ctx, -EINVAL);
+    a.blocks = blocks;
+    a.masks = masks;
+    a.tmp = tmp;
+    memcpy(a.class_start, class_start, sizeof(a.class_start));
+    const int w0 = mi::mc_plan(a, 0), w1 = mi::mc_plan(a, 1);
+    if (w0 < 0 || w1 < 0) return fail(ctx, -EINVAL);
+    hipStream_t s = (hipStream_t)stream;
+    // the tile flags: 32 per 16 mask bytes (a SEG unit has at most 32 tiles), zeroed when
+    // allocated and never reset (each call has its own epoch)
+    const size_t nf = (mask_bytes / 16 + 1) * 32;
+    if (nf > ctx->mc_flags_n) {
+        if (ctx->mc_flags) (void)hipFree(ctx->mc_flags);
+        ctx->mc_flags = nullptr;
+        ctx->mc_flags_n = 0;
+        if (hipMalloc(&ctx->mc_flags, nf * sizeof(uint32_t)) != hipSuccess) return fail(ctx, -ENOMEM);
+        if (hipMemsetAsync(ctx->mc_flags, 0, nf * sizeof(uint32_t), s) != hipSuccess) return fail(ctx, -EIO);
+        ctx->mc_flags_n = nf;
+    }
+    if (!ctx->mc_err) {
+        if (hipMalloc(&ctx->mc_err, sizeof(int)) != hipSuccess) return fail(ctx, -ENOMEM);
+        if (hipMemsetAsync(ctx->mc_err, 0, sizeof(int), s) != hipSuccess) return fail(ctx, -EIO);
+    }
+    if (++ctx->mc_epoch == 0) ctx->mc_epoch = 1;
+    a.seg_flags = ctx->mc_flags;
+    a.seg_epoch = ctx->mc_epoch;
+    a.err = ctx->mc_err;
+    // one grid, the luma group's waves first (see mi_av1dsp.h)
+    const int r = w0 && w1 ? mi::launch_mc(a, 2, w0 + w1, s) : mi::launch_mc(a, w0 ? 0 : 1, w0 ? w0 : w1, s);
+    return r ? fail(ctx, -EIO) : 0;
+}
+
+int mi_mc_sync_status(MiCtx *ctx, void *stream) {
+    if (!ctx) return -EINVAL;
+    if (!ctx->mc_err) return 0;
+    int e = 0;
+    if (hipMemcpyAsync(&e, ctx->mc_err, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+        hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+        return fail(ctx, -EIO);
+    if (e && hipMemsetAsync(ctx->mc_err, 0, sizeof(int), (hipStream_t)stream) != hipSuccess) return fail(ctx, -EIO);
+    return e ? fail(ctx, -EIO) : 0;
+}
+
 int mi_mc_scaled(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
                  const MiMcBlock *blocks, int n, int16_t *tmp, void *stream) {
     if (!ctx || !cur || n < 0) return fail(ctx, -EINVAL);
@@ -369,6 +421,14 @@ int mi_intra_recon(MiCtx *ctx, const MiIntraFrame *frames, int nframes, unsigned
 int mi_ctx_device_status(MiCtx *ctx, void *stream) {
     if (!ctx) return -EINVAL;
     if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(ctx, -EIO);
+    if (ctx->mc_err) {   // a one-grid MC hand-off wait gave up (mi_mc_frame_sync)
+        int e = 0;
+        if (hipMemcpy(&e, ctx->mc_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return fail(ctx, -EIO);
+        if (e) {
+            if (hipMemset(ctx->mc_err, 0, sizeof(int)) != hipSuccess) return fail(ctx, -EIO);
+            return fail(ctx, -ETIMEDOUT);
+        }
+    }
     if (!ctx->ir_words) return 0;
     int w[66];
     if (hipMemcpy(w, ctx->ir_words, sizeof(w), hipMemcpyDeviceToHost) != hipSuccess) return fail(ctx, -EIO);

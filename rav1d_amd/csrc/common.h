@@ -215,6 +215,12 @@ struct McArgs {
     int seg_ss_hor, seg_ss_ver;      // w_mask[chr_layout_idx] subsampling of the SEG mask
     uint32_t class_start[2 * MI_MC_NCLASS + 1];
     uint32_t first_wave[2][MI_MC_NCLASS + 1];
+    // one grid with in-launch hand-off (mi_mc_frame_sync): a SEG unit's tiles publish their
+    // mask with `sc1` word stores and set seg_flags[(mask_off >> 4) * 32 + tile] = seg_epoch;
+    // chroma MASK units flagged MI_MC_AFTER_SEG wait for them (null: no hand-off)
+    uint32_t *seg_flags;
+    uint32_t seg_epoch;
+    int *err;
 };
 // launchers (mc.hip): mc_plan fills first_wave[g] and returns the wave count of group g
 int mc_plan(McArgs &a, int g);

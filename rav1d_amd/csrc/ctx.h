@@ -22,6 +22,12 @@ struct MiCtx {
     size_t ir_gran_n = 0;
     unsigned long long *ir_tl = nullptr;     // MI_IR_TIMELINE stamps (diagnostics)
     size_t ir_tl_n = 0;
+    // one-grid MC with in-launch hand-off (mi_mc_frame_sync): per-tile flags of SEG masks,
+    // epoch (never reset: the flags hold old epochs), error word
+    uint32_t *mc_flags = nullptr;
+    size_t mc_flags_n = 0;
+    uint32_t mc_epoch = 0;
+    int *mc_err = nullptr;
     // frame executor (frame_exec.cpp): device copy of one frame's descriptors, staged through
     // pinned host memory; `fx_ev` marks when the staging buffer may be rewritten
     uint8_t *fx_dev = nullptr, *fx_host = nullptr;
@@ -48,6 +54,8 @@ struct MiCtx {
         if (fx_dev) (void)hipFree(fx_dev);
         if (fx_host) (void)hipHostFree(fx_host);
         if (ir_done) (void)hipFree(ir_done);
+        if (mc_flags) (void)hipFree(mc_flags);
+        if (mc_err) (void)hipFree(mc_err);
         if (ir_words) (void)hipFree(ir_words);
         if (ir_gran) (void)hipFree(ir_gran);
         if (ir_tl) (void)hipFree(ir_tl);

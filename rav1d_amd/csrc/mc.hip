@@ -57,6 +57,18 @@ __device__ __forceinline__ int f2d_type_v(int f) { return (int)((0x210210210ull 
 
 __device__ __forceinline__ uint32_t pack2(int lo, int hi) { return (uint32_t)(lo & 0xffff) | ((uint32_t)hi << 16); }
 
+// agent-scope (`sc1`) word access for the in-launch mask hand-off of mi_mc_frame_sync
+// (MI355X_MICROARCH.md's hand-off rules cover 4-B stores and loads, not bytes)
+typedef __attribute__((address_space(1))) uint32_t *mc_gp32;
+__device__ __forceinline__ void st_u32_sc1(uint8_t *q, uint32_t v) {
+    __hip_atomic_store((mc_gp32)q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_u8_sc1(const uint8_t *q) {
+    const uintptr_t ad = reinterpret_cast<uintptr_t>(q);
+    const uint32_t w = __hip_atomic_load((mc_gp32)(ad & ~(uintptr_t)3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (int)((w >> (8 * (ad & 3))) & 0xff);
+}
+
 // Shape-class geometry (all wave-uniform).
 struct ClassGeom {
     int w, h, TW, R, lanes_u, U, T, TR, ctiles;
@@ -195,7 +207,7 @@ __global__ __launch_bounds__(64, 1) void mc_kernel(McArgs a, int g) {
     }
 
     // this lane's unit, tile origin, column and rows
-    int uu, tx0 = 0, ty0 = 0, rg, col;
+    int uu, tx0 = 0, ty0 = 0, rg, col, tile = 0;
     uint32_t ui;
     if (G.T == 1) {
         uu = lane / G.lanes_u;
@@ -205,7 +217,7 @@ __global__ __launch_bounds__(64, 1) void mc_kernel(McArgs a, int g) {
         ui = cls_begin + (uint32_t)item * G.U + uu;
     } else {
         uu = 0;
-        const int tile = item % G.T;
+        tile = item % G.T;
         ui = cls_begin + (uint32_t)(item / G.T);
         tx0 = (tile % G.ctiles) * G.TW;
         ty0 = (tile / G.ctiles) * G.TR;
@@ -290,6 +302,32 @@ __global__ __launch_bounds__(64, 1) void mc_kernel(McArgs a, int g) {
     __syncthreads();
     KTL(1);
 
+    // mi_mc_frame_sync: a chroma MASK unit whose mask a SEG unit of this grid writes waits for
+    // every tile of that unit (the luma waves precede the chroma ones in the grid, so the waves
+    // waited for have started); lanes of the unit poll the tile flags in parallel
+    const bool after_seg = a.seg_flags && active && b.comp == MI_MC_MASK && (b.param & MI_MC_AFTER_SEG);
+    if (a.seg_flags && __any(after_seg)) {
+        int tl = 0;
+        if (after_seg) {
+            const int lw = b.w << ssh, lh = b.h << ssv;    // the producing (luma) SEG unit
+            tl = class_geom(((31 - __clz(lw)) << 3) | (31 - __clz(lh))).T;
+        }
+        const int li = G.T == 1 ? lane - uu * G.lanes_u : lane, nl = G.T == 1 ? G.lanes_u : 64;
+        const uint32_t *fl = a.seg_flags + (size_t)(b.mask_off >> 4) * 32;
+        bool ok = true;
+        for (unsigned spins = 0;; spins++) {
+            ok = true;
+            for (int t = li; t < tl; t += nl)
+                ok = ok && __hip_atomic_load(fl + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.seg_epoch;
+            if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+            if (spins > (1u << 20)) {
+                if (!ok) atomicOr(a.err, 1);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+
     // everything after staging runs with the rows per lane R as a compile-time constant
     // (min(h, 8) is wave-uniform): no per-row exec masking in the filters and epilogues
     auto finish = [&](auto RC) {
@@ -358,14 +396,26 @@ __global__ __launch_bounds__(64, 1) void mc_kernel(McArgs a, int g) {
                     o0[q] = min(max((t1 * m + t2 * (64 - m) + rnd) >> sh, 0), a.bdmax);
                     // neighbour column (lane ^ 1 holds column ^ 1 of the same rows)
                     const int mn = msh ? __shfl_xor(m, 1) : 0;
+                    // this lane's mask byte (-1: none at this row) and where it goes
+                    int v = -1, row = 0, cb = 0;
                     if (!msh) {
-                        mo[(yb + q) * mstride + xb] = (uint8_t)m;
+                        v = m; row = yb + q; cb = xb;
                     } else if (!msv) {
-                        if (!(col & 1)) mo[(yb + q) * mstride + (xb >> 1)] = (uint8_t)((m + mn + 1 - sign) >> 1);
+                        if (!(col & 1)) { v = (m + mn + 1 - sign) >> 1; row = yb + q; cb = xb >> 1; }
                     } else if (q & 1) {
-                        if (!(col & 1)) mo[((yb + q) >> 1) * mstride + (xb >> 1)] = (uint8_t)((mprev + m + mn + 2 - sign) >> 2);
+                        if (!(col & 1)) { v = (mprev + m + mn + 2 - sign) >> 2; row = (yb + q) >> 1; cb = xb >> 1; }
                     } else {
                         mprev = m + mn;
+                    }
+                    if (!a.seg_flags) {
+                        if (v >= 0) mo[row * mstride + cb] = (uint8_t)v;
+                    } else {
+                        // in-launch hand-off: four bytes of a row to one lane, one `sc1` word store
+                        const int st = msh ? 2 : 1;
+                        const int v1 = __shfl_down(v, st), v2 = __shfl_down(v, 2 * st), v3 = __shfl_down(v, 3 * st);
+                        if (v >= 0 && !(cb & 3))
+                            st_u32_sc1(mo + row * mstride + cb, (uint32_t)v | ((uint32_t)v1 << 8) | ((uint32_t)v2 << 16) |
+                                                                    ((uint32_t)v3 << 24));
                     }
                 }
             }
@@ -381,7 +431,8 @@ __global__ __launch_bounds__(64, 1) void mc_kernel(McArgs a, int g) {
                         const int wt = b.param & 31;
                         v = (o0[q] * wt + o1[q] * (16 - wt) + (8 << ib) + a.bias * 16) >> (ib + 4);
                     } else {
-                        const int m = mk[(ty0 + r0 + q) * b.w + tx0 + col];
+                        const uint8_t *mq = mk + (ty0 + r0 + q) * b.w + tx0 + col;
+                        const int m = after_seg ? ld_u8_sc1(mq) : *mq;
                         const int t1 = sign ? o1[q] : o0[q], t2 = sign ? o0[q] : o1[q];
                         v = (t1 * m + t2 * (64 - m) + (32 << ib) + a.bias * 64) >> (ib + 6);
                     }
@@ -397,6 +448,17 @@ __global__ __launch_bounds__(64, 1) void mc_kernel(McArgs a, int g) {
     if (G.R == 8) finish(std::integral_constant<int, 8>{});
     else if (G.R == 4) finish(std::integral_constant<int, 4>{});
     else finish(std::integral_constant<int, 2>{});
+    // mi_mc_frame_sync: a SEG unit's tile publishes its mask words (the wave drains its stores,
+    // then one lane per unit stores the tile's flag, agent scope)
+    const bool seg_unit = a.seg_flags && active && nref == 2 && b.comp == MI_MC_SEG;
+    if (a.seg_flags && __any(seg_unit)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const int li = G.T == 1 ? lane - uu * G.lanes_u : lane;
+        if (seg_unit && li == 0)
+            __hip_atomic_store(a.seg_flags + (size_t)(b.mask_off >> 4) * 32 + tile, a.seg_epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
     KTLV(6, c + (any2 ? 64 : 0));
     KTL(5);
 }

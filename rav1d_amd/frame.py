@@ -184,6 +184,16 @@ def mc_frame_one_grid(ctx, cur, refs, split, stream=None, tmp=None):
 MI_MC_ONE_GRID = 1
 
 
+def mc_frame_sync(ctx, cur, refs, meta, stream=None, tmp=None):
+    """mi_mc_frame_sync: one grid; chroma units flagged MI_MC_AFTER_SEG wait inside the launch
+    for the SEG unit that writes their mask."""
+    pics = (MiPicture * len(refs))(*[r.picture() for r in refs])
+    check(lib().mi_mc_frame_sync(ctx.h, ctypes.byref(cur.picture()), pics, len(refs),
+                                 ctypes.c_void_p(meta.blocks.data_ptr()), meta.class_start,
+                                 ctypes.c_void_p(meta.masks.data_ptr()), meta.masks.numel(), _dptr(tmp),
+                                 _stream_ptr(stream)), "mi_mc_frame_sync")
+
+
 def _dptr(t):
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
 

@@ -586,15 +586,29 @@ def make_mc_units(w, h, layout, rng, nrefs=2, compound_frac=0.3, mv_px=64, sb=64
             if cmp_ and comp == 2:          # chroma wedge: its own mask at chroma resolution
                 masks.append(rng.integers(0, 65, size=cw * ch).astype(np.uint8))
                 coff, moff = moff, moff + cw * ch
-            elif cmp_ and comp == 3:        # chroma of SEG: mask() with the luma-written mask
+            cparam = param
+            if cmp_ and comp == 3:          # chroma of SEG: mask() with the luma-written mask
                 ccomp = 2
+                cparam = param | MI_MC_AFTER_SEG   # (mi_mc_frame_sync waits for the SEG unit)
             for pl in (1, 2):
-                chroma.append(_mc_record(x >> ss_h, y >> ss_v, cw, ch, pl, f2d, mvs, refs, ccomp, param, coff))
+                chroma.append(_mc_record(x >> ss_h, y >> ss_v, cw, ch, pl, f2d, mvs, refs, ccomp, cparam, coff))
     units, class_start = mc_sort_units(np.array(luma + chroma, dtype=MCBLOCK_DTYPE))
     mask_buf = np.concatenate(masks) if masks else np.zeros(1, np.uint8)
     if mask_buf.size == 0:
         mask_buf = np.zeros(1, np.uint8)
     return units, class_start, mask_buf
+
+
+MI_MC_AFTER_SEG = 0x40   # include/mi_av1dsp.h: a chroma MASK unit reading a SEG mask of the call
+
+
+def mc_sync_ok(units):
+    """Whether mi_mc_frame_sync may run `units`: every SEG and MASK mask offset a multiple of
+    16 and every SEG unit at least 8 wide (a mask row of at least 4 bytes)."""
+    cmp_ = units["ref"][:, 1] >= 0
+    seg = cmp_ & (units["comp"] == 3)
+    msk = cmp_ & ((units["comp"] == 2) | seg)
+    return bool(((units["mask_off"][msk] % 16) == 0).all() and (units["w"][seg] >= 8).all() and (units["h"][seg] >= 8).all())
 
 
 def mc_class_of(units):

@@ -5,8 +5,9 @@ import numpy as np
 import pytest
 import torch
 
-from rav1d_amd.frame import Frame, McMeta, McSplitMeta, mc_frame, mc_frame_one_grid
-from rav1d_amd.synth import make_mc_grid_units, make_mc_units, make_texture
+from rav1d_amd import lib
+from rav1d_amd.frame import Frame, McMeta, McSplitMeta, _stream_ptr, mc_frame, mc_frame_one_grid, mc_frame_sync
+from rav1d_amd.synth import make_mc_grid_units, make_mc_units, make_texture, mc_sync_ok
 from tests import oracle_lib
 
 pytestmark = pytest.mark.gpu
@@ -23,12 +24,17 @@ def make_refs(w, h, bpc, layout, n, rng):
     return refs
 
 
-def run_case(gpu, w, h, bpc, layout, units, class_start, masks, refs, rng, one_grid=False):
+def run_case(gpu, w, h, bpc, layout, units, class_start, masks, refs, rng, one_grid=False, sync=False):
     cur = Frame(w, h, bpc, layout)
     init = [rng.integers(0, 1 << bpc, size=cur.buffer_np(p).shape) for p in range(len(cur.planes))]
     for p, a in enumerate(init):
         cur.set_buffer_np(p, a)
-    if one_grid:
+    if sync:
+        # mi_mc_frame_sync: one grid, chroma units of SEG blocks wait for their mask in-launch
+        meta = McMeta(units, class_start, masks)
+        mc_frame_sync(gpu, cur, refs, meta)
+        assert lib().mi_mc_sync_status(gpu.h, _stream_ptr(None)) == 0, "hand-off wait timed out"
+    elif one_grid:
         # mi_mc_frame_ex(MI_MC_ONE_GRID) + the chroma MASK units in a second call
         meta = McSplitMeta(units, masks)
         mc_frame_one_grid(gpu, cur, refs, meta)
@@ -124,3 +130,17 @@ def test_mc_4k10_matches_oracle(gpu):
     refs = make_refs(w, h, bpc, 1, 2, rng)
     units, ps, masks = make_mc_units(w, h, 1, rng)
     run_case(gpu, w, h, bpc, 1, units, ps, masks, refs, rng)
+
+
+@pytest.mark.parametrize("bpc", [8, 10])
+@pytest.mark.parametrize("layout", [1, 2, 3])
+@pytest.mark.parametrize("size", [(256, 192), (640, 384)])
+def test_mc_frame_sync_matches_oracle(gpu, bpc, layout, size):
+    """mi_mc_frame_sync (one grid, in-launch SEG mask hand-off) against the oracle, SEG masks
+    included, with half of the blocks compound."""
+    w, h = size
+    rng = np.random.default_rng(bpc * 13 + layout * 5 + w)
+    refs = make_refs(w, h, bpc, layout, 3, rng)
+    units, ps, masks = make_mc_units(w, h, layout, rng, nrefs=3, compound_frac=0.5, mv_px=40, min_bs=8)
+    assert mc_sync_ok(units)
+    run_case(gpu, w, h, bpc, layout, units, ps, masks, refs, rng, sync=True)

@@ -1,4 +1,4 @@
-"""One bench stage (STAGE=deblock|cdef|lr|itx) of the 4K10 bench frame, REPS times, for PMC
+"""One bench stage (STAGE=deblock|cdef|lr|itx|mc|mc_onegrid|mc_split|mc_sync) of the 4K10 bench frame, REPS times, for PMC
 passes (diagnostic). The pipeline runs once first so every input is the real one."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -22,6 +22,32 @@ cdef_grid = F.MiCdef.from_buffer_copy(pipe.cdef.s)
 cdef_grid.order = None
 sp = F._stream_ptr(s)
 pa, pb, po, pd = pipe.A.picture(), pipe.B.picture(), pipe.O.picture(), pipe.D.picture()
+def mc(p, flags=0):
+    F.check(L.mi_mc_frame_ex(ctx.h, ctypes.byref(pa), pipe.ref_pics, len(pipe.refs), ctypes.c_void_p(pipe.mc.blocks.data_ptr()),
+                             pipe.mc.class_start, ctypes.c_void_p(pipe.mc.masks.data_ptr()), None, flags, p), "mc")
+
+
+def mc_sync(p):
+    F.check(L.mi_mc_frame_sync(ctx.h, ctypes.byref(pa), pipe.ref_pics, len(pipe.refs), ctypes.c_void_p(pipe.mc.blocks.data_ptr()),
+                               pipe.mc.class_start, ctypes.c_void_p(pipe.mc.masks.data_ptr()), pipe.mc.masks.numel(), None, p),
+            "mc sync")
+
+
+split = None
+
+
+def mc_split(p):
+    """the caller-side split: luma + independent chroma in one grid, the chroma MASK units after"""
+    global split
+    if split is None:
+        split = F.McSplitMeta(fr["mc"][0], fr["mc"][2])
+    F.check(L.mi_mc_frame_ex(ctx.h, ctypes.byref(pa), pipe.ref_pics, len(pipe.refs), ctypes.c_void_p(split.a.blocks.data_ptr()),
+                             split.a.class_start, ctypes.c_void_p(split.masks.data_ptr()), None, 1, p), "mc a")
+    if split.b.n:
+        F.check(L.mi_mc_frame(ctx.h, ctypes.byref(pa), pipe.ref_pics, len(pipe.refs), ctypes.c_void_p(split.b.blocks.data_ptr()),
+                              split.b.class_start, ctypes.c_void_p(split.masks.data_ptr()), None, p), "mc b")
+
+
 def itx(p):
     F.check(L.mi_itx_frame_banded(ctx.h, ctypes.byref(pa), ctypes.c_void_p(pipe.blocks.data_ptr()), pipe.itx_bands,
                                   ctypes.c_void_p(pipe.coefs[0].data_ptr()), bench.ITX_KEEP_COEFS, p), "itx")
@@ -30,6 +56,14 @@ def itx(p):
 for _ in range(int(os.environ.get("REPS", "10"))):
     if st == "itx":
         itx(sp)
+    elif st == "mc":
+        mc(sp)
+    elif st == "mc_onegrid":   # (timing only: chroma units that read a luma SEG mask race with it)
+        mc(sp, 1)
+    elif st == "mc_split":
+        mc_split(sp)
+    elif st == "mc_sync":
+        mc_sync(sp)
     elif st == "deblock":
         F.check(L.mi_deblock_frame_to(ctx.h, ctypes.byref(pa), ctypes.byref(pd), ctypes.byref(pipe.lf.s), sp), "lf")
     elif st == "cdef":
@@ -50,6 +84,14 @@ if os.environ.get("TIME"):
         p = F._stream_ptr(stream)
         if st == "itx":
             itx(p)
+        elif st == "mc":
+            mc(p)
+        elif st == "mc_onegrid":
+            mc(p, 1)
+        elif st == "mc_split":
+            mc_split(p)
+        elif st == "mc_sync":
+            mc_sync(p)
         elif st == "deblock":
             F.check(L.mi_deblock_frame_to(ctx.h, ctypes.byref(pa), ctypes.byref(pd), ctypes.byref(pipe.lf.s), p), "lf")
         elif st == "cdef":
