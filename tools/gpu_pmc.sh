@@ -20,7 +20,7 @@ PASSES=("FETCH_SIZE" "WRITE_SIZE" \
 for P in "${PASSES[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $OUT/$TAG/p$i -o p -- \
-      python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-fg --no-intra --no-extra --no-verify $BENCH_ARGS > $OUT/$TAG/p$i.log 2>&1 \
+      python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-fg --no-intra --no-extra --no-verify --no-two-in-flight $BENCH_ARGS > $OUT/$TAG/p$i.log 2>&1 \
       || { echo "pass $i failed"; tail -20 $OUT/$TAG/p$i.log; exit 1; }
 done
 python3 $R/tools/pmc_summary.py $OUT/$TAG > $OUT/$TAG/summary.txt && cat $OUT/$TAG/summary.txt

@@ -20,7 +20,7 @@ echo "calibration done"
 # the headline command alone (no real-stream / intra / grain legs), so that the per-kernel averages
 # are the headline's launches, comparable with the bench's event-timed launch_us
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o p -- \
-    python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-fg --no-intra --no-extra > $OUT/bench_stats.json 2> $OUT/bench_stats.err \
+    python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-fg --no-intra --no-extra --no-two-in-flight > $OUT/bench_stats.json 2> $OUT/bench_stats.err \
     || { echo "stats run failed"; tail -20 $OUT/bench_stats.err; exit 1; }
 echo "kernel stats done"; cat $OUT/bench_stats.json
 TRAFFIC_ONLY=1 bash $R/tools/gpu_pmc.sh $TAG/pmc > /dev/null || { echo "pmc failed"; exit 1; }
