@@ -922,13 +922,16 @@ def replicas(args, world, rank, local, hw):
     # per-rank correctness: the last timed frame, and one more step from the initial inputs,
     # against the oracle on this rank's host cores (outside the timed region)
     pipe.restore()
+    hw.sync()
     pipe.step(stream)
     hw.sync()
     digest = pipe.output_digest()
     verified = (digest == want and (args.graph or timed_digest == want)) if want is not None else None
     # the other in-flight frames (own buffers, streams and contexts) produce the same picture
     for pk, sk in pipes[1:]:
+        # restore's copies run on the current stream, the step on the frame's own: order them
         pk.restore()
+        hw.sync()
         pk.step(sk)
         hw.sync()
         if verified is not None:
