@@ -391,6 +391,7 @@ def end_to_end_4k10(fr, want=None, steps=20):
     if want is not None:
         for lane in lanes:
             lane[1].refill()
+        torch.cuda.synchronize()             # refill copies on the current stream, the frame on the lane's
         frame(lanes[0], 0)
         torch.cuda.synchronize()
         h = hashlib.sha256()
