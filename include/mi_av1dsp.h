@@ -431,14 +431,18 @@ int mi_mc_frame_ex(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int 
  * that SEG unit's tiles (they publish the mask with agent-scope word stores and a flag per
  * tile; the luma waves precede the chroma ones in the grid, so a waiting wave only waits for
  * waves already started). SEG and MASK mask offsets must be multiples of 16 and mask_bytes
- * the size of the mask buffer. A wait that does not end reports -EIO from
- * mi_mc_sync_status. */
+ * the size of the mask buffer. A wait that does not end is reported as -ETIMEDOUT, a flagged
+ * unit whose mask offset lies past mask_bytes as -EINVAL (the kernel skips its flag access),
+ * by mi_mc_sync_status or mi_ctx_device_status. While `stream` is being captured into a graph
+ * the call runs as mi_mc_frame's two launches: an epoch fixed at capture would let a replay
+ * see the flags of the previous replay. */
 #define MI_MC_AFTER_SEG 0x40u
 int mi_mc_frame_sync(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
                      const MiMcBlock *blocks, const uint32_t class_start[2 * MI_MC_NCLASS + 1],
                      uint8_t *masks, size_t mask_bytes, int16_t *tmp, void *stream);
-/* 0, or -EIO when a hand-off wait of an earlier mi_mc_frame_sync on the context timed out
- * (synchronises the context's stream; clears the status) */
+/* 0, -ETIMEDOUT when a hand-off wait of an earlier mi_mc_frame_sync on the context timed out,
+ * -EINVAL when a flagged unit's mask offset lay past mask_bytes (synchronises `stream`; clears
+ * the status; mi_ctx_device_status reports the same codes) */
 int mi_mc_sync_status(MiCtx *ctx, void *stream);
 /* OBMC: the caller runs mi_mc_frame a second time with the above-neighbour laps
  * (MI_MC_OBMC_H units) and a third time with the left-neighbour laps (MI_MC_OBMC_V), as

@@ -249,6 +249,11 @@ int mi_mc_frame_ex(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int 
     return r ? fail(ctx, -EIO) : 0;
 }
 
+// The device error word of the MC hand-off: bit 1 a unit's mask offset lies past the flag
+// buffer (mask_bytes too small for it: -EINVAL), bit 0 a wait gave up (-ETIMEDOUT). Both
+// status entry points report the same code.
+static int mc_err_code(int e) { return (e & 2) ? -EINVAL : -ETIMEDOUT; }
+
 int mi_mc_frame_sync(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
                      const MiMcBlock *blocks, const uint32_t class_start[2 * MI_MC_NCLASS + 1], uint8_t *masks,
                      size_t mask_bytes, int16_t *tmp, void *stream) {
@@ -266,9 +271,21 @@ int mi_mc_frame_sync(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, in
     const int w0 = mi::mc_plan(a, 0), w1 = mi::mc_plan(a, 1);
     if (w0 < 0 || w1 < 0) return fail(ctx, -EINVAL);
     hipStream_t s = (hipStream_t)stream;
+    // Under stream capture the epoch below would be frozen into the graph: a replay would find
+    // the flags of its previous replay already at "its" epoch and read masks that are still
+    // being rewritten. Captured calls therefore take the two launches of mi_mc_frame (luma,
+    // then chroma; no flags), which any number of replays orders correctly.
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) != hipSuccess) return fail(ctx, -EIO);
+    if (cap != hipStreamCaptureStatusNone) {
+        int r = w0 ? mi::launch_mc(a, 0, w0, s) : 0;
+        if (!r && w1) r = mi::launch_mc(a, 1, w1, s);
+        return r ? fail(ctx, -EIO) : 0;
+    }
     // the tile flags: 32 per 16 mask bytes (a SEG unit has at most 32 tiles), zeroed when
     // allocated and never reset (each call has its own epoch)
     const size_t nf = (mask_bytes / 16 + 1) * 32;
+    if (nf > 0xffffffffu) return fail(ctx, -EINVAL);
     if (nf > ctx->mc_flags_n) {
         if (ctx->mc_flags) (void)hipFree(ctx->mc_flags);
         ctx->mc_flags = nullptr;
@@ -284,6 +301,7 @@ int mi_mc_frame_sync(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, in
     if (++ctx->mc_epoch == 0) ctx->mc_epoch = 1;
     a.seg_flags = ctx->mc_flags;
     a.seg_epoch = ctx->mc_epoch;
+    a.seg_nflags = (uint32_t)nf;
     a.err = ctx->mc_err;
     // one grid, the luma group's waves first (see mi_av1dsp.h)
     const int r = w0 && w1 ? mi::launch_mc(a, 2, w0 + w1, s) : mi::launch_mc(a, w0 ? 0 : 1, w0 ? w0 : w1, s);
@@ -298,7 +316,7 @@ int mi_mc_sync_status(MiCtx *ctx, void *stream) {
         hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
         return fail(ctx, -EIO);
     if (e && hipMemsetAsync(ctx->mc_err, 0, sizeof(int), (hipStream_t)stream) != hipSuccess) return fail(ctx, -EIO);
-    return e ? fail(ctx, -EIO) : 0;
+    return e ? fail(ctx, mc_err_code(e)) : 0;
 }
 
 int mi_mc_scaled(MiCtx *ctx, const MiPicture *cur, const MiPicture *refs, int nrefs,
@@ -426,7 +444,7 @@ int mi_ctx_device_status(MiCtx *ctx, void *stream) {
         if (hipMemcpy(&e, ctx->mc_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return fail(ctx, -EIO);
         if (e) {
             if (hipMemset(ctx->mc_err, 0, sizeof(int)) != hipSuccess) return fail(ctx, -EIO);
-            return fail(ctx, -ETIMEDOUT);
+            return fail(ctx, mc_err_code(e));
         }
     }
     if (!ctx->ir_words) return 0;

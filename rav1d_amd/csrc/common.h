@@ -220,6 +220,7 @@ struct McArgs {
     // chroma MASK units flagged MI_MC_AFTER_SEG wait for them (null: no hand-off)
     uint32_t *seg_flags;
     uint32_t seg_epoch;
+    uint32_t seg_nflags;             // entries of seg_flags: a flag index at or past it is an error
     int *err;
 };
 // launchers (mc.hip): mc_plan fills first_wave[g] and returns the wave count of group g

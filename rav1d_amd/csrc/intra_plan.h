@@ -152,6 +152,9 @@ int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<in
     const int nparts = par(n, 32768, [&](int lo, int hi, int t) {
         part_lo[t] = lo;
         std::vector<int32_t> &pxd = part_xd[t];
+        // a range re-run on the caller's thread after its worker threw (PlanPool::run) must
+        // not keep the failed attempt's entries
+        pxd.clear();
         std::vector<int32_t> add;
         for (int i = lo; i < hi; i++) {
             xs[i] = (int32_t)pxd.size();

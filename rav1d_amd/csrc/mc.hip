@@ -313,7 +313,14 @@ __global__ __launch_bounds__(64, 1) void mc_kernel(McArgs a, int g) {
             tl = class_geom(((31 - __clz(lw)) << 3) | (31 - __clz(lh))).T;
         }
         const int li = G.T == 1 ? lane - uu * G.lanes_u : lane, nl = G.T == 1 ? G.lanes_u : 64;
-        const uint32_t *fl = a.seg_flags + (size_t)(b.mask_off >> 4) * 32;
+        const size_t f0 = (size_t)(b.mask_off >> 4) * 32;
+        // a mask offset past the flag buffer (a caller's mask_bytes too small) is reported,
+        // never read out of bounds: the unit then waits for nothing
+        if (after_seg && f0 + (size_t)tl > a.seg_nflags) {
+            atomicOr(a.err, 2);
+            tl = 0;
+        }
+        const uint32_t *fl = a.seg_flags + f0;
         bool ok = true;
         for (unsigned spins = 0;; spins++) {
             ok = true;
@@ -326,6 +333,14 @@ __global__ __launch_bounds__(64, 1) void mc_kernel(McArgs a, int g) {
             }
             __builtin_amdgcn_s_sleep(1);
         }
+        // No acquire (measured +2.5 us): the mask bytes are read below by `sc1`
+        // word loads of the polling wave itself, issued after the poll's loads returned (a
+        // wave's vector loads issue in program order and the exit branch waits for the poll's
+        // data), so they miss every L1 and see the producer's drained `sc1` stores
+        // (MI355X_MICROARCH.md, correctness boundaries: every store of the handed-off bytes
+        // `sc1`). This compiler barrier keeps those loads below the loop in the emitted code;
+        // tests/test_handoff_isa.py checks the result in the shipped code object.
+        asm volatile("" ::: "memory");
     }
 
     // everything after staging runs with the rows per lane R as a compile-time constant
@@ -455,8 +470,10 @@ __global__ __launch_bounds__(64, 1) void mc_kernel(McArgs a, int g) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         const int li = G.T == 1 ? lane - uu * G.lanes_u : lane;
-        if (seg_unit && li == 0)
-            __hip_atomic_store(a.seg_flags + (size_t)(b.mask_off >> 4) * 32 + tile, a.seg_epoch, __ATOMIC_RELAXED,
+        const size_t fi = (size_t)(b.mask_off >> 4) * 32 + tile;
+        if (seg_unit && li == 0 && fi >= a.seg_nflags) atomicOr(a.err, 2);
+        else if (seg_unit && li == 0)
+            __hip_atomic_store(a.seg_flags + fi, a.seg_epoch, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     }
     KTLV(6, c + (any2 ? 64 : 0));

@@ -79,7 +79,7 @@ def test_mc_frame_one_grid_matches_oracle(gpu, bpc, layout):
 
 def test_mc_frame_ex_rejects_unknown_flags(gpu):
     from rav1d_amd import lib
-    from rav1d_amd.frame import MiPicture
+    from rav1d_amd import MiPicture
     import ctypes
     cur = Frame(64, 64, 8, 1)
     cs = (ctypes.c_uint32 * 129)()
@@ -144,3 +144,49 @@ def test_mc_frame_sync_matches_oracle(gpu, bpc, layout, size):
     units, ps, masks = make_mc_units(w, h, layout, rng, nrefs=3, compound_frac=0.5, mv_px=40, min_bs=8)
     assert mc_sync_ok(units)
     run_case(gpu, w, h, bpc, layout, units, ps, masks, refs, rng, sync=True)
+
+
+def _sync_units(w, h, layout, seed):
+    rng = np.random.default_rng(seed)
+    refs = make_refs(w, h, 10, layout, 3, rng)
+    units, ps, masks = make_mc_units(w, h, layout, rng, nrefs=3, compound_frac=0.5, mv_px=40, min_bs=8)
+    waiting = (units["plane"] > 0) & ((units["param"] & 0x40) != 0)
+    assert waiting.any(), "the case needs chroma units that wait for a SEG mask"
+    return refs, units, ps, masks
+
+
+def test_mc_frame_sync_timeout_reported(gpu):
+    """A chroma unit flagged MI_MC_AFTER_SEG whose SEG unit is not in the call waits until its
+    bound and the status calls report -ETIMEDOUT (mi_mc_sync_status and mi_ctx_device_status
+    agree), then clear."""
+    from rav1d_amd.synth import mc_sort_units
+    w, h = 256, 192
+    refs, units, _, masks = _sync_units(w, h, 1, 0x7E0)
+    keep = ~((units["plane"] == 0) & (units["comp"] == 3))          # drop every luma SEG unit
+    units, ps = mc_sort_units(units[keep])
+    cur = Frame(w, h, 10, 1)
+    meta = McMeta(units, ps, masks)
+    for status in ("mi_mc_sync_status", "mi_ctx_device_status"):
+        mc_frame_sync(gpu, cur, refs, meta)
+        assert getattr(lib(), status)(gpu.h, _stream_ptr(None)) == -110, status    # -ETIMEDOUT
+        assert lib().mi_mc_sync_status(gpu.h, _stream_ptr(None)) == 0, "status not cleared"
+
+
+def test_mc_frame_sync_mask_offset_past_buffer(gpu):
+    """mask_bytes smaller than the units' mask offsets: the kernel skips the flag accesses it
+    cannot bound and the status reports -EINVAL (no out-of-bounds flag access)."""
+    import ctypes
+    from rav1d_amd import MiPicture
+    w, h = 256, 192
+    refs, units, ps, masks = _sync_units(w, h, 1, 0x7E1)
+    assert int(units["mask_off"].max()) >= 64
+    cur = Frame(w, h, 10, 1)
+    meta = McMeta(units, ps, masks)
+    pics = (MiPicture * len(refs))(*[r.picture() for r in refs])
+    rc = lib().mi_mc_frame_sync(gpu.h, ctypes.byref(cur.picture()), pics, len(refs),
+                                ctypes.c_void_p(meta.blocks.data_ptr()), meta.class_start,
+                                ctypes.c_void_p(meta.masks.data_ptr()), 16, None, _stream_ptr(None))
+    assert rc == 0
+    assert lib().mi_mc_sync_status(gpu.h, _stream_ptr(None)) == -22     # -EINVAL
+    assert lib().mi_mc_sync_status(gpu.h, _stream_ptr(None)) == 0
+
