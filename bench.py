@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 
 from rav1d_amd import ITX_KEEP_COEFS  # noqa: E402
 from rav1d_amd import frame as F  # noqa: E402
-from rav1d_amd.synth import frame_bytes, itx_algorithmic_bytes, itx_band_order, make_frame, mc_algorithmic_bytes, mc_sync_ok  # noqa: E402
+from rav1d_amd.synth import frame_bytes, itx_algorithmic_bytes, itx_band_order, itx_dc_runs, make_frame, mc_algorithmic_bytes, mc_sync_ok  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 W, H, BPC, LAYOUT = 3840, 2160, 10, 1
@@ -67,12 +67,15 @@ class Pipeline:
             # (mi_mc_frame_sync, as the frame executor runs it when the offsets allow)
             self.mc_sync = mc_sync_ok(fr["mc"][0])
         self.blocks = torch.from_numpy(fr["blocks"].view(np.uint8).copy()).cuda()
-        # itx over picture bands, one XCD per band (mi_itx_frame_banded, as the frame executor runs it)
+        # itx over picture bands, one XCD per band, each band's DC-only blocks first on the DC
+        # path (mi_itx_frame_runs, as the frame executor runs it)
         ah = (h + 127) & ~127
         ssv = 1 if lay == 1 else 0
         blk, _, bs = itx_band_order(fr["blocks"], [ah, ah >> ssv, ah >> ssv])
+        de = itx_dc_runs(blk, bs)
         self.blocks = torch.from_numpy(blk.view(np.uint8).copy()).cuda()
         self.itx_bands = (ctypes.c_uint32 * bs.size)(*[int(v) for v in bs.reshape(-1)])
+        self.itx_dc_end = (ctypes.c_uint32 * de.size)(*[int(v) for v in de.reshape(-1)])
         self.coef = torch.from_numpy(fr["coef"].copy()).cuda()
         self.coef0 = self.coef.clone()               # itx zeroes the arena it consumes
         self.coefs = [self.coef] + [self.coef0.clone() for _ in range(max(1, ring) - 1)]
@@ -146,8 +149,9 @@ class Pipeline:
             mark.record(stream)
         coef = self.coefs[self.k % len(self.coefs)]
         self.k += 1
-        timed("itx", lambda: F.check(lib.mi_itx_frame_banded(ctx, ctypes.byref(pa), ctypes.c_void_p(self.blocks.data_ptr()),
-                                                             self.itx_bands, ctypes.c_void_p(coef.data_ptr()), ITX_KEEP_COEFS, sp), "itx"))
+        timed("itx", lambda: F.check(lib.mi_itx_frame_runs(ctx, ctypes.byref(pa), ctypes.c_void_p(self.blocks.data_ptr()),
+                                                           self.itx_bands, self.itx_dc_end, ctypes.c_void_p(coef.data_ptr()),
+                                                           ITX_KEEP_COEFS, sp), "itx"))
         timed("deblock", lambda: F.check(lib.mi_deblock_frame_to(ctx, ctypes.byref(pa), ctypes.byref(pd),
                                                                  ctypes.byref(self.lf.s), sp), "lf"))
         timed("cdef", lambda: F.check(lib.mi_cdef_frame(ctx, ctypes.byref(pd), ctypes.byref(pb),

@@ -337,6 +337,15 @@ int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
 int mi_itx_frame_banded(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
                         const uint32_t band_start[MI_N_RECT_TX_SIZES][MI_ITX_BANDS + 1], void *coef,
                         unsigned flags, void *stream);
+/* mi_itx_frame_banded whose bands each begin with a run of DC-only blocks (DCT_DCT, eob < 1):
+ * blocks [band_start[s][q], dc_end[s][q]) of band q of size s, band_start[s][q] <= dc_end[s][q]
+ * <= band_start[s][q + 1]. The runs take a DC path (many blocks per workgroup, whole line
+ * segments); a block in a run that is not DC-only is skipped and reported by
+ * mi_ctx_device_status (-EINVAL). Same pixels as mi_itx_frame over the same blocks. */
+int mi_itx_frame_runs(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
+                      const uint32_t band_start[MI_N_RECT_TX_SIZES][MI_ITX_BANDS + 1],
+                      const uint32_t dc_end[MI_N_RECT_TX_SIZES][MI_ITX_BANDS], void *coef, unsigned flags,
+                      void *stream);
 
 /* Intra prediction of n independent blocks (one wavefront step of a frame, or any set of
  * blocks whose edges are final): writes each block into `pic` from its gathered edges

@@ -139,6 +139,9 @@ def lib():
          [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.POINTER(ctypes.c_uint32), _VP, ctypes.c_uint, _VP])
     _sig(L, "mi_itx_frame_banded", ctypes.c_int,
          [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.POINTER(ctypes.c_uint32), _VP, ctypes.c_uint, _VP])
+    _sig(L, "mi_itx_frame_runs", ctypes.c_int,
+         [_VP, ctypes.POINTER(MiPicture), _VP, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32), _VP,
+          ctypes.c_uint, _VP])
     _sig(L, "mi_dsp_itxfm_add", ctypes.c_int,
          [ctypes.c_int, ctypes.c_int, _VP, ctypes.c_ssize_t, _VP, ctypes.c_int, ctypes.c_int])
     _sig(L, "mi_mc_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture), ctypes.c_int,
@@ -220,7 +223,7 @@ def lib():
 
 # Every symbol include/mi_av1dsp.h declares (checked by tests/test_abi.py).
 EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
-            "mi_itx_frame", "mi_itx_frame_banded", "mi_mc_frame", "mi_mc_frame_ex", "mi_mc_frame_sync", "mi_mc_sync_status", "mi_mc_scaled", "mi_mc_warp", "mi_mc_combine", "mi_superres_frame",
+            "mi_itx_frame", "mi_itx_frame_banded", "mi_itx_frame_runs", "mi_mc_frame", "mi_mc_frame_ex", "mi_mc_frame_sync", "mi_mc_sync_status", "mi_mc_scaled", "mi_mc_warp", "mi_mc_combine", "mi_superres_frame",
             "mi_ipred_blocks", "mi_intra_blocks", "mi_intra_recon", "mi_ctx_device_status", "mi_deblock_frame", "mi_deblock_frame_to", "mi_cdef_frame", "mi_lr_frame", "mi_lr_tile_order", "mi_cdef_tile_order",
             "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply", "mi_frame_run", "mi_frame_end", "mi_frame_validate", "mi_frame_plan_ms",
             "mi_ctx_set_timing", "mi_ctx_timing",

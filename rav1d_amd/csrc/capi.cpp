@@ -108,7 +108,7 @@ int mi_ctx_last_error(const MiCtx *ctx) { return ctx ? ctx->last_error : -EINVAL
 
 static int itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
                      const uint32_t *size_start, const uint32_t *band_start, void *coef, unsigned flags,
-                     void *stream);
+                     void *stream, const uint32_t *dc_end = nullptr);
 
 int mi_itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
                  const uint32_t size_start[MI_N_RECT_TX_SIZES + 1], void *coef, unsigned flags,
@@ -132,9 +132,27 @@ int mi_itx_frame_banded(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *block
     return itx_frame(ctx, pic, blocks, ss, &band_start[0][0], coef, flags, stream);
 }
 
+int mi_itx_frame_runs(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
+                      const uint32_t band_start[MI_N_RECT_TX_SIZES][MI_ITX_BANDS + 1],
+                      const uint32_t dc_end[MI_N_RECT_TX_SIZES][MI_ITX_BANDS], void *coef, unsigned flags,
+                      void *stream) {
+    if (!band_start || !dc_end) return fail(ctx, -EINVAL);
+    uint32_t ss[MI_N_RECT_TX_SIZES + 1];
+    for (int t = 0; t < MI_N_RECT_TX_SIZES; t++) {
+        ss[t] = band_start[t][0];
+        if (t && band_start[t][0] != band_start[t - 1][MI_ITX_BANDS]) return fail(ctx, -EINVAL);
+        for (int q = 0; q < MI_ITX_BANDS; q++)
+            if (band_start[t][q + 1] < band_start[t][q] || dc_end[t][q] < band_start[t][q] ||
+                dc_end[t][q] > band_start[t][q + 1])
+                return fail(ctx, -EINVAL);
+    }
+    ss[MI_N_RECT_TX_SIZES] = band_start[MI_N_RECT_TX_SIZES - 1][MI_ITX_BANDS];
+    return itx_frame(ctx, pic, blocks, ss, &band_start[0][0], coef, flags, stream, &dc_end[0][0]);
+}
+
 static int itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
                      const uint32_t *size_start, const uint32_t *band_start, void *coef, unsigned flags,
-                     void *stream) {
+                     void *stream, const uint32_t *dc_end) {
     if (!ctx || !pic || !size_start) return fail(ctx, -EINVAL);
     if (pic->bpc != 8 && pic->bpc != 10 && pic->bpc != 12) return fail(ctx, -EINVAL);
     mi::ItxArgs a;
@@ -159,7 +177,7 @@ static int itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
     a.err = ctx->ir_words + 65;
     for (int k = 0; k < MI_N_RECT_TX_SIZES; k++)
         if (size_start[k + 1] < size_start[k]) return fail(ctx, -EINVAL);
-    const int wg = mi::itx_fill_schedule(a, size_start, band_start);
+    const int wg = mi::itx_fill_schedule(a, size_start, band_start, dc_end);
     if (wg == 0) return 0;
     if (!blocks || !coef) return fail(ctx, -EINVAL);
     // One launch (itx.hip): the large sizes' workgroups first, the small ones fill in around

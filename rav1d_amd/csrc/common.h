@@ -115,14 +115,18 @@ struct ItxArgs {
     uint8_t *coef;
     int bdmax;
     int zero_coefs;
-    int wg_start[20];   // first workgroup of the i-th size in grid order (kItxLaunchOrder)
-    int wg_size[19];    // tx size of the i-th range
+    int wg_start[39];   // first workgroup of the i-th range in grid order (kItxLaunchOrder)
+    int wg_size[38];    // tx size of the i-th range, | kItxDcRange for a range of DC runs
     int blk_start[20];  // block ranges per tx size (enum order, as the caller groups them)
     // nbands 8: inside a size the blocks are further grouped by horizontal picture band (band q
     // = blocks[band_start[s][q] .. band_start[s][q + 1])), and band q's workgroups get grid
     // indices = q mod 8, i.e. run on XCD q (the dispatcher's round robin): every pixel line of
     // the band is fetched into, and written back from, one XCD's L2 whichever sizes touch it
     int band_start[19][9];
+    // DC runs (mi_itx_frame_runs): the blocks [band_start[s][q], dc_end[s][q]) of a band are
+    // DC-only (DCT_DCT, eob < 1) and take the DC path (itx_dc); the rest of the band the
+    // transform path. dc_end[s][q] == band_start[s][q] when the caller gives no runs.
+    int dc_end[19][8];
     int nbands;         // 1 or 8
     int pw[3], ph[3];   // plane extents (128-aligned picture area; 0 = no such plane)
     int *err;           // device error word: set when a descriptor is rejected
@@ -140,9 +144,17 @@ __host__ __device__ constexpr uint32_t itx_legal_types(int tx) {
 // then the 32-point sizes, then every size with both sides <= 16
 constexpr int kItxLaunchOrder[19] = { 4, 11, 12, 17, 18, 3, 9, 10, 15, 16, 0, 1, 2, 5, 6, 7, 8, 13, 14 };
 constexpr int kItxBands = 8;
-// fills wg_start / wg_size / blk_start (and the band table when band_start, [19][9], is given);
-// returns the grid size
-int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start, const uint32_t *band_start = nullptr);
+constexpr int kItxDcRange = 32;   // wg_size flag: the range's workgroups run DC runs
+// DC path geometry of a size: chunks of min(w, 8) pixels, kItxDcItems chunks per lane, up to
+// 128 blocks per workgroup
+constexpr int kItxDcItems = 16;
+__host__ __device__ constexpr int itx_dc_blocks(int tx) {
+    return imax_c(1, imin_c(128, 64 * kItxDcItems / (tx_dim(tx).h * (tx_dim(tx).w < 8 ? 1 : tx_dim(tx).w / 8))));
+}
+// fills wg_start / wg_size / blk_start (and the band table when band_start, [19][9], is given;
+// DC runs when dc_end, [19][8], is given too); returns the grid size
+int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start, const uint32_t *band_start = nullptr,
+                      const uint32_t *dc_end = nullptr);
 
 // launcher (itx.hip)
 int launch_itx_frame(const ItxArgs &a, int nwg, int bpc, hipStream_t s);

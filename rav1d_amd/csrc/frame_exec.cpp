@@ -587,6 +587,7 @@ struct FramePlan {
     uint32_t mc_cs[2 * MI_MC_NCLASS + 1], lap_cs[2][2 * MI_MC_NCLASS + 1];
     std::vector<MiTxBlock> itx_b;
     uint32_t itx_bs[MI_N_RECT_TX_SIZES][MI_ITX_BANDS + 1];
+    uint32_t itx_dc[MI_N_RECT_TX_SIZES][MI_ITX_BANDS];   // end of each band's DC-only run
     // CDEF and loop-restoration workgroup orders, costliest first (mi_cdef_tile_order /
     // mi_lr_tile_order)
     std::vector<int32_t> cdef_order, lr_order;
@@ -668,26 +669,30 @@ void plan_frame(const MiDecFrame *f, const bool scaled[7], FramePlan &pl) {
                                        (int)pl.lr_order.size());
         pl.lr_order.resize(n > 0 ? n : 0);
     }
-    // residuals grouped by (tx size, picture band) for mi_itx_frame_banded: a counting sort
-    // keeping decode order inside a group
+    // residuals grouped by (tx size, picture band) for mi_itx_frame_runs, each group's DC-only
+    // blocks (DCT_DCT, eob < 1) first: a counting sort keeping decode order inside a group
     std::vector<MiTxBlock> &itx_b = pl.itx_b;
     itx_b.resize(f->n_inter_tx);
     uint32_t (&itx_bs)[MI_N_RECT_TX_SIZES][MI_ITX_BANDS + 1] = pl.itx_bs;
+    uint32_t (&itx_dc)[MI_N_RECT_TX_SIZES][MI_ITX_BANDS] = pl.itx_dc;
     memset(itx_bs, 0, sizeof(itx_bs));
     {
         constexpr int NF = MI_ITX_BANDS;                           // bands per plane
-        constexpr int NK = MI_N_RECT_TX_SIZES * NF;
+        constexpr int NK = MI_N_RECT_TX_SIZES * NF * 2;
         const int ah = (f->h + 127) & ~127, ssv = f->layout == 1;
         auto key = [&](const MiTxBlock &b) {
             const int ph = b.plane ? ah >> ssv : ah;
             const int q = (int)((int64_t)b.y * NF / ph);
-            return (int)b.tx * NF + (q < NF - 1 ? q : NF - 1);
+            const int dc = b.txtp == 0 && b.eob < 1;
+            return ((int)b.tx * NF + (q < NF - 1 ? q : NF - 1)) * 2 + (dc ? 0 : 1);
         };
         std::vector<uint32_t> start(NK + 1, 0);
         for (int i = 0; i < f->n_inter_tx; i++) start[key(f->inter_tx[i]) + 1]++;
         for (int k = 0; k < NK; k++) start[k + 1] += start[k];
-        for (int t = 0; t < MI_N_RECT_TX_SIZES; t++)
-            for (int q = 0; q <= MI_ITX_BANDS; q++) itx_bs[t][q] = start[t * NF + q];
+        for (int t = 0; t < MI_N_RECT_TX_SIZES; t++) {
+            for (int q = 0; q <= MI_ITX_BANDS; q++) itx_bs[t][q] = start[(t * NF + q) * 2];
+            for (int q = 0; q < MI_ITX_BANDS; q++) itx_dc[t][q] = start[(t * NF + q) * 2 + 1];
+        }
         for (int i = 0; i < f->n_inter_tx; i++) itx_b[start[key(f->inter_tx[i])]++] = f->inter_tx[i];
     }
 }
@@ -814,7 +819,7 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
                 return r;
         }
         if (f->n_inter_tx &&
-            (r = mi_itx_frame_banded(ctx, &cur, (const MiTxBlock *)D(20), itx_bs, D(4), MI_ITX_KEEP_COEFS, stream)))
+            (r = mi_itx_frame_runs(ctx, &cur, (const MiTxBlock *)D(20), itx_bs, pl.itx_dc, D(4), MI_ITX_KEEP_COEFS, stream)))
             return r;
     }
 

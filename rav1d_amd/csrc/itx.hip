@@ -105,7 +105,7 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     if (a.nbands > 1) {
         const int q = lwg & 7;
         k = lwg >> 3;
-        bs = KARG(band_start, TX * 9 + q);
+        bs = KARG(dc_end, TX * 8 + q);            // after the band's DC run (itx_dc)
         be = KARG(band_start, TX * 9 + q + 1);
     }
 #ifdef MI_KTL
@@ -309,6 +309,134 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
     }
 }
 
+// DC runs (mi_itx_frame_runs). A DC-only block (DCT_DCT, eob < 1) adds one constant to its
+// pixels: the DC coefficient scaled as inv_txfm_add_rust's dc_only path does (src/itx.rs:64-188:
+// rect2 scaling, the row shift, the final * 181 >> 12 with rounding). In the size paths such a
+// block costs a transform workgroup's whole latency chain for 32-512 bytes; here a one-wave
+// workgroup takes itx_dc_blocks(TX) consecutive blocks of one band's DC run: lanes fetch the
+// descriptors and DC coefficients into LDS, then sweep the blocks' rows in chunks of min(w, 8)
+// pixels, kItxDcItems chunks per lane with every load in flight before the first add.
+// Consecutive lanes take a row's chunks, then the next rows, then the next block, so a run of
+// neighbouring blocks (sorted by position) is read and written in whole line segments.
+template <typename Px, int CP> struct DcVec;
+template <> struct DcVec<uint16_t, 8> { using T = uint4; };
+template <> struct DcVec<uint16_t, 4> { using T = uint2; };
+template <> struct DcVec<uint8_t, 8> { using T = uint2; };
+template <> struct DcVec<uint8_t, 4> { using T = uint32_t; };
+
+// pixels + dc, clipped to [0, bdmax], on a vector of CP pixels
+template <typename Px, typename V>
+__device__ __forceinline__ V dc_add(V v, int dc, int bdmax) {
+    constexpr int NW = sizeof(V) / 4;
+    uint32_t w[NW];
+    __builtin_memcpy(w, &v, sizeof(V));
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        if constexpr (sizeof(Px) == 2) {
+            const int lo = clampi((int)(w[i] & 0xffff) + dc, 0, bdmax), hi = clampi((int)(w[i] >> 16) + dc, 0, bdmax);
+            w[i] = (uint32_t)lo | ((uint32_t)hi << 16);
+        } else {
+            uint32_t o = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) o |= (uint32_t)clampi((int)((w[i] >> (8 * b)) & 0xff) + dc, 0, bdmax) << (8 * b);
+            w[i] = o;
+        }
+    }
+    __builtin_memcpy(&v, w, sizeof(V));
+    return v;
+}
+
+struct ItxDcRec {
+    uint8_t *base;   // the block's top-left pixel; null: skipped
+    int st;          // plane stride in bytes
+    int dc;          // the constant added to every pixel
+};
+
+template <int TX, typename Px, typename Cf>
+__device__ __forceinline__ void itx_dc(const ItxArgs &a, int lwg, uint8_t *lds) {
+    constexpr TxDim D = tx_dim(TX);
+    constexpr int W = D.w, H = D.h, Shift = D.shift, Rnd = (1 << Shift) >> 1;
+    constexpr bool Rect2 = (W == 2 * H) || (H == 2 * W);
+    constexpr int CP = W < 8 ? W : 8, CW = W / CP, IPB = H * CW, NB = itx_dc_blocks(TX);
+    using V = typename DcVec<Px, CP>::T;
+    const int lane = threadIdx.x;
+    const int q = lwg & 7, k = lwg >> 3;
+    const int bs = KARG(band_start, TX * 9 + q) + k * NB;
+    const int nb = min(NB, KARG(dc_end, TX * 8 + q) - bs);
+    uint8_t *const plane3[3] = { a.plane[0], a.plane[1], a.plane[2] };
+    const int64_t stride3[3] = { a.stride[0], a.stride[1], a.stride[2] };
+    const int pw3[3] = { a.pw[0], a.pw[1], a.pw[2] }, ph3[3] = { a.ph[0], a.ph[1], a.ph[2] };
+    ItxDcRec *rec = reinterpret_cast<ItxDcRec *>(lds);
+    // descriptors -> records (base, stride) in LDS; each lane keeps its blocks' DC coefficient
+    // load in flight and writes the scaled DC only after the pixel loads below are issued, so
+    // that the coefficient and pixel round trips overlap
+    constexpr int NR = (NB + 63) / 64;
+    int dcv[NR];
+    const Cf *dcp[NR];
+#pragma unroll
+    for (int rr = 0; rr < NR; rr++) {
+        const int t = rr * 64 + lane;
+        dcp[rr] = nullptr;
+        if (t < NB) {
+            ItxDcRec r{ nullptr, 0, 0 };
+            if (t < nb) {
+                const MiTxBlock b = a.blocks[bs + t];
+                // a block the run may not hold (another size, not DC-only, outside its plane) is
+                // skipped and reported, as the transform path does
+                const bool ok = b.tx == TX && b.txtp == 0 && b.eob < 1 && b.plane < 3 &&
+                                b.x + W <= sel3(pw3, b.plane) && b.y + H <= sel3(ph3, b.plane);
+                if (ok) {
+                    dcp[rr] = reinterpret_cast<const Cf *>(a.coef) + b.coef_off;
+                    const int64_t st = sel3(stride3, b.plane);
+                    r.base = sel3(plane3, b.plane) + (int64_t)b.y * st + (int64_t)b.x * sizeof(Px);
+                    r.st = (int)st;
+                } else {
+                    atomicOr(a.err, 2);
+                }
+            }
+            rec[t] = r;
+        }
+    }
+#pragma unroll
+    for (int rr = 0; rr < NR; rr++) dcv[rr] = dcp[rr] ? (int)dcp[rr][0] : 0;
+    __syncthreads();
+    V px[kItxDcItems];
+#pragma unroll
+    for (int i = 0; i < kItxDcItems; i++) {
+        const int j = lane + 64 * i, blk = j / IPB;
+        if (blk < nb) {
+            const ItxDcRec r = rec[blk];
+            if (r.base)
+                px[i] = *reinterpret_cast<const V *>(r.base + (int64_t)((j / CW) % H) * r.st + (j % CW) * CP * (int)sizeof(Px));
+        }
+    }
+    // the scaled DC of every block into its record (src/itx.rs:64-188 dc_only path)
+#pragma unroll
+    for (int rr = 0; rr < NR; rr++) {
+        const int t = rr * 64 + lane;
+        if (dcp[rr]) {
+            int dc = dcv[rr];
+            if (a.zero_coefs) *const_cast<Cf *>(dcp[rr]) = 0;
+            if (Rect2) dc = (dc * 181 + 128) >> 8;
+            dc = (dc * 181 + 128) >> 8;
+            dc = (dc + Rnd) >> Shift;
+            dc = (dc * 181 + 128 + 2048) >> 12;
+            rec[t].dc = dc;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kItxDcItems; i++) {
+        const int j = lane + 64 * i, blk = j / IPB;
+        if (blk < nb) {
+            const ItxDcRec r = rec[blk];
+            if (r.base)
+                *reinterpret_cast<V *>(r.base + (int64_t)((j / CW) % H) * r.st + (j % CW) * CP * (int)sizeof(Px)) =
+                    dc_add<Px, V>(px[i], r.dc, a.bdmax);
+        }
+    }
+}
+
 // One launch for every size. The workgroups of the 64- and 32-point sizes come first in the
 // grid: they are few but the longest (a 64-point transform per lane, ~15 us at 4K10), so they
 // start first and the small sizes fill the machine around them. Measured against two launches
@@ -325,7 +453,7 @@ __global__ __launch_bounds__(kItxThreads, 4) void itx_frame_kernel(ItxArgs a) {
     // the size range holding this workgroup, with compile-time indices only (a runtime index
     // into the kernel-argument struct makes the compiler copy it to scratch)
     int i = 0;
-    for (int k = 1; k < 19; k++)
+    for (int k = 1; k < 38; k++)
         if (wg >= KARG(wg_start, k)) i = k;
     const int s = KARG(wg_size, i);
     const int lwg = wg - KARG(wg_start, i);
@@ -336,8 +464,10 @@ __global__ __launch_bounds__(kItxThreads, 4) void itx_frame_kernel(ItxArgs a) {
         KTL(4);
     }
 #endif
+    static_assert(sizeof(lds) >= 128 * sizeof(ItxDcRec), "LDS for the DC path's records");
     switch (s) {
-#define CASE(n) case n: itx_size<n, Px, Cf, Lt, Wide>(a, lwg, lds); break;
+#define CASE(n) case n: itx_size<n, Px, Cf, Lt, Wide>(a, lwg, lds); break; \
+                case n | kItxDcRange: itx_dc<n, Px, Cf>(a, lwg, reinterpret_cast<uint8_t *>(lds)); break;
         CASE(0) CASE(1) CASE(2) CASE(5) CASE(6) CASE(7) CASE(8) CASE(13) CASE(14)
         CASE(3) CASE(9) CASE(10) CASE(15) CASE(16)
         CASE(4) CASE(11) CASE(12) CASE(17) CASE(18)
@@ -348,29 +478,51 @@ __global__ __launch_bounds__(kItxThreads, 4) void itx_frame_kernel(ItxArgs a) {
     KTL(5);
 }
 
-int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start, const uint32_t *band_start) {
-    int wg = 0;
+// Where the DC-run ranges go in the grid: 0 before every transform range, 1 after the 64- and
+// 32-point sizes' ranges, 2 after every transform range. 4K10 bench frame, graph-timed with a
+// fresh arena per call: 33.4-33.8 / 34.1-34.4 / 34.6-35.6 us (the banded grid without runs:
+// 36.0-36.5 us)
+#ifndef MI_ITX_DC_POS
+#define MI_ITX_DC_POS 0
+#endif
+
+int itx_fill_schedule(ItxArgs &a, const uint32_t *size_start, const uint32_t *band_start, const uint32_t *dc_end) {
+    int wg = 0, r = 0;
     a.nbands = band_start ? kItxBands : 1;
-    for (int i = 0; i < 19; i++) {
-        const int sz = kItxLaunchOrder[i];
-        a.wg_start[i] = wg;
-        a.wg_size[i] = sz;
-        const int per_wg = itx_blocks_per_wg(sz) * itx_rounds(sz);
+    if (band_start)
+        for (int s = 0; s < 19; s++)
+            for (int q = 0; q < kItxBands; q++)
+                a.dc_end[s][q] = (int)(dc_end ? dc_end[s * kItxBands + q] : band_start[s * (kItxBands + 1) + q]);
+    // one range: 8 x the largest band's workgroup count (grid index 8m + q serves band q), or the
+    // size's count without bands
+    auto add = [&](int sz, bool dcr) {
+        a.wg_start[r] = wg;
+        a.wg_size[r] = sz | (dcr ? kItxDcRange : 0);
+        r++;
+        const int per_wg = dcr ? itx_dc_blocks(sz) : itx_blocks_per_wg(sz) * itx_rounds(sz);
         if (band_start) {
-            // 8 x the largest band's workgroup count: grid index 8m + q serves band q
             const uint32_t *b = band_start + sz * (kItxBands + 1);
             int m = 0;
             for (int q = 0; q < kItxBands; q++) {
-                const int n = (int)(b[q + 1] - b[q]);
-                m = std::max(m, (n + per_wg - 1) / per_wg);
+                const int lo = dcr ? (int)b[q] : a.dc_end[sz][q], hi = dcr ? a.dc_end[sz][q] : (int)b[q + 1];
+                m = std::max(m, (hi - lo + per_wg - 1) / per_wg);
             }
             wg += kItxBands * m;
-        } else {
+        } else if (!dcr) {
             const int n = (int)(size_start[sz + 1] - size_start[sz]);
             wg += (n + per_wg - 1) / per_wg;
         }
+    };
+    auto add_dc = [&]() {
+        for (int i = 18; i >= 0; i--) add(kItxLaunchOrder[i], true);
+    };
+    if (MI_ITX_DC_POS == 0) add_dc();
+    for (int i = 0; i < 19; i++) {
+        add(kItxLaunchOrder[i], false);
+        if (MI_ITX_DC_POS == 1 && i == 9) add_dc();
     }
-    a.wg_start[19] = wg;
+    if (MI_ITX_DC_POS == 2) add_dc();
+    for (int k = r; k < 39; k++) a.wg_start[k] = wg;
     for (int k = 0; k <= 19; k++) a.blk_start[k] = (int)size_start[k];
     if (band_start)
         for (int s = 0; s < 19; s++)

@@ -121,13 +121,21 @@ def _stream_ptr(stream):
     return ctypes.c_void_p(stream.cuda_stream)
 
 
-def itx_frame(ctx, frame, blocks_dev, size_start, coef_dev, flags=0, stream=None, band_start=None):
+def itx_frame(ctx, frame, blocks_dev, size_start, coef_dev, flags=0, stream=None, band_start=None, dc_end=None):
     """mi_itx_frame: inverse transform + add for all blocks of a frame (device tensors).
     band_start ([19][9], synth.itx_band_order): the blocks are also grouped by picture band
-    and run through mi_itx_frame_banded (one XCD per band)."""
+    and run through mi_itx_frame_banded (one XCD per band); with dc_end ([19][8],
+    synth.itx_dc_runs) through mi_itx_frame_runs (each band's leading DC-only run on the DC path)."""
     pic = frame.picture()
     if blocks_dev.dtype != torch.uint8 or not blocks_dev.is_cuda:
         raise MiError("blocks must be a device uint8 tensor holding MiTxBlock records")
+    if band_start is not None and dc_end is not None:
+        bs = (ctypes.c_uint32 * (19 * 9))(*[int(v) for v in np.asarray(band_start).reshape(-1)])
+        de = (ctypes.c_uint32 * (19 * 8))(*[int(v) for v in np.asarray(dc_end).reshape(-1)])
+        rc = lib().mi_itx_frame_runs(ctx.h, ctypes.byref(pic), ctypes.c_void_p(blocks_dev.data_ptr()), bs, de,
+                                     ctypes.c_void_p(coef_dev.data_ptr()), flags, _stream_ptr(stream))
+        check(rc, "mi_itx_frame_runs")
+        return
     if band_start is not None:
         bs = (ctypes.c_uint32 * (19 * 9))(*[int(v) for v in np.asarray(band_start).reshape(-1)])
         rc = lib().mi_itx_frame_banded(ctx.h, ctypes.byref(pic), ctypes.c_void_p(blocks_dev.data_ptr()), bs,

@@ -194,6 +194,20 @@ def itx_band_order(blocks, plane_heights):
     return blocks, size_start, bs
 
 
+def itx_dc_runs(blocks, band_start):
+    """dc_end[19][8] for mi_itx_frame_runs: the end of the DC-only run (DCT_DCT, eob < 1) that
+    begins each (size, band) range of blocks in itx_band_order's order (DC-only blocks first)."""
+    dc = (blocks["txtp"] == 0) & (blocks["eob"] < 1)
+    dc_end = np.empty((N_RECT_TX_SIZES, ITX_BANDS), np.uint32)
+    for t in range(N_RECT_TX_SIZES):
+        for q in range(ITX_BANDS):
+            lo, hi = int(band_start[t][q]), int(band_start[t][q + 1])
+            n = int(dc[lo:hi].sum())
+            assert dc[lo:lo + n].all(), "DC-only blocks must lead their band"
+            dc_end[t][q] = lo + n
+    return dc_end
+
+
 def itx_algorithmic_bytes(blocks, bpc, zero_coefs=True):
     """sum over blocks of coefB*n_coef (+ the zeroing write) + 2*pixB*w*h,
     plus the 16-byte descriptor."""

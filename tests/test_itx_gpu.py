@@ -10,24 +10,26 @@ import torch
 
 from rav1d_amd import ITX_KEEP_COEFS, lib
 from rav1d_amd.frame import Frame, itx_frame
-from rav1d_amd.synth import TX_DIMS, itx_band_order, make_coefs, make_itx_frame, tx_types
+from rav1d_amd.synth import TX_DIMS, itx_band_order, itx_dc_runs, make_coefs, make_itx_frame, tx_types
 from tests import oracle_lib
 from tests.oracle_lib import ptr
 
 pytestmark = pytest.mark.gpu
 
 
-def run_frame(gpu, fr, flags=0, banded=False):
+def run_frame(gpu, fr, flags=0, banded=False, runs=False):
     f = Frame(fr["w"], fr["h"], fr["bpc"], fr["layout"])
     for p, arr in enumerate(fr["planes"]):
         f.set_plane_np(p, arr)
-    blk, bands = fr["blocks"], None
-    if banded:
+    blk, bands, dc_end = fr["blocks"], None, None
+    if banded or runs:
         ah = (fr["h"] + 127) & ~127
         blk, _, bands = itx_band_order(blk, [ah, ah >> 1, ah >> 1])
+        if runs:
+            dc_end = itx_dc_runs(blk, bands)
     blocks = torch.from_numpy(blk.view(np.uint8).copy()).cuda()
     coef = torch.from_numpy(fr["coef"].copy()).cuda()
-    itx_frame(gpu, f, blocks, fr["size_start"], coef, flags, band_start=bands)
+    itx_frame(gpu, f, blocks, fr["size_start"], coef, flags, band_start=bands, dc_end=dc_end)
     torch.cuda.synchronize()
     return [f.plane_np(p) for p in range(len(fr["planes"]))], coef.cpu().numpy()
 
@@ -60,6 +62,65 @@ def test_itx_frame_1080p_matches_oracle(gpu, bpc, banded):
     for p in range(3):
         assert np.array_equal(got[p], ref[p])
     assert not coef_after.any()
+
+
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+@pytest.mark.parametrize("size", [(64, 64), (256, 192), (640, 360), (1920, 1080)])
+def test_itx_runs_match_oracle(gpu, bpc, size):
+    """mi_itx_frame_runs: every band's leading DC-only run on the DC path (up to 128 blocks per
+    workgroup), the rest on the transform path; pixels and the zeroed arena as the oracle's."""
+    w, h = size
+    fr = make_itx_frame(w, h, bpc=bpc, seed=w + bpc, with_wht=True, dc_frac=0.6)
+    got, coef_after = run_frame(gpu, fr, runs=True)
+    ref = oracle_lib.itx_frame([p.copy() for p in fr["planes"]], fr["blocks"], fr["coef"].copy(), bpc)
+    for p in range(3):
+        assert np.array_equal(got[p], ref[p]), (w, h, p)
+    assert not coef_after.any()
+
+
+def test_itx_runs_keep_coefs_and_all_dc(gpu):
+    # every block DC-only (the whole grid on the DC path), arena left untouched
+    fr = make_itx_frame(640, 360, bpc=10, seed=77, dc_frac=1.0)
+    got, coef_after = run_frame(gpu, fr, flags=ITX_KEEP_COEFS, runs=True)
+    ref = oracle_lib.itx_frame([p.copy() for p in fr["planes"]], fr["blocks"], fr["coef"].copy(), 10)
+    for p in range(3):
+        assert np.array_equal(got[p], ref[p]), p
+    assert np.array_equal(coef_after, fr["coef"])
+
+
+def test_itx_runs_reject_bad_tables_and_report_non_dc_blocks(gpu):
+    import ctypes
+    from rav1d_amd.frame import _stream_ptr
+    fr = make_itx_frame(256, 192, bpc=10, seed=9, dc_frac=0.6)
+    ah = 256
+    blk, _, bands = itx_band_order(fr["blocks"], [ah, ah >> 1, ah >> 1])
+    dc_end = itx_dc_runs(blk, bands)
+    f = Frame(256, 192, 10, 1)
+    blocks = torch.from_numpy(blk.view(np.uint8).copy()).cuda()
+    coef = torch.from_numpy(fr["coef"].copy()).cuda()
+    pic = f.picture()
+    bs = (ctypes.c_uint32 * 171)(*[int(v) for v in bands.reshape(-1)])
+
+    def call(de):
+        arr = (ctypes.c_uint32 * 152)(*[int(v) for v in de.reshape(-1)])
+        return lib().mi_itx_frame_runs(gpu.h, ctypes.byref(pic), ctypes.c_void_p(blocks.data_ptr()), bs, arr,
+                                       ctypes.c_void_p(coef.data_ptr()), ITX_KEEP_COEFS, _stream_ptr(None))
+    t, q = np.argwhere(bands[:, 1:] > bands[:, :-1])[0]
+    past = dc_end.copy()
+    past[t, q] = bands[t, q + 1] + 1           # a run ending past its band
+    assert call(past) == -22
+    before = dc_end.copy()
+    before[t, q] = bands[t, q] - 1 if bands[t, q] else 0
+    if bands[t, q]:
+        assert call(before) == -22
+    # a run that claims the band's transform blocks too: they are skipped and reported
+    t2, q2 = np.argwhere(bands[:, 1:] > dc_end)[0]
+    over = dc_end.copy()
+    over[t2, q2] = bands[t2, q2 + 1]
+    assert call(over) == 0
+    assert lib().mi_ctx_device_status(gpu.h, _stream_ptr(None)) == -22
+    assert call(dc_end) == 0
+    assert lib().mi_ctx_device_status(gpu.h, _stream_ptr(None)) == 0
 
 
 @pytest.mark.parametrize("bpc", [8, 10, 12])

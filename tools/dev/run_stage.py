@@ -49,8 +49,8 @@ def mc_split(p):
 
 
 def itx(p):
-    F.check(L.mi_itx_frame_banded(ctx.h, ctypes.byref(pa), ctypes.c_void_p(pipe.blocks.data_ptr()), pipe.itx_bands,
-                                  ctypes.c_void_p(pipe.coefs[0].data_ptr()), bench.ITX_KEEP_COEFS, p), "itx")
+    F.check(L.mi_itx_frame_runs(ctx.h, ctypes.byref(pa), ctypes.c_void_p(pipe.blocks.data_ptr()), pipe.itx_bands,
+                                pipe.itx_dc_end, ctypes.c_void_p(pipe.coefs[0].data_ptr()), bench.ITX_KEEP_COEFS, p), "itx")
 
 
 for _ in range(int(os.environ.get("REPS", "10"))):
