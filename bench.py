@@ -30,9 +30,9 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from rav1d_amd import ITX_KEEP_COEFS  # noqa: E402
+from rav1d_amd import ITX_DC_DEFER, ITX_KEEP_COEFS  # noqa: E402
 from rav1d_amd import frame as F  # noqa: E402
-from rav1d_amd.synth import frame_bytes, itx_algorithmic_bytes, itx_band_order, itx_dc_runs, make_frame, mc_algorithmic_bytes, mc_sync_ok  # noqa: E402
+from rav1d_amd.synth import dc_map_bytes, frame_bytes, itx_algorithmic_bytes, itx_band_order, itx_dc_runs, make_frame, mc_algorithmic_bytes, mc_sync_ok  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 W, H, BPC, LAYOUT = 3840, 2160, 10, 1
@@ -93,8 +93,11 @@ class Pipeline:
         self.algo = {
             # coefficients counted once: the device arena is the frame's staged
             # copy, read once and not zeroed (MI_ITX_KEEP_COEFS, as the frame executor runs it)
-            "itx": itx_algorithmic_bytes(fr["blocks"], bpc, zero_coefs=False),
-            "deblock": 2 * fb + lvl_bytes + mask_bytes,
+            # the DC-only blocks' constant goes through the DC map (MI_ITX_DC_DEFER): itx writes
+            # the map, deblock reads it while staging (as the frame executor runs inter frames
+            # without intra blocks)
+            "itx": itx_algorithmic_bytes(fr["blocks"], bpc, zero_coefs=False, dc_defer=True),
+            "deblock": 2 * fb + lvl_bytes + mask_bytes + dc_map_bytes(w, h, lay),
             "cdef": 2 * fb + mask_bytes,
             "lr": 2 * fb + fb * 4 // 64 + fr["lr"]["lr_mask"].nbytes,
             "fg": 2 * fb,
@@ -151,8 +154,8 @@ class Pipeline:
         self.k += 1
         timed("itx", lambda: F.check(lib.mi_itx_frame_runs(ctx, ctypes.byref(pa), ctypes.c_void_p(self.blocks.data_ptr()),
                                                            self.itx_bands, self.itx_dc_end, ctypes.c_void_p(coef.data_ptr()),
-                                                           ITX_KEEP_COEFS, sp), "itx"))
-        timed("deblock", lambda: F.check(lib.mi_deblock_frame_to(ctx, ctypes.byref(pa), ctypes.byref(pd),
+                                                           ITX_KEEP_COEFS | ITX_DC_DEFER, sp), "itx"))
+        timed("deblock", lambda: F.check(lib.mi_deblock_frame_dc(ctx, ctypes.byref(pa), ctypes.byref(pd),
                                                                  ctypes.byref(self.lf.s), sp), "lf"))
         timed("cdef", lambda: F.check(lib.mi_cdef_frame(ctx, ctypes.byref(pd), ctypes.byref(pb),
                                                         ctypes.byref(self.cdef.s), sp), "cdef"))

@@ -342,6 +342,12 @@ int mi_itx_frame_banded(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *block
  * <= band_start[s][q + 1]. The runs take a DC path (many blocks per workgroup, whole line
  * segments); a block in a run that is not DC-only is skipped and reported by
  * mi_ctx_device_status (-EINVAL). Same pixels as mi_itx_frame over the same blocks. */
+/* MI_ITX_DC_DEFER (mi_itx_frame_runs only): the DC runs' constants are not added to the
+ * pixels; the context records them per 4x4 unit for the next mi_deblock_frame_dc, which adds
+ * them to the pixels it stages, so the deblocked picture equals that of the undeferred call
+ * while the reconstruction `pic` lacks them (for frames whose reconstruction nothing else reads:
+ * no intra block predicts from it). Under stream capture the flag is ignored. */
+#define MI_ITX_DC_DEFER 2u
 int mi_itx_frame_runs(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
                       const uint32_t band_start[MI_N_RECT_TX_SIZES][MI_ITX_BANDS + 1],
                       const uint32_t dc_end[MI_N_RECT_TX_SIZES][MI_ITX_BANDS], void *coef, unsigned flags,
@@ -410,6 +416,12 @@ int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, v
  * bit-identical to mi_deblock_frame. Planes and strides must be 16-byte aligned. With
  * src == dst it runs mi_deblock_frame (in place). */
 int mi_deblock_frame_to(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const MiLoopFilter *lf,
+                        void *stream);
+/* mi_deblock_frame_to that adds, while staging, the DC runs the context's last
+ * mi_itx_frame_runs(MI_ITX_DC_DEFER) recorded (src never written; with lf->filter_y == 0 the
+ * output is src plus the DC). Without a pending deferral it is mi_deblock_frame_to. The picture
+ * geometry must be the deferring call's and src != dst (-EINVAL otherwise). */
+int mi_deblock_frame_dc(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const MiLoopFilter *lf,
                         void *stream);
 
 /* Motion compensation for a whole frame: writes the inter prediction of every unit into

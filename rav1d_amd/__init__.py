@@ -112,6 +112,7 @@ MC_NCLASS = 64
 
 N_RECT_TX_SIZES = 19
 ITX_KEEP_COEFS = 1
+ITX_DC_DEFER = 2       # mi_itx_frame_runs: DC runs deferred to mi_deblock_frame_dc
 
 _VP = ctypes.c_void_p
 
@@ -194,6 +195,8 @@ def lib():
     _sig(L, "mi_deblock_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiLoopFilter), _VP])
     _sig(L, "mi_deblock_frame_to", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
                                                   ctypes.POINTER(MiLoopFilter), _VP])
+    _sig(L, "mi_deblock_frame_dc", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
+                                                  ctypes.POINTER(MiLoopFilter), _VP])
     _sig(L, "mi_cdef_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
                                             ctypes.POINTER(MiCdef), _VP])
     _sig(L, "mi_lr_frame", ctypes.c_int, [_VP, ctypes.POINTER(MiPicture), ctypes.POINTER(MiPicture),
@@ -224,7 +227,7 @@ def lib():
 # Every symbol include/mi_av1dsp.h declares (checked by tests/test_abi.py).
 EXPORTED = ["mi_version", "mi_ctx_create", "mi_ctx_destroy", "mi_ctx_last_error",
             "mi_itx_frame", "mi_itx_frame_banded", "mi_itx_frame_runs", "mi_mc_frame", "mi_mc_frame_ex", "mi_mc_frame_sync", "mi_mc_sync_status", "mi_mc_scaled", "mi_mc_warp", "mi_mc_combine", "mi_superres_frame",
-            "mi_ipred_blocks", "mi_intra_blocks", "mi_intra_recon", "mi_ctx_device_status", "mi_deblock_frame", "mi_deblock_frame_to", "mi_cdef_frame", "mi_lr_frame", "mi_lr_tile_order", "mi_cdef_tile_order",
+            "mi_ipred_blocks", "mi_intra_blocks", "mi_intra_recon", "mi_ctx_device_status", "mi_deblock_frame", "mi_deblock_frame_to", "mi_deblock_frame_dc", "mi_cdef_frame", "mi_lr_frame", "mi_lr_tile_order", "mi_cdef_tile_order",
             "mi_film_grain_frame", "mi_film_grain_prep", "mi_film_grain_apply", "mi_frame_run", "mi_frame_end", "mi_frame_validate", "mi_frame_plan_ms",
             "mi_ctx_set_timing", "mi_ctx_timing",
             "mi_dsp_itxfm_add", "mi_dsp_intra_pred", "mi_dsp_cfl_pred", "mi_dsp_pal_pred", "mi_dsp_cfl_ac",

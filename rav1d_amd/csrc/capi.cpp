@@ -165,6 +165,8 @@ static int itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
     a.coef = (uint8_t *)coef;
     a.bdmax = (1 << pic->bpc) - 1;
     a.zero_coefs = (flags & MI_ITX_KEEP_COEFS) ? 0 : 1;
+    if (flags & ~(MI_ITX_KEEP_COEFS | MI_ITX_DC_DEFER)) return fail(ctx, -EINVAL);
+    if ((flags & MI_ITX_DC_DEFER) && !dc_end) return fail(ctx, -EINVAL);
     {
         const int sh = pic->layout == 1 || pic->layout == 2, sv = pic->layout == 1;
         const int aw = (pic->w + 127) & ~127, ah = (pic->h + 127) & ~127;
@@ -178,6 +180,40 @@ static int itx_frame(MiCtx *ctx, const MiPicture *pic, const MiTxBlock *blocks,
     for (int k = 0; k < MI_N_RECT_TX_SIZES; k++)
         if (size_start[k + 1] < size_start[k]) return fail(ctx, -EINVAL);
     const int wg = mi::itx_fill_schedule(a, size_start, band_start, dc_end);
+    if (flags & MI_ITX_DC_DEFER) {
+        // the DC runs go to the context's DC map for the next mi_deblock_frame_dc; under stream
+        // capture they are added to the pixels as without the flag (a tag fixed in a graph would
+        // let a replay match the map entries of the previous replay)
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing((hipStream_t)stream, &cap) != hipSuccess) return fail(ctx, -EIO);
+        ctx->dc_pending = 0;
+        if (cap == hipStreamCaptureStatusNone) {
+            const mi::DcMapGeom g = mi::dc_map_geom(pic->w, pic->h, pic->layout);
+            if (g.entries > ctx->dc_map_n) {
+                if (ctx->dc_map) (void)hipFree(ctx->dc_map);
+                ctx->dc_map = nullptr;
+                ctx->dc_map_n = 0;
+                if (hipMalloc(&ctx->dc_map, g.entries * 4) != hipSuccess) return fail(ctx, -ENOMEM);
+                if (hipMemsetAsync(ctx->dc_map, 0, g.entries * 4, (hipStream_t)stream) != hipSuccess) return fail(ctx, -EIO);
+                ctx->dc_map_n = g.entries;
+                ctx->dc_tag = 0;
+            }
+            if (++ctx->dc_tag > 0xffffu) {   // the 16-bit tag wraps: no stale entry may match
+                if (hipMemsetAsync(ctx->dc_map, 0, ctx->dc_map_n * 4, (hipStream_t)stream) != hipSuccess) return fail(ctx, -EIO);
+                ctx->dc_tag = 1;
+            }
+            a.dc_map = ctx->dc_map;
+            for (int p = 0; p < 3; p++) {
+                a.dc_off[p] = g.off[p];
+                a.dc_stride[p] = g.stride[p];
+            }
+            a.dc_tag = ctx->dc_tag;
+            ctx->dc_pending = ctx->dc_tag;
+            ctx->dc_w = pic->w;
+            ctx->dc_h = pic->h;
+            ctx->dc_layout = pic->layout;
+        }
+    }
     if (wg == 0) return 0;
     if (!blocks || !coef) return fail(ctx, -EINVAL);
     // One launch (itx.hip): the large sizes' workgroups first, the small ones fill in around
@@ -535,12 +571,33 @@ int mi_deblock_frame(MiCtx *ctx, const MiPicture *pic, const MiLoopFilter *lf, v
     return r ? fail(ctx, -EIO) : 0;
 }
 
+static int deblock_tiles(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const MiLoopFilter *lf,
+                         void *stream, uint32_t dc_tag);
+
 int mi_deblock_frame_to(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const MiLoopFilter *lf,
                         void *stream) {
+    return deblock_tiles(ctx, src, dst, lf, stream, 0);
+}
+
+int mi_deblock_frame_dc(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const MiLoopFilter *lf,
+                        void *stream) {
+    if (!ctx) return -EINVAL;
+    const uint32_t tag = ctx->dc_pending;
+    ctx->dc_pending = 0;
+    if (tag && (!src || src->w != ctx->dc_w || src->h != ctx->dc_h || src->layout != ctx->dc_layout))
+        return fail(ctx, -EINVAL);
+    return deblock_tiles(ctx, src, dst, lf, stream, tag);
+}
+
+static int deblock_tiles(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, const MiLoopFilter *lf,
+                         void *stream, uint32_t dc_tag) {
     if (!ctx || !src || !dst || !lf) return fail(ctx, -EINVAL);
     if (src->bpc != 8 && src->bpc != 10 && src->bpc != 12) return fail(ctx, -EINVAL);
     if (!same_geometry(src, dst)) return fail(ctx, -EINVAL);
-    if (src->data[0] == dst->data[0]) return mi_deblock_frame(ctx, dst, lf, stream);
+    if (src->data[0] == dst->data[0]) {
+        if (dc_tag) return fail(ctx, -EINVAL);   // deferred DC needs the out-of-place tiles
+        return mi_deblock_frame(ctx, dst, lf, stream);
+    }
     const int sh = src->layout == 1 || src->layout == 2, sv = src->layout == 1;
     const int nplanes = src->layout == 0 ? 1 : 3;
     const size_t px = src->bpc == 8 ? 1 : 2;
@@ -549,7 +606,8 @@ int mi_deblock_frame_to(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, 
         if (src->stride[p ? 1 : 0] % 16 || (uintptr_t)src->data[p] % 16 || (uintptr_t)dst->data[p] % 16 ||
             src->stride[p ? 1 : 0] < (ptrdiff_t)(((sb128w * 128) >> (p ? sh : 0)) * px))
             return fail(ctx, -EINVAL);
-    if (!lf->filter_y) {   // deblocking off for the frame: the output is the input
+    const bool edges = lf->filter_y != 0;
+    if (!edges && !dc_tag) {   // deblocking off for the frame: the output is the input
         for (int p = 0; p < nplanes; p++) {
             const size_t rows = (size_t)(sb128h * 128) >> (p ? sv : 0);
             const ptrdiff_t s = src->stride[p ? 1 : 0];
@@ -559,7 +617,7 @@ int mi_deblock_frame_to(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, 
         }
         return 0;
     }
-    if (!lf->level || !lf->masks || lf->sb128w != sb128w || lf->b4_stride < (int64_t)sb128w * 32)
+    if (edges && (!lf->level || !lf->masks || lf->sb128w != sb128w || lf->b4_stride < (int64_t)sb128w * 32))
         return fail(ctx, -EINVAL);
     mi::LfTileArgs a;
     memset(&a, 0, sizeof(a));
@@ -573,7 +631,7 @@ int mi_deblock_frame_to(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, 
     a.ss_ver = sv;
     a.bdmax = (1 << src->bpc) - 1;
     a.bdm8 = src->bpc - 8;
-    const int filter_uv = src->layout != 0 && lf->filter_uv;
+    const int filter_uv = edges && src->layout != 0 && lf->filter_uv;
     memcpy(a.lim_e, lf->lim_e, 64);
     memcpy(a.lim_i, lf->lim_i, 64);
     int n = 0;
@@ -586,15 +644,26 @@ int mi_deblock_frame_to(MiCtx *ctx, const MiPicture *src, const MiPicture *dst, 
         a.stride[p] = src->stride[p ? 1 : 0];
         a.pw[p] = (sb128w * 128) >> h;
         a.ph[p] = (sb128h * 128) >> v;
-        // filter_uv off: chroma tiles are copies (no edge codes)
-        a.cols_ux[p] = p && !filter_uv ? 0 : (a.w4 + h) >> h;
-        a.cols_rows[p] = p && !filter_uv ? 0 : a.ph[p];
-        a.rows_px[p] = p && !filter_uv ? 0 : a.pw[p];
-        a.rows_uy[p] = p && !filter_uv ? 0 : p ? sb128h * (32 >> v) : a.h4;
+        // filter_uv off: chroma tiles are copies (no edge codes); deblocking off (deferred DC
+        // only): every tile is a copy plus its units' DC
+        const bool off = !edges || (p && !filter_uv);
+        a.cols_ux[p] = off ? 0 : (a.w4 + h) >> h;
+        a.cols_rows[p] = off ? 0 : a.ph[p];
+        a.rows_px[p] = off ? 0 : a.pw[p];
+        a.rows_uy[p] = off ? 0 : p ? sb128h * (32 >> v) : a.h4;
         a.tiles_x[p] = (a.pw[p] + mi::kLfTW - 1) / mi::kLfTW;
         n += a.tiles_x[p] * ((a.ph[p] + mi::kLfTH - 1) / mi::kLfTH);
     }
     a.tile_start[3] = n;
+    if (dc_tag) {
+        const mi::DcMapGeom g = mi::dc_map_geom(src->w, src->h, src->layout);
+        a.dc_map = ctx->dc_map;
+        for (int p = 0; p < 3; p++) {
+            a.dc_off[p] = g.off[p];
+            a.dc_stride[p] = g.stride[p];
+        }
+        a.dc_tag = dc_tag;
+    }
     return mi::launch_deblock_tiles(a, src->bpc, (hipStream_t)stream) ? fail(ctx, -EIO) : 0;
 }
 

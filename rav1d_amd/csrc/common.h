@@ -130,7 +130,34 @@ struct ItxArgs {
     int nbands;         // 1 or 8
     int pw[3], ph[3];   // plane extents (128-aligned picture area; 0 = no such plane)
     int *err;           // device error word: set when a descriptor is rejected
+    // MI_ITX_DC_DEFER: the DC runs write their scaled DC into this per-4x4-unit map instead of
+    // adding it to the pixels (the next mi_deblock_frame_dc adds it while staging); entry =
+    // (dc_tag << 16) | (dc & 0xffff), plane p at dc_map + dc_off[p], dc_stride[p] entries a row
+    uint32_t *dc_map;
+    int64_t dc_off[3];
+    int dc_stride[3];
+    uint32_t dc_tag;
 };
+// the DC map of one picture geometry: one entry per 4x4 unit of the 128-aligned plane areas
+struct DcMapGeom {
+    int64_t off[3];
+    int stride[3], rows[3];
+    size_t entries;
+};
+inline DcMapGeom dc_map_geom(int w, int h, int layout) {
+    DcMapGeom g{};
+    const int aw = (w + 127) & ~127, ah = (h + 127) & ~127;
+    const int sh = layout == 1 || layout == 2, sv = layout == 1;
+    size_t n = 0;
+    for (int p = 0; p < (layout ? 3 : 1); p++) {
+        g.off[p] = (int64_t)n;
+        g.stride[p] = (p ? aw >> sh : aw) >> 2;
+        g.rows[p] = (p ? ah >> sv : ah) >> 2;
+        n += (size_t)g.stride[p] * g.rows[p];
+    }
+    g.entries = n;
+    return g;
+}
 
 // Legal TxfmType values of a RectTxfmSize (itx.rs:400-457, 1072-1110): bit t set when the
 // reference's itxfm_add[tx][t] slot is filled.
@@ -193,6 +220,12 @@ struct LfTileArgs {
     int pw[3], ph[3], tiles_x[3];   // staged plane area (128-aligned picture), tiles per row
     int tile_start[4];
     uint8_t lim_e[64], lim_i[64];
+    // mi_deblock_frame_dc: the DC map of mi_itx_frame_runs(MI_ITX_DC_DEFER) (null: none); its
+    // entries tagged dc_tag are added to the staged pixels (ItxArgs::dc_map's layout)
+    const uint32_t *dc_map;
+    int64_t dc_off[3];
+    int dc_stride[3];
+    uint32_t dc_tag;
 };
 int launch_deblock_tiles(const LfTileArgs &a, int bpc, hipStream_t s);
 // launchers (lf.hip)

@@ -28,6 +28,12 @@ struct MiCtx {
     size_t mc_flags_n = 0;
     uint32_t mc_epoch = 0;
     int *mc_err = nullptr;
+    // deferred DC runs (mi_itx_frame_runs MI_ITX_DC_DEFER -> mi_deblock_frame_dc): the map
+    // (zeroed when allocated and when its 16-bit tag wraps), its geometry and the pending tag
+    uint32_t *dc_map = nullptr;
+    size_t dc_map_n = 0;
+    int dc_w = 0, dc_h = 0, dc_layout = -1;
+    uint32_t dc_tag = 0, dc_pending = 0;
     // frame executor (frame_exec.cpp): device copy of one frame's descriptors, staged through
     // pinned host memory; `fx_ev` marks when the staging buffer may be rewritten
     uint8_t *fx_dev = nullptr, *fx_host = nullptr;
@@ -56,6 +62,7 @@ struct MiCtx {
         if (ir_done) (void)hipFree(ir_done);
         if (mc_flags) (void)hipFree(mc_flags);
         if (mc_err) (void)hipFree(mc_err);
+        if (dc_map) (void)hipFree(dc_map);
         if (ir_words) (void)hipFree(ir_words);
         if (ir_gran) (void)hipFree(ir_gran);
         if (ir_tl) (void)hipFree(ir_tl);

@@ -818,8 +818,13 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
                                                        (int)lap_s[k].size(), tmp, stream)))
                 return r;
         }
+        // DC-only residuals deferred into the deblocking pass (MI_ITX_DC_DEFER) when nothing
+        // reads the reconstruction itself: no intra block predicts from it, and deblocking runs
+        // out of place (its output is what CDEF, LR and the reference picture read)
+        const bool dc_defer = n == 0 && f->filter_y && pics->recon.data[0] != pics->deblocked.data[0];
         if (f->n_inter_tx &&
-            (r = mi_itx_frame_runs(ctx, &cur, (const MiTxBlock *)D(20), itx_bs, pl.itx_dc, D(4), MI_ITX_KEEP_COEFS, stream)))
+            (r = mi_itx_frame_runs(ctx, &cur, (const MiTxBlock *)D(20), itx_bs, pl.itx_dc, D(4),
+                                   MI_ITX_KEEP_COEFS | (dc_defer ? MI_ITX_DC_DEFER : 0u), stream)))
             return r;
     }
 
@@ -876,7 +881,8 @@ int frame_run(MiCtx *ctx, const MiDecFrame *f, const MiFramePictures *pics, int 
         lf.filter_uv = f->filter_uv;
         memcpy(lf.lim_e, f->lim_e, 64);
         memcpy(lf.lim_i, f->lim_i, 64);
-        if ((r = mi_deblock_frame_to(ctx, cur, &cp[1], &lf, stream))) return r;
+        // (adds the DC runs an inter frame's residual call deferred, if any)
+        if ((r = mi_deblock_frame_dc(ctx, cur, &cp[1], &lf, stream))) return r;
         cur = &cp[1];
         idx = 1;
     }

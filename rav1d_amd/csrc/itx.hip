@@ -366,6 +366,8 @@ __device__ __forceinline__ void itx_dc(const ItxArgs &a, int lwg, uint8_t *lds) 
     uint8_t *const plane3[3] = { a.plane[0], a.plane[1], a.plane[2] };
     const int64_t stride3[3] = { a.stride[0], a.stride[1], a.stride[2] };
     const int pw3[3] = { a.pw[0], a.pw[1], a.pw[2] }, ph3[3] = { a.ph[0], a.ph[1], a.ph[2] };
+    const int64_t dco3[3] = { a.dc_off[0], a.dc_off[1], a.dc_off[2] };
+    const int dcs3[3] = { a.dc_stride[0], a.dc_stride[1], a.dc_stride[2] };
     ItxDcRec *rec = reinterpret_cast<ItxDcRec *>(lds);
     // descriptors -> records (base, stride) in LDS; each lane keeps its blocks' DC coefficient
     // load in flight and writes the scaled DC only after the pixel loads below are issued, so
@@ -387,9 +389,16 @@ __device__ __forceinline__ void itx_dc(const ItxArgs &a, int lwg, uint8_t *lds) 
                                 b.x + W <= sel3(pw3, b.plane) && b.y + H <= sel3(ph3, b.plane);
                 if (ok) {
                     dcp[rr] = reinterpret_cast<const Cf *>(a.coef) + b.coef_off;
-                    const int64_t st = sel3(stride3, b.plane);
-                    r.base = sel3(plane3, b.plane) + (int64_t)b.y * st + (int64_t)b.x * sizeof(Px);
-                    r.st = (int)st;
+                    if (a.dc_map) {
+                        // MI_ITX_DC_DEFER: the block's first entry of the DC map
+                        const int ms = sel3(dcs3, b.plane);
+                        r.base = reinterpret_cast<uint8_t *>(a.dc_map + sel3(dco3, b.plane) + (int64_t)(b.y >> 2) * ms + (b.x >> 2));
+                        r.st = ms * 4;
+                    } else {
+                        const int64_t st = sel3(stride3, b.plane);
+                        r.base = sel3(plane3, b.plane) + (int64_t)b.y * st + (int64_t)b.x * sizeof(Px);
+                        r.st = (int)st;
+                    }
                 } else {
                     atomicOr(a.err, 2);
                 }
@@ -399,6 +408,36 @@ __device__ __forceinline__ void itx_dc(const ItxArgs &a, int lwg, uint8_t *lds) 
     }
 #pragma unroll
     for (int rr = 0; rr < NR; rr++) dcv[rr] = dcp[rr] ? (int)dcp[rr][0] : 0;
+    if (a.dc_map) {
+        // deferred: every 4x4 unit of the run's blocks gets its block's tagged DC
+        constexpr int UW = W / 4, IPBM = UW * (H / 4);
+        static_assert(IPBM * NB <= 64 * kItxDcItems, "map items fit the pixel sweep's budget");
+#pragma unroll
+        for (int rr = 0; rr < NR; rr++) {
+            const int t = rr * 64 + lane;
+            if (dcp[rr]) {
+                int dc = dcv[rr];
+                if (a.zero_coefs) *const_cast<Cf *>(dcp[rr]) = 0;
+                if (Rect2) dc = (dc * 181 + 128) >> 8;
+                dc = (dc * 181 + 128) >> 8;
+                dc = (dc + Rnd) >> Shift;
+                dc = (dc * 181 + 128 + 2048) >> 12;
+                rec[t].dc = dc;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kItxDcItems; i++) {
+            const int j = lane + 64 * i, blk = j / IPBM;
+            if (i * 64 < IPBM * NB && blk < nb) {
+                const ItxDcRec r = rec[blk];
+                if (r.base)
+                    *reinterpret_cast<uint32_t *>(r.base + (int64_t)((j / UW) % (H / 4)) * r.st + (j % UW) * 4) =
+                        (a.dc_tag << 16) | ((uint32_t)r.dc & 0xffffu);
+            }
+        }
+        return;
+    }
     __syncthreads();
     V px[kItxDcItems];
 #pragma unroll

@@ -712,6 +712,66 @@ __device__ __forceinline__ void lf_commit_pixels(Px *t, const uint4 (&sv)[LfShap
     }
 }
 
+// ---- deferred DC runs (mi_deblock_frame_dc) ----
+// mi_itx_frame_runs(MI_ITX_DC_DEFER) leaves the DC-only blocks' constant out of the pixels and
+// records it per 4x4 unit (tagged with the call's 16-bit tag); the tile adds it while staging,
+// so the deblocked picture is the one of the undeferred residual and the DC-only blocks cost
+// no pass of their own over the picture. kLfDcW x kLfDcH units cover the staged image.
+constexpr int kLfDcW = kLfCols / 4, kLfDcH = kLfRows / 4;
+static_assert(kLfDcW % 2 == 0 && (kLfDcW * kLfDcH) / 2 <= kLfThreads, "two map entries per lane");
+
+// each lane's two map entries (units 2 tid, 2 tid + 1 of the staged image): one 8-B load
+__device__ __forceinline__ uint2 lf_dc_fetch(const LfTileArgs &a, const LfTile &g) {
+    const int e = 2 * (int)threadIdx.x;
+    uint2 v = make_uint2(0, 0);
+    if (e < kLfDcW * kLfDcH) {
+        const int uy = (g.y0 >> 2) - 3 + e / kLfDcW, ux = (g.x0 >> 2) - 4 + e % kLfDcW;
+        const int st = KARG_OF(LfTileArgs, dc_stride, g.p);
+        if (uy >= 0 && uy < (g.ph >> 2) && ux >= 0 && ux + 1 < st)
+            v = *reinterpret_cast<const uint2 *>(a.dc_map + KARG_OF(LfTileArgs, dc_off, g.p) + (int64_t)uy * st + ux);
+    }
+    return v;
+}
+// the entries' DC (0 for another call's tag) into the tile's LDS table
+__device__ __forceinline__ void lf_dc_commit(const LfTileArgs &a, uint2 v, int *dcs) {
+    const int e = 2 * (int)threadIdx.x;
+    if (e < kLfDcW * kLfDcH) {
+        dcs[e] = (v.x >> 16) == a.dc_tag ? (int)(int16_t)(v.x & 0xffff) : 0;
+        dcs[e + 1] = (v.y >> 16) == a.dc_tag ? (int)(int16_t)(v.y & 0xffff) : 0;
+    }
+}
+// the staged vectors plus their units' DC, clipped to [0, bdmax], into LDS
+template <typename Px>
+__device__ __forceinline__ void lf_commit_pixels_dc(Px *t, const uint4 (&sv)[LfShape<Px>::NS], const int *dcs, int bdmax) {
+    using S = LfShape<Px>;
+    const int tid = (int)threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < S::NS; j++) {
+        const int i = tid + kLfThreads * j;
+        if (i < kLfRows * S::VPR) {
+            const int r = i / S::VPR, c = (i % S::VPR) * S::VPX;
+            const int *d = dcs + (r >> 2) * kLfDcW + (c >> 2);
+            uint32_t w[4] = { sv[j].x, sv[j].y, sv[j].z, sv[j].w };
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if constexpr (sizeof(Px) == 2) {
+                    // pixels 2k, 2k + 1 (one unit: (2k) / 4) in packed 16-bit arithmetic: a pixel
+                    // (< 4096) plus a DC (|dc| < 2^15 - 4096 for 12-bit coefficients) fits int16
+                    const lf_s2 v = __builtin_bit_cast(lf_s2, w[k]) + pk_splat(d[k >> 1]);
+                    w[k] = __builtin_bit_cast(uint32_t, pk_clamp(v, pk_splat(0), pk_splat(bdmax)));
+                } else {
+                    const int dc = d[k];        // pixels 4k .. 4k + 3: unit k
+                    uint32_t o = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; b++) o |= (uint32_t)min(max((int)((w[k] >> (8 * b)) & 0xff) + dc, 0), bdmax) << (8 * b);
+                    w[k] = o;
+                }
+            }
+            *reinterpret_cast<uint4 *>(&t[r * S::P + c]) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+}
+
 // Decode the edge units and bucket the filtered ones by width class (cnt[] zeroed and visible)
 template <typename Px>
 __device__ __forceinline__ void lf_build_lists(const LfTile &g, const LfEdgeRaw (&raw)[LfShape<Px>::NU],
@@ -762,6 +822,7 @@ __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
     __shared__ uint16_t listv[2][S::NV], listh[2][S::NH];
     __shared__ int cnt[8];
     __shared__ uint8_t le[64], li[64];
+    __shared__ int dcs[kLfDcW * kLfDcH];   // deferred DC per staged 4x4 unit (mi_deblock_frame_dc)
     const int tid = threadIdx.x;
     KTL(0);
     if (tid < 64) { le[tid] = a.lim_e[tid]; li[tid] = a.lim_i[tid]; }
@@ -770,8 +831,16 @@ __global__ __launch_bounds__(kLfThreads) void lf_tile_kernel(LfTileArgs a) {
     __syncthreads();
     uint4 sv[S::NS];
     LfEdgeRaw raw[S::NU];
+    // the DC map's entries first (after the pixels: no measurable difference)
+    const uint2 dcv = a.dc_map ? lf_dc_fetch(a, g) : make_uint2(0, 0);
     lf_fetch<Px>(a, g, sv, raw);
-    lf_commit_pixels<Px>(t, sv);
+    if (a.dc_map) {
+        lf_dc_commit(a, dcv, dcs);
+        __syncthreads();
+        lf_commit_pixels_dc<Px>(t, sv, dcs, a.bdmax);
+    } else {
+        lf_commit_pixels<Px>(t, sv);
+    }
     KTL(1);
     lf_build_lists<Px>(g, raw, listv, listh, cnt);
     __syncthreads();

@@ -208,9 +208,10 @@ def itx_dc_runs(blocks, band_start):
     return dc_end
 
 
-def itx_algorithmic_bytes(blocks, bpc, zero_coefs=True):
+def itx_algorithmic_bytes(blocks, bpc, zero_coefs=True, dc_defer=False):
     """sum over blocks of coefB*n_coef (+ the zeroing write) + 2*pixB*w*h,
-    plus the 16-byte descriptor."""
+    plus the 16-byte descriptor. dc_defer (MI_ITX_DC_DEFER): a DC-only block writes its 4-byte
+    DC-map entry per 4x4 unit instead of reading and writing its pixels."""
     pxb = 1 if bpc == 8 else 2
     cb = 2 if bpc == 8 else 4
     dims = np.array(TX_DIMS)
@@ -219,8 +220,23 @@ def itx_algorithmic_bytes(blocks, bpc, zero_coefs=True):
     ncoef = np.minimum(w, 32) * np.minimum(h, 32)
     dconly = (blocks["txtp"] == 0) & (blocks["eob"] < 1)
     ncoef = np.where(dconly, 1, ncoef)
-    per = cb * ncoef * (2 if zero_coefs else 1) + 2 * pxb * w * h + 16
+    pix = 2 * pxb * w * h
+    if dc_defer:
+        pix = np.where(dconly, 4 * (w // 4) * (h // 4), pix)
+    per = cb * ncoef * (2 if zero_coefs else 1) + pix + 16
     return int(per.sum())
+
+
+def dc_map_bytes(w, h, layout):
+    """Bytes of the deferred-DC map (one 4-byte entry per 4x4 unit of the 128-aligned planes,
+    rav1d_amd/csrc/common.h dc_map_geom): what mi_deblock_frame_dc reads on top of the picture."""
+    aw, ah = (w + 127) & ~127, (h + 127) & ~127
+    sh = 1 if layout in (1, 2) else 0
+    sv = 1 if layout == 1 else 0
+    n = (aw >> 2) * (ah >> 2)
+    if layout:
+        n += 2 * ((aw >> sh) >> 2) * ((ah >> sv) >> 2)
+    return 4 * n
 
 
 # ---------------------------------------------------------------------------------------

@@ -21,7 +21,7 @@ for k in $(seq ${PASSES:-3}); do
   for v in base "$@"; do
     if [ "${BENCH:-0}" = 1 ]; then
       MI_LIB=$(lib_of $v) timeout -k 10 200 python $R/bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-fg --no-intra --no-extra > $OUT/bench_${v}_$k.json || { echo "$v bench failed"; exit 1; }
-      python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], d['value'], d['ms_per_step'], d.get('verified'))" $OUT/bench_${v}_$k.json $v
+      python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], d['value'], d['ms_per_step'], d.get('verified'), d.get('stage_ms'))" $OUT/bench_${v}_$k.json $v
     else
       MI_LIB=$(lib_of $v) STAGE=${STAGE:?set STAGE} REPS=1 TIME=1 timeout -k 10 120 python -u $R/tools/dev/run_stage.py 2>&1 | tail -1 | sed "s/^/$v /" || exit 1
     fi
