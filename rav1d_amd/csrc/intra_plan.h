@@ -84,21 +84,30 @@ int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<in
     }
     // The owner of a cell is its LAST writer in decode order: an inter-intra item and the
     // residual items over the same rectangle (MI_INTRA_II then MI_INTRA_RESID) overlap, and the
-    // residual must win. Several threads fill the map, so each cell keeps the maximum index
-    // (a relaxed CAS loop; the pool's join orders it before the reads below).
+    // residual must win. One range walks the blocks in decode order, so a plain store leaves the
+    // last writer; with several ranges on several threads a cell keeps the maximum index (a
+    // relaxed CAS loop; the pool's join orders it before the reads below). The CAS costs ~6 ms
+    // on a 4K10 intra frame's 168 K blocks on one thread, the plain store 0.5.
     par(n, 32768, [&](int lo, int hi, int) {
+        const bool whole = lo == 0 && hi == n;
         for (int i = lo; i < hi; i++) {
             const MiIntraBlock &b = f->intra[i];
             const int xl = b.plane ? b.x << ssh : b.x;
             strip[i] = (int8_t)(std::upper_bound(sx.begin(), sx.end(), xl) - sx.begin() - 1);
-            for (int y = b.y >> 2; y < (b.y + b.h) >> 2; y++)
+            for (int y = b.y >> 2; y < (b.y + b.h) >> 2; y++) {
+                int32_t *row = &own[b.plane][(size_t)y * pw4[b.plane]];
                 for (int x = b.x >> 2; x < (b.x + b.w) >> 2; x++) {
-                    int32_t *cell = &own[b.plane][(size_t)y * pw4[b.plane] + x];
+                    int32_t *cell = row + x;
+                    if (whole) {
+                        *cell = i;
+                        continue;
+                    }
                     int32_t cur = __atomic_load_n(cell, __ATOMIC_RELAXED);
                     while (cur < i && !__atomic_compare_exchange_n(cell, &cur, i, true, __ATOMIC_RELAXED,
                                                                    __ATOMIC_RELAXED)) {
                     }
                 }
+            }
         }
     });
     xs.assign(n + 1, 0);

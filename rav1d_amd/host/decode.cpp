@@ -734,17 +734,33 @@ void FrameDec::add_deps(int plane, int x0, int y0, int x1, int y1, std::vector<i
     x0 = imax(x0, (ts->col_start * 4) >> sh);
     y0 = imax(y0, (ts->row_start * 4) >> sv);
     const Span<int32_t> &o = owner[plane];
-    for (int y = y0 >> 2; y < (y1 + 3) >> 2; y++)
-        for (int x = x0 >> 2; x < (x1 + 3) >> 2; x++) {
-            if (x < 0 || y < 0 || x >= owner_stride) continue;
-            const size_t k = (size_t)y * owner_stride + x;
-            if (k >= o.size()) continue;
-            const int32_t v = o[k];
+    // (the unit range clipped once; runs of units with one owner are checked once: an edge
+    // mostly lies along few, large neighbours)
+    const int ux0 = imax(x0 >> 2, 0), ux1 = imin((x1 + 3) >> 2, owner_stride);
+    const int uy0 = imax(y0 >> 2, 0), uy1 = (y1 + 3) >> 2;
+    int32_t last = -1;
+    // a one-unit-wide column (a left edge) jumps over the rows its current owner covers: every
+    // cell of a block's rectangle holds that block unless a later item overwrote it, which only
+    // happens under an inter-intra item (MI_INTRA_II; its residual items follow it)
+    const bool column = ux1 - ux0 == 1;
+    for (int y = uy0; y < uy1; y++) {
+        const size_t row = (size_t)y * owner_stride;
+        if (row >= o.size()) break;
+        const int xe = (int)std::min<size_t>((size_t)ux1, o.size() - row);
+        for (int x = ux0; x < xe; x++) {
+            const int32_t v = o[row + x];
             if (v < 0) continue;
+            if (column && (size_t)v < fw.intra.size()) {
+                const MiIntraBlock &ob = fw.intra[v];
+                if (ob.plane == plane && !(ob.flags & MI_INTRA_II)) y = imax(y, ((ob.y + ob.h) >> 2) - 1);
+            }
+            if (v == last) continue;
+            last = v;
             bool dup = false;
             for (int32_t d : out) dup |= d == v;
             if (!dup) out.push_back(v);
         }
+    }
 }
 
 void FrameDec::emit_intra(const Block &b, int edge_flags, const uint8_t *pal_idx, const uint16_t (*pal)[8]) {
