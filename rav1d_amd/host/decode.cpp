@@ -738,6 +738,9 @@ void FrameDec::add_deps(int plane, int x0, int y0, int x1, int y1, std::vector<i
     // mostly lies along few, large neighbours)
     const int ux0 = imax(x0 >> 2, 0), ux1 = imin((x1 + 3) >> 2, owner_stride);
     const int uy0 = imax(y0 >> 2, 0), uy1 = (y1 + 3) >> 2;
+    // duplicates by a stamp per dependency list (a new list starts empty), not by scanning the
+    // list: a CfL block's luma rectangle can hold hundreds of owners
+    if (out.empty()) ++dep_stamp;
     int32_t last = -1;
     // a one-unit-wide column (a left edge) jumps over the rows its current owner covers: every
     // cell of a block's rectangle holds that block unless a later item overwrote it, which only
@@ -756,9 +759,10 @@ void FrameDec::add_deps(int plane, int x0, int y0, int x1, int y1, std::vector<i
             }
             if (v == last) continue;
             last = v;
-            bool dup = false;
-            for (int32_t d : out) dup |= d == v;
-            if (!dup) out.push_back(v);
+            if ((size_t)v >= dep_seen.size()) dep_seen.resize(std::max<size_t>((size_t)v + 1, 2 * dep_seen.size()), 0);
+            if (dep_seen[v] == dep_stamp) continue;
+            dep_seen[v] = dep_stamp;
+            out.push_back(v);
         }
     }
 }

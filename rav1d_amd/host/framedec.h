@@ -184,6 +184,8 @@ private:
     Span<uint8_t> f2d_map;
     int rmv_stride = 0;
     std::vector<int32_t> dep_tmp;     // one block's dependency list (reused)
+    std::vector<uint32_t> dep_seen;   // add_deps: per owner, the stamp of the list holding it
+    uint32_t dep_stamp = 0;
     RefMvBlock &rmv_at(int y4, int x4) { return rmv[(size_t)(y4 + 8) * rmv_stride + (x4 + 8)]; }
     uint8_t &f2d_at(int y4, int x4) { return f2d_map[(size_t)(y4 + 8) * rmv_stride + (x4 + 8)]; }
     void splat(const RefMvBlock &r, int bw4, int bh4);
