@@ -802,6 +802,9 @@ def parse_args(argv):
                     help="also time two independent frames per step on two streams (two_frames_in_flight; "
                          "reported beside the headline, never as `value`)")
     ap.add_argument("--stagger", type=int, default=0, help="with --inflight > 1: frame k's MC waits for frame k-1's")
+    ap.add_argument("--dense-coefs", action="store_true",
+                    help="the coefficient arena dense (min(w,32) x min(h,32) per non-DC block) instead of "
+                         "the front-end's packed corners (MI_TX_PACKED)")
     ap.add_argument("--mv", choices=["uniform", "coherent"], default="uniform",
                     help="motion field of the timed frame (uniform: SURVEY.md 8(d) config 3)")
     return ap.parse_args(argv)
@@ -842,7 +845,7 @@ def replicas(args, world, rank, local, hw):
     cfg = broadcast_config({"w": fw, "h": fh, "bpc": BPC, "layout": LAYOUT,
                             "seeds": [0x4C100001 + r for r in range(world)]}, world)
     fr = make_frame(cfg["w"], cfg["h"], cfg["bpc"], cfg["layout"], seed=cfg["seeds"][rank], with_fg=False,
-                    with_mc=True, mv_mode=args.mv)
+                    with_mc=True, mv_mode=args.mv, packed=not args.dense_coefs)
     ctx = hw.context(local)
     # one pre-filled coefficient arena per timed step (each step reads a fresh one)
     ring = min(max(args.steps, 1), 512)

@@ -52,14 +52,27 @@ typedef struct MiPicture {
 /* One transform block of the frame's coefficient arena (pass-2 input of itxfm_add:
  * src/recon.rs:1781-1788, 2674-2682, 3116, 4013). The arena stores each block's
  * coefficients column-major with column height min(h,32) — exactly the layout itxfm_add
- * reads (coeff[y + x*sh], src/itx.rs:128-142). 16 bytes. */
+ * reads (coeff[y + x*sh], src/itx.rs:128-142). 16 bytes.
+ *
+ * Packed blocks (flags & MI_TX_PACKED): every non-zero coefficient lies in the top-left
+ * CW x CH corner (CW = MI_TX_PACKED_CW(flags) <= min(w,32), CH = MI_TX_PACKED_CH(flags) <=
+ * min(h,32), multiples of 4), and the arena holds only that corner, ROW-major (coefficient
+ * (x, y) at coef_off + y*CW + x, coef_off a multiple of 4); the rest of the block reads as
+ * zero. A low-frequency block of a large transform then costs CW*CH arena entries instead of
+ * min(w,32)*min(h,32), and a transform row is CW/4 vector loads. The front-end emits every
+ * non-DC block of more than 16 coefficients packed. Other flag bits: 0. The DSP-table entry
+ * points (itxfm_add) keep the reference's dense layout. */
+#define MI_TX_PACKED 0x80u
+#define MI_TX_PACKED_CW(f) (((((unsigned)(f)) >> 3) & 7u) * 4u + 4u)
+#define MI_TX_PACKED_CH(f) ((((unsigned)(f)) & 7u) * 4u + 4u)
+#define MI_TX_PACK(cw, ch) ((uint8_t)(MI_TX_PACKED | ((((cw) >> 2) - 1) << 3) | (((ch) >> 2) - 1)))
 typedef struct MiTxBlock {
     uint32_t coef_off;       /* offset in coefficients (not bytes) into the arena */
     uint16_t x, y;           /* top-left pixel in `plane` */
     uint8_t  plane;          /* 0 Y, 1 U, 2 V */
     uint8_t  tx;             /* RectTxfmSize (src/levels.rs:46-82) */
     uint8_t  txtp;           /* TxfmType 0..15, or 16 = WHT_WHT (lossless) */
-    uint8_t  flags;          /* reserved, 0 */
+    uint8_t  flags;          /* 0, or MI_TX_PACK(cw, ch): the arena holds the packed corner */
     int32_t  eob;            /* end-of-block as passed to itxfm_add */
 } MiTxBlock;
 

@@ -616,6 +616,24 @@ void oracle_itx_frame(void *const planes[3], const ptrdiff_t strides[3], const v
         uint8_t *dst = (uint8_t *)planes[pl] + (ptrdiff_t)b[i].y * strides[pl] +
                        (ptrdiff_t)b[i].x * (hbd ? 2 : 1);
         void *cf = (uint8_t *)arena + (size_t)b[i].coef_off * (hbd ? 4 : 2);
+        if (b[i].flags & 0x80) {
+            /* packed (MI_TX_PACKED, include/mi_av1dsp.h): the arena holds the CW x CH corner,
+             * row-major; expand it to itxfm_add's dense layout (column-major, column height
+             * min(h,32)), transform, and consume the corner as itxfm_add consumes the dense
+             * block (its entries zeroed) */
+            const int cw = ((b[i].flags >> 3) & 7) * 4 + 4, ch = (b[i].flags & 7) * 4 + 4;
+            const int sh = tx_h[b[i].tx] < 32 ? tx_h[b[i].tx] : 32;
+            int32_t dense32[32 * 32];
+            int16_t *dense16 = (int16_t *)dense32;
+            memset(dense32, 0, sizeof(dense32));
+            for (int x = 0; x < cw; x++)
+                for (int y = 0; y < ch; y++) {
+                    if (hbd) { dense32[y + x * sh] = ((int32_t *)cf)[y * cw + x]; ((int32_t *)cf)[y * cw + x] = 0; }
+                    else { dense16[y + x * sh] = ((int16_t *)cf)[y * cw + x]; ((int16_t *)cf)[y * cw + x] = 0; }
+                }
+            oracle_itxfm_add(b[i].tx, b[i].txtp, dst, strides[pl], dense32, b[i].eob, bdmax);
+            continue;
+        }
         oracle_itxfm_add(b[i].tx, b[i].txtp, dst, strides[pl], cf, b[i].eob, bdmax);
     }
 }

@@ -161,6 +161,71 @@ inline DcMapGeom dc_map_geom(int w, int h, int layout) {
 
 // Legal TxfmType values of a RectTxfmSize (itx.rs:400-457, 1072-1110): bit t set when the
 // reference's itxfm_add[tx][t] slot is filled.
+// The stored coefficients of one block (MiTxBlock): the dense min(w,32) x min(h,32) layout
+// (column-major, column height min(h,32)), or with MI_TX_PACKED the CW x CH corner stored
+// row-major (coefficient (x, y) at y * CW + x, every other one zero).
+struct TxCoefShape { int cw, ch; };
+__host__ __device__ inline TxCoefShape tx_coef_shape(uint8_t flags, int sw, int sh) {
+    if (flags & MI_TX_PACKED) return { (int)MI_TX_PACKED_CW(flags), (int)MI_TX_PACKED_CH(flags) };
+    return { sw, sh };
+}
+// a descriptor's flags are legal for a block of sw x sh stored coefficients at arena offset
+// coef_off (a packed corner starts on a 4-coefficient boundary: its rows are vector loads)
+__host__ __device__ inline bool tx_flags_ok(uint8_t flags, int sw, int sh, uint32_t coef_off) {
+    if (!flags) return true;
+    return (flags & 0x40) == 0 && (flags & MI_TX_PACKED) && (int)MI_TX_PACKED_CW(flags) <= sw &&
+           (int)MI_TX_PACKED_CH(flags) <= sh && (coef_off & 3) == 0;
+}
+
+#ifdef __HIPCC__
+// Lane j's row of a block's coefficients (x = 0 .. SW-1) for the row transform. Dense: one word
+// per x at j + x * SH (consecutive lanes read consecutive words). Packed: the row's CW
+// coefficients are contiguous, read as 4-coefficient vectors (16 B for int32, 8 B for int16)
+// with a guard per vector, not per coefficient; rows j >= CH and columns >= CW read as zero.
+template <int SW, int SH, typename Cf>
+__device__ __forceinline__ void tx_load_row(const Cf *cf, uint8_t flags, int j, int (&v)[SW]) {
+    if (flags & MI_TX_PACKED) {
+        const int cw = (int)MI_TX_PACKED_CW(flags), ch = (int)MI_TX_PACKED_CH(flags);
+        const Cf *rp = cf + j * cw;
+#pragma unroll
+        for (int g = 0; g < SW / 4; g++) {
+            if (j < ch && 4 * g < cw) {
+                if constexpr (sizeof(Cf) == 4) {
+                    const int4 q = *reinterpret_cast<const int4 *>(rp + 4 * g);
+                    v[4 * g] = q.x; v[4 * g + 1] = q.y; v[4 * g + 2] = q.z; v[4 * g + 3] = q.w;
+                } else {
+                    const uint2 q = *reinterpret_cast<const uint2 *>(rp + 4 * g);
+                    v[4 * g] = (int)(int16_t)(q.x & 0xffff); v[4 * g + 1] = (int)(int16_t)(q.x >> 16);
+                    v[4 * g + 2] = (int)(int16_t)(q.y & 0xffff); v[4 * g + 3] = (int)(int16_t)(q.y >> 16);
+                }
+            } else {
+                v[4 * g] = v[4 * g + 1] = v[4 * g + 2] = v[4 * g + 3] = 0;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int x = 0; x < SW; x++) v[x] = (int)cf[j + x * SH];
+    }
+}
+// zero what tx_load_row read (itxfm_add consumes its coefficients)
+template <int SW, int SH, typename Cf>
+__device__ __forceinline__ void tx_zero_row(Cf *cf, uint8_t flags, int j) {
+    if (flags & MI_TX_PACKED) {
+        const int cw = (int)MI_TX_PACKED_CW(flags), ch = (int)MI_TX_PACKED_CH(flags);
+        Cf *rp = cf + j * cw;
+#pragma unroll
+        for (int g = 0; g < SW / 4; g++)
+            if (j < ch && 4 * g < cw) {
+                if constexpr (sizeof(Cf) == 4) *reinterpret_cast<int4 *>(rp + 4 * g) = make_int4(0, 0, 0, 0);
+                else *reinterpret_cast<uint2 *>(rp + 4 * g) = make_uint2(0, 0);
+            }
+    } else {
+#pragma unroll
+        for (int x = 0; x < SW; x++) cf[j + x * SH] = 0;
+    }
+}
+#endif
+
 __host__ __device__ constexpr uint32_t itx_legal_types(int tx) {
     return tx == 0 ? 0x1ffffu
          : imax_c(tx_dim(tx).w, tx_dim(tx).h) == 64 ? 0x1u
@@ -205,8 +270,11 @@ struct LfArgs {
 #ifndef MI_LF_TH
 #define MI_LF_TH 128   // 64x128 tiles, 512 lanes: 29.0-29.2 us at 4K10 against 31.5-32.3 for 64x64 (256 lanes)
 #endif
+#ifndef MI_LF_LPR
+#define MI_LF_LPR 4   // lanes per tile row
+#endif
 constexpr int kLfTW = MI_LF_TW, kLfTH = MI_LF_TH;
-constexpr int kLfThreads = kLfTH * 4;   // lf_tile_kernel workgroup: 256 lanes per 64 tile rows
+constexpr int kLfThreads = kLfTH * MI_LF_LPR;   // lf_tile_kernel workgroup: 256 lanes per 64 tile rows
 struct LfTileArgs {
     const uint8_t *src[3];
     uint8_t *dst[3];

@@ -838,16 +838,14 @@ __device__ __forceinline__ int itx_rows(const MiTxBlock &b, Cf *cf, bool zero, i
         int r[Wd];
 #pragma unroll
         for (int x = 0; x < Wd; x++) r[x] = 0;
+        int cv[SW];
+        tx_load_row<SW, SH, Cf>(cf, b.flags, j, cv);
 #pragma unroll
         for (int x = 0; x < SW; x++) {
-            const int v = (int)cf[j + x * SH];
-            if constexpr (Rect2) r[x] = (v * 181 + 128) >> 8;
-            else r[x] = v;
+            if constexpr (Rect2) r[x] = (cv[x] * 181 + 128) >> 8;
+            else r[x] = cv[x];
         }
-        if (zero) {
-#pragma unroll
-            for (int x = 0; x < SW; x++) cf[j + x * SH] = 0;
-        }
+        if (zero) tx_zero_row<SW, SH, Cf>(cf, b.flags, j);
         if (TX == 0 && b.txtp == 16) {
             if constexpr (TX == 0) {
 #pragma unroll
@@ -1010,7 +1008,8 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
             const TxDim td = tx_dim(tb.tx < 19 ? tb.tx : 0);
             const bool ok_ = ib.plane < fr.nplanes && ib.x + ib.w <= (fr.pw >> sh) && ib.y + ib.h <= (fr.ph >> sv) &&
                             tb.tx < 19 && td.w == ib.w && td.h == ib.h && tb.x == ib.x && tb.y == ib.y &&
-                            tb.plane == ib.plane && (tb.eob < 0 || (tb.txtp < 17 && ((itx_legal_types(tb.tx) >> tb.txtp) & 1)));
+                            tb.plane == ib.plane && (tb.eob < 0 || (tb.txtp < 17 && ((itx_legal_types(tb.tx) >> tb.txtp) & 1) &&
+                                                                    tx_flags_ok(tb.flags, imin_c(td.w, 32), imin_c(td.h, 32), tb.coef_off)));
             const bool ok = __builtin_amdgcn_readfirstlane((int)ok_) != 0;
             if (!ok) {
                 if (lane == 0) {

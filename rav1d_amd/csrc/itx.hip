@@ -143,6 +143,7 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
             // a descriptor the reference could never issue (wrong size group, a type the
             // size's table slot lacks, a rectangle outside its plane) is skipped and reported
             const bool ok = b.tx == TX && b.txtp < 17 && ((itx_legal_types(TX) >> b.txtp) & 1) &&
+                            tx_flags_ok(b.flags, SW, SH, b.coef_off) &&
                             b.plane < 3 && b.x + Wd <= sel3(pw3, b.plane) && b.y + Ht <= sel3(ph3, b.plane);
             if (!ok) {
                 valid = false;
@@ -161,8 +162,10 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
         if constexpr (ROUNDS > 1) {
             const Cf *cq = reinterpret_cast<const Cf *>(a.coef) + b.coef_off;
             const bool need = valid && !(b.txtp == 0 && b.eob < 1) && j < SH;
+            if (need) tx_load_row<CW, SH, Cf>(cq, b.flags, j, ck[rd]);
+            else
 #pragma unroll
-            for (int x = 0; x < CW; x++) ck[rd][x] = need ? (int)cq[j + x * SH] : 0;
+                for (int x = 0; x < CW; x++) ck[rd][x] = 0;
         }
         bk[rd] = b;
         vk[rd] = valid;
@@ -207,18 +210,19 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
         int r[Wd];
 #pragma unroll
         for (int x = 0; x < Wd; x++) r[x] = 0;
+        int cv[SW];
+        if constexpr (ROUNDS > 1) {
+#pragma unroll
+            for (int x = 0; x < SW; x++) cv[x] = ck[rd][x];
+        } else {
+            tx_load_row<SW, SH, Cf>(cf, b.flags, j, cv);
+        }
 #pragma unroll
         for (int x = 0; x < SW; x++) {
-            int v;
-            if constexpr (ROUNDS > 1) v = ck[rd][x];
-            else v = (int)cf[j + x * SH];
-            if constexpr (Rect2) r[x] = (v * 181 + 128) >> 8;
-            else r[x] = v;
+            if constexpr (Rect2) r[x] = (cv[x] * 181 + 128) >> 8;
+            else r[x] = cv[x];
         }
-        if (a.zero_coefs) {
-#pragma unroll
-            for (int x = 0; x < SW; x++) cf[j + x * SH] = 0;
-        }
+        if (a.zero_coefs) tx_zero_row<SW, SH, Cf>(cf, b.flags, j);
         if constexpr (TX == 0) {
             if (wht) {
 #pragma unroll

@@ -801,10 +801,10 @@ __device__ __forceinline__ void lf_store_tile(const LfTile &g, const Px *t) {
     using S = LfShape<Px>;
     const int tid = (int)threadIdx.x;
     uint8_t *dst = KARG_OF(LfTileArgs, dst, g.p);
-    static_assert((kLfTH * S::VPT) % kLfThreads == 0, "whole store rounds");
 #pragma unroll
-    for (int j = 0; j < kLfTH * S::VPT / kLfThreads; j++) {
+    for (int j = 0; j < (kLfTH * S::VPT + kLfThreads - 1) / kLfThreads; j++) {
         const int i = tid + kLfThreads * j;
+        if ((kLfTH * S::VPT) % kLfThreads && i >= kLfTH * S::VPT) break;
         const int r = i / S::VPT, c = (i % S::VPT) * S::VPX;
         const int y = g.y0 + r, x = g.x0 + c;
         if (y < g.ph && x < g.pw)

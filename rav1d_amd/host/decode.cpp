@@ -454,24 +454,61 @@ int FrameDec::decode_coefs(uint8_t *actx, uint8_t *lctx, int tx, int bs, const B
     return eob;
 }
 
-// copy a decoded block into the frame's coefficient arena (itxfm_add layout, min(w,32) x
-// min(h,32) column-major), return its offset in coefficients. A DC-only block (DCT_DCT with
-// eob 0: itxfm_add's dc-only path reads and clears coefficient 0 alone) keeps only its DC,
-// which shrinks the arena the device path uploads.
-uint32_t FrameDec::store_coefs(const int32_t *cf, int tx, int txtp, int eob) {
+// copy a decoded block into the frame's coefficient arena, return its offset in coefficients.
+// A DC-only block (DCT_DCT with eob 0: itxfm_add's dc-only path reads and clears coefficient 0
+// alone) keeps only its DC. Any other block of more than 16 coefficients keeps only the corner
+// of whole 4 x 4 groups that holds its non-zero coefficients, row-major, from a 4-coefficient
+// boundary (MI_TX_PACKED in *flags: the layout of include/mi_av1dsp.h): the arena the device
+// path uploads and reads shrinks, and a transform row is a few vector loads. A 4x4 block keeps
+// itxfm_add's layout (min(w,32) x min(h,32) column-major).
+uint32_t FrameDec::store_coefs(const int32_t *cf, int tx, int txtp, int eob, uint8_t *flags) {
     const TxDim &t = k_txdim[tx];
-    const int n = txtp == 0 && eob < 1 ? 1 : imin(t.w * 4, 32) * imin(t.h * 4, 32);
-    const uint32_t off = (uint32_t)fw.ncoef;
+    const int sw = imin(t.w * 4, 32), sh = imin(t.h * 4, 32);
     const int cb = s.bpc == 8 ? 2 : 4;
-    fw.coef.resize((fw.ncoef + n) * cb);
+    *flags = 0;
+    if ((txtp == 0 && eob < 1) || sw * sh <= 16) {
+        const int n = txtp == 0 && eob < 1 ? 1 : sw * sh;
+        const uint32_t off = (uint32_t)fw.ncoef;
+        fw.coef.resize((fw.ncoef + n) * cb);
+        if (cb == 2) {
+            int16_t *d = reinterpret_cast<int16_t *>(fw.coef.data()) + off;
+            for (int i = 0; i < n; i++) d[i] = (int16_t)cf[i];
+        } else {
+            memcpy(fw.coef.data() + (size_t)off * 4, cf, n * 4);
+        }
+        fw.ncoef += n;
+        return off;
+    }
+    // the last column and the last row group holding a non-zero coefficient
+    uint32_t rows = 0;   // bit y / 4: a non-zero in rows 4 (y / 4) .. + 3
+    int lastx = -1;
+    for (int x = 0; x < sw; x++) {
+        const int32_t *c = cf + x * sh;
+        uint32_t any = 0;
+        for (int y = 0; y < sh; y += 4) {
+            const uint32_t g = (uint32_t)(c[y] | c[y + 1] | c[y + 2] | c[y + 3]);
+            any |= g;
+            rows |= (uint32_t)(g != 0) << (y >> 2);
+        }
+        if (any) lastx = x;
+    }
+    const int cw = lastx < 0 ? 4 : ((lastx >> 2) + 1) * 4;
+    const int ch = rows ? (32 - __builtin_clz(rows)) * 4 : 4;
+    *flags = MI_TX_PACK(cw, ch);
+    const size_t pad = (4 - (fw.ncoef & 3)) & 3;
+    const uint32_t off = (uint32_t)(fw.ncoef + pad);
+    const int n = cw * ch;
+    fw.coef.resize((off + n) * cb, 0);
     if (cb == 2) {
         int16_t *d = reinterpret_cast<int16_t *>(fw.coef.data()) + off;
-        for (int i = 0; i < n; i++) d[i] = (int16_t)cf[i];
+        for (int y = 0; y < ch; y++)
+            for (int x = 0; x < cw; x++) d[y * cw + x] = (int16_t)cf[y + x * sh];
     } else {
         int32_t *d = reinterpret_cast<int32_t *>(fw.coef.data()) + off;
-        memcpy(d, cf, n * 4);
+        for (int y = 0; y < ch; y++)
+            for (int x = 0; x < cw; x++) d[y * cw + x] = cf[y + x * sh];
     }
-    fw.ncoef += n;
+    fw.ncoef = off + n;
     return off;
 }
 
@@ -824,7 +861,7 @@ void FrameDec::emit_intra(const Block &b, int edge_flags, const uint8_t *pal_idx
             memset(lctx, res, nlct);
             tb.txtp = (uint8_t)txtp;
             tb.eob = eob;
-            if (eob >= 0) tb.coef_off = store_coefs(cf, txs, txtp, eob);
+            if (eob >= 0) tb.coef_off = store_coefs(cf, txs, txtp, eob, &tb.flags);
         } else {
             memset(actx, 0x40, nact);
             memset(lctx, 0x40, nlct);
@@ -1221,7 +1258,7 @@ void FrameDec::push_ibc(const Block &b, Mv mv, int plane, int tx, int tbx, int t
         memset(lctx, res, nlct);
         tb.txtp = (uint8_t)*txtp;
         tb.eob = eob;
-        if (eob >= 0) tb.coef_off = store_coefs(cf, tx, *txtp, eob);
+        if (eob >= 0) tb.coef_off = store_coefs(cf, tx, *txtp, eob, &tb.flags);
     }
     fw.intra_tx.push_back(tb);
     Span<int32_t> &o = owner[plane];
@@ -2171,6 +2208,12 @@ int FrameDec::decode_tile(int k, bool tile_tmvs) {
 // Append tile decoder t's work lists, rebasing every index into the lists and arenas it
 // points at (intra blocks of dependencies, coefficient / idx / palette / mask / tmp arenas)
 void FrameDec::merge_tile(const FrameWork &t) {
+    // packed blocks start on 4-coefficient boundaries of their tile's arena: keep them there
+    if (fw.ncoef & 3) {
+        const size_t pad = 4 - (fw.ncoef & 3);
+        fw.coef.resize((fw.ncoef + pad) * (s.bpc == 8 ? 2 : 4), 0);
+        fw.ncoef += pad;
+    }
     const uint32_t intra_base = (uint32_t)fw.intra.size(), deps_base = (uint32_t)fw.deps.size();
     const uint32_t coef_base = (uint32_t)fw.ncoef, idx_base = (uint32_t)fw.idx.size();
     const uint32_t pal_base = (uint32_t)(fw.pal.size() / (s.bpc == 8 ? 1 : 2));

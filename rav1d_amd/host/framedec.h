@@ -170,7 +170,7 @@ private:
     int decode_coefs(uint8_t *actx, uint8_t *lctx, int tx, int bs, const Block &b, int intra, int plane, int32_t *cf,
                      int *txtp, uint8_t *res_ctx);
     void emit_intra(const Block &b, int edge_flags, const uint8_t *pal_idx, const uint16_t (*pal)[8]);
-    uint32_t store_coefs(const int32_t *cf, int tx, int txtp, int eob);
+    uint32_t store_coefs(const int32_t *cf, int tx, int txtp, int eob, uint8_t *flags);
     void add_deps(int plane, int x0, int y0, int x1, int y1, std::vector<int32_t> &out);
     void mask_edges_intra(int by4, int bx4, int w4_, int h4_, int tx, uint8_t *actx, uint8_t *lctx, uint16_t (*masks)[32][3][2]);
     void mask_edges_chroma(int cby4, int cbx4, int cw4, int ch4, int skip_inter, int tx, uint8_t *actx, uint8_t *lctx,

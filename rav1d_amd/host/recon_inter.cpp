@@ -341,7 +341,7 @@ void FrameDec::emit_inter_residual(const Block &b, int has_chroma) {
         tb.tx = (uint8_t)tx;
         tb.txtp = (uint8_t)txtp;
         tb.eob = eob;
-        tb.coef_off = store_coefs(cf, tx, txtp, eob);
+        tb.coef_off = store_coefs(cf, tx, txtp, eob, &tb.flags);
         if (!ii) {
             fw.inter_tx.push_back(tb);
             return;

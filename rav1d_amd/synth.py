@@ -116,8 +116,8 @@ def make_texture(rng, w, h, bpc):
 
 
 def make_itx_frame(w, h, bpc=10, layout=1, seed=0x1D1C0001, dc_frac=0.6, full_frac=0.1,
-                   with_wht=False):
-    """Synthetic frame for the itx stage.
+                   with_wht=False, packed=False):
+    """Synthetic frame for the itx stage (packed: non-DC blocks as pack_coefs stores them).
 
     Returns dict(blocks=structured array sorted by size/type (device order),
     size_start=20 offsets, coef=arena (int16/int32, decode order), planes=[Y,U,V] numpy
@@ -146,9 +146,15 @@ def make_itx_frame(w, h, bpc=10, layout=1, seed=0x1D1C0001, dc_frac=0.6, full_fr
             c, eob = make_coefs(rng, tx, txtp, regime, bpc)
             if txtp == 16:
                 c = np.clip(c // 64, -(1 << (bpc + 2)), (1 << (bpc + 2)))
+            flags = 0
             if txtp == 0 and eob < 1:
                 c = c.reshape(-1)[:1]     # a DC-only block keeps its DC alone (as the front-end stores it)
-            recs.append((off, x, y, p, tx, txtp, 0, eob))
+            elif packed:
+                c, flags = pack_coefs(c, tx)
+                if flags and off % 4:
+                    coef_chunks.append(np.zeros(4 - off % 4, dtype=c.dtype))
+                    off += 4 - off % 4
+            recs.append((off, x, y, p, tx, txtp, flags, eob))
             coef_chunks.append(c)
             off += c.size
     blocks = np.array(recs, dtype=TXBLOCK_DTYPE)
@@ -210,7 +216,7 @@ def itx_dc_runs(blocks, band_start):
 
 def itx_algorithmic_bytes(blocks, bpc, zero_coefs=True, dc_defer=False):
     """sum over blocks of coefB*n_coef (+ the zeroing write) + 2*pixB*w*h,
-    plus the 16-byte descriptor. dc_defer (MI_ITX_DC_DEFER): a DC-only block writes its 4-byte
+    plus the 16-byte descriptor (n_coef: the stored coefficients, a packed block's corner). dc_defer (MI_ITX_DC_DEFER): a DC-only block writes its 4-byte
     DC-map entry per 4x4 unit instead of reading and writing its pixels."""
     pxb = 1 if bpc == 8 else 2
     cb = 2 if bpc == 8 else 4
@@ -218,6 +224,8 @@ def itx_algorithmic_bytes(blocks, bpc, zero_coefs=True, dc_defer=False):
     w = dims[blocks["tx"], 0]
     h = dims[blocks["tx"], 1]
     ncoef = np.minimum(w, 32) * np.minimum(h, 32)
+    fl = blocks["flags"].astype(np.int64)
+    ncoef = np.where(fl & 0x80, (((fl >> 3) & 7) * 4 + 4) * ((fl & 7) * 4 + 4), ncoef)   # MI_TX_PACKED
     dconly = (blocks["txtp"] == 0) & (blocks["eob"] < 1)
     ncoef = np.where(dconly, 1, ncoef)
     pix = 2 * pxb * w * h
@@ -464,7 +472,24 @@ def make_fg_params(rng, layout=1, force_y=True):
                 overlap_flag=int(rng.random() < 0.7), clip_to_restricted_range=int(rng.random() < 0.5))
 
 
-def itx_blocks_from_tilings(tilings, bpc, rng, dc_frac=0.6, full_frac=0.1):
+def pack_coefs(c, tx):
+    """The front-end's packed form of one block's dense coefficients (rav1d_amd/host/decode.cpp
+    store_coefs, MI_TX_PACKED in include/mi_av1dsp.h): the corner of whole 4 x 4 groups holding
+    every non-zero coefficient, row-major, for every block of more than 16 coefficients.
+    Returns (coefficients, flags); the caller starts a packed block on a 4-coefficient boundary."""
+    w, h = TX_DIMS[tx]
+    sw, sh = min(w, 32), min(h, 32)
+    d = c.reshape(sw, sh)      # d[x, y]
+    if sw * sh <= 16:
+        return c, 0
+    nzx, nzy = np.nonzero(d)
+    cw = (int(nzx.max()) // 4 + 1) * 4 if nzx.size else 4
+    ch = (int(nzy.max()) // 4 + 1) * 4 if nzy.size else 4
+    return np.ascontiguousarray(d[:cw, :ch].T).reshape(-1), 0x80 | ((cw // 4 - 1) << 3) | (ch // 4 - 1)
+
+
+def itx_blocks_from_tilings(tilings, bpc, rng, dc_frac=0.6, full_frac=0.1, packed=False):
+    """packed: non-DC blocks stored as the front-end stores them (pack_coefs)."""
     recs, chunks, off = [], [], 0
     for p, blocks in enumerate(tilings):
         for (x, y, tx) in blocks:
@@ -475,9 +500,15 @@ def itx_blocks_from_tilings(tilings, bpc, rng, dc_frac=0.6, full_frac=0.1):
                 txtp = types[int(rng.integers(len(types)))]
                 regime = 2 if rng.random() < full_frac / (1 - dc_frac) else 1
             c, eob = make_coefs(rng, tx, txtp, regime, bpc)
+            flags = 0
             if txtp == 0 and eob < 1:
                 c = c.reshape(-1)[:1]     # a DC-only block keeps its DC alone (as the front-end stores it)
-            recs.append((off, x, y, p, tx, txtp, 0, eob))
+            elif packed:
+                c, flags = pack_coefs(c, tx)
+                if flags and off % 4:
+                    chunks.append(np.zeros(4 - off % 4, dtype=c.dtype))
+                    off += 4 - off % 4
+            recs.append((off, x, y, p, tx, txtp, flags, eob))
             chunks.append(c)
             off += c.size
     blocks = np.array(recs, dtype=TXBLOCK_DTYPE)
@@ -487,15 +518,16 @@ def itx_blocks_from_tilings(tilings, bpc, rng, dc_frac=0.6, full_frac=0.1):
 
 
 def make_frame(w, h, bpc=10, layout=1, seed=0x4C100001, sb128=1, with_fg=True, with_mc=False, nrefs=2,
-               mv_mode="uniform"):
+               mv_mode="uniform", packed=False):
     """One synthetic frame's worth of post-entropy descriptors for every implemented stage,
     all derived from one transform tiling: prediction planes, itx blocks + coefficient arena,
     deblock masks/levels, CDEF indices/strengths, LR units, film-grain parameters.
+    packed: the coefficient arena in the front-end's packed form (pack_coefs).
     with_mc: an inter frame — `nrefs` textured reference
     pictures and MC units whose prediction replaces the resident prediction planes."""
     rng = np.random.default_rng(seed)
     til = make_tilings(w, h, layout, rng)
-    blocks, size_start, coef = itx_blocks_from_tilings(til, bpc, rng)
+    blocks, size_start, coef = itx_blocks_from_tilings(til, bpc, rng, packed=packed)
     lf = make_lf_meta(til, w, h, layout, rng)
     cd = add_cdef_meta(lf, rng)
     lr = make_lr_meta(w, h, layout, rng, sb128=sb128)

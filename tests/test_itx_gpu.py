@@ -47,6 +47,42 @@ def test_itx_frame_matches_oracle(gpu, bpc, seed):
     assert not coef_after.any() and not ref_coef.any()
 
 
+@pytest.mark.parametrize("bpc", [8, 10, 12])
+@pytest.mark.parametrize("path", ["plain", "banded", "runs"])
+def test_itx_packed_blocks_match_dense(gpu, bpc, path):
+    """MI_TX_PACKED: the front-end's packed corners give the pixels of the dense arena, consume
+    exactly the packed entries, and agree with the oracle (which expands them)."""
+    kw = dict(bpc=bpc, seed=40 + bpc, with_wht=True)
+    dense, packed = make_itx_frame(640, 360, **kw), make_itx_frame(640, 360, packed=True, **kw)
+    assert (packed["blocks"]["flags"] & 0x80).any() and packed["coef"].size < dense["coef"].size
+    opts = dict(banded=path == "banded", runs=path == "runs")
+    got_d, _ = run_frame(gpu, dense, **opts)
+    got_p, coef_after = run_frame(gpu, packed, **opts)
+    ref_coef = packed["coef"].copy()
+    ref = oracle_lib.itx_frame([p.copy() for p in packed["planes"]], packed["blocks"], ref_coef, bpc)
+    for p in range(3):
+        assert np.array_equal(got_p[p], got_d[p]), f"plane {p}: packed != dense"
+        assert np.array_equal(got_p[p], ref[p]), f"plane {p}: packed != oracle"
+    assert not coef_after.any() and not ref_coef.any()
+
+
+def test_itx_packed_flags_rejected(gpu):
+    """a packed corner larger than the block's stored coefficients, or a reserved flag bit, is
+    skipped and reported (the context's device status -EINVAL), as any illegal descriptor"""
+    from rav1d_amd.frame import _stream_ptr
+    for bad in (0x80 | (7 << 3) | 7, 0x40):
+        fr = make_itx_frame(64, 64, bpc=10, seed=8)
+        blk = fr["blocks"].copy()
+        k = int(np.nonzero((blk["tx"] == 0) & (blk["txtp"] != 0))[0][0])   # a 4x4 block: 16 entries only
+        blk["flags"][k] = bad
+        fr["blocks"] = blk
+        before = [p.copy() for p in fr["planes"]]
+        got, _ = run_frame(gpu, fr)
+        assert lib().mi_ctx_device_status(gpu.h, _stream_ptr(None)) == -22
+        x, y, p = int(blk["x"][k]), int(blk["y"][k]), int(blk["plane"][k])
+        assert np.array_equal(got[p][y:y + 4, x:x + 4], before[p][y:y + 4, x:x + 4])
+
+
 def test_itx_keep_coefs_flag(gpu):
     fr = make_itx_frame(128, 128, bpc=10, seed=5)
     _, coef_after = run_frame(gpu, fr, flags=ITX_KEEP_COEFS)

@@ -8,7 +8,7 @@ import torch
 import bench
 from rav1d_amd import frame as F
 from rav1d_amd.synth import make_frame
-fr = make_frame(3840, 2160, 10, 1, seed=0x4C100001, with_fg=False, with_mc=True)
+fr = make_frame(3840, 2160, 10, 1, seed=0x4C100001, with_fg=False, with_mc=True, packed=not os.environ.get("DENSE"))
 ctx = F.Context(0)
 pipe = bench.Pipeline(ctx, fr, ring=2)
 s = torch.cuda.current_stream()
