@@ -60,9 +60,13 @@ typedef struct MiPicture {
  * (x, y) at coef_off + y*CW + x, coef_off a multiple of 4); the rest of the block reads as
  * zero. A low-frequency block of a large transform then costs CW*CH arena entries instead of
  * min(w,32)*min(h,32), and a transform row is CW/4 vector loads. The front-end emits every
- * non-DC block of more than 16 coefficients packed. Other flag bits: 0. The DSP-table entry
- * points (itxfm_add) keep the reference's dense layout. */
+ * non-DC block of more than 16 coefficients packed. With MI_TX_I16 as well (10/12-bit arenas
+ * only) the corner's coefficients are int16: coefficient (x, y) is
+ * ((const int16_t *)(arena + coef_off))[y*CW + x] and the block spans CW*CH/2 int32 entries
+ * (the front-end sets it when every coefficient of the corner fits). Other flag bits: 0. The
+ * DSP-table entry points (itxfm_add) keep the reference's dense layout. */
 #define MI_TX_PACKED 0x80u
+#define MI_TX_I16 0x40u
 #define MI_TX_PACKED_CW(f) (((((unsigned)(f)) >> 3) & 7u) * 4u + 4u)
 #define MI_TX_PACKED_CH(f) ((((unsigned)(f)) & 7u) * 4u + 4u)
 #define MI_TX_PACK(cw, ch) ((uint8_t)(MI_TX_PACKED | ((((cw) >> 2) - 1) << 3) | (((ch) >> 2) - 1)))

@@ -628,7 +628,9 @@ void oracle_itx_frame(void *const planes[3], const ptrdiff_t strides[3], const v
             memset(dense32, 0, sizeof(dense32));
             for (int x = 0; x < cw; x++)
                 for (int y = 0; y < ch; y++) {
-                    if (hbd) { dense32[y + x * sh] = ((int32_t *)cf)[y * cw + x]; ((int32_t *)cf)[y * cw + x] = 0; }
+                    if (hbd && (b[i].flags & 0x40)) {   /* MI_TX_I16: int16 corner in the int32 arena */
+                        dense32[y + x * sh] = ((int16_t *)cf)[y * cw + x]; ((int16_t *)cf)[y * cw + x] = 0;
+                    } else if (hbd) { dense32[y + x * sh] = ((int32_t *)cf)[y * cw + x]; ((int32_t *)cf)[y * cw + x] = 0; }
                     else { dense16[y + x * sh] = ((int16_t *)cf)[y * cw + x]; ((int16_t *)cf)[y * cw + x] = 0; }
                 }
             oracle_itxfm_add(b[i].tx, b[i].txtp, dst, strides[pl], dense32, b[i].eob, bdmax);

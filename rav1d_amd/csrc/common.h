@@ -170,10 +170,11 @@ __host__ __device__ inline TxCoefShape tx_coef_shape(uint8_t flags, int sw, int 
     return { sw, sh };
 }
 // a descriptor's flags are legal for a block of sw x sh stored coefficients at arena offset
-// coef_off (a packed corner starts on a 4-coefficient boundary: its rows are vector loads)
-__host__ __device__ inline bool tx_flags_ok(uint8_t flags, int sw, int sh, uint32_t coef_off) {
+// coef_off (a packed corner starts on a 4-coefficient boundary: its rows are vector loads;
+// int16 corners only in the int32 arenas of 10/12-bit frames)
+__host__ __device__ inline bool tx_flags_ok(uint8_t flags, int sw, int sh, uint32_t coef_off, bool hbd) {
     if (!flags) return true;
-    return (flags & 0x40) == 0 && (flags & MI_TX_PACKED) && (int)MI_TX_PACKED_CW(flags) <= sw &&
+    return (flags & MI_TX_PACKED) && (!(flags & MI_TX_I16) || hbd) && (int)MI_TX_PACKED_CW(flags) <= sw &&
            (int)MI_TX_PACKED_CH(flags) <= sh && (coef_off & 3) == 0;
 }
 
@@ -187,16 +188,18 @@ __device__ __forceinline__ void tx_load_row(const Cf *cf, uint8_t flags, int j, 
     if (flags & MI_TX_PACKED) {
         const int cw = (int)MI_TX_PACKED_CW(flags), ch = (int)MI_TX_PACKED_CH(flags);
         const Cf *rp = cf + j * cw;
+        const int16_t *rh = reinterpret_cast<const int16_t *>(cf) + j * cw;   // MI_TX_I16
+        const bool i16 = sizeof(Cf) == 4 && (flags & MI_TX_I16);
 #pragma unroll
         for (int g = 0; g < SW / 4; g++) {
             if (j < ch && 4 * g < cw) {
-                if constexpr (sizeof(Cf) == 4) {
-                    const int4 q = *reinterpret_cast<const int4 *>(rp + 4 * g);
-                    v[4 * g] = q.x; v[4 * g + 1] = q.y; v[4 * g + 2] = q.z; v[4 * g + 3] = q.w;
-                } else {
-                    const uint2 q = *reinterpret_cast<const uint2 *>(rp + 4 * g);
+                if (sizeof(Cf) == 2 || i16) {
+                    const uint2 q = *reinterpret_cast<const uint2 *>((sizeof(Cf) == 2 ? reinterpret_cast<const int16_t *>(rp) : rh) + 4 * g);
                     v[4 * g] = (int)(int16_t)(q.x & 0xffff); v[4 * g + 1] = (int)(int16_t)(q.x >> 16);
                     v[4 * g + 2] = (int)(int16_t)(q.y & 0xffff); v[4 * g + 3] = (int)(int16_t)(q.y >> 16);
+                } else {
+                    const int4 q = *reinterpret_cast<const int4 *>(rp + 4 * g);
+                    v[4 * g] = q.x; v[4 * g + 1] = q.y; v[4 * g + 2] = q.z; v[4 * g + 3] = q.w;
                 }
             } else {
                 v[4 * g] = v[4 * g + 1] = v[4 * g + 2] = v[4 * g + 3] = 0;
@@ -213,11 +216,14 @@ __device__ __forceinline__ void tx_zero_row(Cf *cf, uint8_t flags, int j) {
     if (flags & MI_TX_PACKED) {
         const int cw = (int)MI_TX_PACKED_CW(flags), ch = (int)MI_TX_PACKED_CH(flags);
         Cf *rp = cf + j * cw;
+        int16_t *rh = reinterpret_cast<int16_t *>(cf) + j * cw;   // MI_TX_I16
+        const bool i16 = sizeof(Cf) == 4 && (flags & MI_TX_I16);
 #pragma unroll
         for (int g = 0; g < SW / 4; g++)
             if (j < ch && 4 * g < cw) {
-                if constexpr (sizeof(Cf) == 4) *reinterpret_cast<int4 *>(rp + 4 * g) = make_int4(0, 0, 0, 0);
-                else *reinterpret_cast<uint2 *>(rp + 4 * g) = make_uint2(0, 0);
+                if (sizeof(Cf) == 2 || i16)
+                    *reinterpret_cast<uint2 *>((sizeof(Cf) == 2 ? reinterpret_cast<int16_t *>(rp) : rh) + 4 * g) = make_uint2(0, 0);
+                else *reinterpret_cast<int4 *>(rp + 4 * g) = make_int4(0, 0, 0, 0);
             }
     } else {
 #pragma unroll

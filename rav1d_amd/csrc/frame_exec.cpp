@@ -175,13 +175,13 @@ thread_local const char *g_why = nullptr;
 
 // the coefficients a transform block reads from the arena: a DC-only block (DCT_DCT, eob < 1)
 // its DC alone (the front-end stores only that), a packed block its CW x CH corner
-// (MI_TX_PACKED), any other the min(w,32) x min(h,32) run; illegal flags: more than any arena
-size_t coef_span(const mi::TxDim &d, int txtp, int eob, uint8_t flags, uint32_t coef_off) {
+// (MI_TX_PACKED; half as many int32 entries with MI_TX_I16), any other the min(w,32) x min(h,32) run; illegal flags: more than any arena
+size_t coef_span(const mi::TxDim &d, int txtp, int eob, uint8_t flags, uint32_t coef_off, bool hbd) {
     const int sw = std::min(d.w, 32), sh = std::min(d.h, 32);
-    if (!mi::tx_flags_ok(flags, sw, sh, coef_off)) return SIZE_MAX / 2;
+    if (!mi::tx_flags_ok(flags, sw, sh, coef_off, hbd)) return SIZE_MAX / 2;
     if (txtp == 0 && eob < 1) return 1;
     const mi::TxCoefShape cs = mi::tx_coef_shape(flags, sw, sh);
-    return (size_t)cs.cw * cs.ch;
+    return (size_t)cs.cw * cs.ch / (flags & MI_TX_I16 ? 2 : 1);
 }
 #define BADF() (g_why = "frame_exec.cpp:" STR(__LINE__), false)
 
@@ -289,7 +289,7 @@ int validate_inter(const MiDecFrame *f, const MiFramePictures *p, const bool sca
         const mi::TxDim d = mi::tx_dim(t.tx);
         const int sh = t.plane ? ss_hor : 0, sv = t.plane ? ss_ver : 0;
         if (t.x + d.w > (aw >> sh) || t.y + d.h > (ah >> sv)) return BAD();
-        if ((size_t)t.coef_off + coef_span(d, t.txtp, t.eob, t.flags, t.coef_off) > f->ncoef) return BAD();
+        if ((size_t)t.coef_off + coef_span(d, t.txtp, t.eob, t.flags, t.coef_off, f->bpc > 8) > f->ncoef) return BAD();
     }
     return 0;
 }
@@ -341,7 +341,7 @@ int validate(const MiDecFrame *f, const MiFramePictures *p) {
         if (t.eob >= 0) {
             if (!legal_txtp(tx, t.txtp)) return BAD();
             const mi::TxDim d = mi::tx_dim(tx);
-            if ((size_t)t.coef_off + coef_span(d, t.txtp, t.eob, t.flags, t.coef_off) > f->ncoef) return BAD();
+            if ((size_t)t.coef_off + coef_span(d, t.txtp, t.eob, t.flags, t.coef_off, f->bpc > 8) > f->ncoef) return BAD();
         } else if (t.coef_off + 16 > f->ncoef || (t.txtp != 0 && t.txtp != 16)) {
             return BAD();
         }

@@ -1009,7 +1009,7 @@ __global__ __launch_bounds__(64) void intra_recon_kernel(IntraReconArgs a) {
             const bool ok_ = ib.plane < fr.nplanes && ib.x + ib.w <= (fr.pw >> sh) && ib.y + ib.h <= (fr.ph >> sv) &&
                             tb.tx < 19 && td.w == ib.w && td.h == ib.h && tb.x == ib.x && tb.y == ib.y &&
                             tb.plane == ib.plane && (tb.eob < 0 || (tb.txtp < 17 && ((itx_legal_types(tb.tx) >> tb.txtp) & 1) &&
-                                                                    tx_flags_ok(tb.flags, imin_c(td.w, 32), imin_c(td.h, 32), tb.coef_off)));
+                                                                    tx_flags_ok(tb.flags, imin_c(td.w, 32), imin_c(td.h, 32), tb.coef_off, sizeof(Cf) == 4)));
             const bool ok = __builtin_amdgcn_readfirstlane((int)ok_) != 0;
             if (!ok) {
                 if (lane == 0) {

@@ -143,7 +143,7 @@ __device__ __forceinline__ void itx_size(const ItxArgs &a, int lwg, Lt *lds) {
             // a descriptor the reference could never issue (wrong size group, a type the
             // size's table slot lacks, a rectangle outside its plane) is skipped and reported
             const bool ok = b.tx == TX && b.txtp < 17 && ((itx_legal_types(TX) >> b.txtp) & 1) &&
-                            tx_flags_ok(b.flags, SW, SH, b.coef_off) &&
+                            tx_flags_ok(b.flags, SW, SH, b.coef_off, sizeof(Cf) == 4) &&
                             b.plane < 3 && b.x + Wd <= sel3(pw3, b.plane) && b.y + Ht <= sel3(ph3, b.plane);
             if (!ok) {
                 valid = false;

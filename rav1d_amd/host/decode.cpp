@@ -456,17 +456,23 @@ int FrameDec::decode_coefs(uint8_t *actx, uint8_t *lctx, int tx, int bs, const B
 
 // copy a decoded block into the frame's coefficient arena, return its offset in coefficients.
 // A DC-only block (DCT_DCT with eob 0: itxfm_add's dc-only path reads and clears coefficient 0
-// alone) keeps only its DC. Any other block of more than 16 coefficients keeps only the corner
+// alone) keeps only its DC. Any other block (a 4x4 one only as int16) keeps only the corner
 // of whole 4 x 4 groups that holds its non-zero coefficients, row-major, from a 4-coefficient
-// boundary (MI_TX_PACKED in *flags: the layout of include/mi_av1dsp.h): the arena the device
-// path uploads and reads shrinks, and a transform row is a few vector loads. A 4x4 block keeps
-// itxfm_add's layout (min(w,32) x min(h,32) column-major).
+// boundary, as int16 where they fit (MI_TX_PACKED, MI_TX_I16 in *flags: the layout of
+// include/mi_av1dsp.h): the arena the device
+// path uploads and reads shrinks, and a transform row is a few vector loads. Other 4x4 blocks
+// keep itxfm_add's layout (min(w,32) x min(h,32) column-major).
 uint32_t FrameDec::store_coefs(const int32_t *cf, int tx, int txtp, int eob, uint8_t *flags) {
     const TxDim &t = k_txdim[tx];
     const int sw = imin(t.w * 4, 32), sh = imin(t.h * 4, 32);
     const int cb = s.bpc == 8 ? 2 : 4;
     *flags = 0;
-    if ((txtp == 0 && eob < 1) || sw * sh <= 16) {
+    // a 4x4 block stays dense unless int16 storage halves it (10/12-bit)
+    bool small_dense = sw * sh <= 16 && cb == 2;
+    if (sw * sh <= 16 && !small_dense)
+        for (int i = 0; i < 16; i++)
+            if (cf[i] < -32768 || cf[i] > 32767) small_dense = true;
+    if ((txtp == 0 && eob < 1) || small_dense) {
         const int n = txtp == 0 && eob < 1 ? 1 : sw * sh;
         const uint32_t off = (uint32_t)fw.ncoef;
         fw.coef.resize((fw.ncoef + n) * cb);
@@ -495,15 +501,30 @@ uint32_t FrameDec::store_coefs(const int32_t *cf, int tx, int txtp, int eob, uin
     const int cw = lastx < 0 ? 4 : ((lastx >> 2) + 1) * 4;
     const int ch = rows ? (32 - __builtin_clz(rows)) * 4 : 4;
     *flags = MI_TX_PACK(cw, ch);
+    // 10/12-bit: int16 storage when every coefficient of the corner fits (MI_TX_I16)
+    bool i16 = cb == 2;
+    if (!i16) {
+        int32_t lo = 0, hi = 0;
+        for (int x = 0; x < cw; x++)
+            for (int y = 0; y < ch; y++) {
+                lo = imin(lo, cf[y + x * sh]);
+                hi = imax(hi, cf[y + x * sh]);
+            }
+        i16 = lo >= -32768 && hi <= 32767;
+        if (i16) *flags |= MI_TX_I16;
+    }
     const size_t pad = (4 - (fw.ncoef & 3)) & 3;
     const uint32_t off = (uint32_t)(fw.ncoef + pad);
-    const int n = cw * ch;
-    fw.coef.resize((off + n) * cb, 0);
-    if (cb == 2) {
-        int16_t *d = reinterpret_cast<int16_t *>(fw.coef.data()) + off;
+    const int n = cw * ch, slots = cb == 4 && i16 ? n / 2 : n;
+    fw.coef.resize((off + slots) * cb, 0);
+    if (i16) {
+        int16_t *d = reinterpret_cast<int16_t *>(fw.coef.data() + (size_t)off * cb);
         for (int y = 0; y < ch; y++)
             for (int x = 0; x < cw; x++) d[y * cw + x] = (int16_t)cf[y + x * sh];
-    } else {
+        fw.ncoef = off + slots;
+        return off;
+    }
+    {
         int32_t *d = reinterpret_cast<int32_t *>(fw.coef.data()) + off;
         for (int y = 0; y < ch; y++)
             for (int x = 0; x < cw; x++) d[y * cw + x] = cf[y + x * sh];

@@ -150,7 +150,7 @@ def make_itx_frame(w, h, bpc=10, layout=1, seed=0x1D1C0001, dc_frac=0.6, full_fr
             if txtp == 0 and eob < 1:
                 c = c.reshape(-1)[:1]     # a DC-only block keeps its DC alone (as the front-end stores it)
             elif packed:
-                c, flags = pack_coefs(c, tx)
+                c, flags = pack_coefs(c, tx, bpc > 8)
                 if flags and off % 4:
                     coef_chunks.append(np.zeros(4 - off % 4, dtype=c.dtype))
                     off += 4 - off % 4
@@ -226,6 +226,7 @@ def itx_algorithmic_bytes(blocks, bpc, zero_coefs=True, dc_defer=False):
     ncoef = np.minimum(w, 32) * np.minimum(h, 32)
     fl = blocks["flags"].astype(np.int64)
     ncoef = np.where(fl & 0x80, (((fl >> 3) & 7) * 4 + 4) * ((fl & 7) * 4 + 4), ncoef)   # MI_TX_PACKED
+    ncoef = np.where(fl & 0x40, ncoef // 2, ncoef)                                       # MI_TX_I16
     dconly = (blocks["txtp"] == 0) & (blocks["eob"] < 1)
     ncoef = np.where(dconly, 1, ncoef)
     pix = 2 * pxb * w * h
@@ -472,20 +473,27 @@ def make_fg_params(rng, layout=1, force_y=True):
                 overlap_flag=int(rng.random() < 0.7), clip_to_restricted_range=int(rng.random() < 0.5))
 
 
-def pack_coefs(c, tx):
+def pack_coefs(c, tx, hbd=False):
     """The front-end's packed form of one block's dense coefficients (rav1d_amd/host/decode.cpp
     store_coefs, MI_TX_PACKED in include/mi_av1dsp.h): the corner of whole 4 x 4 groups holding
-    every non-zero coefficient, row-major, for every block of more than 16 coefficients.
-    Returns (coefficients, flags); the caller starts a packed block on a 4-coefficient boundary."""
+    every non-zero coefficient, row-major, for every block of more than 16 coefficients; hbd
+    (10/12-bit, int32 arena): as int16 pairs when the corner fits (MI_TX_I16), then 4x4 blocks
+    too.
+    Returns (arena entries, flags); the caller starts a packed block on a 4-entry boundary."""
     w, h = TX_DIMS[tx]
     sw, sh = min(w, 32), min(h, 32)
     d = c.reshape(sw, sh)      # d[x, y]
-    if sw * sh <= 16:
-        return c, 0
+    if sw * sh <= 16 and not (hbd and c.min() >= -32768 and c.max() <= 32767):
+        return c, 0            # a 4x4 block is packed only as int16
     nzx, nzy = np.nonzero(d)
     cw = (int(nzx.max()) // 4 + 1) * 4 if nzx.size else 4
     ch = (int(nzy.max()) // 4 + 1) * 4 if nzy.size else 4
-    return np.ascontiguousarray(d[:cw, :ch].T).reshape(-1), 0x80 | ((cw // 4 - 1) << 3) | (ch // 4 - 1)
+    corner = np.ascontiguousarray(d[:cw, :ch].T).reshape(-1)
+    flags = 0x80 | ((cw // 4 - 1) << 3) | (ch // 4 - 1)
+    if hbd and corner.min() >= -32768 and corner.max() <= 32767:
+        # MI_TX_I16: int16 coefficients in the int32 arena, two per entry (little-endian)
+        return corner.astype(np.int16).view(np.int32).astype(np.int64), flags | 0x40
+    return corner, flags
 
 
 def itx_blocks_from_tilings(tilings, bpc, rng, dc_frac=0.6, full_frac=0.1, packed=False):
@@ -504,7 +512,7 @@ def itx_blocks_from_tilings(tilings, bpc, rng, dc_frac=0.6, full_frac=0.1, packe
             if txtp == 0 and eob < 1:
                 c = c.reshape(-1)[:1]     # a DC-only block keeps its DC alone (as the front-end stores it)
             elif packed:
-                c, flags = pack_coefs(c, tx)
+                c, flags = pack_coefs(c, tx, bpc > 8)
                 if flags and off % 4:
                     chunks.append(np.zeros(4 - off % 4, dtype=c.dtype))
                     off += 4 - off % 4

@@ -54,7 +54,10 @@ def test_itx_packed_blocks_match_dense(gpu, bpc, path):
     exactly the packed entries, and agree with the oracle (which expands them)."""
     kw = dict(bpc=bpc, seed=40 + bpc, with_wht=True)
     dense, packed = make_itx_frame(640, 360, **kw), make_itx_frame(640, 360, packed=True, **kw)
-    assert (packed["blocks"]["flags"] & 0x80).any() and packed["coef"].size < dense["coef"].size
+    fl = packed["blocks"]["flags"]
+    assert (fl & 0x80).any() and packed["coef"].size < dense["coef"].size
+    if bpc > 8:   # int16 corners (MI_TX_I16) in the int32 arena; at 12 bits int32 ones too
+        assert (fl & 0x40).any() and (bpc == 10 or ((fl & 0xc0) == 0x80).any())
     opts = dict(banded=path == "banded", runs=path == "runs")
     got_d, _ = run_frame(gpu, dense, **opts)
     got_p, coef_after = run_frame(gpu, packed, **opts)
@@ -70,8 +73,8 @@ def test_itx_packed_flags_rejected(gpu):
     """a packed corner larger than the block's stored coefficients, or a reserved flag bit, is
     skipped and reported (the context's device status -EINVAL), as any illegal descriptor"""
     from rav1d_amd.frame import _stream_ptr
-    for bad in (0x80 | (7 << 3) | 7, 0x40):
-        fr = make_itx_frame(64, 64, bpc=10, seed=8)
+    for bad, bpc in ((0x80 | (7 << 3) | 7, 10), (0x40, 10), (0xc0, 8)):
+        fr = make_itx_frame(64, 64, bpc=bpc, seed=8)
         blk = fr["blocks"].copy()
         k = int(np.nonzero((blk["tx"] == 0) & (blk["txtp"] != 0))[0][0])   # a 4x4 block: 16 entries only
         blk["flags"][k] = bad

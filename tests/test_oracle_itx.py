@@ -146,6 +146,7 @@ def test_packed_arena_equals_dense(bpc):
     dense, packed = make_itx_frame(192, 128, **kw), make_itx_frame(192, 128, packed=True, **kw)
     fl = packed["blocks"]["flags"]
     assert (fl & 0x80).any() and packed["coef"].size < dense["coef"].size
+    assert ((fl & 0x40) != 0).any() == (bpc > 8)
     cd, cp = dense["coef"].copy(), packed["coef"].copy()
     a = oracle_lib.itx_frame([p.copy() for p in dense["planes"]], dense["blocks"], cd, bpc)
     b = oracle_lib.itx_frame([p.copy() for p in packed["planes"]], packed["blocks"], cp, bpc)
