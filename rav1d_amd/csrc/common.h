@@ -93,7 +93,10 @@ __host__ __device__ constexpr int itx_blocks_per_wg(int tx) { return kItxThreads
 // Rounds of itx_blocks_per_wg blocks per workgroup: the small sizes' loads of all rounds are in
 // flight together (4-lane blocks: 4 rounds; 8-lane blocks: 1 (banded grid, 4K10: 49.8 vs
 // 50.7-51.3 us with 2; 4 rounds 56-58)).
-__host__ __device__ constexpr int itx_rounds(int tx) { return itx_lanes(tx) <= 4 ? 4 : 1; }
+#ifndef MI_ITX_SMALL_ROUNDS
+#define MI_ITX_SMALL_ROUNDS 4
+#endif
+__host__ __device__ constexpr int itx_rounds(int tx) { return itx_lanes(tx) <= 4 ? MI_ITX_SMALL_ROUNDS : 1; }
 
 // Which transform types are legal for a size (src/itx.rs:400-457): 16 types for sizes up to
 // 16 on both sides except 16x16 (12 types), DCT_DCT + IDTX when a side is 32, DCT_DCT only
@@ -240,7 +243,13 @@ __host__ __device__ constexpr uint32_t itx_legal_types(int tx) {
 }
 // order of the tx sizes in the itx grid: the 64-point sizes first (few workgroups, the longest),
 // then the 32-point sizes, then every size with both sides <= 16
-constexpr int kItxLaunchOrder[19] = { 4, 11, 12, 17, 18, 3, 9, 10, 15, 16, 0, 1, 2, 5, 6, 7, 8, 13, 14 };
+// (4x4 right after the 64-point sizes: its 64-block workgroups live longest after them, 14.9 us
+// in the round-6 timeline, and started last among the long ones; 27.43-27.52 against
+// 27.69-27.74 us for the DC-deferred stage, profiles/r06_itx_order.txt)
+#ifndef MI_ITX_ORDER
+#define MI_ITX_ORDER 4, 11, 12, 0, 17, 18, 3, 9, 10, 15, 16, 1, 2, 5, 6, 7, 8, 13, 14
+#endif
+constexpr int kItxLaunchOrder[19] = { MI_ITX_ORDER };
 constexpr int kItxBands = 8;
 constexpr int kItxDcRange = 32;   // wg_size flag: the range's workgroups run DC runs
 // DC path geometry of a size: chunks of min(w, 8) pixels, kItxDcItems chunks per lane, up to

@@ -21,7 +21,7 @@ bufs = {}
 for u in UNITS:
     b = torch.zeros(1 << 20, dtype=torch.int64, device="cuda")   # 131072 workgroups x 8 slots
     bufs[u] = b
-fr = make_frame(3840, 2160, 10, 1, seed=0x4C100001, with_fg=False, with_mc=True)
+fr = make_frame(3840, 2160, 10, 1, seed=0x4C100001, with_fg=False, with_mc=True, packed=True)
 ctx = F.Context(0)
 pipe = bench.Pipeline(ctx, fr, ring=2)
 s = torch.cuda.current_stream()

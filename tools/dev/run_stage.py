@@ -49,12 +49,14 @@ def mc_split(p):
 
 
 def itx(p):
+    # STAGE=itx_dc: as the bench runs it, the DC-only runs deferred into the DC map
+    fl = bench.ITX_KEEP_COEFS | (bench.ITX_DC_DEFER if st == "itx_dc" else 0)
     F.check(L.mi_itx_frame_runs(ctx.h, ctypes.byref(pa), ctypes.c_void_p(pipe.blocks.data_ptr()), pipe.itx_bands,
-                                pipe.itx_dc_end, ctypes.c_void_p(pipe.coefs[0].data_ptr()), bench.ITX_KEEP_COEFS, p), "itx")
+                                pipe.itx_dc_end, ctypes.c_void_p(pipe.coefs[0].data_ptr()), fl, p), "itx")
 
 
 for _ in range(int(os.environ.get("REPS", "10"))):
-    if st == "itx":
+    if st in ("itx", "itx_dc"):
         itx(sp)
     elif st == "mc":
         mc(sp)
@@ -82,7 +84,7 @@ if os.environ.get("TIME"):
 
     def one(stream):
         p = F._stream_ptr(stream)
-        if st == "itx":
+        if st in ("itx", "itx_dc"):
             itx(p)
         elif st == "mc":
             mc(p)
