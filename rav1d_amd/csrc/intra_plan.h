@@ -55,6 +55,13 @@ int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<in
     if (ns < 2) return 1;
     std::vector<int> sx(ns + 1);
     for (int q = 0; q <= ns; q++) sx[q] = (int)((int64_t)q * units / ns) * unit;
+    // the strip of every `unit`-wide column group (a table instead of a binary search per block)
+    std::vector<int8_t> strip_of(units + 1);
+    for (int u = 0, q = 0; u <= units; u++) {
+        while (q + 1 < ns && sx[q + 1] <= u * unit) q++;
+        strip_of[u] = (int8_t)q;
+    }
+    auto strip_at = [&](int xl) { return strip_of[std::min(xl / unit, units)]; };
     // strip of every block (by its luma column) and the owner of every 4x4 unit of each plane
     strip.resize(n);
     // with edge granules only intra block copy reads pixels across strips (CfL's luma lies in
@@ -65,12 +72,14 @@ int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<in
         for (int i = 0; i < n; i++) {
             const MiIntraBlock &b = f->intra[i];
             const int xl = b.plane ? b.x << ssh : b.x;
-            strip[i] = (int8_t)(std::upper_bound(sx.begin(), sx.end(), xl) - sx.begin() - 1);
+            strip[i] = strip_at(xl);
         }
         xs.assign(n + 1, 0);
         xd.clear();
         return ns;
     }
+    using sclk = std::chrono::steady_clock;
+    const auto s0 = sclk::now();
     const int aw = (f->w + 127) & ~127, ah = (f->h + 127) & ~127;
     int pw4[3], ph4[3];
     // (per-thread scratch kept across frames: a fresh multi-MB map per frame costs its page
@@ -93,7 +102,7 @@ int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<in
         for (int i = lo; i < hi; i++) {
             const MiIntraBlock &b = f->intra[i];
             const int xl = b.plane ? b.x << ssh : b.x;
-            strip[i] = (int8_t)(std::upper_bound(sx.begin(), sx.end(), xl) - sx.begin() - 1);
+            strip[i] = strip_at(xl);
             for (int y = b.y >> 2; y < (b.y + b.h) >> 2; y++) {
                 int32_t *row = &own[b.plane][(size_t)y * pw4[b.plane]];
                 for (int x = b.x >> 2; x < (b.x + b.w) >> 2; x++) {
@@ -110,6 +119,7 @@ int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<in
             }
         }
     });
+    const auto s1 = sclk::now();
     xs.assign(n + 1, 0);
     xd.clear();
     const int lpx = 128 / pxb;                                // plane px per line
@@ -119,6 +129,12 @@ int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<in
         const MiIntraBlock &b = f->intra[i];
         const int p = b.plane;
         add.clear();
+        {
+            // most blocks read only their own strip: nothing to scan
+            bool cross = false;
+            for (int d = f->dep_start[i]; d < f->dep_start[i + 1] && !cross; d++) cross = strip[f->deps[d]] != strip[i];
+            if (!cross) return true;
+        }
         // the pixels this block may read: its edges (rows y-1 .. y+2h-1, columns x-1 .. x+2w-1),
         // or for intra block copy the source rectangle (+1 for the bilinear phase, +-1 margin)
         int bx0 = std::max(0, (int)b.x - 1), by0 = std::max(0, (int)b.y - 1);
@@ -174,6 +190,11 @@ int intra_strips(const MiDecFrame *f, std::vector<int8_t> &strip, std::vector<in
             pxd.insert(pxd.end(), add.begin(), add.end());
         }
     });
+    static const bool sprof = getenv("MI_FX_PROFILE") != nullptr;
+    if (sprof) {
+        auto ms = [](sclk::time_point a, sclk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        fprintf(stderr, "intra_strips owner map %.3f scan %.3f ms\n", ms(s0, s1), ms(s1, sclk::now()));
+    }
     if (!split_ok) return 1;
     for (int t = 0; t < nparts; t++) {
         const int lo = part_lo[t], hi = t + 1 < nparts ? part_lo[t + 1] : n;
