@@ -525,12 +525,12 @@ def per_launch(v, launches):
 
 
 def pmc_traffic(stage, name=None):
-    """HBM bytes per step of `stage` from the committed PMC run (profiles/r05_traffic.json,
+    """HBM bytes per step of `stage` from the committed PMC run (profiles/r06_traffic.json,
     written by tools/traffic_json.py from tools/gpu_pmc.sh's FETCH_SIZE / WRITE_SIZE passes of
     this same bench command, calibrated per access width by tools/pmc_calib; the round-1 file
     when this round's is absent). None if absent."""
     path = None
-    for n in ([name] if name else ["r05_traffic.json", "r04_traffic.json", "r03_traffic.json", "r02_traffic.json",
+    for n in ([name] if name else ["r06_traffic.json", "r05_traffic.json", "r04_traffic.json", "r03_traffic.json", "r02_traffic.json",
                                    "r01_traffic.json"]):
         if os.path.exists(os.path.join(ROOT, "profiles", n)):
             path = os.path.join(ROOT, "profiles", n)
