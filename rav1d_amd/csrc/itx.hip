@@ -489,7 +489,10 @@ __device__ __forceinline__ void itx_dc(const ItxArgs &a, int lwg, uint8_t *lds) 
 // (64-point transforms on lane pairs, a persistent grid, and a schedule interleaving every size
 // in 4 or 8 rounds were measured slower and removed: DESIGN.md §5)
 template <typename Px, typename Cf, typename Lt, bool Wide>
-__global__ __launch_bounds__(kItxThreads, 4) void itx_frame_kernel(ItxArgs a) {
+#ifndef MI_ITX_MIN_WAVES
+#define MI_ITX_MIN_WAVES 4   // waves per SIMD the register budget must allow
+#endif
+__global__ __launch_bounds__(kItxThreads, MI_ITX_MIN_WAVES) void itx_frame_kernel(ItxArgs a) {
     __shared__ Lt lds[itx_lds_max(true) > itx_lds_max(false) ? itx_lds_max(true) : itx_lds_max(false)];
     KTL(0);
     const int wg = blockIdx.x;
