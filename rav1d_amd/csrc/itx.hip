@@ -490,7 +490,8 @@ __device__ __forceinline__ void itx_dc(const ItxArgs &a, int lwg, uint8_t *lds) 
 // in 4 or 8 rounds were measured slower and removed: DESIGN.md §5)
 template <typename Px, typename Cf, typename Lt, bool Wide>
 #ifndef MI_ITX_MIN_WAVES
-#define MI_ITX_MIN_WAVES 4   // waves per SIMD the register budget must allow
+#define MI_ITX_MIN_WAVES 4   // waves per SIMD the register budget must allow (5: 96 VGPRs + 128 B of
+                             // spills, 27.8 us; 6: 80 + 220 B, 32.2; 4: 27.6-27.8; r06_itx_waves.txt)
 #endif
 __global__ __launch_bounds__(kItxThreads, MI_ITX_MIN_WAVES) void itx_frame_kernel(ItxArgs a) {
     __shared__ Lt lds[itx_lds_max(true) > itx_lds_max(false) ? itx_lds_max(true) : itx_lds_max(false)];
