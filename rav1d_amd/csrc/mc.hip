@@ -35,8 +35,12 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 #define MC_MAX_U 16
 #endif
 constexpr int kMaxU = MC_MAX_U;    // units packed per wave
+// (5 window loads in flight per lane: the one-grid stage 62.0-62.6 us against 65.2-65.8 for 8,
+// 63.8-64.2 for 6, 65.8-66.0 for 7, 67.5-68.6 for 4; 12 and 16 spill; same 92 VGPRs for 4-8.
+// Fewer slots of a batch fall past a window's last quad, where they repeat a load:
+// profiles/r06_mc_batch.txt)
 #ifndef MC_STAGE_BATCH
-#define MC_STAGE_BATCH 8
+#define MC_STAGE_BATCH 5
 #endif
 constexpr int kStageBatch = MC_STAGE_BATCH;   // window loads in flight per lane before their LDS stores
 constexpr int kWinElems = 2240;    // window budget (elements), 4x16 units: 8 x 23 x 12 = 2208
